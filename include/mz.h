@@ -1,0 +1,185 @@
+/*
+ * mz.h — C ABI of libmz, the MI355X-native MuZero self-play + learner engine.
+ *
+ * This is the drop-in boundary for the reference's hot path.
+ * The reference (deveshjawla/MuZero.jl) is Julia; a maintainer binds these
+ * symbols with `ccall`; tests bind them with ctypes.
+ *
+ * Conventions (SURVEY §8b "Conventions"):
+ *   - every entry point returns int status: 0 = OK, < 0 = error; the message
+ *     is in mz_last_error(h) (the reference raises Julia exceptions / @assert,
+ *     e.g. src/SelfPlay.jl:243-244);
+ *   - host buffers are caller-owned and borrowed for the duration of the call;
+ *     `_dev` variants take device pointers and a hipStream_t (as void*);
+ *   - one handle per GPU, one host thread per handle; calls are synchronous
+ *     at return (the `_dev` variants are stream-ordered instead);
+ *   - action ids are 1-based (Julia convention), arrays are column-major with
+ *     the reference's shapes (W,H,C,N): feature index = w + W*h + W*H*c.
+ */
+#ifndef MZ_H
+#define MZ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MZ_MAX_ACTIONS 32
+
+/* Config — field names and defaults of src/Constructors.jl:18-52.
+ * Julia `dirichlet_α`/`exploration_ϵ` are spelled dirichlet_alpha /
+ * exploration_eps; `temperature_threshold = nothing` is -1; `action_space`
+ * is 1:action_space_size; `players` is 1:players.                         */
+typedef struct mz_config {
+    int32_t seed;                    /* 1337 (Constructors.jl:19, never used by the reference) */
+    int32_t observation_shape[3];    /* (W,H,C) per observation, e.g. (3,3,3) */
+    int32_t action_space_size;       /* |action_space| = 9 for TicTacToe */
+    int32_t players;                 /* |players| = 2 */
+    int32_t stacked_observations;    /* 1 */
+    int32_t muzero_player;           /* 1 */
+    int32_t intermediate_rewards;    /* false */
+    int32_t num_workers;
+    int32_t selfplay_on_gpu;
+    int32_t max_moves;               /* 9 */
+    int32_t temperature_threshold;   /* -1 = nothing */
+    float dirichlet_alpha;           /* 0.25 */
+    float exploration_eps;           /* 0.25 */
+    int32_t pb_c_base;               /* 19652 */
+    float pb_c_init;                 /* 1.25 */
+    float discount;                  /* 0.997 */
+    int32_t num_iters;               /* simulations per move */
+    int32_t replay_buffer_size;      /* 10000 */
+    int32_t num_unroll_steps;        /* K = 5 */
+    int32_t td_steps;                /* 5 */
+    int32_t PER;                     /* false */
+    int32_t PER_alpha;               /* 1 */
+    int32_t training_steps;          /* 10000 */
+    int32_t batch_size;              /* 32 */
+    int32_t checkpoint_interval;     /* 10 */
+    float value_loss_weight;         /* 0.25 (never applied by the reference, Q11) */
+} mz_config;
+
+enum { MZ_ACT_IDENTITY = 0, MZ_ACT_RELU = 1, MZ_ACT_TANH = 2 };
+
+/* FeedForwardHP — src/Constructors.jl:62-75 */
+typedef struct mz_ffhp {
+    int32_t width_hidden;            /* 64 */
+    int32_t depth_representation;    /* 3 */
+    int32_t depth_prediction;        /* 3 */
+    int32_t depth_dynamics;          /* 3 */
+    int32_t depth_policy;            /* 1 */
+    int32_t depth_value;             /* 1 */
+    int32_t depth_reward;            /* 1 */
+    int32_t depth_state_head;        /* 3 */
+    int32_t use_batch_norm;          /* false (BatchNorm FC path not supported: error) */
+    float batch_norm_momentum;       /* 0.6 */
+    int32_t hidden_state_size;       /* 27 = prod(observation_shape) */
+    int32_t reward_activation;       /* MZ_ACT_TANH */
+} mz_ffhp;
+
+/* The three networks of the `NNs` NamedTuple (SelfPlay.jl:230). */
+enum { MZ_NET_REPR = 0, MZ_NET_PRED = 1, MZ_NET_DYN = 2 };
+
+typedef struct mz_handle mz_handle;
+
+/* Create an engine on HIP device `device` (replaces init_* + the Julia
+ * process setup of games/tictactoe/main.jl:15-28).  `max_games` bounds the
+ * batch G of mz_mcts_search; `rng_seed` keys every Philox stream.         */
+int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device,
+                     int max_games, uint64_t rng_seed, mz_handle** out);
+void mz_engine_destroy(mz_handle* h);
+const char* mz_last_error(const mz_handle* h);
+/* message of the last failed mz_engine_create (no handle exists then) */
+const char* mz_create_error(void);
+
+/* Parameter counts and exchange in Flux order: for every Dense, W (out,in)
+ * column-major then b; Chain order, Split paths in order
+ * (Learning.jl:87-142).  FC TicTacToe: 18331 / 23242 / 33308 floats.      */
+int mz_net_param_count(const mz_handle* h, int net, size_t* n);
+int mz_weights_set(mz_handle* h, int net, const float* flat, size_t n);
+int mz_weights_get(mz_handle* h, int net, float* flat, size_t n);
+
+/* Batched forward of one net (the Flux Chain call, Learning.jl:87-142).
+ *   REPR: x = stacked obs (W,H,Cs,n) -> out0 = h (hidden,n)
+ *   PRED: x = h (hidden,n)          -> out0 = value (1,n), out1 = policy probs (A,n)
+ *   DYN : x = state-action (W,H,C+1,n) -> out0 = h' (hidden,n), out1 = reward (1,n) */
+int mz_net_forward(mz_handle* h, int net, const float* x, int n, float* out0, float* out1);
+
+/* Batched run_mcts + select_action + store_search_stats! for G games
+ * (SelfPlay.jl:230-306, 115-122).
+ *   obs        (W,H,Cs,G) stacked observations (get_stacked_observations)
+ *   legal_mask (A,G) uint8, nonzero = legal (legal_action_space), >= 1 per game
+ *   to_play    (G) current player, 1-based
+ *   exploration  add Dirichlet noise at the root (SelfPlay.jl:247-249)
+ *   rng_step   move counter keying the Philox streams; game_offset = global id
+ *              of game 0 (shard offset on multi-GPU)
+ *   temperature  visit_softmax_temperature (0 = argmax, INFINITY = uniform)
+ * outputs: child_visits (A,G) = N_a / sum N, root_value (G) = node_value(root),
+ *          action_out (G) in 1..A.                                         */
+int mz_mcts_search(mz_handle* h, int G, const float* obs, const uint8_t* legal_mask,
+                   const int32_t* to_play, int exploration, uint32_t rng_step,
+                   uint32_t game_offset, float temperature,
+                   float* child_visits, float* root_value, int32_t* action_out);
+
+/* Same, all buffers in device memory, stream-ordered on `stream` (hipStream_t). */
+int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* legal_mask,
+                       const int32_t* to_play, int exploration, uint32_t rng_step,
+                       uint32_t game_offset, float temperature,
+                       float* child_visits, float* root_value, int32_t* action_out,
+                       void* stream);
+
+/* Debug/parity: copy the last search's tree statistics to host.  Per game,
+ * expanded-node slots e = 0..S (0 = root, e = s+1 expanded by simulation s)
+ * and child slots a = 0..A-1:
+ *   edge_N/edge_W/edge_P/edge_R: (A, S+1, G), edge_child: expanded slot or -1,
+ *   node_to_play (S+1, G); any pointer may be NULL.                        */
+int mz_debug_tree(mz_handle* h, int G, int32_t* edge_N, float* edge_W, float* edge_P,
+                  float* edge_R, int32_t* edge_child, int32_t* node_to_play);
+
+/* One learner batch, the tuple returned by get_batch (ReplayBuffer.jl:216),
+ * column-major as in the reference:
+ *   observation (W,H,Cs,B), actions (K+1,B) as float action ids,
+ *   target_values (K+1,B), target_rewards (K+1,B), target_policies (A,K+1,B),
+ *   gradient_scale (B).  PER weights are not supported (PER=false).        */
+typedef struct mz_batch {
+    int32_t batch_size;
+    const float* observation;
+    const float* actions;
+    const float* target_values;
+    const float* target_rewards;
+    const float* target_policies;
+    const float* gradient_scale;
+} mz_batch;
+
+/* Learner step in ref_semantics (Learning.jl:327-413, quirks Q10/Q11):
+ * K-step unroll forward, losses, gradient 2θ, ADAM(β=(0.9,0.999), ϵ=1e-8)
+ * with learning rate `eta` (the host evaluates Cos(λ0=1e-4, λ1=1e-1,
+ * period=10) and passes it; Learning.jl:319,382).
+ * losses_out[6] = {value, reward, policy, l2_repr, l2_pred, l2_dyn}; the
+ * reference's three reported losses are value+reward+policy+l2_net.
+ * `grad_dev`, when not NULL, is a device buffer of all params (repr, pred,
+ * dyn concatenated, device order) that is filled with the gradient before
+ * the update and then used for it — the host may all-reduce it in between
+ * through mz_learner_step_split (multi-GPU).                  */
+int mz_learner_step(mz_handle* h, const mz_batch* batch, double eta, float* losses_out);
+
+/* Split learner step for data-parallel training: (1) forward + losses +
+ * gradient into grad_dev (device, mz_grad_count floats), (2) the caller
+ * all-reduces (sum) grad_dev across ranks, (3) apply ADAM with scale
+ * 1/world.  Stream-ordered on `stream`.                                   */
+int mz_grad_count(const mz_handle* h, size_t* n);
+int mz_learner_grad_dev(mz_handle* h, const mz_batch* dev_batch, float* grad_dev,
+                        float* losses_dev, void* stream);
+int mz_learner_apply_dev(mz_handle* h, const float* grad_dev, float grad_scale,
+                         double eta, void* stream);
+
+/* Synchronize the handle's stream. */
+int mz_sync(mz_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MZ_H */

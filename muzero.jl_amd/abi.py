@@ -1,0 +1,209 @@
+"""ctypes binding of libmz (include/mz.h) — the Python side of the drop-in
+boundary.  The Julia side a maintainer would add is in INTEGRATION.md.
+
+The product path has no fallback: if libmz.so is missing or no HIP device is
+present, `Engine(...)` raises.  Arrays crossing the ABI are numpy arrays in the
+reference's column-major shapes, stored here as C-contiguous arrays whose LAST
+axis is Julia's FIRST (e.g. Julia (A, G) == numpy (G, A)).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import LIB_PATH
+from .config import MzConfig, MzFFHP, to_c_config, to_c_ffhp, stacked_features
+
+NET_REPR, NET_PRED, NET_DYN = 0, 1, 2
+
+_lib = None
+
+_F = ctypes.POINTER(ctypes.c_float)
+_I = ctypes.POINTER(ctypes.c_int32)
+_U8 = ctypes.POINTER(ctypes.c_uint8)
+_VP = ctypes.c_void_p
+
+
+class MzBatch(ctypes.Structure):
+    _fields_ = [("batch_size", ctypes.c_int32), ("observation", _VP), ("actions", _VP),
+                ("target_values", _VP), ("target_rewards", _VP), ("target_policies", _VP),
+                ("gradient_scale", _VP)]
+
+
+# exported symbol -> (restype, argtypes); tests check every one is present
+SIGNATURES = {
+    "mz_engine_create": (ctypes.c_int, [ctypes.POINTER(MzConfig), ctypes.POINTER(MzFFHP), ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(_VP)]),
+    "mz_engine_destroy": (None, [_VP]),
+    "mz_last_error": (ctypes.c_char_p, [_VP]),
+    "mz_create_error": (ctypes.c_char_p, []),
+    "mz_net_param_count": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
+    "mz_weights_set": (ctypes.c_int, [_VP, ctypes.c_int, _VP, ctypes.c_size_t]),
+    "mz_weights_get": (ctypes.c_int, [_VP, ctypes.c_int, _VP, ctypes.c_size_t]),
+    "mz_net_forward": (ctypes.c_int, [_VP, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP]),
+    "mz_mcts_search": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, ctypes.c_int, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.c_float, _VP, _VP, _VP]),
+    "mz_mcts_search_dev": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, ctypes.c_int, ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_float, _VP, _VP, _VP, _VP]),
+    "mz_debug_tree": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "mz_learner_step": (ctypes.c_int, [_VP, ctypes.POINTER(MzBatch), ctypes.c_double, _VP]),
+    "mz_grad_count": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_size_t)]),
+    "mz_learner_grad_dev": (ctypes.c_int, [_VP, ctypes.POINTER(MzBatch), _VP, _VP, _VP]),
+    "mz_learner_apply_dev": (ctypes.c_int, [_VP, _VP, ctypes.c_float, ctypes.c_double, _VP]),
+    "mz_sync": (ctypes.c_int, [_VP]),
+}
+
+
+def load_library(path=LIB_PATH):
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"libmz.so not built at {path}: run __graft_entry__.build() "
+                           "(there is no CPU fallback for the engine)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(_VP)
+
+
+class MzError(RuntimeError):
+    pass
+
+
+class Engine:
+    """One libmz handle = one GPU (SURVEY §8b conventions)."""
+
+    def __init__(self, conf, hyper, device=0, max_games=512, rng_seed=0):
+        lib = load_library()
+        self.lib = lib
+        self.conf = conf
+        self.hyper = hyper
+        self._cconf = to_c_config(conf)
+        self._chp = to_c_ffhp(hyper)
+        h = _VP()
+        rc = lib.mz_engine_create(ctypes.byref(self._cconf), ctypes.byref(self._chp), device, max_games,
+                                  rng_seed, ctypes.byref(h))
+        if rc != 0:
+            raise MzError(f"mz_engine_create: {lib.mz_create_error().decode()}")
+        self.h = h
+        self.max_games = max_games
+        self.A = len(conf.action_space)
+        self.H = hyper.hidden_state_size
+        self.obs_feat = stacked_features(conf)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.mz_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise MzError(f"{what}: {self.lib.mz_last_error(self.h).decode()}")
+
+    # ---- weights (Flux order per net)
+    def param_count(self, net):
+        n = ctypes.c_size_t()
+        self._check(self.lib.mz_net_param_count(self.h, net, ctypes.byref(n)), "mz_net_param_count")
+        return n.value
+
+    def set_weights(self, net, flat):
+        flat = np.ascontiguousarray(flat, dtype=np.float32)
+        self._check(self.lib.mz_weights_set(self.h, net, _p(flat), flat.size), "mz_weights_set")
+
+    def get_weights(self, net):
+        out = np.empty(self.param_count(net), dtype=np.float32)
+        self._check(self.lib.mz_weights_get(self.h, net, _p(out), out.size), "mz_weights_get")
+        return out
+
+    # ---- batched net forward (Flux Chain call)
+    def forward(self, net, x):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        n = x.shape[0]
+        if net == NET_PRED:
+            o0 = np.empty((n, 1), np.float32)
+            o1 = np.empty((n, self.A), np.float32)
+        elif net == NET_DYN:
+            o0 = np.empty((n, self.H), np.float32)
+            o1 = np.empty((n, 1), np.float32)
+        else:
+            o0 = np.empty((n, self.H), np.float32)
+            o1 = None
+        self._check(self.lib.mz_net_forward(self.h, net, _p(x), n, _p(o0), _p(o1)), "mz_net_forward")
+        return (o0, o1) if o1 is not None else o0
+
+    # ---- batched run_mcts
+    def mcts_search(self, obs, legal_mask, to_play, exploration=True, rng_step=0, game_offset=0,
+                    temperature=1.0):
+        obs = np.ascontiguousarray(obs, dtype=np.float32)
+        G = obs.shape[0]
+        legal = np.ascontiguousarray(legal_mask, dtype=np.uint8)
+        tp = np.ascontiguousarray(to_play, dtype=np.int32)
+        cv = np.empty((G, self.A), np.float32)
+        rv = np.empty(G, np.float32)
+        act = np.empty(G, np.int32)
+        self._check(self.lib.mz_mcts_search(self.h, G, _p(obs), _p(legal), _p(tp), int(exploration),
+                                            rng_step & 0xffffffff, game_offset, temperature,
+                                            _p(cv), _p(rv), _p(act)), "mz_mcts_search")
+        return cv, rv, act
+
+    def mcts_search_dev(self, G, obs_ptr, legal_ptr, tp_ptr, cv_ptr, rv_ptr, act_ptr, exploration=True,
+                        rng_step=0, game_offset=0, temperature=1.0, stream=None):
+        self._check(self.lib.mz_mcts_search_dev(self.h, G, obs_ptr, legal_ptr, tp_ptr, int(exploration),
+                                                rng_step & 0xffffffff, game_offset, temperature, cv_ptr,
+                                                rv_ptr, act_ptr, stream), "mz_mcts_search_dev")
+
+    def debug_tree(self, G):
+        S, A = self.conf.num_iters, self.A
+        eN = np.empty((G, S + 1, A), np.int32)
+        eW = np.empty((G, S + 1, A), np.float32)
+        eP = np.empty((G, S + 1, A), np.float32)
+        eR = np.empty((G, S + 1, A), np.float32)
+        eC = np.empty((G, S + 1, A), np.int32)
+        ntp = np.empty((G, S + 1), np.int32)
+        self._check(self.lib.mz_debug_tree(self.h, G, _p(eN), _p(eW), _p(eP), _p(eR), _p(eC), _p(ntp)),
+                    "mz_debug_tree")
+        return dict(N=eN, W=eW, P=eP, R=eR, C=eC, to_play=ntp)
+
+    # ---- learner
+    def learner_step(self, batch, eta):
+        """batch: dict with observation (B, F), actions (B, K+1), target_values (B, K+1),
+        target_rewards (B, K+1), target_policies (B, K+1, A), gradient_scale (B)."""
+        arrs = {k: np.ascontiguousarray(batch[k], dtype=np.float32) for k in
+                ("observation", "actions", "target_values", "target_rewards", "target_policies", "gradient_scale")}
+        b = MzBatch(arrs["observation"].shape[0], _p(arrs["observation"]), _p(arrs["actions"]),
+                    _p(arrs["target_values"]), _p(arrs["target_rewards"]), _p(arrs["target_policies"]),
+                    _p(arrs["gradient_scale"]))
+        losses = np.empty(6, np.float32)
+        self._check(self.lib.mz_learner_step(self.h, ctypes.byref(b), float(eta), _p(losses)), "mz_learner_step")
+        return losses
+
+    def grad_count(self):
+        n = ctypes.c_size_t()
+        self._check(self.lib.mz_grad_count(self.h, ctypes.byref(n)), "mz_grad_count")
+        return n.value
+
+    def learner_grad_dev(self, dev_batch_ptrs, B, grad_ptr, losses_ptr=None, stream=None):
+        b = MzBatch(B, *dev_batch_ptrs)
+        self._check(self.lib.mz_learner_grad_dev(self.h, ctypes.byref(b), grad_ptr, losses_ptr, stream),
+                    "mz_learner_grad_dev")
+
+    def learner_apply_dev(self, grad_ptr, grad_scale, eta, stream=None):
+        self._check(self.lib.mz_learner_apply_dev(self.h, grad_ptr, grad_scale, float(eta), stream),
+                    "mz_learner_apply_dev")
+
+    def sync(self):
+        self._check(self.lib.mz_sync(self.h), "mz_sync")

@@ -1,0 +1,587 @@
+// mz_engine.hip — host side of libmz: the C ABI of include/mz.h.
+//
+// Builds the layer/plan description of the FeedForwardHP networks
+// (Learning.jl:87-142), packs Flux-order weights into the MFMA fragment
+// image, owns every device buffer of one engine (one handle per GPU), and
+// launches the search / forward / learner kernels on the handle's stream.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mz_internal.h"
+
+extern "C" __global__ void mz_search_kernel(SearchParams P);
+
+extern "C" __global__ void mz_unroll_kernel(UnrollParams P);
+extern "C" __global__ void mz_forward_kernel(const int* plan, const float* Wp, const float* Bp, int total_lds,
+                                             int in_off, int in_feat, const float* x, int n, int out0_off, int o0,
+                                             float* out0, int out1_off, int o1, float* out1, int sm1);
+extern "C" __global__ void mz_loss_kernel(int B, int K, int A, const float* pv, const float* pp, const float* tv,
+                                          const float* tp, const float* gscale, float* out);
+extern "C" __global__ void mz_sqnorm_kernel(const float* P, size_t n, double* out);
+extern "C" __global__ void mz_l2_finish_kernel(const double* sq, float* out);
+extern "C" __global__ void mz_grad_2theta_kernel(const float* P, float* G, size_t n);
+extern "C" __global__ void mz_adam_kernel(float* P, float* M, float* V, const float* G, float gscale, size_t n,
+                                          double bp1, double bp2, double eta);
+extern "C" __global__ void mz_repack_kernel(const float* flat, const int* src, float* packed, size_t n);
+
+namespace {
+
+enum { CH_TRUNK = 0, CH_HEAD1 = 1, CH_HEAD2 = 2 };
+
+struct LayerSpec {
+    int net, chain, in, out, act;
+    size_t flux_w, flux_b;     // offsets in the global flat parameter vector
+    int nq, n_ob;
+    int packed_w, packed_b;    // offsets in the packed images
+};
+
+struct PlanBuild {
+    std::vector<std::vector<std::pair<int, int>>> stages;
+    std::vector<LayerDesc> layers;
+    void ensure(int n) { if ((int)stages.size() < n) stages.resize(n); }
+    std::vector<int> image() const {
+        std::vector<int> v;
+        int nt = 0;
+        for (auto& s : stages) nt += (int)s.size();
+        v.push_back((int)stages.size()); v.push_back((int)layers.size()); v.push_back(nt);
+        int acc = 0;
+        for (auto& s : stages) { v.push_back(acc); acc += (int)s.size(); }
+        v.push_back(acc);
+        for (auto& s : stages) for (auto& t : s) { v.push_back(t.first); v.push_back(t.second); }
+        for (auto& L : layers) {
+            const int* p = reinterpret_cast<const int*>(&L);
+            for (size_t i = 0; i < sizeof(LayerDesc) / sizeof(int); ++i) v.push_back(p[i]);
+        }
+        return v;
+    }
+};
+
+thread_local std::string g_create_error;
+
+}  // namespace
+
+struct mz_handle {
+    mz_config conf;
+    mz_ffhp hp;
+    int device = 0, max_games = 0;
+    uint64_t seed = 0;
+    std::string err;
+    hipStream_t stream = nullptr;
+
+    std::vector<LayerSpec> layers;
+    std::vector<int> chains[3][3];          // [net][chain] -> layer indices
+    size_t nparams[3] = {0, 0, 0}, flat_off[3] = {0, 0, 0}, nflat = 0;
+    size_t packed_w_n = 0, packed_b_n = 0;
+    int obs_feat = 0, plane = 0, H = 0, A = 0, S = 0;
+    ActLayout lay{};
+    int chain_buf[3][3][2];                 // LDS ping-pong buffers per chain
+
+    float* d_flat = nullptr; float* d_Wp = nullptr; float* d_Bp = nullptr;
+    int* d_srcW = nullptr; int* d_srcB = nullptr;
+    int* d_plan[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // repr, pred, dyn, root, sim
+    double* d_pbc = nullptr; double* d_sqrt = nullptr; float* d_aval = nullptr;
+    int32_t* d_eN = nullptr; int32_t* d_eC = nullptr; int32_t* d_ntp = nullptr;
+    float* d_eW = nullptr; float* d_eP = nullptr; float* d_eR = nullptr; float* d_hid = nullptr;
+    float* d_obs = nullptr; uint8_t* d_legal = nullptr; int32_t* d_tp = nullptr;
+    float* d_cv = nullptr; float* d_rv = nullptr; int32_t* d_act = nullptr;
+    // learner
+    float* d_m = nullptr; float* d_v = nullptr; float* d_grad = nullptr;
+    double bp1 = 0.9, bp2 = 0.999;
+    int bcap = 0;
+    float *d_bobs = nullptr, *d_bact = nullptr, *d_btv = nullptr, *d_btr = nullptr, *d_btp = nullptr,
+          *d_bgs = nullptr, *d_pv = nullptr, *d_pp = nullptr, *d_pr = nullptr, *d_loss = nullptr;
+    double* d_sq = nullptr;
+    std::vector<void*> allocs;
+};
+
+#define MZ_TRY(h, expr)                                                                  \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            (h)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                \
+            return -1;                                                                   \
+        }                                                                                \
+    } while (0)
+
+static int fail(mz_handle* h, const std::string& m) { h->err = m; return -2; }
+
+template <typename T>
+static hipError_t dalloc(mz_handle* h, T** p, size_t n) {
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T) + 16);
+    if (e == hipSuccess) h->allocs.push_back(*p);
+    return e;
+}
+
+// ------------------------------------------------------------ specs & plans
+static void add_layer(mz_handle* h, int net, int chain, int in, int out, int act) {
+    LayerSpec L;
+    L.net = net; L.chain = chain; L.in = in; L.out = out; L.act = act;
+    L.flux_w = h->flat_off[net] + h->nparams[net]; h->nparams[net] += (size_t)in * out;
+    L.flux_b = h->flat_off[net] + h->nparams[net]; h->nparams[net] += (size_t)out;
+    L.nq = (in + 15) / 16;
+    L.n_ob = (out + 15) / 16;
+    L.packed_w = (int)h->packed_w_n; h->packed_w_n += (size_t)L.n_ob * 4 * L.nq * 64;
+    L.packed_b = (int)h->packed_b_n; h->packed_b_n += (size_t)L.n_ob * 16;
+    h->chains[net][chain].push_back((int)h->layers.size());
+    h->layers.push_back(L);
+}
+
+// init_representation / init_prediction / init_dynamics (Learning.jl:87-142)
+static void build_specs(mz_handle* h) {
+    const mz_config& c = h->conf;
+    const mz_ffhp& p = h->hp;
+    const int W = c.observation_shape[0], Hh = c.observation_shape[1], C = c.observation_shape[2];
+    const int hs = p.width_hidden, hid = p.hidden_state_size, A = c.action_space_size;
+    h->obs_feat = W * Hh * (C * (c.stacked_observations + 1) + c.stacked_observations);   // :88
+    h->plane = W * Hh;
+    h->H = hid; h->A = A; h->S = c.num_iters;
+    // repr
+    h->flat_off[MZ_NET_REPR] = 0;
+    add_layer(h, MZ_NET_REPR, CH_TRUNK, h->obs_feat, hs, MZ_ACT_RELU);
+    for (int i = 0; i < p.depth_representation; ++i) add_layer(h, MZ_NET_REPR, CH_TRUNK, hs, hs, MZ_ACT_RELU);
+    add_layer(h, MZ_NET_REPR, CH_TRUNK, hs, hid, MZ_ACT_IDENTITY);
+    // pred
+    h->flat_off[MZ_NET_PRED] = h->nparams[MZ_NET_REPR];
+    add_layer(h, MZ_NET_PRED, CH_TRUNK, hid, hs, MZ_ACT_RELU);
+    for (int i = 0; i < p.depth_prediction; ++i) add_layer(h, MZ_NET_PRED, CH_TRUNK, hs, hs, MZ_ACT_RELU);
+    for (int i = 0; i < p.depth_value; ++i) add_layer(h, MZ_NET_PRED, CH_HEAD1, hs, hs, MZ_ACT_RELU);
+    add_layer(h, MZ_NET_PRED, CH_HEAD1, hs, 1, MZ_ACT_TANH);
+    for (int i = 0; i < p.depth_policy; ++i) add_layer(h, MZ_NET_PRED, CH_HEAD2, hs, hs, MZ_ACT_RELU);
+    add_layer(h, MZ_NET_PRED, CH_HEAD2, hs, A, MZ_ACT_IDENTITY);
+    // dyn
+    h->flat_off[MZ_NET_DYN] = h->flat_off[MZ_NET_PRED] + h->nparams[MZ_NET_PRED];
+    add_layer(h, MZ_NET_DYN, CH_TRUNK, W * Hh * (C + 1), hs, MZ_ACT_RELU);                 // :120
+    for (int i = 0; i < p.depth_dynamics; ++i) add_layer(h, MZ_NET_DYN, CH_TRUNK, hs, hs, MZ_ACT_RELU);
+    for (int i = 0; i < p.depth_state_head; ++i) add_layer(h, MZ_NET_DYN, CH_HEAD1, hs, hs, MZ_ACT_RELU);
+    add_layer(h, MZ_NET_DYN, CH_HEAD1, hs, hid, MZ_ACT_IDENTITY);
+    for (int i = 0; i < p.depth_reward; ++i) add_layer(h, MZ_NET_DYN, CH_HEAD2, hs, hs, MZ_ACT_RELU);
+    add_layer(h, MZ_NET_DYN, CH_HEAD2, hs, 1, p.reward_activation);
+    h->nflat = h->flat_off[MZ_NET_DYN] + h->nparams[MZ_NET_DYN];
+
+    // LDS activation layout (floats), every region [rows][16]
+    int off = 0;
+    auto region = [&](int rows) { int o = off; off += rows * 16; return o; };
+    auto in_rows = [&](int net) { return 16 * h->layers[h->chains[net][CH_TRUNK][0]].nq; };
+    h->lay.rows_rep = in_rows(MZ_NET_REPR);
+    h->lay.rows_pred = in_rows(MZ_NET_PRED);
+    h->lay.rows_dyn = in_rows(MZ_NET_DYN);
+    h->lay.x_rep = region(h->lay.rows_rep);
+    h->lay.x_pred = region(h->lay.rows_pred);
+    h->lay.x_dyn = region(h->lay.rows_dyn);
+    h->lay.h_out = region(mz_round16(hid));
+    h->lay.v_out = region(16);
+    h->lay.p_out = region(mz_round16(A));
+    h->lay.r_out = region(16);
+    for (int net = 0; net < 3; ++net)
+        for (int ch = 0; ch < 3; ++ch) {
+            int rows = 0;
+            for (int li : h->chains[net][ch]) rows = std::max(rows, 16 * h->layers[li].n_ob);
+            if (rows == 0) { h->chain_buf[net][ch][0] = h->chain_buf[net][ch][1] = -1; continue; }
+            h->chain_buf[net][ch][0] = region(rows);
+            h->chain_buf[net][ch][1] = region(rows);
+        }
+    h->lay.total = off;
+}
+
+// Place chain `ch` of `net` in plan `pb` from stage `st0`; returns the end stage.
+static int place_chain(mz_handle* h, PlanBuild& pb, int net, int ch, int st0, int in_first, int out_last) {
+    const std::vector<int>& ls = h->chains[net][ch];
+    const int n = (int)ls.size();
+    pb.ensure(st0 + n);
+    for (int i = 0; i < n; ++i) {
+        const LayerSpec& S = h->layers[ls[i]];
+        LayerDesc d;
+        d.w_off = S.packed_w; d.b_off = S.packed_b; d.nq = S.nq; d.n_ob = S.n_ob; d.act = S.act;
+        d.in_off = i == 0 ? in_first : h->chain_buf[net][ch][(i - 1) & 1];
+        d.out_off = i == n - 1 ? out_last : h->chain_buf[net][ch][i & 1];
+        d.out_rows = S.out;
+        const int di = (int)pb.layers.size();
+        pb.layers.push_back(d);
+        for (int ob = 0; ob < S.n_ob; ++ob) pb.stages[st0 + i].push_back({di, ob});
+    }
+    return st0 + n;
+}
+static int trunk_out(mz_handle* h, int net) {
+    const int n = (int)h->chains[net][CH_TRUNK].size();
+    return h->chain_buf[net][CH_TRUNK][(n - 1) & 1];
+}
+// A two-headed net (pred / dyn) from stage st0 with trunk input `in`.
+static int place_split_net(mz_handle* h, PlanBuild& pb, int net, int st0, int in) {
+    const int t = place_chain(h, pb, net, CH_TRUNK, st0, in, trunk_out(h, net));
+    const int to = trunk_out(h, net);
+    int e1, e2;
+    if (net == MZ_NET_PRED) {
+        e1 = place_chain(h, pb, net, CH_HEAD1, t, to, h->lay.v_out);
+        e2 = place_chain(h, pb, net, CH_HEAD2, t, to, h->lay.p_out);
+    } else {
+        e1 = place_chain(h, pb, net, CH_HEAD1, t, to, h->lay.h_out);
+        e2 = place_chain(h, pb, net, CH_HEAD2, t, to, h->lay.r_out);
+    }
+    return std::max(e1, e2);
+}
+
+static int upload_plan(mz_handle* h, const PlanBuild& pb, int** dst) {
+    std::vector<int> img = pb.image();
+    MZ_TRY(h, dalloc(h, dst, img.size()));
+    MZ_TRY(h, hipMemcpy(*dst, img.data(), img.size() * sizeof(int), hipMemcpyHostToDevice));
+    return 0;
+}
+
+static int build_plans(mz_handle* h) {
+    PlanBuild repr, pred, dyn, root, sim;
+    place_chain(h, repr, MZ_NET_REPR, CH_TRUNK, 0, h->lay.x_rep, h->lay.h_out);
+    place_split_net(h, pred, MZ_NET_PRED, 0, h->lay.x_pred);
+    place_split_net(h, dyn, MZ_NET_DYN, 0, h->lay.x_dyn);
+    const int e = place_chain(h, root, MZ_NET_REPR, CH_TRUNK, 0, h->lay.x_rep, h->lay.h_out);
+    place_split_net(h, root, MZ_NET_PRED, e, h->lay.h_out);
+    place_split_net(h, sim, MZ_NET_PRED, 0, h->lay.x_pred);
+    place_split_net(h, sim, MZ_NET_DYN, 0, h->lay.x_dyn);
+    const PlanBuild* all[5] = {&repr, &pred, &dyn, &root, &sim};
+    for (int i = 0; i < 5; ++i)
+        if (all[i]->stages.size() > MZ_MAX_STAGES) return fail(h, "network too deep for the plan executor");
+    for (int i = 0; i < 5; ++i) if (upload_plan(h, *all[i], &h->d_plan[i])) return -1;
+    return 0;
+}
+
+// MFMA fragment image: packed W [ob][ks][lane] <- W[ob*16 + (lane&15)][ks*4 + (lane>>4)]
+// (Flux W is (out,in) column-major: element (o,i) at flux_w + o + out*i).
+static int build_pack_index(mz_handle* h) {
+    std::vector<int> sw(h->packed_w_n, -1), sb(h->packed_b_n, -1);
+    for (const LayerSpec& L : h->layers) {
+        const int nks = 4 * L.nq;
+        for (int ob = 0; ob < L.n_ob; ++ob)
+            for (int ks = 0; ks < nks; ++ks)
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int o = ob * 16 + (lane & 15), k = ks * 4 + (lane >> 4);
+                    const size_t dst = (size_t)L.packed_w + ((size_t)ob * nks + ks) * 64 + lane;
+                    if (o < L.out && k < L.in) sw[dst] = (int)(L.flux_w + o + (size_t)L.out * k);
+                }
+        for (int o = 0; o < L.out; ++o) sb[(size_t)L.packed_b + o] = (int)(L.flux_b + o);
+    }
+    MZ_TRY(h, dalloc(h, &h->d_srcW, sw.size()));
+    MZ_TRY(h, dalloc(h, &h->d_srcB, sb.size()));
+    MZ_TRY(h, hipMemcpy(h->d_srcW, sw.data(), sw.size() * sizeof(int), hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(h->d_srcB, sb.data(), sb.size() * sizeof(int), hipMemcpyHostToDevice));
+    return 0;
+}
+
+static int repack(mz_handle* h) {
+    const int T = 256;
+    hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_w_n + T - 1) / T)), dim3(T), 0, h->stream,
+                       h->d_flat, h->d_srcW, h->d_Wp, h->packed_w_n);
+    hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_b_n + T - 1) / T)), dim3(T), 0, h->stream,
+                       h->d_flat, h->d_srcB, h->d_Bp, h->packed_b_n);
+    MZ_TRY(h, hipGetLastError());
+    return 0;
+}
+
+static size_t search_lds_bytes(const mz_handle* h) {
+    return (size_t)h->lay.total * 4 + (size_t)(160 + 16 * (h->S + 2)) * 4;
+}
+
+// ------------------------------------------------------------------- ABI
+extern "C" {
+
+const char* mz_create_error(void) { return g_create_error.c_str(); }
+const char* mz_last_error(const mz_handle* h) { return h ? h->err.c_str() : g_create_error.c_str(); }
+
+void mz_engine_destroy(mz_handle* h) {
+    if (!h) return;
+    hipSetDevice(h->device);
+    for (void* p : h->allocs) hipFree(p);
+    if (h->stream) hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, int max_games, uint64_t rng_seed,
+                     mz_handle** out) {
+    g_create_error.clear();
+    if (!conf || !hyper || !out) { g_create_error = "null argument"; return -2; }
+    *out = nullptr;
+    mz_handle* h = new mz_handle();
+    h->conf = *conf; h->hp = *hyper; h->device = device; h->max_games = max_games; h->seed = rng_seed;
+    auto bad = [&](const std::string& m) { g_create_error = m; delete h; return -2; };
+    const mz_config& c = *conf;
+    if (c.action_space_size < 1 || c.action_space_size > 16)
+        return bad("action_space_size must be in 1..16 (16-lane select groups)");
+    if (c.players < 1 || c.players > 2) return bad("players must be 1 or 2");
+    if (c.num_iters < 1 || c.num_iters >= (1 << 20)) return bad("num_iters out of range");
+    if (hyper->use_batch_norm) return bad("FeedForwardHP.use_batch_norm is not supported");
+    if (hyper->hidden_state_size != c.observation_shape[0] * c.observation_shape[1] * c.observation_shape[2])
+        return bad("hidden_state_size must equal prod(observation_shape) (the FC path reshapes h to it)");
+    if (max_games < 1) return bad("max_games must be >= 1");
+    if (hipSetDevice(device) != hipSuccess) return bad("hipSetDevice failed (no GPU?)");
+    build_specs(h);
+    if (search_lds_bytes(h) > 160 * 1024) return bad("LDS budget exceeded (width/num_iters too large)");
+    int rc = 0;
+#define CK(x) do { if ((rc = (x)) != 0) { g_create_error = h->err; mz_engine_destroy(h); return rc; } } while (0)
+    CK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess ? 0 : fail(h, "hipStreamCreate"));
+    CK(build_plans(h));
+    CK(build_pack_index(h));
+    const int S = h->S, A = h->A, H = h->H;
+    const size_t G = (size_t)max_games;
+    auto al = [&](auto** p, size_t n) -> int { MZ_TRY(h, dalloc(h, p, n)); return 0; };
+    CK(al(&h->d_flat, h->nflat));
+    CK(al(&h->d_Wp, h->packed_w_n));
+    CK(al(&h->d_Bp, h->packed_b_n));
+    CK(hipMemset(h->d_flat, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
+    CK(repack(h));
+    // tables: libm log2/sqrt on the host, the values the oracle computes inline
+    std::vector<double> pbc(S + 2), sq(S + 2);
+    for (int n = 0; n < S + 2; ++n) {
+        pbc[n] = std::log2((double)(n + c.pb_c_base + 1) / (double)c.pb_c_base) + (double)c.pb_c_init;
+        sq[n] = std::sqrt((double)n);
+    }
+    std::vector<float> av(A);
+    for (int a = 0; a < A; ++a) av[a] = (float)((double)(a + 1) / (double)A);
+    CK(al(&h->d_pbc, pbc.size()));
+    CK(al(&h->d_sqrt, sq.size()));
+    CK(al(&h->d_aval, av.size()));
+    CK(hipMemcpy(h->d_pbc, pbc.data(), pbc.size() * 8, hipMemcpyHostToDevice) == hipSuccess ? 0 : fail(h, "copy"));
+    CK(hipMemcpy(h->d_sqrt, sq.data(), sq.size() * 8, hipMemcpyHostToDevice) == hipSuccess ? 0 : fail(h, "copy"));
+    CK(hipMemcpy(h->d_aval, av.data(), av.size() * 4, hipMemcpyHostToDevice) == hipSuccess ? 0 : fail(h, "copy"));
+    const size_t E = G * (size_t)(S + 1) * A;
+    CK(al(&h->d_eN, E)); CK(al(&h->d_eC, E)); CK(al(&h->d_eW, E)); CK(al(&h->d_eP, E)); CK(al(&h->d_eR, E));
+    CK(al(&h->d_ntp, G * (S + 1)));
+    CK(al(&h->d_hid, G * (S + 1) * H));
+    CK(al(&h->d_obs, G * h->obs_feat)); CK(al(&h->d_legal, G * A)); CK(al(&h->d_tp, G));
+    CK(al(&h->d_cv, G * A)); CK(al(&h->d_rv, G)); CK(al(&h->d_act, G));
+    CK(al(&h->d_m, h->nflat)); CK(al(&h->d_v, h->nflat)); CK(al(&h->d_grad, h->nflat));
+    CK(hipMemset(h->d_m, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
+    CK(hipMemset(h->d_v, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
+    CK(al(&h->d_loss, 8)); CK(al(&h->d_sq, 4));
+    CK(hipFuncSetAttribute((const void*)mz_search_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)search_lds_bytes(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute"));
+    CK(hipStreamSynchronize(h->stream) == hipSuccess ? 0 : fail(h, "sync"));
+#undef CK
+    *out = h;
+    return 0;
+}
+
+int mz_net_param_count(const mz_handle* h, int net, size_t* n) {
+    if (!h || !n || net < 0 || net > 2) return -2;
+    *n = h->nparams[net];
+    return 0;
+}
+
+int mz_grad_count(const mz_handle* h, size_t* n) {
+    if (!h || !n) return -2;
+    *n = h->nflat;
+    return 0;
+}
+
+int mz_weights_set(mz_handle* h, int net, const float* flat, size_t n) {
+    if (!h) return -2;
+    if (net < 0 || net > 2) return fail(h, "bad net id");
+    if (n != h->nparams[net]) return fail(h, "weights_set: wrong parameter count");
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipMemcpyAsync(h->d_flat + h->flat_off[net], flat, n * 4, hipMemcpyHostToDevice, h->stream));
+    if (repack(h)) return -1;
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int mz_weights_get(mz_handle* h, int net, float* flat, size_t n) {
+    if (!h) return -2;
+    if (net < 0 || net > 2) return fail(h, "bad net id");
+    if (n != h->nparams[net]) return fail(h, "weights_get: wrong parameter count");
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipMemcpyAsync(flat, h->d_flat + h->flat_off[net], n * 4, hipMemcpyDeviceToHost, h->stream));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int mz_net_forward(mz_handle* h, int net, const float* x, int n, float* out0, float* out1) {
+    if (!h) return -2;
+    if (net < 0 || net > 2) return fail(h, "bad net id");
+    if (n < 0) return fail(h, "negative batch");
+    if (n == 0) return 0;
+    MZ_TRY(h, hipSetDevice(h->device));
+    const int H = h->H, A = h->A;
+    const int in_feat = net == MZ_NET_REPR ? h->obs_feat : net == MZ_NET_PRED ? H : H + h->plane;
+    const int in_off = net == MZ_NET_REPR ? h->lay.x_rep : net == MZ_NET_PRED ? h->lay.x_pred : h->lay.x_dyn;
+    const int o0 = net == MZ_NET_PRED ? 1 : H;
+    const int o0_off = net == MZ_NET_PRED ? h->lay.v_out : h->lay.h_out;
+    const int o1 = net == MZ_NET_PRED ? A : 1;
+    const int o1_off = net == MZ_NET_PRED ? h->lay.p_out : h->lay.r_out;
+    float *dx = nullptr, *d0 = nullptr, *d1 = nullptr;
+    MZ_TRY(h, hipMalloc(&dx, (size_t)n * in_feat * 4));
+    MZ_TRY(h, hipMalloc(&d0, (size_t)n * o0 * 4));
+    MZ_TRY(h, hipMalloc(&d1, (size_t)n * o1 * 4));
+    hipMemcpyAsync(dx, x, (size_t)n * in_feat * 4, hipMemcpyHostToDevice, h->stream);
+    hipLaunchKernelGGL(mz_forward_kernel, dim3((n + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
+                       (size_t)h->lay.total * 4, h->stream, h->d_plan[net], h->d_Wp, h->d_Bp, h->lay.total, in_off,
+                       in_feat, dx, n, o0_off, o0, d0, o1_off, o1, net == MZ_NET_REPR ? nullptr : d1,
+                       net == MZ_NET_PRED ? 1 : 0);
+    hipError_t le = hipGetLastError();
+    hipMemcpyAsync(out0, d0, (size_t)n * o0 * 4, hipMemcpyDeviceToHost, h->stream);
+    if (out1 && net != MZ_NET_REPR) hipMemcpyAsync(out1, d1, (size_t)n * o1 * 4, hipMemcpyDeviceToHost, h->stream);
+    hipError_t se = hipStreamSynchronize(h->stream);
+    hipFree(dx); hipFree(d0); hipFree(d1);
+    MZ_TRY(h, le);
+    MZ_TRY(h, se);
+    return 0;
+}
+
+int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* legal_mask, const int32_t* to_play,
+                       int exploration, uint32_t rng_step, uint32_t game_offset, float temperature,
+                       float* child_visits, float* root_value, int32_t* action_out, void* stream) {
+    if (!h) return -2;
+    if (G < 0 || G > h->max_games) return fail(h, "G exceeds max_games");
+    if (G == 0) return 0;
+    SearchParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.G = G; P.S = h->S; P.A = h->A; P.H = h->H; P.players = h->conf.players; P.obs_feat = h->obs_feat;
+    P.plane = h->plane; P.exploration = exploration; P.rng_step = rng_step; P.game_offset = game_offset;
+    P.seed = h->seed; P.temperature = temperature; P.discount = h->conf.discount;
+    P.dirichlet_alpha = h->conf.dirichlet_alpha; P.exploration_eps = h->conf.exploration_eps;
+    P.obs = obs; P.legal = legal_mask; P.to_play = to_play;
+    P.child_visits = child_visits; P.root_value = root_value; P.action_out = action_out;
+    P.Wp = h->d_Wp; P.Bp = h->d_Bp; P.plan_root = h->d_plan[3]; P.plan_sim = h->d_plan[4];
+    P.lay = h->lay; P.pbc_tab = h->d_pbc; P.sqrt_tab = h->d_sqrt; P.aval_tab = h->d_aval;
+    P.eN = h->d_eN; P.eW = h->d_eW; P.eP = h->d_eP; P.eR = h->d_eR; P.eC = h->d_eC; P.ntp = h->d_ntp;
+    P.hid = h->d_hid; P.tree_stride = (h->S + 1) * h->A;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    hipLaunchKernelGGL(mz_search_kernel, dim3((G + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
+                       search_lds_bytes(h), st, P);
+    MZ_TRY(h, hipGetLastError());
+    return 0;
+}
+
+int mz_mcts_search(mz_handle* h, int G, const float* obs, const uint8_t* legal_mask, const int32_t* to_play,
+                   int exploration, uint32_t rng_step, uint32_t game_offset, float temperature, float* child_visits,
+                   float* root_value, int32_t* action_out) {
+    if (!h) return -2;
+    if (G < 0 || G > h->max_games) return fail(h, "G exceeds max_games");
+    if (G == 0) return 0;
+    const int A = h->A;
+    for (int g = 0; g < G; ++g) {       // @assert !isempty(legal_actions) (SelfPlay.jl:243)
+        int any = 0;
+        for (int a = 0; a < A; ++a) any |= legal_mask[(size_t)g * A + a] != 0;
+        if (!any) return fail(h, "Legal actions should not be an empty array (game " + std::to_string(g) + ")");
+        if (to_play[g] < 1 || to_play[g] > h->conf.players) return fail(h, "to_play out of range");
+    }
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipMemcpyAsync(h->d_obs, obs, (size_t)G * h->obs_feat * 4, hipMemcpyHostToDevice, h->stream));
+    MZ_TRY(h, hipMemcpyAsync(h->d_legal, legal_mask, (size_t)G * A, hipMemcpyHostToDevice, h->stream));
+    MZ_TRY(h, hipMemcpyAsync(h->d_tp, to_play, (size_t)G * 4, hipMemcpyHostToDevice, h->stream));
+    int rc = mz_mcts_search_dev(h, G, h->d_obs, h->d_legal, h->d_tp, exploration, rng_step, game_offset, temperature,
+                                h->d_cv, h->d_rv, h->d_act, h->stream);
+    if (rc) return rc;
+    MZ_TRY(h, hipMemcpyAsync(child_visits, h->d_cv, (size_t)G * A * 4, hipMemcpyDeviceToHost, h->stream));
+    MZ_TRY(h, hipMemcpyAsync(root_value, h->d_rv, (size_t)G * 4, hipMemcpyDeviceToHost, h->stream));
+    MZ_TRY(h, hipMemcpyAsync(action_out, h->d_act, (size_t)G * 4, hipMemcpyDeviceToHost, h->stream));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int mz_debug_tree(mz_handle* h, int G, int32_t* eN, float* eW, float* eP, float* eR, int32_t* eC, int32_t* ntp) {
+    if (!h) return -2;
+    if (G < 0 || G > h->max_games) return fail(h, "G exceeds max_games");
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    const size_t E = (size_t)G * (h->S + 1) * h->A;
+    if (eN) MZ_TRY(h, hipMemcpy(eN, h->d_eN, E * 4, hipMemcpyDeviceToHost));
+    if (eW) MZ_TRY(h, hipMemcpy(eW, h->d_eW, E * 4, hipMemcpyDeviceToHost));
+    if (eP) MZ_TRY(h, hipMemcpy(eP, h->d_eP, E * 4, hipMemcpyDeviceToHost));
+    if (eR) MZ_TRY(h, hipMemcpy(eR, h->d_eR, E * 4, hipMemcpyDeviceToHost));
+    if (eC) MZ_TRY(h, hipMemcpy(eC, h->d_eC, E * 4, hipMemcpyDeviceToHost));
+    if (ntp) MZ_TRY(h, hipMemcpy(ntp, h->d_ntp, (size_t)G * (h->S + 1) * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+// ------------------------------------------------------------- learner
+static int ensure_batch(mz_handle* h, int B) {
+    if (B <= h->bcap) return 0;
+    const int K = h->conf.num_unroll_steps, A = h->A;
+    float** bufs[] = {&h->d_bobs, &h->d_bact, &h->d_btv, &h->d_btr, &h->d_btp, &h->d_bgs, &h->d_pv, &h->d_pp, &h->d_pr};
+    size_t sizes[] = {(size_t)B * h->obs_feat, (size_t)B * (K + 1), (size_t)B * (K + 1), (size_t)B * (K + 1),
+                      (size_t)B * (K + 1) * A, (size_t)B, (size_t)B * (K + 1), (size_t)B * (K + 1) * A,
+                      (size_t)B * (K + 1)};
+    for (int i = 0; i < 9; ++i) MZ_TRY(h, dalloc(h, bufs[i], sizes[i]));
+    h->bcap = B;
+    return 0;
+}
+
+// forward unroll + losses + ∇ = 2θ into grad_dev (device batch pointers)
+int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, void* stream) {
+    if (!h || !b) return -2;
+    const int B = b->batch_size, K = h->conf.num_unroll_steps, A = h->A;
+    if (B < 1) return fail(h, "batch_size must be >= 1");
+    if (ensure_batch(h, B)) return -1;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    UnrollParams U;
+    U.B = B; U.K = K; U.A = A; U.H = h->H; U.plane = h->plane; U.obs_feat = h->obs_feat;
+    U.obs = b->observation; U.actions = b->actions; U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
+    U.Wp = h->d_Wp; U.Bp = h->d_Bp; U.plan_repr = h->d_plan[0]; U.plan_sim = h->d_plan[4]; U.lay = h->lay;
+    hipLaunchKernelGGL(mz_unroll_kernel, dim3((B + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
+                       (size_t)h->lay.total * 4, st, U);
+    float* lo = losses_dev ? losses_dev : h->d_loss;
+    hipLaunchKernelGGL(mz_loss_kernel, dim3(1), dim3(MZ_THREADS), 0, st, B, K, A, h->d_pv, h->d_pp,
+                       b->target_values, b->target_policies, b->gradient_scale, lo);
+    MZ_TRY(h, hipMemsetAsync(h->d_sq, 0, 3 * sizeof(double), st));
+    for (int net = 0; net < 3; ++net)
+        hipLaunchKernelGGL(mz_sqnorm_kernel, dim3(64), dim3(MZ_THREADS), 0, st, h->d_flat + h->flat_off[net],
+                           h->nparams[net], h->d_sq + net);
+    hipLaunchKernelGGL(mz_l2_finish_kernel, dim3(1), dim3(64), 0, st, h->d_sq, lo);
+    float* g = grad_dev ? grad_dev : h->d_grad;
+    hipLaunchKernelGGL(mz_grad_2theta_kernel, dim3(128), dim3(MZ_THREADS), 0, st, h->d_flat, g, h->nflat);
+    MZ_TRY(h, hipGetLastError());
+    return 0;
+}
+
+int mz_learner_apply_dev(mz_handle* h, const float* grad_dev, float grad_scale, double eta, void* stream) {
+    if (!h) return -2;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    const float* g = grad_dev ? grad_dev : h->d_grad;
+    hipLaunchKernelGGL(mz_adam_kernel, dim3(128), dim3(MZ_THREADS), 0, st, h->d_flat, h->d_m, h->d_v, g,
+                       grad_scale, h->nflat, h->bp1, h->bp2, eta);
+    h->bp1 = h->bp1 * 0.9;                  // βp .= βp .* β
+    h->bp2 = h->bp2 * 0.999;
+    const int T = 256;
+    hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_w_n + T - 1) / T)), dim3(T), 0, st, h->d_flat,
+                       h->d_srcW, h->d_Wp, h->packed_w_n);
+    hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_b_n + T - 1) / T)), dim3(T), 0, st, h->d_flat,
+                       h->d_srcB, h->d_Bp, h->packed_b_n);
+    MZ_TRY(h, hipGetLastError());
+    return 0;
+}
+
+int mz_learner_step(mz_handle* h, const mz_batch* b, double eta, float* losses_out) {
+    if (!h || !b) return -2;
+    const int B = b->batch_size, K = h->conf.num_unroll_steps, A = h->A;
+    MZ_TRY(h, hipSetDevice(h->device));
+    if (B < 1) return fail(h, "batch_size must be >= 1");
+    if (ensure_batch(h, B)) return -1;
+    hipStream_t st = h->stream;
+    MZ_TRY(h, hipMemcpyAsync(h->d_bobs, b->observation, (size_t)B * h->obs_feat * 4, hipMemcpyHostToDevice, st));
+    MZ_TRY(h, hipMemcpyAsync(h->d_bact, b->actions, (size_t)B * (K + 1) * 4, hipMemcpyHostToDevice, st));
+    MZ_TRY(h, hipMemcpyAsync(h->d_btv, b->target_values, (size_t)B * (K + 1) * 4, hipMemcpyHostToDevice, st));
+    MZ_TRY(h, hipMemcpyAsync(h->d_btr, b->target_rewards, (size_t)B * (K + 1) * 4, hipMemcpyHostToDevice, st));
+    MZ_TRY(h, hipMemcpyAsync(h->d_btp, b->target_policies, (size_t)B * (K + 1) * A * 4, hipMemcpyHostToDevice, st));
+    MZ_TRY(h, hipMemcpyAsync(h->d_bgs, b->gradient_scale, (size_t)B * 4, hipMemcpyHostToDevice, st));
+    mz_batch db = *b;
+    db.observation = h->d_bobs; db.actions = h->d_bact; db.target_values = h->d_btv;
+    db.target_rewards = h->d_btr; db.target_policies = h->d_btp; db.gradient_scale = h->d_bgs;
+    int rc = mz_learner_grad_dev(h, &db, h->d_grad, h->d_loss, st);
+    if (rc) return rc;
+    rc = mz_learner_apply_dev(h, h->d_grad, 1.0f, eta, st);
+    if (rc) return rc;
+    if (losses_out) MZ_TRY(h, hipMemcpyAsync(losses_out, h->d_loss, 6 * 4, hipMemcpyDeviceToHost, st));
+    MZ_TRY(h, hipStreamSynchronize(st));
+    return 0;
+}
+
+int mz_sync(mz_handle* h) {
+    if (!h) return -2;
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+}  // extern "C"

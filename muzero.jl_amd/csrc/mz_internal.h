@@ -1,0 +1,103 @@
+// mz_internal.h — shared declarations of the libmz HIP engine (gfx950).
+//
+// The three FC networks (Learning.jl:87-142) are executed as "plans": a plan
+// is a list of stages separated by workgroup barriers; a stage is a list of
+// tasks; a task is one 16-row output block of one Dense layer, computed by
+// one wavefront as a 16 (outputs) x 16 (games/samples) tile with f32 MFMA
+// (v_mfma_f32_16x16x4_f32).  Activations live in LDS as [rows][16] f32
+// (row = feature, column = game of the workgroup's tile).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mz.h"
+#include "../../include/mz_detmath.h"
+
+#pragma clang fp contract(off)
+
+#define MZ_TILE 16          // games (or samples) per workgroup tile = MFMA N
+#define MZ_THREADS 256      // 4 wavefronts
+#define MZ_MAX_STAGES 64
+
+// One Dense layer inside a plan.  All offsets are in floats.
+struct LayerDesc {
+    int w_off;     // packed weights: [n_ob][4*nq k-steps][64 lanes]
+    int b_off;     // packed bias: [n_ob*16]
+    int nq;        // k-steps per quarter (= ceil(K/16)); kq = 4*nq k values
+    int n_ob;      // output blocks of 16 rows
+    int act;       // MZ_ACT_*
+    int in_off;    // LDS activation input  [16*nq*4 rows][16]
+    int out_off;   // LDS activation output [n_ob*16 rows][16]
+    int out_rows;  // real outputs
+};
+
+// Device plan image (int array):
+//   [0] n_stages, [1] n_layers, [2] n_tasks,
+//   [3 .. 3+n_stages]            stage_begin (n_stages+1 entries),
+//   then n_tasks x {layer, ob},  then n_layers x LayerDesc.
+struct PlanView {
+    int n_stages, n_layers, n_tasks;
+    const int* stage_begin;
+    const int* tasks;
+    const LayerDesc* layers;
+};
+
+__device__ __forceinline__ PlanView plan_view(const int* p) {
+    PlanView v;
+    v.n_stages = p[0]; v.n_layers = p[1]; v.n_tasks = p[2];
+    v.stage_begin = p + 3;
+    v.tasks = v.stage_begin + v.n_stages + 1;
+    v.layers = reinterpret_cast<const LayerDesc*>(v.tasks + 2 * v.n_tasks);
+    return v;
+}
+
+// LDS region offsets of the standard activation layout (floats); the host
+// fills this and passes it by value.
+struct ActLayout {
+    int x_rep, x_pred, x_dyn;     // inputs: stacked obs, hidden, state-action
+    int h_out, v_out, p_out, r_out;
+    int rows_rep, rows_pred, rows_dyn;   // padded input rows (zeroed)
+    int total;                    // floats
+};
+
+// Search-kernel parameters (passed by value).
+struct SearchParams {
+    int G, S, A, H, players, obs_feat;     // obs_feat = stacked features
+    int plane;                             // W*H of the board (action plane size)
+    int exploration;
+    uint32_t rng_step, game_offset;
+    uint64_t seed;
+    float temperature, discount, dirichlet_alpha, exploration_eps;
+    // inputs
+    const float* obs; const uint8_t* legal; const int32_t* to_play;
+    // outputs
+    float* child_visits; float* root_value; int32_t* action_out;
+    // model
+    const float* Wp; const float* Bp;
+    const int* plan_root; const int* plan_sim;
+    ActLayout lay;
+    // tables (host-computed with libm so the oracle matches bit-exactly)
+    const double* pbc_tab;    // log2((N + base + 1)/base) + c_init, N = 0..S+1
+    const double* sqrt_tab;   // sqrt(N), N = 0..S+1
+    const float* aval_tab;    // Float32(a / |A|), a = 1..A
+    // tree storage (global): edges [G][S+1][A], node to_play [G][S+1], hidden [G][S+1][H]
+    int32_t* eN; float* eW; float* eP; float* eR; int32_t* eC; int32_t* ntp;
+    float* hid;
+    int tree_stride;          // (S+1)*A per game
+};
+
+// Learner unroll-kernel parameters.
+struct UnrollParams {
+    int B, K, A, H, plane, obs_feat;
+    const float* obs;        // (obs_feat, B)
+    const float* actions;    // (K+1, B) float action ids
+    float* pv;               // (K+1, B) predicted values
+    float* pp;               // (A, K+1, B) predicted policies (probabilities)
+    float* pr;               // (K+1, B) predicted rewards
+    const float* Wp; const float* Bp;
+    const int* plan_repr; const int* plan_sim;
+    ActLayout lay;
+};
+
+__host__ __device__ inline int mz_round16(int x) { return (x + 15) & ~15; }

@@ -1,0 +1,790 @@
+/*
+ * mz_oracle.c — CPU ORACLE (test infrastructure only).
+ *
+ * A plain-C restatement of deveshjawla/MuZero.jl's hot path in its
+ * documented `ref_semantics` (SURVEY.md §2.1, quirks Q1–Q17), used ONLY by
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the
+ * checker.  The product (libmz) never links, loads or calls it.
+ *
+ * PARITY UNPINNED: the reference is Julia-only and Julia is absent from this
+ * image and the GPU box, and the reference ships no tests,
+ * fixtures or golden vectors.  This restatement is therefore checked by an
+ * independent Python mirror written from the Julia source
+ * (tests/mirror_ref.py) and the networks against torch-CPU fp32 autograd-free
+ * forwards; golden vectors under tests/golden/ are generated from it by
+ * tests/golden/make_golden.py.
+ *
+ * Contract decisions where the reference is not reproducible (Q6) or its
+ * third-party arithmetic is unavailable (Flux/NNlib/Distributions):
+ *   - RNG: Philox4x32-10 streams (include/mz_detmath.h) replace Julia's
+ *     global unseeded RNG and MersenneTwister(1234);
+ *   - children are visited in ascending action order (reference: Dict order);
+ *   - Dense dot products use the canonical order of mz_dot below;
+ *   - exp/tanh/log are the deterministic det_* functions.
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/mz.h"
+#include "../include/mz_detmath.h"
+
+#define EXPORT __attribute__((visibility("default")))
+#define MAXA MZ_MAX_ACTIONS
+
+/* ===================================================================== nets
+ * Learning.jl:70-142.  Layer list of each FC net in Flux.params order.   */
+typedef struct { int in, out, act; size_t woff, boff; } OLayer;
+typedef struct {
+    int n[3];            /* layers in trunk, head 1, head 2 (head counts 0 for repr) */
+    OLayer L[3][64];
+    size_t nparams;
+    int softmax_head2;   /* prediction policy head ends in softmax (Learning.jl:113-114) */
+} ONet;
+
+static void onet_add(ONet* net, int part, int in, int out, int act) {
+    OLayer* l = &net->L[part][net->n[part]++];
+    l->in = in; l->out = out; l->act = act;
+    l->woff = net->nparams; net->nparams += (size_t)in * out;
+    l->boff = net->nparams; net->nparams += (size_t)out;
+}
+
+/* init_representation (Learning.jl:87-98) / init_prediction (:100-116) /
+ * init_dynamics (:118-142) for FeedForwardHP. */
+static void onet_build(ONet* net, int which, const mz_config* c, const mz_ffhp* hp) {
+    memset(net, 0, sizeof(*net));
+    int W = c->observation_shape[0], H = c->observation_shape[1], C = c->observation_shape[2];
+    int hs = hp->width_hidden, hid = hp->hidden_state_size, A = c->action_space_size;
+    if (which == MZ_NET_REPR) {
+        int indim = W * H * (C * (c->stacked_observations + 1) + c->stacked_observations); /* :88 */
+        onet_add(net, 0, indim, hs, MZ_ACT_RELU);
+        for (int i = 0; i < hp->depth_representation; ++i) onet_add(net, 0, hs, hs, MZ_ACT_RELU);
+        onet_add(net, 0, hs, hid, MZ_ACT_IDENTITY);
+    } else if (which == MZ_NET_PRED) {
+        onet_add(net, 0, hid, hs, MZ_ACT_RELU);
+        for (int i = 0; i < hp->depth_prediction; ++i) onet_add(net, 0, hs, hs, MZ_ACT_RELU);
+        for (int i = 0; i < hp->depth_value; ++i) onet_add(net, 1, hs, hs, MZ_ACT_RELU);
+        onet_add(net, 1, hs, 1, MZ_ACT_TANH);                                  /* :110 */
+        for (int i = 0; i < hp->depth_policy; ++i) onet_add(net, 2, hs, hs, MZ_ACT_RELU);
+        onet_add(net, 2, hs, A, MZ_ACT_IDENTITY);                              /* :113 */
+        net->softmax_head2 = 1;                                                 /* :114 */
+    } else {
+        int indim = W * H * (C + 1);                                            /* :120 */
+        onet_add(net, 0, indim, hs, MZ_ACT_RELU);
+        for (int i = 0; i < hp->depth_dynamics; ++i) onet_add(net, 0, hs, hs, MZ_ACT_RELU);
+        for (int i = 0; i < hp->depth_state_head; ++i) onet_add(net, 1, hs, hs, MZ_ACT_RELU);
+        onet_add(net, 1, hs, hid, MZ_ACT_IDENTITY);                            /* :136 */
+        for (int i = 0; i < hp->depth_reward; ++i) onet_add(net, 2, hs, hs, MZ_ACT_RELU);
+        onet_add(net, 2, hs, 1, hp->reward_activation);                        /* :140 */
+    }
+}
+
+/* Canonical dot product of the engine: four partial fmaf chains over
+ * contiguous k-quarters of length kq = 4*ceil(K/16), each started at +0,
+ * combined as ((p0+p1)+(p2+p3)).  Flux's `W*x` (BLAS) has no fixed order;
+ * this one is what the GPU's four-accumulator f32 MFMA chain computes.   */
+static float mz_dot(const float* Wcol /* W(out,in) col-major */, int out, int in, int o, const float* x) {
+    int kq = 4 * ((in + 15) / 16);
+    float p[4];
+    for (int q = 0; q < 4; ++q) {
+        p[q] = 0.0f;
+        int k1 = (q + 1) * kq < in ? (q + 1) * kq : in;
+        for (int k = q * kq; k < k1; ++k) p[q] = fmaf(Wcol[o + (size_t)out * k], x[k], p[q]);
+    }
+    return (p[0] + p[1]) + (p[2] + p[3]);
+}
+
+static float act_apply(int act, float v) {
+    if (act == MZ_ACT_RELU) return mz_relu(v);
+    if (act == MZ_ACT_TANH) return det_tanhf(v);
+    return v;
+}
+
+/* Flux Dense: σ.(W*x .+ b) */
+static void dense_fwd(const OLayer* l, const float* P, const float* x, float* y) {
+    for (int o = 0; o < l->out; ++o)
+        y[o] = act_apply(l->act, mz_dot(P + l->woff, l->out, l->in, o, x) + P[l->boff + o]);
+}
+
+/* NNlib softmax over n entries: max, exp(x - max), sequential sum, divide. */
+static void softmax_n(const float* x, int n, float* y) {
+    float m = x[0];
+    for (int i = 1; i < n; ++i) m = m > x[i] ? m : x[i];
+    float s = 0.0f;
+    for (int i = 0; i < n; ++i) { y[i] = det_expf(x[i] - m); s = s + y[i]; }
+    for (int i = 0; i < n; ++i) y[i] = y[i] / s;
+}
+
+static void run_chain(const ONet* net, int part, const float* P, const float* x, float* y) {
+    float a[1024], b[1024];
+    const float* cur = x;
+    for (int i = 0; i < net->n[part]; ++i) {
+        float* dst = (i & 1) ? b : a;
+        dense_fwd(&net->L[part][i], P, cur, dst);
+        cur = dst;
+    }
+    memcpy(y, cur, sizeof(float) * net->L[part][net->n[part] - 1].out);
+}
+
+/* forward of one sample; REPR: out0 = h; PRED: out0 = value, out1 = policy;
+ * DYN: out0 = h', out1 = reward.  The Split applies both heads to the trunk
+ * output (Learning.jl:68). */
+static void net_forward1(const ONet* net, const float* P, const float* x, float* out0, float* out1) {
+    float t[1024];
+    run_chain(net, 0, P, x, net->n[1] ? t : out0);
+    if (!net->n[1]) return;
+    run_chain(net, 1, P, t, out0);
+    if (net->softmax_head2) {
+        float lg[MAXA];
+        run_chain(net, 2, P, t, lg);
+        softmax_n(lg, net->L[2][net->n[2] - 1].out, out1);
+    } else {
+        run_chain(net, 2, P, t, out1);
+    }
+}
+
+EXPORT size_t ora_param_count(const mz_config* c, const mz_ffhp* hp, int which) {
+    ONet n; onet_build(&n, which, c, hp); return n.nparams;
+}
+
+/* batched forward, column-major (features, n) */
+EXPORT void ora_net_forward(const mz_config* c, const mz_ffhp* hp, int which, const float* P,
+                            const float* x, int n, float* out0, float* out1) {
+    ONet net; onet_build(&net, which, c, hp);
+    int in = net.L[0][0].in;
+    int o0 = which == MZ_NET_PRED ? 1 : hp->hidden_state_size;
+    int o1 = which == MZ_NET_PRED ? c->action_space_size : 1;
+    for (int i = 0; i < n; ++i)
+        net_forward1(&net, P, x + (size_t)i * in, out0 + (size_t)i * o0, out1 ? out1 + (size_t)i * o1 : NULL);
+}
+
+/* ===================================================================== MCTS
+ * SelfPlay.jl:22-306 */
+typedef struct {
+    int visit_count;      /* :63 */
+    int to_play;          /* :64 default 1 */
+    float prior;          /* :65 */
+    float value_sum;      /* :66 */
+    int expanded;         /* children !== nothing (:72) */
+    int child[MAXA];      /* node index per action (0-based action), -1 = none */
+    int hslot;            /* hidden_state (expanded slot), -1 = nothing */
+    float reward;         /* :69 */
+    int eslot;            /* expanded-node slot (0 = root, s+1 = sim s), -1 */
+} ONode;
+
+typedef struct { float min, max; } MinMax;                       /* :22-25 */
+static void mm_update(MinMax* m, float v) {                       /* :27-31 */
+    m->min = m->min < v ? m->min : v;
+    m->max = m->max > v ? m->max : v;
+}
+static float mm_normalize(const MinMax* m, float v) {             /* :33-39 */
+    if (m->max > m->min) return (v - m->min) / (m->max - m->min);
+    return v;
+}
+
+typedef struct {
+    const mz_config* c;
+    const mz_ffhp* hp;
+    ONet nrep, npred, ndyn;
+    const float *Prep, *Ppred, *Pdyn;
+    uint64_t seed;
+    int H, A, S;
+    ONode* nodes; int nn;
+    float* hid;            /* (S+1) * H */
+} OCtx;
+
+static float node_value(const ONode* n) {                         /* :76-82 */
+    if (n->visit_count == 0) return 0.0f;
+    return n->value_sum / (float)n->visit_count;
+}
+
+static int new_node(OCtx* X, float prior) {
+    ONode* n = &X->nodes[X->nn];
+    memset(n, 0, sizeof(*n));
+    n->to_play = 1; n->prior = prior; n->hslot = -1; n->eslot = -1;
+    for (int a = 0; a < MAXA; ++a) n->child[a] = -1;
+    return X->nn++;
+}
+
+/* expand_node! (:88-96): priors = softmax over the (already softmaxed, Q3)
+ * policy entries of `actions` (the ROOT's legal set at every depth, Q4). */
+static void expand_node(OCtx* X, int ni, const uint8_t* legal, int to_play, float reward,
+                        const float* policy, int hslot, int eslot) {
+    float v[MAXA], p[MAXA]; int acts[MAXA], n = 0;
+    for (int a = 0; a < X->A; ++a) if (legal[a]) { acts[n] = a; v[n] = policy[a]; ++n; }
+    softmax_n(v, n, p);
+    for (int i = 0; i < n; ++i) {
+        int ci = new_node(X, p[i]);
+        X->nodes[ni].child[acts[i]] = ci;
+    }
+    ONode* node = &X->nodes[ni];
+    node->expanded = 1;
+    node->to_play = to_play;
+    node->reward = reward;
+    node->hslot = hslot;
+    node->eslot = eslot;
+}
+
+/* add_exploration_noise! (:102-109) */
+static void add_noise(OCtx* X, int ni, uint32_t game, uint32_t step) {
+    ONode* node = &X->nodes[ni];
+    int acts[MAXA], n = 0;
+    for (int a = 0; a < X->A; ++a) if (node->child[a] >= 0) acts[n++] = a;
+    float noise[MAXA];
+    mz_dirichlet(X->seed, game, step, n, X->c->dirichlet_alpha, noise);
+    float one_m = 1.0f - X->c->exploration_eps;
+    for (int i = 0; i < n; ++i) {
+        ONode* ch = &X->nodes[node->child[acts[i]]];
+        ch->prior = ch->prior * one_m + noise[i] * X->c->exploration_eps;
+    }
+}
+
+/* ucb_score (:171-184), quirk Q5: pb_c and prior_score in Float64, the sum
+ * rounded once to Float32 by the ::Float32 return annotation. */
+static float ucb_score(OCtx* X, const ONode* parent, const ONode* child, const MinMax* mm) {
+    const mz_config* c = X->c;
+    double pb_c = log2((double)(parent->visit_count + c->pb_c_base + 1) / (double)c->pb_c_base)
+                  + (double)c->pb_c_init;
+    pb_c = pb_c * (sqrt((double)parent->visit_count) / (double)(child->visit_count + 1));
+    double prior_score = pb_c * (double)child->prior;
+    float value_score = 0.0f;
+    if (child->visit_count > 0) {
+        float q = node_value(child);
+        float t = c->players == 1 ? c->discount * q : c->discount * (-q);
+        value_score = mm_normalize(mm, child->reward + t);
+    }
+    return (float)(prior_score + (double)value_score);
+}
+
+/* select_child (:157-166): argmax UCB, uniform tie-break (Philox TIE). */
+static int select_child(OCtx* X, int ni, const MinMax* mm, uint32_t game, uint32_t step,
+                        int sim, int depth, int* action_out) {
+    const ONode* node = &X->nodes[ni];
+    float u[MAXA]; int acts[MAXA], n = 0;
+    for (int a = 0; a < X->A; ++a) if (node->child[a] >= 0) {
+        acts[n] = a; u[n] = ucb_score(X, node, &X->nodes[node->child[a]], mm); ++n;
+    }
+    float m = u[0];
+    for (int i = 1; i < n; ++i) m = m > u[i] ? m : u[i];     /* maximum */
+    int ties[MAXA], nt = 0;
+    for (int i = 0; i < n; ++i) if (u[i] == m) ties[nt++] = i;
+    uint32_t r = mz_rng_u32(X->seed, MZ_RNG_TIE, game, step, ((uint32_t)sim << 12) | (uint32_t)depth);
+    int pick = ties[mz_rng_below(r, (uint32_t)nt)];
+    *action_out = acts[pick];
+    return node->child[acts[pick]];
+}
+
+/* backpropagate! (:190-217), quirk Q7 */
+static void backpropagate(OCtx* X, const int* path, int len, float value, int to_play, MinMax* mm) {
+    const mz_config* c = X->c;
+    if (c->players == 1) {
+        for (int i = len - 1; i >= 0; --i) {
+            ONode* node = &X->nodes[path[i]];
+            node->value_sum = node->value_sum + value;
+            node->visit_count += 1;
+            mm_update(mm, node->reward + c->discount * node_value(node));
+            value = node->reward + c->discount * value;
+        }
+    } else if (c->players == 2) {
+        for (int i = len - 1; i >= 0; --i) {
+            ONode* node = &X->nodes[path[i]];
+            if (node->to_play == to_play) node->value_sum = node->value_sum + value;
+            else node->value_sum = node->value_sum - value;
+            node->visit_count += 1;
+            mm_update(mm, node->reward + c->discount * node_value(node));
+            if (node->to_play == to_play) value = -node->reward;
+            else value = node->reward + c->discount * value;
+        }
+    }
+    /* > 2 players: the reference builds an ErrorException it never throws (:214) */
+}
+
+/* run_mcts (:230-285).  Returns the root node index.  `sims` statistics:
+ * stats[0] += sum of select depths, stats[1] = max depth. */
+static int run_mcts(OCtx* X, const float* obs, const uint8_t* legal, int to_play, int exploration,
+                    uint32_t game, uint32_t step, int64_t* stats) {
+    const mz_config* c = X->c;
+    int H = X->H, A = X->A;
+    X->nn = 0;
+    int root = new_node(X, 0.0f);                                   /* :232 */
+    float* h0 = X->hid;                                             /* slot 0 */
+    net_forward1(&X->nrep, X->Prep, obs, h0, NULL);                 /* :234 */
+    float v0, pol[MAXA];
+    net_forward1(&X->npred, X->Ppred, h0, &v0, pol);                /* :239 */
+    expand_node(X, root, legal, to_play, 0.0f, pol, 0, 0);          /* :245 */
+    if (exploration) add_noise(X, root, game, step);                /* :247-249 */
+    MinMax mm = {INFINITY, -INFINITY};                              /* :251 */
+    int* path = (int*)malloc(sizeof(int) * (X->S + 2));
+    float sa[1024];
+    for (int it = 0; it < X->S; ++it) {                             /* :254 */
+        int node = root, vtp = to_play, len = 0, depth = 0, action = 0;
+        path[len++] = node;
+        while (X->nodes[node].expanded) {                           /* :261 */
+            depth += 1;
+            node = select_child(X, node, &mm, game, step, it, depth, &action);
+            path[len++] = node;
+            vtp = (vtp % c->players) + 1;                           /* mod1(vtp+1, P), :267 */
+        }
+        if (stats) { stats[0] += depth; if (depth > stats[1]) stats[1] = depth; }
+        ONode* parent = &X->nodes[path[len - 2]];                   /* :270 */
+        float* ph = X->hid + (size_t)parent->hslot * H;
+        float value, pl[MAXA];
+        net_forward1(&X->npred, X->Ppred, ph, &value, pl);          /* :271 (Q2) */
+        /* make_state_action (:7-14): parent.hidden_state .*= 2 IN PLACE (Q1),
+         * action plane Float32(a / |A|) with a 1-based. */
+        for (int i = 0; i < H; ++i) ph[i] = ph[i] * 2.0f;
+        memcpy(sa, ph, sizeof(float) * H);
+        int plane = c->observation_shape[0] * c->observation_shape[1];
+        float aval = (float)((double)(action + 1) / (double)A);
+        for (int i = 0; i < plane; ++i) sa[H + i] = aval;
+        int slot = it + 1;
+        float* nh = X->hid + (size_t)slot * H;
+        float reward;
+        net_forward1(&X->ndyn, X->Pdyn, sa, nh, &reward);           /* :275 */
+        expand_node(X, node, legal, vtp, reward, pl, slot, slot);   /* :280 */
+        backpropagate(X, path, len, value, vtp, &mm);               /* :281 */
+    }
+    free(path);
+    return root;
+}
+
+/* select_action (:293-306) with Philox ACTION stream; T==1 samples the
+ * integer visit counts exactly. Returns the 0-based action. */
+static int select_action(OCtx* X, int root, float temperature, uint32_t game, uint32_t step) {
+    const ONode* node = &X->nodes[root];
+    int acts[MAXA], cnt[MAXA], n = 0;
+    for (int a = 0; a < X->A; ++a) if (node->child[a] >= 0) {
+        acts[n] = a; cnt[n] = X->nodes[node->child[a]].visit_count; ++n;
+    }
+    uint32_t r = mz_rng_u32(X->seed, MZ_RNG_ACTION, game, step, 0);
+    if (temperature == 0.0f) {
+        int best = 0;
+        for (int i = 1; i < n; ++i) if (cnt[i] > cnt[best]) best = i;
+        return acts[best];
+    }
+    if (isinf(temperature)) return acts[mz_rng_below(r, (uint32_t)n)];
+    if (temperature == 1.0f) {
+        uint32_t tot = 0;
+        for (int i = 0; i < n; ++i) tot += (uint32_t)cnt[i];
+        if (tot == 0) return acts[mz_rng_below(r, (uint32_t)n)];
+        uint32_t t = mz_rng_below(r, tot), cum = 0;
+        for (int i = 0; i < n; ++i) { cum += (uint32_t)cnt[i]; if (cum > t) return acts[i]; }
+        return acts[n - 1];
+    }
+    float e = 1.0f / temperature;
+    float w[MAXA], s = 0.0f;
+    for (int i = 0; i < n; ++i) {
+        w[i] = cnt[i] > 0 ? (float)det_exp(det_log((double)cnt[i]) * (double)e) : 0.0f;
+        s = s + w[i];
+    }
+    float u = (float)(r >> 8) * 5.9604644775390625e-08f * s;
+    float cum = 0.0f;
+    for (int i = 0; i < n; ++i) { cum = cum + w[i]; if (cum > u) return acts[i]; }
+    return acts[n - 1];
+}
+
+static void ctx_init(OCtx* X, const mz_config* c, const mz_ffhp* hp, const float* Prep,
+                     const float* Ppred, const float* Pdyn, uint64_t seed) {
+    X->c = c; X->hp = hp;
+    onet_build(&X->nrep, MZ_NET_REPR, c, hp);
+    onet_build(&X->npred, MZ_NET_PRED, c, hp);
+    onet_build(&X->ndyn, MZ_NET_DYN, c, hp);
+    X->Prep = Prep; X->Ppred = Ppred; X->Pdyn = Pdyn;
+    X->seed = seed;
+    X->H = hp->hidden_state_size; X->A = c->action_space_size; X->S = c->num_iters;
+    X->nodes = (ONode*)malloc(sizeof(ONode) * (size_t)(1 + (X->S + 1) * X->A));
+    X->hid = (float*)malloc(sizeof(float) * (size_t)(X->S + 1) * X->H);
+}
+static void ctx_free(OCtx* X) { free(X->nodes); free(X->hid); }
+
+/* store_search_stats! (:115-122) for one game */
+static void search_stats(OCtx* X, int root, float* child_visits, float* root_value) {
+    const ONode* node = &X->nodes[root];
+    int sum = 0;
+    for (int a = 0; a < X->A; ++a) if (node->child[a] >= 0) sum += X->nodes[node->child[a]].visit_count;
+    for (int a = 0; a < X->A; ++a)
+        child_visits[a] = node->child[a] >= 0
+            ? (float)((double)X->nodes[node->child[a]].visit_count / (double)sum) : 0.0f;
+    *root_value = node_value(node);
+}
+
+/* Dump the tree in the engine's slot layout (see mz_debug_tree). */
+static void dump_tree(OCtx* X, int g, int G, int32_t* eN, float* eW, float* eP, float* eR,
+                      int32_t* ech, int32_t* ntp) {
+    int S = X->S, A = X->A;
+    for (int i = 0; i < X->nn; ++i) {
+        const ONode* n = &X->nodes[i];
+        if (!n->expanded) continue;
+        int e = n->eslot;
+        if (ntp) ntp[(size_t)g * (S + 1) + e] = n->to_play;
+        for (int a = 0; a < A; ++a) {
+            size_t k = ((size_t)g * (S + 1) + e) * A + a;
+            int ci = n->child[a];
+            const ONode* ch = ci >= 0 ? &X->nodes[ci] : NULL;
+            if (eN) eN[k] = ch ? ch->visit_count : 0;
+            if (eW) eW[k] = ch ? ch->value_sum : 0.0f;
+            if (eP) eP[k] = ch ? ch->prior : 0.0f;
+            if (eR) eR[k] = ch && ch->expanded ? ch->reward : 0.0f;
+            if (ech) ech[k] = ch && ch->expanded ? ch->eslot : -1;
+        }
+    }
+    (void)G;
+}
+
+/* Batched search: the ABI of mz_mcts_search, on the CPU. */
+EXPORT int ora_mcts_search(const mz_config* c, const mz_ffhp* hp, const float* Prep, const float* Ppred,
+                           const float* Pdyn, uint64_t seed, int G, const float* obs,
+                           const uint8_t* legal_mask, const int32_t* to_play, int exploration,
+                           uint32_t rng_step, uint32_t game_offset, float temperature,
+                           float* child_visits, float* root_value, int32_t* action_out,
+                           int32_t* eN, float* eW, float* eP, float* eR, int32_t* ech, int32_t* ntp,
+                           int64_t* stats) {
+    OCtx X; ctx_init(&X, c, hp, Prep, Ppred, Pdyn, seed);
+    int A = X.A;
+    int in = X.nrep.L[0][0].in;
+    for (int g = 0; g < G; ++g) {
+        uint32_t gid = game_offset + (uint32_t)g;
+        int root = run_mcts(&X, obs + (size_t)g * in, legal_mask + (size_t)g * A, to_play[g],
+                            exploration, gid, rng_step, stats);
+        search_stats(&X, root, child_visits + (size_t)g * A, root_value + g);
+        action_out[g] = select_action(&X, root, temperature, gid, rng_step) + 1;
+        if (eN || eW || eP || eR || ech || ntp) dump_tree(&X, g, G, eN, eW, eP, eR, ech, ntp);
+    }
+    ctx_free(&X);
+    return 0;
+}
+
+/* ============================================================== TicTacToe
+ * games/tictactoe/game.jl, quirk Q14.  Board = BitArray(3,3,3) planes
+ * [p1, p2, empty]; action a -> CartesianIndices((3,3))[a] = cell a-1.    */
+typedef struct { uint8_t b[27]; int player; } OTTT;
+
+static const int LINES[8][3] = {{0,3,6},{1,4,7},{2,5,8},{0,1,2},{3,4,5},{6,7,8},{0,4,8},{6,4,2}};
+
+static void ttt_reset(OTTT* e) {                                   /* :15-20 */
+    memset(e->b, 0, 27); for (int i = 0; i < 9; ++i) e->b[18 + i] = 1; e->player = 1;
+}
+/* is_win(env, _): checks env.player's plane (the player TO MOVE), :102-115 */
+static int ttt_is_win(const OTTT* e) {
+    const uint8_t* pl = e->b + 9 * (e->player - 1);
+    for (int l = 0; l < 8; ++l) if (pl[LINES[l][0]] && pl[LINES[l][1]] && pl[LINES[l][2]]) return 1;
+    return 0;
+}
+static void ttt_legal(const OTTT* e, uint8_t* mask) {               /* :35-43 */
+    int w = ttt_is_win(e);
+    for (int i = 0; i < 9; ++i) mask[i] = w ? 0 : e->b[18 + i];
+}
+static void ttt_step(OTTT* e, int a1) {                             /* :45-52 */
+    int c = a1 - 1;
+    e->b[18 + c] = 0; e->b[9 * (e->player - 1) + c] = 1;
+    e->player = (e->player % 2) + 1;
+}
+/* state-table entry built by walk (:117-147): winner = 1 if the side to
+ * move has a line (labelled 1 whoever owns it), terminated = full || win. */
+static int ttt_terminated(const OTTT* e) {
+    int empty = 0; for (int i = 0; i < 9; ++i) empty |= e->b[18 + i];
+    return !(empty && !ttt_is_win(e));
+}
+static float ttt_reward(const OTTT* e, int p) {                     /* :87-100 */
+    if (!ttt_terminated(e)) return 0.0f;
+    if (!ttt_is_win(e)) return 0.0f;
+    return p == 1 ? 1.0f : -1.0f;
+}
+
+EXPORT void ora_ttt_step(uint8_t* board, int32_t* player, int action, uint8_t* legal_out,
+                         float* reward_out, int32_t* done_out) {
+    OTTT e; memcpy(e.b, board, 27); e.player = *player;
+    int p = e.player;
+    ttt_step(&e, action);
+    memcpy(board, e.b, 27); *player = e.player;
+    if (legal_out) ttt_legal(&e, legal_out);
+    if (reward_out) *reward_out = ttt_reward(&e, p);
+    if (done_out) *done_out = ttt_terminated(&e);
+}
+
+/* get_stacked_observations (SelfPlay.jl:128-149), Q15: channels
+ * [obs_t, action plane (raw action id), obs_{t-1}, ...], zeros before t=1.
+ * obs_hist is (W*H*C, T) column-major; index is 1-based. */
+EXPORT void ora_stacked_obs(const mz_config* c, const float* obs_hist, const int32_t* action_hist,
+                            int index, float* out) {
+    int plane = c->observation_shape[0] * c->observation_shape[1];
+    int osz = plane * c->observation_shape[2];
+    memcpy(out, obs_hist + (size_t)(index - 1) * osz, sizeof(float) * osz);
+    float* o = out + osz;
+    for (int past = index - 1; past >= index - c->stacked_observations; --past) {
+        if (past >= 1) {
+            for (int i = 0; i < plane; ++i) o[i] = (float)action_hist[past - 1];
+            memcpy(o + plane, obs_hist + (size_t)(past - 1) * osz, sizeof(float) * osz);
+        } else {
+            memset(o, 0, sizeof(float) * (plane + osz));
+        }
+        o += plane + osz;
+    }
+}
+
+/* play_game (SelfPlay.jl:330-382) for one TicTacToe game, opponent "self".
+ * Move t uses RNG step step0 + t.  Outputs are GameHistory columns sized
+ * for max_moves+1 moves; returns the number of moves T.                   */
+EXPORT int ora_play_game(const mz_config* c, const mz_ffhp* hp, const float* Prep, const float* Ppred,
+                         const float* Pdyn, uint64_t seed, uint32_t game_id, uint32_t step0,
+                         float temperature, float* obs_hist, int32_t* action_hist, float* reward_hist,
+                         int32_t* to_play_hist, float* child_visits, float* root_values) {
+    OCtx X; ctx_init(&X, c, hp, Prep, Ppred, Pdyn, seed);
+    OTTT env; ttt_reset(&env);
+    int A = X.A, T = 0, done = 0;
+    float stacked[1024];
+    while (!done && T <= c->max_moves) {                           /* :343 */
+        float temp = temperature;
+        if (c->temperature_threshold >= 0 && T >= c->temperature_threshold) temp = 0.0f;
+        int p = env.player;                                         /* :351 */
+        for (int i = 0; i < 27; ++i) obs_hist[(size_t)T * 27 + i] = (float)env.b[i];   /* :352 */
+        ora_stacked_obs(c, obs_hist, action_hist, T + 1, stacked);  /* :355 */
+        uint8_t legal[MAXA]; ttt_legal(&env, legal);
+        uint32_t step = step0 + (uint32_t)T;
+        int root = run_mcts(&X, stacked, legal, p, 1, game_id, step, NULL);   /* :359 */
+        int a = select_action(&X, root, temp, game_id, step) + 1; /* :360 */
+        ttt_step(&env, a);                                          /* :366 */
+        float r = ttt_reward(&env, p);                              /* :367 */
+        done = ttt_terminated(&env);                                /* :368 */
+        search_stats(&X, root, child_visits + (size_t)T * A, root_values + T);   /* :375 */
+        action_hist[T] = a; reward_hist[T] = r; to_play_hist[T] = p; /* :377-379 */
+        ++T;
+    }
+    ctx_free(&X);
+    return T;
+}
+
+/* ========================================================= replay buffer
+ * src/ReplayBuffer.jl.  A history is passed as column arrays of length T. */
+typedef struct {
+    int32_t T;
+    const float* obs;          /* (27, T) observation_history */
+    const int32_t* actions;    /* (T) action_history, 1-based ids */
+    const float* rewards;      /* (T) reward_history */
+    const int32_t* to_play;    /* (T) to_play_history */
+    const float* child_visits; /* (A, T) */
+    const float* root_values;  /* (T) */
+} OHist;
+
+/* discount^n: Julia's Float32^Int (llvm.pow.f32) ≈ round-to-f32 of pow(f64) */
+static float disc_pow(float g, int n) { return (float)pow((double)g, (double)n); }
+
+/* compute_target_value (:5-20), Q9; index is 1-based */
+EXPORT float ora_compute_target_value(const mz_config* c, const OHist* h, int index) {
+    int bi = index + c->td_steps;
+    float value;
+    if (bi < h->T) {
+        float rv = h->root_values[bi - 1];
+        float last = h->to_play[bi - 1] == h->to_play[index - 1] ? rv : -rv;
+        value = last * disc_pow(c->discount, c->td_steps);
+        for (int i = 1; i <= c->td_steps + 1; ++i) {                 /* enumerate(reward_history[index:bi]) */
+            float r = h->rewards[index + i - 2];
+            float sr = h->to_play[index - 1] == h->to_play[index + i - 1] ? r : -r;
+            value = value + sr * disc_pow(c->discount, i);
+        }
+    } else {
+        value = 0.0f;
+    }
+    return value;
+}
+
+/* make_target (:25-50); absorbing-state actions from Philox ABSORB */
+static void make_target(const mz_config* c, const OHist* h, int state_index, uint64_t seed,
+                        uint32_t sample, uint32_t step, float* tv, float* tr, float* tp, float* ta) {
+    int A = c->action_space_size, K = c->num_unroll_steps;
+    for (int k = 0; k <= K; ++k) {
+        int ci = state_index + k;
+        if (ci < h->T) {
+            tv[k] = ora_compute_target_value(c, h, ci);
+            tr[k] = h->rewards[ci - 1];
+            for (int a = 0; a < A; ++a) tp[(size_t)k * A + a] = h->child_visits[(size_t)(ci - 1) * A + a];
+            ta[k] = (float)h->actions[ci - 1];
+        } else if (ci == h->T) {
+            tv[k] = 0.0f;
+            tr[k] = h->rewards[ci - 1];
+            for (int a = 0; a < A; ++a) tp[(size_t)k * A + a] = 1.0f / (float)A;
+            ta[k] = (float)h->actions[ci - 1];
+        } else {
+            tv[k] = 0.0f; tr[k] = 0.0f;
+            for (int a = 0; a < A; ++a) tp[(size_t)k * A + a] = 1.0f / (float)A;
+            ta[k] = (float)(mz_rng_below(mz_rng_u32(seed, MZ_RNG_ABSORB, sample, step, (uint32_t)k), (uint32_t)A) + 1);
+        }
+    }
+}
+
+/* get_batch (:188-217) over a buffer of n histories (ids first_id..).
+ * Uniform sampling (PER=false): sample_n_games (:102), sample_position (:80).
+ * Outputs column-major as the reference's batch tuple; idx_out (2,B) =
+ * (game_id, position). */
+EXPORT void ora_get_batch(const mz_config* c, const OHist* hist, int n, int first_id, uint64_t seed,
+                          uint32_t step, float* obs, float* actions, float* values, float* rewards,
+                          float* policies, float* gscale, int32_t* idx_out) {
+    int A = c->action_space_size, K = c->num_unroll_steps, B = c->batch_size;
+    int osz = c->observation_shape[0] * c->observation_shape[1] *
+              (c->observation_shape[2] * (c->stacked_observations + 1) + c->stacked_observations);
+    for (int b = 0; b < B; ++b) {
+        int gi = (int)mz_rng_below(mz_rng_u32(seed, MZ_RNG_GAME, (uint32_t)b, step, 0), (uint32_t)n);
+        const OHist* h = &hist[gi];
+        int pos = (int)mz_rng_below(mz_rng_u32(seed, MZ_RNG_POS, (uint32_t)b, step, 0), (uint32_t)h->T) + 1;
+        make_target(c, h, pos, seed, (uint32_t)b, step, values + (size_t)b * (K + 1),
+                    rewards + (size_t)b * (K + 1), policies + (size_t)b * (K + 1) * A,
+                    actions + (size_t)b * (K + 1));
+        ora_stacked_obs(c, h->obs, h->actions, pos, obs + (size_t)b * osz);
+        int gs = h->T + 1 - pos;                                     /* :212 */
+        gscale[b] = (float)(K < gs ? K : gs);
+        idx_out[2 * b] = first_id + gi; idx_out[2 * b + 1] = pos;
+    }
+}
+
+/* ================================================================ learner
+ * Learning.jl:261-413 in ref_semantics (Q10, Q11). */
+
+/* logsoftmax (NNlib) + logitcrossentropy for one (A) column */
+static float policy_ce(const float* yhat, const float* y, int A) {
+    float m = yhat[0];
+    for (int i = 1; i < A; ++i) m = m > yhat[i] ? m : yhat[i];
+    float s = 0.0f;
+    for (int i = 0; i < A; ++i) s = s + det_expf(yhat[i] - m);
+    float ls = det_logf(s);
+    float ce = 0.0f;
+    for (int i = 0; i < A; ++i) ce = ce + y[i] * ((yhat[i] - m) - ls);
+    return -ce;
+}
+
+/* The forward unroll: predictions values (K+1,B), policies (A,K+1,B),
+ * rewards (K+1,B) exactly as Learning.jl:347-370 builds them (Q10). */
+EXPORT void ora_unroll(const mz_config* c, const mz_ffhp* hp, const float* Prep, const float* Ppred,
+                       const float* Pdyn, int B, const float* obs, const float* actions,
+                       float* pv, float* pp, float* pr) {
+    ONet nr, np, nd;
+    onet_build(&nr, MZ_NET_REPR, c, hp); onet_build(&np, MZ_NET_PRED, c, hp); onet_build(&nd, MZ_NET_DYN, c, hp);
+    int H = hp->hidden_state_size, A = c->action_space_size, K = c->num_unroll_steps;
+    int in = nr.L[0][0].in;
+    int plane = c->observation_shape[0] * c->observation_shape[1];
+    float h[1024], sa[1024], v, pol[MAXA];
+    for (int b = 0; b < B; ++b) {
+        net_forward1(&nr, Prep, obs + (size_t)b * in, h, NULL);          /* :347 */
+        net_forward1(&np, Ppred, h, &v, pol);                            /* :351 */
+        pv[(size_t)b * (K + 1)] = v; pr[(size_t)b * (K + 1)] = 0.0f;      /* :352 zeros */
+        memcpy(pp + (size_t)b * (K + 1) * A, pol, sizeof(float) * A);
+        for (int i = 1; i <= K; ++i) {                                   /* :355 */
+            net_forward1(&np, Ppred, h, &v, pol);                        /* :356 */
+            /* make_dynamics_input (:293-304): actions ./= |A| (Float32), 2h */
+            float a = actions[(size_t)b * (K + 1) + (i - 1)] / (float)A;
+            for (int j = 0; j < H; ++j) sa[j] = h[j] * 2.0f;
+            for (int j = 0; j < plane; ++j) sa[H + j] = a;
+            float r;
+            net_forward1(&nd, Pdyn, sa, h, &r);                          /* :362 */
+            pv[(size_t)b * (K + 1) + i] = v;                             /* :367-369 */
+            pr[(size_t)b * (K + 1) + i] = r;
+            memcpy(pp + ((size_t)b * (K + 1) + i) * A, pol, sizeof(float) * A);
+        }
+    }
+}
+
+/* loss (:261-288) data terms; l2 = sum(sqnorm, params) per net in f64. */
+EXPORT void ora_losses(const mz_config* c, int B, const float* pv, const float* pp, const float* tv,
+                       const float* tp, const float* gscale, float* value_loss, float* policy_loss) {
+    int A = c->action_space_size, K = c->num_unroll_steps;
+    /* value: mse(agg = mean((sum(x, dims=1) ./ g) .* 1)) */
+    float vs = 0.0f;
+    for (int j = 0; j < B; ++j) {
+        float s = 0.0f;
+        for (int k = 0; k <= K; ++k) {
+            float d = pv[(size_t)j * (K + 1) + k] - tv[(size_t)j * (K + 1) + k];
+            s = s + d * d;
+        }
+        vs = vs + s / gscale[j];
+    }
+    *value_loss = vs / (float)B;
+    /* policy: (1,1,B) ./ (1,B) broadcast to (1,B,B) then mean (Q11) */
+    float ce[4096];
+    for (int j = 0; j < B; ++j) {
+        float s = 0.0f;
+        for (int k = 0; k <= K; ++k)
+            s = s + policy_ce(pp + ((size_t)j * (K + 1) + k) * A, tp + ((size_t)j * (K + 1) + k) * A, A);
+        ce[j] = s;
+    }
+    float ps = 0.0f;
+    for (int j = 0; j < B; ++j)
+        for (int k = 0; k < B; ++k) ps = ps + ce[k] / gscale[j];
+    *policy_loss = ps / (float)((size_t)B * B);
+}
+
+EXPORT double ora_sqnorm(const float* P, size_t n) {
+    double s = 0.0;
+    for (size_t i = 0; i < n; ++i) s += (double)P[i] * (double)P[i];
+    return s;
+}
+
+/* Flux 0.12 ADAMW() = Optimiser(ADAM(η, (0.9, 0.999)), WeightDecay(0));
+ * apply!(ADAM): mt, vt in Float32 arrays, arithmetic in Float64 (β, η are
+ * Float64), Δ^2 in Float32 (literal_pow); WeightDecay(0) is the identity.
+ * The gradient is 2θ (Q11).  bp = βp state (Float64[β1^t, β2^t]).        */
+EXPORT void ora_adam_2theta(float* P, float* m, float* v, size_t n, const double* bp, double eta) {
+    const double b1 = 0.9, b2 = 0.999, eps = 1e-8;
+    for (size_t i = 0; i < n; ++i) {
+        float g = P[i] * 2.0f;
+        m[i] = (float)(b1 * (double)m[i] + (1.0 - b1) * (double)g);
+        float g2 = g * g;
+        v[i] = (float)(b2 * (double)v[i] + (1.0 - b2) * (double)g2);
+        float d = (float)((double)m[i] / (1.0 - bp[0]) / (sqrt((double)v[i] / (1.0 - bp[1])) + eps) * eta);
+        P[i] = P[i] - d;
+    }
+}
+
+/* ParameterSchedulers 0.2.3 Cos(λ0, λ1, period) with Stateful (1-based t):
+ * |λ0−λ1|·(1 + cos(2π(t−1)/period))/2 + min(λ0, λ1). */
+EXPORT double ora_cos_schedule(double l0, double l1, int period, int t) {
+    double range = fabs(l0 - l1), off = l0 < l1 ? l0 : l1;
+    double a = 6.283185307179586 * (double)(t - 1) / (double)period;
+    return range * (1.0 + cos(a)) / 2.0 + off;
+}
+
+/* One full ref_semantics learner step: forward unroll + losses + ADAM on
+ * all three nets; bp is advanced (βp .= βp .* β).                          */
+EXPORT void ora_learner_step(const mz_config* c, const mz_ffhp* hp, float* Prep, float* Ppred, float* Pdyn,
+                             float* m_all, float* v_all, double* bp, int B, const float* obs,
+                             const float* actions, const float* tv, const float* tp, const float* gscale,
+                             double eta, float* losses) {
+    int A = c->action_space_size, K = c->num_unroll_steps;
+    float* pv = (float*)malloc(sizeof(float) * (size_t)B * (K + 1));
+    float* pr = (float*)malloc(sizeof(float) * (size_t)B * (K + 1));
+    float* pp = (float*)malloc(sizeof(float) * (size_t)B * (K + 1) * A);
+    ora_unroll(c, hp, Prep, Ppred, Pdyn, B, obs, actions, pv, pp, pr);
+    ora_losses(c, B, pv, pp, tv, tp, gscale, &losses[0], &losses[2]);
+    losses[1] = 0.0f;                                  /* intermediate_rewards = false */
+    size_t n0 = ora_param_count(c, hp, MZ_NET_REPR), n1 = ora_param_count(c, hp, MZ_NET_PRED),
+           n2 = ora_param_count(c, hp, MZ_NET_DYN);
+    losses[3] = (float)ora_sqnorm(Prep, n0);
+    losses[4] = (float)ora_sqnorm(Ppred, n1);
+    losses[5] = (float)ora_sqnorm(Pdyn, n2);
+    ora_adam_2theta(Prep, m_all, v_all, n0, bp, eta);
+    ora_adam_2theta(Ppred, m_all + n0, v_all + n0, n1, bp, eta);
+    ora_adam_2theta(Pdyn, m_all + n0 + n1, v_all + n0 + n1, n2, bp, eta);
+    bp[0] = bp[0] * 0.9; bp[1] = bp[1] * 0.999;
+    free(pv); free(pr); free(pp);
+}
+
+/* ======================================================== detmath exports
+ * for tests (accuracy vs libm) and the Python mirror */
+EXPORT float ora_det_expf(float x) { return det_expf(x); }
+EXPORT float ora_det_tanhf(float x) { return det_tanhf(x); }
+EXPORT float ora_det_logf(float x) { return det_logf(x); }
+EXPORT double ora_det_exp(double x) { return det_exp(x); }
+EXPORT double ora_det_log(double x) { return det_log(x); }
+EXPORT uint32_t ora_rng_u32(uint64_t seed, uint32_t purpose, uint32_t id, uint32_t step, uint32_t idx) {
+    return mz_rng_u32(seed, purpose, id, step, idx);
+}
+EXPORT void ora_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t* out) {
+    mz_u32x4 r = mz_philox(c0, c1, c2, c3, k0, k1);
+    memcpy(out, r.v, 16);
+}
+EXPORT void ora_dirichlet(uint64_t seed, uint32_t game, uint32_t step, int n, float alpha, float* out) {
+    mz_dirichlet(seed, game, step, n, alpha, out);
+}
+EXPORT void ora_softmax(const float* x, int n, float* y) { softmax_n(x, n, y); }
+EXPORT float ora_dot(const float* Wcol, int out, int in, int o, const float* x) { return mz_dot(Wcol, out, in, o, x); }

@@ -1,0 +1,202 @@
+"""ctypes wrapper of the CPU oracle (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg as the checker; never by the product package.
+PARITY UNPINNED (see mz_oracle.c header): the Julia reference cannot run here.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+_VP = ctypes.c_void_p
+_lib = None
+
+
+class OHist(ctypes.Structure):
+    _fields_ = [("T", ctypes.c_int32), ("obs", _VP), ("actions", _VP), ("rewards", _VP),
+                ("to_play", _VP), ("child_visits", _VP), ("root_values", _VP)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        L.ora_param_count.restype = ctypes.c_size_t
+        L.ora_param_count.argtypes = [_VP, _VP, ctypes.c_int]
+        L.ora_net_forward.argtypes = [_VP, _VP, ctypes.c_int, _VP, _VP, ctypes.c_int, _VP, _VP]
+        L.ora_mcts_search.restype = ctypes.c_int
+        L.ora_mcts_search.argtypes = [_VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_int, _VP, _VP, _VP,
+                                      ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float,
+                                      _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]
+        L.ora_play_game.restype = ctypes.c_int
+        L.ora_play_game.argtypes = [_VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                    ctypes.c_float, _VP, _VP, _VP, _VP, _VP, _VP]
+        L.ora_ttt_step.argtypes = [_VP, _VP, ctypes.c_int, _VP, _VP, _VP]
+        L.ora_stacked_obs.argtypes = [_VP, _VP, _VP, ctypes.c_int, _VP]
+        L.ora_compute_target_value.restype = ctypes.c_float
+        L.ora_compute_target_value.argtypes = [_VP, ctypes.POINTER(OHist), ctypes.c_int]
+        L.ora_get_batch.argtypes = [_VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32,
+                                    _VP, _VP, _VP, _VP, _VP, _VP, _VP]
+        L.ora_unroll.argtypes = [_VP, _VP, _VP, _VP, _VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP]
+        L.ora_losses.argtypes = [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP, _VP]
+        L.ora_sqnorm.restype = ctypes.c_double
+        L.ora_sqnorm.argtypes = [_VP, ctypes.c_size_t]
+        L.ora_adam_2theta.argtypes = [_VP, _VP, _VP, ctypes.c_size_t, _VP, ctypes.c_double]
+        L.ora_cos_schedule.restype = ctypes.c_double
+        L.ora_cos_schedule.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int]
+        L.ora_learner_step.argtypes = [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_int, _VP, _VP, _VP,
+                                       _VP, _VP, ctypes.c_double, _VP]
+        for n, r, a in [("ora_det_expf", ctypes.c_float, [ctypes.c_float]),
+                        ("ora_det_tanhf", ctypes.c_float, [ctypes.c_float]),
+                        ("ora_det_logf", ctypes.c_float, [ctypes.c_float]),
+                        ("ora_det_exp", ctypes.c_double, [ctypes.c_double]),
+                        ("ora_det_log", ctypes.c_double, [ctypes.c_double])]:
+            getattr(L, n).restype = r
+            getattr(L, n).argtypes = a
+        L.ora_rng_u32.restype = ctypes.c_uint32
+        L.ora_rng_u32.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+        L.ora_philox.argtypes = [ctypes.c_uint32] * 6 + [_VP]
+        L.ora_dirichlet.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_float, _VP]
+        L.ora_softmax.argtypes = [_VP, ctypes.c_int, _VP]
+        L.ora_dot.restype = ctypes.c_float
+        L.ora_dot.argtypes = [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, _VP]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(_VP)
+
+
+class Oracle:
+    """The oracle bound to one (Config, FeedForwardHP) and three flat weight vectors."""
+
+    def __init__(self, cconf, chp, seed=0):
+        self.L = lib()
+        self.cconf = cconf
+        self.chp = chp
+        self.seed = seed
+        self.A = cconf.action_space_size
+        self.H = chp.hidden_state_size
+        self.S = cconf.num_iters
+        self.K = cconf.num_unroll_steps
+        self.params = [np.zeros(self.param_count(i), np.float32) for i in range(3)]
+
+    def _c(self):
+        return ctypes.byref(self.cconf), ctypes.byref(self.chp)
+
+    def param_count(self, net):
+        c, h = self._c()
+        return self.L.ora_param_count(c, h, net)
+
+    def set_weights(self, net, flat):
+        self.params[net] = np.ascontiguousarray(flat, dtype=np.float32).copy()
+
+    def forward(self, net, x):
+        c, h = self._c()
+        x = np.ascontiguousarray(x, np.float32)
+        n = x.shape[0]
+        if net == 1:
+            o0, o1 = np.empty((n, 1), np.float32), np.empty((n, self.A), np.float32)
+        elif net == 2:
+            o0, o1 = np.empty((n, self.H), np.float32), np.empty((n, 1), np.float32)
+        else:
+            o0, o1 = np.empty((n, self.H), np.float32), None
+        self.L.ora_net_forward(c, h, net, _p(self.params[net]), _p(x), n, _p(o0), _p(o1))
+        return (o0, o1) if o1 is not None else o0
+
+    def mcts_search(self, obs, legal, to_play, exploration=True, rng_step=0, game_offset=0, temperature=1.0,
+                    dump=False):
+        c, h = self._c()
+        obs = np.ascontiguousarray(obs, np.float32)
+        G = obs.shape[0]
+        legal = np.ascontiguousarray(legal, np.uint8)
+        tp = np.ascontiguousarray(to_play, np.int32)
+        cv = np.empty((G, self.A), np.float32)
+        rv = np.empty(G, np.float32)
+        act = np.empty(G, np.int32)
+        stats = np.zeros(2, np.int64)
+        tree = None
+        if dump:
+            S, A = self.S, self.A
+            tree = dict(N=np.zeros((G, S + 1, A), np.int32), W=np.zeros((G, S + 1, A), np.float32),
+                        P=np.zeros((G, S + 1, A), np.float32), R=np.zeros((G, S + 1, A), np.float32),
+                        C=np.full((G, S + 1, A), -1, np.int32), to_play=np.zeros((G, S + 1), np.int32))
+        t = tree or {}
+        self.L.ora_mcts_search(c, h, _p(self.params[0]), _p(self.params[1]), _p(self.params[2]), self.seed, G,
+                               _p(obs), _p(legal), _p(tp), int(exploration), rng_step & 0xffffffff, game_offset,
+                               temperature, _p(cv), _p(rv), _p(act), _p(t.get("N")), _p(t.get("W")),
+                               _p(t.get("P")), _p(t.get("R")), _p(t.get("C")), _p(t.get("to_play")), _p(stats))
+        out = (cv, rv, act)
+        if dump:
+            return out + (tree, stats)
+        return out
+
+    def play_game(self, game_id=0, step0=0, temperature=1.0):
+        c, h = self._c()
+        M = self.cconf.max_moves + 1
+        A = self.A
+        obs = np.zeros((M, 27), np.float32)
+        acts = np.zeros(M, np.int32)
+        rew = np.zeros(M, np.float32)
+        tp = np.zeros(M, np.int32)
+        cv = np.zeros((M, A), np.float32)
+        rv = np.zeros(M, np.float32)
+        T = self.L.ora_play_game(c, h, _p(self.params[0]), _p(self.params[1]), _p(self.params[2]), self.seed,
+                                 game_id, step0, temperature, _p(obs), _p(acts), _p(rew), _p(tp), _p(cv), _p(rv))
+        return dict(observation=obs[:T].copy(), action=acts[:T].copy(), reward=rew[:T].copy(),
+                    to_play=tp[:T].copy(), child_visits=cv[:T].copy(), root_values=rv[:T].copy())
+
+    def unroll(self, obs, actions):
+        c, h = self._c()
+        B = obs.shape[0]
+        K, A = self.K, self.A
+        pv = np.empty((B, K + 1), np.float32)
+        pp = np.empty((B, K + 1, A), np.float32)
+        pr = np.empty((B, K + 1), np.float32)
+        self.L.ora_unroll(c, h, _p(self.params[0]), _p(self.params[1]), _p(self.params[2]), B,
+                          _p(np.ascontiguousarray(obs, np.float32)), _p(np.ascontiguousarray(actions, np.float32)),
+                          _p(pv), _p(pp), _p(pr))
+        return pv, pp, pr
+
+    def learner_state(self):
+        n = sum(p.size for p in self.params)
+        return dict(m=np.zeros(n, np.float32), v=np.zeros(n, np.float32), bp=np.array([0.9, 0.999]))
+
+    def learner_step(self, state, batch, eta):
+        c, h = self._c()
+        a = {k: np.ascontiguousarray(batch[k], np.float32) for k in
+             ("observation", "actions", "target_values", "target_policies", "gradient_scale")}
+        losses = np.empty(6, np.float32)
+        B = a["observation"].shape[0]
+        self.L.ora_learner_step(c, h, _p(self.params[0]), _p(self.params[1]), _p(self.params[2]), _p(state["m"]),
+                                _p(state["v"]), _p(state["bp"]), B, _p(a["observation"]), _p(a["actions"]),
+                                _p(a["target_values"]), _p(a["target_policies"]), _p(a["gradient_scale"]),
+                                eta, _p(losses))
+        return losses
+
+
+def histories_to_c(histories):
+    """list of dicts (observation (T,27), action, reward, to_play, child_visits (T,A), root_values)
+    -> (array of OHist, keepalive)."""
+    arr = (OHist * len(histories))()
+    keep = []
+    for i, hst in enumerate(histories):
+        cols = [np.ascontiguousarray(hst["observation"], np.float32), np.ascontiguousarray(hst["action"], np.int32),
+                np.ascontiguousarray(hst["reward"], np.float32), np.ascontiguousarray(hst["to_play"], np.int32),
+                np.ascontiguousarray(hst["child_visits"], np.float32),
+                np.ascontiguousarray(hst["root_values"], np.float32)]
+        keep.append(cols)
+        arr[i] = OHist(len(cols[1]), *[_p(x) for x in cols])
+    return arr, keep
