@@ -1,0 +1,202 @@
+"""bench.py — MCTS node-expansions/s (+ learner steps/s) on MI355X.
+
+Workload (BASELINE.json configs[1]): TicTacToe FC net (games/tictactoe/
+params.jl hyper, 74,881 fp32 params, random glorot init), 512 concurrent
+games per GPU, 50 simulations per move.  One step = one batched run_mcts +
+select_action over the 512 games (a single search-kernel launch) from real
+TicTacToe positions already resident in HBM; each step uses a fresh RNG step
+key.  Multi-GPU: games shard across ranks (no data-path collective) ->
+"scaling": "weak"; the learner leg all-reduces its gradient bucket over RCCL.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import dataclasses
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (import before libmz: one shared HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+import _mzpkg  # noqa: E402
+
+_mzpkg.load()
+from muzero_jl_amd.abi import Engine  # noqa: E402
+from muzero_jl_amd.config import cos_schedule, to_c_config, to_c_ffhp  # noqa: E402
+from muzero_jl_amd.games import tictactoe as ttt  # noqa: E402
+from muzero_jl_amd.networks import init_nets  # noqa: E402
+from muzero_jl_amd.selfplay import random_positions  # noqa: E402
+
+METRIC = "self-play MCTS node-expansions/sec + train steps/sec, TicTacToe FC net, 1-8 GPU"
+F_EXP = 2 * (22848 + 32768)          # FLOP per expansion: prediction + dynamics
+F_ROOT = 2 * (18048 + 22848)         # FLOP per root: representation + prediction
+PEAK_F32 = 157.3                     # TFLOP/s, MI355X_MICROARCH.md (f32 MFMA = f32 vector peak)
+
+
+def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0):
+    """The oracle (C restatement of the reference semantics, 1 thread) on a
+    bounded sample of the same workload: 32-game batches of the same
+    positions, 50 sims/move, until `budget_s` of CPU time has been spent."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    o = Oracle(to_c_config(conf), to_c_ffhp(hyper), seed=1)
+    for n, w in enumerate(nets):
+        o.set_weights(n, w)
+    n_games, t0, step = 0, time.perf_counter(), 0
+    while time.perf_counter() - t0 < budget_s:
+        i = (step * 32) % (obs.shape[0] - 32 + 1)
+        o.mcts_search(obs[i:i + 32], legal[i:i + 32], tp[i:i + 32], exploration=True, rng_step=step)
+        n_games += 32
+        step += 1
+    dt = time.perf_counter() - t0
+    return dict(value=n_games * conf.num_iters / dt, unit="node-expansions/s", cores=1, kind="port",
+                sample=f"{n_games} games x {conf.num_iters} sims (32-game batches of the bench positions), "
+                       f"oracle/mz_oracle.c single thread, {dt:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--games", type=int, default=512)
+    ap.add_argument("--sims", type=int, default=50)
+    ap.add_argument("--learner-steps", type=int, default=50)
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.Stream(device=dev)        # non-null stream shared with libmz (events see it)
+    torch.cuda.set_stream(stream)
+    sp = stream.cuda_stream
+
+    conf = dataclasses.replace(ttt.conf, num_iters=args.sims)
+    hyper = ttt.hyper
+    G, S = args.games, args.sims
+    nets = init_nets(conf, hyper, seed=1234)              # identical replicas on every rank
+    eng = Engine(conf, hyper, device=local, max_games=G, rng_seed=1)
+    for n, w in enumerate(nets):
+        eng.set_weights(n, w)
+
+    obs, legal, tp = random_positions(ttt.BatchedTicTacToe, G, seed=100 + rank)
+    d_obs = torch.from_numpy(obs).to(dev)
+    d_legal = torch.from_numpy(legal.astype(np.uint8)).to(dev)
+    d_tp = torch.from_numpy(tp.astype(np.int32)).to(dev)
+    d_cv = torch.empty((G, 9), dtype=torch.float32, device=dev)
+    d_rv = torch.empty(G, dtype=torch.float32, device=dev)
+    d_act = torch.empty(G, dtype=torch.int32, device=dev)
+
+    def step(k):
+        eng.mcts_search_dev(G, d_obs.data_ptr(), d_legal.data_ptr(), d_tp.data_ptr(), d_cv.data_ptr(),
+                            d_rv.data_ptr(), d_act.data_ptr(), exploration=True, rng_step=k,
+                            game_offset=rank * G, temperature=1.0, stream=sp)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        step(args.warmup + k)
+        evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    assert np.all(legal[np.arange(G), d_act.cpu().numpy() - 1]), "illegal action selected"
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # ---- learner leg: ref_semantics learner step at B = batch_size (32),
+    # gradient bucket all-reduced over RCCL when world > 1
+    B, K, A = conf.batch_size, conf.num_unroll_steps, 9
+    rng = np.random.default_rng(7 + rank)
+    tpol = rng.random((B, K + 1, A)).astype(np.float32)
+    tpol /= tpol.sum(-1, keepdims=True)
+    bt = [torch.from_numpy(x).to(dev) for x in (
+        (rng.random((B, 63)) < 0.4).astype(np.float32), rng.integers(1, 10, (B, K + 1)).astype(np.float32),
+        rng.uniform(-1, 1, (B, K + 1)).astype(np.float32), np.zeros((B, K + 1), np.float32), tpol,
+        rng.integers(1, K + 1, B).astype(np.float32))]
+    grad = torch.empty(eng.grad_count(), dtype=torch.float32, device=dev)
+    losses = torch.empty(8, dtype=torch.float32, device=dev)
+
+    def lstep(k):
+        eng.learner_grad_dev([x.data_ptr() for x in bt], B, grad.data_ptr(), losses.data_ptr(), stream=sp)
+        if world > 1:
+            dist.all_reduce(grad)
+        eng.learner_apply_dev(grad.data_ptr(), 1.0 / world, cos_schedule(k + 1), stream=sp)
+
+    for k in range(5):
+        lstep(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    tl0 = time.perf_counter()
+    for k in range(args.learner_steps):
+        lstep(5 + k)
+    torch.cuda.synchronize()
+    tl = torch.tensor([time.perf_counter() - tl0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tl, op=dist.ReduceOp.MAX)
+    learner_sps = args.learner_steps / float(tl.item())
+
+    if rank == 0:
+        total_exp = world * G * S * args.steps
+        value = total_exp / elapsed
+        flop_launch = G * S * F_EXP + G * F_ROOT
+        achieved = flop_launch / (kern_ms * 1e-3) / 1e12
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_search_r01.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(conf, hyper, nets, obs, legal, tp, args.cpu_budget)
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "node-expansions/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: random-play TicTacToe positions, random glorot weights",
+            "config": {"workload": f"TicTacToe FC (params.jl hyper), {G} games/GPU x {S} sims/move (configs[1])",
+                       "games_per_gpu": G, "sims_per_move": S, "global_games": G * world,
+                       "parallelism": f"games sharded x{world}, learner dp{world} (RCCL all-reduce)"},
+            "learner_steps_per_s": round(learner_sps, 1),
+            "learner_config": {"batch_size": B, "num_unroll_steps": K, "mode": "ref_semantics"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 4), "peak": PEAK_F32, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_F32, 5), "traffic": traffic,
+                         "kernel": "mz_search_kernel", "kernel_ms": round(kern_ms, 4),
+                         "flop_per_launch": flop_launch},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -130,6 +130,10 @@ int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* leg
                        float* child_visits, float* root_value, int32_t* action_out,
                        void* stream);
 
+/* Debug/parity: flags & 1 = keep a copy of every search's final tree in HBM
+ * (the LDS-resident tree is otherwise discarded at kernel exit). */
+int mz_debug_enable(mz_handle* h, int flags);
+
 /* Debug/parity: copy the last search's tree statistics to host.  Per game,
  * expanded-node slots e = 0..S (0 = root, e = s+1 expanded by simulation s)
  * and child slots a = 0..A-1:

@@ -45,6 +45,7 @@ SIGNATURES = {
                                       ctypes.c_uint32, ctypes.c_float, _VP, _VP, _VP]),
     "mz_mcts_search_dev": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, ctypes.c_int, ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_float, _VP, _VP, _VP, _VP]),
+    "mz_debug_enable": (ctypes.c_int, [_VP, ctypes.c_int]),
     "mz_debug_tree": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP]),
     "mz_learner_step": (ctypes.c_int, [_VP, ctypes.POINTER(MzBatch), ctypes.c_double, _VP]),
     "mz_grad_count": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_size_t)]),
@@ -165,6 +166,9 @@ class Engine:
         self._check(self.lib.mz_mcts_search_dev(self.h, G, obs_ptr, legal_ptr, tp_ptr, int(exploration),
                                                 rng_step & 0xffffffff, game_offset, temperature, cv_ptr,
                                                 rv_ptr, act_ptr, stream), "mz_mcts_search_dev")
+
+    def debug_enable(self, flags=1):
+        self._check(self.lib.mz_debug_enable(self.h, flags), "mz_debug_enable")
 
     def debug_tree(self, G):
         S, A = self.conf.num_iters, self.A

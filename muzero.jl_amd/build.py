@@ -5,7 +5,7 @@ import subprocess
 from . import PKG_DIR, LIB_PATH
 
 SOURCES = ["mz_engine.hip", "mz_search.hip", "mz_nets.hip"]
-HEADERS = ["mz_internal.h", "mz_mlp_device.h"]
+HEADERS = ["mz_internal.h", "mz_mlp_device.h", "mz_tree_device.h"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
          # the numerics contract (include/mz_detmath.h): no FP contraction, IEEE
          # division/sqrt, f32 denormals kept (hipcc defaults for the last two)

@@ -14,7 +14,8 @@
 
 #include "mz_internal.h"
 
-extern "C" __global__ void mz_search_kernel(SearchParams P);
+extern "C" __global__ void mz_search_kernel_lds(SearchParams P);
+extern "C" __global__ void mz_search_kernel_hbm(SearchParams P);
 
 extern "C" __global__ void mz_unroll_kernel(UnrollParams P);
 extern "C" __global__ void mz_forward_kernel(const int* plan, const float* Wp, const float* Bp, int total_lds,
@@ -85,8 +86,8 @@ struct mz_handle {
     int* d_srcW = nullptr; int* d_srcB = nullptr;
     int* d_plan[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // repr, pred, dyn, root, sim
     double* d_pbc = nullptr; double* d_sqrt = nullptr; float* d_aval = nullptr;
-    int32_t* d_eN = nullptr; int32_t* d_eC = nullptr; int32_t* d_ntp = nullptr;
-    float* d_eW = nullptr; float* d_eP = nullptr; float* d_eR = nullptr; float* d_hid = nullptr;
+    char* d_tree = nullptr; size_t tree_game_bytes = 0; bool lds_tree = false; int dump_tree = 0;
+    float* d_hid = nullptr;
     float* d_obs = nullptr; uint8_t* d_legal = nullptr; int32_t* d_tp = nullptr;
     float* d_cv = nullptr; float* d_rv = nullptr; int32_t* d_act = nullptr;
     // learner
@@ -96,6 +97,7 @@ struct mz_handle {
     float *d_bobs = nullptr, *d_bact = nullptr, *d_btv = nullptr, *d_btr = nullptr, *d_btp = nullptr,
           *d_bgs = nullptr, *d_pv = nullptr, *d_pp = nullptr, *d_pr = nullptr, *d_loss = nullptr;
     double* d_sq = nullptr;
+    unsigned long long* d_stamps = nullptr;
     std::vector<void*> allocs;
 };
 
@@ -170,14 +172,13 @@ static void build_specs(mz_handle* h) {
     h->lay.rows_rep = in_rows(MZ_NET_REPR);
     h->lay.rows_pred = in_rows(MZ_NET_PRED);
     h->lay.rows_dyn = in_rows(MZ_NET_DYN);
-    h->lay.x_rep = region(h->lay.rows_rep);
     h->lay.x_pred = region(h->lay.rows_pred);
     h->lay.x_dyn = region(h->lay.rows_dyn);
     h->lay.h_out = region(mz_round16(hid));
     h->lay.v_out = region(16);
     h->lay.p_out = region(mz_round16(A));
     h->lay.r_out = region(16);
-    for (int net = 0; net < 3; ++net)
+    auto chain_bufs = [&](int net) {
         for (int ch = 0; ch < 3; ++ch) {
             int rows = 0;
             for (int li : h->chains[net][ch]) rows = std::max(rows, 16 * h->layers[li].n_ob);
@@ -185,6 +186,17 @@ static void build_specs(mz_handle* h) {
             h->chain_buf[net][ch][0] = region(rows);
             h->chain_buf[net][ch][1] = region(rows);
         }
+    };
+    chain_bufs(MZ_NET_PRED);
+    // the representation (input + chain) only runs before / apart from the
+    // dynamics net in every plan: they share one LDS union
+    const int u0 = off;
+    chain_bufs(MZ_NET_DYN);
+    const int dyn_end = off;
+    off = u0;
+    h->lay.x_rep = region(h->lay.rows_rep);
+    chain_bufs(MZ_NET_REPR);
+    off = std::max(off, dyn_end);
     h->lay.total = off;
 }
 
@@ -280,9 +292,17 @@ static int repack(mz_handle* h) {
     return 0;
 }
 
-static size_t search_lds_bytes(const mz_handle* h) {
-    return (size_t)h->lay.total * 4 + (size_t)(160 + 16 * (h->S + 2)) * 4;
+static size_t tree_game_bytes(int S, int A) {
+    const size_t E = (size_t)(S + 1) * A, NN = (size_t)(S + 1);
+    return (12 * E + 4 * NN + NN + 15) & ~(size_t)15;
 }
+static size_t search_lds_base(const mz_handle* h) {
+    return (size_t)h->lay.total * 4 + (size_t)(416 + 16 * 2 * (h->S + 2)) * 4;
+}
+static size_t search_lds_bytes(const mz_handle* h) {
+    return search_lds_base(h) + (h->lds_tree ? (size_t)MZ_TILE * h->tree_game_bytes : 0);
+}
+static const size_t kLdsMax = 160 * 1024;
 
 // ------------------------------------------------------------------- ABI
 extern "C" {
@@ -317,7 +337,10 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
     if (max_games < 1) return bad("max_games must be >= 1");
     if (hipSetDevice(device) != hipSuccess) return bad("hipSetDevice failed (no GPU?)");
     build_specs(h);
-    if (search_lds_bytes(h) > 160 * 1024) return bad("LDS budget exceeded (width/num_iters too large)");
+    if (c.num_iters > 65000) return bad("num_iters must be <= 65000 (16-bit visit counts in the tree)");
+    h->tree_game_bytes = tree_game_bytes(c.num_iters, c.action_space_size);
+    h->lds_tree = search_lds_base(h) + (size_t)MZ_TILE * h->tree_game_bytes <= kLdsMax;
+    if (search_lds_bytes(h) > kLdsMax) return bad("LDS budget exceeded (width/num_iters too large)");
     int rc = 0;
 #define CK(x) do { if ((rc = (x)) != 0) { g_create_error = h->err; mz_engine_destroy(h); return rc; } } while (0)
     CK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess ? 0 : fail(h, "hipStreamCreate"));
@@ -345,9 +368,7 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
     CK(hipMemcpy(h->d_pbc, pbc.data(), pbc.size() * 8, hipMemcpyHostToDevice) == hipSuccess ? 0 : fail(h, "copy"));
     CK(hipMemcpy(h->d_sqrt, sq.data(), sq.size() * 8, hipMemcpyHostToDevice) == hipSuccess ? 0 : fail(h, "copy"));
     CK(hipMemcpy(h->d_aval, av.data(), av.size() * 4, hipMemcpyHostToDevice) == hipSuccess ? 0 : fail(h, "copy"));
-    const size_t E = G * (size_t)(S + 1) * A;
-    CK(al(&h->d_eN, E)); CK(al(&h->d_eC, E)); CK(al(&h->d_eW, E)); CK(al(&h->d_eP, E)); CK(al(&h->d_eR, E));
-    CK(al(&h->d_ntp, G * (S + 1)));
+    CK(al(&h->d_tree, G * h->tree_game_bytes));
     CK(al(&h->d_hid, G * (S + 1) * H));
     CK(al(&h->d_obs, G * h->obs_feat)); CK(al(&h->d_legal, G * A)); CK(al(&h->d_tp, G));
     CK(al(&h->d_cv, G * A)); CK(al(&h->d_rv, G)); CK(al(&h->d_act, G));
@@ -355,8 +376,9 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
     CK(hipMemset(h->d_m, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
     CK(hipMemset(h->d_v, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
     CK(al(&h->d_loss, 8)); CK(al(&h->d_sq, 4));
-    CK(hipFuncSetAttribute((const void*)mz_search_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                           (int)search_lds_bytes(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute"));
+    CK(hipFuncSetAttribute(h->lds_tree ? (const void*)mz_search_kernel_lds : (const void*)mz_search_kernel_hbm,
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)search_lds_bytes(h)) == hipSuccess
+           ? 0 : fail(h, "hipFuncSetAttribute"));
     CK(hipStreamSynchronize(h->stream) == hipSuccess ? 0 : fail(h, "sync"));
 #undef CK
     *out = h;
@@ -444,11 +466,19 @@ int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* leg
     P.child_visits = child_visits; P.root_value = root_value; P.action_out = action_out;
     P.Wp = h->d_Wp; P.Bp = h->d_Bp; P.plan_root = h->d_plan[3]; P.plan_sim = h->d_plan[4];
     P.lay = h->lay; P.pbc_tab = h->d_pbc; P.sqrt_tab = h->d_sqrt; P.aval_tab = h->d_aval;
-    P.eN = h->d_eN; P.eW = h->d_eW; P.eP = h->d_eP; P.eR = h->d_eR; P.eC = h->d_eC; P.ntp = h->d_ntp;
-    P.hid = h->d_hid; P.tree_stride = (h->S + 1) * h->A;
+    P.tree = h->d_tree; P.tree_game_bytes = h->tree_game_bytes; P.dump_tree = h->dump_tree;
+    P.hid = h->d_hid;
+#ifdef MZ_STAMPS
+    if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * ((h->max_games + MZ_TILE - 1) / MZ_TILE)));
+    P.stamps = h->d_stamps;
+#endif
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    hipLaunchKernelGGL(mz_search_kernel, dim3((G + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
-                       search_lds_bytes(h), st, P);
+    if (h->lds_tree)
+        hipLaunchKernelGGL(mz_search_kernel_lds, dim3((G + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
+                           search_lds_bytes(h), st, P);
+    else
+        hipLaunchKernelGGL(mz_search_kernel_hbm, dim3((G + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
+                           search_lds_bytes(h), st, P);
     MZ_TRY(h, hipGetLastError());
     return 0;
 }
@@ -480,18 +510,47 @@ int mz_mcts_search(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     return 0;
 }
 
+int mz_debug_enable(mz_handle* h, int flags) {
+    if (!h) return -2;
+    h->dump_tree = flags & 1;
+    return 0;
+}
+
 int mz_debug_tree(mz_handle* h, int G, int32_t* eN, float* eW, float* eP, float* eR, int32_t* eC, int32_t* ntp) {
     if (!h) return -2;
     if (G < 0 || G > h->max_games) return fail(h, "G exceeds max_games");
+    if (h->lds_tree && !h->dump_tree) return fail(h, "mz_debug_tree needs mz_debug_enable(h, 1) before the search");
     MZ_TRY(h, hipSetDevice(h->device));
     MZ_TRY(h, hipStreamSynchronize(h->stream));
-    const size_t E = (size_t)G * (h->S + 1) * h->A;
-    if (eN) MZ_TRY(h, hipMemcpy(eN, h->d_eN, E * 4, hipMemcpyDeviceToHost));
-    if (eW) MZ_TRY(h, hipMemcpy(eW, h->d_eW, E * 4, hipMemcpyDeviceToHost));
-    if (eP) MZ_TRY(h, hipMemcpy(eP, h->d_eP, E * 4, hipMemcpyDeviceToHost));
-    if (eR) MZ_TRY(h, hipMemcpy(eR, h->d_eR, E * 4, hipMemcpyDeviceToHost));
-    if (eC) MZ_TRY(h, hipMemcpy(eC, h->d_eC, E * 4, hipMemcpyDeviceToHost));
-    if (ntp) MZ_TRY(h, hipMemcpy(ntp, h->d_ntp, (size_t)G * (h->S + 1) * 4, hipMemcpyDeviceToHost));
+    const int S = h->S, A = h->A, NN = S + 1, E = NN * A;
+    const size_t gb = h->tree_game_bytes;
+    std::vector<char> buf((size_t)G * gb);
+    MZ_TRY(h, hipMemcpy(buf.data(), h->d_tree, buf.size(), hipMemcpyDeviceToHost));
+    for (int g = 0; g < G; ++g) {
+        const char* b = buf.data() + (size_t)g * gb;
+        const uint32_t* nc = reinterpret_cast<const uint32_t*>(b);
+        const float* w = reinterpret_cast<const float*>(b + 4 * (size_t)E);
+        const float* p = reinterpret_cast<const float*>(b + 8 * (size_t)E);
+        const float* nr = reinterpret_cast<const float*>(b + 12 * (size_t)E);
+        const int8_t* tp = reinterpret_cast<const int8_t*>(b + 12 * (size_t)E + 4 * (size_t)NN);
+        // only expanded slots hold data: slot e is expanded iff e == 0 or some edge points at it
+        std::vector<char> expd(NN, 0);
+        expd[0] = 1;
+        for (int i = 0; i < E; ++i) if ((nc[i] >> 16) != 0 && expd[i / A]) expd[(nc[i] >> 16) - 1] = 1;
+        for (int e = 0; e < NN; ++e) {
+            if (ntp) ntp[(size_t)g * NN + e] = expd[e] ? tp[e] : 0;
+            for (int a = 0; a < A; ++a) {
+                const size_t k = ((size_t)g * NN + e) * A + a, i = (size_t)e * A + a;
+                const bool x = expd[e] != 0;
+                const int c = x ? (int)(nc[i] >> 16) - 1 : -1;
+                if (eN) eN[k] = x ? (int32_t)(nc[i] & 0xffffu) : 0;
+                if (eW) eW[k] = x ? w[i] : 0.0f;
+                if (eP) eP[k] = x ? p[i] : 0.0f;
+                if (eR) eR[k] = c >= 0 ? nr[c] : 0.0f;
+                if (eC) eC[k] = c;
+            }
+        }
+    }
     return 0;
 }
 
@@ -575,6 +634,20 @@ int mz_learner_step(mz_handle* h, const mz_batch* b, double eta, float* losses_o
     if (losses_out) MZ_TRY(h, hipMemcpyAsync(losses_out, h->d_loss, 6 * 4, hipMemcpyDeviceToHost, st));
     MZ_TRY(h, hipStreamSynchronize(st));
     return 0;
+}
+
+// Diagnostic: per-workgroup phase cycles of the last search (stamp build only).
+int mz_debug_stamps(mz_handle* h, unsigned long long* out, int n_blocks) {
+    if (!h) return -2;
+#ifdef MZ_STAMPS
+    if (!h->d_stamps) return fail(h, "no stamps recorded");
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, hipMemcpy(out, h->d_stamps, (size_t)n_blocks * 8 * 8, hipMemcpyDeviceToHost));
+    return 0;
+#else
+    (void)out; (void)n_blocks;
+    return fail(h, "libmz built without -DMZ_STAMPS");
+#endif
 }
 
 int mz_sync(mz_handle* h) {

@@ -81,10 +81,13 @@ struct SearchParams {
     const double* pbc_tab;    // log2((N + base + 1)/base) + c_init, N = 0..S+1
     const double* sqrt_tab;   // sqrt(N), N = 0..S+1
     const float* aval_tab;    // Float32(a / |A|), a = 1..A
-    // tree storage (global): edges [G][S+1][A], node to_play [G][S+1], hidden [G][S+1][H]
-    int32_t* eN; float* eW; float* eP; float* eR; int32_t* eC; int32_t* ntp;
-    float* hid;
-    int tree_stride;          // (S+1)*A per game
+    // tree storage in HBM: per game tree_game_bytes (mz_tree_device.h layout);
+    // the working copy when the tree does not fit in LDS, else the debug dump
+    char* tree;
+    size_t tree_game_bytes;
+    int dump_tree;            // LDS-tree kernel: copy the final tree to `tree`
+    float* hid;               // hidden states [G][S+1][H]
+    unsigned long long* stamps;   // diagnostic build (-DMZ_STAMPS) only: [grid][8] cycles
 };
 
 // Learner unroll-kernel parameters.

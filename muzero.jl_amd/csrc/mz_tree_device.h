@@ -1,0 +1,277 @@
+// mz_tree_device.h — the MCTS tree phases shared by the search kernels
+// (SelfPlay.jl:88-217, 293-306): select, expand, backup, search statistics.
+//
+// Tree of one game (slot e = 0 is the root, e = s+1 the node expanded by
+// simulation s; edge (e, a) = child a of expanded node e):
+//   nc[e*A + a]  u32  visit count N (low 16 bits) | child slot + 1 (high 16; 0 = none)
+//   w [e*A + a]  f32  value_sum of the child
+//   p [e*A + a]  f32  prior of the child
+//   nr[e]        f32  reward of expanded node e (node.reward)
+//   ntp[e]       i8   to_play of expanded node e
+// 12 bytes per edge: 16 games x 50 sims x 9 actions fit in LDS next to the
+// network activations; the same code runs on an HBM copy when they do not.
+// Threads are grouped 16 lanes per game (lane a = child slot a, A <= 16).
+#pragma once
+#include "mz_internal.h"
+
+struct TreeView {
+    uint32_t* nc;
+    float* w;
+    float* p;
+    float* nr;
+    int8_t* ntp;
+};
+
+// max over the 16-lane group (= one DPP row): quad_perm [1,0,3,2],
+// quad_perm [2,3,0,1], row_half_mirror, row_mirror.  Exact (comparisons only).
+__device__ __forceinline__ float dpp_f(float v, int ctrl) {
+    switch (ctrl) {
+        case 0xB1: return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+        case 0x4E: return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+        case 0x141: return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+        default: return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+    }
+}
+__device__ __forceinline__ float g16_max(float v) {
+    float t;
+    t = dpp_f(v, 0xB1); v = v > t ? v : t;
+    t = dpp_f(v, 0x4E); v = v > t ? v : t;
+    t = dpp_f(v, 0x141); v = v > t ? v : t;
+    t = dpp_f(v, 0x140); v = v > t ? v : t;
+    return v;
+}
+__device__ __forceinline__ float g16_min(float v) {
+    float t;
+    t = dpp_f(v, 0xB1); v = v < t ? v : t;
+    t = dpp_f(v, 0x4E); v = v < t ? v : t;
+    t = dpp_f(v, 0x141); v = v < t ? v : t;
+    t = dpp_f(v, 0x140); v = v < t ? v : t;
+    return v;
+}
+
+__device__ __forceinline__ int g16_isum(int v) {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 16);
+    return v;
+}
+
+// sequential (ascending) f32 sum of lanes 0..n-1 of the 16-lane group; every
+// lane returns the same value (the oracle's `s = s + y[i]` loop order).  The
+// values are staged through this group's 16-float LDS slot `st` (same wave:
+// LDS ops complete in order) and read back as four broadcast b128 loads.
+__device__ __forceinline__ float g16_seqsum(float v, int n, float* st, int a) {
+    st[a] = v;
+    __builtin_amdgcn_wave_barrier();
+    float x[16];
+#pragma unroll
+    for (int b = 0; b < 16; b += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(st + b);
+        x[b] = q.x; x[b + 1] = q.y; x[b + 2] = q.z; x[b + 3] = q.w;
+    }
+    __builtin_amdgcn_wave_barrier();
+    float s = 0.0f;
+#pragma unroll
+    for (int b = 0; b < 16; ++b) if (b < n) s = s + x[b];
+    return s;
+}
+
+__device__ __forceinline__ int nth_set_bit(uint32_t m, int k) {
+    for (int i = 0; i < k; ++i) m &= m - 1;
+    return __builtin_ctz(m);
+}
+
+// expand_node! (SelfPlay.jl:88-96) priors for the 16-lane group: the policy
+// head's softmax over all A logits (Learning.jl:114), then the softmax over
+// the legal entries (:89, Q3).  `logit` is this lane's logit (a < A).
+__device__ __forceinline__ float double_softmax_prior(float logit, int a, int A, uint32_t legal, float* st) {
+    const bool in = a < A;
+    const float x = in ? logit : -INFINITY;
+    const float m = g16_max(x);
+    const float ex = in ? det_expf(x - m) : 0.0f;
+    const float s = g16_seqsum(ex, A, st, a);
+    const float prob = in ? ex / s : 0.0f;
+    const bool lg = in && ((legal >> a) & 1u);
+    const float m2 = g16_max(lg ? prob : -INFINITY);
+    const float e2 = lg ? det_expf(prob - m2) : 0.0f;
+    const float s2 = g16_seqsum(e2, A, st, a);   // illegal lanes add +0: same as the legal-only sum
+    return lg ? e2 / s2 : 0.0f;
+}
+
+// Write the A child edges of expanded slot e (N=0, W=0, prior, no child).
+__device__ __forceinline__ void init_edges(const TreeView& t, int e, int a, int A, float prior) {
+    if (a < A) {
+        const int i = e * A + a;
+        t.nc[i] = 0u; t.w[i] = 0.0f; t.p[i] = prior;
+    }
+}
+
+struct SelectOut { int leaf_e, leaf_a, vtp, depth; };
+
+// Path of one simulation: path[2d] = edge index e*A + a taken at depth d,
+// path[2d+1] = child slot it leads to (-1 for the leaf until expanded).
+
+// select_child loop (SelfPlay.jl:256-268) for the game of this 16-lane group.
+// pUCT (ucb_score :171-184) in f64 with one rounding to f32 (Q5); ties by
+// exact equality, broken by the Philox TIE stream keyed (sim, depth) — the
+// draw only matters (and is only computed) when there is more than one tie.
+__device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, int root_N, int root_tp,
+                                                 uint32_t legal, float mmin, float mmax, int a, int lane,
+                                                 int A, int players, float discount, const double* pbc_tab,
+                                                 const double* sqrt_tab, uint64_t seed, uint32_t gid,
+                                                 uint32_t step, int sim) {
+    const bool lg = a < A && ((legal >> a) & 1u);
+    const bool norm = mmax > mmin;
+    int e = 0, Np = root_N, depth = 0, vtp = root_tp;
+    for (;;) {
+        const int i = e * A + a;
+        float u = -INFINITY;
+        if (lg) {
+            const uint32_t nc = t.nc[i];
+            const int Nc = (int)(nc & 0xffffu);
+            const double pb_c = pbc_tab[Np] * (sqrt_tab[Np] / (double)(Nc + 1));
+            const double prior_score = pb_c * (double)t.p[i];
+            float vs = 0.0f;
+            if (Nc > 0) {
+                const float q = t.w[i] / (float)Nc;
+                const float tq = players == 1 ? discount * q : discount * (-q);
+                const float v = t.nr[(int)(nc >> 16) - 1] + tq;
+                vs = norm ? (v - mmin) / (mmax - mmin) : v;
+            }
+            u = (float)(prior_score + (double)vs);
+        }
+        const float m = g16_max(u);
+        const uint64_t bal = __ballot(lg && u == m);
+        const uint32_t mask = (uint32_t)(bal >> (lane & 48)) & 0xffffu;
+        const int nt = __builtin_popcount(mask);
+        depth += 1;
+        int ach;
+        if (nt == 1) {
+            ach = __builtin_ctz(mask);
+        } else {
+            const uint32_t r = mz_rng_u32(seed, MZ_RNG_TIE, gid, step, ((uint32_t)sim << 12) | (uint32_t)depth);
+            ach = nth_set_bit(mask, (int)mz_rng_below(r, (uint32_t)nt));
+        }
+        const int ei = e * A + ach;
+        const uint32_t ncc = t.nc[ei];                  // same address across the group: broadcast
+        const int Cch = (int)(ncc >> 16);
+        if (a == 0) { path[2 * depth] = ei; path[2 * depth + 1] = Cch - 1; }
+        vtp = (vtp % players) + 1;                      // mod1(vtp + 1, |players|), :267
+        if (Cch == 0) return SelectOut{e, ach, vtp, depth};
+        e = Cch - 1; Np = (int)(ncc & 0xffffu);
+    }
+}
+
+// backpropagate! (SelfPlay.jl:190-217), quirk Q7, for the 16-lane group.
+// Node d of the path (0 = root ... depth = the just-expanded leaf with
+// to_play tl) receives v_in(d): v_in(depth) = the leaf value; otherwise
+// v_in(d) = v_out(d+1) with v_out(k) = (tp_k == tl) ? -R_k : R_k + γ v_in(k).
+// v_out resets wherever tp_k == tl, so every level's v_in is the same f32
+// expression chain the sequential loop evaluates, started at the nearest
+// reset below it (one or two levels away in 2-player games, where to_play
+// alternates with depth): all levels update in parallel, bit-exactly.  The
+// min-max fold is order-independent (exact comparisons).  1-player games
+// have no resets and run the sequential loop on lane 0.
+__device__ __forceinline__ void backup_path(const TreeView& t, const int* path, int depth, float value, int tl,
+                                            int A, int players, float discount, int& root_N, float& root_W,
+                                            int root_tp, float& mmin, float& mmax, int a) {
+    if (players != 2) {
+        if (a == 0) {
+            float v = value;
+            for (int d = depth; d >= 0; --d) {
+                int N; float W, R; int i = 0;
+                uint32_t nc = 0;
+                if (d > 0) {
+                    i = path[2 * d]; nc = t.nc[i];
+                    N = (int)(nc & 0xffffu); W = t.w[i]; R = t.nr[path[2 * d + 1]];
+                } else {
+                    N = root_N; W = root_W; R = 0.0f;
+                }
+                W = W + v; N += 1;
+                const float upd = R + discount * (W / (float)N);
+                mmin = mmin < upd ? mmin : upd; mmax = mmax > upd ? mmax : upd;
+                v = R + discount * v;
+                if (d > 0) { t.nc[i] = (nc & 0xffff0000u) | (uint32_t)N; t.w[i] = W; }
+                else { root_N = N; root_W = W; }
+            }
+        }
+        root_N = __shfl(root_N, 0, 16); root_W = __shfl(root_W, 0, 16);
+        mmin = __shfl(mmin, 0, 16); mmax = __shfl(mmax, 0, 16);
+        return;
+    }
+    float lmin = INFINITY, lmax = -INFINITY;
+    int rN = root_N; float rW = root_W;
+    for (int base = 0; base <= depth; base += 16) {
+        const int d = base + a;
+        if (d <= depth) {
+            int N, i = 0, tp; float W, R;
+            uint32_t nc = 0;
+            if (d > 0) {
+                i = path[2 * d]; nc = t.nc[i];
+                const int c = path[2 * d + 1];
+                N = (int)(nc & 0xffffu); W = t.w[i]; R = t.nr[c]; tp = t.ntp[c];
+            } else {
+                N = root_N; W = root_W; R = 0.0f; tp = root_tp;
+            }
+            float vin;
+            if (d == depth) {
+                vin = value;
+            } else {
+                int k0 = d + 1;                         // nearest reset at or below d+1
+                while (k0 < depth && t.ntp[path[2 * k0 + 1]] != tl) ++k0;
+                // the leaf always resets (its to_play is tl); a non-leaf k0 resets
+                float v = -t.nr[path[2 * k0 + 1]];
+                for (int k = k0 - 1; k >= d + 1; --k) v = t.nr[path[2 * k + 1]] + discount * v;
+                vin = v;
+            }
+            W = tp == tl ? W + vin : W - vin;
+            N += 1;
+            const float upd = R + discount * (W / (float)N);
+            lmin = lmin < upd ? lmin : upd;
+            lmax = lmax > upd ? lmax : upd;
+            if (d > 0) { t.nc[i] = (nc & 0xffff0000u) | (uint32_t)N; t.w[i] = W; }
+            else { rN = N; rW = W; }
+        }
+    }
+    lmin = g16_min(lmin);
+    lmax = g16_max(lmax);
+    mmin = mmin < lmin ? mmin : lmin;
+    mmax = mmax > lmax ? mmax : lmax;
+    root_N = __shfl(rN, 0, 16); root_W = __shfl(rW, 0, 16);
+}
+
+// select_action (SelfPlay.jl:293-306): same rule as the oracle.
+__device__ int select_action_dev(const int* cnt, uint32_t legal, int A, float temperature, uint32_t r) {
+    int acts[16], c[16], n = 0;
+    for (int a = 0; a < A; ++a) if ((legal >> a) & 1u) { acts[n] = a; c[n] = cnt[a]; ++n; }
+    if (temperature == 0.0f) {
+        int best = 0;
+        for (int i = 1; i < n; ++i) if (c[i] > c[best]) best = i;
+        return acts[best];
+    }
+    if (isinf(temperature)) return acts[mz_rng_below(r, (uint32_t)n)];
+    if (temperature == 1.0f) {
+        uint32_t tot = 0;
+        for (int i = 0; i < n; ++i) tot += (uint32_t)c[i];
+        if (tot == 0) return acts[mz_rng_below(r, (uint32_t)n)];
+        uint32_t tt = mz_rng_below(r, tot), cum = 0;
+        for (int i = 0; i < n; ++i) { cum += (uint32_t)c[i]; if (cum > tt) return acts[i]; }
+        return acts[n - 1];
+    }
+    float e = 1.0f / temperature;
+    float w[16], s = 0.0f;
+    for (int i = 0; i < n; ++i) {
+        w[i] = c[i] > 0 ? (float)det_exp(det_log((double)c[i]) * (double)e) : 0.0f;
+        s = s + w[i];
+    }
+    float u = (float)(r >> 8) * 5.9604644775390625e-08f * s;
+    float cum = 0.0f;
+    for (int i = 0; i < n; ++i) { cum = cum + w[i]; if (cum > u) return acts[i]; }
+    return acts[n - 1];
+}
+
+// Copy one game's tree to the global debug buffers (parity tests only).
+__device__ __forceinline__ void dump_tree(const TreeView& t, const TreeView& dst, int n_edges, int n_nodes,
+                                          int lane16) {
+    for (int i = lane16; i < n_edges; i += 16) { dst.nc[i] = t.nc[i]; dst.w[i] = t.w[i]; dst.p[i] = t.p[i]; }
+    for (int i = lane16; i < n_nodes; i += 16) { dst.nr[i] = t.nr[i]; dst.ntp[i] = t.ntp[i]; }
+}

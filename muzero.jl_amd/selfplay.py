@@ -1,0 +1,165 @@
+"""Self-play host driver — the Python mirror of src/SelfPlay.jl over libmz.
+
+The search itself (run_mcts + select_action + store_search_stats!,
+SelfPlay.jl:115-306) runs as one HIP kernel per move for the whole batch of
+games; this module keeps the reference's game loop (play_game, :330-382),
+the stacked observations (:128-149) and the GameHistory records
+(Constructors.jl:6-16).  Games advance in lockstep; a finished slot is reset
+and starts a new game (continuous batched self-play).  RNG step keys: the
+global move counter `step` (unique per move across the run), game id = slot.
+"""
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+from .config import stacked_features
+
+
+def visit_softmax_temperature_fn(trained_steps: int) -> float:   # SelfPlay.jl:48-56
+    if trained_steps < 500e3:
+        return 1.0
+    elif trained_steps < 750e3:
+        return 0.5
+    return 0.25
+
+
+@dataclass
+class GameHistory:                                               # Constructors.jl:6-16
+    observation_history: List[np.ndarray] = field(default_factory=list)   # (W*H*C,) per move
+    action_history: List[int] = field(default_factory=list)
+    reward_history: List[float] = field(default_factory=list)
+    to_play_history: List[int] = field(default_factory=list)
+    child_visits: List[np.ndarray] = field(default_factory=list)          # (A,) per move
+    root_values: List[float] = field(default_factory=list)
+    reanalysed_predicted_root_values: Optional[list] = None
+    priorities: Optional[np.ndarray] = None
+    game_priority: Optional[float] = None
+
+    def as_arrays(self):
+        return dict(observation=np.array(self.observation_history, np.float32),
+                    action=np.array(self.action_history, np.int32),
+                    reward=np.array(self.reward_history, np.float32),
+                    to_play=np.array(self.to_play_history, np.int32),
+                    child_visits=np.array(self.child_visits, np.float32),
+                    root_values=np.array(self.root_values, np.float32))
+
+
+def get_stacked_observations(obs_hist, action_hist, index, num_stacked, plane):
+    """SelfPlay.jl:128-149 (Q15): [obs_t, (action plane, obs_{t-1}) ...], zeros before
+    the first move; the action plane holds the raw action id.  `index` is 1-based."""
+    parts = [np.asarray(obs_hist[index - 1], np.float32)]
+    osz = parts[0].size
+    for past in range(index - 1, index - num_stacked - 1, -1):
+        if past >= 1:
+            parts.append(np.full(plane, float(action_hist[past - 1]), np.float32))
+            parts.append(np.asarray(obs_hist[past - 1], np.float32))
+        else:
+            parts.append(np.zeros(plane + osz, np.float32))
+    return np.concatenate(parts)
+
+
+class BatchedSelfPlay:
+    """G TicTacToe games played in lockstep on one engine (one GPU)."""
+
+    def __init__(self, engine, env_cls, G, game_offset=0, step0=0):
+        self.eng = engine
+        self.conf = engine.conf
+        self.G = G
+        self.env = env_cls(G)
+        self.game_offset = game_offset
+        self.step = step0
+        self.plane = self.conf.observation_shape[0] * self.conf.observation_shape[1]
+        self.histories = [GameHistory() for _ in range(G)]
+        self.finished: List[GameHistory] = []
+
+    def _stacked(self):
+        c = self.conf
+        out = np.empty((self.G, stacked_features(c)), np.float32)
+        for g, h in enumerate(self.histories):
+            out[g] = get_stacked_observations(h.observation_history, h.action_history,
+                                              len(h.observation_history), c.stacked_observations, self.plane)
+        return out
+
+    def play_move(self, temperature=1.0):
+        """One move of every game (play_game's loop body, SelfPlay.jl:343-380)."""
+        c = self.conf
+        tp = self.env.player.copy()                                           # :351
+        for g, h in enumerate(self.histories):
+            h.observation_history.append(self.env.board[g].astype(np.float32))  # :352
+        obs = self._stacked()                                                 # :355
+        legal = self.env.legal_mask()
+        temps = temperature
+        if c.temperature_threshold is not None:
+            # per-game threshold (:344-346) needs per-game temperatures: split by group
+            moves = np.array([len(h.action_history) for h in self.histories])
+            if np.any(moves >= c.temperature_threshold):
+                raise NotImplementedError("temperature_threshold with mixed move counts")
+        cv, rv, act = self.eng.mcts_search(obs, legal, tp, exploration=True, rng_step=self.step,
+                                           game_offset=self.game_offset, temperature=temps)  # :359-360
+        reward, done = self.env.step(act)                                     # :366-368
+        for g, h in enumerate(self.histories):                                # :375-379
+            h.child_visits.append(cv[g])
+            h.root_values.append(float(rv[g]))
+            h.action_history.append(int(act[g]))
+            h.reward_history.append(float(reward[g]))
+            h.to_play_history.append(int(tp[g]))
+        too_long = np.array([len(h.action_history) > c.max_moves for h in self.histories])
+        ended = np.flatnonzero(done | too_long)
+        for g in ended:
+            self.finished.append(self.histories[g])
+            self.histories[g] = GameHistory()
+        if len(ended):
+            self.env.reset(ended)
+        self.step += 1
+        return ended
+
+    def play_games(self, temperature=1.0):
+        """Play every slot's current game to the end (no new games started);
+        returns the histories in slot order."""
+        results: List[Optional[GameHistory]] = [None] * self.G
+        active = np.ones(self.G, bool)
+        while active.any():
+            n0 = len(self.finished)
+            ended = self.play_move(temperature)
+            for k, g in enumerate(ended):
+                if active[g]:
+                    results[g] = self.finished[n0 + k]
+                    active[g] = False
+        return results
+
+
+def random_positions(env_cls, G, seed=0, max_plies=6):
+    """Real TicTacToe positions for benchmarking: random legal play from the
+    initial board for 0..max_plies plies; returns stacked observations
+    (G, F), legal masks (G, A) and to_play (G,).  Positions that ended are
+    replaced by the initial board."""
+    rng = np.random.default_rng(seed)
+    env = env_cls(G)
+    prev_obs = np.zeros((G, 27), np.float32)
+    prev_act = np.zeros(G, np.int32)
+    plies = rng.integers(0, max_plies + 1, G)
+    alive = np.ones(G, bool)
+    for t in range(max_plies):
+        legal = env.legal_mask()
+        go = (plies > t) & alive & legal.any(1)
+        if not go.any():
+            break
+        choice = np.array([rng.choice(np.flatnonzero(legal[g])) + 1 if go[g] else 1 for g in range(G)], np.int32)
+        before = env.board.astype(np.float32)
+        board_save, player_save = env.board.copy(), env.player.copy()
+        _, done = env.step(choice)
+        env.board[~go] = board_save[~go]
+        env.player[~go] = player_save[~go]
+        prev_obs[go] = before[go]
+        prev_act[go] = choice[go]
+        ended = go & done
+        if ended.any():
+            env.reset(np.flatnonzero(ended))
+            prev_obs[ended] = 0
+            prev_act[ended] = 0
+            alive &= ~ended
+    cur = env.board.astype(np.float32)
+    plane = np.repeat(prev_act[:, None].astype(np.float32), 9, axis=1)
+    obs = np.concatenate([cur, plane, prev_obs], axis=1)
+    return obs, env.legal_mask(), env.player.copy()

@@ -88,6 +88,7 @@ def test_search_bitexact(ttt, nets, S, G, explore, temp, seed):
     conf = dataclasses.replace(ttt.conf, num_iters=S)
     eng, ora = _engine(conf, ttt.hyper, nets, G, seed), _oracle(conf, ttt.hyper, nets, seed)
     obs, legal, tp = random_positions(G, seed)
+    eng.debug_enable(1)
     cv, rv, act = eng.mcts_search(obs, legal, tp, exploration=explore, rng_step=seed * 3, game_offset=100,
                                   temperature=temp)
     tree_g = eng.debug_tree(G)

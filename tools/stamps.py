@@ -1,0 +1,53 @@
+"""Diagnostic: per-phase cycle breakdown of mz_search_kernel from a separate
+-DMZ_STAMPS build (libmz_stamps.so).  Shares only; never quote its run time."""
+import ctypes
+import dataclasses
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import _mzpkg  # noqa: E402
+
+pkg = _mzpkg.load()
+from muzero_jl_amd import abi, build as mzbuild  # noqa: E402
+from muzero_jl_amd.games import tictactoe as ttt  # noqa: E402
+from muzero_jl_amd.networks import init_nets  # noqa: E402
+from muzero_jl_amd.selfplay import random_positions  # noqa: E402
+
+PHASES = ["root", "select", "gather", "nets", "expand", "backup", "finish", "-"]
+
+
+def main():
+    lib = os.path.join(pkg.PKG_DIR, "lib", "libmz_stamps.so")
+    srcs = [os.path.join(pkg.PKG_DIR, "csrc", s) for s in mzbuild.SOURCES]
+    if "--no-build" not in sys.argv:
+        subprocess.run(["/opt/rocm/bin/hipcc"] + mzbuild.FLAGS + ["-DMZ_STAMPS", "-o", lib] + srcs, check=True)
+    abi._lib = None
+    L = abi.load_library(lib)
+    L.mz_debug_stamps.restype = ctypes.c_int
+    L.mz_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    G = int(os.environ.get("G", "512"))
+    S = int(os.environ.get("S", "50"))
+    conf = dataclasses.replace(ttt.conf, num_iters=S)
+    eng = abi.Engine(conf, ttt.hyper, device=0, max_games=G, rng_seed=1)
+    for n, w in enumerate(init_nets(conf, ttt.hyper, seed=1234)):
+        eng.set_weights(n, w)
+    obs, legal, tp = random_positions(ttt.BatchedTicTacToe, G, seed=100)
+    for k in range(3):
+        eng.mcts_search(obs, legal, tp, rng_step=k)
+    nb = (G + 15) // 16
+    out = np.zeros((nb, 8), np.uint64)
+    assert L.mz_debug_stamps(eng.h, out.ctypes.data_as(ctypes.c_void_p), nb) == 0
+    tot = out.sum(1).astype(np.float64)
+    med = np.median(out.astype(np.float64), axis=0)
+    print(f"G={G} S={S}: median cycles per workgroup (s_memtime ticks, 100 MHz ref? see note)")
+    for i, p in enumerate(PHASES[:7]):
+        print(f"  {p:8s} {med[i]:12.0f}  per-sim {med[i] / S:10.1f}  share {med[i] / np.median(tot):6.3f}")
+    print("  total   ", np.median(tot))
+
+
+if __name__ == "__main__":
+    main()
