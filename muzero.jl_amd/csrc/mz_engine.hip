@@ -8,6 +8,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -16,11 +17,14 @@
 
 extern "C" __global__ void mz_search_kernel_lds(SearchParams P);
 extern "C" __global__ void mz_search_kernel_hbm(SearchParams P);
+extern "C" __global__ void mz_search_kernel_lds_res(SearchParams P);
+extern "C" __global__ void mz_search_kernel_hbm_res(SearchParams P);
 
 extern "C" __global__ void mz_unroll_kernel(UnrollParams P);
 extern "C" __global__ void mz_forward_kernel(const int* plan, const float* Wp, const float* Bp, int total_lds,
                                              int in_off, int in_feat, const float* x, int n, int out0_off, int o0,
-                                             float* out0, int out1_off, int o1, float* out1, int sm1);
+                                             float* out0, int out1_off, int o1, float* out1, int sm1, int act0,
+                                             int act1);
 extern "C" __global__ void mz_loss_kernel(int B, int K, int A, const float* pv, const float* pp, const float* tv,
                                           const float* tp, const float* gscale, float* out);
 extern "C" __global__ void mz_sqnorm_kernel(const float* P, size_t n, double* out);
@@ -85,8 +89,10 @@ struct mz_handle {
     float* d_flat = nullptr; float* d_Wp = nullptr; float* d_Bp = nullptr;
     int* d_srcW = nullptr; int* d_srcB = nullptr;
     int* d_plan[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // repr, pred, dyn, root, sim
+    int* d_plan_sim_res = nullptr;          // register-resident image of the sim plan (or null)
     double* d_pbc = nullptr; double* d_sqrt = nullptr; float* d_aval = nullptr;
     char* d_tree = nullptr; size_t tree_game_bytes = 0; bool lds_tree = false; int dump_tree = 0;
+    bool use_res = false;                   // register-resident sim-plan kernel
     float* d_hid = nullptr;
     float* d_obs = nullptr; uint8_t* d_legal = nullptr; int32_t* d_tp = nullptr;
     float* d_cv = nullptr; float* d_rv = nullptr; int32_t* d_act = nullptr;
@@ -212,6 +218,9 @@ static int place_chain(mz_handle* h, PlanBuild& pb, int net, int ch, int st0, in
         d.in_off = i == 0 ? in_first : h->chain_buf[net][ch][(i - 1) & 1];
         d.out_off = i == n - 1 ? out_last : h->chain_buf[net][ch][i & 1];
         d.out_rows = S.out;
+        // value / reward heads' output activation is applied at read-out
+        if (i == n - 1 && ch == CH_HEAD1 && net == MZ_NET_PRED) { h->lay.v_act = d.act; d.act = MZ_ACT_IDENTITY; }
+        if (i == n - 1 && ch == CH_HEAD2 && net == MZ_NET_DYN) { h->lay.r_act = d.act; d.act = MZ_ACT_IDENTITY; }
         const int di = (int)pb.layers.size();
         pb.layers.push_back(d);
         for (int ob = 0; ob < S.n_ob; ++ob) pb.stages[st0 + i].push_back({di, ob});
@@ -257,6 +266,31 @@ static int build_plans(mz_handle* h) {
     for (int i = 0; i < 5; ++i)
         if (all[i]->stages.size() > MZ_MAX_STAGES) return fail(h, "network too deep for the plan executor");
     for (int i = 0; i < 5; ++i) if (upload_plan(h, *all[i], &h->d_plan[i])) return -1;
+    // Register-resident image: the tasks of each stage go round-robin to the
+    // 4 waves exactly as run_plan deals them; eligible when every wave has
+    // <= MZ_RES_TASKS tasks of K <= 64 (nq <= 4).
+    const int NW = MZ_THREADS / 64, NT = 16, RT = 9;    // MZ_RES_TASKS, ints per ResTask
+    std::vector<std::vector<int>> per(NW);
+    bool ok = true;
+    for (int st = 0; st < (int)sim.stages.size(); ++st)
+        for (int t = 0; t < (int)sim.stages[st].size(); ++t) {
+            const LayerDesc& L = sim.layers[sim.stages[st][t].first];
+            const int w = t % NW;
+            if (L.nq > 4) ok = false;
+            const int rt[RT] = {st, L.w_off, L.b_off, L.nq, sim.stages[st][t].second, L.act, L.in_off, L.out_off, 0};
+            per[w].insert(per[w].end(), rt, rt + RT);
+        }
+    for (auto& v : per) if ((int)v.size() / RT > NT) ok = false;
+    if (ok) {
+        std::vector<int> img = {(int)sim.stages.size(), NT};
+        for (auto& v : per) {
+            img.push_back((int)v.size() / RT);
+            img.insert(img.end(), v.begin(), v.end());
+            img.resize(img.size() + (size_t)(NT * RT - (int)v.size()), 0);
+        }
+        MZ_TRY(h, dalloc(h, &h->d_plan_sim_res, img.size()));
+        MZ_TRY(h, hipMemcpy(h->d_plan_sim_res, img.data(), img.size() * sizeof(int), hipMemcpyHostToDevice));
+    }
     return 0;
 }
 
@@ -303,6 +337,12 @@ static size_t search_lds_bytes(const mz_handle* h) {
     return search_lds_base(h) + (h->lds_tree ? (size_t)MZ_TILE * h->tree_game_bytes : 0);
 }
 static const size_t kLdsMax = 160 * 1024;
+
+typedef void (*search_fn)(SearchParams);
+static search_fn search_kernel(const mz_handle* h) {
+    if (h->use_res) return h->lds_tree ? mz_search_kernel_lds_res : mz_search_kernel_hbm_res;
+    return h->lds_tree ? mz_search_kernel_lds : mz_search_kernel_hbm;
+}
 
 // ------------------------------------------------------------------- ABI
 extern "C" {
@@ -376,9 +416,14 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
     CK(hipMemset(h->d_m, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
     CK(hipMemset(h->d_v, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
     CK(al(&h->d_loss, 8)); CK(al(&h->d_sq, 4));
-    CK(hipFuncSetAttribute(h->lds_tree ? (const void*)mz_search_kernel_lds : (const void*)mz_search_kernel_hbm,
-                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)search_lds_bytes(h)) == hipSuccess
-           ? 0 : fail(h, "hipFuncSetAttribute"));
+    h->use_res = h->d_plan_sim_res != nullptr && std::getenv("MZ_NO_RESIDENT") == nullptr;
+    {
+        const search_fn ks[4] = {mz_search_kernel_lds, mz_search_kernel_hbm, mz_search_kernel_lds_res,
+                                 mz_search_kernel_hbm_res};
+        for (auto k : ks)
+            CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)search_lds_bytes(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute"));
+    }
     CK(hipStreamSynchronize(h->stream) == hipSuccess ? 0 : fail(h, "sync"));
 #undef CK
     *out = h;
@@ -439,7 +484,8 @@ int mz_net_forward(mz_handle* h, int net, const float* x, int n, float* out0, fl
     hipLaunchKernelGGL(mz_forward_kernel, dim3((n + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
                        (size_t)h->lay.total * 4, h->stream, h->d_plan[net], h->d_Wp, h->d_Bp, h->lay.total, in_off,
                        in_feat, dx, n, o0_off, o0, d0, o1_off, o1, net == MZ_NET_REPR ? nullptr : d1,
-                       net == MZ_NET_PRED ? 1 : 0);
+                       net == MZ_NET_PRED ? 1 : 0, net == MZ_NET_PRED ? h->lay.v_act : MZ_ACT_IDENTITY,
+                       net == MZ_NET_DYN ? h->lay.r_act : MZ_ACT_IDENTITY);
     hipError_t le = hipGetLastError();
     hipMemcpyAsync(out0, d0, (size_t)n * o0 * 4, hipMemcpyDeviceToHost, h->stream);
     if (out1 && net != MZ_NET_REPR) hipMemcpyAsync(out1, d1, (size_t)n * o1 * 4, hipMemcpyDeviceToHost, h->stream);
@@ -465,6 +511,7 @@ int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* leg
     P.obs = obs; P.legal = legal_mask; P.to_play = to_play;
     P.child_visits = child_visits; P.root_value = root_value; P.action_out = action_out;
     P.Wp = h->d_Wp; P.Bp = h->d_Bp; P.plan_root = h->d_plan[3]; P.plan_sim = h->d_plan[4];
+    P.plan_sim_res = h->use_res ? h->d_plan_sim_res : nullptr;
     P.lay = h->lay; P.pbc_tab = h->d_pbc; P.sqrt_tab = h->d_sqrt; P.aval_tab = h->d_aval;
     P.tree = h->d_tree; P.tree_game_bytes = h->tree_game_bytes; P.dump_tree = h->dump_tree;
     P.hid = h->d_hid;
@@ -473,12 +520,8 @@ int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* leg
     P.stamps = h->d_stamps;
 #endif
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    if (h->lds_tree)
-        hipLaunchKernelGGL(mz_search_kernel_lds, dim3((G + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
-                           search_lds_bytes(h), st, P);
-    else
-        hipLaunchKernelGGL(mz_search_kernel_hbm, dim3((G + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
-                           search_lds_bytes(h), st, P);
+    hipLaunchKernelGGL(search_kernel(h), dim3((G + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
+                       search_lds_bytes(h), st, P);
     MZ_TRY(h, hipGetLastError());
     return 0;
 }

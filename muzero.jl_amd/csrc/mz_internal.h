@@ -58,6 +58,7 @@ struct ActLayout {
     int x_rep, x_pred, x_dyn;     // inputs: stacked obs, hidden, state-action
     int h_out, v_out, p_out, r_out;
     int rows_rep, rows_pred, rows_dyn;   // padded input rows (zeroed)
+    int v_act, r_act;             // activations of the value / reward output layers (applied at read-out)
     int total;                    // floats
 };
 
@@ -76,6 +77,7 @@ struct SearchParams {
     // model
     const float* Wp; const float* Bp;
     const int* plan_root; const int* plan_sim;
+    const int* plan_sim_res;  // register-resident image of plan_sim (NULL: not eligible)
     ActLayout lay;
     // tables (host-computed with libm so the oracle matches bit-exactly)
     const double* pbc_tab;    // log2((N + base + 1)/base) + c_init, N = 0..S+1

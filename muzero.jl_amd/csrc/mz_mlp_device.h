@@ -18,7 +18,14 @@
 
 typedef float mz_f32x4 __attribute__((ext_vector_type(4)));
 
+// In-block activations are relu / identity only: the value and reward output
+// layers (tanh, Learning.jl:110,140) are planned as identity and their
+// activation is applied once where the value / reward is read (mz_post_act),
+// which keeps the f64 tanh out of every block epilogue (instruction cache).
 __device__ __forceinline__ float mz_act(int act, float v) {
+    return act == MZ_ACT_RELU ? mz_relu(v) : v;
+}
+__device__ __forceinline__ float mz_post_act(int act, float v) {
     if (act == MZ_ACT_RELU) return mz_relu(v);
     if (act == MZ_ACT_TANH) return det_tanhf(v);
     return v;
@@ -97,4 +104,102 @@ __device__ __forceinline__ void run_plan(const int* plan, const float* __restric
         }
         __syncthreads();
     }
+}
+
+// ---------------------------------------------------------------------------
+// Register-resident plan (the simulation loop's prediction ‖ dynamics plan).
+// Every wave owns a fixed list of <= MZ_RES_TASKS tasks; their weight
+// fragments are loaded ONCE per kernel into wr[16*k .. 16*k + 4*nq) and the
+// loop over k is fully unrolled so every register index is static.  With one
+// 256-thread workgroup per CU a wave may use up to 512 VGPRs
+// (__launch_bounds__(256, 1)).  Image (int array):
+//   [0] n_stages, [1] NT (task slots per wave), then per wave w:
+//   [ntasks, NT x ResTask].
+#define MZ_RES_TASKS 16
+struct ResTask { int stage, w_off, b_off, nq, ob, act, in_off, out_off, pad; };
+
+__device__ __forceinline__ const ResTask* res_tasks(const int* img, int wave, int& nt) {
+    const int NT = img[1];
+    const int* wl = img + 2 + wave * (1 + NT * (int)(sizeof(ResTask) / sizeof(int)));
+    nt = wl[0];
+    return reinterpret_cast<const ResTask*>(wl + 1);
+}
+
+template <int K>
+__device__ __forceinline__ void res_load_k(const ResTask* T, int nt, float (&wr)[16 * MZ_RES_TASKS],
+                                           const float* __restrict__ Wp, int lane) {
+    if constexpr (K < MZ_RES_TASKS) {
+        if (K < nt) {
+            const int nq = T[K].nq;
+            const float* wb = Wp + T[K].w_off + T[K].ob * (4 * nq * 64) + lane;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) wr[16 * K + i] = i < 4 * nq ? wb[i * 64] : 0.0f;
+        }
+        res_load_k<K + 1>(T, nt, wr, Wp, lane);
+    }
+}
+
+__device__ __forceinline__ void res_load(const int* img, float (&wr)[16 * MZ_RES_TASKS], const float* __restrict__ Wp) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int nt;
+    const ResTask* T = res_tasks(img, wave, nt);
+    res_load_k<0>(T, nt, wr, Wp, lane);
+}
+
+template <int NQ, int OFF>
+__device__ __forceinline__ void res_block(const ResTask& t, const float (&wr)[16 * MZ_RES_TASKS],
+                                          const float* __restrict__ Bp, float* lds, int lane) {
+    const float* xin = lds + t.in_off + lane;
+    const float* bb = Bp + t.b_off + t.ob * 16 + (lane >> 4) * 4;
+    const float b0 = bb[0], b1 = bb[1], b2 = bb[2], b3 = bb[3];
+    float x[4 * NQ];
+#pragma unroll
+    for (int i = 0; i < 4 * NQ; ++i) x[i] = xin[i * 64];
+    mz_f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[OFF + 0 * NQ + j], x[0 * NQ + j], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[OFF + 1 * NQ + j], x[1 * NQ + j], acc1, 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[OFF + 2 * NQ + j], x[2 * NQ + j], acc2, 0, 0, 0);
+        acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[OFF + 3 * NQ + j], x[3 * NQ + j], acc3, 0, 0, 0);
+    }
+    float* out = lds + t.out_off + (t.ob * 16 + (lane >> 4) * 4) * 16 + (lane & 15);
+    float d;
+    d = (acc0[0] + acc1[0]) + (acc2[0] + acc3[0]); d = d + b0; out[0] = mz_act(t.act, d);
+    d = (acc0[1] + acc1[1]) + (acc2[1] + acc3[1]); d = d + b1; out[16] = mz_act(t.act, d);
+    d = (acc0[2] + acc1[2]) + (acc2[2] + acc3[2]); d = d + b2; out[32] = mz_act(t.act, d);
+    d = (acc0[3] + acc1[3]) + (acc2[3] + acc3[3]); d = d + b3; out[48] = mz_act(t.act, d);
+}
+
+template <int K>
+__device__ __forceinline__ void res_run_k(const ResTask* T, int nt, int& cur, const float (&wr)[16 * MZ_RES_TASKS],
+                                          const float* __restrict__ Bp, float* lds, int lane) {
+    if constexpr (K < MZ_RES_TASKS) {
+        if (K < nt) {
+            const ResTask t = T[K];
+            while (cur < t.stage) { __syncthreads(); ++cur; }
+            switch (t.nq) {
+                case 1: res_block<1, 16 * K>(t, wr, Bp, lds, lane); break;
+                case 2: res_block<2, 16 * K>(t, wr, Bp, lds, lane); break;
+                case 3: res_block<3, 16 * K>(t, wr, Bp, lds, lane); break;
+                default: res_block<4, 16 * K>(t, wr, Bp, lds, lane); break;
+            }
+            res_run_k<K + 1>(T, nt, cur, wr, Bp, lds, lane);
+        }
+    }
+}
+
+// Run the resident plan: the same stage barriers as run_plan (every wave
+// executes exactly n_stages barriers, advancing to each task's stage).
+__device__ __forceinline__ void res_run(const int* img, const float (&wr)[16 * MZ_RES_TASKS],
+                                        const float* __restrict__ Bp, float* lds) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ns = img[0];
+    int nt;
+    const ResTask* T = res_tasks(img, wave, nt);
+    int cur = 0;
+    res_run_k<0>(T, nt, cur, wr, Bp, lds, lane);
+    while (cur < ns) { __syncthreads(); ++cur; }
 }

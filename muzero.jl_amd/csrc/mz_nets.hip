@@ -8,7 +8,8 @@
 // LDS -> plan -> out0 (o0 rows) / out1 (o1 rows, softmaxed if sm1).
 extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_forward_kernel(
     const int* plan, const float* Wp, const float* Bp, int total_lds, int in_off, int in_feat,
-    const float* x, int n, int out0_off, int o0, float* out0, int out1_off, int o1, float* out1, int sm1) {
+    const float* x, int n, int out0_off, int o0, float* out0, int out1_off, int o1, float* out1, int sm1,
+    int act0, int act1) {
     extern __shared__ __attribute__((aligned(16))) float act[];
     const int tid = threadIdx.x;
     const int t0 = blockIdx.x * MZ_TILE;
@@ -22,7 +23,7 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_forward_kernel(
     run_plan(plan, Wp, Bp, act);
     for (int i = tid; i < MZ_TILE * o0; i += blockDim.x) {
         const int j = i / o0, k = i - j * o0;
-        if (t0 + j < n) out0[(size_t)(t0 + j) * o0 + k] = act[out0_off + k * 16 + j];
+        if (t0 + j < n) out0[(size_t)(t0 + j) * o0 + k] = mz_post_act(act0, act[out0_off + k * 16 + j]);
     }
     if (out1) {
         if (sm1) {
@@ -38,7 +39,7 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_forward_kernel(
         } else {
             for (int i = tid; i < MZ_TILE * o1; i += blockDim.x) {
                 const int j = i / o1, k = i - j * o1;
-                if (t0 + j < n) out1[(size_t)(t0 + j) * o1 + k] = act[out1_off + k * 16 + j];
+                if (t0 + j < n) out1[(size_t)(t0 + j) * o1 + k] = mz_post_act(act1, act[out1_off + k * 16 + j]);
             }
         }
     }
@@ -80,7 +81,7 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_unroll_kernel(Unroll
         if (tid < MZ_TILE && t0 + tid < P.B) {
             const int j = tid;
             const size_t b = (size_t)(t0 + j);
-            const float v = act[P.lay.v_out + j];
+            const float v = mz_post_act(P.lay.v_act, act[P.lay.v_out + j]);
             float m = act[P.lay.p_out + j];
             for (int k = 1; k < A; ++k) { const float x = act[P.lay.p_out + k * 16 + j]; m = m > x ? m : x; }
             float s = 0.0f;
@@ -91,7 +92,7 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_unroll_kernel(Unroll
                 if (i == 1) P.pp[(b * (K + 1)) * A + k] = p;
             }
             P.pv[b * (K + 1) + i] = v;
-            P.pr[b * (K + 1) + i] = act[P.lay.r_out + j];
+            P.pr[b * (K + 1) + i] = mz_post_act(P.lay.r_act, act[P.lay.r_out + j]);
             if (i == 1) { P.pv[b * (K + 1)] = v; P.pr[b * (K + 1)] = 0.0f; }
         }
         __syncthreads();

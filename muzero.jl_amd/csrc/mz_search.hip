@@ -43,7 +43,7 @@ __device__ __forceinline__ TreeView tree_at(char* base, int E, int NN) {
     return t;
 }
 
-template <bool LDS_TREE>
+template <bool LDS_TREE, bool RES>
 __device__ __forceinline__ void search_body(const SearchParams& P) {
 #ifdef MZ_STAMPS
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -98,6 +98,10 @@ __device__ __forceinline__ void search_body(const SearchParams& P) {
         sg_mmin[g] = INFINITY; sg_mmax[g] = -INFINITY;          // MinMaxStats(Inf, -Inf), :251
     }
     __syncthreads();
+
+    // prediction ‖ dynamics weights stay in registers for all S simulations
+    float wr[16 * MZ_RES_TASKS];
+    if (RES) res_load(P.plan_sim_res, wr, P.Wp);
 
     // ---- representation (:234) -> h_out, prediction(h) (:239) -> v_out, p_out
     run_plan(P.plan_root, P.Wp, P.Bp, act);
@@ -164,7 +168,8 @@ __device__ __forceinline__ void search_body(const SearchParams& P) {
         MZ_STAMP(2);
 
         // ---- prediction(parent.h) ‖ dynamics(2h ⊕ a/|A|)
-        run_plan(P.plan_sim, P.Wp, P.Bp, act);
+        if (RES) res_run(P.plan_sim_res, wr, P.Bp, act);
+        else run_plan(P.plan_sim, P.Wp, P.Bp, act);
         MZ_STAMP(3);
 
         // ---- expand the leaf as slot s+1 (:280)
@@ -187,14 +192,14 @@ __device__ __forceinline__ void search_body(const SearchParams& P) {
             if (a == 0) {
                 const int li = sg_leaf_e[g] * A + sg_leaf_a[g];
                 tree.nc[li] = (tree.nc[li] & 0xffffu) | ((uint32_t)(e_new + 1) << 16);
-                tree.nr[e_new] = act[P.lay.r_out + g];
+                tree.nr[e_new] = mz_post_act(P.lay.r_act, act[P.lay.r_out + g]);
                 tree.ntp[e_new] = (int8_t)tl;
                 path[2 * depth + 1] = e_new;
             }
             __builtin_amdgcn_wave_barrier();
             int rN = sg_rootN[g];
             float rW = sg_rootW[g], mmin = sg_mmin[g], mmax = sg_mmax[g];
-            backup_path(tree, path, depth, act[P.lay.v_out + g], tl, A, P.players, P.discount, rN, rW,
+            backup_path(tree, path, depth, mz_post_act(P.lay.v_act, act[P.lay.v_out + g]), tl, A, P.players, P.discount, rN, rW,
                         sg_root_tp[g], mmin, mmax, a);
             if (a == 0) { sg_rootN[g] = rN; sg_rootW[g] = rW; sg_mmin[g] = mmin; sg_mmax[g] = mmax; }
         }
@@ -226,9 +231,15 @@ __device__ __forceinline__ void search_body(const SearchParams& P) {
 #endif
 }
 
+extern "C" __global__ __launch_bounds__(MZ_THREADS, 1) void mz_search_kernel_lds_res(SearchParams P) {
+    search_body<true, true>(P);
+}
+extern "C" __global__ __launch_bounds__(MZ_THREADS, 1) void mz_search_kernel_hbm_res(SearchParams P) {
+    search_body<false, true>(P);
+}
 extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_search_kernel_lds(SearchParams P) {
-    search_body<true>(P);
+    search_body<true, false>(P);
 }
 extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_search_kernel_hbm(SearchParams P) {
-    search_body<false>(P);
+    search_body<false, false>(P);
 }

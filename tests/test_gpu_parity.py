@@ -159,3 +159,18 @@ def test_learner_steps_bitexact(ttt, nets, B):
         for n in range(3):
             assert np.array_equal(eng.get_weights(n), ora.params[n]), f"step {t} net {n} params differ"
     eng.close()
+
+
+@pytest.mark.parametrize("S,G", [(50, 40), (100, 20)])
+def test_search_bitexact_nonresident_kernel(ttt, nets, S, G, monkeypatch):
+    """The generic (weights streamed from L2) plan executor must agree with the
+    register-resident one and the oracle."""
+    monkeypatch.setenv("MZ_NO_RESIDENT", "1")
+    conf = dataclasses.replace(ttt.conf, num_iters=S)
+    eng, ora = _engine(conf, ttt.hyper, nets, G, 21), _oracle(conf, ttt.hyper, nets, 21)
+    obs, legal, tp = random_positions(G, 21)
+    out_g = eng.mcts_search(obs, legal, tp, rng_step=2)
+    out_o = ora.mcts_search(obs, legal, tp, rng_step=2)
+    for a, b in zip(out_g, out_o):
+        assert np.array_equal(a, b)
+    eng.close()
