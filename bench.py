@@ -187,7 +187,7 @@ def main():
             "learner_config": {"batch_size": B, "num_unroll_steps": K, "mode": "ref_semantics"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 4), "peak": PEAK_F32, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_F32, 5), "traffic": traffic,
-                         "kernel": "mz_search_kernel", "kernel_ms": round(kern_ms, 4),
+                         "kernel": eng.search_variant(), "kernel_ms": round(kern_ms, 4),
                          "flop_per_launch": flop_launch},
             "cpu_baseline": cpu,
         }

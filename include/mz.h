@@ -179,6 +179,9 @@ int mz_learner_grad_dev(mz_handle* h, const mz_batch* dev_batch, float* grad_dev
 int mz_learner_apply_dev(mz_handle* h, const float* grad_dev, float grad_scale,
                          double eta, void* stream);
 
+/* Name of the search kernel variant this handle launches (for profiles). */
+const char* mz_search_variant(const mz_handle* h);
+
 /* Synchronize the handle's stream. */
 int mz_sync(mz_handle* h);
 

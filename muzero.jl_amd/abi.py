@@ -51,6 +51,7 @@ SIGNATURES = {
     "mz_grad_count": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_size_t)]),
     "mz_learner_grad_dev": (ctypes.c_int, [_VP, ctypes.POINTER(MzBatch), _VP, _VP, _VP]),
     "mz_learner_apply_dev": (ctypes.c_int, [_VP, _VP, ctypes.c_float, ctypes.c_double, _VP]),
+    "mz_search_variant": (ctypes.c_char_p, [_VP]),
     "mz_sync": (ctypes.c_int, [_VP]),
 }
 
@@ -208,6 +209,9 @@ class Engine:
     def learner_apply_dev(self, grad_ptr, grad_scale, eta, stream=None):
         self._check(self.lib.mz_learner_apply_dev(self.h, grad_ptr, grad_scale, float(eta), stream),
                     "mz_learner_apply_dev")
+
+    def search_variant(self):
+        return self.lib.mz_search_variant(self.h).decode()
 
     def sync(self):
         self._check(self.lib.mz_sync(self.h), "mz_sync")

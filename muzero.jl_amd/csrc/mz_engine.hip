@@ -693,6 +693,12 @@ int mz_debug_stamps(mz_handle* h, unsigned long long* out, int n_blocks) {
 #endif
 }
 
+const char* mz_search_variant(const mz_handle* h) {
+    if (!h) return "";
+    if (h->use_res) return h->lds_tree ? "mz_search_kernel_lds_res" : "mz_search_kernel_hbm_res";
+    return h->lds_tree ? "mz_search_kernel_lds" : "mz_search_kernel_hbm";
+}
+
 int mz_sync(mz_handle* h) {
     if (!h) return -2;
     MZ_TRY(h, hipSetDevice(h->device));
