@@ -179,7 +179,10 @@ int mz_learner_grad_dev(mz_handle* h, const mz_batch* dev_batch, float* grad_dev
 int mz_learner_apply_dev(mz_handle* h, const float* grad_dev, float grad_scale,
                          double eta, void* stream);
 
-/* Name of the search kernel variant this handle launches (for profiles). */
+/* Name of the search kernel variant the last search launched (for profiles):
+ * mz_search_small{1,2,4} (T games per workgroup, G <= 4 x #CUs) or the
+ * 16-game MFMA tile kernel mz_search_kernel_{lds,hbm}[_res].  Environment
+ * MZ_SEARCH_KERNEL=tile16|small (read at create) forces a family.          */
 const char* mz_search_variant(const mz_handle* h);
 
 /* Synchronize the handle's stream. */

@@ -8,6 +8,8 @@
 
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -18,6 +20,10 @@
 extern "C" __global__ void mz_search_kernel_lds(SearchParams P);
 extern "C" __global__ void mz_search_kernel_hbm(SearchParams P);
 extern "C" __global__ void mz_search_kernel_lds_res(SearchParams P);
+#include "mz_small_params.h"
+extern "C" __global__ void mz_search_small1(SmallParams P);
+extern "C" __global__ void mz_search_small2(SmallParams P);
+extern "C" __global__ void mz_search_small4(SmallParams P);
 extern "C" __global__ void mz_search_kernel_hbm_res(SearchParams P);
 
 extern "C" __global__ void mz_unroll_kernel(UnrollParams P);
@@ -93,6 +99,20 @@ struct mz_handle {
     double* d_pbc = nullptr; double* d_sqrt = nullptr; float* d_aval = nullptr;
     char* d_tree = nullptr; size_t tree_game_bytes = 0; bool lds_tree = false; int dump_tree = 0;
     bool use_res = false;                   // register-resident sim-plan kernel
+    // small-batch kernel (mz_small.hip): schedule images + LDS layout
+    bool small_ok = false;
+    int n_cu = 256;
+    int sm_n_sim = 0, sm_n_root = 0;
+    float* d_sm_w = nullptr;                // [n_sim + n_root][2][256][16] weight image (sim then root)
+    float* d_sm_bias = nullptr;             // [n_sim + n_root][2][64]
+    int* d_sm_srcw = nullptr; int* d_sm_srcb = nullptr;
+    size_t sm_w_n = 0, sm_b_n = 0;
+    int* d_sm_rec[3] = {nullptr, nullptr, nullptr};   // per T in {1,2,4}
+    int sm_lay[3][8];                       // per T: act_total, x_rep, x_pred, x_dyn, h_out, v_out, p_out, r_out
+    size_t sm_lds[3] = {0, 0, 0};
+    int force_kernel = 0;                   // 0 auto, 1 tile16, 2 small
+    std::string last_variant = "none";
+    int force_T = 0;                        // MZ_SMALL_T=1|2|4 (tests)
     float* d_hid = nullptr;
     float* d_obs = nullptr; uint8_t* d_legal = nullptr; int32_t* d_tp = nullptr;
     float* d_cv = nullptr; float* d_rv = nullptr; int32_t* d_act = nullptr;
@@ -294,6 +314,183 @@ static int build_plans(mz_handle* h) {
     return 0;
 }
 
+
+// ------------------------------------------------------------- small kernel
+// Schedule the layers of one network set onto stages x 2 slots x 16 4-row
+// blocks (mz_small.hip): list scheduling by longest remaining path; layers
+// sharing a slot must have equal kq.  Returns false if not eligible.
+struct SmSched {
+    int n_stages = 0;
+    std::vector<int> stage;            // per layer-in-set
+    std::vector<int> slot, block0;
+    std::vector<int> kq[SM_MAX_SIM > SM_MAX_ROOT ? SM_MAX_SIM : SM_MAX_ROOT];
+};
+
+static bool sm_schedule(const mz_handle* h, const std::vector<int>& set, const std::vector<std::vector<int>>& deps,
+                        int max_stages, std::vector<int>& st, std::vector<int>& sl, std::vector<int>& b0,
+                        std::vector<std::array<int, 2>>& stage_kq) {
+    const int n = (int)set.size();
+    std::vector<int> prio(n, 1);
+    for (int it = 0; it < n; ++it)             // longest path to the end (deps point backwards)
+        for (int i = 0; i < n; ++i)
+            for (int d : deps[i]) prio[d] = std::max(prio[d], prio[i] + 1);
+    st.assign(n, -1); sl.assign(n, -1); b0.assign(n, -1);
+    stage_kq.clear();
+    int done = 0;
+    for (int s = 0; done < n; ++s) {
+        if (s >= max_stages) return false;
+        std::vector<int> ready;
+        for (int i = 0; i < n; ++i) {
+            if (st[i] >= 0) continue;
+            bool ok = true;
+            for (int d : deps[i]) ok &= st[d] >= 0 && st[d] < s;
+            if (ok) ready.push_back(i);
+        }
+        std::stable_sort(ready.begin(), ready.end(), [&](int a, int b) { return prio[a] > prio[b]; });
+        int fr[2] = {16, 16};
+        std::array<int, 2> kq = {0, 0};
+        for (int i : ready) {
+            const LayerSpec& L = h->layers[set[i]];
+            const int nb = (L.out + 3) / 4, k = 4 * ((L.in + 15) / 16);
+            for (int x = 0; x < 2; ++x)
+                if (fr[x] >= nb && (kq[x] == 0 || kq[x] == k)) {
+                    st[i] = s; sl[i] = x; b0[i] = 16 - fr[x]; fr[x] -= nb; kq[x] = k; ++done;
+                    break;
+                }
+        }
+        stage_kq.push_back(kq);
+    }
+    return true;
+}
+
+static int build_small(mz_handle* h) {
+    for (const LayerSpec& L : h->layers)
+        if (L.in > 64 || L.out > 64) return 0;          // not eligible: tile-16 kernel only
+    if (h->A > 16) return 0;
+    // network sets: SIM = prediction + dynamics, ROOT = representation
+    std::vector<int> sim, root;
+    auto add_net = [&](std::vector<int>& set, int net) {
+        for (int ch = 0; ch < 3; ++ch) for (int li : h->chains[net][ch]) set.push_back(li);
+    };
+    add_net(sim, MZ_NET_PRED); add_net(sim, MZ_NET_DYN); add_net(root, MZ_NET_REPR);
+    auto deps_of = [&](const std::vector<int>& set) {
+        std::vector<std::vector<int>> d(set.size());
+        auto pos = [&](int li) { for (size_t i = 0; i < set.size(); ++i) if (set[i] == li) return (int)i; return -1; };
+        for (size_t i = 0; i < set.size(); ++i) {
+            const LayerSpec& L = h->layers[set[i]];
+            const auto& chain = h->chains[L.net][L.chain];
+            const int k = (int)(std::find(chain.begin(), chain.end(), set[i]) - chain.begin());
+            if (k > 0) d[i].push_back(pos(chain[k - 1]));
+            else if (L.chain != CH_TRUNK) d[i].push_back(pos(h->chains[L.net][CH_TRUNK].back()));
+        }
+        return d;
+    };
+    std::vector<int> st_s, sl_s, b0_s, st_r, sl_r, b0_r;
+    std::vector<std::array<int, 2>> kq_s, kq_r;
+    if (!sm_schedule(h, sim, deps_of(sim), SM_MAX_SIM, st_s, sl_s, b0_s, kq_s)) return 0;
+    if (!sm_schedule(h, root, deps_of(root), SM_MAX_ROOT, st_r, sl_r, b0_r, kq_r)) return 0;
+    h->sm_n_sim = (int)kq_s.size();
+    h->sm_n_root = (int)kq_r.size();
+    const int nrec = h->sm_n_sim + h->sm_n_root;
+    // weight / bias gather images: [rec][slot][q*64 + lane][16] and [rec][slot][row]
+    std::vector<int> sw((size_t)nrec * 2 * 256 * 16, -1), sb((size_t)nrec * 2 * 64, -1);
+    auto fill = [&](const std::vector<int>& set, const std::vector<int>& st, const std::vector<int>& sl,
+                    const std::vector<int>& b0, int rec0) {
+        for (size_t i = 0; i < set.size(); ++i) {
+            const LayerSpec& L = h->layers[set[i]];
+            const int kq = 4 * ((L.in + 15) / 16), r = rec0 + st[i];
+            for (int row = 0; row < L.out; ++row) {
+                const int srow = 4 * b0[i] + row;                       // slot row
+                sb[((size_t)r * 2 + sl[i]) * 64 + srow] = (int)(L.flux_b + row);
+                for (int q = 0; q < 4; ++q)
+                    for (int j = 0; j < kq; ++j) {
+                        const int k = q * kq + j;
+                        if (k >= L.in) continue;
+                        sw[(((size_t)r * 2 + sl[i]) * 256 + q * 64 + srow) * 16 + j] =
+                            (int)(L.flux_w + row + (size_t)L.out * k);
+                    }
+            }
+        }
+    };
+    fill(sim, st_s, sl_s, b0_s, 0);
+    fill(root, st_r, sl_r, b0_r, h->sm_n_sim);
+    h->sm_w_n = sw.size(); h->sm_b_n = sb.size();
+    MZ_TRY(h, dalloc(h, &h->d_sm_srcw, sw.size()));
+    MZ_TRY(h, dalloc(h, &h->d_sm_srcb, sb.size()));
+    MZ_TRY(h, dalloc(h, &h->d_sm_w, sw.size()));
+    MZ_TRY(h, dalloc(h, &h->d_sm_bias, sb.size()));
+    MZ_TRY(h, hipMemcpy(h->d_sm_srcw, sw.data(), sw.size() * 4, hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(h->d_sm_srcb, sb.data(), sb.size() * 4, hipMemcpyHostToDevice));
+    // per-T LDS layouts and records
+    const int Ts[3] = {1, 2, 4};
+    for (int ti = 0; ti < 3; ++ti) {
+        const int T = Ts[ti];
+        int off = 0;
+        auto region = [&](int rows) { int o = off; off += (rows * T + 3) / 4 * 4; return o; };
+        auto in_rows = [&](int net) { const LayerSpec& L = h->layers[h->chains[net][CH_TRUNK][0]]; return 4 * 4 * ((L.in + 15) / 16); };
+        int* lay = h->sm_lay[ti];
+        lay[1] = region(in_rows(MZ_NET_REPR));
+        lay[2] = region(in_rows(MZ_NET_PRED));
+        lay[3] = region(in_rows(MZ_NET_DYN));
+        lay[4] = region(h->H);
+        lay[5] = region(1);
+        lay[6] = region(h->A);
+        lay[7] = region(1);
+        int cb[3][3][2];
+        for (int net = 0; net < 3; ++net)
+            for (int ch = 0; ch < 3; ++ch) { cb[net][ch][0] = region(64); cb[net][ch][1] = region(64); }
+        lay[0] = off;
+        auto io = [&](int li, int& in_off, int& out_off) {
+            const LayerSpec& L = h->layers[li];
+            const auto& chain = h->chains[L.net][L.chain];
+            const int k = (int)(std::find(chain.begin(), chain.end(), li) - chain.begin());
+            const int n = (int)chain.size();
+            const auto& trunk = h->chains[L.net][CH_TRUNK];
+            const int trunk_out = cb[L.net][CH_TRUNK][((int)trunk.size() - 1) & 1];
+            if (k > 0) in_off = cb[L.net][L.chain][(k - 1) & 1];
+            else if (L.chain != CH_TRUNK) in_off = trunk_out;
+            else in_off = L.net == MZ_NET_REPR ? lay[1] : L.net == MZ_NET_PRED ? lay[2] : lay[3];
+            if (k < n - 1) out_off = cb[L.net][L.chain][k & 1];
+            else if (L.chain == CH_TRUNK) out_off = L.net == MZ_NET_REPR ? lay[4] : trunk_out;
+            else if (L.net == MZ_NET_PRED) out_off = L.chain == CH_HEAD1 ? lay[5] : lay[6];
+            else out_off = L.chain == CH_HEAD1 ? lay[4] : lay[7];
+        };
+        std::vector<int> rec((size_t)nrec * SM_REC_INTS, 0);
+        for (int r = 0; r < nrec; ++r) {
+            int* R = rec.data() + (size_t)r * SM_REC_INTS;
+            for (int i = 2; i < 2 + 256; ++i) R[i] = -1;       // xb and ob
+            const auto& kq = r < h->sm_n_sim ? kq_s[r] : kq_r[r - h->sm_n_sim];
+            R[0] = kq[0]; R[1] = kq[1];
+        }
+        auto rec_fill = [&](const std::vector<int>& set, const std::vector<int>& st, const std::vector<int>& sl,
+                            const std::vector<int>& b0, int rec0) {
+            for (size_t i = 0; i < set.size(); ++i) {
+                const LayerSpec& L = h->layers[set[i]];
+                int in_off, out_off;
+                io(set[i], in_off, out_off);
+                int* R = rec.data() + (size_t)(rec0 + st[i]) * SM_REC_INTS;
+                const int nb = (L.out + 3) / 4;
+                for (int b = b0[i]; b < b0[i] + nb; ++b)
+                    for (int gm = 0; gm < 4; ++gm) R[2 + sl[i] * 64 + 4 * b + gm] = gm < T ? in_off + gm : -1;
+                for (int row = 0; row < L.out; ++row) {
+                    const int srow = 4 * b0[i] + row;
+                    R[130 + sl[i] * 64 + srow] = out_off + row * T;
+                    R[386 + sl[i] * 64 + srow] = L.act == MZ_ACT_RELU ? 1 : 0;
+                }
+            }
+        };
+        rec_fill(sim, st_s, sl_s, b0_s, 0);
+        rec_fill(root, st_r, sl_r, b0_r, h->sm_n_sim);
+        MZ_TRY(h, dalloc(h, &h->d_sm_rec[ti], rec.size()));
+        MZ_TRY(h, hipMemcpy(h->d_sm_rec[ti], rec.data(), rec.size() * 4, hipMemcpyHostToDevice));
+        const int S = h->S, NN = S + 1, PS = 2 * (S + 2);
+        size_t ints = (size_t)lay[0] + 2048 + ((size_t)nrec * SM_REC_INTS + 3) / 4 * 4 +
+                      ((size_t)T * NN * h->H + 3) / 4 * 4 + 224 + ((size_t)T * PS + 3) / 4 * 4;
+        h->sm_lds[ti] = ints * 4 + (size_t)T * h->tree_game_bytes;
+    }
+    return 1;
+}
+
 // MFMA fragment image: packed W [ob][ks][lane] <- W[ob*16 + (lane&15)][ks*4 + (lane>>4)]
 // (Flux W is (out,in) column-major: element (o,i) at flux_w + o + out*i).
 static int build_pack_index(mz_handle* h) {
@@ -316,12 +513,19 @@ static int build_pack_index(mz_handle* h) {
     return 0;
 }
 
-static int repack(mz_handle* h) {
+static int repack(mz_handle* h, hipStream_t st = nullptr) {
     const int T = 256;
-    hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_w_n + T - 1) / T)), dim3(T), 0, h->stream,
+    if (!st) st = h->stream;
+    hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_w_n + T - 1) / T)), dim3(T), 0, st,
                        h->d_flat, h->d_srcW, h->d_Wp, h->packed_w_n);
-    hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_b_n + T - 1) / T)), dim3(T), 0, h->stream,
+    hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_b_n + T - 1) / T)), dim3(T), 0, st,
                        h->d_flat, h->d_srcB, h->d_Bp, h->packed_b_n);
+    if (h->small_ok) {
+        hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->sm_w_n + T - 1) / T)), dim3(T), 0, st,
+                           h->d_flat, h->d_sm_srcw, h->d_sm_w, h->sm_w_n);
+        hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->sm_b_n + T - 1) / T)), dim3(T), 0, st,
+                           h->d_flat, h->d_sm_srcb, h->d_sm_bias, h->sm_b_n);
+    }
     MZ_TRY(h, hipGetLastError());
     return 0;
 }
@@ -386,6 +590,25 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
     CK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess ? 0 : fail(h, "hipStreamCreate"));
     CK(build_plans(h));
     CK(build_pack_index(h));
+    {
+        int r = build_small(h);
+        if (r < 0) { g_create_error = h->err; mz_engine_destroy(h); return r; }
+        h->small_ok = r == 1;
+        for (int ti = 0; ti < 3 && h->small_ok; ++ti) h->small_ok = h->sm_lds[ti] <= kLdsMax;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess) h->n_cu = prop.multiProcessorCount;
+        const char* fk = std::getenv("MZ_SEARCH_KERNEL");
+        if (fk) h->force_kernel = std::strcmp(fk, "tile16") == 0 ? 1 : std::strcmp(fk, "small") == 0 ? 2 : 0;
+        const char* ft = std::getenv("MZ_SMALL_T");
+        if (ft) { const int t = std::atoi(ft); h->force_T = (t == 1 || t == 2 || t == 4) ? t : 0; }
+        if (h->small_ok) {
+            const void* ks[3] = {(const void*)mz_search_small1, (const void*)mz_search_small2,
+                                 (const void*)mz_search_small4};
+            for (int ti = 0; ti < 3; ++ti)
+                CK(hipFuncSetAttribute(ks[ti], hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->sm_lds[ti]) ==
+                           hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(small)"));
+        }
+    }
     const int S = h->S, A = h->A, H = h->H;
     const size_t G = (size_t)max_games;
     auto al = [&](auto** p, size_t n) -> int { MZ_TRY(h, dalloc(h, p, n)); return 0; };
@@ -516,12 +739,46 @@ int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* leg
     P.tree = h->d_tree; P.tree_game_bytes = h->tree_game_bytes; P.dump_tree = h->dump_tree;
     P.hid = h->d_hid;
 #ifdef MZ_STAMPS
-    if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * ((h->max_games + MZ_TILE - 1) / MZ_TILE)));
+    if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * h->max_games));
     P.stamps = h->d_stamps;
 #endif
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    hipLaunchKernelGGL(search_kernel(h), dim3((G + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
-                       search_lds_bytes(h), st, P);
+    const bool small = h->small_ok && h->force_kernel != 1 && (h->force_kernel == 2 || G <= 4 * h->n_cu);
+    if (small) {
+        const int T = h->force_T ? h->force_T : G <= h->n_cu ? 1 : G <= 2 * h->n_cu ? 2 : 4;
+        const int ti = T == 1 ? 0 : T == 2 ? 1 : 2;
+        SmallParams Q;
+        std::memset(&Q, 0, sizeof(Q));
+        Q.G = G; Q.S = h->S; Q.A = h->A; Q.H = h->H; Q.players = h->conf.players; Q.obs_feat = h->obs_feat;
+        Q.plane = h->plane; Q.exploration = exploration; Q.rng_step = rng_step; Q.game_offset = game_offset;
+        Q.seed = h->seed; Q.temperature = temperature; Q.discount = h->conf.discount;
+        Q.dirichlet_alpha = h->conf.dirichlet_alpha; Q.exploration_eps = h->conf.exploration_eps;
+        Q.obs = obs; Q.legal = legal_mask; Q.to_play = to_play;
+        Q.child_visits = child_visits; Q.root_value = root_value; Q.action_out = action_out;
+        Q.n_sim = h->sm_n_sim; Q.n_root = h->sm_n_root;
+        Q.w_sim = h->d_sm_w;
+        Q.w_root = h->d_sm_w + (size_t)h->sm_n_sim * SM_SLOTS * SM_THREADS * 16;
+        Q.rec = h->d_sm_rec[ti]; Q.bias = h->d_sm_bias;
+        const int* lay = h->sm_lay[ti];
+        Q.act_total = lay[0]; Q.x_rep = lay[1]; Q.x_pred = lay[2]; Q.x_dyn = lay[3]; Q.h_out = lay[4];
+        Q.v_out = lay[5]; Q.p_out = lay[6]; Q.r_out = lay[7];
+        Q.v_act = h->lay.v_act; Q.r_act = h->lay.r_act;
+        Q.pbc_tab = h->d_pbc; Q.sqrt_tab = h->d_sqrt; Q.aval_tab = h->d_aval;
+        Q.tree = h->d_tree; Q.tree_game_bytes = h->tree_game_bytes; Q.dump_tree = h->dump_tree;
+#ifdef MZ_STAMPS
+        Q.stamps = h->d_stamps;
+#endif
+        const void* k = T == 1 ? (const void*)mz_search_small1 : T == 2 ? (const void*)mz_search_small2
+                                                                        : (const void*)mz_search_small4;
+        void* args[] = {&Q};
+        MZ_TRY(h, hipLaunchKernel(k, dim3((G + T - 1) / T), dim3(SM_THREADS), args, h->sm_lds[ti], st));
+        h->last_variant = T == 1 ? "mz_search_small1" : T == 2 ? "mz_search_small2" : "mz_search_small4";
+    } else {
+        hipLaunchKernelGGL(search_kernel(h), dim3((G + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
+                           search_lds_bytes(h), st, P);
+        h->last_variant = h->use_res ? (h->lds_tree ? "mz_search_kernel_lds_res" : "mz_search_kernel_hbm_res")
+                                     : (h->lds_tree ? "mz_search_kernel_lds" : "mz_search_kernel_hbm");
+    }
     MZ_TRY(h, hipGetLastError());
     return 0;
 }
@@ -645,13 +902,7 @@ int mz_learner_apply_dev(mz_handle* h, const float* grad_dev, float grad_scale, 
                        grad_scale, h->nflat, h->bp1, h->bp2, eta);
     h->bp1 = h->bp1 * 0.9;                  // βp .= βp .* β
     h->bp2 = h->bp2 * 0.999;
-    const int T = 256;
-    hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_w_n + T - 1) / T)), dim3(T), 0, st, h->d_flat,
-                       h->d_srcW, h->d_Wp, h->packed_w_n);
-    hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_b_n + T - 1) / T)), dim3(T), 0, st, h->d_flat,
-                       h->d_srcB, h->d_Bp, h->packed_b_n);
-    MZ_TRY(h, hipGetLastError());
-    return 0;
+    return repack(h, st);
 }
 
 int mz_learner_step(mz_handle* h, const mz_batch* b, double eta, float* losses_out) {
@@ -695,8 +946,7 @@ int mz_debug_stamps(mz_handle* h, unsigned long long* out, int n_blocks) {
 
 const char* mz_search_variant(const mz_handle* h) {
     if (!h) return "";
-    if (h->use_res) return h->lds_tree ? "mz_search_kernel_lds_res" : "mz_search_kernel_hbm_res";
-    return h->lds_tree ? "mz_search_kernel_lds" : "mz_search_kernel_hbm";
+    return h->last_variant.c_str();
 }
 
 int mz_sync(mz_handle* h) {

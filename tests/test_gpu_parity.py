@@ -80,11 +80,25 @@ def _compare_trees(tg, to, G):
             assert np.array_equal(a, b), f"tree {k} differs at {np.argwhere(a != b)[:5]}"
 
 
+KERNELS = [("tile16", None), ("small", "1"), ("small", "2"), ("small", "4")]
+
+
+def _force(monkeypatch, kernel):
+    fam, t = kernel
+    monkeypatch.setenv("MZ_SEARCH_KERNEL", fam)
+    if t:
+        monkeypatch.setenv("MZ_SMALL_T", t)
+    else:
+        monkeypatch.delenv("MZ_SMALL_T", raising=False)
+
+
+@pytest.mark.parametrize("kernel", KERNELS, ids=["tile16", "small1", "small2", "small4"])
 @pytest.mark.parametrize("S,G,explore,temp,seed", [
     (1, 16, True, 1.0, 1), (10, 16, True, 1.0, 2), (25, 33, True, 1.0, 3),
     (50, 64, True, 1.0, 4), (50, 20, False, 0.0, 5), (12, 48, True, float("inf"), 6),
     (12, 17, True, 0.5, 7), (100, 16, True, 1.0, 8)])
-def test_search_bitexact(ttt, nets, S, G, explore, temp, seed):
+def test_search_bitexact(ttt, nets, S, G, explore, temp, seed, kernel, monkeypatch):
+    _force(monkeypatch, kernel)
     conf = dataclasses.replace(ttt.conf, num_iters=S)
     eng, ora = _engine(conf, ttt.hyper, nets, G, seed), _oracle(conf, ttt.hyper, nets, seed)
     obs, legal, tp = random_positions(G, seed)
@@ -103,7 +117,9 @@ def test_search_bitexact(ttt, nets, S, G, explore, temp, seed):
     eng.close()
 
 
-def test_search_single_legal_and_one_player(ttt, nets):
+@pytest.mark.parametrize("kernel", KERNELS, ids=["tile16", "small1", "small2", "small4"])
+def test_search_single_legal_and_one_player(ttt, nets, kernel, monkeypatch):
+    _force(monkeypatch, kernel)
     conf = dataclasses.replace(ttt.conf, num_iters=20, players=[1])
     G = 24
     eng, ora = _engine(conf, ttt.hyper, nets, G, 9), _oracle(conf, ttt.hyper, nets, 9)
@@ -166,6 +182,7 @@ def test_search_bitexact_nonresident_kernel(ttt, nets, S, G, monkeypatch):
     """The generic (weights streamed from L2) plan executor must agree with the
     register-resident one and the oracle."""
     monkeypatch.setenv("MZ_NO_RESIDENT", "1")
+    monkeypatch.setenv("MZ_SEARCH_KERNEL", "tile16")
     conf = dataclasses.replace(ttt.conf, num_iters=S)
     eng, ora = _engine(conf, ttt.hyper, nets, G, 21), _oracle(conf, ttt.hyper, nets, 21)
     obs, legal, tp = random_positions(G, 21)
@@ -174,3 +191,20 @@ def test_search_bitexact_nonresident_kernel(ttt, nets, S, G, monkeypatch):
     for a, b in zip(out_g, out_o):
         assert np.array_equal(a, b)
     eng.close()
+
+
+def test_search_auto_dispatch_large_batches(ttt, nets, monkeypatch):
+    """G = 512 (the benchmark batch) picks the 2-games-per-CU small kernel and
+    G = 1536 the 16-game tile kernel; both bit-exact vs the oracle."""
+    monkeypatch.delenv("MZ_SEARCH_KERNEL", raising=False)
+    monkeypatch.delenv("MZ_SMALL_T", raising=False)
+    conf = dataclasses.replace(ttt.conf, num_iters=12)
+    for G, fam in [(512, "mz_search_small2"), (1536, "mz_search_kernel")]:
+        eng, ora = _engine(conf, ttt.hyper, nets, G, 33), _oracle(conf, ttt.hyper, nets, 33)
+        obs, legal, tp = random_positions(G, 40 + G)
+        out_g = eng.mcts_search(obs, legal, tp, rng_step=3)
+        assert eng.search_variant().startswith(fam), eng.search_variant()
+        out_o = ora.mcts_search(obs, legal, tp, rng_step=3)
+        for a, b in zip(out_g, out_o):
+            assert np.array_equal(a, b)
+        eng.close()
