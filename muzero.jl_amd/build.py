@@ -9,7 +9,11 @@ HEADERS = ["mz_internal.h", "mz_mlp_device.h", "mz_tree_device.h", "mz_small_par
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
          # the numerics contract (include/mz_detmath.h): no FP contraction, IEEE
          # division/sqrt, f32 denormals kept (hipcc defaults for the last two)
-         "-ffp-contract=off", "-fno-fast-math", "-Wno-unused-result"]
+         "-ffp-contract=off", "-fno-fast-math", "-Wno-unused-result",
+         # the SLP vectorizer packs the small kernel's per-game fmaf chains into
+         # v_pk_fma_f32 with each resident weight duplicated into a register
+         # pair (2x the weight registers -> spills); scalar fmaf keeps 1x
+         "-fno-slp-vectorize"]
 
 
 def build(force=False, verbose=False):

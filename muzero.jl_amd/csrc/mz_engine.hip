@@ -427,11 +427,12 @@ static int build_small(mz_handle* h) {
         const int T = Ts[ti];
         int off = 0;
         auto region = [&](int rows) { int o = off; off += (rows * T + 3) / 4 * 4; return o; };
-        auto in_rows = [&](int net) { const LayerSpec& L = h->layers[h->chains[net][CH_TRUNK][0]]; return 4 * 4 * ((L.in + 15) / 16); };
+        // every input buffer has 64 rows (zero beyond K): the kernel runs 16
+        // steps per quarter and reads rows up to 3*kq + 15 < 64
         int* lay = h->sm_lay[ti];
-        lay[1] = region(in_rows(MZ_NET_REPR));
-        lay[2] = region(in_rows(MZ_NET_PRED));
-        lay[3] = region(in_rows(MZ_NET_DYN));
+        lay[1] = region(64);
+        lay[2] = region(64);
+        lay[3] = region(64);
         lay[4] = region(h->H);
         lay[5] = region(1);
         lay[6] = region(h->A);
@@ -455,13 +456,11 @@ static int build_small(mz_handle* h) {
             else if (L.net == MZ_NET_PRED) out_off = L.chain == CH_HEAD1 ? lay[5] : lay[6];
             else out_off = L.chain == CH_HEAD1 ? lay[4] : lay[7];
         };
+        // int4 per [stage][slot][row]: {input base, kq, out | relu << 30 (-1 =
+        // unused), bias (filled on device)}; unused rows read offset 0 with
+        // zero weights
         std::vector<int> rec((size_t)nrec * SM_REC_INTS, 0);
-        for (int r = 0; r < nrec; ++r) {
-            int* R = rec.data() + (size_t)r * SM_REC_INTS;
-            for (int i = 2; i < 2 + 256; ++i) R[i] = -1;       // xb and ob
-            const auto& kq = r < h->sm_n_sim ? kq_s[r] : kq_r[r - h->sm_n_sim];
-            R[0] = kq[0]; R[1] = kq[1];
-        }
+        for (size_t i = 0; i < rec.size(); i += 4) rec[i + 2] = -1;
         auto rec_fill = [&](const std::vector<int>& set, const std::vector<int>& st, const std::vector<int>& sl,
                             const std::vector<int>& b0, int rec0) {
             for (size_t i = 0; i < set.size(); ++i) {
@@ -469,13 +468,12 @@ static int build_small(mz_handle* h) {
                 int in_off, out_off;
                 io(set[i], in_off, out_off);
                 int* R = rec.data() + (size_t)(rec0 + st[i]) * SM_REC_INTS;
-                const int nb = (L.out + 3) / 4;
-                for (int b = b0[i]; b < b0[i] + nb; ++b)
-                    for (int gm = 0; gm < 4; ++gm) R[2 + sl[i] * 64 + 4 * b + gm] = gm < T ? in_off + gm : -1;
+                const int kq = 4 * ((L.in + 15) / 16);
                 for (int row = 0; row < L.out; ++row) {
-                    const int srow = 4 * b0[i] + row;
-                    R[130 + sl[i] * 64 + srow] = out_off + row * T;
-                    R[386 + sl[i] * 64 + srow] = L.act == MZ_ACT_RELU ? 1 : 0;
+                    int* e = R + 4 * (sl[i] * 64 + 4 * b0[i] + row);
+                    e[0] = in_off;
+                    e[1] = kq;
+                    e[2] = (out_off + row * T) | (L.act == MZ_ACT_RELU ? 1 << 30 : 0);
                 }
             }
         };
@@ -484,7 +482,7 @@ static int build_small(mz_handle* h) {
         MZ_TRY(h, dalloc(h, &h->d_sm_rec[ti], rec.size()));
         MZ_TRY(h, hipMemcpy(h->d_sm_rec[ti], rec.data(), rec.size() * 4, hipMemcpyHostToDevice));
         const int S = h->S, NN = S + 1, PS = 2 * (S + 2);
-        size_t ints = (size_t)lay[0] + 2048 + ((size_t)nrec * SM_REC_INTS + 3) / 4 * 4 +
+        size_t ints = (size_t)lay[0] + (size_t)(nrec + 1) * SM_REC_INTS +
                       ((size_t)T * NN * h->H + 3) / 4 * 4 + 224 + ((size_t)T * PS + 3) / 4 * 4;
         h->sm_lds[ti] = ints * 4 + (size_t)T * h->tree_game_bytes;
     }
@@ -757,7 +755,7 @@ int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* leg
         Q.child_visits = child_visits; Q.root_value = root_value; Q.action_out = action_out;
         Q.n_sim = h->sm_n_sim; Q.n_root = h->sm_n_root;
         Q.w_sim = h->d_sm_w;
-        Q.w_root = h->d_sm_w + (size_t)h->sm_n_sim * SM_SLOTS * SM_THREADS * 16;
+        Q.w_root = h->d_sm_w + (size_t)h->sm_n_sim * SM_SLOTS * 256 * 16;
         Q.rec = h->d_sm_rec[ti]; Q.bias = h->d_sm_bias;
         const int* lay = h->sm_lay[ti];
         Q.act_total = lay[0]; Q.x_rep = lay[1]; Q.x_pred = lay[2]; Q.x_dyn = lay[3]; Q.h_out = lay[4];

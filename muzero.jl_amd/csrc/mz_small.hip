@@ -1,18 +1,17 @@
-// mz_small.hip — batched MCTS for SMALL batches (G <= 4 x #CUs): one 256-
+// mz_small.hip — batched MCTS for SMALL batches (G <= 4 x #CUs): one 512-
 // thread workgroup per T in {1, 2, 4} games, so G = 512 spreads over all 256
 // CUs of an MI355X instead of the 32 tiles of the 16-game MFMA kernel
 // (mz_search.hip), and each simulation waits for the deepest of T games only.
 //
-// Networks with v_mfma_f32_4x4x1_16b_f32 (16 blocks x 4 rows = one 64-row
-// Dense layer, 4 columns = up to 4 games, K = 1 per instruction: a chain of
-// them is a k-ordered fmaf chain, bit for bit — tools/mfma4x4_probe.hip).
-// Wave q of the workgroup runs k-quarter q of the canonical dot order
-// (mz_dot): kq steps over k in [q*kq, (q+1)*kq), weights resident as the MFMA
-// A operand for the whole search.  Every wave serves TWO layers ("slots") per
-// stage; a layer narrower than 64 rows uses only some 4-row blocks, and a slot
-// may hold several such layers (block b reads its own input: the B operand of
-// lane 4b+g is game g of that block's input).  The four quarter partials meet
-// in LDS and one combine pass forms ((p0+p1)+(p2+p3)) + b and the activation.
+// Networks on the VALU.  A stage runs two layers ("slots"), one per 256
+// threads; thread -> (slot row r, k-quarter q) runs the 16-step fmaf chain of
+// quarter q of the canonical dot order (mz_dot) for its T games with its 16
+// weights resident in registers for the whole search, and a quad DPP
+// exchange forms ((p0+p1)+(p2+p3)) + b.  A dependent fma costs a few cycles
+// where a dependent v_mfma_f32_4x4x1 costs 45 (tools/mfma_rate_probe.hip),
+// and each quarter is a 16-step dependent chain, so the VALU is the
+// latency-optimal unit here.  A slot row belongs to one layer (4-row blocks;
+// narrow layers share a slot).
 // Tree (mz_tree_device.h) and hidden states live in LDS; the host builds the
 // stage schedule (mz_engine.hip, build_small_schedule).
 #include "mz_mlp_device.h"
@@ -32,79 +31,94 @@
 #define SM_STAMP(i) do {} while (0)
 #endif
 
-// One stage: both slots' quarter chains, partials to LDS, combine.
+// One stage on the VALU.  Thread t: slot = t >> 8, slot row r = (t & 255) >> 2,
+// k-quarter q = t & 3.  The lane runs the 16-step fmaf chain of its quarter
+// for each of the T games (weights resident; zero beyond the layer's kq, and
+// the 64-row input buffers are zero beyond K, so the extra steps are exact
+// no-ops), then a quad DPP exchange forms ((p0+p1)+(p2+p3)) and lane q == 0
+// adds the bias, applies the activation and writes the output row.
+// rec4 points at this thread's record of stage K; the record of stage K+1
+// (constant for the whole kernel) is fetched while stage K computes.
 template <int T>
-__device__ __forceinline__ void sm_stage(const float (&wa)[16], const float (&wb)[16], const int* rec,
-                                         float* lds, float* part) {
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int q = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ka = rec[0], kb = rec[1];
-    const int xa = rec[2 + lane], xb = rec[2 + 64 + lane];
-    sm_f32x4 da = {0.f, 0.f, 0.f, 0.f}, db = da;
+__device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int4* rec_next, float* lds) {
+    const int q = threadIdx.x & 3;
+    // all 16*T inputs of the quarter issued at once (contiguous, 16-byte
+    // aligned; batches of 32 registers), then the fmaf chain
+    const float4* x = reinterpret_cast<const float4*>(lds + R.x + q * R.y * T);
+    constexpr int NB = T == 4 ? 2 : 1, PER = 4 * T / NB, JB = 16 / NB;
+    float acc[T];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        if (j < ka) {
-            const float va = xa >= 0 ? lds[xa + (q * ka + j) * T] : 0.0f;
-            da = __builtin_amdgcn_mfma_f32_4x4x1f32(wa[j], va, da, 0, 0, 0);
-        }
-        if (j < kb) {
-            const float vb = xb >= 0 ? lds[xb + (q * kb + j) * T] : 0.0f;
-            db = __builtin_amdgcn_mfma_f32_4x4x1f32(wb[j], vb, db, 0, 0, 0);
+    for (int g = 0; g < T; ++g) acc[g] = 0.0f;
+    int4 Rn;
+#pragma unroll
+    for (int bt = 0; bt < NB; ++bt) {
+        float4 v[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) v[i] = x[bt * PER + i];
+        if (bt == 0) Rn = *rec_next;
+        __builtin_amdgcn_sched_barrier(0);
+        const float* xv = reinterpret_cast<const float*>(v);
+#pragma unroll
+        for (int j = 0; j < JB; ++j)
+#pragma unroll
+            for (int g = 0; g < T; ++g) acc[g] = fmaf(w[bt * JB + j], xv[j * T + g], acc[g]);
+    }
+#pragma unroll
+    for (int g = 0; g < T; ++g) {
+        const float t = acc[g] + dpp_f(acc[g], 0xB1);      // lane q0: p0+p1, q2: p2+p3
+        acc[g] = t + dpp_f(t, 0x4E);                         // lane q0: (p0+p1)+(p2+p3)
+    }
+    if (q == 0 && R.z >= 0) {
+        const int o = R.z & 0x3fffffff;
+        const bool relu = (R.z >> 30) != 0;
+        const float bias = __int_as_float(R.w);
+#pragma unroll
+        for (int g = 0; g < T; ++g) {
+            const float d = acc[g] + bias;
+            lds[o + g] = relu ? mz_relu(d) : d;
         }
     }
-    // partials: part[slot][q][lane][4]
-    *reinterpret_cast<sm_f32x4*>(part + ((0 * 4 + q) * 64 + lane) * 4) = da;
-    *reinterpret_cast<sm_f32x4*>(part + ((1 * 4 + q) * 64 + lane) * 4) = db;
     __syncthreads();
-    // combine: output (slot, row r, game g) <- D lane 4*(r/4) + g, reg r%4
-    const int* obp = rec + 2 + 128;
-    for (int i = tid; i < SM_SLOTS * 64 * T; i += SM_THREADS) {
-        const int sl = i / (64 * T), rem = i - sl * 64 * T;
-        const int r = rem / T, gm = rem - r * T;
-        const int o = obp[sl * 64 + r];
-        if (o >= 0) {
-            const int src = (4 * (r >> 2) + gm) * 4 + (r & 3);
-            const float p0 = part[(sl * 4 + 0) * 256 + src], p1 = part[(sl * 4 + 1) * 256 + src];
-            const float p2 = part[(sl * 4 + 2) * 256 + src], p3 = part[(sl * 4 + 3) * 256 + src];
-            const float d = ((p0 + p1) + (p2 + p3)) + __int_as_float(obp[128 + sl * 64 + r]);
-            lds[o + gm] = obp[256 + sl * 64 + r] ? mz_relu(d) : d;
-        }
-    }
-    __syncthreads();
+    return Rn;
 }
 
+// rec: this thread's record of stage 0 ([stage][slot][row] int4, stride 128)
 template <int T, int NMAX, int K = 0>
-__device__ __forceinline__ void sm_run(int n, const float (&wr)[NMAX][SM_SLOTS][16], const int* rec, float* lds,
-                                       float* part) {
+__device__ __forceinline__ void sm_run_k(int n, const float (&wr)[NMAX][16], int4 R, const int4* rec, float* lds) {
     if constexpr (K < NMAX) {
         if (K < n) {
-            sm_stage<T>(wr[K][0], wr[K][1], rec + K * SM_REC_INTS, lds, part);
-            sm_run<T, NMAX, K + 1>(n, wr, rec, lds, part);
+            const int4 Rn = sm_stage<T>(wr[K], R, rec + (K + 1) * (SM_SLOTS * 64), lds);
+            sm_run_k<T, NMAX, K + 1>(n, wr, Rn, rec, lds);
         }
     }
 }
 
+template <int T, int NMAX>
+__device__ __forceinline__ void sm_run(int n, const float (&wr)[NMAX][16], const int4* rec, float* lds) {
+    sm_run_k<T, NMAX>(n, wr, rec[0], rec, lds);
+}
+
+// Weights of this thread's (slot, row, quarter) for stages 0..n-1 from the
+// host image [stage][slot][q*64 + row][16].
 template <int NMAX>
-__device__ __forceinline__ void sm_load(int n, const float* W, float (&wr)[NMAX][SM_SLOTS][16]) {
-    const int tid = threadIdx.x;          // = q * 64 + lane
+__device__ __forceinline__ void sm_load(int n, const float* W, float (&wr)[NMAX][16]) {
+    const int tid = threadIdx.x;
+    const int sl = tid >> 8, r = (tid & 255) >> 2, q = tid & 3;
 #pragma unroll
-    for (int k = 0; k < NMAX; ++k)
+    for (int k = 0; k < NMAX; ++k) {
+        if (k < n) {
+            const float4* src = reinterpret_cast<const float4*>(
+                W + (((size_t)k * SM_SLOTS + sl) * 256 + q * 64 + r) * 16);
 #pragma unroll
-        for (int sl = 0; sl < SM_SLOTS; ++sl) {
-            if (k < n) {
-                const float4* src =
-                    reinterpret_cast<const float4*>(W + (((size_t)k * SM_SLOTS + sl) * SM_THREADS + tid) * 16);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float4 v = src[i];
-                    wr[k][sl][4 * i] = v.x; wr[k][sl][4 * i + 1] = v.y;
-                    wr[k][sl][4 * i + 2] = v.z; wr[k][sl][4 * i + 3] = v.w;
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) wr[k][sl][i] = 0.0f;
+            for (int i = 0; i < 4; ++i) {
+                const float4 v = src[i];
+                wr[k][4 * i] = v.x; wr[k][4 * i + 1] = v.y; wr[k][4 * i + 2] = v.z; wr[k][4 * i + 3] = v.w;
             }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) wr[k][i] = 0.0f;
         }
+    }
 }
 
 // once-per-move helpers kept out of line
@@ -147,9 +161,8 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     const int PS = 2 * (S + 2);
     const int nrec = P.n_sim + P.n_root;
     float* act = smem;                                           // act_total floats (multiple of 4)
-    float* part = act + P.act_total;                             // [2][4][64][4]
-    int* rec = reinterpret_cast<int*>(part + 2048);              // [nrec][SM_REC_INTS]
-    float* hid = reinterpret_cast<float*>(rec + (nrec * SM_REC_INTS + 3) / 4 * 4);   // [T][S+1][H]
+    int* rec = reinterpret_cast<int*>(act + P.act_total);        // [nrec][SM_REC_INTS]
+    float* hid = reinterpret_cast<float*>(rec + (nrec + 1) * SM_REC_INTS);   // [T][S+1][H] (+1: look-ahead slack)
     int* si = reinterpret_cast<int*>(hid + ((size_t)T * NN * H + 3) / 4 * 4);
     uint32_t* sg_legal = reinterpret_cast<uint32_t*>(si);       // 16-entry blocks
     int* sg_root_tp = si + 16;
@@ -174,14 +187,16 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     const uint32_t gid = P.game_offset + (uint32_t)gg;
     int* path = sg_path + (tree_thread ? g : 0) * PS;
     TreeView tree = sm_tree_at(lds_tree + (size_t)(tree_thread ? g : 0) * P.tree_game_bytes, E, NN);
-    const int* rec_sim = rec;
-    const int* rec_root = rec + P.n_sim * SM_REC_INTS;
+    // this thread's (slot, row) record column; one extra stage of slack is
+    // read (never used) past each schedule's last stage
+    const int4* rec_sim = reinterpret_cast<const int4*>(rec) + (tid >> 2);
+    const int4* rec_root = rec_sim + P.n_sim * (SM_SLOTS * 64);
 
     for (int i = tid; i < P.act_total; i += SM_THREADS) act[i] = 0.0f;
     for (int i = tid; i < nrec * SM_REC_INTS; i += SM_THREADS) rec[i] = P.rec[i];
     __syncthreads();
     for (int i = tid; i < nrec * 128; i += SM_THREADS)
-        rec[(i >> 7) * SM_REC_INTS + 258 + (i & 127)] = __float_as_int(P.bias[i]);
+        rec[4 * i + 3] = __float_as_int(P.bias[i]);
     // ---- root inputs
     for (int i = tid; i < T * P.obs_feat; i += SM_THREADS) {
         const int gl = i / P.obs_feat, k = i - gl * P.obs_feat;
@@ -200,12 +215,11 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     }
     __syncthreads();
 
-    // ---- representation (SelfPlay.jl:234): its own schedule, weights loaded once
-    {
-        float wr[SM_MAX_ROOT][SM_SLOTS][16];
-        sm_load<SM_MAX_ROOT>(P.n_root, P.w_root, wr);
-        sm_run<T, SM_MAX_ROOT>(P.n_root, wr, rec_root, act, part);
-    }
+    // ---- representation (SelfPlay.jl:234): its own schedule; the weight
+    // registers are then reloaded with the prediction ‖ dynamics weights
+    float wr[SM_MAX_SIM][16];
+    sm_load<SM_MAX_SIM>(P.n_root, P.w_root, wr);
+    sm_run<T, SM_MAX_SIM>(P.n_root, wr, rec_root, act);
     for (int i = tid; i < T * H; i += SM_THREADS) {     // h -> hidden slot 0 and the prediction input
         const int gl = i / H, k = i - gl * H;
         const float h = act[P.h_out + k * T + gl];
@@ -213,11 +227,10 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         act[P.x_pred + k * T + gl] = h;
     }
     // prediction ‖ dynamics weights: resident for the whole search
-    float wr[SM_MAX_SIM][SM_SLOTS][16];
     sm_load<SM_MAX_SIM>(P.n_sim, P.w_sim, wr);
     __syncthreads();
     // prediction(h) for the root (:239); the dynamics half runs on zeros, unused
-    sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act, part);
+    sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act);
 
     const uint32_t legal = tree_thread ? sg_legal[g] : 0u;
     if (tree_thread) {   // expand_node!(root, legal, to_play, 0, policy, h) (:245)
@@ -263,7 +276,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         __syncthreads();
         SM_STAMP(2);
         // ---- prediction(parent.h) ‖ dynamics(2h ⊕ a/|A|)
-        sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act, part);
+        sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act);
         SM_STAMP(3);
         // ---- expand slot s+1 (:280) + store h'
         const int e_new = s + 1;

@@ -3,20 +3,20 @@
 #pragma once
 #include "mz_internal.h"
 
-#define SM_THREADS 256
+#define SM_THREADS 512
 #define SM_SLOTS 2
 #define SM_MAX_SIM 8       // stages of the prediction ‖ dynamics schedule
 #define SM_MAX_ROOT 6      // stages of the representation schedule
 
 typedef float sm_f32x4 __attribute__((ext_vector_type(4)));
 
-// Per stage, the host-built record (ints, copied to LDS):
-//   [0..1]      kq of slot 0 / 1 (k steps per quarter; 0 = slot idle)
-//   [2..129]    xb[slot][lane]: B-operand base = in_off + (lane & 3), -1 = zero
-//   [130..257]  ob[slot][row]: output offset of slot row r (-1 = unused)
-//   [258..385]  bias bits [slot][row]
-//   [386..513]  relu flag [slot][row]
-#define SM_REC_INTS (2 + 4 * 128)
+// Per stage, the host-built record: one int4 per [slot][row] (copied to LDS)
+//   .x  input base of the row's layer in the activation buffer (0 if unused:
+//       the row's weights are zero and its output is dropped)
+//   .y  kq of the layer (k steps per quarter)
+//   .z  output offset of the row | relu << 30, or -1 = unused row
+//   .w  bias bits (filled at kernel start from the re-gathered bias image)
+#define SM_REC_INTS (SM_SLOTS * 64 * 4)
 
 struct SmallParams {
     int G, S, A, H, players, obs_feat, plane, exploration;
