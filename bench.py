@@ -11,6 +11,7 @@ key.  Multi-GPU: games shard across ranks (no data-path collective) ->
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import glob
 import dataclasses
 import json
 import os
@@ -167,11 +168,14 @@ def main():
         value = total_exp / elapsed
         flop_launch = G * S * F_EXP + G * F_ROOT
         achieved = flop_launch / (kern_ms * 1e-3) / 1e12
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_search_r01.json")
-        if os.path.exists(pmc):
+        # HBM bytes per launch from the committed PMC summary of THIS kernel
+        # variant (tools/pmc_summary.py; latest round wins), else null
+        traffic, variant = None, eng.search_variant()
+        for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
             with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                rec = json.load(f)
+            if rec.get("kernel") == variant:
+                traffic = rec.get("hbm_bytes_per_launch")
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(conf, hyper, nets, obs, legal, tp, args.cpu_budget)
@@ -187,7 +191,7 @@ def main():
             "learner_config": {"batch_size": B, "num_unroll_steps": K, "mode": "ref_semantics"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 4), "peak": PEAK_F32, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_F32, 5), "traffic": traffic,
-                         "kernel": eng.search_variant(), "kernel_ms": round(kern_ms, 4),
+                         "kernel": variant, "kernel_ms": round(kern_ms, 4),
                          "flop_per_launch": flop_launch},
             "cpu_baseline": cpu,
         }

@@ -163,10 +163,7 @@ typedef struct mz_batch {
  * period=10) and passes it; Learning.jl:319,382).
  * losses_out[6] = {value, reward, policy, l2_repr, l2_pred, l2_dyn}; the
  * reference's three reported losses are value+reward+policy+l2_net.
- * `grad_dev`, when not NULL, is a device buffer of all params (repr, pred,
- * dyn concatenated, device order) that is filled with the gradient before
- * the update and then used for it — the host may all-reduce it in between
- * through mz_learner_step_split (multi-GPU).                  */
+ * Single-GPU form; data-parallel training uses the split form below.      */
 int mz_learner_step(mz_handle* h, const mz_batch* batch, double eta, float* losses_out);
 
 /* Split learner step for data-parallel training: (1) forward + losses +
