@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "mz_internal.h"
+#include "mz_tree_device.h"   // tree_bytes (tree layout shared with the kernels)
 
 extern "C" __global__ void mz_search_kernel_lds(SearchParams P);
 extern "C" __global__ void mz_search_kernel_hbm(SearchParams P);
@@ -483,7 +484,8 @@ static int build_small(mz_handle* h) {
         MZ_TRY(h, hipMemcpy(h->d_sm_rec[ti], rec.data(), rec.size() * 4, hipMemcpyHostToDevice));
         const int S = h->S, NN = S + 1, PS = 2 * (S + 2);
         size_t ints = (size_t)lay[0] + (size_t)(nrec + 1) * SM_REC_INTS +
-                      ((size_t)T * NN * h->H + 3) / 4 * 4 + 224 + ((size_t)T * PS + 3) / 4 * 4;
+                      ((size_t)T * NN * h->H + 3) / 4 * 4 + 224 + ((size_t)T * PS + 3) / 4 * 4 +
+                      (size_t)4 * (S + 2) + MZ_MAX_ACTIONS;
         h->sm_lds[ti] = ints * 4 + (size_t)T * h->tree_game_bytes;
     }
     return 1;
@@ -529,8 +531,7 @@ static int repack(mz_handle* h, hipStream_t st = nullptr) {
 }
 
 static size_t tree_game_bytes(int S, int A) {
-    const size_t E = (size_t)(S + 1) * A, NN = (size_t)(S + 1);
-    return (12 * E + 4 * NN + NN + 15) & ~(size_t)15;
+    return tree_bytes((S + 1) * A, S + 1);
 }
 static size_t search_lds_base(const mz_handle* h) {
     return (size_t)h->lay.total * 4 + (size_t)(416 + 16 * 2 * (h->S + 2)) * 4;
@@ -829,8 +830,8 @@ int mz_debug_tree(mz_handle* h, int G, int32_t* eN, float* eW, float* eP, float*
         const uint32_t* nc = reinterpret_cast<const uint32_t*>(b);
         const float* w = reinterpret_cast<const float*>(b + 4 * (size_t)E);
         const float* p = reinterpret_cast<const float*>(b + 8 * (size_t)E);
-        const float* nr = reinterpret_cast<const float*>(b + 12 * (size_t)E);
-        const int8_t* tp = reinterpret_cast<const int8_t*>(b + 12 * (size_t)E + 4 * (size_t)NN);
+        const float* nr = reinterpret_cast<const float*>(b + 16 * (size_t)E);
+        const int8_t* tp = reinterpret_cast<const int8_t*>(b + 16 * (size_t)E + 4 * (size_t)NN);
         // only expanded slots hold data: slot e is expanded iff e == 0 or some edge points at it
         std::vector<char> expd(NN, 0);
         expd[0] = 1;

@@ -33,15 +33,6 @@
 #define MZ_STAMP(i) do {} while (0)
 #endif
 
-__device__ __forceinline__ TreeView tree_at(char* base, int E, int NN) {
-    TreeView t;
-    t.nc = reinterpret_cast<uint32_t*>(base);
-    t.w = reinterpret_cast<float*>(base + 4 * (size_t)E);
-    t.p = reinterpret_cast<float*>(base + 8 * (size_t)E);
-    t.nr = reinterpret_cast<float*>(base + 12 * (size_t)E);
-    t.ntp = reinterpret_cast<int8_t*>(base + 12 * (size_t)E + 4 * (size_t)NN);
-    return t;
-}
 
 template <bool LDS_TREE, bool RES>
 __device__ __forceinline__ void search_body(const SearchParams& P) {
@@ -76,8 +67,8 @@ __device__ __forceinline__ void search_body(const SearchParams& P) {
     const bool active = gg < P.G;
     const uint32_t gid = P.game_offset + (uint32_t)gg;
     int* path = sg_path + g * PS;
-    TreeView gtree = tree_at(P.tree + (size_t)(active ? gg : 0) * P.tree_game_bytes, E, NN);
-    TreeView tree = LDS_TREE ? tree_at(lds_tree + (size_t)g * P.tree_game_bytes, E, NN) : gtree;
+    TreeView gtree = tree_view(P.tree + (size_t)(active ? gg : 0) * P.tree_game_bytes, E, NN);
+    TreeView tree = LDS_TREE ? tree_view(lds_tree + (size_t)g * P.tree_game_bytes, E, NN) : gtree;
 
     for (int i = tid; i < P.lay.total; i += blockDim.x) act[i] = 0.0f;
     __syncthreads();

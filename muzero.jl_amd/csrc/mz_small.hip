@@ -139,15 +139,6 @@ __device__ __noinline__ int sm_select_action(const int* cnt, uint32_t legal, int
     return select_action_dev(cnt, legal, A, temperature, r);
 }
 
-__device__ __forceinline__ TreeView sm_tree_at(char* base, int E, int NN) {
-    TreeView t;
-    t.nc = reinterpret_cast<uint32_t*>(base);
-    t.w = reinterpret_cast<float*>(base + 4 * (size_t)E);
-    t.p = reinterpret_cast<float*>(base + 8 * (size_t)E);
-    t.nr = reinterpret_cast<float*>(base + 12 * (size_t)E);
-    t.ntp = reinterpret_cast<int8_t*>(base + 12 * (size_t)E + 4 * (size_t)NN);
-    return t;
-}
 
 template <int T>
 __device__ __forceinline__ void small_body(const SmallParams& P) {
@@ -176,7 +167,11 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     int* sg_depth = si + 144;
     float* sg_stage = reinterpret_cast<float*>(si + 160);       // [4][16]
     int* sg_path = si + 224;                                      // [T][2(S+2)]
-    char* lds_tree = reinterpret_cast<char*>(si + 224 + (T * PS + 3) / 4 * 4);
+    // select / gather tables in LDS (they sit on the per-level critical path)
+    double* l_pbc = reinterpret_cast<double*>(si + 224 + (T * PS + 3) / 4 * 4);   // [S+2]
+    double* l_sqrt = l_pbc + (S + 2);                                           // [S+2]
+    float* l_aval = reinterpret_cast<float*>(l_sqrt + (S + 2));                 // [32]
+    char* lds_tree = reinterpret_cast<char*>(l_aval + MZ_MAX_ACTIONS);
 
     const int tid = threadIdx.x;
     const int g = tid >> 4, a = tid & 15, lane = tid & 63;
@@ -186,13 +181,15 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     const bool active = tree_thread && gg < P.G;
     const uint32_t gid = P.game_offset + (uint32_t)gg;
     int* path = sg_path + (tree_thread ? g : 0) * PS;
-    TreeView tree = sm_tree_at(lds_tree + (size_t)(tree_thread ? g : 0) * P.tree_game_bytes, E, NN);
+    TreeView tree = tree_view(lds_tree + (size_t)(tree_thread ? g : 0) * P.tree_game_bytes, E, NN);
     // this thread's (slot, row) record column; one extra stage of slack is
     // read (never used) past each schedule's last stage
     const int4* rec_sim = reinterpret_cast<const int4*>(rec) + (tid >> 2);
     const int4* rec_root = rec_sim + P.n_sim * (SM_SLOTS * 64);
 
     for (int i = tid; i < P.act_total; i += SM_THREADS) act[i] = 0.0f;
+    for (int i = tid; i < S + 2; i += SM_THREADS) { l_pbc[i] = P.pbc_tab[i]; l_sqrt[i] = P.sqrt_tab[i]; }
+    if (tid < A) l_aval[tid] = P.aval_tab[tid];
     for (int i = tid; i < nrec * SM_REC_INTS; i += SM_THREADS) rec[i] = P.rec[i];
     __syncthreads();
     for (int i = tid; i < nrec * 128; i += SM_THREADS)
@@ -251,7 +248,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         // ---- select (:256-268)
         if (active) {
             const SelectOut so = select_path(tree, path, sg_rootN[g], sg_root_tp[g], legal, sg_mmin[g], sg_mmax[g],
-                                             a, lane, A, P.players, P.discount, P.pbc_tab, P.sqrt_tab, P.seed,
+                                             a, lane, A, P.players, P.discount, l_pbc, l_sqrt, P.seed,
                                              gid, P.rng_step, s);
             if (a == 0) { sg_leaf_e[g] = so.leaf_e; sg_leaf_a[g] = so.leaf_a; sg_vtp[g] = so.vtp; sg_depth[g] = so.depth; }
         }
@@ -271,7 +268,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         for (int i = tid; i < T * P.plane; i += SM_THREADS) {
             const int gl = i / P.plane, k = i - gl * P.plane;
             if (tile0 + gl >= P.G) continue;
-            act[P.x_dyn + (H + k) * T + gl] = P.aval_tab[sg_leaf_a[gl]];
+            act[P.x_dyn + (H + k) * T + gl] = l_aval[sg_leaf_a[gl]];
         }
         __syncthreads();
         SM_STAMP(2);
@@ -328,7 +325,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
             P.action_out[gg] = sm_select_action(cnt, legal, A, P.temperature, r) + 1;
         }
         if (P.dump_tree) {
-            TreeView dst = sm_tree_at(P.tree + (size_t)gg * P.tree_game_bytes, E, NN);
+            TreeView dst = tree_view(P.tree + (size_t)gg * P.tree_game_bytes, E, NN);
             dump_tree(tree, dst, E, NN, a);
         }
     }

@@ -6,10 +6,12 @@
 //   nc[e*A + a]  u32  visit count N (low 16 bits) | child slot + 1 (high 16; 0 = none)
 //   w [e*A + a]  f32  value_sum of the child
 //   p [e*A + a]  f32  prior of the child
+//   ev[e*A + a]  f32  the child's value term of ucb_score (SelfPlay.jl:176-181)
+//                     R_c + γ·(±W/N), written by backup with the exact f32 ops
+//                     select would evaluate (valid when N > 0)
 //   nr[e]        f32  reward of expanded node e (node.reward)
 //   ntp[e]       i8   to_play of expanded node e
-// 12 bytes per edge: 16 games x 50 sims x 9 actions fit in LDS next to the
-// network activations; the same code runs on an HBM copy when they do not.
+// 16 bytes per edge; the same code runs on an LDS or an HBM copy.
 // Threads are grouped 16 lanes per game (lane a = child slot a, A <= 16).
 #pragma once
 #include "mz_internal.h"
@@ -18,9 +20,25 @@ struct TreeView {
     uint32_t* nc;
     float* w;
     float* p;
+    float* ev;
     float* nr;
     int8_t* ntp;
 };
+
+__host__ __device__ __forceinline__ size_t tree_bytes(int E, int NN) {
+    return (16 * (size_t)E + 4 * (size_t)NN + (size_t)NN + 15) & ~(size_t)15;
+}
+
+__device__ __forceinline__ TreeView tree_view(char* base, int E, int NN) {
+    TreeView t;
+    t.nc = reinterpret_cast<uint32_t*>(base);
+    t.w = reinterpret_cast<float*>(base + 4 * (size_t)E);
+    t.p = reinterpret_cast<float*>(base + 8 * (size_t)E);
+    t.ev = reinterpret_cast<float*>(base + 12 * (size_t)E);
+    t.nr = reinterpret_cast<float*>(base + 16 * (size_t)E);
+    t.ntp = reinterpret_cast<int8_t*>(base + 16 * (size_t)E + 4 * (size_t)NN);
+    return t;
+}
 
 // max over the 16-lane group (= one DPP row): quad_perm [1,0,3,2],
 // quad_perm [2,3,0,1], row_half_mirror, row_mirror.  Exact (comparisons only).
@@ -46,6 +64,16 @@ __device__ __forceinline__ float g16_min(float v) {
     t = dpp_f(v, 0x4E); v = v < t ? v : t;
     t = dpp_f(v, 0x141); v = v < t ? v : t;
     t = dpp_f(v, 0x140); v = v < t ? v : t;
+    return v;
+}
+
+// OR over the 16-lane group (same DPP pattern): used to broadcast the value
+// held by exactly one lane (the others contribute 0).
+__device__ __forceinline__ uint32_t g16_or(uint32_t v) {
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
     return v;
 }
 
@@ -101,7 +129,7 @@ __device__ __forceinline__ float double_softmax_prior(float logit, int a, int A,
 __device__ __forceinline__ void init_edges(const TreeView& t, int e, int a, int A, float prior) {
     if (a < A) {
         const int i = e * A + a;
-        t.nc[i] = 0u; t.w[i] = 0.0f; t.p[i] = prior;
+        t.nc[i] = 0u; t.w[i] = 0.0f; t.p[i] = prior; t.ev[i] = 0.0f;
     }
 }
 
@@ -125,18 +153,18 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
     for (;;) {
         const int i = e * A + a;
         float u = -INFINITY;
+        uint32_t nc = 0u;
         if (lg) {
-            const uint32_t nc = t.nc[i];
+            // one LDS round trip per level: the edge (nc, p, ev) and the
+            // parent-count tables
+            nc = t.nc[i];
+            const float pr = t.p[i], ev = t.ev[i];
+            const double pbn = pbc_tab[Np], sqn = sqrt_tab[Np];
             const int Nc = (int)(nc & 0xffffu);
-            const double pb_c = pbc_tab[Np] * (sqrt_tab[Np] / (double)(Nc + 1));
-            const double prior_score = pb_c * (double)t.p[i];
+            const double pb_c = pbn * (sqn / (double)(Nc + 1));
+            const double prior_score = pb_c * (double)pr;
             float vs = 0.0f;
-            if (Nc > 0) {
-                const float q = t.w[i] / (float)Nc;
-                const float tq = players == 1 ? discount * q : discount * (-q);
-                const float v = t.nr[(int)(nc >> 16) - 1] + tq;
-                vs = norm ? (v - mmin) / (mmax - mmin) : v;
-            }
+            if (Nc > 0) vs = norm ? (ev - mmin) / (mmax - mmin) : ev;
             u = (float)(prior_score + (double)vs);
         }
         const float m = g16_max(u);
@@ -152,10 +180,10 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
             ach = nth_set_bit(mask, (int)mz_rng_below(r, (uint32_t)nt));
         }
         const int ei = e * A + ach;
-        const uint32_t ncc = t.nc[ei];                  // same address across the group: broadcast
+        const uint32_t ncc = g16_or(a == ach ? nc : 0u);   // the chosen lane's nc, via DPP
         const int Cch = (int)(ncc >> 16);
         if (a == 0) { path[2 * depth] = ei; path[2 * depth + 1] = Cch - 1; }
-        vtp = (vtp % players) + 1;                      // mod1(vtp + 1, |players|), :267
+        vtp = vtp >= players ? 1 : vtp + 1;             // mod1(vtp + 1, |players|), :267
         if (Cch == 0) return SelectOut{e, ach, vtp, depth};
         e = Cch - 1; Np = (int)(ncc & 0xffffu);
     }
@@ -187,10 +215,14 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
                     N = root_N; W = root_W; R = 0.0f;
                 }
                 W = W + v; N += 1;
-                const float upd = R + discount * (W / (float)N);
+                const float q = W / (float)N;
+                const float upd = R + discount * q;
                 mmin = mmin < upd ? mmin : upd; mmax = mmax > upd ? mmax : upd;
                 v = R + discount * v;
-                if (d > 0) { t.nc[i] = (nc & 0xffff0000u) | (uint32_t)N; t.w[i] = W; }
+                if (d > 0) {
+                    t.nc[i] = (nc & 0xffff0000u) | (uint32_t)N; t.w[i] = W;
+                    t.ev[i] = R + (players == 1 ? discount * q : discount * (-q));
+                }
                 else { root_N = N; root_W = W; }
             }
         }
@@ -225,10 +257,11 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
             }
             W = tp == tl ? W + vin : W - vin;
             N += 1;
-            const float upd = R + discount * (W / (float)N);
+            const float q = W / (float)N;
+            const float upd = R + discount * q;
             lmin = lmin < upd ? lmin : upd;
             lmax = lmax > upd ? lmax : upd;
-            if (d > 0) { t.nc[i] = (nc & 0xffff0000u) | (uint32_t)N; t.w[i] = W; }
+            if (d > 0) { t.nc[i] = (nc & 0xffff0000u) | (uint32_t)N; t.w[i] = W; t.ev[i] = R + discount * (-q); }
             else { rN = N; rW = W; }
         }
     }

@@ -24,7 +24,9 @@ def main():
     lib = os.path.join(pkg.PKG_DIR, "lib", "libmz_stamps.so")
     srcs = [os.path.join(pkg.PKG_DIR, "csrc", s) for s in mzbuild.SOURCES]
     if "--no-build" not in sys.argv:
-        subprocess.run(["/opt/rocm/bin/hipcc"] + mzbuild.FLAGS + ["-DMZ_STAMPS", "-o", lib] + srcs, check=True)
+        extra = os.environ.get("STAMPS_DEFS", "").split()
+        subprocess.run(["/opt/rocm/bin/hipcc"] + mzbuild.FLAGS + ["-DMZ_STAMPS"] + extra + ["-o", lib] + srcs,
+                       check=True)
     abi._lib = None
     L = abi.load_library(lib)
     L.mz_debug_stamps.restype = ctypes.c_int
