@@ -348,14 +348,16 @@ static bool sm_schedule(const mz_handle* h, const std::vector<int>& set, const s
             if (ok) ready.push_back(i);
         }
         std::stable_sort(ready.begin(), ready.end(), [&](int a, int b) { return prio[a] > prio[b]; });
-        int fr[2] = {16, 16};
+        // 4 groups of 16 rows per slot: the 16 lanes of a DPP row serve the
+        // 16 rows of one group and broadcast one shared input vector
+        int fr[2] = {4, 4};
         std::array<int, 2> kq = {0, 0};
         for (int i : ready) {
             const LayerSpec& L = h->layers[set[i]];
-            const int nb = (L.out + 3) / 4, k = 4 * ((L.in + 15) / 16);
+            const int nb = (L.out + 15) / 16;
             for (int x = 0; x < 2; ++x)
-                if (fr[x] >= nb && (kq[x] == 0 || kq[x] == k)) {
-                    st[i] = s; sl[i] = x; b0[i] = 16 - fr[x]; fr[x] -= nb; kq[x] = k; ++done;
+                if (fr[x] >= nb) {
+                    st[i] = s; sl[i] = x; b0[i] = 4 * (4 - fr[x]); fr[x] -= nb; ++done;   // b0 in 4-row units
                     break;
                 }
         }
@@ -470,11 +472,15 @@ static int build_small(mz_handle* h) {
                 io(set[i], in_off, out_off);
                 int* R = rec.data() + (size_t)(rec0 + st[i]) * SM_REC_INTS;
                 const int kq = 4 * ((L.in + 15) / 16);
-                for (int row = 0; row < L.out; ++row) {
+                // every row of the layer's 16-row groups carries the input base
+                // and kq (the DPP row broadcasts them); rows beyond L.out have
+                // zero weights and no output
+                const int rows = (L.out + 15) / 16 * 16;
+                for (int row = 0; row < rows; ++row) {
                     int* e = R + 4 * (sl[i] * 64 + 4 * b0[i] + row);
                     e[0] = in_off;
                     e[1] = kq;
-                    e[2] = (out_off + row * T) | (L.act == MZ_ACT_RELU ? 1 << 30 : 0);
+                    e[2] = row < L.out ? (out_off + row * T) | (L.act == MZ_ACT_RELU ? 1 << 30 : 0) : -1;
                 }
             }
         };

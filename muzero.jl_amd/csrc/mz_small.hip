@@ -3,15 +3,19 @@
 // CUs of an MI355X instead of the 32 tiles of the 16-game MFMA kernel
 // (mz_search.hip), and each simulation waits for the deepest of T games only.
 //
-// Networks on the VALU.  A stage runs two layers ("slots"), one per 256
-// threads; thread -> (slot row r, k-quarter q) runs the 16-step fmaf chain of
-// quarter q of the canonical dot order (mz_dot) for its T games with its 16
-// weights resident in registers for the whole search, and a quad DPP
-// exchange forms ((p0+p1)+(p2+p3)) + b.  A dependent fma costs a few cycles
-// where a dependent v_mfma_f32_4x4x1 costs 45 (tools/mfma_rate_probe.hip),
-// and each quarter is a 16-step dependent chain, so the VALU is the
-// latency-optimal unit here.  A slot row belongs to one layer (4-row blocks;
-// narrow layers share a slot).
+// Networks on the VALU.  A stage runs two 64-row "slots", one per 256
+// threads (4 waves).  Wave w of a slot owns slot rows 16(w&3)..+15; its four
+// 16-lane DPP rows are the four k-quarters q of the canonical dot order
+// (mz_dot), lane i of DPP row q is slot row 16(w&3)+i.  Each thread keeps its
+// 16 weights W[row][q*kq + j] resident in registers for the whole search and
+// loads ONE input element per game, x[q*kq + i]; step j of the 16-step fmaf
+// chain takes x[q*kq + j] from lane j of its DPP row as the row_newbcast
+// operand of v_fmac_f32_dpp (so the 16 rows of a DPP row must share one input
+// vector: the host schedules layers in 16-row groups).  permlane16/32 swaps
+// then form ((p0+p1)+(p2+p3)) in every lane, and DPP row 0 adds the bias,
+// applies the activation and writes the row.  A dependent fma costs a few
+// cycles where a dependent v_mfma_f32_4x4x1 costs 45
+// (tools/mfma_rate_probe.hip): the VALU is the latency-optimal unit here.
 // Tree (mz_tree_device.h) and hidden states live in LDS; the host builds the
 // stage schedule (mz_engine.hip, build_small_schedule).
 #include "mz_mlp_device.h"
@@ -31,42 +35,63 @@
 #define SM_STAMP(i) do {} while (0)
 #endif
 
-// One stage on the VALU.  Thread t: slot = t >> 8, slot row r = (t & 255) >> 2,
-// k-quarter q = t & 3.  The lane runs the 16-step fmaf chain of its quarter
-// for each of the T games (weights resident; zero beyond the layer's kq, and
-// the 64-row input buffers are zero beyond K, so the extra steps are exact
-// no-ops), then a quad DPP exchange forms ((p0+p1)+(p2+p3)) and lane q == 0
-// adds the bias, applies the activation and writes the output row.
-// rec4 points at this thread's record of stage K; the record of stage K+1
+// Thread -> (slot, slot row, quarter): see the header comment.
+__device__ __forceinline__ int sm_slot_row(int tid) {
+    return (tid >> 8) * 64 + ((tid >> 6) & 3) * 16 + (tid & 15);   // slot*64 + row
+}
+
+// acc += x(lane j of this DPP row) * w, one v_fmac_f32_dpp (fused, IEEE: the
+// fmaf of the canonical chain).  Not expressible through the builtins: the
+// DPP combiner does not fold into the tied-operand fmac.
+template <int J>
+__device__ __forceinline__ void fmac_bcast(float& acc, float x, float w) {
+    asm volatile("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(x), "v"(w), "i"(J));
+}
+
+template <int T, int J = 0>
+__device__ __forceinline__ void sm_chain(const float (&w)[16], const float (&x)[T], float (&acc)[T]) {
+    if constexpr (J < 16) {
+#pragma unroll
+        for (int g = 0; g < T; ++g) fmac_bcast<J>(acc[g], x[g], w[J]);
+        sm_chain<T, J + 1>(w, x, acc);
+    }
+}
+
+// One stage.  R = this thread's record of stage K; the record of stage K+1
 // (constant for the whole kernel) is fetched while stage K computes.
 template <int T>
 __device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int4* rec_next, float* lds) {
-    const int q = threadIdx.x & 3;
-    // all 16*T inputs of the quarter issued at once (contiguous, 16-byte
-    // aligned; batches of 32 registers), then the fmaf chain
-    const float4* x = reinterpret_cast<const float4*>(lds + R.x + q * R.y * T);
-    constexpr int NB = T == 4 ? 2 : 1, PER = 4 * T / NB, JB = 16 / NB;
+    const int q = (threadIdx.x >> 4) & 3, i = threadIdx.x & 15;
+    // x[q*kq + i] of the T games (rows beyond kq meet zero weights; the 64-row
+    // input buffers are zero beyond K, so every step is exact)
+    const float* xp = lds + R.x + (q * R.y + i) * T;
+    float x[T];
+    if constexpr (T == 1) {
+        x[0] = xp[0];
+    } else if constexpr (T == 2) {
+        const float2 v = *reinterpret_cast<const float2*>(xp);
+        x[0] = v.x; x[1] = v.y;
+    } else {
+        const float4 v = *reinterpret_cast<const float4*>(xp);
+        x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+    }
+    const int4 Rn = *rec_next;
     float acc[T];
 #pragma unroll
     for (int g = 0; g < T; ++g) acc[g] = 0.0f;
-    int4 Rn;
-#pragma unroll
-    for (int bt = 0; bt < NB; ++bt) {
-        float4 v[PER];
-#pragma unroll
-        for (int i = 0; i < PER; ++i) v[i] = x[bt * PER + i];
-        if (bt == 0) Rn = *rec_next;
-        __builtin_amdgcn_sched_barrier(0);
-        const float* xv = reinterpret_cast<const float*>(v);
-#pragma unroll
-        for (int j = 0; j < JB; ++j)
-#pragma unroll
-            for (int g = 0; g < T; ++g) acc[g] = fmaf(w[bt * JB + j], xv[j * T + g], acc[g]);
-    }
+    sm_chain<T>(w, x, acc);
+    // ((p0+p1)+(p2+p3)) in every lane: with both operands equal, the two
+    // halves of a permlane swap are {own, partner} in row order, so their sum
+    // is p_even + p_odd in both rows of each pair
 #pragma unroll
     for (int g = 0; g < T; ++g) {
-        const float t = acc[g] + dpp_f(acc[g], 0xB1);      // lane q0: p0+p1, q2: p2+p3
-        acc[g] = t + dpp_f(t, 0x4E);                         // lane q0: (p0+p1)+(p2+p3)
+        const auto s1 = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, acc[g]),
+                                                         __builtin_bit_cast(unsigned, acc[g]), false, false);
+        const float t = __builtin_bit_cast(float, (unsigned)s1[0]) + __builtin_bit_cast(float, (unsigned)s1[1]);
+        const auto s2 = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, t),
+                                                         __builtin_bit_cast(unsigned, t), false, false);
+        acc[g] = __builtin_bit_cast(float, (unsigned)s2[0]) + __builtin_bit_cast(float, (unsigned)s2[1]);
     }
     if (q == 0 && R.z >= 0) {
         const int o = R.z & 0x3fffffff;
@@ -103,7 +128,7 @@ __device__ __forceinline__ void sm_run(int n, const float (&wr)[NMAX][16], const
 template <int NMAX>
 __device__ __forceinline__ void sm_load(int n, const float* W, float (&wr)[NMAX][16]) {
     const int tid = threadIdx.x;
-    const int sl = tid >> 8, r = (tid & 255) >> 2, q = tid & 3;
+    const int sr = sm_slot_row(tid), sl = sr >> 6, r = sr & 63, q = (tid >> 4) & 3;
 #pragma unroll
     for (int k = 0; k < NMAX; ++k) {
         if (k < n) {
@@ -184,7 +209,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     TreeView tree = tree_view(lds_tree + (size_t)(tree_thread ? g : 0) * P.tree_game_bytes, E, NN);
     // this thread's (slot, row) record column; one extra stage of slack is
     // read (never used) past each schedule's last stage
-    const int4* rec_sim = reinterpret_cast<const int4*>(rec) + (tid >> 2);
+    const int4* rec_sim = reinterpret_cast<const int4*>(rec) + sm_slot_row(tid);
     const int4* rec_root = rec_sim + P.n_sim * (SM_SLOTS * 64);
 
     for (int i = tid; i < P.act_total; i += SM_THREADS) act[i] = 0.0f;

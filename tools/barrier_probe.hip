@@ -1,0 +1,70 @@
+// Micro-probe: cost of the small search kernel's per-stage skeleton on one
+// CU with 512 threads (8 waves, two per SIMD):
+//   (a) s_barrier alone;
+//   (b) ds_write -> s_barrier -> dependent ds_read (the stage hand-off);
+//   (c) (b) + a 16-step dependent v_fmac_f32_dpp chain x2 games per lane.
+// Prints s_memtime ticks per iteration (wave 0 lane 0, median over blocks).
+// Build: hipcc --offload-arch=gfx950 -O3 tools/barrier_probe.hip -o tools/barrier_probe
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+constexpr int ITERS = 2000;
+
+template <int J>
+__device__ __forceinline__ void fmac_bcast(float& acc, float x, float w) {
+    asm volatile("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(x), "v"(w), "i"(J));
+}
+template <int J = 0>
+__device__ __forceinline__ void chain(float w, float x0, float x1, float& a0, float& a1) {
+    if constexpr (J < 16) {
+        fmac_bcast<J>(a0, x0, w);
+        fmac_bcast<J>(a1, x1, w);
+        chain<J + 1>(w, x0, x1, a0, a1);
+    }
+}
+
+extern "C" __global__ __launch_bounds__(512, 1) void probe(int mode, unsigned long long* out, float* sink) {
+    __shared__ float buf[2][1024];
+    const int tid = threadIdx.x;
+    buf[0][tid] = (float)tid; buf[1][tid] = 0.0f;
+    __syncthreads();
+    float acc = 0.0f;
+    const float w = 1.0f + tid * 1e-7f;
+    unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < ITERS; ++it) {
+        if (mode == 0) {
+            __syncthreads();
+        } else {
+            const int src = it & 1;
+            const float2 x = *reinterpret_cast<const float2*>(&buf[src][(tid * 7) & 1022]);
+            float a0 = acc, a1 = 0.0f;
+            if (mode == 2) chain(w, x.x, x.y, a0, a1);
+            else { a0 += x.x; a1 += x.y; }
+            buf[src ^ 1][tid] = a0 + a1;
+            acc = a0 * 1e-3f;
+            __syncthreads();
+        }
+    }
+    unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (tid == 0) out[blockIdx.x] = t1 - t0;
+    if (acc == 12345.0f) sink[tid] = acc;
+}
+
+int main() {
+    const int blocks = 256;
+    unsigned long long* d; float* sink;
+    hipMalloc(&d, blocks * 8); hipMalloc(&sink, 4096);
+    const char* names[3] = {"barrier only", "ds_write+barrier+ds_read", "+ 16-step x2 dpp fmac chain"};
+    for (int mode = 0; mode < 3; ++mode) {
+        for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL(probe, dim3(blocks), dim3(512), 0, 0, mode, d, sink);
+        hipDeviceSynchronize();
+        std::vector<unsigned long long> h(blocks);
+        hipMemcpy(h.data(), d, blocks * 8, hipMemcpyDeviceToHost);
+        std::sort(h.begin(), h.end());
+        printf("%-32s %8.1f ticks/iter (median over %d blocks)\n", names[mode], (double)h[blocks / 2] / ITERS, blocks);
+    }
+    return 0;
+}
