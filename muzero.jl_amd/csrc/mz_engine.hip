@@ -18,6 +18,8 @@
 #include "mz_internal.h"
 #include "mz_tree_device.h"   // tree_bytes (tree layout shared with the kernels)
 
+static const size_t kLdsMax = 160 * 1024;   // LDS per workgroup on gfx950
+
 extern "C" __global__ void mz_search_kernel_lds(SearchParams P);
 extern "C" __global__ void mz_search_kernel_hbm(SearchParams P);
 extern "C" __global__ void mz_search_kernel_lds_res(SearchParams P);
@@ -98,6 +100,7 @@ struct mz_handle {
     int* d_plan[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // repr, pred, dyn, root, sim
     int* d_plan_sim_res = nullptr;          // register-resident image of the sim plan (or null)
     double* d_pbc = nullptr; double* d_sqrt = nullptr; float* d_aval = nullptr;
+    double* d_pbterm = nullptr;             // pbc(Np) * (sqrt(Np) / (Nc + 1)), triangle
     char* d_tree = nullptr; size_t tree_game_bytes = 0; bool lds_tree = false; int dump_tree = 0;
     bool use_res = false;                   // register-resident sim-plan kernel
     // small-batch kernel (mz_small.hip): schedule images + LDS layout
@@ -492,7 +495,9 @@ static int build_small(mz_handle* h) {
         size_t ints = (size_t)lay[0] + (size_t)(nrec + 1) * SM_REC_INTS +
                       ((size_t)T * NN * h->H + 3) / 4 * 4 + 224 + ((size_t)T * PS + 3) / 4 * 4 +
                       (size_t)4 * (S + 2) + MZ_MAX_ACTIONS;
-        h->sm_lds[ti] = ints * 4 + (size_t)T * h->tree_game_bytes;
+        // + the pb_term triangle (the small kernel requires it in LDS; when
+        // the total exceeds the LDS budget the tile-16 kernel is used)
+        h->sm_lds[ti] = ints * 4 + (size_t)T * h->tree_game_bytes + pbterm_count(S) * 8;
     }
     return 1;
 }
@@ -545,7 +550,6 @@ static size_t search_lds_base(const mz_handle* h) {
 static size_t search_lds_bytes(const mz_handle* h) {
     return search_lds_base(h) + (h->lds_tree ? (size_t)MZ_TILE * h->tree_game_bytes : 0);
 }
-static const size_t kLdsMax = 160 * 1024;
 
 typedef void (*search_fn)(SearchParams);
 static search_fn search_kernel(const mz_handle* h) {
@@ -636,6 +640,12 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
     CK(hipMemcpy(h->d_pbc, pbc.data(), pbc.size() * 8, hipMemcpyHostToDevice) == hipSuccess ? 0 : fail(h, "copy"));
     CK(hipMemcpy(h->d_sqrt, sq.data(), sq.size() * 8, hipMemcpyHostToDevice) == hipSuccess ? 0 : fail(h, "copy"));
     CK(hipMemcpy(h->d_aval, av.data(), av.size() * 4, hipMemcpyHostToDevice) == hipSuccess ? 0 : fail(h, "copy"));
+    // the same f64 expression select evaluates, tabulated (Nc < Np <= S+1)
+    std::vector<double> pbt(pbterm_count(S), 0.0);
+    for (int np = 0; np <= S + 1; ++np)
+        for (int nc = 0; nc <= np; ++nc) pbt[pbterm_index(np, nc)] = pbc[np] * (sq[np] / (double)(nc + 1));
+    CK(al(&h->d_pbterm, pbt.size()));
+    CK(hipMemcpy(h->d_pbterm, pbt.data(), pbt.size() * 8, hipMemcpyHostToDevice) == hipSuccess ? 0 : fail(h, "copy"));
     CK(al(&h->d_tree, G * h->tree_game_bytes));
     CK(al(&h->d_hid, G * (S + 1) * H));
     CK(al(&h->d_obs, G * h->obs_feat)); CK(al(&h->d_legal, G * A)); CK(al(&h->d_tp, G));
@@ -769,6 +779,7 @@ int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* leg
         Q.v_out = lay[5]; Q.p_out = lay[6]; Q.r_out = lay[7];
         Q.v_act = h->lay.v_act; Q.r_act = h->lay.r_act;
         Q.pbc_tab = h->d_pbc; Q.sqrt_tab = h->d_sqrt; Q.aval_tab = h->d_aval;
+        Q.pbterm = h->d_pbterm;
         Q.tree = h->d_tree; Q.tree_game_bytes = h->tree_game_bytes; Q.dump_tree = h->dump_tree;
 #ifdef MZ_STAMPS
         Q.stamps = h->d_stamps;
@@ -833,24 +844,26 @@ int mz_debug_tree(mz_handle* h, int G, int32_t* eN, float* eW, float* eP, float*
     MZ_TRY(h, hipMemcpy(buf.data(), h->d_tree, buf.size(), hipMemcpyDeviceToHost));
     for (int g = 0; g < G; ++g) {
         const char* b = buf.data() + (size_t)g * gb;
-        const uint32_t* nc = reinterpret_cast<const uint32_t*>(b);
-        const float* w = reinterpret_cast<const float*>(b + 4 * (size_t)E);
-        const float* p = reinterpret_cast<const float*>(b + 8 * (size_t)E);
+        // edge records {nc, w, p, ev} (mz_tree_device.h)
+        const uint32_t* rec = reinterpret_cast<const uint32_t*>(b);
+        auto nc = [&](size_t i) { return rec[4 * i]; };
+        auto w = [&](size_t i) { float v; std::memcpy(&v, rec + 4 * i + 1, 4); return v; };
+        auto p = [&](size_t i) { float v; std::memcpy(&v, rec + 4 * i + 2, 4); return v; };
         const float* nr = reinterpret_cast<const float*>(b + 16 * (size_t)E);
         const int8_t* tp = reinterpret_cast<const int8_t*>(b + 16 * (size_t)E + 4 * (size_t)NN);
         // only expanded slots hold data: slot e is expanded iff e == 0 or some edge points at it
         std::vector<char> expd(NN, 0);
         expd[0] = 1;
-        for (int i = 0; i < E; ++i) if ((nc[i] >> 16) != 0 && expd[i / A]) expd[(nc[i] >> 16) - 1] = 1;
+        for (int i = 0; i < E; ++i) if ((nc(i) >> 16) != 0 && expd[i / A]) expd[(nc(i) >> 16) - 1] = 1;
         for (int e = 0; e < NN; ++e) {
             if (ntp) ntp[(size_t)g * NN + e] = expd[e] ? tp[e] : 0;
             for (int a = 0; a < A; ++a) {
                 const size_t k = ((size_t)g * NN + e) * A + a, i = (size_t)e * A + a;
                 const bool x = expd[e] != 0;
-                const int c = x ? (int)(nc[i] >> 16) - 1 : -1;
-                if (eN) eN[k] = x ? (int32_t)(nc[i] & 0xffffu) : 0;
-                if (eW) eW[k] = x ? w[i] : 0.0f;
-                if (eP) eP[k] = x ? p[i] : 0.0f;
+                const int c = x ? (int)(nc(i) >> 16) - 1 : -1;
+                if (eN) eN[k] = x ? (int32_t)(nc(i) & 0xffffu) : 0;
+                if (eW) eW[k] = x ? w(i) : 0.0f;
+                if (eP) eP[k] = x ? p(i) : 0.0f;
                 if (eR) eR[k] = c >= 0 ? nr[c] : 0.0f;
                 if (eC) eC[k] = c;
             }

@@ -119,7 +119,7 @@ __device__ __forceinline__ void search_body(const SearchParams& P) {
         const float one_m = 1.0f - P.exploration_eps;
         int i = 0;
         for (int b = 0; b < A; ++b) if ((legal >> b) & 1u) {
-            tree.p[b] = tree.p[b] * one_m + noise[i] * P.exploration_eps;
+            tree.p(b) = tree.p(b) * one_m + noise[i] * P.exploration_eps;
             ++i;
         }
     }
@@ -130,8 +130,8 @@ __device__ __forceinline__ void search_body(const SearchParams& P) {
     for (int s = 0; s < S; ++s) {
         // ---- select (:256-268)
         if (active) {
-            const SelectOut so = select_path(tree, path, sg_rootN[g], sg_root_tp[g], legal, sg_mmin[g], sg_mmax[g],
-                                             a, lane, A, P.players, P.discount, P.pbc_tab, P.sqrt_tab, P.seed,
+            const SelectOut so = select_path<false>(tree, path, sg_rootN[g], sg_root_tp[g], legal, sg_mmin[g], sg_mmax[g],
+                                             a, lane, A, P.players, P.discount, nullptr, P.pbc_tab, P.sqrt_tab, P.seed,
                                              gid, P.rng_step, s);
             if (a == 0) { sg_leaf_e[g] = so.leaf_e; sg_leaf_a[g] = so.leaf_a; sg_vtp[g] = so.vtp; sg_depth[g] = so.depth; }
         }
@@ -182,7 +182,7 @@ __device__ __forceinline__ void search_body(const SearchParams& P) {
             const int depth = sg_depth[g];
             if (a == 0) {
                 const int li = sg_leaf_e[g] * A + sg_leaf_a[g];
-                tree.nc[li] = (tree.nc[li] & 0xffffu) | ((uint32_t)(e_new + 1) << 16);
+                tree.nc(li) = (tree.nc(li) & 0xffffu) | ((uint32_t)(e_new + 1) << 16);
                 tree.nr[e_new] = mz_post_act(P.lay.r_act, act[P.lay.r_out + g]);
                 tree.ntp[e_new] = (int8_t)tl;
                 path[2 * depth + 1] = e_new;
@@ -201,7 +201,7 @@ __device__ __forceinline__ void search_body(const SearchParams& P) {
     // ---- store_search_stats! (:115-122) + select_action (:293-306)
     if (active) {
         const bool lg = a < A && ((legal >> a) & 1u);
-        const int Nc = lg ? (int)(tree.nc[a] & 0xffffu) : 0;
+        const int Nc = lg ? (int)(tree.nc(a) & 0xffffu) : 0;
         const int sum = g16_isum(Nc);
         if (a < A) P.child_visits[(size_t)gg * A + a] = lg ? (float)((double)Nc / (double)sum) : 0.0f;
         int cnt[16];

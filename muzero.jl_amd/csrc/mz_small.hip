@@ -147,7 +147,7 @@ __device__ __forceinline__ void sm_load(int n, const float* W, float (&wr)[NMAX]
 }
 
 // once-per-move helpers kept out of line
-__device__ __noinline__ void sm_root_noise(float* p, uint32_t legal, int A, uint64_t seed, uint32_t gid,
+__device__ __noinline__ void sm_root_noise(TreeView t, uint32_t legal, int A, uint64_t seed, uint32_t gid,
                                            uint32_t step, float alpha, float eps) {
     const int n = __builtin_popcount(legal);
     float noise[MZ_MAX_ACTIONS];
@@ -155,7 +155,7 @@ __device__ __noinline__ void sm_root_noise(float* p, uint32_t legal, int A, uint
     const float one_m = 1.0f - eps;
     int i = 0;
     for (int b = 0; b < A; ++b) if ((legal >> b) & 1u) {
-        p[b] = p[b] * one_m + noise[i] * eps;
+        t.p(b) = t.p(b) * one_m + noise[i] * eps;
         ++i;
     }
 }
@@ -196,7 +196,8 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     double* l_pbc = reinterpret_cast<double*>(si + 224 + (T * PS + 3) / 4 * 4);   // [S+2]
     double* l_sqrt = l_pbc + (S + 2);                                           // [S+2]
     float* l_aval = reinterpret_cast<float*>(l_sqrt + (S + 2));                 // [32]
-    char* lds_tree = reinterpret_cast<char*>(l_aval + MZ_MAX_ACTIONS);
+    double* l_pbterm = reinterpret_cast<double*>(l_aval + MZ_MAX_ACTIONS);     // [pbterm_count(S)]
+    char* lds_tree = reinterpret_cast<char*>(l_pbterm + pbterm_count(S));
 
     const int tid = threadIdx.x;
     const int g = tid >> 4, a = tid & 15, lane = tid & 63;
@@ -215,6 +216,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     for (int i = tid; i < P.act_total; i += SM_THREADS) act[i] = 0.0f;
     for (int i = tid; i < S + 2; i += SM_THREADS) { l_pbc[i] = P.pbc_tab[i]; l_sqrt[i] = P.sqrt_tab[i]; }
     if (tid < A) l_aval[tid] = P.aval_tab[tid];
+    for (int i = tid; i < (int)pbterm_count(S); i += SM_THREADS) l_pbterm[i] = P.pbterm[i];
     for (int i = tid; i < nrec * SM_REC_INTS; i += SM_THREADS) rec[i] = P.rec[i];
     __syncthreads();
     for (int i = tid; i < nrec * 128; i += SM_THREADS)
@@ -265,20 +267,27 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     }
     __syncthreads();
     if (P.exploration && active && a == 0)                   // add_exploration_noise! (:102-109)
-        sm_root_noise(tree.p, legal, A, P.seed, gid, P.rng_step, P.dirichlet_alpha, P.exploration_eps);
+        sm_root_noise(tree, legal, A, P.seed, gid, P.rng_step, P.dirichlet_alpha, P.exploration_eps);
     __syncthreads();
     SM_STAMP(0);
 
     for (int s = 0; s < S; ++s) {
         // ---- select (:256-268)
         if (active) {
-            const SelectOut so = select_path(tree, path, sg_rootN[g], sg_root_tp[g], legal, sg_mmin[g], sg_mmax[g],
-                                             a, lane, A, P.players, P.discount, l_pbc, l_sqrt, P.seed,
+            const SelectOut so = select_path<true>(tree, path, sg_rootN[g], sg_root_tp[g], legal, sg_mmin[g], sg_mmax[g],
+                                             a, lane, A, P.players, P.discount, l_pbterm, l_pbc, l_sqrt, P.seed,
                                              gid, P.rng_step, s);
             if (a == 0) { sg_leaf_e[g] = so.leaf_e; sg_leaf_a[g] = so.leaf_a; sg_vtp[g] = so.vtp; sg_depth[g] = so.depth; }
         }
         __syncthreads();
         SM_STAMP(1);
+#ifdef MZ_STAMPS
+        if (threadIdx.x == 0) {                 // slot 7: select levels walked (max over the T games)
+            int md = 0;
+            for (int gl = 0; gl < T; ++gl) md = md > sg_depth[gl] ? md : sg_depth[gl];
+            st_acc[7] += (unsigned long long)md;
+        }
+#endif
         // ---- gather: parent h -> prediction input; h *= 2 in place (Q1) -> dynamics input
         for (int i = tid; i < T * H; i += SM_THREADS) {
             const int gl = i / H, k = i - gl * H;
@@ -318,7 +327,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
             const int depth = sg_depth[g];
             if (a == 0) {
                 const int li = sg_leaf_e[g] * A + sg_leaf_a[g];
-                tree.nc[li] = (tree.nc[li] & 0xffffu) | ((uint32_t)(e_new + 1) << 16);
+                tree.nc(li) = (tree.nc(li) & 0xffffu) | ((uint32_t)(e_new + 1) << 16);
                 tree.nr[e_new] = mz_post_act(P.r_act, act[P.r_out + g]);
                 tree.ntp[e_new] = (int8_t)tl;
                 path[2 * depth + 1] = e_new;
@@ -337,7 +346,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     // ---- store_search_stats! (:115-122) + select_action (:293-306)
     if (active) {
         const bool lg = a < A && ((legal >> a) & 1u);
-        const int Nc = lg ? (int)(tree.nc[a] & 0xffffu) : 0;
+        const int Nc = lg ? (int)(tree.nc(a) & 0xffffu) : 0;
         const int sum = g16_isum(Nc);
         if (a < A) P.child_visits[(size_t)gg * A + a] = lg ? (float)((double)Nc / (double)sum) : 0.0f;
         int cnt[16];

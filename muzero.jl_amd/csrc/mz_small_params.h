@@ -34,6 +34,7 @@ struct SmallParams {
     int x_rep, x_pred, x_dyn, h_out, v_out, p_out, r_out;
     int v_act, r_act;
     const double* pbc_tab; const double* sqrt_tab; const float* aval_tab;
+    const double* pbterm;  // pb_term triangle (mz_tree_device.h), copied to LDS
     char* tree; size_t tree_game_bytes; int dump_tree;
     unsigned long long* stamps;
 };

@@ -2,27 +2,30 @@
 // (SelfPlay.jl:88-217, 293-306): select, expand, backup, search statistics.
 //
 // Tree of one game (slot e = 0 is the root, e = s+1 the node expanded by
-// simulation s; edge (e, a) = child a of expanded node e):
-//   nc[e*A + a]  u32  visit count N (low 16 bits) | child slot + 1 (high 16; 0 = none)
-//   w [e*A + a]  f32  value_sum of the child
-//   p [e*A + a]  f32  prior of the child
-//   ev[e*A + a]  f32  the child's value term of ucb_score (SelfPlay.jl:176-181)
-//                     R_c + γ·(±W/N), written by backup with the exact f32 ops
-//                     select would evaluate (valid when N > 0)
-//   nr[e]        f32  reward of expanded node e (node.reward)
-//   ntp[e]       i8   to_play of expanded node e
-// 16 bytes per edge; the same code runs on an LDS or an HBM copy.
+// simulation s; edge (e, a) = child a of expanded node e).  Edge i = e*A + a
+// is one 16-byte record (a single ds_read_b128 in select):
+//   .nc  u32  visit count N (low 16 bits) | child slot + 1 (high 16; 0 = none)
+//   .w   f32  value_sum of the child
+//   .p   f32  prior of the child
+//   .ev  f32  the child's value term of ucb_score (SelfPlay.jl:176-181),
+//             R_c + γ·(±W/N), written by backup with the exact f32 ops select
+//             would evaluate (valid when N > 0)
+// and per expanded node
+//   nr[e]  f32  reward of expanded node e (node.reward)
+//   ntp[e] i8   to_play of expanded node e
+// The same code runs on an LDS or an HBM copy.
 // Threads are grouped 16 lanes per game (lane a = child slot a, A <= 16).
 #pragma once
 #include "mz_internal.h"
 
 struct TreeView {
-    uint32_t* nc;
-    float* w;
-    float* p;
-    float* ev;
+    float4* e;          // edge records {nc bits, w, p, ev}
     float* nr;
     int8_t* ntp;
+    __device__ __forceinline__ uint32_t& nc(int i) const { return reinterpret_cast<uint32_t*>(e + i)[0]; }
+    __device__ __forceinline__ float& w(int i) const { return reinterpret_cast<float*>(e + i)[1]; }
+    __device__ __forceinline__ float& p(int i) const { return reinterpret_cast<float*>(e + i)[2]; }
+    __device__ __forceinline__ float& ev(int i) const { return reinterpret_cast<float*>(e + i)[3]; }
 };
 
 __host__ __device__ __forceinline__ size_t tree_bytes(int E, int NN) {
@@ -31,10 +34,7 @@ __host__ __device__ __forceinline__ size_t tree_bytes(int E, int NN) {
 
 __device__ __forceinline__ TreeView tree_view(char* base, int E, int NN) {
     TreeView t;
-    t.nc = reinterpret_cast<uint32_t*>(base);
-    t.w = reinterpret_cast<float*>(base + 4 * (size_t)E);
-    t.p = reinterpret_cast<float*>(base + 8 * (size_t)E);
-    t.ev = reinterpret_cast<float*>(base + 12 * (size_t)E);
+    t.e = reinterpret_cast<float4*>(base);
     t.nr = reinterpret_cast<float*>(base + 16 * (size_t)E);
     t.ntp = reinterpret_cast<int8_t*>(base + 16 * (size_t)E + 4 * (size_t)NN);
     return t;
@@ -129,7 +129,7 @@ __device__ __forceinline__ float double_softmax_prior(float logit, int a, int A,
 __device__ __forceinline__ void init_edges(const TreeView& t, int e, int a, int A, float prior) {
     if (a < A) {
         const int i = e * A + a;
-        t.nc[i] = 0u; t.w[i] = 0.0f; t.p[i] = prior; t.ev[i] = 0.0f;
+        t.e[i] = make_float4(0.0f, 0.0f, prior, 0.0f);     // nc = 0 (bits), w = 0, p, ev
     }
 }
 
@@ -138,55 +138,91 @@ struct SelectOut { int leaf_e, leaf_a, vtp, depth; };
 // Path of one simulation: path[2d] = edge index e*A + a taken at depth d,
 // path[2d+1] = child slot it leads to (-1 for the leaf until expanded).
 
+// pb_term table index: the host tabulates pbc(Np) * (sqrt(Np) / (Nc + 1))
+// (the f64 subexpression of ucb_score, SelfPlay.jl:172-174) for Nc < Np <=
+// S+1 as a triangle, so select replaces an f64 division by one LDS read.
+__host__ __device__ __forceinline__ int pbterm_index(int Np, int Nc) { return Np * (Np + 1) / 2 + Nc; }
+__host__ __device__ __forceinline__ size_t pbterm_count(int S) { return (size_t)(S + 2) * (S + 3) / 2; }
+
+// max over the 16-lane group, one v_max_f32_dpp per step (the hazard pad —
+// a DPP read of a VGPR written by the previous VALU needs 2 wait states — is
+// inside the string).  For select's argmax this equals g16_max: no NaNs
+// occur, and -0/+0 compare equal in the tie test that follows.
+__device__ __forceinline__ float g16_vmax(float v) {
+    asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1"
+                 : "+v"(v));
+    return v;
+}
+
 // select_child loop (SelfPlay.jl:256-268) for the game of this 16-lane group.
 // pUCT (ucb_score :171-184) in f64 with one rounding to f32 (Q5); ties by
 // exact equality, broken by the Philox TIE stream keyed (sim, depth) — the
 // draw only matters (and is only computed) when there is more than one tie.
+// Per level: one LDS round trip (the 16-byte edge record, then the pb_term
+// entry when TAB, else the pbc/sqrt entries and an f64 division), a
+// branch-free score (illegal lanes score a clamped real edge and are masked
+// to -inf), a DPP max, a ballot, and the chosen edge's record by DPP.  The
+// path stays in registers while depth < 16 (lane d keeps level d) and is
+// written to `path` once at the end; deeper levels are stored directly.
+template <bool TAB>
 __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, int root_N, int root_tp,
                                                  uint32_t legal, float mmin, float mmax, int a, int lane,
-                                                 int A, int players, float discount, const double* pbc_tab,
-                                                 const double* sqrt_tab, uint64_t seed, uint32_t gid,
-                                                 uint32_t step, int sim) {
+                                                 int A, int players, float discount, const double* pbterm,
+                                                 const double* pbc_tab, const double* sqrt_tab, uint64_t seed,
+                                                 uint32_t gid, uint32_t step, int sim) {
     const bool lg = a < A && ((legal >> a) & 1u);
     const bool norm = mmax > mmin;
+    const float den = mmax - mmin;
+    const int ac = a < A ? a : A - 1;
     int e = 0, Np = root_N, depth = 0, vtp = root_tp;
+    int pe = 0, pc = 0;
+    SelectOut out;
     for (;;) {
-        const int i = e * A + a;
-        float u = -INFINITY;
-        uint32_t nc = 0u;
-        if (lg) {
-            // one LDS round trip per level: the edge (nc, p, ev) and the
-            // parent-count tables
-            nc = t.nc[i];
-            const float pr = t.p[i], ev = t.ev[i];
-            const double pbn = pbc_tab[Np], sqn = sqrt_tab[Np];
-            const int Nc = (int)(nc & 0xffffu);
-            const double pb_c = pbn * (sqn / (double)(Nc + 1));
-            const double prior_score = pb_c * (double)pr;
-            float vs = 0.0f;
-            if (Nc > 0) vs = norm ? (ev - mmin) / (mmax - mmin) : ev;
-            u = (float)(prior_score + (double)vs);
-        }
-        const float m = g16_max(u);
-        const uint64_t bal = __ballot(lg && u == m);
-        const uint32_t mask = (uint32_t)(bal >> (lane & 48)) & 0xffffu;
-        const int nt = __builtin_popcount(mask);
-        depth += 1;
-        int ach;
-        if (nt == 1) {
-            ach = __builtin_ctz(mask);
+        const float4 ed = t.e[e * A + ac];
+        const uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
+        const int Nc = (int)(nc & 0xffffu);
+        double pb_c;
+        if constexpr (TAB) {
+            pb_c = pbterm[pbterm_index(Np, Nc < Np ? Nc : Np)];
         } else {
-            const uint32_t r = mz_rng_u32(seed, MZ_RNG_TIE, gid, step, ((uint32_t)sim << 12) | (uint32_t)depth);
-            ach = nth_set_bit(mask, (int)mz_rng_below(r, (uint32_t)nt));
+            const double pbn = pbc_tab[Np], sqn = sqrt_tab[Np];
+            pb_c = pbn * (sqn / (double)(Nc + 1));
+        }
+        const double prior_score = pb_c * (double)ed.z;
+        const float vn = (ed.w - mmin) / den;            // discarded unless norm
+        const float vs = Nc > 0 ? (norm ? vn : ed.w) : 0.0f;
+        const float us = (float)(prior_score + (double)vs);
+        const float u = lg ? us : -INFINITY;
+        const float m = g16_vmax(u);
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(lg && u == m);
+        const uint32_t mask = (uint32_t)(bal >> (lane & 48)) & 0xffffu;
+        depth += 1;
+        int ach = __builtin_ctz(mask);
+        // ties (rare): one wave-uniform test, then the Philox draw per group
+        if (__builtin_amdgcn_ballot_w64((mask & (mask - 1)) != 0) != 0) {
+            const int nt = __builtin_popcount(mask);
+            if (nt > 1) {
+                const uint32_t r = mz_rng_u32(seed, MZ_RNG_TIE, gid, step, ((uint32_t)sim << 12) | (uint32_t)depth);
+                ach = nth_set_bit(mask, (int)mz_rng_below(r, (uint32_t)nt));
+            }
         }
         const int ei = e * A + ach;
         const uint32_t ncc = g16_or(a == ach ? nc : 0u);   // the chosen lane's nc, via DPP
         const int Cch = (int)(ncc >> 16);
-        if (a == 0) { path[2 * depth] = ei; path[2 * depth + 1] = Cch - 1; }
+        const bool keep = a == depth;                     // depth < 16: lane `depth` keeps the level
+        pe = keep ? ei : pe;
+        pc = keep ? Cch - 1 : pc;
+        if (depth >= 16 && a == 0) { path[2 * depth] = ei; path[2 * depth + 1] = Cch - 1; }
         vtp = vtp >= players ? 1 : vtp + 1;             // mod1(vtp + 1, |players|), :267
-        if (Cch == 0) return SelectOut{e, ach, vtp, depth};
+        if (Cch == 0) { out = SelectOut{e, ach, vtp, depth}; break; }
         e = Cch - 1; Np = (int)(ncc & 0xffffu);
     }
+    if (a >= 1 && a <= out.depth) { path[2 * a] = pe; path[2 * a + 1] = pc; }
+    return out;
 }
 
 // backpropagate! (SelfPlay.jl:190-217), quirk Q7, for the 16-lane group.
@@ -209,8 +245,8 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
                 int N; float W, R; int i = 0;
                 uint32_t nc = 0;
                 if (d > 0) {
-                    i = path[2 * d]; nc = t.nc[i];
-                    N = (int)(nc & 0xffffu); W = t.w[i]; R = t.nr[path[2 * d + 1]];
+                    i = path[2 * d]; nc = t.nc(i);
+                    N = (int)(nc & 0xffffu); W = t.w(i); R = t.nr[path[2 * d + 1]];
                 } else {
                     N = root_N; W = root_W; R = 0.0f;
                 }
@@ -220,8 +256,8 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
                 mmin = mmin < upd ? mmin : upd; mmax = mmax > upd ? mmax : upd;
                 v = R + discount * v;
                 if (d > 0) {
-                    t.nc[i] = (nc & 0xffff0000u) | (uint32_t)N; t.w[i] = W;
-                    t.ev[i] = R + (players == 1 ? discount * q : discount * (-q));
+                    t.nc(i) = (nc & 0xffff0000u) | (uint32_t)N; t.w(i) = W;
+                    t.ev(i) = R + (players == 1 ? discount * q : discount * (-q));
                 }
                 else { root_N = N; root_W = W; }
             }
@@ -238,9 +274,9 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
             int N, i = 0, tp; float W, R;
             uint32_t nc = 0;
             if (d > 0) {
-                i = path[2 * d]; nc = t.nc[i];
+                i = path[2 * d]; nc = t.nc(i);
                 const int c = path[2 * d + 1];
-                N = (int)(nc & 0xffffu); W = t.w[i]; R = t.nr[c]; tp = t.ntp[c];
+                N = (int)(nc & 0xffffu); W = t.w(i); R = t.nr[c]; tp = t.ntp[c];
             } else {
                 N = root_N; W = root_W; R = 0.0f; tp = root_tp;
             }
@@ -261,7 +297,7 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
             const float upd = R + discount * q;
             lmin = lmin < upd ? lmin : upd;
             lmax = lmax > upd ? lmax : upd;
-            if (d > 0) { t.nc[i] = (nc & 0xffff0000u) | (uint32_t)N; t.w[i] = W; t.ev[i] = R + discount * (-q); }
+            if (d > 0) { t.nc(i) = (nc & 0xffff0000u) | (uint32_t)N; t.w(i) = W; t.ev(i) = R + discount * (-q); }
             else { rN = N; rW = W; }
         }
     }
@@ -305,6 +341,6 @@ __device__ int select_action_dev(const int* cnt, uint32_t legal, int A, float te
 // Copy one game's tree to the global debug buffers (parity tests only).
 __device__ __forceinline__ void dump_tree(const TreeView& t, const TreeView& dst, int n_edges, int n_nodes,
                                           int lane16) {
-    for (int i = lane16; i < n_edges; i += 16) { dst.nc[i] = t.nc[i]; dst.w[i] = t.w[i]; dst.p[i] = t.p[i]; }
+    for (int i = lane16; i < n_edges; i += 16) dst.e[i] = t.e[i];
     for (int i = lane16; i < n_nodes; i += 16) { dst.nr[i] = t.nr[i]; dst.ntp[i] = t.ntp[i]; }
 }

@@ -1,4 +1,4 @@
-"""Diagnostic: per-phase cycle breakdown of mz_search_kernel from a separate
+"""Diagnostic: per-phase cycle breakdown of the search kernels from a separate
 -DMZ_STAMPS build (libmz_stamps.so).  Shares only; never quote its run time."""
 import ctypes
 import dataclasses
@@ -44,12 +44,16 @@ def main():
     assert L.mz_debug_stamps(eng.h, out.ctypes.data_as(ctypes.c_void_p), G) == 0
     out = out[out.sum(1) > 0]
     print("variant", eng.search_variant(), "blocks", len(out))
+    levels = out[:, 7].astype(np.float64)
+    out[:, 7] = 0
     tot = out.sum(1).astype(np.float64)
     med = np.median(out.astype(np.float64), axis=0)
     print(f"G={G} S={S}: median cycles per workgroup (s_memtime ticks, 100 MHz ref? see note)")
     for i, p in enumerate(PHASES[:7]):
         print(f"  {p:8s} {med[i]:12.0f}  per-sim {med[i] / S:10.1f}  share {med[i] / np.median(tot):6.3f}")
     print("  total   ", np.median(tot))
+    print(f"  select levels per sim (max over the workgroup's games): {np.median(levels) / S:.2f}; "
+          f"ticks per level {med[1] / np.median(levels):.1f}")
 
 
 if __name__ == "__main__":
