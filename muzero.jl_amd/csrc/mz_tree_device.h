@@ -141,7 +141,9 @@ struct SelectOut { int leaf_e, leaf_a, vtp, depth; };
 // pb_term table index: the host tabulates pbc(Np) * (sqrt(Np) / (Nc + 1))
 // (the f64 subexpression of ucb_score, SelfPlay.jl:172-174) for Nc < Np <=
 // S+1 as a triangle, so select replaces an f64 division by one LDS read.
-__host__ __device__ __forceinline__ int pbterm_index(int Np, int Nc) { return Np * (Np + 1) / 2 + Nc; }
+__host__ __device__ __forceinline__ int pbterm_index(int Np, int Nc) {
+    return (int)(((unsigned)Np * (unsigned)(Np + 1)) >> 1) + Nc;
+}
 __host__ __device__ __forceinline__ size_t pbterm_count(int S) { return (size_t)(S + 2) * (S + 3) / 2; }
 
 // max over the 16-lane group, one v_max_f32_dpp per step (the hazard pad —
@@ -182,7 +184,11 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
     int pe = 0, pc = 0;
     SelectOut out;
     for (;;) {
-        const float4 ed = t.e[e * A + ac];
+        float4 ed = t.e[e * A + ac];
+        // keep the whole record one load and the score branch-free: without
+        // these the compiler sinks the ev load and the division into an
+        // Nc > 0 branch (a second LDS round trip and two exec branches)
+        asm volatile("" : "+v"(ed.x), "+v"(ed.y), "+v"(ed.z), "+v"(ed.w));
         const uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
         const int Nc = (int)(nc & 0xffffu);
         double pb_c;
@@ -193,7 +199,8 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
             pb_c = pbn * (sqn / (double)(Nc + 1));
         }
         const double prior_score = pb_c * (double)ed.z;
-        const float vn = (ed.w - mmin) / den;            // discarded unless norm
+        float vn = (ed.w - mmin) / den;                  // discarded unless norm and Nc > 0
+        asm volatile("" : "+v"(vn));
         const float vs = Nc > 0 ? (norm ? vn : ed.w) : 0.0f;
         const float us = (float)(prior_score + (double)vs);
         const float u = lg ? us : -INFINITY;
@@ -266,46 +273,53 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
         mmin = __shfl(mmin, 0, 16); mmax = __shfl(mmax, 0, 16);
         return;
     }
+    // two players: to_play alternates with depth (node k has mod1(root_tp + k),
+    // the virtual_to_play of SelfPlay.jl:267), so below level d < depth the
+    // nearest reset is k0 = d+1 if tp(d+1) == tl, else d+2 (the leaf, level
+    // depth, always resets): v_in(d) = -R(d+1) or R(d+1) + γ(-R(d+2)).  Each
+    // lane issues its reads in two round trips: path entries of d, d+1, d+2,
+    // then the edge record and the children's R / to_play.
     float lmin = INFINITY, lmax = -INFINITY;
     int rN = root_N; float rW = root_W;
     for (int base = 0; base <= depth; base += 16) {
         const int d = base + a;
         if (d <= depth) {
-            int N, i = 0, tp; float W, R;
-            uint32_t nc = 0;
-            if (d > 0) {
-                i = path[2 * d]; nc = t.nc(i);
-                const int c = path[2 * d + 1];
-                N = (int)(nc & 0xffffu); W = t.w(i); R = t.nr[c]; tp = t.ntp[c];
-            } else {
-                N = root_N; W = root_W; R = 0.0f; tp = root_tp;
-            }
+            const int i = d > 0 ? path[2 * d] : 0;
+            const int c = d > 0 ? path[2 * d + 1] : 0;
+            const int c1 = d + 1 <= depth ? path[2 * d + 3] : 0;
+            const int c2 = d + 2 <= depth ? path[2 * d + 5] : 0;
+            const float4 ed = t.e[i];
+            const float Rc = t.nr[c];
+            const int tpc = t.ntp[c];
+            const float R1 = t.nr[c1], R2 = t.nr[c2];
+            const int tp1 = t.ntp[c1];
+            uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
+            int N; float W, R; int tp;
+            if (d > 0) { N = (int)(nc & 0xffffu); W = ed.y; R = Rc; tp = tpc; }
+            else { N = root_N; W = root_W; R = 0.0f; tp = root_tp; }
             float vin;
-            if (d == depth) {
-                vin = value;
-            } else {
-                int k0 = d + 1;                         // nearest reset at or below d+1
-                while (k0 < depth && t.ntp[path[2 * k0 + 1]] != tl) ++k0;
-                // the leaf always resets (its to_play is tl); a non-leaf k0 resets
-                float v = -t.nr[path[2 * k0 + 1]];
-                for (int k = k0 - 1; k >= d + 1; --k) v = t.nr[path[2 * k + 1]] + discount * v;
-                vin = v;
-            }
+            if (d == depth) vin = value;
+            else if (tp1 == tl) vin = -R1;
+            else vin = R1 + discount * (-R2);
             W = tp == tl ? W + vin : W - vin;
             N += 1;
             const float q = W / (float)N;
             const float upd = R + discount * q;
             lmin = lmin < upd ? lmin : upd;
             lmax = lmax > upd ? lmax : upd;
-            if (d > 0) { t.nc(i) = (nc & 0xffff0000u) | (uint32_t)N; t.w(i) = W; t.ev(i) = R + discount * (-q); }
-            else { rN = N; rW = W; }
+            if (d > 0) {
+                nc = (nc & 0xffff0000u) | (uint32_t)N;
+                t.nc(i) = nc; t.w(i) = W; t.ev(i) = R + discount * (-q);
+            } else { rN = N; rW = W; }
         }
     }
     lmin = g16_min(lmin);
     lmax = g16_max(lmax);
     mmin = mmin < lmin ? mmin : lmin;
     mmax = mmax > lmax ? mmax : lmax;
-    root_N = __shfl(rN, 0, 16); root_W = __shfl(rW, 0, 16);
+    // lane 0 of the group (level 0 = the root) to all 16 lanes: DPP row broadcast
+    root_N = __builtin_amdgcn_update_dpp(0, rN, 0x150, 0xF, 0xF, false);
+    root_W = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, rW), 0x150, 0xF, 0xF, false));
 }
 
 // select_action (SelfPlay.jl:293-306): same rule as the oracle.
