@@ -191,9 +191,11 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     int* sg_vtp = si + 128;
     int* sg_depth = si + 144;
     float* sg_stage = reinterpret_cast<float*>(si + 160);       // [4][16]
-    int* sg_path = si + 224;                                      // [T][2(S+2)]
+    float* sg_val = reinterpret_cast<float*>(si + 224);         // [4] leaf value (read-out activation applied)
+    float* sg_rew = reinterpret_cast<float*>(si + 228);         // [4] leaf reward
+    int* sg_path = si + 232;                                      // [T][2(S+2)]
     // select / gather tables in LDS (they sit on the per-level critical path)
-    double* l_pbc = reinterpret_cast<double*>(si + 224 + (T * PS + 3) / 4 * 4);   // [S+2]
+    double* l_pbc = reinterpret_cast<double*>(si + 232 + (T * PS + 3) / 4 * 4);   // [S+2]
     double* l_sqrt = l_pbc + (S + 2);                                           // [S+2]
     float* l_aval = reinterpret_cast<float*>(l_sqrt + (S + 2));                 // [32]
     double* l_pbterm = reinterpret_cast<double*>(l_aval + MZ_MAX_ACTIONS);     // [pbterm_count(S)]
@@ -271,77 +273,91 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     __syncthreads();
     SM_STAMP(0);
 
+    // Per simulation, three workgroup barriers besides the 8 network stages:
+    // wave 0 owns the trees (T <= 4 games x 16 lanes), so select -> gather and
+    // backup -> next select need only wave-local ordering.
     for (int s = 0; s < S; ++s) {
-        // ---- select (:256-268)
-        if (active) {
-            const SelectOut so = select_path<true>(tree, path, sg_rootN[g], sg_root_tp[g], legal, sg_mmin[g], sg_mmax[g],
-                                             a, lane, A, P.players, P.discount, l_pbterm, l_pbc, l_sqrt, P.seed,
-                                             gid, P.rng_step, s);
-            if (a == 0) { sg_leaf_e[g] = so.leaf_e; sg_leaf_a[g] = so.leaf_a; sg_vtp[g] = so.vtp; sg_depth[g] = so.depth; }
-        }
-        __syncthreads();
-        SM_STAMP(1);
+        if (tid < 64) {
+            // ---- select (:256-268)
+            if (active) {
+                const SelectOut so = select_path<true>(tree, path, sg_rootN[g], sg_root_tp[g], legal, sg_mmin[g],
+                                                       sg_mmax[g], a, lane, A, P.players, P.discount, l_pbterm, l_pbc,
+                                                       l_sqrt, P.seed, gid, P.rng_step, s);
+                if (a == 0) { sg_leaf_e[g] = so.leaf_e; sg_leaf_a[g] = so.leaf_a; sg_vtp[g] = so.vtp; sg_depth[g] = so.depth; }
+            }
+            __builtin_amdgcn_wave_barrier();
+            SM_STAMP(1);
 #ifdef MZ_STAMPS
-        if (threadIdx.x == 0) {                 // slot 7: select levels walked (max over the T games)
-            int md = 0;
-            for (int gl = 0; gl < T; ++gl) md = md > sg_depth[gl] ? md : sg_depth[gl];
-            st_acc[7] += (unsigned long long)md;
-        }
+            if (threadIdx.x == 0) {             // slot 7: select levels walked (max over the T games)
+                int md = 0;
+                for (int gl = 0; gl < T; ++gl) md = md > sg_depth[gl] ? md : sg_depth[gl];
+                st_acc[7] += (unsigned long long)md;
+            }
 #endif
-        // ---- gather: parent h -> prediction input; h *= 2 in place (Q1) -> dynamics input
-        for (int i = tid; i < T * H; i += SM_THREADS) {
-            const int gl = i / H, k = i - gl * H;
-            if (tile0 + gl >= P.G) continue;                  // inactive game of a partial tile
-            float* hp = hid + ((size_t)gl * NN + sg_leaf_e[gl]) * H + k;
-            const float hv = *hp;
-            const float h2 = hv * 2.0f;
-            *hp = h2;
-            act[P.x_pred + k * T + gl] = hv;
-            act[P.x_dyn + k * T + gl] = h2;
-        }
-        for (int i = tid; i < T * P.plane; i += SM_THREADS) {
-            const int gl = i / P.plane, k = i - gl * P.plane;
-            if (tile0 + gl >= P.G) continue;
-            act[P.x_dyn + (H + k) * T + gl] = l_aval[sg_leaf_a[gl]];
+            // ---- gather: parent h -> prediction input; h *= 2 in place (Q1) -> dynamics input
+            for (int i = tid; i < T * H; i += 64) {
+                const int gl = i / H, k = i - gl * H;
+                if (tile0 + gl >= P.G) continue;              // inactive game of a partial tile
+                float* hp = hid + ((size_t)gl * NN + sg_leaf_e[gl]) * H + k;
+                const float hv = *hp;
+                const float h2 = hv * 2.0f;
+                *hp = h2;
+                act[P.x_pred + k * T + gl] = hv;
+                act[P.x_dyn + k * T + gl] = h2;
+            }
+            for (int i = tid; i < T * P.plane; i += 64) {
+                const int gl = i / P.plane, k = i - gl * P.plane;
+                if (tile0 + gl >= P.G) continue;
+                act[P.x_dyn + (H + k) * T + gl] = l_aval[sg_leaf_a[gl]];
+            }
         }
         __syncthreads();
         SM_STAMP(2);
         // ---- prediction(parent.h) ‖ dynamics(2h ⊕ a/|A|)
         sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act);
         SM_STAMP(3);
-        // ---- expand slot s+1 (:280) + store h'
         const int e_new = s + 1;
-        if (tree_thread) {
-            const float prior = double_softmax_prior(a < A ? act[P.p_out + a * T + g] : 0.0f, a, A, legal,
-                                                     sg_stage + 16 * g);
-            if (active) init_edges(tree, e_new, a, A, prior);
+        if (tid < 64) {
+            // ---- expand slot s+1 (:280)
+            if (tree_thread) {
+                const float prior = double_softmax_prior(a < A ? act[P.p_out + a * T + g] : 0.0f, a, A, legal,
+                                                         sg_stage + 16 * g);
+                if (active) init_edges(tree, e_new, a, A, prior);
+            }
+        } else if (tid < 64 + T) {
+            // wave 1: the value / reward read-out activations (f64 tanh) off
+            // wave 0's critical path
+            const int gl = tid - 64;
+            sg_val[gl] = mz_post_act(P.v_act, act[P.v_out + gl]);
+            sg_rew[gl] = mz_post_act(P.r_act, act[P.r_out + gl]);
+        } else if (tid >= 128) {
+            for (int i = tid - 128; i < T * H; i += SM_THREADS - 128)     // store h'
+                hid[((size_t)(i / H) * NN + e_new) * H + (i % H)] = act[P.h_out + (i % H) * T + i / H];
         }
-        for (int i = tid; i < T * H; i += SM_THREADS) {
-            const int gl = i / H, k = i - gl * H;
-            hid[((size_t)gl * NN + e_new) * H + k] = act[P.h_out + k * T + gl];
-        }
+        __syncthreads();
         SM_STAMP(4);
-        // ---- backpropagate! (:190-217)
+        // ---- backpropagate! (:190-217); no barrier after: only wave 0 reads the tree
         if (active) {
             const int tl = sg_vtp[g];
             const int depth = sg_depth[g];
             if (a == 0) {
                 const int li = sg_leaf_e[g] * A + sg_leaf_a[g];
                 tree.nc(li) = (tree.nc(li) & 0xffffu) | ((uint32_t)(e_new + 1) << 16);
-                tree.nr[e_new] = mz_post_act(P.r_act, act[P.r_out + g]);
+                tree.nr[e_new] = sg_rew[g];
                 tree.ntp[e_new] = (int8_t)tl;
                 path[2 * depth + 1] = e_new;
             }
             __builtin_amdgcn_wave_barrier();
             int rN = sg_rootN[g];
             float rW = sg_rootW[g], mmin = sg_mmin[g], mmax = sg_mmax[g];
-            backup_path(tree, path, depth, mz_post_act(P.v_act, act[P.v_out + g]), tl, A, P.players, P.discount,
-                        rN, rW, sg_root_tp[g], mmin, mmax, a);
+            backup_path(tree, path, depth, sg_val[g], tl, A, P.players, P.discount, rN, rW, sg_root_tp[g], mmin,
+                        mmax, a);
             if (a == 0) { sg_rootN[g] = rN; sg_rootW[g] = rW; sg_mmin[g] = mmin; sg_mmax[g] = mmax; }
         }
-        __syncthreads();
+        __builtin_amdgcn_wave_barrier();
         SM_STAMP(5);
     }
+    __syncthreads();
 
     // ---- store_search_stats! (:115-122) + select_action (:293-306)
     if (active) {
