@@ -248,14 +248,25 @@ MZ_HD double mz_stream_gamma(mz_stream* s, double alpha) {
     return g;
 }
 
-/* Dirichlet(n, alpha) noise into out[0..n) as f32, the draw order being the
- * ascending legal-action order (reference: Dict key order, SelfPlay.jl:103).
- * As in Distributions._rand!: x_i = Float32(gamma_i); x .*= inv(sum(x)).  */
+/* Component i (0-based, ascending legal-action order; reference: Dict key
+ * order, SelfPlay.jl:103) of Dirichlet(n, alpha) before normalisation:
+ * Float32(Gamma(alpha, 1)) drawn from its OWN stream (NOISE, game, step,
+ * idx = i << 24 + draw), so the n components are independent and a device
+ * lane draws each (Julia's global-RNG draw order is not reproducible
+ * anyway, quirk Q6).                                                      */
+MZ_HD float mz_dirichlet_gamma(uint64_t seed, uint32_t game, uint32_t step, int i, float alpha) {
+    mz_stream s; s.seed = seed; s.purpose = MZ_RNG_NOISE; s.id = game; s.step = step;
+    s.idx = (uint32_t)i << 24;
+    return (float)mz_stream_gamma(&s, (double)alpha);
+}
+
+/* Dirichlet(n, alpha) noise into out[0..n) as f32.  As in
+ * Distributions._rand!: x_i = Float32(gamma_i); x .*= inv(sum(x)), the sum
+ * taken in ascending i.                                                    */
 MZ_HD void mz_dirichlet(uint64_t seed, uint32_t game, uint32_t step, int n, float alpha, float* out) {
-    mz_stream s; s.seed = seed; s.purpose = MZ_RNG_NOISE; s.id = game; s.step = step; s.idx = 0;
     float sum = 0.0f;
     for (int i = 0; i < n; ++i) {
-        out[i] = (float)mz_stream_gamma(&s, (double)alpha);
+        out[i] = mz_dirichlet_gamma(seed, game, step, i, alpha);
         sum = sum + out[i];
     }
     float inv = 1.0f / sum;

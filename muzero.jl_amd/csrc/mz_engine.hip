@@ -493,7 +493,7 @@ static int build_small(mz_handle* h) {
         MZ_TRY(h, hipMemcpy(h->d_sm_rec[ti], rec.data(), rec.size() * 4, hipMemcpyHostToDevice));
         const int S = h->S, NN = S + 1, PS = 2 * (S + 2);
         size_t ints = (size_t)lay[0] + (size_t)(nrec + 1) * SM_REC_INTS +
-                      ((size_t)T * NN * h->H + 3) / 4 * 4 + 232 + ((size_t)T * PS + 3) / 4 * 4 +
+                      ((size_t)T * NN * h->H + 3) / 4 * 4 + 296 + ((size_t)T * PS + 3) / 4 * 4 +
                       (size_t)4 * (S + 2) + MZ_MAX_ACTIONS;
         // + the pb_term triangle (the small kernel requires it in LDS; when
         // the total exceeds the LDS budget the tile-16 kernel is used)

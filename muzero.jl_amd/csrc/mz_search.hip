@@ -112,16 +112,9 @@ __device__ __forceinline__ void search_body(const SearchParams& P) {
         }
     }
     __syncthreads();
-    if (P.exploration && active && a == 0) {                 // add_exploration_noise! (:102-109)
-        const int n = __builtin_popcount(legal);
-        float noise[MZ_MAX_ACTIONS];
-        mz_dirichlet(P.seed, gid, P.rng_step, n, P.dirichlet_alpha, noise);
-        const float one_m = 1.0f - P.exploration_eps;
-        int i = 0;
-        for (int b = 0; b < A; ++b) if ((legal >> b) & 1u) {
-            tree.p(b) = tree.p(b) * one_m + noise[i] * P.exploration_eps;
-            ++i;
-        }
+    if (P.exploration && active) {                           // add_exploration_noise! (:102-109)
+        const float nz = root_noise_lane(legal, a, A, P.seed, gid, P.rng_step, P.dirichlet_alpha, sg_stage + 16 * g);
+        if (a < A && ((legal >> a) & 1u)) tree.p(a) = tree.p(a) * (1.0f - P.exploration_eps) + nz * P.exploration_eps;
     }
     __syncthreads();
     MZ_STAMP(0);

@@ -147,19 +147,6 @@ __device__ __forceinline__ void sm_load(int n, const float* W, float (&wr)[NMAX]
 }
 
 // once-per-move helpers kept out of line
-__device__ __noinline__ void sm_root_noise(TreeView t, uint32_t legal, int A, uint64_t seed, uint32_t gid,
-                                           uint32_t step, float alpha, float eps) {
-    const int n = __builtin_popcount(legal);
-    float noise[MZ_MAX_ACTIONS];
-    mz_dirichlet(seed, gid, step, n, alpha, noise);
-    const float one_m = 1.0f - eps;
-    int i = 0;
-    for (int b = 0; b < A; ++b) if ((legal >> b) & 1u) {
-        t.p(b) = t.p(b) * one_m + noise[i] * eps;
-        ++i;
-    }
-}
-
 __device__ __noinline__ int sm_select_action(const int* cnt, uint32_t legal, int A, float temperature, uint32_t r) {
     return select_action_dev(cnt, legal, A, temperature, r);
 }
@@ -193,9 +180,10 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     float* sg_stage = reinterpret_cast<float*>(si + 160);       // [4][16]
     float* sg_val = reinterpret_cast<float*>(si + 224);         // [4] leaf value (read-out activation applied)
     float* sg_rew = reinterpret_cast<float*>(si + 228);         // [4] leaf reward
-    int* sg_path = si + 232;                                      // [T][2(S+2)]
+    float* sg_noise = reinterpret_cast<float*>(si + 232);       // [4][16] root exploration noise
+    int* sg_path = si + 296;                                      // [T][2(S+2)]
     // select / gather tables in LDS (they sit on the per-level critical path)
-    double* l_pbc = reinterpret_cast<double*>(si + 232 + (T * PS + 3) / 4 * 4);   // [S+2]
+    double* l_pbc = reinterpret_cast<double*>(si + 296 + (T * PS + 3) / 4 * 4);   // [S+2]
     double* l_sqrt = l_pbc + (S + 2);                                           // [S+2]
     float* l_aval = reinterpret_cast<float*>(l_sqrt + (S + 2));                 // [32]
     double* l_pbterm = reinterpret_cast<double*>(l_aval + MZ_MAX_ACTIONS);     // [pbterm_count(S)]
@@ -245,6 +233,11 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     // registers are then reloaded with the prediction ‖ dynamics weights
     float wr[SM_MAX_SIM][16];
     sm_load<SM_MAX_SIM>(P.n_root, P.w_root, wr);
+    // the root's exploration noise depends only on the legal set: drawn here,
+    // lane-parallel, while the weight loads are in flight
+    if (P.exploration && active)
+        sg_noise[16 * g + a] = root_noise_lane(sg_legal[g], a, A, P.seed, gid, P.rng_step, P.dirichlet_alpha,
+                                               sg_stage + 16 * g);
     sm_run<T, SM_MAX_SIM>(P.n_root, wr, rec_root, act);
     for (int i = tid; i < T * H; i += SM_THREADS) {     // h -> hidden slot 0 and the prediction input
         const int gl = i / H, k = i - gl * H;
@@ -268,8 +261,8 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         }
     }
     __syncthreads();
-    if (P.exploration && active && a == 0)                   // add_exploration_noise! (:102-109)
-        sm_root_noise(tree, legal, A, P.seed, gid, P.rng_step, P.dirichlet_alpha, P.exploration_eps);
+    if (P.exploration && active && a < A && ((legal >> a) & 1u))     // add_exploration_noise! (:102-109)
+        tree.p(a) = tree.p(a) * (1.0f - P.exploration_eps) + sg_noise[16 * g + a] * P.exploration_eps;
     __syncthreads();
     SM_STAMP(0);
 

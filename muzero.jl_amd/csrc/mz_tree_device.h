@@ -125,6 +125,20 @@ __device__ __forceinline__ float double_softmax_prior(float logit, int a, int A,
     return lg ? e2 / s2 : 0.0f;
 }
 
+// add_exploration_noise! (SelfPlay.jl:102-109) noise for the 16-lane group,
+// lane-parallel: legal lane a draws Dirichlet component rank(a) from its own
+// stream (mz_dirichlet_gamma); the f32 sum runs in ascending action order
+// (illegal lanes add +0, exact); returns the normalised noise (0 if illegal).
+__device__ __forceinline__ float root_noise_lane(uint32_t legal, int a, int A, uint64_t seed, uint32_t gid,
+                                                 uint32_t step, float alpha, float* st) {
+    const bool lg = a < A && ((legal >> a) & 1u);
+    const int r = __builtin_popcount(legal & ((1u << a) - 1u));
+    const float gm = lg ? mz_dirichlet_gamma(seed, gid, step, r, alpha) : 0.0f;
+    const float sum = g16_seqsum(gm, A, st, a);
+    const float inv = 1.0f / sum;
+    return lg ? gm * inv : 0.0f;
+}
+
 // Write the A child edges of expanded slot e (N=0, W=0, prior, no child).
 __device__ __forceinline__ void init_edges(const TreeView& t, int e, int a, int A, float prior) {
     if (a < A) {

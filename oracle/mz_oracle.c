@@ -213,7 +213,7 @@ static int new_node(OCtx* X, float prior) {
  * policy entries of `actions` (the ROOT's legal set at every depth, Q4). */
 static void expand_node(OCtx* X, int ni, const uint8_t* legal, int to_play, float reward,
                         const float* policy, int hslot, int eslot) {
-    float v[MAXA], p[MAXA]; int acts[MAXA], n = 0;
+    float v[MAXA] = {0}, p[MAXA]; int acts[MAXA], n = 0;
     for (int a = 0; a < X->A; ++a) if (legal[a]) { acts[n] = a; v[n] = policy[a]; ++n; }
     softmax_n(v, n, p);
     for (int i = 0; i < n; ++i) {
