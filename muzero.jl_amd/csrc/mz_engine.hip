@@ -27,6 +27,8 @@ extern "C" __global__ void mz_search_kernel_lds_res(SearchParams P);
 extern "C" __global__ void mz_search_small1(SmallParams P);
 extern "C" __global__ void mz_search_small2(SmallParams P);
 extern "C" __global__ void mz_search_small4(SmallParams P);
+extern "C" __global__ void mz_unroll_small1(SmallUnrollParams P);
+extern "C" __global__ void mz_unroll_small2(SmallUnrollParams P);
 extern "C" __global__ void mz_search_kernel_hbm_res(SearchParams P);
 
 extern "C" __global__ void mz_unroll_kernel(UnrollParams P);
@@ -35,9 +37,10 @@ extern "C" __global__ void mz_forward_kernel(const int* plan, const float* Wp, c
                                              float* out0, int out1_off, int o1, float* out1, int sm1, int act0,
                                              int act1);
 extern "C" __global__ void mz_loss_kernel(int B, int K, int A, const float* pv, const float* pp, const float* tv,
-                                          const float* tp, const float* gscale, float* out);
-extern "C" __global__ void mz_sqnorm_kernel(const float* P, size_t n, double* out);
-extern "C" __global__ void mz_l2_finish_kernel(const double* sq, float* out);
+                                          const float* tp, const float* gscale, float* terms, float* out);
+#define MZ_L2_BLOCKS 32
+extern "C" __global__ void mz_sqnorm_kernel(const float* flat, const size_t* off, const size_t* cnt, double* part);
+extern "C" __global__ void mz_l2_finish_kernel(const double* part, float* out);
 extern "C" __global__ void mz_grad_2theta_kernel(const float* P, float* G, size_t n);
 extern "C" __global__ void mz_adam_kernel(float* P, float* M, float* V, const float* G, float gscale, size_t n,
                                           double bp1, double bp2, double eta);
@@ -115,6 +118,7 @@ struct mz_handle {
     int sm_lay[3][8];                       // per T: act_total, x_rep, x_pred, x_dyn, h_out, v_out, p_out, r_out
     size_t sm_lds[3] = {0, 0, 0};
     int force_kernel = 0;                   // 0 auto, 1 tile16, 2 small
+    bool images_dirty = false;              // d_flat changed since the last repack (learner update)
     std::string last_variant = "none";
     int force_T = 0;                        // MZ_SMALL_T=1|2|4 (tests)
     float* d_hid = nullptr;
@@ -126,7 +130,9 @@ struct mz_handle {
     int bcap = 0;
     float *d_bobs = nullptr, *d_bact = nullptr, *d_btv = nullptr, *d_btr = nullptr, *d_btp = nullptr,
           *d_bgs = nullptr, *d_pv = nullptr, *d_pp = nullptr, *d_pr = nullptr, *d_loss = nullptr;
-    double* d_sq = nullptr;
+    double* d_sq = nullptr;                 // [3][MZ_L2_BLOCKS] partial Σθ²
+    size_t* d_netoff = nullptr;             // [3] flat offset, [3] count per net
+    float* d_lterm = nullptr;               // [2][B(K+1)] loss terms
     unsigned long long* d_stamps = nullptr;
     std::vector<void*> allocs;
 };
@@ -538,7 +544,19 @@ static int repack(mz_handle* h, hipStream_t st = nullptr) {
                            h->d_flat, h->d_sm_srcb, h->d_sm_bias, h->sm_b_n);
     }
     MZ_TRY(h, hipGetLastError());
+    h->images_dirty = false;
     return 0;
+}
+
+// The packed images are rebuilt lazily, on the stream of the call that reads
+// them, after learner updates (the learner itself gathers from d_flat).
+static int ensure_images(mz_handle* h, hipStream_t st) {
+    return h->images_dirty ? repack(h, st) : 0;
+}
+
+// LDS of mz_unroll_small{1,2}: activations, records (+1 slack stage), staging
+static size_t unroll_small_lds(const mz_handle* h, int ti) {
+    return ((size_t)h->sm_lay[ti][0] + (size_t)(h->sm_n_sim + h->sm_n_root + 1) * SM_REC_INTS + 64) * 4;
 }
 
 static size_t tree_game_bytes(int S, int A) {
@@ -616,6 +634,11 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
             for (int ti = 0; ti < 3; ++ti)
                 CK(hipFuncSetAttribute(ks[ti], hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->sm_lds[ti]) ==
                            hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(small)"));
+            const void* ku[2] = {(const void*)mz_unroll_small1, (const void*)mz_unroll_small2};
+            for (int ti = 0; ti < 2; ++ti)
+                CK(hipFuncSetAttribute(ku[ti], hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)unroll_small_lds(h, ti)) == hipSuccess
+                       ? 0 : fail(h, "hipFuncSetAttribute(unroll_small)"));
         }
     }
     const int S = h->S, A = h->A, H = h->H;
@@ -653,7 +676,12 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
     CK(al(&h->d_m, h->nflat)); CK(al(&h->d_v, h->nflat)); CK(al(&h->d_grad, h->nflat));
     CK(hipMemset(h->d_m, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
     CK(hipMemset(h->d_v, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
-    CK(al(&h->d_loss, 8)); CK(al(&h->d_sq, 4));
+    CK(al(&h->d_loss, 8)); CK(al(&h->d_sq, 3 * MZ_L2_BLOCKS));
+    {
+        size_t oc[6] = {h->flat_off[0], h->flat_off[1], h->flat_off[2], h->nparams[0], h->nparams[1], h->nparams[2]};
+        CK(al(&h->d_netoff, 6));
+        CK(hipMemcpy(h->d_netoff, oc, sizeof(oc), hipMemcpyHostToDevice) == hipSuccess ? 0 : fail(h, "copy"));
+    }
     h->use_res = h->d_plan_sim_res != nullptr && std::getenv("MZ_NO_RESIDENT") == nullptr;
     {
         const search_fn ks[4] = {mz_search_kernel_lds, mz_search_kernel_hbm, mz_search_kernel_lds_res,
@@ -715,6 +743,7 @@ int mz_net_forward(mz_handle* h, int net, const float* x, int n, float* out0, fl
     const int o1 = net == MZ_NET_PRED ? A : 1;
     const int o1_off = net == MZ_NET_PRED ? h->lay.p_out : h->lay.r_out;
     float *dx = nullptr, *d0 = nullptr, *d1 = nullptr;
+    if (ensure_images(h, h->stream)) return -1;
     MZ_TRY(h, hipMalloc(&dx, (size_t)n * in_feat * 4));
     MZ_TRY(h, hipMalloc(&d0, (size_t)n * o0 * 4));
     MZ_TRY(h, hipMalloc(&d1, (size_t)n * o1 * 4));
@@ -758,6 +787,7 @@ int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* leg
     P.stamps = h->d_stamps;
 #endif
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    if (ensure_images(h, st)) return -1;     // after learner updates (stream-ordered with this search)
     const bool small = h->small_ok && h->force_kernel != 1 && (h->force_kernel == 2 || G <= 4 * h->n_cu);
     if (small) {
         const int T = h->force_T ? h->force_T : G <= h->n_cu ? 1 : G <= 2 * h->n_cu ? 2 : 4;
@@ -881,6 +911,7 @@ static int ensure_batch(mz_handle* h, int B) {
                       (size_t)B * (K + 1) * A, (size_t)B, (size_t)B * (K + 1), (size_t)B * (K + 1) * A,
                       (size_t)B * (K + 1)};
     for (int i = 0; i < 9; ++i) MZ_TRY(h, dalloc(h, bufs[i], sizes[i]));
+    MZ_TRY(h, dalloc(h, &h->d_lterm, (size_t)2 * B * (K + 1)));
     h->bcap = B;
     return 0;
 }
@@ -892,19 +923,35 @@ int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float*
     if (B < 1) return fail(h, "batch_size must be >= 1");
     if (ensure_batch(h, B)) return -1;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    UnrollParams U;
-    U.B = B; U.K = K; U.A = A; U.H = h->H; U.plane = h->plane; U.obs_feat = h->obs_feat;
-    U.obs = b->observation; U.actions = b->actions; U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
-    U.Wp = h->d_Wp; U.Bp = h->d_Bp; U.plan_repr = h->d_plan[0]; U.plan_sim = h->d_plan[4]; U.lay = h->lay;
-    hipLaunchKernelGGL(mz_unroll_kernel, dim3((B + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
-                       (size_t)h->lay.total * 4, st, U);
+    if (h->small_ok) {
+        // the search's stage schedule, T samples per workgroup, weights
+        // gathered from d_flat (no repack between learner steps)
+        const int ti = B <= 4 * h->n_cu ? 0 : 1, T = ti + 1;
+        const int* lay = h->sm_lay[ti];
+        SmallUnrollParams U;
+        U.B = B; U.K = K; U.A = A; U.H = h->H; U.plane = h->plane; U.obs_feat = h->obs_feat;
+        U.obs = b->observation; U.actions = b->actions; U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
+        U.n_sim = h->sm_n_sim; U.n_root = h->sm_n_root; U.flat = h->d_flat; U.srcw = h->d_sm_srcw;
+        U.srcb = h->d_sm_srcb; U.rec = h->d_sm_rec[ti]; U.act_total = lay[0];
+        U.x_rep = lay[1]; U.x_pred = lay[2]; U.x_dyn = lay[3]; U.h_out = lay[4]; U.v_out = lay[5];
+        U.p_out = lay[6]; U.r_out = lay[7]; U.v_act = h->lay.v_act; U.r_act = h->lay.r_act;
+        void* args[] = {&U};
+        MZ_TRY(h, hipLaunchKernel(ti == 0 ? (const void*)mz_unroll_small1 : (const void*)mz_unroll_small2,
+                                  dim3((B + T - 1) / T), dim3(SM_THREADS), args, unroll_small_lds(h, ti), st));
+    } else {
+        if (ensure_images(h, st)) return -1;
+        UnrollParams U;
+        U.B = B; U.K = K; U.A = A; U.H = h->H; U.plane = h->plane; U.obs_feat = h->obs_feat;
+        U.obs = b->observation; U.actions = b->actions; U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
+        U.Wp = h->d_Wp; U.Bp = h->d_Bp; U.plan_repr = h->d_plan[0]; U.plan_sim = h->d_plan[4]; U.lay = h->lay;
+        hipLaunchKernelGGL(mz_unroll_kernel, dim3((B + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
+                           (size_t)h->lay.total * 4, st, U);
+    }
     float* lo = losses_dev ? losses_dev : h->d_loss;
     hipLaunchKernelGGL(mz_loss_kernel, dim3(1), dim3(MZ_THREADS), 0, st, B, K, A, h->d_pv, h->d_pp,
-                       b->target_values, b->target_policies, b->gradient_scale, lo);
-    MZ_TRY(h, hipMemsetAsync(h->d_sq, 0, 3 * sizeof(double), st));
-    for (int net = 0; net < 3; ++net)
-        hipLaunchKernelGGL(mz_sqnorm_kernel, dim3(64), dim3(MZ_THREADS), 0, st, h->d_flat + h->flat_off[net],
-                           h->nparams[net], h->d_sq + net);
+                       b->target_values, b->target_policies, b->gradient_scale, h->d_lterm, lo);
+    hipLaunchKernelGGL(mz_sqnorm_kernel, dim3(MZ_L2_BLOCKS, 3), dim3(MZ_THREADS), 0, st, h->d_flat,
+                       h->d_netoff, h->d_netoff + 3, h->d_sq);
     hipLaunchKernelGGL(mz_l2_finish_kernel, dim3(1), dim3(64), 0, st, h->d_sq, lo);
     float* g = grad_dev ? grad_dev : h->d_grad;
     hipLaunchKernelGGL(mz_grad_2theta_kernel, dim3(128), dim3(MZ_THREADS), 0, st, h->d_flat, g, h->nflat);
@@ -920,7 +967,9 @@ int mz_learner_apply_dev(mz_handle* h, const float* grad_dev, float grad_scale, 
                        grad_scale, h->nflat, h->bp1, h->bp2, eta);
     h->bp1 = h->bp1 * 0.9;                  // βp .= βp .* β
     h->bp2 = h->bp2 * 0.999;
-    return repack(h, st);
+    h->images_dirty = true;                 // search / forward images rebuilt when next read
+    MZ_TRY(h, hipGetLastError());
+    return 0;
 }
 
 int mz_learner_step(mz_handle* h, const mz_batch* b, double eta, float* losses_out) {

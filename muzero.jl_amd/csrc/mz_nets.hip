@@ -100,34 +100,42 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_unroll_kernel(Unroll
 }
 
 // Losses of Learning.jl:261-288 (diagnostic in ref_semantics, Q11): one
-// workgroup, per-sample terms in the oracle's order, cross-sample sums in
+// workgroup.  The per-(sample, step) terms — squared value error and the
+// policy cross-entropy of that step — are computed by all threads into
+// `terms` (2 x B(K+1) floats, global scratch); then each sample folds its
+// steps in ascending k as the oracle does, and the cross-sample sums are
 // f64 (tolerance-checked, not bitwise).  out[0] value, out[2] policy.
 extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_loss_kernel(
     int B, int K, int A, const float* pv, const float* pp, const float* tv, const float* tp,
-    const float* gscale, float* out) {
+    const float* gscale, float* terms, float* out) {
     __shared__ double red_v[MZ_THREADS], red_p[MZ_THREADS], red_c[MZ_THREADS];
     const int tid = threadIdx.x;
+    const int n = B * (K + 1);
+    float* vsq = terms;
+    float* cet = terms + n;
+    for (int t = tid; t < n; t += blockDim.x) {
+        const float d = pv[t] - tv[t];
+        vsq[t] = d * d;
+        const float* yh = pp + (size_t)t * A;
+        const float* y = tp + (size_t)t * A;
+        float m = yh[0];
+        for (int i = 1; i < A; ++i) m = m > yh[i] ? m : yh[i];
+        float se = 0.0f;
+        for (int i = 0; i < A; ++i) se = se + det_expf(yh[i] - m);
+        const float ls = det_logf(se);
+        float ce = 0.0f;
+        for (int i = 0; i < A; ++i) ce = ce + y[i] * ((yh[i] - m) - ls);
+        cet[t] = ce;
+    }
+    __syncthreads();                            // block-scope: the terms are visible
     double sv = 0.0, sg = 0.0, sc = 0.0;
     for (int j = tid; j < B; j += blockDim.x) {
-        float s = 0.0f;
+        float s = 0.0f, c = 0.0f;
         for (int k = 0; k <= K; ++k) {
-            const float d = pv[(size_t)j * (K + 1) + k] - tv[(size_t)j * (K + 1) + k];
-            s = s + d * d;
+            s = s + vsq[(size_t)j * (K + 1) + k];
+            c = c + (-cet[(size_t)j * (K + 1) + k]);
         }
         sv += (double)(s / gscale[j]);
-        float c = 0.0f;
-        for (int k = 0; k <= K; ++k) {
-            const float* yh = pp + ((size_t)j * (K + 1) + k) * A;
-            const float* y = tp + ((size_t)j * (K + 1) + k) * A;
-            float m = yh[0];
-            for (int i = 1; i < A; ++i) m = m > yh[i] ? m : yh[i];
-            float se = 0.0f;
-            for (int i = 0; i < A; ++i) se = se + det_expf(yh[i] - m);
-            const float ls = det_logf(se);
-            float ce = 0.0f;
-            for (int i = 0; i < A; ++i) ce = ce + y[i] * ((yh[i] - m) - ls);
-            c = c + (-ce);
-        }
         sc += (double)c;                        // Σ_k ce_k
         sg += 1.0 / (double)gscale[j];          // Σ_j 1/g_j
     }
@@ -144,9 +152,16 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_loss_kernel(
     }
 }
 
-// Σθ² per net (sum(sqnorm, params), :287) in f64; out is zeroed by the host.
-extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_sqnorm_kernel(const float* P, size_t n, double* out) {
+// Σθ² per net (sum(sqnorm, params), :287) in f64, deterministic: block b of
+// net `blockIdx.y` sums a fixed slice in a fixed order into part[net][b];
+// mz_l2_finish_kernel adds the partials in ascending b.
+#define MZ_L2_BLOCKS 32
+extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_sqnorm_kernel(const float* flat, const size_t* off,
+                                                                          const size_t* cnt, double* part) {
     __shared__ double red[MZ_THREADS];
+    const int net = blockIdx.y;
+    const float* P = flat + off[net];
+    const size_t n = cnt[net];
     double s = 0.0;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         s += (double)P[i] * (double)P[i];
@@ -156,11 +171,15 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_sqnorm_kernel(const 
         if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
         __syncthreads();
     }
-    if (threadIdx.x == 0) atomicAdd(out, red[0]);
+    if (threadIdx.x == 0) part[net * MZ_L2_BLOCKS + blockIdx.x] = red[0];
 }
 
-extern "C" __global__ void mz_l2_finish_kernel(const double* sq, float* out) {
-    if (threadIdx.x < 3) out[3 + threadIdx.x] = (float)sq[threadIdx.x];
+extern "C" __global__ void mz_l2_finish_kernel(const double* part, float* out) {
+    if (threadIdx.x < 3) {
+        double s = 0.0;
+        for (int b = 0; b < MZ_L2_BLOCKS; ++b) s += part[threadIdx.x * MZ_L2_BLOCKS + b];
+        out[3 + threadIdx.x] = (float)s;
+    }
 }
 
 // gradient of the ref_semantics loss: only sum(sqnorm, params) depends on
