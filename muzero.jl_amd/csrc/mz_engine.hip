@@ -36,14 +36,14 @@ extern "C" __global__ void mz_forward_kernel(const int* plan, const float* Wp, c
                                              int in_off, int in_feat, const float* x, int n, int out0_off, int o0,
                                              float* out0, int out1_off, int o1, float* out1, int sm1, int act0,
                                              int act1);
-extern "C" __global__ void mz_loss_kernel(int B, int K, int A, const float* pv, const float* pp, const float* tv,
-                                          const float* tp, const float* gscale, float* terms, float* out);
 #define MZ_L2_BLOCKS 32
-extern "C" __global__ void mz_sqnorm_kernel(const float* flat, const size_t* off, const size_t* cnt, double* part);
-extern "C" __global__ void mz_l2_finish_kernel(const double* part, float* out);
-extern "C" __global__ void mz_grad_2theta_kernel(const float* P, float* G, size_t n);
+extern "C" __global__ void mz_learner_grad_kernel(int B, int K, int A, int v_act, int r_act, float* pv, float* pp,
+                                                  float* pr, const float* tv, const float* tp, const float* gscale,
+                                                  float* terms, const float* flat, const size_t* netoff, float* G,
+                                                  double* part, unsigned* counter, float* out);
 extern "C" __global__ void mz_adam_kernel(float* P, float* M, float* V, const float* G, float gscale, size_t n,
-                                          double bp1, double bp2, double eta);
+                                          double bp1, double bp2, double eta, float* Wp, float* Bp,
+                                          const int* inv_tile, float* smw, float* smb, const int* inv_small);
 extern "C" __global__ void mz_repack_kernel(const float* flat, const int* src, float* packed, size_t n);
 
 namespace {
@@ -118,7 +118,11 @@ struct mz_handle {
     int sm_lay[3][8];                       // per T: act_total, x_rep, x_pred, x_dyn, h_out, v_out, p_out, r_out
     size_t sm_lds[3] = {0, 0, 0};
     int force_kernel = 0;                   // 0 auto, 1 tile16, 2 small
-    bool images_dirty = false;              // d_flat changed since the last repack (learner update)
+    // inverse image maps, one code per flat parameter: >= 0 position in the
+    // weight image, <= -2 position -code-2 in the bias image, -1 none.  ADAM
+    // scatters every update into the images through them (no repack).
+    std::vector<int> inv_tile, inv_small;
+    int* d_inv_tile = nullptr; int* d_inv_small = nullptr;
     std::string last_variant = "none";
     int force_T = 0;                        // MZ_SMALL_T=1|2|4 (tests)
     float* d_hid = nullptr;
@@ -132,6 +136,7 @@ struct mz_handle {
           *d_bgs = nullptr, *d_pv = nullptr, *d_pp = nullptr, *d_pr = nullptr, *d_loss = nullptr;
     double* d_sq = nullptr;                 // [3][MZ_L2_BLOCKS] partial Σθ²
     size_t* d_netoff = nullptr;             // [3] flat offset, [3] count per net
+    unsigned* d_counter = nullptr;          // last-block counter of mz_learner_grad_kernel
     float* d_lterm = nullptr;               // [2][B(K+1)] loss terms
     unsigned long long* d_stamps = nullptr;
     std::vector<void*> allocs;
@@ -427,6 +432,9 @@ static int build_small(mz_handle* h) {
     fill(sim, st_s, sl_s, b0_s, 0);
     fill(root, st_r, sl_r, b0_r, h->sm_n_sim);
     h->sm_w_n = sw.size(); h->sm_b_n = sb.size();
+    h->inv_small.assign(h->nflat, -1);
+    for (size_t i = 0; i < sw.size(); ++i) if (sw[i] >= 0) h->inv_small[(size_t)sw[i]] = (int)i;
+    for (size_t i = 0; i < sb.size(); ++i) if (sb[i] >= 0) h->inv_small[(size_t)sb[i]] = -(int)i - 2;
     MZ_TRY(h, dalloc(h, &h->d_sm_srcw, sw.size()));
     MZ_TRY(h, dalloc(h, &h->d_sm_srcb, sb.size()));
     MZ_TRY(h, dalloc(h, &h->d_sm_w, sw.size()));
@@ -523,6 +531,9 @@ static int build_pack_index(mz_handle* h) {
                 }
         for (int o = 0; o < L.out; ++o) sb[(size_t)L.packed_b + o] = (int)(L.flux_b + o);
     }
+    h->inv_tile.assign(h->nflat, -1);
+    for (size_t i = 0; i < sw.size(); ++i) if (sw[i] >= 0) h->inv_tile[(size_t)sw[i]] = (int)i;
+    for (size_t i = 0; i < sb.size(); ++i) if (sb[i] >= 0) h->inv_tile[(size_t)sb[i]] = -(int)i - 2;
     MZ_TRY(h, dalloc(h, &h->d_srcW, sw.size()));
     MZ_TRY(h, dalloc(h, &h->d_srcB, sb.size()));
     MZ_TRY(h, hipMemcpy(h->d_srcW, sw.data(), sw.size() * sizeof(int), hipMemcpyHostToDevice));
@@ -544,14 +555,7 @@ static int repack(mz_handle* h, hipStream_t st = nullptr) {
                            h->d_flat, h->d_sm_srcb, h->d_sm_bias, h->sm_b_n);
     }
     MZ_TRY(h, hipGetLastError());
-    h->images_dirty = false;
     return 0;
-}
-
-// The packed images are rebuilt lazily, on the stream of the call that reads
-// them, after learner updates (the learner itself gathers from d_flat).
-static int ensure_images(mz_handle* h, hipStream_t st) {
-    return h->images_dirty ? repack(h, st) : 0;
 }
 
 // LDS of mz_unroll_small{1,2}: activations, records (+1 slack stage), staging
@@ -617,6 +621,11 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
     CK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess ? 0 : fail(h, "hipStreamCreate"));
     CK(build_plans(h));
     CK(build_pack_index(h));
+    auto al_i = [&](int** p, const std::vector<int>& v) -> int {
+        MZ_TRY(h, dalloc(h, p, v.size()));
+        MZ_TRY(h, hipMemcpy(*p, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+        return 0;
+    };
     {
         int r = build_small(h);
         if (r < 0) { g_create_error = h->err; mz_engine_destroy(h); return r; }
@@ -624,6 +633,9 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
         for (int ti = 0; ti < 3 && h->small_ok; ++ti) h->small_ok = h->sm_lds[ti] <= kLdsMax;
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) h->n_cu = prop.multiProcessorCount;
+        if (!h->small_ok) h->inv_small.assign(h->nflat, -1);
+        CK(al_i(&h->d_inv_tile, h->inv_tile));
+        CK(al_i(&h->d_inv_small, h->inv_small));
         const char* fk = std::getenv("MZ_SEARCH_KERNEL");
         if (fk) h->force_kernel = std::strcmp(fk, "tile16") == 0 ? 1 : std::strcmp(fk, "small") == 0 ? 2 : 0;
         const char* ft = std::getenv("MZ_SMALL_T");
@@ -680,6 +692,8 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
     {
         size_t oc[6] = {h->flat_off[0], h->flat_off[1], h->flat_off[2], h->nparams[0], h->nparams[1], h->nparams[2]};
         CK(al(&h->d_netoff, 6));
+        CK(al(&h->d_counter, 1));
+        CK(hipMemset(h->d_counter, 0, 4) == hipSuccess ? 0 : fail(h, "memset"));
         CK(hipMemcpy(h->d_netoff, oc, sizeof(oc), hipMemcpyHostToDevice) == hipSuccess ? 0 : fail(h, "copy"));
     }
     h->use_res = h->d_plan_sim_res != nullptr && std::getenv("MZ_NO_RESIDENT") == nullptr;
@@ -743,7 +757,6 @@ int mz_net_forward(mz_handle* h, int net, const float* x, int n, float* out0, fl
     const int o1 = net == MZ_NET_PRED ? A : 1;
     const int o1_off = net == MZ_NET_PRED ? h->lay.p_out : h->lay.r_out;
     float *dx = nullptr, *d0 = nullptr, *d1 = nullptr;
-    if (ensure_images(h, h->stream)) return -1;
     MZ_TRY(h, hipMalloc(&dx, (size_t)n * in_feat * 4));
     MZ_TRY(h, hipMalloc(&d0, (size_t)n * o0 * 4));
     MZ_TRY(h, hipMalloc(&d1, (size_t)n * o1 * 4));
@@ -787,7 +800,6 @@ int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* leg
     P.stamps = h->d_stamps;
 #endif
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    if (ensure_images(h, st)) return -1;     // after learner updates (stream-ordered with this search)
     const bool small = h->small_ok && h->force_kernel != 1 && (h->force_kernel == 2 || G <= 4 * h->n_cu);
     if (small) {
         const int T = h->force_T ? h->force_T : G <= h->n_cu ? 1 : G <= 2 * h->n_cu ? 2 : 4;
@@ -924,22 +936,27 @@ int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float*
     if (ensure_batch(h, B)) return -1;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     if (h->small_ok) {
-        // the search's stage schedule, T samples per workgroup, weights
-        // gathered from d_flat (no repack between learner steps)
+        // the search's stage schedule and register images, T samples per
+        // workgroup (ADAM keeps the images current)
         const int ti = B <= 4 * h->n_cu ? 0 : 1, T = ti + 1;
         const int* lay = h->sm_lay[ti];
         SmallUnrollParams U;
         U.B = B; U.K = K; U.A = A; U.H = h->H; U.plane = h->plane; U.obs_feat = h->obs_feat;
         U.obs = b->observation; U.actions = b->actions; U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
-        U.n_sim = h->sm_n_sim; U.n_root = h->sm_n_root; U.flat = h->d_flat; U.srcw = h->d_sm_srcw;
-        U.srcb = h->d_sm_srcb; U.rec = h->d_sm_rec[ti]; U.act_total = lay[0];
+        U.n_sim = h->sm_n_sim; U.n_root = h->sm_n_root; U.w_sim = h->d_sm_w;
+        U.w_root = h->d_sm_w + (size_t)h->sm_n_sim * SM_SLOTS * 256 * 16;
+        U.bias = h->d_sm_bias; U.rec = h->d_sm_rec[ti]; U.act_total = lay[0];
         U.x_rep = lay[1]; U.x_pred = lay[2]; U.x_dyn = lay[3]; U.h_out = lay[4]; U.v_out = lay[5];
         U.p_out = lay[6]; U.r_out = lay[7]; U.v_act = h->lay.v_act; U.r_act = h->lay.r_act;
+        U.stamps = nullptr;
+#ifdef MZ_STAMPS
+        if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * std::max(h->max_games, B)));
+        U.stamps = h->d_stamps;
+#endif
         void* args[] = {&U};
         MZ_TRY(h, hipLaunchKernel(ti == 0 ? (const void*)mz_unroll_small1 : (const void*)mz_unroll_small2,
                                   dim3((B + T - 1) / T), dim3(SM_THREADS), args, unroll_small_lds(h, ti), st));
     } else {
-        if (ensure_images(h, st)) return -1;
         UnrollParams U;
         U.B = B; U.K = K; U.A = A; U.H = h->H; U.plane = h->plane; U.obs_feat = h->obs_feat;
         U.obs = b->observation; U.actions = b->actions; U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
@@ -948,13 +965,10 @@ int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float*
                            (size_t)h->lay.total * 4, st, U);
     }
     float* lo = losses_dev ? losses_dev : h->d_loss;
-    hipLaunchKernelGGL(mz_loss_kernel, dim3(1), dim3(MZ_THREADS), 0, st, B, K, A, h->d_pv, h->d_pp,
-                       b->target_values, b->target_policies, b->gradient_scale, h->d_lterm, lo);
-    hipLaunchKernelGGL(mz_sqnorm_kernel, dim3(MZ_L2_BLOCKS, 3), dim3(MZ_THREADS), 0, st, h->d_flat,
-                       h->d_netoff, h->d_netoff + 3, h->d_sq);
-    hipLaunchKernelGGL(mz_l2_finish_kernel, dim3(1), dim3(64), 0, st, h->d_sq, lo);
     float* g = grad_dev ? grad_dev : h->d_grad;
-    hipLaunchKernelGGL(mz_grad_2theta_kernel, dim3(128), dim3(MZ_THREADS), 0, st, h->d_flat, g, h->nflat);
+    hipLaunchKernelGGL(mz_learner_grad_kernel, dim3(1 + 3 * MZ_L2_BLOCKS), dim3(MZ_THREADS), 0, st, B, K, A,
+                       h->lay.v_act, h->lay.r_act, h->d_pv, h->d_pp, h->d_pr, b->target_values, b->target_policies,
+                       b->gradient_scale, h->d_lterm, h->d_flat, h->d_netoff, g, h->d_sq, h->d_counter, lo);
     MZ_TRY(h, hipGetLastError());
     return 0;
 }
@@ -964,10 +978,10 @@ int mz_learner_apply_dev(mz_handle* h, const float* grad_dev, float grad_scale, 
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     const float* g = grad_dev ? grad_dev : h->d_grad;
     hipLaunchKernelGGL(mz_adam_kernel, dim3(128), dim3(MZ_THREADS), 0, st, h->d_flat, h->d_m, h->d_v, g,
-                       grad_scale, h->nflat, h->bp1, h->bp2, eta);
+                       grad_scale, h->nflat, h->bp1, h->bp2, eta, h->d_Wp, h->d_Bp, h->d_inv_tile, h->d_sm_w,
+                       h->d_sm_bias, h->d_inv_small);
     h->bp1 = h->bp1 * 0.9;                  // βp .= βp .* β
     h->bp2 = h->bp2 * 0.999;
-    h->images_dirty = true;                 // search / forward images rebuilt when next read
     MZ_TRY(h, hipGetLastError());
     return 0;
 }

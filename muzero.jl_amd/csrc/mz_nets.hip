@@ -78,122 +78,140 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_unroll_kernel(Unroll
         }
         __syncthreads();
         run_plan(P.plan_sim, P.Wp, P.Bp, act);
-        if (tid < MZ_TILE && t0 + tid < P.B) {
+        if (tid < MZ_TILE && t0 + tid < P.B) {        // raw outputs; read-outs in mz_learner_grad_kernel
             const int j = tid;
             const size_t b = (size_t)(t0 + j);
-            const float v = mz_post_act(P.lay.v_act, act[P.lay.v_out + j]);
-            float m = act[P.lay.p_out + j];
-            for (int k = 1; k < A; ++k) { const float x = act[P.lay.p_out + k * 16 + j]; m = m > x ? m : x; }
-            float s = 0.0f;
-            for (int k = 0; k < A; ++k) s = s + det_expf(act[P.lay.p_out + k * 16 + j] - m);
             for (int k = 0; k < A; ++k) {
-                const float p = det_expf(act[P.lay.p_out + k * 16 + j] - m) / s;
-                P.pp[(b * (K + 1) + i) * A + k] = p;
-                if (i == 1) P.pp[(b * (K + 1)) * A + k] = p;
+                const float x = act[P.lay.p_out + k * 16 + j];
+                P.pp[(b * (K + 1) + i) * A + k] = x;
+                if (i == 1) P.pp[(b * (K + 1)) * A + k] = x;
             }
+            const float v = act[P.lay.v_out + j];
             P.pv[b * (K + 1) + i] = v;
-            P.pr[b * (K + 1) + i] = mz_post_act(P.lay.r_act, act[P.lay.r_out + j]);
+            P.pr[b * (K + 1) + i] = act[P.lay.r_out + j];
             if (i == 1) { P.pv[b * (K + 1)] = v; P.pr[b * (K + 1)] = 0.0f; }
         }
         __syncthreads();
     }
 }
 
-// Losses of Learning.jl:261-288 (diagnostic in ref_semantics, Q11): one
-// workgroup.  The per-(sample, step) terms — squared value error and the
-// policy cross-entropy of that step — are computed by all threads into
-// `terms` (2 x B(K+1) floats, global scratch); then each sample folds its
-// steps in ascending k as the oracle does, and the cross-sample sums are
-// f64 (tolerance-checked, not bitwise).  out[0] value, out[2] policy.
-extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_loss_kernel(
-    int B, int K, int A, const float* pv, const float* pp, const float* tv, const float* tp,
-    const float* gscale, float* terms, float* out) {
-    __shared__ double red_v[MZ_THREADS], red_p[MZ_THREADS], red_c[MZ_THREADS];
-    const int tid = threadIdx.x;
-    const int n = B * (K + 1);
-    float* vsq = terms;
-    float* cet = terms + n;
-    for (int t = tid; t < n; t += blockDim.x) {
-        const float d = pv[t] - tv[t];
-        vsq[t] = d * d;
-        const float* yh = pp + (size_t)t * A;
-        const float* y = tp + (size_t)t * A;
-        float m = yh[0];
-        for (int i = 1; i < A; ++i) m = m > yh[i] ? m : yh[i];
-        float se = 0.0f;
-        for (int i = 0; i < A; ++i) se = se + det_expf(yh[i] - m);
-        const float ls = det_logf(se);
-        float ce = 0.0f;
-        for (int i = 0; i < A; ++i) ce = ce + y[i] * ((yh[i] - m) - ls);
-        cet[t] = ce;
-    }
-    __syncthreads();                            // block-scope: the terms are visible
-    double sv = 0.0, sg = 0.0, sc = 0.0;
-    for (int j = tid; j < B; j += blockDim.x) {
-        float s = 0.0f, c = 0.0f;
-        for (int k = 0; k <= K; ++k) {
-            s = s + vsq[(size_t)j * (K + 1) + k];
-            c = c + (-cet[(size_t)j * (K + 1) + k]);
-        }
-        sv += (double)(s / gscale[j]);
-        sc += (double)c;                        // Σ_k ce_k
-        sg += 1.0 / (double)gscale[j];          // Σ_j 1/g_j
-    }
-    red_v[tid] = sv; red_p[tid] = sg; red_c[tid] = sc;
-    __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-        if (tid < o) { red_v[tid] += red_v[tid + o]; red_p[tid] += red_p[tid + o]; red_c[tid] += red_c[tid + o]; }
-        __syncthreads();
-    }
-    if (tid == 0) {
-        out[0] = (float)(red_v[0] / (double)B);
-        out[1] = 0.0f;                          // intermediate_rewards = false (:276-280)
-        out[2] = (float)(red_c[0] * red_p[0] / ((double)B * (double)B));  // mean over (1,B,B), Q11
-    }
-}
-
-// Σθ² per net (sum(sqnorm, params), :287) in f64, deterministic: block b of
-// net `blockIdx.y` sums a fixed slice in a fixed order into part[net][b];
-// mz_l2_finish_kernel adds the partials in ascending b.
+// One launch after the unroll (Learning.jl:261-288, 380-393 in ref_semantics):
+//  * block 0 applies the read-outs to the raw unroll outputs — policy =
+//    softmax of the logits (max, det_expf, ascending sum, divide), value /
+//    reward = their activations — then the losses: per-(sample, step) terms
+//    by all threads, each sample folding its steps in ascending k, the
+//    cross-sample sums in f64 (tolerance-checked, not bitwise);
+//  * blocks 1.. (3 nets x MZ_L2_BLOCKS) sum θ² of a fixed slice in f64 and
+//    write ∇ = 2θ for it (Q11: only sum(sqnorm, params) depends on θ);
+//  * the last block to finish adds the partials in ascending order (the
+//    same order on every run) and resets the counter.
+// out: [0] value, [1] reward (0, intermediate_rewards = false), [2] policy,
+// [3..5] Σθ² of repr / pred / dyn.
 #define MZ_L2_BLOCKS 32
-extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_sqnorm_kernel(const float* flat, const size_t* off,
-                                                                          const size_t* cnt, double* part) {
-    __shared__ double red[MZ_THREADS];
-    const int net = blockIdx.y;
-    const float* P = flat + off[net];
-    const size_t n = cnt[net];
-    double s = 0.0;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        s += (double)P[i] * (double)P[i];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_grad_kernel(
+    int B, int K, int A, int v_act, int r_act, float* pv, float* pp, float* pr, const float* tv, const float* tp,
+    const float* gscale, float* terms, const float* flat, const size_t* netoff, float* G, double* part,
+    unsigned* counter, float* out) {
+    __shared__ double red_v[MZ_THREADS], red_p[MZ_THREADS], red_c[MZ_THREADS];
+    __shared__ bool last;
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0) {
+        const int n = B * (K + 1);
+        float* vsq = terms;
+        float* cet = terms + n;
+        for (int t = tid; t < n; t += blockDim.x) {
+            const float v = mz_post_act(v_act, pv[t]);
+            pv[t] = v;
+            pr[t] = mz_post_act(r_act, pr[t]);
+            float* yh = pp + (size_t)t * A;
+            float m = yh[0];
+            for (int i = 1; i < A; ++i) m = m > yh[i] ? m : yh[i];
+            float s = 0.0f;
+            for (int i = 0; i < A; ++i) s = s + det_expf(yh[i] - m);
+            for (int i = 0; i < A; ++i) yh[i] = det_expf(yh[i] - m) / s;
+            const float d = v - tv[t];
+            vsq[t] = d * d;
+            // logitcrossentropy of the probabilities (Q11's double softmax)
+            const float* y = tp + (size_t)t * A;
+            float m2 = yh[0];
+            for (int i = 1; i < A; ++i) m2 = m2 > yh[i] ? m2 : yh[i];
+            float se = 0.0f;
+            for (int i = 0; i < A; ++i) se = se + det_expf(yh[i] - m2);
+            const float ls = det_logf(se);
+            float ce = 0.0f;
+            for (int i = 0; i < A; ++i) ce = ce + y[i] * ((yh[i] - m2) - ls);
+            cet[t] = ce;
+        }
+        __syncthreads();                        // block-scope: the terms are visible
+        double sv = 0.0, sg = 0.0, sc = 0.0;
+        for (int j = tid; j < B; j += blockDim.x) {
+            float s = 0.0f, c = 0.0f;
+            for (int k = 0; k <= K; ++k) {
+                s = s + vsq[(size_t)j * (K + 1) + k];
+                c = c + (-cet[(size_t)j * (K + 1) + k]);
+            }
+            sv += (double)(s / gscale[j]);
+            sc += (double)c;                    // Σ_k ce_k
+            sg += 1.0 / (double)gscale[j];      // Σ_j 1/g_j
+        }
+        red_v[tid] = sv; red_p[tid] = sg; red_c[tid] = sc;
         __syncthreads();
-    }
-    if (threadIdx.x == 0) part[net * MZ_L2_BLOCKS + blockIdx.x] = red[0];
-}
-
-extern "C" __global__ void mz_l2_finish_kernel(const double* part, float* out) {
-    if (threadIdx.x < 3) {
+        for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+            if (tid < o) { red_v[tid] += red_v[tid + o]; red_p[tid] += red_p[tid + o]; red_c[tid] += red_c[tid + o]; }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            out[0] = (float)(red_v[0] / (double)B);
+            out[1] = 0.0f;                      // intermediate_rewards = false (:276-280)
+            out[2] = (float)(red_c[0] * red_p[0] / ((double)B * (double)B));  // mean over (1,B,B), Q11
+        }
+    } else {
+        const int net = (blockIdx.x - 1) / MZ_L2_BLOCKS, blk = (blockIdx.x - 1) % MZ_L2_BLOCKS;
+        const size_t off = netoff[net], n = netoff[3 + net];
         double s = 0.0;
-        for (int b = 0; b < MZ_L2_BLOCKS; ++b) s += part[threadIdx.x * MZ_L2_BLOCKS + b];
-        out[3 + threadIdx.x] = (float)s;
+        for (size_t i = (size_t)blk * blockDim.x + tid; i < n; i += (size_t)MZ_L2_BLOCKS * blockDim.x) {
+            const float x = flat[off + i];
+            s += (double)x * (double)x;
+            G[off + i] = x * 2.0f;
+        }
+        red_v[tid] = s;
+        __syncthreads();
+        for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+            if (tid < o) red_v[tid] += red_v[tid + o];
+            __syncthreads();
+        }
+        if (tid == 0) part[net * MZ_L2_BLOCKS + blk] = red_v[0];
     }
-}
-
-// gradient of the ref_semantics loss: only sum(sqnorm, params) depends on
-// the parameters (Q11), so ∇ = 2θ exactly.
-extern "C" __global__ void mz_grad_2theta_kernel(const float* P, float* G, size_t n) {
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        G[i] = P[i] * 2.0f;
+    // last block out folds the Σθ² partials in a fixed order
+    if (tid == 0) {
+        __threadfence();
+        last = atomicAdd(counter, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && tid < 3) {
+        __threadfence();
+        double s = 0.0;
+        for (int b = 0; b < MZ_L2_BLOCKS; ++b) s += __hip_atomic_load(part + tid * MZ_L2_BLOCKS + b, __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT);
+        out[3 + tid] = (float)s;
+        if (tid == 0) *counter = 0u;
+    }
 }
 
 // Flux 0.12 apply!(ADAM) + WeightDecay(0) + `x .-= Δ` (Learning.jl:395-397).
 // grad = G[i] * gscale (gscale = 1/world after an all-reduce sum; exact for
-// power-of-two world sizes).  bp = (β1^t, β2^t) of the current step.
+// power-of-two world sizes).  bp = (β1^t, β2^t) of the current step.  The
+// new value is also scattered into the search / unroll images through the
+// inverse maps (each parameter has one position in each image), so the
+// images never need a repack after a learner step.
+__device__ __forceinline__ void mz_scatter(float x, int code, float* w, float* b) {
+    if (code >= 0) w[code] = x;
+    else if (code <= -2) b[-code - 2] = x;
+}
+
 extern "C" __global__ void mz_adam_kernel(float* P, float* M, float* V, const float* G, float gscale,
-                                          size_t n, double bp1, double bp2, double eta) {
+                                          size_t n, double bp1, double bp2, double eta, float* Wp, float* Bp,
+                                          const int* inv_tile, float* smw, float* smb, const int* inv_small) {
     const double b1 = 0.9, b2 = 0.999, eps = 1e-8;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const float g = G[i] * gscale;
@@ -202,7 +220,10 @@ extern "C" __global__ void mz_adam_kernel(float* P, float* M, float* V, const fl
         const float v = (float)(b2 * (double)V[i] + (1.0 - b2) * (double)g2);
         M[i] = m; V[i] = v;
         const float d = (float)((double)m / (1.0 - bp1) / (sqrt((double)v / (1.0 - bp2)) + eps) * eta);
-        P[i] = P[i] - d;
+        const float x = P[i] - d;
+        P[i] = x;
+        mz_scatter(x, inv_tile[i], Wp, Bp);
+        mz_scatter(x, inv_small[i], smw, smb);
     }
 }
 

@@ -152,31 +152,6 @@ __device__ __noinline__ int sm_select_action(const int* cnt, uint32_t legal, int
 }
 
 
-// Same register image, gathered from the Flux-order parameters through the
-// host index map (the learner updates `flat` every step; no repack).
-template <int NMAX>
-__device__ __forceinline__ void sm_load_gather(int n, const float* flat, const int* srcw, float (&wr)[NMAX][16]) {
-    const int tid = threadIdx.x;
-    const int sr = sm_slot_row(tid), sl = sr >> 6, r = sr & 63, q = (tid >> 4) & 3;
-#pragma unroll
-    for (int k = 0; k < NMAX; ++k) {
-        if (k < n) {
-            const int4* src = reinterpret_cast<const int4*>(srcw + (((size_t)k * SM_SLOTS + sl) * 256 + q * 64 + r) * 16);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int4 ix = src[i];
-                wr[k][4 * i] = ix.x >= 0 ? flat[ix.x] : 0.0f;
-                wr[k][4 * i + 1] = ix.y >= 0 ? flat[ix.y] : 0.0f;
-                wr[k][4 * i + 2] = ix.z >= 0 ? flat[ix.z] : 0.0f;
-                wr[k][4 * i + 3] = ix.w >= 0 ? flat[ix.w] : 0.0f;
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) wr[k][i] = 0.0f;
-        }
-    }
-}
-
 template <int T>
 __device__ __forceinline__ void small_body(const SmallParams& P) {
 #ifdef MZ_STAMPS
@@ -414,36 +389,40 @@ extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_search_small4(Sma
 // dynamics(2h_{i-1} ⊕ a_{i-1}/|A|) on the search's stage schedule.  Stored:
 // pv/pp at i (and at 0 for i = 1) = prediction of h_{i-1}; pr at i = reward
 // of step i, pr at 0 = 0.  Policy = softmax of the logits in the oracle's
-// order; value / reward with their read-out activations.
+// order; value / reward with their read-out activations — applied by the
+// loss kernel, which visits every (sample, step) pair in parallel.
 template <int T>
 __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
+#ifdef MZ_STAMPS
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int K = P.K, A = P.A, H = P.H;
     const int nrec = P.n_sim + P.n_root;
     float* act = smem;
     int* rec = reinterpret_cast<int*>(act + P.act_total);
-    float* stg = reinterpret_cast<float*>(rec + (nrec + 1) * SM_REC_INTS);      // [4][16] staging
     const int tid = threadIdx.x;
     const int tile0 = blockIdx.x * T;
-    const int g = tid >> 4, a = tid & 15;
     for (int i = tid; i < P.act_total; i += SM_THREADS) act[i] = 0.0f;
     for (int i = tid; i < nrec * SM_REC_INTS; i += SM_THREADS) rec[i] = P.rec[i];
     __syncthreads();
-    for (int i = tid; i < nrec * 128; i += SM_THREADS) {
-        const int sb = P.srcb[i];
-        rec[4 * i + 3] = __float_as_int(sb >= 0 ? P.flat[sb] : 0.0f);
-    }
+    for (int i = tid; i < nrec * 128; i += SM_THREADS) rec[4 * i + 3] = __float_as_int(P.bias[i]);
     for (int i = tid; i < T * P.obs_feat; i += SM_THREADS) {
         const int gl = i / P.obs_feat, k = i - gl * P.obs_feat;
         act[P.x_rep + k * T + gl] = tile0 + gl < P.B ? P.obs[(size_t)(tile0 + gl) * P.obs_feat + k] : 0.0f;
     }
     __syncthreads();
+    SM_STAMP(0);                                   // setup: records, bias gather, inputs
     const int4* rec_sim = reinterpret_cast<const int4*>(rec) + sm_slot_row(tid);
     const int4* rec_root = rec_sim + P.n_sim * (SM_SLOTS * 64);
     float wr[SM_MAX_SIM][16];
-    sm_load_gather<SM_MAX_SIM>(P.n_root, P.flat, P.srcw + (size_t)P.n_sim * SM_SLOTS * 256 * 16, wr);
+    sm_load<SM_MAX_SIM>(P.n_root, P.w_root, wr);
     sm_run<T, SM_MAX_SIM>(P.n_root, wr, rec_root, act);
-    sm_load_gather<SM_MAX_SIM>(P.n_sim, P.flat, P.srcw, wr);
+    SM_STAMP(1);                                   // repr gather + stages
+    sm_load<SM_MAX_SIM>(P.n_sim, P.w_sim, wr);
+    __syncthreads();
+    SM_STAMP(2);                                   // sim gather
     for (int i = 1; i <= K; ++i) {
         for (int t = tid; t < T * H; t += SM_THREADS) {          // make_dynamics_input (:293-304)
             const int gl = t / H, k = t - gl * H;
@@ -457,29 +436,43 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
             act[P.x_dyn + (H + k) * T + gl] = b < P.B ? P.actions[(size_t)b * (K + 1) + (i - 1)] / (float)A : 0.0f;
         }
         __syncthreads();
+        SM_STAMP(3);                               // step inputs
         sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act);
-        const int b = tile0 + g;
-        if (tid < 16 * T && b < P.B) {
-            // softmax over the A logits: max, exp, sum in ascending order, divide
-            const float x = a < A ? act[P.p_out + a * T + g] : -INFINITY;
-            const float m = g16_max(x);
-            const float ex = a < A ? det_expf(x - m) : 0.0f;
-            const float sum = g16_seqsum(ex, A, stg + 16 * g, a);
-            if (a < A) {
-                const float p = ex / sum;
-                P.pp[((size_t)b * (K + 1) + i) * A + a] = p;
-                if (i == 1) P.pp[((size_t)b * (K + 1)) * A + a] = p;
+        SM_STAMP(4);                               // the 8 stages
+        // raw outputs (logits, value, reward before their read-out
+        // activations); mz_learner_post_kernel applies softmax / tanh for all
+        // (sample, step) pairs in parallel
+        for (int t = tid; t < T * (A + 2); t += SM_THREADS) {
+            const int gl = t / (A + 2), c = t - gl * (A + 2);
+            const int bb = tile0 + gl;
+            if (bb >= P.B) continue;
+            float x;
+            float* dst;
+            float* dst0 = nullptr;
+            if (c < A) {
+                x = act[P.p_out + c * T + gl];
+                dst = P.pp + ((size_t)bb * (K + 1) + i) * A + c;
+                if (i == 1) dst0 = P.pp + ((size_t)bb * (K + 1)) * A + c;
+            } else if (c == A) {
+                x = act[P.v_out + gl];
+                dst = P.pv + (size_t)bb * (K + 1) + i;
+                if (i == 1) dst0 = P.pv + (size_t)bb * (K + 1);
+            } else {
+                x = act[P.r_out + gl];
+                dst = P.pr + (size_t)bb * (K + 1) + i;
+                if (i == 1) P.pr[(size_t)bb * (K + 1)] = 0.0f;   // raw 0: every read-out maps 0 to 0
             }
-        } else if (tid >= 64 && tid < 64 + T && tile0 + (tid - 64) < P.B) {
-            const int gl = tid - 64, bb = tile0 + gl;
-            const float v = mz_post_act(P.v_act, act[P.v_out + gl]);
-            P.pv[(size_t)bb * (K + 1) + i] = v;
-            P.pr[(size_t)bb * (K + 1) + i] = mz_post_act(P.r_act, act[P.r_out + gl]);
-            if (i == 1) { P.pv[(size_t)bb * (K + 1)] = v; P.pr[(size_t)bb * (K + 1)] = 0.0f; }
+            *dst = x;
+            if (dst0) *dst0 = x;
         }
         // the next step's input copy reads h_out and writes x_pred / x_dyn,
         // which nothing above reads: no barrier needed here
+        SM_STAMP(5);                               // raw output writes
     }
+#ifdef MZ_STAMPS
+    if (threadIdx.x == 0 && P.stamps)
+        for (int i = 0; i < 8; ++i) P.stamps[blockIdx.x * 8 + i] = st_acc[i];
+#endif
 }
 
 extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small1(SmallUnrollParams P) { unroll_body<1>(P); }

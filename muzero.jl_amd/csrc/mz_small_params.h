@@ -40,20 +40,20 @@ struct SmallParams {
 };
 
 // Learner unroll on the small-kernel schedule (mz_unroll_small*): T samples
-// per workgroup; weights gathered from the Flux-order parameters through the
-// image index maps (no repack between learner steps).
+// per workgroup, the search's register images (kept current by ADAM).
 struct SmallUnrollParams {
     int B, K, A, H, plane, obs_feat;
     const float* obs;      // (obs_feat, B)
     const float* actions;  // (K+1, B) float action ids
     float* pv; float* pp; float* pr;   // (K+1,B), (A,K+1,B), (K+1,B)
     int n_sim, n_root;
-    const float* flat;     // Flux-order parameters
-    const int* srcw;       // weight image index map [n_sim + n_root][slot][q*64 + row][16] (-1 = 0)
-    const int* srcb;       // bias image index map [n_sim + n_root][slot][64]
+    const float* w_sim;    // [n_sim][slot][q*64 + row][16] register image (as the search)
+    const float* w_root;   // [n_root][slot][q*64 + row][16]
+    const float* bias;     // [n_sim + n_root][slot][64]
     const int* rec;        // [n_sim + n_root][SM_REC_INTS]
     int act_total;
     int x_rep, x_pred, x_dyn, h_out, v_out, p_out, r_out;
     int v_act, r_act;
+    unsigned long long* stamps;   // -DMZ_STAMPS builds: [blocks][8] phase ticks (else unused)
 };
 
