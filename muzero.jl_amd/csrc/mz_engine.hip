@@ -966,7 +966,8 @@ int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float*
     }
     float* lo = losses_dev ? losses_dev : h->d_loss;
     float* g = grad_dev ? grad_dev : h->d_grad;
-    hipLaunchKernelGGL(mz_learner_grad_kernel, dim3(1 + 3 * MZ_L2_BLOCKS), dim3(MZ_THREADS), 0, st, B, K, A,
+    const int nlb = (B * (K + 1) + MZ_THREADS / 16 - 1) / (MZ_THREADS / 16);
+    hipLaunchKernelGGL(mz_learner_grad_kernel, dim3(nlb + 3 * MZ_L2_BLOCKS), dim3(MZ_THREADS), 0, st, B, K, A,
                        h->lay.v_act, h->lay.r_act, h->d_pv, h->d_pp, h->d_pr, b->target_values, b->target_policies,
                        b->gradient_scale, h->d_lterm, h->d_flat, h->d_netoff, g, h->d_sq, h->d_counter, lo);
     MZ_TRY(h, hipGetLastError());

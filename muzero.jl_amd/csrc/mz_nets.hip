@@ -3,6 +3,7 @@
 // ref_semantics: K-step unroll (Q10), losses (:261-288), gradient 2θ (Q11),
 // ADAM (Flux 0.12 ADAMW()[1]) and re-packing of the MFMA weight image.
 #include "mz_mlp_device.h"
+#include "mz_tree_device.h"
 
 // One plan over tiles of 16 samples: x (in_feat, n) column-major in HBM ->
 // LDS -> plan -> out0 (o0 rows) / out1 (o1 rows, softmaxed if sm1).
@@ -96,15 +97,17 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_unroll_kernel(Unroll
 }
 
 // One launch after the unroll (Learning.jl:261-288, 380-393 in ref_semantics):
-//  * block 0 applies the read-outs to the raw unroll outputs — policy =
-//    softmax of the logits (max, det_expf, ascending sum, divide), value /
-//    reward = their activations — then the losses: per-(sample, step) terms
-//    by all threads, each sample folding its steps in ascending k, the
-//    cross-sample sums in f64 (tolerance-checked, not bitwise);
-//  * blocks 1.. (3 nets x MZ_L2_BLOCKS) sum θ² of a fixed slice in f64 and
-//    write ∇ = 2θ for it (Q11: only sum(sqnorm, params) depends on θ);
-//  * the last block to finish adds the partials in ascending order (the
-//    same order on every run) and resets the counter.
+//  * blocks [0, nlb): one 16-lane group per (sample, step) t, lane a = action
+//    a: read-outs on the raw unroll outputs — policy = softmax of the logits
+//    (max, det_expf, ascending sum, divide), value / reward = their
+//    activations — then the step's terms: squared value error and the
+//    logitcrossentropy of the probabilities (Q11's double softmax), every
+//    sum in ascending action order (g16_seqsum);
+//  * blocks [nlb, nlb + 3·MZ_L2_BLOCKS): θ² of a fixed slice summed in f64,
+//    and ∇ = 2θ written for it (Q11: only sum(sqnorm, params) depends on θ);
+//  * the last block to finish folds each sample's steps in ascending k, the
+//    cross-sample sums in f64 (tolerance-checked, not bitwise), and the Σθ²
+//    partials in ascending order, then resets the counter.
 // out: [0] value, [1] reward (0, intermediate_rewards = false), [2] policy,
 // [3..5] Σθ² of repr / pred / dyn.
 #define MZ_L2_BLOCKS 32
@@ -113,63 +116,46 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_grad_kernel(
     const float* gscale, float* terms, const float* flat, const size_t* netoff, float* G, double* part,
     unsigned* counter, float* out) {
     __shared__ double red_v[MZ_THREADS], red_p[MZ_THREADS], red_c[MZ_THREADS];
+    __shared__ float stg[MZ_THREADS];
     __shared__ bool last;
     const int tid = threadIdx.x;
-    if (blockIdx.x == 0) {
-        const int n = B * (K + 1);
-        float* vsq = terms;
-        float* cet = terms + n;
-        for (int t = tid; t < n; t += blockDim.x) {
-            const float v = mz_post_act(v_act, pv[t]);
-            pv[t] = v;
-            pr[t] = mz_post_act(r_act, pr[t]);
+    const int n = B * (K + 1);
+    const int nlb = (n + MZ_THREADS / 16 - 1) / (MZ_THREADS / 16);
+    float* vsq = terms;
+    float* cet = terms + n;
+    if ((int)blockIdx.x < nlb) {
+        const int t = blockIdx.x * (MZ_THREADS / 16) + (tid >> 4), a = tid & 15;
+        float* st = stg + (tid & ~15);
+        if (t < n) {                            // whole 16-lane groups are in or out
+            const bool in = a < A;
             float* yh = pp + (size_t)t * A;
-            float m = yh[0];
-            for (int i = 1; i < A; ++i) m = m > yh[i] ? m : yh[i];
-            float s = 0.0f;
-            for (int i = 0; i < A; ++i) s = s + det_expf(yh[i] - m);
-            for (int i = 0; i < A; ++i) yh[i] = det_expf(yh[i] - m) / s;
-            const float d = v - tv[t];
-            vsq[t] = d * d;
-            // logitcrossentropy of the probabilities (Q11's double softmax)
-            const float* y = tp + (size_t)t * A;
-            float m2 = yh[0];
-            for (int i = 1; i < A; ++i) m2 = m2 > yh[i] ? m2 : yh[i];
-            float se = 0.0f;
-            for (int i = 0; i < A; ++i) se = se + det_expf(yh[i] - m2);
+            const float x = in ? yh[a] : -INFINITY;
+            const float m = g16_max(x);
+            const float e = in ? det_expf(x - m) : 0.0f;
+            const float s = g16_seqsum(e, A, st, a);
+            const float p = in ? e / s : -INFINITY;
+            if (in) yh[a] = p;
+            const float m2 = g16_max(p);
+            const float e2 = in ? det_expf(p - m2) : 0.0f;
+            const float se = g16_seqsum(e2, A, st, a);
             const float ls = det_logf(se);
-            float ce = 0.0f;
-            for (int i = 0; i < A; ++i) ce = ce + y[i] * ((yh[i] - m2) - ls);
-            cet[t] = ce;
-        }
-        __syncthreads();                        // block-scope: the terms are visible
-        double sv = 0.0, sg = 0.0, sc = 0.0;
-        for (int j = tid; j < B; j += blockDim.x) {
-            float s = 0.0f, c = 0.0f;
-            for (int k = 0; k <= K; ++k) {
-                s = s + vsq[(size_t)j * (K + 1) + k];
-                c = c + (-cet[(size_t)j * (K + 1) + k]);
+            const float term = in ? tp[(size_t)t * A + a] * ((p - m2) - ls) : 0.0f;
+            const float ce = g16_seqsum(term, A, st, a);
+            if (a == 0) {
+                const float v = mz_post_act(v_act, pv[t]);
+                pv[t] = v;
+                pr[t] = mz_post_act(r_act, pr[t]);
+                const float d = v - tv[t];
+                vsq[t] = d * d;
+                cet[t] = ce;
             }
-            sv += (double)(s / gscale[j]);
-            sc += (double)c;                    // Σ_k ce_k
-            sg += 1.0 / (double)gscale[j];      // Σ_j 1/g_j
-        }
-        red_v[tid] = sv; red_p[tid] = sg; red_c[tid] = sc;
-        __syncthreads();
-        for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-            if (tid < o) { red_v[tid] += red_v[tid + o]; red_p[tid] += red_p[tid + o]; red_c[tid] += red_c[tid + o]; }
-            __syncthreads();
-        }
-        if (tid == 0) {
-            out[0] = (float)(red_v[0] / (double)B);
-            out[1] = 0.0f;                      // intermediate_rewards = false (:276-280)
-            out[2] = (float)(red_c[0] * red_p[0] / ((double)B * (double)B));  // mean over (1,B,B), Q11
         }
     } else {
-        const int net = (blockIdx.x - 1) / MZ_L2_BLOCKS, blk = (blockIdx.x - 1) % MZ_L2_BLOCKS;
-        const size_t off = netoff[net], n = netoff[3 + net];
+        const int nb = blockIdx.x - nlb;
+        const int net = nb / MZ_L2_BLOCKS, blk = nb % MZ_L2_BLOCKS;
+        const size_t off = netoff[net], cnt = netoff[3 + net];
         double s = 0.0;
-        for (size_t i = (size_t)blk * blockDim.x + tid; i < n; i += (size_t)MZ_L2_BLOCKS * blockDim.x) {
+        for (size_t i = (size_t)blk * blockDim.x + tid; i < cnt; i += (size_t)MZ_L2_BLOCKS * blockDim.x) {
             const float x = flat[off + i];
             s += (double)x * (double)x;
             G[off + i] = x * 2.0f;
@@ -182,19 +168,43 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_grad_kernel(
         }
         if (tid == 0) part[net * MZ_L2_BLOCKS + blk] = red_v[0];
     }
-    // last block out folds the Σθ² partials in a fixed order
+    // the last block out folds
+    __syncthreads();
     if (tid == 0) {
         __threadfence();
         last = atomicAdd(counter, 1u) == gridDim.x - 1;
     }
     __syncthreads();
-    if (last && tid < 3) {
-        __threadfence();
+    if (!last) return;
+    __threadfence();
+    double sv = 0.0, sg = 0.0, sc = 0.0;
+    for (int j = tid; j < B; j += blockDim.x) {
+        float s = 0.0f, c = 0.0f;
+        for (int k = 0; k <= K; ++k) {
+            s = s + __hip_atomic_load(vsq + (size_t)j * (K + 1) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            c = c + (-__hip_atomic_load(cet + (size_t)j * (K + 1) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
+        sv += (double)(s / gscale[j]);
+        sc += (double)c;                        // Σ_k ce_k
+        sg += 1.0 / (double)gscale[j];          // Σ_j 1/g_j
+    }
+    red_v[tid] = sv; red_p[tid] = sg; red_c[tid] = sc;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if (tid < o) { red_v[tid] += red_v[tid + o]; red_p[tid] += red_p[tid + o]; red_c[tid] += red_c[tid + o]; }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        out[0] = (float)(red_v[0] / (double)B);
+        out[1] = 0.0f;                          // intermediate_rewards = false (:276-280)
+        out[2] = (float)(red_c[0] * red_p[0] / ((double)B * (double)B));  // mean over (1,B,B), Q11
+        *counter = 0u;
+    }
+    if (tid < 3) {
         double s = 0.0;
-        for (int b = 0; b < MZ_L2_BLOCKS; ++b) s += __hip_atomic_load(part + tid * MZ_L2_BLOCKS + b, __ATOMIC_RELAXED,
-                                                                       __HIP_MEMORY_SCOPE_AGENT);
+        for (int b = 0; b < MZ_L2_BLOCKS; ++b)
+            s += __hip_atomic_load(part + tid * MZ_L2_BLOCKS + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         out[3 + tid] = (float)s;
-        if (tid == 0) *counter = 0u;
     }
 }
 
