@@ -935,10 +935,14 @@ int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float*
     if (B < 1) return fail(h, "batch_size must be >= 1");
     if (ensure_batch(h, B)) return -1;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    if (h->small_ok) {
+    const int ti_u = B <= 4 * h->n_cu ? 0 : 1;
+    // one item per thread in the unroll's per-step loops; a/|A| staging of 64 floats
+    const bool small_unroll = h->small_ok && (ti_u + 1) * h->H <= 256 && (ti_u + 1) * h->plane <= 256 &&
+                              (ti_u + 1) * (A + 2) <= SM_THREADS && (ti_u + 1) * (K + 1) <= 64;
+    if (small_unroll) {
         // the search's stage schedule and register images, T samples per
         // workgroup (ADAM keeps the images current)
-        const int ti = B <= 4 * h->n_cu ? 0 : 1, T = ti + 1;
+        const int ti = ti_u, T = ti + 1;
         const int* lay = h->sm_lay[ti];
         SmallUnrollParams U;
         U.B = B; U.K = K; U.A = A; U.H = h->H; U.plane = h->plane; U.obs_feat = h->obs_feat;

@@ -125,13 +125,16 @@ __device__ __forceinline__ void sm_run(int n, const float (&wr)[NMAX][16], const
 
 // Weights of this thread's (slot, row, quarter) for stages 0..n-1 from the
 // host image [stage][slot][q*64 + row][16].
+// Stages [k0, k1) only (others untouched: sm_run never reads stages >= n,
+// so the representation's free registers can be filled with sim stages
+// while it runs).
 template <int NMAX>
-__device__ __forceinline__ void sm_load(int n, const float* W, float (&wr)[NMAX][16]) {
+__device__ __forceinline__ void sm_load(int k0, int k1, const float* W, float (&wr)[NMAX][16]) {
     const int tid = threadIdx.x;
     const int sr = sm_slot_row(tid), sl = sr >> 6, r = sr & 63, q = (tid >> 4) & 3;
 #pragma unroll
     for (int k = 0; k < NMAX; ++k) {
-        if (k < n) {
+        if (k >= k0 && k < k1) {
             const float4* src = reinterpret_cast<const float4*>(
                 W + (((size_t)k * SM_SLOTS + sl) * 256 + q * 64 + r) * 16);
 #pragma unroll
@@ -139,9 +142,6 @@ __device__ __forceinline__ void sm_load(int n, const float* W, float (&wr)[NMAX]
                 const float4 v = src[i];
                 wr[k][4 * i] = v.x; wr[k][4 * i + 1] = v.y; wr[k][4 * i + 2] = v.z; wr[k][4 * i + 3] = v.w;
             }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) wr[k][i] = 0.0f;
         }
     }
 }
@@ -203,6 +203,12 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     const int4* rec_sim = reinterpret_cast<const int4*>(rec) + sm_slot_row(tid);
     const int4* rec_root = rec_sim + P.n_sim * (SM_SLOTS * 64);
 
+    // ---- weight-image loads first: in flight under the setup copies.  The
+    // representation (SelfPlay.jl:234) runs on its own schedule; the sim
+    // stages it leaves free are preloaded, the rest reloaded after it.
+    float wr[SM_MAX_SIM][16];
+    sm_load<SM_MAX_SIM>(0, P.n_root, P.w_root, wr);
+    sm_load<SM_MAX_SIM>(P.n_root, P.n_sim, P.w_sim, wr);
     for (int i = tid; i < P.act_total; i += SM_THREADS) act[i] = 0.0f;
     for (int i = tid; i < S + 2; i += SM_THREADS) { l_pbc[i] = P.pbc_tab[i]; l_sqrt[i] = P.sqrt_tab[i]; }
     if (tid < A) l_aval[tid] = P.aval_tab[tid];
@@ -229,10 +235,6 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     }
     __syncthreads();
 
-    // ---- representation (SelfPlay.jl:234): its own schedule; the weight
-    // registers are then reloaded with the prediction ‖ dynamics weights
-    float wr[SM_MAX_SIM][16];
-    sm_load<SM_MAX_SIM>(P.n_root, P.w_root, wr);
     // the root's exploration noise depends only on the legal set: drawn here,
     // lane-parallel, while the weight loads are in flight
     if (P.exploration && active)
@@ -246,7 +248,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         act[P.x_pred + k * T + gl] = h;
     }
     // prediction ‖ dynamics weights: resident for the whole search
-    sm_load<SM_MAX_SIM>(P.n_sim, P.w_sim, wr);
+    sm_load<SM_MAX_SIM>(0, P.n_root < P.n_sim ? P.n_root : P.n_sim, P.w_sim, wr);
     __syncthreads();
     // prediction(h) for the root (:239); the dynamics half runs on zeros, unused
     sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act);
@@ -402,8 +404,18 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
     const int nrec = P.n_sim + P.n_root;
     float* act = smem;
     int* rec = reinterpret_cast<int*>(act + P.act_total);
+    float* aval = reinterpret_cast<float*>(rec + (nrec + 1) * SM_REC_INTS);    // [T][K+1] a/|A| per step
     const int tid = threadIdx.x;
     const int tile0 = blockIdx.x * T;
+    // per-thread item of the per-step loops (each has < SM_THREADS items)
+    const int h_gl = tid / H, h_k = tid - h_gl * H;                   // h copy: tid < T*H
+    const int pl_t = tid - 256;                                       // a/|A| plane: threads 256..
+    const int pl_gl = pl_t >= 0 ? pl_t / P.plane : 0, pl_k = pl_t - pl_gl * P.plane;
+    const int o_gl = tid / (A + 2), o_c = tid - o_gl * (A + 2);      // raw outputs: tid < T*(A+2)
+    // weight-image loads first: in flight under the setup copies
+    float wr[SM_MAX_SIM][16];
+    sm_load<SM_MAX_SIM>(0, P.n_root, P.w_root, wr);
+    sm_load<SM_MAX_SIM>(P.n_root, P.n_sim, P.w_sim, wr);   // sim stages the representation leaves free
     for (int i = tid; i < P.act_total; i += SM_THREADS) act[i] = 0.0f;
     for (int i = tid; i < nrec * SM_REC_INTS; i += SM_THREADS) rec[i] = P.rec[i];
     __syncthreads();
@@ -412,40 +424,37 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
         const int gl = i / P.obs_feat, k = i - gl * P.obs_feat;
         act[P.x_rep + k * T + gl] = tile0 + gl < P.B ? P.obs[(size_t)(tile0 + gl) * P.obs_feat + k] : 0.0f;
     }
+    for (int i = tid; i < T * (K + 1); i += SM_THREADS) {          // make_dynamics_input's a/|A| (:294)
+        const int gl = i / (K + 1), k = i - gl * (K + 1);
+        aval[i] = tile0 + gl < P.B ? P.actions[(size_t)(tile0 + gl) * (K + 1) + k] / (float)A : 0.0f;
+    }
     __syncthreads();
     SM_STAMP(0);                                   // setup: records, bias gather, inputs
     const int4* rec_sim = reinterpret_cast<const int4*>(rec) + sm_slot_row(tid);
     const int4* rec_root = rec_sim + P.n_sim * (SM_SLOTS * 64);
-    float wr[SM_MAX_SIM][16];
-    sm_load<SM_MAX_SIM>(P.n_root, P.w_root, wr);
     sm_run<T, SM_MAX_SIM>(P.n_root, wr, rec_root, act);
-    SM_STAMP(1);                                   // repr gather + stages
-    sm_load<SM_MAX_SIM>(P.n_sim, P.w_sim, wr);
+    SM_STAMP(1);                                   // repr stages
+    sm_load<SM_MAX_SIM>(0, P.n_root < P.n_sim ? P.n_root : P.n_sim, P.w_sim, wr);
     __syncthreads();
     SM_STAMP(2);                                   // sim gather
     for (int i = 1; i <= K; ++i) {
-        for (int t = tid; t < T * H; t += SM_THREADS) {          // make_dynamics_input (:293-304)
-            const int gl = t / H, k = t - gl * H;
-            const float h = act[P.h_out + k * T + gl];
-            act[P.x_pred + k * T + gl] = h;
-            act[P.x_dyn + k * T + gl] = h * 2.0f;
-        }
-        for (int t = tid; t < T * P.plane; t += SM_THREADS) {
-            const int gl = t / P.plane, k = t - gl * P.plane;
-            const int b = tile0 + gl;
-            act[P.x_dyn + (H + k) * T + gl] = b < P.B ? P.actions[(size_t)b * (K + 1) + (i - 1)] / (float)A : 0.0f;
+        if (tid < T * H) {                                         // make_dynamics_input (:293-304)
+            const float h = act[P.h_out + h_k * T + h_gl];
+            act[P.x_pred + h_k * T + h_gl] = h;
+            act[P.x_dyn + h_k * T + h_gl] = h * 2.0f;
+        } else if (pl_t >= 0 && pl_t < T * P.plane) {
+            act[P.x_dyn + (H + pl_k) * T + pl_gl] = aval[pl_gl * (K + 1) + (i - 1)];
         }
         __syncthreads();
         SM_STAMP(3);                               // step inputs
         sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act);
         SM_STAMP(4);                               // the 8 stages
         // raw outputs (logits, value, reward before their read-out
-        // activations); mz_learner_post_kernel applies softmax / tanh for all
+        // activations); mz_learner_grad_kernel applies softmax / tanh for all
         // (sample, step) pairs in parallel
-        for (int t = tid; t < T * (A + 2); t += SM_THREADS) {
-            const int gl = t / (A + 2), c = t - gl * (A + 2);
+        if (tid < T * (A + 2) && tile0 + o_gl < P.B) {
+            const int gl = o_gl, c = o_c;
             const int bb = tile0 + gl;
-            if (bb >= P.B) continue;
             float x;
             float* dst;
             float* dst0 = nullptr;
