@@ -79,6 +79,29 @@ typedef struct mz_ffhp {
     int32_t reward_activation;       /* MZ_ACT_TANH */
 } mz_ffhp;
 
+/* ResNetHP — src/Constructors.jl:77-90, the residual conv towers of
+ * Learning.jl:148-255.  The reference's ResNet constructors cannot run
+ * (SURVEY §2.1 Q12); the engine builds their intended architecture
+ * (DESIGN.md §9): stride-1 zero-padded Conv (Flux convolution, kernel
+ * flipped), BatchNorm in test mode (the reference's forward runs outside the
+ * pullback) with its running statistics, residual blocks
+ * conv-BN-relu-conv-BN-(+x)-relu, 1x1 convs in prediction / dynamics, and the
+ * heads' Dense layers of width `width_hidden` (a field the reference reads
+ * from ResNetHP but never declares).                                       */
+typedef struct mz_resnet_hp {
+    int32_t num_blocks;              /* residual blocks per tower */
+    int32_t num_filters;             /* nf */
+    int32_t conv_kernel_size[2];     /* representation kernel (odd), e.g. (3,3) */
+    int32_t num_second_head_filters; /* 2: policy head 1x1 conv channels */
+    int32_t num_first_head_filters;  /* 1: value / reward head 1x1 conv channels */
+    float batch_norm_momentum;       /* 0.6 (unused in test mode) */
+    int32_t downsample;              /* false (the Atari downsampler is not built) */
+    int32_t depth_policy;            /* hidden Dense layers (the reference reuses depth_value, kept) */
+    int32_t depth_value;             /* hidden Dense layers of the value / reward / policy heads */
+    int32_t width_hidden;            /* 64: Dense width of the heads */
+    int32_t reward_activation;       /* MZ_ACT_TANH */
+} mz_resnet_hp;
+
 /* The three networks of the `NNs` NamedTuple (SelfPlay.jl:230). */
 enum { MZ_NET_REPR = 0, MZ_NET_PRED = 1, MZ_NET_DYN = 2 };
 
@@ -89,6 +112,10 @@ typedef struct mz_handle mz_handle;
  * batch G of mz_mcts_search; `rng_seed` keys every Philox stream.         */
 int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device,
                      int max_games, uint64_t rng_seed, mz_handle** out);
+/* Same engine with the ResNet networks (ResNetHP, configs 3-5).  Hidden
+ * state = (W, H, num_filters); the dynamics input is (W, H, num_filters+1). */
+int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, int device,
+                            int max_games, uint64_t rng_seed, mz_handle** out);
 void mz_engine_destroy(mz_handle* h);
 const char* mz_last_error(const mz_handle* h);
 /* message of the last failed mz_engine_create (no handle exists then) */

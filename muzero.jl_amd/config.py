@@ -72,6 +72,10 @@ class ResNetHP:                                 # Constructors.jl:77-90 (path no
     num_first_head_filters: int = 1
     batch_norm_momentum: float = 0.6
     downsample: bool = False
+    # read by the reference's ResNet heads (Learning.jl:203,235) but never
+    # declared in ResNetHP (Q12): the intended architecture's Dense width
+    width_hidden: int = 64
+    reward_activation: object = "tanh"
 
 
 class MzConfig(ctypes.Structure):
@@ -99,6 +103,16 @@ class MzFFHP(ctypes.Structure):
         ("depth_reward", ctypes.c_int32), ("depth_state_head", ctypes.c_int32),
         ("use_batch_norm", ctypes.c_int32), ("batch_norm_momentum", ctypes.c_float),
         ("hidden_state_size", ctypes.c_int32), ("reward_activation", ctypes.c_int32),
+    ]
+
+
+class MzResNetHP(ctypes.Structure):
+    _fields_ = [
+        ("num_blocks", ctypes.c_int32), ("num_filters", ctypes.c_int32),
+        ("conv_kernel_size", ctypes.c_int32 * 2), ("num_second_head_filters", ctypes.c_int32),
+        ("num_first_head_filters", ctypes.c_int32), ("batch_norm_momentum", ctypes.c_float),
+        ("downsample", ctypes.c_int32), ("depth_policy", ctypes.c_int32), ("depth_value", ctypes.c_int32),
+        ("width_hidden", ctypes.c_int32), ("reward_activation", ctypes.c_int32),
     ]
 
 
@@ -153,6 +167,30 @@ def to_c_ffhp(h: FeedForwardHP) -> MzFFHP:
         act = act.__name__
     m.reward_activation = _ACTS[act]
     return m
+
+
+def to_c_resnet_hp(h: ResNetHP) -> MzResNetHP:
+    if h.downsample:
+        raise ValueError("ResNetHP.downsample: the Atari downsampler is not built")
+    m = MzResNetHP()
+    for f in ("num_blocks", "num_filters", "num_second_head_filters", "num_first_head_filters",
+              "depth_policy", "depth_value", "width_hidden"):
+        setattr(m, f, getattr(h, f))
+    m.conv_kernel_size[0], m.conv_kernel_size[1] = h.conv_kernel_size
+    m.batch_norm_momentum = h.batch_norm_momentum
+    m.downsample = 0
+    act = h.reward_activation
+    if callable(act):
+        act = act.__name__
+    m.reward_activation = _ACTS[act]
+    return m
+
+
+def hidden_size(conf: Config, hyper) -> int:
+    """Hidden-state floats: FeedForwardHP.hidden_state_size, or W*H*num_filters."""
+    if isinstance(hyper, ResNetHP):
+        return conf.observation_shape[0] * conf.observation_shape[1] * hyper.num_filters
+    return hyper.hidden_state_size
 
 
 def stacked_features(c: Config) -> int:

@@ -9,7 +9,7 @@ line winner=1 and terminates on it or on a full board (game.jl:117-147).
 """
 import numpy as np
 
-from ..config import Config, FeedForwardHP
+from ..config import Config, FeedForwardHP, ResNetHP
 
 LINES = np.array([[0, 3, 6], [1, 4, 7], [2, 5, 8], [0, 1, 2], [3, 4, 5], [6, 7, 8], [0, 4, 8], [6, 4, 2]])
 
@@ -43,6 +43,15 @@ hyper = FeedForwardHP(
     hidden_state_size=27,
     reward_activation="tanh",
 )
+
+# BASELINE config 3: the ResNet networks (intended architecture, SURVEY §2.1
+# Q12; the reference ships no ResNet config): 3x3 representation convs,
+# 64 filters, 2 residual blocks per tower, 1x1 convs in prediction / dynamics.
+resnet_hyper = ResNetHP(
+    num_blocks=2, depth_representation=0, num_filters=64, conv_kernel_size=(3, 3),
+    hidden_state_size=3 * 3 * 64, representation_output_size=(3, 3, 64), depth_policy=1, depth_value=1,
+    num_second_head_filters=2, num_first_head_filters=1, batch_norm_momentum=0.6, downsample=False,
+    width_hidden=64, reward_activation="tanh")
 
 
 class TicTacToe:

@@ -1,13 +1,17 @@
-"""The FC representation / prediction / dynamics networks (Learning.jl:70-142)
-as flat Flux-order parameter vectors.
+"""The representation / prediction / dynamics networks as flat Flux-order
+parameter vectors: FC (Learning.jl:70-142) and ResNet (Learning.jl:148-255,
+the intended architecture of SURVEY §2.1 Q12 / DESIGN.md §9).
 
-Flux order per net: for every Dense in Chain order (Split paths in order),
-W (out, in) column-major then b.  `layer_specs` lists (chain, in, out, act)
+Flux order per net, in Chain order with Split paths in order:
+  Dense     W (out, in) column-major, then b
+  Conv      weight (kw, kh, cin, cout) column-major, then b
+  BatchNorm β, then γ (running μ = 0, σ² = 1 are state, not params)
+`layer_specs` (FC) lists (chain, in, out, act); `resnet_specs` lists dicts
 with chain 0 = trunk, 1 = first Split path, 2 = second Split path.
 """
 import numpy as np
 
-from .config import ACT_IDENTITY, ACT_RELU, ACT_TANH, stacked_features
+from .config import ACT_IDENTITY, ACT_RELU, ACT_TANH, ResNetHP, stacked_features
 
 NET_REPR, NET_PRED, NET_DYN = 0, 1, 2
 
@@ -39,7 +43,77 @@ def layer_specs(conf, hyper, net):
     return L
 
 
+def _act(a):
+    if callable(a):
+        a = a.__name__
+    return {"tanh": ACT_TANH, "relu": ACT_RELU, "identity": ACT_IDENTITY}[a]
+
+
+def resnet_specs(conf, hyper, net):
+    """Intended ResNet architecture (Learning.jl:148-255 with Q12 fixed), in
+    the oracle's op order (oracle/mz_oracle.c onet_build_resnet)."""
+    W, H, C = conf.observation_shape
+    nf, nb, hs, A = hyper.num_filters, hyper.num_blocks, hyper.width_hidden, len(conf.action_space)
+    P, nvf, npf = W * H, hyper.num_first_head_filters, hyper.num_second_head_filters
+    ops = []
+
+    def conv(ch, cin, cout, k, act=ACT_RELU):
+        ops.append(dict(chain=ch, kind="conv", cin=cin, cout=cout, kw=k[0], kh=k[1], W=W, H=H, bn=True,
+                        act=act, res_save=False, res_add=False))
+
+    def block(ch, n, k):                                   # resnet_block (:148-158)
+        conv(ch, n, n, k)
+        ops[-1]["res_save"] = True
+        conv(ch, n, n, k)
+        ops[-1]["res_add"] = True
+
+    def dense(ch, i, o, act):
+        ops.append(dict(chain=ch, kind="dense", cin=i, cout=o, act=act))
+
+    k1 = (1, 1)
+    if net == NET_REPR:                                    # :160-191
+        k = tuple(hyper.conv_kernel_size)
+        conv(0, C * (conf.stacked_observations + 1) + conf.stacked_observations, nf, k)
+        for _ in range(nb):
+            block(0, nf, k)
+    elif net == NET_PRED:                                  # :193-226
+        conv(0, nf, nf, k1)
+        for _ in range(nb):
+            block(0, nf, k1)
+        conv(1, nf, nvf, k1)
+        dense(1, P * nvf, hs, ACT_RELU)
+        for _ in range(hyper.depth_value):
+            dense(1, hs, hs, ACT_RELU)
+        dense(1, hs, 1, ACT_TANH)
+        conv(2, nf, npf, k1)
+        dense(2, P * npf, hs, ACT_IDENTITY)
+        for _ in range(hyper.depth_value):                 # :222 reuses depth_value
+            dense(2, hs, hs, ACT_RELU)
+        dense(2, hs, A, ACT_IDENTITY)                      # then softmax
+    else:                                                  # :228-255
+        conv(0, nf + 1, nf, k1)
+        for _ in range(nb):
+            block(0, nf, k1)
+        conv(1, nf, nf, k1)
+        for _ in range(nb):
+            block(1, nf, k1)
+        conv(2, nf, nvf, k1)
+        dense(2, P * nvf, hs, ACT_RELU)
+        for _ in range(hyper.depth_value):
+            dense(2, hs, hs, ACT_RELU)
+        dense(2, hs, 1, _act(hyper.reward_activation))
+    return ops
+
+
+def _op_params(op):
+    if op["kind"] == "dense":
+        return op["cin"] * op["cout"] + op["cout"]
+    return op["kw"] * op["kh"] * op["cin"] * op["cout"] + op["cout"] + (2 * op["cout"] if op["bn"] else 0)
+
+
 def param_count(conf, hyper, net):
+    if isinstance(hyper, ResNetHP):
+        return sum(_op_params(op) for op in resnet_specs(conf, hyper, net))
     return sum(i * o + o for _, i, o, _ in layer_specs(conf, hyper, net))
 
 
@@ -49,10 +123,29 @@ def glorot_uniform(rng, out, inp):
     return ((u - np.float32(0.5)) * np.float32(np.sqrt(np.float32(24.0) / np.float32(inp + out)))).astype(np.float32)
 
 
+def glorot_uniform_conv(rng, kw, kh, cin, cout):
+    """Flux glorot_uniform(kw, kh, cin, cout): nfan = (kw*kh*cin, kw*kh*cout); column-major flat."""
+    u = rng.random(kw * kh * cin * cout, dtype=np.float32)
+    return ((u - np.float32(0.5)) * np.float32(np.sqrt(np.float32(24.0) /
+                                                       np.float32(kw * kh * (cin + cout))))).astype(np.float32)
+
+
 def init_net(conf, hyper, net, seed=0):
-    """init_representation / init_prediction / init_dynamics: glorot W, zero b (Q17)."""
+    """init_representation / init_prediction / init_dynamics: glorot W, zero b (Q17);
+    BatchNorm β = 0, γ = 1."""
     rng = np.random.default_rng(seed * 3 + net)
     parts = []
+    if isinstance(hyper, ResNetHP):
+        for op in resnet_specs(conf, hyper, net):
+            if op["kind"] == "dense":
+                parts.append(glorot_uniform(rng, op["cout"], op["cin"]).reshape(-1))
+                parts.append(np.zeros(op["cout"], np.float32))
+            else:
+                parts.append(glorot_uniform_conv(rng, op["kw"], op["kh"], op["cin"], op["cout"]))
+                parts.append(np.zeros(op["cout"], np.float32))
+                parts.append(np.zeros(op["cout"], np.float32))       # β
+                parts.append(np.ones(op["cout"], np.float32))        # γ
+        return np.concatenate(parts)
     for _, i, o, _ in layer_specs(conf, hyper, net):
         parts.append(glorot_uniform(rng, o, i).reshape(-1))
         parts.append(np.zeros(o, np.float32))
@@ -61,6 +154,31 @@ def init_net(conf, hyper, net, seed=0):
 
 def init_nets(conf, hyper, seed=0):
     return [init_net(conf, hyper, n, seed) for n in range(3)]
+
+
+def unflatten_resnet(conf, hyper, net, flat):
+    """-> the resnet_specs dicts with arrays: conv "w" (cout, cin, kh, kw) — Flux (kw,kh,cin,cout)
+    column-major transposed — "b", "beta", "gamma"; dense "w" (out, in), "b"."""
+    out, off = [], 0
+    for op in resnet_specs(conf, hyper, net):
+        op = dict(op)
+        if op["kind"] == "dense":
+            i, o = op["cin"], op["cout"]
+            op["w"] = flat[off: off + i * o].reshape(i, o).T
+            off += i * o
+        else:
+            kw, kh, ci, co = op["kw"], op["kh"], op["cin"], op["cout"]
+            n = kw * kh * ci * co
+            op["w"] = flat[off: off + n].reshape(co, ci, kh, kw)
+            off += n
+        op["b"] = flat[off: off + op["cout"]]
+        off += op["cout"]
+        if op["kind"] == "conv":
+            op["beta"] = flat[off: off + op["cout"]]
+            op["gamma"] = flat[off + op["cout"]: off + 2 * op["cout"]]
+            off += 2 * op["cout"]
+        out.append(op)
+    return out
 
 
 def unflatten(conf, hyper, net, flat):

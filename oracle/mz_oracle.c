@@ -36,26 +36,116 @@
 #define MAXA MZ_MAX_ACTIONS
 
 /* ===================================================================== nets
- * Learning.jl:70-142.  Layer list of each FC net in Flux.params order.   */
-typedef struct { int in, out, act; size_t woff, boff; } OLayer;
+ * Learning.jl:70-142 (FeedForwardHP) and 148-255 (ResNetHP, the intended
+ * architecture of SURVEY §2.1 Q12 / DESIGN.md §9).  Layer list of each net
+ * in Flux.params order: Dense W (out,in) col-major then b; Conv weight
+ * (kw,kh,cin,cout) col-major then b; BatchNorm β then γ (its running μ = 0,
+ * σ² = 1 are state, not params, and the reference's test-mode forward never
+ * changes them).                                                           */
+typedef struct { int32_t kind; mz_ffhp ff; mz_resnet_hp rn; } ora_nethp;   /* kind 0 FC, 1 ResNet */
+
+typedef struct {
+    int in, out, act;          /* Dense: features; Conv: channels */
+    size_t woff, boff;
+    int conv, kw, kh, pw, ph, W, H;   /* Conv (stride 1, zero pad, kernel flipped) over W x H */
+    int bn; size_t bnoff;      /* BatchNorm(out) after the affine: β at bnoff, γ at bnoff + out */
+    int res_save, res_add;     /* block input saved here / added before the activation */
+} OLayer;
 typedef struct {
     int n[3];            /* layers in trunk, head 1, head 2 (head counts 0 for repr) */
-    OLayer L[3][64];
+    OLayer L[3][96];
     size_t nparams;
     int softmax_head2;   /* prediction policy head ends in softmax (Learning.jl:113-114) */
+    int maxact;          /* largest activation (floats) */
 } ONet;
 
-static void onet_add(ONet* net, int part, int in, int out, int act) {
+static int olayer_insize(const OLayer* l) { return l->conv ? l->in * l->W * l->H : l->in; }
+static int olayer_outsize(const OLayer* l) { return l->conv ? l->out * l->W * l->H : l->out; }
+
+static OLayer* onet_add(ONet* net, int part, int in, int out, int act) {
     OLayer* l = &net->L[part][net->n[part]++];
+    memset(l, 0, sizeof(*l));
     l->in = in; l->out = out; l->act = act;
     l->woff = net->nparams; net->nparams += (size_t)in * out;
     l->boff = net->nparams; net->nparams += (size_t)out;
+    return l;
+}
+
+/* Conv(k, in => out, pad = k .÷ 2) [+ BatchNorm(out, act)] on a W x H board */
+static OLayer* onet_conv(ONet* net, int part, int in, int out, int kw, int kh, int W, int H, int bn, int act) {
+    OLayer* l = &net->L[part][net->n[part]++];
+    memset(l, 0, sizeof(*l));
+    l->conv = 1; l->in = in; l->out = out; l->act = act;
+    l->kw = kw; l->kh = kh; l->pw = kw / 2; l->ph = kh / 2; l->W = W; l->H = H;
+    l->woff = net->nparams; net->nparams += (size_t)kw * kh * in * out;
+    l->boff = net->nparams; net->nparams += (size_t)out;
+    if (bn) { l->bn = 1; l->bnoff = net->nparams; net->nparams += (size_t)2 * out; }
+    return l;
+}
+
+/* resnet_block (Learning.jl:148-158): conv-BN-relu-conv-BN, + x, relu */
+static void onet_resblock(ONet* net, int part, int n, int k, int W, int H) {
+    OLayer* a = onet_conv(net, part, n, n, k, k, W, H, 1, MZ_ACT_RELU);
+    a->res_save = 1;
+    OLayer* b = onet_conv(net, part, n, n, k, k, W, H, 1, MZ_ACT_RELU);
+    b->res_add = 1;
+}
+
+static int nethp_hidden(const mz_config* c, const ora_nethp* hp) {
+    if (hp->kind == 0) return hp->ff.hidden_state_size;
+    return c->observation_shape[0] * c->observation_shape[1] * hp->rn.num_filters;
+}
+
+static void onet_finish(ONet* net) {
+    net->maxact = 0;
+    for (int p = 0; p < 3; ++p)
+        for (int i = 0; i < net->n[p]; ++i) {
+            const OLayer* l = &net->L[p][i];
+            if (olayer_insize(l) > net->maxact) net->maxact = olayer_insize(l);
+            if (olayer_outsize(l) > net->maxact) net->maxact = olayer_outsize(l);
+        }
+}
+
+/* init_representation / init_prediction / init_dynamics for ResNetHP */
+static void onet_build_resnet(ONet* net, int which, const mz_config* c, const mz_resnet_hp* hp) {
+    int W = c->observation_shape[0], H = c->observation_shape[1], C = c->observation_shape[2];
+    int nf = hp->num_filters, nb = hp->num_blocks, hs = hp->width_hidden, A = c->action_space_size;
+    int P = W * H, nvf = hp->num_first_head_filters, npf = hp->num_second_head_filters;
+    if (which == MZ_NET_REPR) {                                           /* :160-191 */
+        int cin = C * (c->stacked_observations + 1) + c->stacked_observations;   /* Q12: the stacked input */
+        int kw = hp->conv_kernel_size[0], kh = hp->conv_kernel_size[1];
+        onet_conv(net, 0, cin, nf, kw, kh, W, H, 1, MZ_ACT_RELU);
+        for (int i = 0; i < nb; ++i) onet_resblock(net, 0, nf, kw, W, H);
+    } else if (which == MZ_NET_PRED) {                                    /* :193-226 */
+        onet_conv(net, 0, nf, nf, 1, 1, W, H, 1, MZ_ACT_RELU);
+        for (int i = 0; i < nb; ++i) onet_resblock(net, 0, nf, 1, W, H);
+        onet_conv(net, 1, nf, nvf, 1, 1, W, H, 1, MZ_ACT_RELU);           /* value head */
+        onet_add(net, 1, P * nvf, hs, MZ_ACT_RELU);
+        for (int i = 0; i < hp->depth_value; ++i) onet_add(net, 1, hs, hs, MZ_ACT_RELU);
+        onet_add(net, 1, hs, 1, MZ_ACT_TANH);
+        onet_conv(net, 2, nf, npf, 1, 1, W, H, 1, MZ_ACT_RELU);           /* policy head */
+        onet_add(net, 2, P * npf, hs, MZ_ACT_IDENTITY);
+        for (int i = 0; i < hp->depth_value; ++i) onet_add(net, 2, hs, hs, MZ_ACT_RELU);   /* :222 depth_value */
+        onet_add(net, 2, hs, A, MZ_ACT_IDENTITY);
+        net->softmax_head2 = 1;
+    } else {                                                              /* :228-255 */
+        onet_conv(net, 0, nf + 1, nf, 1, 1, W, H, 1, MZ_ACT_RELU);        /* Q12: + the one action plane */
+        for (int i = 0; i < nb; ++i) onet_resblock(net, 0, nf, 1, W, H);
+        onet_conv(net, 1, nf, nf, 1, 1, W, H, 1, MZ_ACT_RELU);            /* state head */
+        for (int i = 0; i < nb; ++i) onet_resblock(net, 1, nf, 1, W, H);
+        onet_conv(net, 2, nf, nvf, 1, 1, W, H, 1, MZ_ACT_RELU);           /* reward head */
+        onet_add(net, 2, P * nvf, hs, MZ_ACT_RELU);
+        for (int i = 0; i < hp->depth_value; ++i) onet_add(net, 2, hs, hs, MZ_ACT_RELU);
+        onet_add(net, 2, hs, 1, hp->reward_activation);
+    }
 }
 
 /* init_representation (Learning.jl:87-98) / init_prediction (:100-116) /
  * init_dynamics (:118-142) for FeedForwardHP. */
-static void onet_build(ONet* net, int which, const mz_config* c, const mz_ffhp* hp) {
+static void onet_build(ONet* net, int which, const mz_config* c, const ora_nethp* nh) {
     memset(net, 0, sizeof(*net));
+    if (nh->kind == 1) { onet_build_resnet(net, which, c, &nh->rn); onet_finish(net); return; }
+    const mz_ffhp* hp = &nh->ff;
     int W = c->observation_shape[0], H = c->observation_shape[1], C = c->observation_shape[2];
     int hs = hp->width_hidden, hid = hp->hidden_state_size, A = c->action_space_size;
     if (which == MZ_NET_REPR) {
@@ -80,21 +170,26 @@ static void onet_build(ONet* net, int which, const mz_config* c, const mz_ffhp* 
         for (int i = 0; i < hp->depth_reward; ++i) onet_add(net, 2, hs, hs, MZ_ACT_RELU);
         onet_add(net, 2, hs, 1, hp->reward_activation);                        /* :140 */
     }
+    onet_finish(net);
 }
 
 /* Canonical dot product of the engine: four partial fmaf chains over
  * contiguous k-quarters of length kq = 4*ceil(K/16), each started at +0,
  * combined as ((p0+p1)+(p2+p3)).  Flux's `W*x` (BLAS) has no fixed order;
- * this one is what the GPU's four-accumulator f32 MFMA chain computes.   */
-static float mz_dot(const float* Wcol /* W(out,in) col-major */, int out, int in, int o, const float* x) {
+ * this one is what the GPU's four-accumulator f32 MFMA chain computes.
+ * Element k of output o's weight row is w[o*so + k*sk].                   */
+static float mz_dot_s(const float* w, size_t sk, const float* x, int in) {
     int kq = 4 * ((in + 15) / 16);
     float p[4];
     for (int q = 0; q < 4; ++q) {
         p[q] = 0.0f;
         int k1 = (q + 1) * kq < in ? (q + 1) * kq : in;
-        for (int k = q * kq; k < k1; ++k) p[q] = fmaf(Wcol[o + (size_t)out * k], x[k], p[q]);
+        for (int k = q * kq; k < k1; ++k) p[q] = fmaf(w[(size_t)k * sk], x[k], p[q]);
     }
     return (p[0] + p[1]) + (p[2] + p[3]);
+}
+static float mz_dot(const float* Wcol /* W(out,in) col-major */, int out, int in, int o, const float* x) {
+    return mz_dot_s(Wcol + o, (size_t)out, x, in);
 }
 
 static float act_apply(int act, float v) {
@@ -103,10 +198,45 @@ static float act_apply(int act, float v) {
     return v;
 }
 
+/* Flux BatchNorm in test mode: λ.(γ .* (x .- μ) ./ sqrt.(σ² .+ ϵ) .+ β), μ = 0,
+ * σ² = 1, ϵ = 1f-5 (the running statistics the reference never updates) */
+static float bn_apply(const OLayer* l, const float* P, int o, float t) {
+    const float s = sqrtf(1.0f + 1e-5f);
+    const float xh = (t - 0.0f) / s;
+    return P[l->bnoff + l->out + o] * xh + P[l->bnoff + o];
+}
+
 /* Flux Dense: σ.(W*x .+ b) */
 static void dense_fwd(const OLayer* l, const float* P, const float* x, float* y) {
     for (int o = 0; o < l->out; ++o)
         y[o] = act_apply(l->act, mz_dot(P + l->woff, l->out, l->in, o, x) + P[l->boff + o]);
+}
+
+/* Flux Conv (stride 1, zero padding, kernel flipped) on a (W, H, cin)
+ * column-major activation: the im2col row of position (w, h) is, for k = i +
+ * kw*j + kw*kh*c (the weight's column-major order), x[w + (kw-1-i) - pw,
+ * h + (kh-1-j) - ph, c].  Then bias, BatchNorm, the saved block input, act. */
+static void conv_fwd(const OLayer* l, const float* P, const float* x, float* y, const float* res) {
+    const int W = l->W, H = l->H, Pn = W * H, K = l->kw * l->kh * l->in;
+    float* col = (float*)malloc(sizeof(float) * (size_t)K);
+    for (int hh = 0; hh < H; ++hh)
+        for (int ww = 0; ww < W; ++ww) {
+            for (int c = 0; c < l->in; ++c)
+                for (int j = 0; j < l->kh; ++j)
+                    for (int i = 0; i < l->kw; ++i) {
+                        const int sx = ww + (l->kw - 1 - i) - l->pw, sy = hh + (l->kh - 1 - j) - l->ph;
+                        const int k = i + l->kw * j + l->kw * l->kh * c;
+                        col[k] = (sx >= 0 && sx < W && sy >= 0 && sy < H) ? x[sx + W * sy + Pn * c] : 0.0f;
+                    }
+            const int p = ww + W * hh;
+            for (int o = 0; o < l->out; ++o) {
+                float t = mz_dot_s(P + l->woff + (size_t)K * o, 1, col, K) + P[l->boff + o];
+                if (l->bn) t = bn_apply(l, P, o, t);
+                if (l->res_add) t = t + res[p + (size_t)Pn * o];
+                y[p + (size_t)Pn * o] = act_apply(l->act, t);
+            }
+        }
+    free(col);
 }
 
 /* NNlib softmax over n entries: max, exp(x - max), sequential sum, divide. */
@@ -119,43 +249,51 @@ static void softmax_n(const float* x, int n, float* y) {
 }
 
 static void run_chain(const ONet* net, int part, const float* P, const float* x, float* y) {
-    float a[1024], b[1024];
+    const size_t sz = (size_t)net->maxact;
+    float* a = (float*)malloc(sizeof(float) * sz * 3);
+    float *b = a + sz, *res = a + 2 * sz;
     const float* cur = x;
     for (int i = 0; i < net->n[part]; ++i) {
+        const OLayer* l = &net->L[part][i];
         float* dst = (i & 1) ? b : a;
-        dense_fwd(&net->L[part][i], P, cur, dst);
+        if (l->res_save) memcpy(res, cur, sizeof(float) * (size_t)olayer_insize(l));
+        if (l->conv) conv_fwd(l, P, cur, dst, res);
+        else dense_fwd(l, P, cur, dst);
         cur = dst;
     }
-    memcpy(y, cur, sizeof(float) * net->L[part][net->n[part] - 1].out);
+    memcpy(y, cur, sizeof(float) * (size_t)olayer_outsize(&net->L[part][net->n[part] - 1]));
+    free(a);
 }
 
 /* forward of one sample; REPR: out0 = h; PRED: out0 = value, out1 = policy;
  * DYN: out0 = h', out1 = reward.  The Split applies both heads to the trunk
  * output (Learning.jl:68). */
 static void net_forward1(const ONet* net, const float* P, const float* x, float* out0, float* out1) {
-    float t[1024];
+    float* t = (float*)malloc(sizeof(float) * (size_t)net->maxact);
     run_chain(net, 0, P, x, net->n[1] ? t : out0);
-    if (!net->n[1]) return;
-    run_chain(net, 1, P, t, out0);
-    if (net->softmax_head2) {
-        float lg[MAXA];
-        run_chain(net, 2, P, t, lg);
-        softmax_n(lg, net->L[2][net->n[2] - 1].out, out1);
-    } else {
-        run_chain(net, 2, P, t, out1);
+    if (net->n[1]) {
+        run_chain(net, 1, P, t, out0);
+        if (net->softmax_head2) {
+            float lg[MAXA];
+            run_chain(net, 2, P, t, lg);
+            softmax_n(lg, net->L[2][net->n[2] - 1].out, out1);
+        } else {
+            run_chain(net, 2, P, t, out1);
+        }
     }
+    free(t);
 }
 
-EXPORT size_t ora_param_count(const mz_config* c, const mz_ffhp* hp, int which) {
+EXPORT size_t ora_param_count(const mz_config* c, const ora_nethp* hp, int which) {
     ONet n; onet_build(&n, which, c, hp); return n.nparams;
 }
 
 /* batched forward, column-major (features, n) */
-EXPORT void ora_net_forward(const mz_config* c, const mz_ffhp* hp, int which, const float* P,
+EXPORT void ora_net_forward(const mz_config* c, const ora_nethp* hp, int which, const float* P,
                             const float* x, int n, float* out0, float* out1) {
     ONet net; onet_build(&net, which, c, hp);
-    int in = net.L[0][0].in;
-    int o0 = which == MZ_NET_PRED ? 1 : hp->hidden_state_size;
+    int in = olayer_insize(&net.L[0][0]);
+    int o0 = which == MZ_NET_PRED ? 1 : nethp_hidden(c, hp);
     int o1 = which == MZ_NET_PRED ? c->action_space_size : 1;
     for (int i = 0; i < n; ++i)
         net_forward1(&net, P, x + (size_t)i * in, out0 + (size_t)i * o0, out1 ? out1 + (size_t)i * o1 : NULL);
@@ -187,7 +325,7 @@ static float mm_normalize(const MinMax* m, float v) {             /* :33-39 */
 
 typedef struct {
     const mz_config* c;
-    const mz_ffhp* hp;
+    const ora_nethp* hp;
     ONet nrep, npred, ndyn;
     const float *Prep, *Ppred, *Pdyn;
     uint64_t seed;
@@ -318,7 +456,7 @@ static int run_mcts(OCtx* X, const float* obs, const uint8_t* legal, int to_play
     if (exploration) add_noise(X, root, game, step);                /* :247-249 */
     MinMax mm = {INFINITY, -INFINITY};                              /* :251 */
     int* path = (int*)malloc(sizeof(int) * (X->S + 2));
-    float sa[1024];
+    float* sa = (float*)malloc(sizeof(float) * (size_t)olayer_insize(&X->ndyn.L[0][0]));
     for (int it = 0; it < X->S; ++it) {                             /* :254 */
         int node = root, vtp = to_play, len = 0, depth = 0, action = 0;
         path[len++] = node;
@@ -348,6 +486,7 @@ static int run_mcts(OCtx* X, const float* obs, const uint8_t* legal, int to_play
         backpropagate(X, path, len, value, vtp, &mm);               /* :281 */
     }
     free(path);
+    free(sa);
     return root;
 }
 
@@ -386,7 +525,7 @@ static int select_action(OCtx* X, int root, float temperature, uint32_t game, ui
     return acts[n - 1];
 }
 
-static void ctx_init(OCtx* X, const mz_config* c, const mz_ffhp* hp, const float* Prep,
+static void ctx_init(OCtx* X, const mz_config* c, const ora_nethp* hp, const float* Prep,
                      const float* Ppred, const float* Pdyn, uint64_t seed) {
     X->c = c; X->hp = hp;
     onet_build(&X->nrep, MZ_NET_REPR, c, hp);
@@ -394,7 +533,7 @@ static void ctx_init(OCtx* X, const mz_config* c, const mz_ffhp* hp, const float
     onet_build(&X->ndyn, MZ_NET_DYN, c, hp);
     X->Prep = Prep; X->Ppred = Ppred; X->Pdyn = Pdyn;
     X->seed = seed;
-    X->H = hp->hidden_state_size; X->A = c->action_space_size; X->S = c->num_iters;
+    X->H = nethp_hidden(c, hp); X->A = c->action_space_size; X->S = c->num_iters;
     X->nodes = (ONode*)malloc(sizeof(ONode) * (size_t)(1 + (X->S + 1) * X->A));
     X->hid = (float*)malloc(sizeof(float) * (size_t)(X->S + 1) * X->H);
 }
@@ -435,7 +574,7 @@ static void dump_tree(OCtx* X, int g, int G, int32_t* eN, float* eW, float* eP, 
 }
 
 /* Batched search: the ABI of mz_mcts_search, on the CPU. */
-EXPORT int ora_mcts_search(const mz_config* c, const mz_ffhp* hp, const float* Prep, const float* Ppred,
+EXPORT int ora_mcts_search(const mz_config* c, const ora_nethp* hp, const float* Prep, const float* Ppred,
                            const float* Pdyn, uint64_t seed, int G, const float* obs,
                            const uint8_t* legal_mask, const int32_t* to_play, int exploration,
                            uint32_t rng_step, uint32_t game_offset, float temperature,
@@ -444,7 +583,7 @@ EXPORT int ora_mcts_search(const mz_config* c, const mz_ffhp* hp, const float* P
                            int64_t* stats) {
     OCtx X; ctx_init(&X, c, hp, Prep, Ppred, Pdyn, seed);
     int A = X.A;
-    int in = X.nrep.L[0][0].in;
+    int in = olayer_insize(&X.nrep.L[0][0]);
     for (int g = 0; g < G; ++g) {
         uint32_t gid = game_offset + (uint32_t)g;
         int root = run_mcts(&X, obs + (size_t)g * in, legal_mask + (size_t)g * A, to_play[g],
@@ -528,7 +667,7 @@ EXPORT void ora_stacked_obs(const mz_config* c, const float* obs_hist, const int
 /* play_game (SelfPlay.jl:330-382) for one TicTacToe game, opponent "self".
  * Move t uses RNG step step0 + t.  Outputs are GameHistory columns sized
  * for max_moves+1 moves; returns the number of moves T.                   */
-EXPORT int ora_play_game(const mz_config* c, const mz_ffhp* hp, const float* Prep, const float* Ppred,
+EXPORT int ora_play_game(const mz_config* c, const ora_nethp* hp, const float* Prep, const float* Ppred,
                          const float* Pdyn, uint64_t seed, uint32_t game_id, uint32_t step0,
                          float temperature, float* obs_hist, int32_t* action_hist, float* reward_hist,
                          int32_t* to_play_hist, float* child_visits, float* root_values) {
@@ -656,15 +795,17 @@ static float policy_ce(const float* yhat, const float* y, int A) {
 
 /* The forward unroll: predictions values (K+1,B), policies (A,K+1,B),
  * rewards (K+1,B) exactly as Learning.jl:347-370 builds them (Q10). */
-EXPORT void ora_unroll(const mz_config* c, const mz_ffhp* hp, const float* Prep, const float* Ppred,
+EXPORT void ora_unroll(const mz_config* c, const ora_nethp* hp, const float* Prep, const float* Ppred,
                        const float* Pdyn, int B, const float* obs, const float* actions,
                        float* pv, float* pp, float* pr) {
     ONet nr, np, nd;
     onet_build(&nr, MZ_NET_REPR, c, hp); onet_build(&np, MZ_NET_PRED, c, hp); onet_build(&nd, MZ_NET_DYN, c, hp);
-    int H = hp->hidden_state_size, A = c->action_space_size, K = c->num_unroll_steps;
-    int in = nr.L[0][0].in;
+    int H = nethp_hidden(c, hp), A = c->action_space_size, K = c->num_unroll_steps;
+    int in = olayer_insize(&nr.L[0][0]);
     int plane = c->observation_shape[0] * c->observation_shape[1];
-    float h[1024], sa[1024], v, pol[MAXA];
+    float* h = (float*)malloc(sizeof(float) * (size_t)H);
+    float* sa = (float*)malloc(sizeof(float) * (size_t)(H + plane));
+    float v, pol[MAXA];
     for (int b = 0; b < B; ++b) {
         net_forward1(&nr, Prep, obs + (size_t)b * in, h, NULL);          /* :347 */
         net_forward1(&np, Ppred, h, &v, pol);                            /* :351 */
@@ -683,6 +824,7 @@ EXPORT void ora_unroll(const mz_config* c, const mz_ffhp* hp, const float* Prep,
             memcpy(pp + ((size_t)b * (K + 1) + i) * A, pol, sizeof(float) * A);
         }
     }
+    free(h); free(sa);
 }
 
 /* loss (:261-288) data terms; l2 = sum(sqnorm, params) per net in f64. */
@@ -746,7 +888,7 @@ EXPORT double ora_cos_schedule(double l0, double l1, int period, int t) {
 
 /* One full ref_semantics learner step: forward unroll + losses + ADAM on
  * all three nets; bp is advanced (βp .= βp .* β).                          */
-EXPORT void ora_learner_step(const mz_config* c, const mz_ffhp* hp, float* Prep, float* Ppred, float* Pdyn,
+EXPORT void ora_learner_step(const mz_config* c, const ora_nethp* hp, float* Prep, float* Ppred, float* Pdyn,
                              float* m_all, float* v_all, double* bp, int B, const float* obs,
                              const float* actions, const float* tv, const float* tp, const float* gscale,
                              double eta, float* losses) {

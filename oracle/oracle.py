@@ -79,16 +79,34 @@ def _p(a):
     return None if a is None else a.ctypes.data_as(_VP)
 
 
+def nethp(chp):
+    """Tagged network hyper-parameters of the oracle (ora_nethp): FC or ResNet."""
+    from muzero_jl_amd.config import MzFFHP, MzResNetHP   # registered by _mzpkg.load()
+
+    class OraNetHP(ctypes.Structure):
+        _fields_ = [("kind", ctypes.c_int32), ("ff", MzFFHP), ("rn", MzResNetHP)]
+
+    o = OraNetHP()
+    if isinstance(chp, MzResNetHP):
+        o.kind, o.rn = 1, chp
+    else:
+        o.kind, o.ff = 0, chp
+    return o
+
+
 class Oracle:
-    """The oracle bound to one (Config, FeedForwardHP) and three flat weight vectors."""
+    """The oracle bound to one (Config, FeedForwardHP | ResNetHP) and three flat weight vectors."""
 
     def __init__(self, cconf, chp, seed=0):
         self.L = lib()
         self.cconf = cconf
-        self.chp = chp
+        self.chp = nethp(chp)
         self.seed = seed
         self.A = cconf.action_space_size
-        self.H = chp.hidden_state_size
+        if self.chp.kind == 1:
+            self.H = cconf.observation_shape[0] * cconf.observation_shape[1] * chp.num_filters
+        else:
+            self.H = chp.hidden_state_size
         self.S = cconf.num_iters
         self.K = cconf.num_unroll_steps
         self.params = [np.zeros(self.param_count(i), np.float32) for i in range(3)]
