@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 from . import LIB_PATH
-from .config import MzConfig, MzFFHP, to_c_config, to_c_ffhp, stacked_features
+from .config import (MzConfig, MzFFHP, MzResNetHP, ResNetHP, hidden_size, stacked_features, to_c_config,
+                     to_c_ffhp, to_c_resnet_hp)
 
 NET_REPR, NET_PRED, NET_DYN = 0, 1, 2
 
@@ -34,6 +35,8 @@ class MzBatch(ctypes.Structure):
 SIGNATURES = {
     "mz_engine_create": (ctypes.c_int, [ctypes.POINTER(MzConfig), ctypes.POINTER(MzFFHP), ctypes.c_int,
                                         ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(_VP)]),
+    "mz_engine_create_resnet": (ctypes.c_int, [ctypes.POINTER(MzConfig), ctypes.POINTER(MzResNetHP), ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(_VP)]),
     "mz_engine_destroy": (None, [_VP]),
     "mz_last_error": (ctypes.c_char_p, [_VP]),
     "mz_create_error": (ctypes.c_char_p, []),
@@ -89,16 +92,21 @@ class Engine:
         self.conf = conf
         self.hyper = hyper
         self._cconf = to_c_config(conf)
-        self._chp = to_c_ffhp(hyper)
         h = _VP()
-        rc = lib.mz_engine_create(ctypes.byref(self._cconf), ctypes.byref(self._chp), device, max_games,
-                                  rng_seed, ctypes.byref(h))
+        if isinstance(hyper, ResNetHP):        # row a14: the ResNet networks
+            self._chp = to_c_resnet_hp(hyper)
+            rc = lib.mz_engine_create_resnet(ctypes.byref(self._cconf), ctypes.byref(self._chp), device, max_games,
+                                             rng_seed, ctypes.byref(h))
+        else:
+            self._chp = to_c_ffhp(hyper)
+            rc = lib.mz_engine_create(ctypes.byref(self._cconf), ctypes.byref(self._chp), device, max_games,
+                                      rng_seed, ctypes.byref(h))
         if rc != 0:
             raise MzError(f"mz_engine_create: {lib.mz_create_error().decode()}")
         self.h = h
         self.max_games = max_games
         self.A = len(conf.action_space)
-        self.H = hyper.hidden_state_size
+        self.H = hidden_size(conf, hyper)
         self.obs_feat = stacked_features(conf)
 
     def close(self):

@@ -24,6 +24,8 @@ extern "C" __global__ void mz_search_kernel_lds(SearchParams P);
 extern "C" __global__ void mz_search_kernel_hbm(SearchParams P);
 extern "C" __global__ void mz_search_kernel_lds_res(SearchParams P);
 #include "mz_small_params.h"
+#include "mz_resnet_params.h"
+extern "C" __global__ void mz_rnet_forward_kernel(RNetParams Q);
 extern "C" __global__ void mz_search_small1(SmallParams P);
 extern "C" __global__ void mz_search_small2(SmallParams P);
 extern "C" __global__ void mz_search_small4(SmallParams P);
@@ -85,6 +87,14 @@ thread_local std::string g_create_error;
 struct mz_handle {
     mz_config conf;
     mz_ffhp hp;
+    int kind = 0;                           // 0 FeedForwardHP, 1 ResNetHP
+    mz_resnet_hp rhp{};
+    // ResNet networks (mz_resnet.hip): host plans, device copies, tile width
+    std::vector<RPlan> rplan;               // [3]
+    RPlan* d_rplan = nullptr;               // [3]
+    int rn_ng = 0;
+    size_t rn_lds[3] = {0, 0, 0};
+    float bn_s = 1.0f;
     int device = 0, max_games = 0;
     uint64_t seed = 0;
     std::string err;
@@ -546,8 +556,9 @@ static int repack(mz_handle* h, hipStream_t st = nullptr) {
     if (!st) st = h->stream;
     hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_w_n + T - 1) / T)), dim3(T), 0, st,
                        h->d_flat, h->d_srcW, h->d_Wp, h->packed_w_n);
-    hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_b_n + T - 1) / T)), dim3(T), 0, st,
-                       h->d_flat, h->d_srcB, h->d_Bp, h->packed_b_n);
+    if (h->packed_b_n)
+        hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_b_n + T - 1) / T)), dim3(T), 0, st,
+                           h->d_flat, h->d_srcB, h->d_Bp, h->packed_b_n);
     if (h->small_ok) {
         hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->sm_w_n + T - 1) / T)), dim3(T), 0, st,
                            h->d_flat, h->d_sm_srcw, h->d_sm_w, h->sm_w_n);
@@ -584,6 +595,227 @@ extern "C" {
 
 const char* mz_create_error(void) { return g_create_error.c_str(); }
 const char* mz_last_error(const mz_handle* h) { return h ? h->err.c_str() : g_create_error.c_str(); }
+
+// ------------------------------------------------------------- ResNet nets
+// Row a14: the intended architecture of Learning.jl:148-255,
+// op for op as oracle/mz_oracle.c onet_build_resnet, in Flux.params order:
+// Conv weight (kw,kh,cin,cout) col-major, bias, BatchNorm β, γ; Dense W
+// (out,in) col-major, b.
+struct RSpec {
+    int chain, conv, cin, cout, kw, kh, act, bn, res_save, res_add;
+    size_t woff, boff, bnoff;               // local to the net
+};
+
+static std::vector<RSpec> rn_specs(const mz_config& c, const mz_resnet_hp& hp, int net, size_t* nparams) {
+    const int W = c.observation_shape[0], H = c.observation_shape[1], C = c.observation_shape[2];
+    const int nf = hp.num_filters, nb = hp.num_blocks, hs = hp.width_hidden, A = c.action_space_size;
+    const int P = W * H, nvf = hp.num_first_head_filters, npf = hp.num_second_head_filters;
+    std::vector<RSpec> v;
+    size_t n = 0;
+    auto conv = [&](int ch, int cin, int cout, int kw, int kh) {
+        RSpec r{ch, 1, cin, cout, kw, kh, MZ_ACT_RELU, 1, 0, 0, 0, 0, 0};
+        r.woff = n; n += (size_t)kw * kh * cin * cout;
+        r.boff = n; n += (size_t)cout;
+        r.bnoff = n; n += (size_t)2 * cout;
+        v.push_back(r);
+    };
+    auto block = [&](int ch, int f, int k) { conv(ch, f, f, k, k); v.back().res_save = 1; conv(ch, f, f, k, k);
+                                             v.back().res_add = 1; };
+    auto dense = [&](int ch, int in, int out, int act) {
+        RSpec r{ch, 0, in, out, 1, 1, act, 0, 0, 0, 0, 0, 0};
+        r.woff = n; n += (size_t)in * out;
+        r.boff = n; n += (size_t)out;
+        v.push_back(r);
+    };
+    if (net == MZ_NET_REPR) {
+        const int kw = hp.conv_kernel_size[0], kh = hp.conv_kernel_size[1];
+        conv(0, C * (c.stacked_observations + 1) + c.stacked_observations, nf, kw, kh);
+        for (int i = 0; i < nb; ++i) block(0, nf, kw);
+    } else if (net == MZ_NET_PRED) {
+        conv(0, nf, nf, 1, 1);
+        for (int i = 0; i < nb; ++i) block(0, nf, 1);
+        conv(1, nf, nvf, 1, 1);
+        dense(1, P * nvf, hs, MZ_ACT_RELU);
+        for (int i = 0; i < hp.depth_value; ++i) dense(1, hs, hs, MZ_ACT_RELU);
+        dense(1, hs, 1, MZ_ACT_TANH);
+        conv(2, nf, npf, 1, 1);
+        dense(2, P * npf, hs, MZ_ACT_IDENTITY);
+        for (int i = 0; i < hp.depth_value; ++i) dense(2, hs, hs, MZ_ACT_RELU);    // :222 depth_value
+        dense(2, hs, A, MZ_ACT_IDENTITY);
+    } else {
+        conv(0, nf + 1, nf, 1, 1);
+        for (int i = 0; i < nb; ++i) block(0, nf, 1);
+        conv(1, nf, nf, 1, 1);
+        for (int i = 0; i < nb; ++i) block(1, nf, 1);
+        conv(2, nf, nvf, 1, 1);
+        dense(2, P * nvf, hs, MZ_ACT_RELU);
+        for (int i = 0; i < hp.depth_value; ++i) dense(2, hs, hs, MZ_ACT_RELU);
+        dense(2, hs, 1, hp.reward_activation);
+    }
+    *nparams = n;
+    return v;
+}
+
+// LDS plan of one net for a tile of NG games (floats).  Trunk: X -> B0, each
+// block B0 -> B1 -> B0 (residual in place); head 1 reads B0 (the dynamics
+// state head runs its tower in B2 / B1, B2 aliasing the dead input X); head 2
+// reads B0 through the small buffers S0..S2; outputs O0 / O1.
+static RPlan rn_plan(const mz_handle* h, const std::vector<RSpec>& sp, int net, int NG, size_t flat_off,
+                     int& w_img, std::vector<int>* srcw) {
+    const mz_config& c = h->conf;
+    const int W = c.observation_shape[0], Hh = c.observation_shape[1], P = W * Hh;
+    const int nf = h->rhp.num_filters, hs = h->rhp.width_hidden;
+    const int in_feat = net == MZ_NET_REPR ? h->obs_feat : net == MZ_NET_PRED ? h->H : h->H + h->plane;
+    const int big = nf * P * NG;
+    int off = 0;
+    auto region = [&](int n) { int o = off; off += (n + 3) / 4 * 4; return o; };
+    RPlan R;
+    std::memset(&R, 0, sizeof(R));
+    const int X = region(std::max(in_feat * NG, net == MZ_NET_DYN ? big : 0));
+    const int B0 = region(big), B1 = region(big);
+    const int B2 = X;                                                // dynamics state head (X is dead by then)
+    int headc = 0;
+    for (const RSpec& r : sp) if (r.chain && r.conv && r.cout != nf) headc = std::max(headc, r.cout * P * NG);
+    const int S0 = region(std::max(headc, hs * NG)), S1 = region(hs * NG), S2 = region(hs * NG);
+    const int O0 = net == MZ_NET_PRED ? region(NG) : B0;             // REPR / DYN out0 = h (B0 / B2)
+    const int O1 = net == MZ_NET_REPR ? 0 : region((net == MZ_NET_PRED ? h->A : 1) * NG);
+    R.in_off = X; R.in_feat = in_feat;
+    int cur[3] = {X, B0, B0};                                        // current input of each chain
+    int ping[3] = {0, S1, S1};
+    for (size_t i = 0; i < sp.size(); ++i) {
+        const RSpec& r = sp[i];
+        RLayer& L = R.L[R.n++];
+        L.kk = r.kw * r.kh; L.kw = r.kw; L.kh = r.kh; L.pw = r.kw / 2; L.ph = r.kh / 2;
+        L.K = r.conv ? r.kw * r.kh * r.cin : r.cin;
+        L.cout = r.cout; L.nq = (L.K + 15) / 16; L.n_ob = (r.cout + 15) / 16;
+        L.spatial = r.conv; L.act = r.act; L.bn = r.bn; L.res_add = r.res_add;
+        L.boff = (int)(flat_off + r.boff); L.bnoff = (int)(flat_off + r.bnoff);
+        L.ktab = -1;
+        L.in_off = cur[r.chain];
+        const bool last_in_chain = i + 1 == sp.size() || sp[i + 1].chain != r.chain;
+        if (r.chain == 0) {
+            if (r.res_add) { L.out_off = B0; L.res_off = B0; L.in_off = B1; }
+            else if (r.res_save) L.out_off = B1;
+            else L.out_off = B0;
+            cur[0] = r.res_save ? B1 : B0;
+            if (r.res_add) cur[0] = B0;
+            if (last_in_chain) { cur[1] = cur[2] = B0; }
+        } else if (r.chain == 1 && net == MZ_NET_DYN) {            // state head tower in B2 / B1
+            if (r.res_add) { L.in_off = B1; L.out_off = B2; L.res_off = B2; }
+            else if (r.res_save) { L.out_off = B1; }
+            else L.out_off = B2;
+            cur[1] = r.res_save ? B1 : B2;
+        } else {                                                    // conv head -> Dense chain
+            if (last_in_chain) L.out_off = r.chain == 1 ? O0 : O1;
+            else if (r.conv) L.out_off = S0;
+            else { L.out_off = ping[r.chain]; ping[r.chain] = ping[r.chain] == S1 ? S2 : S1; }
+            cur[r.chain] = L.out_off;
+        }
+        L.w_img = w_img;
+        const int nks = 4 * L.nq;
+        for (int ob = 0; ob < L.n_ob; ++ob)
+            for (int ks = 0; ks < nks; ++ks)
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int o = ob * 16 + (lane & 15), k = ks * 4 + (lane >> 4);
+                    int src = -1;
+                    if (o < r.cout && k < L.K)
+                        src = (int)(flat_off + r.woff + (r.conv ? (size_t)k + (size_t)L.K * o
+                                                                : (size_t)o + (size_t)r.cout * k));
+                    if (srcw) srcw->push_back(src);
+                }
+        w_img += L.n_ob * nks * 64;
+        if (L.kk > 1) L.ktab = region(L.K);
+    }
+    if (net == MZ_NET_REPR) { R.out0_off = B0; R.out0_n = h->H; R.out1_n = 0; }
+    else if (net == MZ_NET_PRED) { R.out0_off = O0; R.out0_n = 1; R.out1_off = O1; R.out1_n = h->A; }
+    else { R.out0_off = B2; R.out0_n = h->H; R.out1_off = O1; R.out1_n = 1; }
+    R.lds_floats = off;
+    return R;
+}
+
+int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, int device, int max_games,
+                            uint64_t rng_seed, mz_handle** out) {
+    g_create_error.clear();
+    if (!conf || !hyper || !out) { g_create_error = "null argument"; return -2; }
+    *out = nullptr;
+    mz_handle* h = new mz_handle();
+    h->kind = 1; h->conf = *conf; h->rhp = *hyper; h->device = device; h->max_games = max_games;
+    h->seed = rng_seed;
+    auto bad = [&](const std::string& m) { g_create_error = m; delete h; return -2; };
+    const mz_config& c = *conf;
+    if (c.action_space_size < 1 || c.action_space_size > 16)
+        return bad("action_space_size must be in 1..16 (16-lane select groups)");
+    if (c.players < 1 || c.players > 2) return bad("players must be 1 or 2");
+    if (c.num_iters < 1 || c.num_iters > 65000) return bad("num_iters out of range");
+    if (hyper->downsample) return bad("ResNetHP.downsample: the Atari downsampler is not built");
+    if (hyper->conv_kernel_size[0] % 2 == 0 || hyper->conv_kernel_size[1] % 2 == 0 ||
+        hyper->conv_kernel_size[0] > 15 || hyper->conv_kernel_size[1] > 15)
+        return bad("conv_kernel_size must be odd and <= 15 (Learning.jl:164 asserts odd)");
+    if (hyper->num_filters < 1 || hyper->num_blocks < 0 || hyper->width_hidden < 1) return bad("bad ResNetHP");
+    if (max_games < 1) return bad("max_games must be >= 1");
+    if (hipSetDevice(device) != hipSuccess) return bad("hipSetDevice failed (no GPU?)");
+    const int W = c.observation_shape[0], Hh = c.observation_shape[1], C = c.observation_shape[2];
+    h->obs_feat = W * Hh * (C * (c.stacked_observations + 1) + c.stacked_observations);
+    h->plane = W * Hh;
+    h->H = W * Hh * hyper->num_filters; h->A = c.action_space_size; h->S = c.num_iters;
+    std::vector<RSpec> sp[3];
+    size_t off = 0;
+    for (int n = 0; n < 3; ++n) {
+        sp[n] = rn_specs(c, *hyper, n, &h->nparams[n]);
+        h->flat_off[n] = off; off += h->nparams[n];
+    }
+    h->nflat = off;
+    // widest tile whose three plans fit the LDS
+    for (int ng = 16; ng >= 1 && !h->rn_ng; ng /= 2) {
+        int wi = 0;
+        bool fits = true;
+        for (int n = 0; n < 3; ++n)
+            fits &= (size_t)rn_plan(h, sp[n], n, ng, h->flat_off[n], wi, nullptr).lds_floats * 4 <= kLdsMax;
+        if (fits) h->rn_ng = ng;
+    }
+    if (!h->rn_ng) return bad("ResNet activations exceed the LDS even for one game per tile");
+    h->bn_s = sqrtf(1.0f + 1e-5f);
+    int rc = 0;
+#define CK(x) do { if ((rc = (x)) != 0) { g_create_error = h->err; mz_engine_destroy(h); return rc; } } while (0)
+    CK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess ? 0 : fail(h, "hipStreamCreate"));
+    std::vector<int> sw;
+    int wi = 0;
+    h->rplan.resize(3);
+    for (int n = 0; n < 3; ++n) {
+        h->rplan[n] = rn_plan(h, sp[n], n, h->rn_ng, h->flat_off[n], wi, &sw);
+        h->rn_lds[n] = (size_t)h->rplan[n].lds_floats * 4;
+    }
+    h->packed_w_n = sw.size(); h->packed_b_n = 0;
+    h->inv_tile.assign(h->nflat, -1);
+    for (size_t i = 0; i < sw.size(); ++i) if (sw[i] >= 0) h->inv_tile[(size_t)sw[i]] = (int)i;
+    h->inv_small.assign(h->nflat, -1);
+    auto al = [&](auto** p, size_t n) -> int { MZ_TRY(h, dalloc(h, p, n)); return 0; };
+    auto al_i = [&](int** p, const std::vector<int>& v) -> int {
+        MZ_TRY(h, dalloc(h, p, v.size()));
+        MZ_TRY(h, hipMemcpy(*p, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+        return 0;
+    };
+    CK(al_i(&h->d_srcW, sw));
+    CK(al_i(&h->d_inv_tile, h->inv_tile));
+    CK(al_i(&h->d_inv_small, h->inv_small));
+    CK(al(&h->d_rplan, 3));
+    CK(hipMemcpy(h->d_rplan, h->rplan.data(), 3 * sizeof(RPlan), hipMemcpyHostToDevice) == hipSuccess
+           ? 0 : fail(h, "copy"));
+    CK(al(&h->d_flat, h->nflat));
+    CK(al(&h->d_Wp, h->packed_w_n));
+    CK(hipMemset(h->d_flat, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
+    CK(repack(h));
+    CK(al(&h->d_m, h->nflat)); CK(al(&h->d_v, h->nflat)); CK(al(&h->d_grad, h->nflat));
+    CK(hipMemset(h->d_m, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
+    CK(hipMemset(h->d_v, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
+    const size_t lmax = std::max(h->rn_lds[0], std::max(h->rn_lds[1], h->rn_lds[2]));
+    CK(hipFuncSetAttribute((const void*)mz_rnet_forward_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)lmax) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(rnet)"));
+    CK(hipStreamSynchronize(h->stream) == hipSuccess ? 0 : fail(h, "sync"));
+#undef CK
+    *out = h;
+    return 0;
+}
 
 void mz_engine_destroy(mz_handle* h) {
     if (!h) return;
@@ -743,12 +975,36 @@ int mz_weights_get(mz_handle* h, int net, float* flat, size_t n) {
     return 0;
 }
 
+static int rnet_forward(mz_handle* h, int net, const float* x, int n, float* out0, float* out1) {
+    const RPlan& R = h->rplan[net];
+    float *dx = nullptr, *d0 = nullptr, *d1 = nullptr;
+    MZ_TRY(h, hipMalloc(&dx, (size_t)n * R.in_feat * 4));
+    MZ_TRY(h, hipMalloc(&d0, (size_t)n * R.out0_n * 4));
+    MZ_TRY(h, hipMalloc(&d1, (size_t)n * std::max(R.out1_n, 1) * 4));
+    hipMemcpyAsync(dx, x, (size_t)n * R.in_feat * 4, hipMemcpyHostToDevice, h->stream);
+    RNetParams Q;
+    Q.ng = h->rn_ng; Q.W = h->conf.observation_shape[0]; Q.H = h->conf.observation_shape[1];
+    Q.P = Q.W * Q.H; Q.n_items = n; Q.softmax1 = net == MZ_NET_PRED; Q.bn_s = h->bn_s;
+    Q.plan = h->d_rplan + net; Q.Wimg = h->d_Wp; Q.flat = h->d_flat; Q.x = dx; Q.out0 = d0; Q.out1 = d1;
+    void* args[] = {&Q};
+    hipError_t le = hipLaunchKernel((const void*)mz_rnet_forward_kernel, dim3((n + Q.ng - 1) / Q.ng), dim3(256),
+                                    args, h->rn_lds[net], h->stream);
+    hipMemcpyAsync(out0, d0, (size_t)n * R.out0_n * 4, hipMemcpyDeviceToHost, h->stream);
+    if (out1 && R.out1_n) hipMemcpyAsync(out1, d1, (size_t)n * R.out1_n * 4, hipMemcpyDeviceToHost, h->stream);
+    hipError_t se = hipStreamSynchronize(h->stream);
+    hipFree(dx); hipFree(d0); hipFree(d1);
+    MZ_TRY(h, le);
+    MZ_TRY(h, se);
+    return 0;
+}
+
 int mz_net_forward(mz_handle* h, int net, const float* x, int n, float* out0, float* out1) {
     if (!h) return -2;
     if (net < 0 || net > 2) return fail(h, "bad net id");
     if (n < 0) return fail(h, "negative batch");
     if (n == 0) return 0;
     MZ_TRY(h, hipSetDevice(h->device));
+    if (h->kind == 1) return rnet_forward(h, net, x, n, out0, out1);
     const int H = h->H, A = h->A;
     const int in_feat = net == MZ_NET_REPR ? h->obs_feat : net == MZ_NET_PRED ? H : H + h->plane;
     const int in_off = net == MZ_NET_REPR ? h->lay.x_rep : net == MZ_NET_PRED ? h->lay.x_pred : h->lay.x_dyn;

@@ -1,0 +1,48 @@
+// mz_resnet_params.h — plans of the ResNet networks (row a14) shared by the
+// host plan builder (mz_engine.hip) and the kernels (mz_resnet.hip).
+//
+// Every op is a generalised Dense  y[o][n] = Σ_k W[o][k] · B(k, n)  on a tile
+// of NG games.  Activations live in LDS as [feature][game] with feature
+// f = p + P·c for a (W, H, C) conv tensor (p = w + W·h): a conv layer has
+// P·NG columns n = p·NG + g, a Dense layer (after Flux.flatten, which is the
+// same column-major order) has NG columns.  K order of a conv: k = i + kw·j +
+// kw·kh·c (the Flux weight's column-major order); B(k, n) of a kernel > 1x1
+// reads x[w + (kw-1-i) - pw, h + (kh-1-j) - ph, c] (Flux convolution, kernel
+// flipped) or 0 outside the board.
+#pragma once
+
+#define RN_MAX_LAYERS 96
+
+struct RLayer {
+    int kk;              // kw * kh (1: Dense or 1x1 conv; > 1: im2col gather through the k table)
+    int kw, kh, pw, ph;
+    int K, cout;         // reduction length, output rows (channels / features)
+    int nq, n_ob;        // k-steps per quarter (ceil(K/16)), 16-row output blocks
+    int spatial;         // columns = P·NG (conv) or NG (Dense)
+    int act, bn, res_add;
+    int w_img;           // packed A fragments [n_ob][4·nq][64] in the image
+    int boff, bnoff;     // absolute offsets in the flat parameters (bias; β then γ)
+    int in_off, out_off, res_off;   // LDS offsets (floats)
+    int ktab;            // LDS offset of the k table (kk > 1), else -1
+};
+
+struct RPlan {
+    int n;
+    RLayer L[RN_MAX_LAYERS];
+    int in_off, in_feat;               // input buffer (features x NG)
+    int out0_off, out0_n;              // out0: h (REPR, DYN) or value (PRED)
+    int out1_off, out1_n;              // out1: policy logits (PRED) or reward (DYN), n = 0 if none
+    int lds_floats;                    // LDS per workgroup (floats), k tables included
+};
+
+struct RNetParams {
+    int ng, W, H, P;                   // tile width, board
+    int n_items;                       // items (games / samples) in total
+    int softmax1;                      // out1 is a policy: write probabilities (mz_net_forward)
+    float bn_s;                        // sqrtf(1 + 1e-5): BatchNorm test-mode denominator (σ² = 1)
+    const RPlan* plan;                 // device copy
+    const float* Wimg;                 // packed A fragments
+    const float* flat;                 // Flux-order parameters (biases, BatchNorm)
+    const float* x;                    // (in_feat, n_items) column-major input
+    float* out0; float* out1;          // (out0_n, n_items), (out1_n, n_items)
+};

@@ -1,0 +1,46 @@
+"""GPU parity of the ResNet networks (row a14) through the C ABI: the MFMA
+kernels against the CPU oracle, bit for bit (same canonical dot order,
+BatchNorm and softmax sequences), plus the torch fp32 pin at 1e-5."""
+import numpy as np
+import pytest
+
+from test_resnet_oracle import _perturb_bn, _resnet_oracle, _torch_forward
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rn(ttt):
+    from muzero_jl_amd import abi
+    conf, hyper = ttt.conf, ttt.resnet_hyper
+    o, nets = _resnet_oracle(conf, hyper, seed=9)
+    nets = _perturb_bn(conf, hyper, nets, seed=4)
+    eng = abi.Engine(conf, hyper, device=0, max_games=64, rng_seed=3)
+    for n, w in enumerate(nets):
+        o.set_weights(n, w)
+        eng.set_weights(n, w)
+    yield conf, hyper, o, eng, nets
+    eng.close()
+
+
+def _inputs(o, net, n, seed):
+    rng = np.random.default_rng(seed)
+    if net == 0:
+        return (rng.random((n, 63)) < 0.4).astype(np.float32)
+    if net == 1:
+        return rng.normal(0, 1, (n, o.H)).astype(np.float32)
+    return np.concatenate([rng.normal(0, 1, (n, o.H)), np.full((n, 9), 2 / 9)], 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("net", [0, 1, 2])
+@pytest.mark.parametrize("n", [1, 7, 33])
+def test_resnet_forward_bitexact(rn, net, n):
+    conf, hyper, o, eng, nets = rn
+    x = _inputs(o, net, n, 100 * net + n)
+    want = o.forward(net, x)
+    got = eng.forward(net, x)
+    if net == 0:
+        assert np.array_equal(got, want)
+        np.testing.assert_allclose(got, _torch_forward(conf, hyper, net, nets[net], x), rtol=1e-5, atol=1e-5)
+    else:
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
