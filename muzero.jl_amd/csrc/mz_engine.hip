@@ -26,6 +26,9 @@ extern "C" __global__ void mz_search_kernel_lds_res(SearchParams P);
 #include "mz_small_params.h"
 #include "mz_resnet_params.h"
 extern "C" __global__ void mz_rnet_forward_kernel(RNetParams Q);
+extern "C" __global__ void mz_rsearch_root(RSearchParams P);
+extern "C" __global__ void mz_rsearch_tree(RSearchParams P);
+extern "C" __global__ void mz_rsearch_nets(RSearchParams P);
 extern "C" __global__ void mz_search_small1(SmallParams P);
 extern "C" __global__ void mz_search_small2(SmallParams P);
 extern "C" __global__ void mz_search_small4(SmallParams P);
@@ -95,6 +98,8 @@ struct mz_handle {
     int rn_ng = 0;
     size_t rn_lds[3] = {0, 0, 0};
     float bn_s = 1.0f;
+    int* d_rpath = nullptr; int* d_rgst = nullptr;          // ResNet search: [G][2(S+2)], [G][RG_INTS]
+    float* d_rxpred = nullptr; float* d_rov = nullptr; float* d_rologit = nullptr; float* d_ror = nullptr;
     int device = 0, max_games = 0;
     uint64_t seed = 0;
     std::string err;
@@ -733,6 +738,39 @@ static RPlan rn_plan(const mz_handle* h, const std::vector<RSpec>& sp, int net, 
     return R;
 }
 
+// pUCT tables (libm log2/sqrt on the host: the values the oracle computes
+// inline), the action-plane values a/|A|, and the pb_term triangle
+static int alloc_search_tables(mz_handle* h) {
+    const mz_config& c = h->conf;
+    const int S = h->S, A = h->A;
+    std::vector<double> pbc(S + 2), sq(S + 2);
+    for (int n = 0; n < S + 2; ++n) {
+        pbc[n] = std::log2((double)(n + c.pb_c_base + 1) / (double)c.pb_c_base) + (double)c.pb_c_init;
+        sq[n] = std::sqrt((double)n);
+    }
+    std::vector<float> av(A);
+    for (int a = 0; a < A; ++a) av[a] = (float)((double)(a + 1) / (double)A);
+    std::vector<double> pbt(pbterm_count(S), 0.0);
+    for (int np = 0; np <= S + 1; ++np)
+        for (int nc = 0; nc <= np; ++nc) pbt[pbterm_index(np, nc)] = pbc[np] * (sq[np] / (double)(nc + 1));
+    MZ_TRY(h, dalloc(h, &h->d_pbc, pbc.size()));
+    MZ_TRY(h, dalloc(h, &h->d_sqrt, sq.size()));
+    MZ_TRY(h, dalloc(h, &h->d_aval, av.size()));
+    MZ_TRY(h, dalloc(h, &h->d_pbterm, pbt.size()));
+    MZ_TRY(h, hipMemcpy(h->d_pbc, pbc.data(), pbc.size() * 8, hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(h->d_sqrt, sq.data(), sq.size() * 8, hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(h->d_aval, av.data(), av.size() * 4, hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(h->d_pbterm, pbt.data(), pbt.size() * 8, hipMemcpyHostToDevice));
+    return 0;
+}
+
+static size_t rsearch_root_lds(const mz_handle* h) {
+    return (size_t)std::max(h->rplan[0].lds_floats, h->rplan[1].lds_floats) * 4 + 512 * 4;
+}
+static size_t rsearch_nets_lds(const mz_handle* h) {
+    return (size_t)std::max(h->rplan[1].lds_floats, h->rplan[2].lds_floats) * 4;
+}
+
 int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, int device, int max_games,
                             uint64_t rng_seed, mz_handle** out) {
     g_create_error.clear();
@@ -811,6 +849,23 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
     const size_t lmax = std::max(h->rn_lds[0], std::max(h->rn_lds[1], h->rn_lds[2]));
     CK(hipFuncSetAttribute((const void*)mz_rnet_forward_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)lmax) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(rnet)"));
+    CK(rsearch_root_lds(h) > kLdsMax ? fail(h, "ResNet root tile exceeds the LDS") : 0);
+    CK(hipFuncSetAttribute((const void*)mz_rsearch_root, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)rsearch_root_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(root)"));
+    CK(hipFuncSetAttribute((const void*)mz_rsearch_nets, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)rsearch_nets_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(nets)"));
+    // search buffers (trees and hidden states in HBM)
+    {
+        const size_t G = (size_t)max_games, S = (size_t)h->S, A = (size_t)h->A, H = (size_t)h->H;
+        h->tree_game_bytes = tree_game_bytes(h->S, h->A);
+        CK(alloc_search_tables(h));
+        CK(al(&h->d_tree, G * h->tree_game_bytes));
+        CK(al(&h->d_hid, G * (S + 1) * H));
+        CK(al(&h->d_rpath, G * 2 * (S + 2))); CK(al(&h->d_rgst, G * RG_INTS));
+        CK(al(&h->d_rxpred, G * H)); CK(al(&h->d_rov, G)); CK(al(&h->d_rologit, G * A)); CK(al(&h->d_ror, G));
+        CK(al(&h->d_obs, G * h->obs_feat)); CK(al(&h->d_legal, G * A)); CK(al(&h->d_tp, G));
+        CK(al(&h->d_cv, G * A)); CK(al(&h->d_rv, G)); CK(al(&h->d_act, G));
+    }
     CK(hipStreamSynchronize(h->stream) == hipSuccess ? 0 : fail(h, "sync"));
 #undef CK
     *out = h;
@@ -1032,12 +1087,47 @@ int mz_net_forward(mz_handle* h, int net, const float* x, int n, float* out0, fl
     return 0;
 }
 
+// ResNet search: root launch, S x (tree step, networks), final tree step
+static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_mask, const int32_t* to_play,
+                   int exploration, uint32_t rng_step, uint32_t game_offset, float temperature, float* child_visits,
+                   float* root_value, int32_t* action_out, hipStream_t st) {
+    RSearchParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.G = G; P.S = h->S; P.A = h->A; P.H = h->H; P.W = h->conf.observation_shape[0];
+    P.P = h->plane; P.players = h->conf.players; P.obs_feat = h->obs_feat; P.exploration = exploration;
+    P.rng_step = rng_step; P.game_offset = game_offset; P.seed = h->seed; P.temperature = temperature;
+    P.discount = h->conf.discount; P.dirichlet_alpha = h->conf.dirichlet_alpha;
+    P.exploration_eps = h->conf.exploration_eps;
+    P.obs = obs; P.legal = legal_mask; P.to_play = to_play;
+    P.child_visits = child_visits; P.root_value = root_value; P.action_out = action_out;
+    P.pbc_tab = h->d_pbc; P.sqrt_tab = h->d_sqrt; P.aval_tab = h->d_aval;
+    P.tree = h->d_tree; P.tree_game_bytes = h->tree_game_bytes; P.hid = h->d_hid;
+    P.path = h->d_rpath; P.gst = h->d_rgst; P.x_pred = h->d_rxpred;
+    P.o_v = h->d_rov; P.o_logit = h->d_rologit; P.o_r = h->d_ror;
+    P.ng = h->rn_ng; P.bn_s = h->bn_s; P.plans = h->d_rplan; P.Wimg = h->d_Wp; P.flat = h->d_flat;
+    void* args[] = {&P};
+    const unsigned tiles = (unsigned)((G + P.ng - 1) / P.ng), groups = (unsigned)((G + 15) / 16);
+    MZ_TRY(h, hipLaunchKernel((const void*)mz_rsearch_root, dim3(tiles), dim3(256), args, rsearch_root_lds(h), st));
+    for (int s = 0; s <= h->S; ++s) {
+        P.s = s;
+        MZ_TRY(h, hipLaunchKernel((const void*)mz_rsearch_tree, dim3(groups), dim3(256), args, 0, st));
+        if (s < h->S)
+            MZ_TRY(h, hipLaunchKernel((const void*)mz_rsearch_nets, dim3(tiles, 2), dim3(256), args,
+                                      rsearch_nets_lds(h), st));
+    }
+    h->last_variant = "mz_rsearch";
+    return 0;
+}
+
 int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* legal_mask, const int32_t* to_play,
                        int exploration, uint32_t rng_step, uint32_t game_offset, float temperature,
                        float* child_visits, float* root_value, int32_t* action_out, void* stream) {
     if (!h) return -2;
     if (G < 0 || G > h->max_games) return fail(h, "G exceeds max_games");
     if (G == 0) return 0;
+    if (h->kind == 1)
+        return rsearch(h, G, obs, legal_mask, to_play, exploration, rng_step, game_offset, temperature,
+                       child_visits, root_value, action_out, stream ? (hipStream_t)stream : h->stream);
     SearchParams P;
     std::memset(&P, 0, sizeof(P));
     P.G = G; P.S = h->S; P.A = h->A; P.H = h->H; P.players = h->conf.players; P.obs_feat = h->obs_feat;
@@ -1184,9 +1274,14 @@ static int ensure_batch(mz_handle* h, int B) {
     return 0;
 }
 
+static int rlearner_grad(mz_handle* h, const mz_batch*, float*, float*, void*) {
+    return fail(h, "the ResNet learner unroll is not built yet");
+}
+
 // forward unroll + losses + ∇ = 2θ into grad_dev (device batch pointers)
 int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, void* stream) {
     if (!h || !b) return -2;
+    if (h->kind == 1) return rlearner_grad(h, b, grad_dev, losses_dev, stream);
     const int B = b->batch_size, K = h->conf.num_unroll_steps, A = h->A;
     if (B < 1) return fail(h, "batch_size must be >= 1");
     if (ensure_batch(h, B)) return -1;

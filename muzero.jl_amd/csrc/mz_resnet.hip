@@ -133,3 +133,178 @@ extern "C" __global__ __launch_bounds__(256) void mz_rnet_forward_kernel(RNetPar
         }
     }
 }
+
+// ================================================================= search
+#include "mz_tree_device.h"
+
+__device__ __forceinline__ TreeView rs_tree(const RSearchParams& P, int gg) {
+    const int E = (P.S + 1) * P.A, NN = P.S + 1;
+    return tree_view(P.tree + (size_t)gg * P.tree_game_bytes, E, NN);
+}
+
+// Root (SelfPlay.jl:230-251): representation + prediction of NG games per
+// tile, h0 -> hidden slot 0, root expansion with the double softmax (Q3),
+// exploration noise, per-game state.
+extern "C" __global__ __launch_bounds__(256) void mz_rsearch_root(RSearchParams P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const RPlan& Rr = P.plans[MZ_NET_REPR];
+    const RPlan& Rp = P.plans[MZ_NET_PRED];
+    const int NG = P.ng, t0 = blockIdx.x * NG, H = P.H, A = P.A;
+    const int nplan = Rr.lds_floats > Rp.lds_floats ? Rr.lds_floats : Rp.lds_floats;
+    float* stg = lds + nplan;                       // [16][16] softmax / noise staging
+    float* noise = stg + 256;                       // [16][16]
+    rn_fill_ktabs(Rr, lds);
+    for (int i = threadIdx.x; i < Rr.in_feat * NG; i += blockDim.x) {
+        const int f = i / NG, g = i - f * NG;
+        lds[Rr.in_off + i] = t0 + g < P.G ? P.obs[(size_t)(t0 + g) * P.obs_feat + f] : 0.0f;
+    }
+    __syncthreads();
+    rn_run(Rr, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s);                    // :234
+    for (int i = threadIdx.x; i < H * NG; i += blockDim.x) {
+        const int f = i / NG, g = i - f * NG;
+        if (t0 + g < P.G) P.hid[(size_t)(t0 + g) * (P.S + 1) * H + f] = lds[Rr.out0_off + i];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < H * NG; i += blockDim.x) {                  // prediction input = h0
+        const int f = i / NG, g = i - f * NG;
+        lds[Rp.in_off + i] = t0 + g < P.G ? P.hid[(size_t)(t0 + g) * (P.S + 1) * H + f] : 0.0f;
+    }
+    __syncthreads();
+    rn_run(Rp, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s);                    // :239
+    const int gl = threadIdx.x >> 4, a = threadIdx.x & 15, gg = t0 + gl;
+    const bool active = gl < NG && gg < P.G;
+    if (active) {
+        uint32_t legal = 0;
+        for (int b = 0; b < A; ++b) if (P.legal[(size_t)gg * A + b]) legal |= 1u << b;
+        const uint32_t gid = P.game_offset + (uint32_t)gg;
+        TreeView tree = rs_tree(P, gg);
+        const float prior = double_softmax_prior(a < A ? lds[Rp.out1_off + a * NG + gl] : 0.0f, a, A, legal,
+                                                 stg + 16 * gl);
+        init_edges(tree, 0, a, A, prior);                                       // :245
+        if (P.exploration) {                                                    // :247-249
+            const float nz = root_noise_lane(legal, a, A, P.seed, gid, P.rng_step, P.dirichlet_alpha,
+                                             noise + 16 * gl);
+            if (a < A && ((legal >> a) & 1u))
+                tree.p(a) = tree.p(a) * (1.0f - P.exploration_eps) + nz * P.exploration_eps;
+        }
+        if (a == 0) {
+            int* st = P.gst + (size_t)gg * RG_INTS;
+            tree.nr[0] = 0.0f; tree.ntp[0] = (int8_t)P.to_play[gg];
+            st[RG_LEGAL] = (int)legal; st[RG_ROOT_TP] = P.to_play[gg];
+            st[RG_ROOTN] = 0; st[RG_ROOTW] = __float_as_int(0.0f);
+            st[RG_MMIN] = __float_as_int(INFINITY); st[RG_MMAX] = __float_as_int(-INFINITY);   // :251
+            st[RG_LEAF_E] = 0; st[RG_LEAF_A] = 0; st[RG_VTP] = 1; st[RG_DEPTH] = 0;
+        }
+    }
+}
+
+// Tree step s: expand + backup of simulation s-1 (s > 0), then select +
+// gather for simulation s (s < S), or the search statistics and the action
+// (s == S).  16 lanes per game, 16 games per workgroup.
+extern "C" __global__ __launch_bounds__(256) void mz_rsearch_tree(RSearchParams P) {
+    __shared__ float stg[256];
+    const int gl = threadIdx.x >> 4, a = threadIdx.x & 15, lane = threadIdx.x & 63;
+    const int gg = blockIdx.x * 16 + gl;
+    if (gg >= P.G) return;                          // whole 16-lane groups leave together
+    const int A = P.A, H = P.H, S = P.S, PS = 2 * (S + 2);
+    int* st = P.gst + (size_t)gg * RG_INTS;
+    int* path = P.path + (size_t)gg * PS;
+    TreeView tree = rs_tree(P, gg);
+    const uint32_t legal = (uint32_t)st[RG_LEGAL];
+    const uint32_t gid = P.game_offset + (uint32_t)gg;
+    if (P.s > 0) {
+        const int e_new = P.s;                      // the node simulation s-1 expanded (:280)
+        const float prior = double_softmax_prior(a < A ? P.o_logit[(size_t)gg * A + a] : 0.0f, a, A, legal,
+                                                 stg + 16 * gl);
+        init_edges(tree, e_new, a, A, prior);
+        const int tl = st[RG_VTP], depth = st[RG_DEPTH];
+        if (a == 0) {
+            const int li = st[RG_LEAF_E] * A + st[RG_LEAF_A];
+            tree.nc(li) = (tree.nc(li) & 0xffffu) | ((uint32_t)(e_new + 1) << 16);
+            tree.nr[e_new] = P.o_r[gg];
+            tree.ntp[e_new] = (int8_t)tl;
+            path[2 * depth + 1] = e_new;
+        }
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        int rN = st[RG_ROOTN];
+        float rW = __int_as_float(st[RG_ROOTW]);
+        float mmin = __int_as_float(st[RG_MMIN]), mmax = __int_as_float(st[RG_MMAX]);
+        backup_path(tree, path, depth, P.o_v[gg], tl, A, P.players, P.discount, rN, rW, st[RG_ROOT_TP], mmin,
+                    mmax, a);                                                   // :281
+        __builtin_amdgcn_wave_barrier();
+        if (a == 0) {
+            st[RG_ROOTN] = rN; st[RG_ROOTW] = __float_as_int(rW);
+            st[RG_MMIN] = __float_as_int(mmin); st[RG_MMAX] = __float_as_int(mmax);
+        }
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (P.s < S) {
+        const SelectOut so = select_path<false>(tree, path, st[RG_ROOTN], st[RG_ROOT_TP], legal,
+                                                __int_as_float(st[RG_MMIN]), __int_as_float(st[RG_MMAX]), a, lane,
+                                                A, P.players, P.discount, nullptr, P.pbc_tab, P.sqrt_tab, P.seed,
+                                                gid, P.rng_step, P.s);                    // :256-268
+        if (a == 0) {
+            st[RG_LEAF_E] = so.leaf_e; st[RG_LEAF_A] = so.leaf_a; st[RG_VTP] = so.vtp; st[RG_DEPTH] = so.depth;
+        }
+        // parent h -> prediction input; h *= 2 in place (Q1), read by the dynamics launch
+        float* hp = P.hid + ((size_t)gg * (S + 1) + so.leaf_e) * H;
+        float* xp = P.x_pred + (size_t)gg * H;
+        for (int k = a; k < H; k += 16) {
+            const float hv = hp[k];
+            xp[k] = hv;
+            hp[k] = hv * 2.0f;
+        }
+    } else {                                        // store_search_stats! (:115-122) + select_action (:293-306)
+        const bool lg = a < A && ((legal >> a) & 1u);
+        const int Nc = lg ? (int)(tree.nc(a) & 0xffffu) : 0;
+        const int sum = g16_isum(Nc);
+        if (a < A) P.child_visits[(size_t)gg * A + a] = lg ? (float)((double)Nc / (double)sum) : 0.0f;
+        int cnt[16];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) cnt[b] = __shfl(Nc, b, 16);
+        if (a == 0) {
+            const int rN = st[RG_ROOTN];
+            P.root_value[gg] = rN == 0 ? 0.0f : __int_as_float(st[RG_ROOTW]) / (float)rN;
+            const uint32_t r = mz_rng_u32(P.seed, MZ_RNG_ACTION, gid, P.rng_step, 0);
+            P.action_out[gg] = select_action_dev(cnt, legal, A, P.temperature, r) + 1;
+        }
+    }
+}
+
+// Networks of simulation s: blockIdx.y = 0 prediction(parent h), 1 dynamics
+// (2h ⊕ a/|A|, Q1) writing h' into hidden slot s+1.
+extern "C" __global__ __launch_bounds__(256) void mz_rsearch_nets(RSearchParams P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int net = blockIdx.y == 0 ? MZ_NET_PRED : MZ_NET_DYN;
+    const RPlan& R = P.plans[net];
+    const int NG = P.ng, t0 = blockIdx.x * NG, H = P.H, S = P.S;
+    for (int i = threadIdx.x; i < R.in_feat * NG; i += blockDim.x) {
+        const int f = i / NG, g = i - f * NG, gg = t0 + g;
+        float v = 0.0f;
+        if (gg < P.G) {
+            const int* st = P.gst + (size_t)gg * RG_INTS;
+            if (net == MZ_NET_PRED) v = P.x_pred[(size_t)gg * H + f];
+            else if (f < H) v = P.hid[((size_t)gg * (S + 1) + st[RG_LEAF_E]) * H + f];
+            else v = P.aval_tab[st[RG_LEAF_A]];
+        }
+        lds[R.in_off + i] = v;
+    }
+    __syncthreads();
+    rn_run(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s);
+    if (net == MZ_NET_PRED) {
+        for (int i = threadIdx.x; i < (1 + P.A) * NG; i += blockDim.x) {
+            const int r = i / NG, g = i - r * NG, gg = t0 + g;
+            if (gg >= P.G) continue;
+            if (r == 0) P.o_v[gg] = lds[R.out0_off + g];
+            else P.o_logit[(size_t)gg * P.A + (r - 1)] = lds[R.out1_off + (r - 1) * NG + g];
+        }
+    } else {
+        for (int i = threadIdx.x; i < H * NG; i += blockDim.x) {
+            const int f = i / NG, g = i - f * NG, gg = t0 + g;
+            if (gg < P.G) P.hid[((size_t)gg * (S + 1) + P.s + 1) * H + f] = lds[R.out0_off + i];
+        }
+        if (threadIdx.x < NG && t0 + (int)threadIdx.x < P.G) P.o_r[t0 + threadIdx.x] = lds[R.out1_off + threadIdx.x];
+    }
+}

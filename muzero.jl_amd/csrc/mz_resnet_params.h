@@ -46,3 +46,29 @@ struct RNetParams {
     const float* x;                    // (in_feat, n_items) column-major input
     float* out0; float* out1;          // (out0_n, n_items), (out1_n, n_items)
 };
+
+// Batched search with the ResNet networks: a root launch, then per
+// simulation a tree step (16 lanes per game; trees and hidden states in HBM)
+// and one network launch (prediction ‖ dynamics).  Per-game state gst[g][16]:
+// legal, root_tp, rootN, rootW, mmin, mmax, leaf_e, leaf_a, vtp, depth.
+enum { RG_LEGAL = 0, RG_ROOT_TP, RG_ROOTN, RG_ROOTW, RG_MMIN, RG_MMAX, RG_LEAF_E, RG_LEAF_A, RG_VTP, RG_DEPTH,
+       RG_INTS = 16 };
+
+struct RSearchParams {
+    int G, S, A, H, W, P, players, obs_feat, exploration, s;
+    uint32_t rng_step, game_offset;
+    uint64_t seed;
+    float temperature, discount, dirichlet_alpha, exploration_eps;
+    const float* obs; const uint8_t* legal; const int32_t* to_play;
+    float* child_visits; float* root_value; int32_t* action_out;
+    const double* pbc_tab; const double* sqrt_tab; const float* aval_tab;
+    char* tree; size_t tree_game_bytes;
+    float* hid;            // [G][S+1][H]
+    int* path;             // [G][2(S+2)]
+    int* gst;              // [G][RG_INTS]
+    float* x_pred;         // [G][H] prediction input of this simulation
+    float* o_v; float* o_logit; float* o_r;   // [G], [G][A], [G]
+    int ng; float bn_s;
+    const RPlan* plans;    // repr, pred, dyn
+    const float* Wimg; const float* flat;
+};

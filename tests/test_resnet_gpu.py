@@ -44,3 +44,33 @@ def test_resnet_forward_bitexact(rn, net, n):
         np.testing.assert_allclose(got, _torch_forward(conf, hyper, net, nets[net], x), rtol=1e-5, atol=1e-5)
     else:
         assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+
+
+@pytest.mark.parametrize("S,G,explore,temp,seed", [
+    (1, 5, True, 1.0, 1), (8, 20, True, 1.0, 2), (16, 33, False, 0.0, 3), (12, 17, True, float("inf"), 4),
+    (25, 40, True, 0.5, 5)])
+def test_resnet_search_bitexact(ttt, S, G, explore, temp, seed):
+    """Batched search with the ResNet nets (root launch, S x (tree step,
+    networks), final step) against the oracle: trees, visits, values, actions."""
+    import dataclasses
+    from conftest import random_positions
+    from muzero_jl_amd import abi
+    from test_gpu_parity import _compare_trees
+    conf = dataclasses.replace(ttt.conf, num_iters=S)
+    o, nets = _resnet_oracle(conf, ttt.resnet_hyper, seed=seed)
+    nets = _perturb_bn(conf, ttt.resnet_hyper, nets, seed=seed)
+    eng = abi.Engine(conf, ttt.resnet_hyper, device=0, max_games=G, rng_seed=o.seed)
+    for n, w in enumerate(nets):
+        o.set_weights(n, w)
+        eng.set_weights(n, w)
+    obs, legal, tp = random_positions(G, 40 + seed)
+    eng.debug_enable(1)
+    cv, rv, act = eng.mcts_search(obs, legal, tp, exploration=explore, rng_step=seed * 7, game_offset=11,
+                                  temperature=temp)
+    assert eng.search_variant() == "mz_rsearch"
+    tree_g = eng.debug_tree(G)
+    cv2, rv2, act2, tree_o, _ = o.mcts_search(obs, legal, tp, exploration=explore, rng_step=seed * 7,
+                                              game_offset=11, temperature=temp, dump=True)
+    _compare_trees(tree_g, tree_o, G)
+    assert np.array_equal(cv, cv2) and np.array_equal(rv, rv2) and np.array_equal(act, act2)
+    eng.close()
