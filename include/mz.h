@@ -169,6 +169,13 @@ int mz_debug_enable(mz_handle* h, int flags);
 int mz_debug_tree(mz_handle* h, int G, int32_t* edge_N, float* edge_W, float* edge_P,
                   float* edge_R, int32_t* edge_child, int32_t* node_to_play);
 
+/* Debug/parity: the last learner unroll's read-outs (Learning.jl:347-370)
+ * for its first B samples: values (K+1, B) and rewards (K+1, B) after their
+ * activations, policies (A, K+1, B) as probabilities — the predictions the
+ * loss reads (Q10 alignment: step 0 and step 1 both predict from h0,
+ * reward 0 at step 0).  Any pointer may be NULL.                          */
+int mz_debug_unroll(mz_handle* h, int B, float* values, float* policies, float* rewards);
+
 /* One learner batch, the tuple returned by get_batch (ReplayBuffer.jl:216),
  * column-major as in the reference:
  *   observation (W,H,Cs,B), actions (K+1,B) as float action ids,

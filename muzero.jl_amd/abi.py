@@ -50,6 +50,7 @@ SIGNATURES = {
                                           ctypes.c_uint32, ctypes.c_float, _VP, _VP, _VP, _VP]),
     "mz_debug_enable": (ctypes.c_int, [_VP, ctypes.c_int]),
     "mz_debug_tree": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "mz_debug_unroll": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP]),
     "mz_learner_step": (ctypes.c_int, [_VP, ctypes.POINTER(MzBatch), ctypes.c_double, _VP]),
     "mz_grad_count": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_size_t)]),
     "mz_learner_grad_dev": (ctypes.c_int, [_VP, ctypes.POINTER(MzBatch), _VP, _VP, _VP]),
@@ -190,6 +191,16 @@ class Engine:
         self._check(self.lib.mz_debug_tree(self.h, G, _p(eN), _p(eW), _p(eP), _p(eR), _p(eC), _p(ntp)),
                     "mz_debug_tree")
         return dict(N=eN, W=eW, P=eP, R=eR, C=eC, to_play=ntp)
+
+    def debug_unroll(self, B):
+        """Read-outs of the last learner unroll: values (B, K+1), policies
+        (B, K+1, A) as probabilities, rewards (B, K+1)."""
+        K1 = self.conf.num_unroll_steps + 1
+        pv = np.empty((B, K1), np.float32)
+        pp = np.empty((B, K1, self.A), np.float32)
+        pr = np.empty((B, K1), np.float32)
+        self._check(self.lib.mz_debug_unroll(self.h, B, _p(pv), _p(pp), _p(pr)), "mz_debug_unroll")
+        return pv, pp, pr
 
     # ---- learner
     def learner_step(self, batch, eta):

@@ -29,6 +29,7 @@ extern "C" __global__ void mz_rnet_forward_kernel(RNetParams Q);
 extern "C" __global__ void mz_rsearch_root(RSearchParams P);
 extern "C" __global__ void mz_rsearch_tree(RSearchParams P);
 extern "C" __global__ void mz_rsearch_nets(RSearchParams P);
+extern "C" __global__ void mz_runroll_kernel(RUnrollParams U);
 extern "C" __global__ void mz_search_small1(SmallParams P);
 extern "C" __global__ void mz_search_small2(SmallParams P);
 extern "C" __global__ void mz_search_small4(SmallParams P);
@@ -100,6 +101,7 @@ struct mz_handle {
     float bn_s = 1.0f;
     int* d_rpath = nullptr; int* d_rgst = nullptr;          // ResNet search: [G][2(S+2)], [G][RG_INTS]
     float* d_rxpred = nullptr; float* d_rov = nullptr; float* d_rologit = nullptr; float* d_ror = nullptr;
+    float* d_rhs = nullptr;                 // [bcap][H] learner unroll scratch (h between the nets)
     int device = 0, max_games = 0;
     uint64_t seed = 0;
     std::string err;
@@ -764,6 +766,19 @@ static int alloc_search_tables(mz_handle* h) {
     return 0;
 }
 
+// loss / Σθ² scratch, per-net offsets and the last-block counter of
+// mz_learner_grad_kernel
+static int alloc_learner(mz_handle* h) {
+    MZ_TRY(h, dalloc(h, &h->d_loss, 8));
+    MZ_TRY(h, dalloc(h, &h->d_sq, 3 * MZ_L2_BLOCKS));
+    size_t oc[6] = {h->flat_off[0], h->flat_off[1], h->flat_off[2], h->nparams[0], h->nparams[1], h->nparams[2]};
+    MZ_TRY(h, dalloc(h, &h->d_netoff, 6));
+    MZ_TRY(h, dalloc(h, &h->d_counter, 1));
+    MZ_TRY(h, hipMemset(h->d_counter, 0, 4));
+    MZ_TRY(h, hipMemcpy(h->d_netoff, oc, sizeof(oc), hipMemcpyHostToDevice));
+    return 0;
+}
+
 static size_t rsearch_root_lds(const mz_handle* h) {
     return (size_t)std::max(h->rplan[0].lds_floats, h->rplan[1].lds_floats) * 4 + 512 * 4;
 }
@@ -846,12 +861,15 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
     CK(al(&h->d_m, h->nflat)); CK(al(&h->d_v, h->nflat)); CK(al(&h->d_grad, h->nflat));
     CK(hipMemset(h->d_m, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
     CK(hipMemset(h->d_v, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
+    CK(alloc_learner(h));
     const size_t lmax = std::max(h->rn_lds[0], std::max(h->rn_lds[1], h->rn_lds[2]));
     CK(hipFuncSetAttribute((const void*)mz_rnet_forward_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)lmax) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(rnet)"));
     CK(rsearch_root_lds(h) > kLdsMax ? fail(h, "ResNet root tile exceeds the LDS") : 0);
     CK(hipFuncSetAttribute((const void*)mz_rsearch_root, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)rsearch_root_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(root)"));
+    CK(hipFuncSetAttribute((const void*)mz_runroll_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)lmax) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll)"));
     CK(hipFuncSetAttribute((const void*)mz_rsearch_nets, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)rsearch_nets_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(nets)"));
     // search buffers (trees and hidden states in HBM)
@@ -874,9 +892,9 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
 
 void mz_engine_destroy(mz_handle* h) {
     if (!h) return;
-    hipSetDevice(h->device);
-    for (void* p : h->allocs) hipFree(p);
-    if (h->stream) hipStreamDestroy(h->stream);
+    (void)hipSetDevice(h->device);
+    for (void* p : h->allocs) (void)hipFree(p);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
 
@@ -975,14 +993,7 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
     CK(al(&h->d_m, h->nflat)); CK(al(&h->d_v, h->nflat)); CK(al(&h->d_grad, h->nflat));
     CK(hipMemset(h->d_m, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
     CK(hipMemset(h->d_v, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
-    CK(al(&h->d_loss, 8)); CK(al(&h->d_sq, 3 * MZ_L2_BLOCKS));
-    {
-        size_t oc[6] = {h->flat_off[0], h->flat_off[1], h->flat_off[2], h->nparams[0], h->nparams[1], h->nparams[2]};
-        CK(al(&h->d_netoff, 6));
-        CK(al(&h->d_counter, 1));
-        CK(hipMemset(h->d_counter, 0, 4) == hipSuccess ? 0 : fail(h, "memset"));
-        CK(hipMemcpy(h->d_netoff, oc, sizeof(oc), hipMemcpyHostToDevice) == hipSuccess ? 0 : fail(h, "copy"));
-    }
+    CK(alloc_learner(h));
     h->use_res = h->d_plan_sim_res != nullptr && std::getenv("MZ_NO_RESIDENT") == nullptr;
     {
         const search_fn ks[4] = {mz_search_kernel_lds, mz_search_kernel_hbm, mz_search_kernel_lds_res,
@@ -1036,7 +1047,7 @@ static int rnet_forward(mz_handle* h, int net, const float* x, int n, float* out
     MZ_TRY(h, hipMalloc(&dx, (size_t)n * R.in_feat * 4));
     MZ_TRY(h, hipMalloc(&d0, (size_t)n * R.out0_n * 4));
     MZ_TRY(h, hipMalloc(&d1, (size_t)n * std::max(R.out1_n, 1) * 4));
-    hipMemcpyAsync(dx, x, (size_t)n * R.in_feat * 4, hipMemcpyHostToDevice, h->stream);
+    (void)hipMemcpyAsync(dx, x, (size_t)n * R.in_feat * 4, hipMemcpyHostToDevice, h->stream);
     RNetParams Q;
     Q.ng = h->rn_ng; Q.W = h->conf.observation_shape[0]; Q.H = h->conf.observation_shape[1];
     Q.P = Q.W * Q.H; Q.n_items = n; Q.softmax1 = net == MZ_NET_PRED; Q.bn_s = h->bn_s;
@@ -1044,10 +1055,10 @@ static int rnet_forward(mz_handle* h, int net, const float* x, int n, float* out
     void* args[] = {&Q};
     hipError_t le = hipLaunchKernel((const void*)mz_rnet_forward_kernel, dim3((n + Q.ng - 1) / Q.ng), dim3(256),
                                     args, h->rn_lds[net], h->stream);
-    hipMemcpyAsync(out0, d0, (size_t)n * R.out0_n * 4, hipMemcpyDeviceToHost, h->stream);
-    if (out1 && R.out1_n) hipMemcpyAsync(out1, d1, (size_t)n * R.out1_n * 4, hipMemcpyDeviceToHost, h->stream);
+    (void)hipMemcpyAsync(out0, d0, (size_t)n * R.out0_n * 4, hipMemcpyDeviceToHost, h->stream);
+    if (out1 && R.out1_n) (void)hipMemcpyAsync(out1, d1, (size_t)n * R.out1_n * 4, hipMemcpyDeviceToHost, h->stream);
     hipError_t se = hipStreamSynchronize(h->stream);
-    hipFree(dx); hipFree(d0); hipFree(d1);
+    (void)hipFree(dx); (void)hipFree(d0); (void)hipFree(d1);
     MZ_TRY(h, le);
     MZ_TRY(h, se);
     return 0;
@@ -1071,17 +1082,17 @@ int mz_net_forward(mz_handle* h, int net, const float* x, int n, float* out0, fl
     MZ_TRY(h, hipMalloc(&dx, (size_t)n * in_feat * 4));
     MZ_TRY(h, hipMalloc(&d0, (size_t)n * o0 * 4));
     MZ_TRY(h, hipMalloc(&d1, (size_t)n * o1 * 4));
-    hipMemcpyAsync(dx, x, (size_t)n * in_feat * 4, hipMemcpyHostToDevice, h->stream);
+    (void)hipMemcpyAsync(dx, x, (size_t)n * in_feat * 4, hipMemcpyHostToDevice, h->stream);
     hipLaunchKernelGGL(mz_forward_kernel, dim3((n + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
                        (size_t)h->lay.total * 4, h->stream, h->d_plan[net], h->d_Wp, h->d_Bp, h->lay.total, in_off,
                        in_feat, dx, n, o0_off, o0, d0, o1_off, o1, net == MZ_NET_REPR ? nullptr : d1,
                        net == MZ_NET_PRED ? 1 : 0, net == MZ_NET_PRED ? h->lay.v_act : MZ_ACT_IDENTITY,
                        net == MZ_NET_DYN ? h->lay.r_act : MZ_ACT_IDENTITY);
     hipError_t le = hipGetLastError();
-    hipMemcpyAsync(out0, d0, (size_t)n * o0 * 4, hipMemcpyDeviceToHost, h->stream);
-    if (out1 && net != MZ_NET_REPR) hipMemcpyAsync(out1, d1, (size_t)n * o1 * 4, hipMemcpyDeviceToHost, h->stream);
+    (void)hipMemcpyAsync(out0, d0, (size_t)n * o0 * 4, hipMemcpyDeviceToHost, h->stream);
+    if (out1 && net != MZ_NET_REPR) (void)hipMemcpyAsync(out1, d1, (size_t)n * o1 * 4, hipMemcpyDeviceToHost, h->stream);
     hipError_t se = hipStreamSynchronize(h->stream);
-    hipFree(dx); hipFree(d0); hipFree(d1);
+    (void)hipFree(dx); (void)hipFree(d0); (void)hipFree(d1);
     MZ_TRY(h, le);
     MZ_TRY(h, se);
     return 0;
@@ -1270,12 +1281,34 @@ static int ensure_batch(mz_handle* h, int B) {
                       (size_t)B * (K + 1)};
     for (int i = 0; i < 9; ++i) MZ_TRY(h, dalloc(h, bufs[i], sizes[i]));
     MZ_TRY(h, dalloc(h, &h->d_lterm, (size_t)2 * B * (K + 1)));
+    if (h->kind == 1) MZ_TRY(h, dalloc(h, &h->d_rhs, (size_t)B * h->H));
     h->bcap = B;
     return 0;
 }
 
-static int rlearner_grad(mz_handle* h, const mz_batch*, float*, float*, void*) {
-    return fail(h, "the ResNet learner unroll is not built yet");
+static size_t runroll_lds(const mz_handle* h) {
+    return std::max(h->rn_lds[0], std::max(h->rn_lds[1], h->rn_lds[2]));
+}
+
+static int learner_losses(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, hipStream_t st,
+                          int v_act, int r_act);
+
+// ResNet learner: the unroll on the network kernels, then the shared loss /
+// ∇ = 2θ kernel (the plans' outputs are already activated)
+static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, void* stream) {
+    const int B = b->batch_size;
+    if (B < 1) return fail(h, "batch_size must be >= 1");
+    if (ensure_batch(h, B)) return -1;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    RUnrollParams U;
+    U.B = B; U.K = h->conf.num_unroll_steps; U.A = h->A; U.H = h->H;
+    U.W = h->conf.observation_shape[0]; U.P = h->plane; U.obs_feat = h->obs_feat; U.ng = h->rn_ng; U.bn_s = h->bn_s;
+    U.obs = b->observation; U.actions = b->actions; U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
+    U.hs = h->d_rhs; U.plans = h->d_rplan; U.Wimg = h->d_Wp; U.flat = h->d_flat;
+    void* args[] = {&U};
+    MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_kernel, dim3((B + U.ng - 1) / U.ng), dim3(256), args,
+                              runroll_lds(h), st));
+    return learner_losses(h, b, grad_dev, losses_dev, st, MZ_ACT_IDENTITY, MZ_ACT_IDENTITY);
 }
 
 // forward unroll + losses + ∇ = 2θ into grad_dev (device batch pointers)
@@ -1319,11 +1352,18 @@ int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float*
         hipLaunchKernelGGL(mz_unroll_kernel, dim3((B + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
                            (size_t)h->lay.total * 4, st, U);
     }
+    return learner_losses(h, b, grad_dev, losses_dev, st, h->lay.v_act, h->lay.r_act);
+}
+
+// losses + ∇ = 2θ from the unroll outputs in d_pv / d_pp / d_pr
+static int learner_losses(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, hipStream_t st,
+                          int v_act, int r_act) {
+    const int B = b->batch_size, K = h->conf.num_unroll_steps, A = h->A;
     float* lo = losses_dev ? losses_dev : h->d_loss;
     float* g = grad_dev ? grad_dev : h->d_grad;
     const int nlb = (B * (K + 1) + MZ_THREADS / 16 - 1) / (MZ_THREADS / 16);
     hipLaunchKernelGGL(mz_learner_grad_kernel, dim3(nlb + 3 * MZ_L2_BLOCKS), dim3(MZ_THREADS), 0, st, B, K, A,
-                       h->lay.v_act, h->lay.r_act, h->d_pv, h->d_pp, h->d_pr, b->target_values, b->target_policies,
+                       v_act, r_act, h->d_pv, h->d_pp, h->d_pr, b->target_values, b->target_policies,
                        b->gradient_scale, h->d_lterm, h->d_flat, h->d_netoff, g, h->d_sq, h->d_counter, lo);
     MZ_TRY(h, hipGetLastError());
     return 0;
@@ -1364,6 +1404,18 @@ int mz_learner_step(mz_handle* h, const mz_batch* b, double eta, float* losses_o
     if (rc) return rc;
     if (losses_out) MZ_TRY(h, hipMemcpyAsync(losses_out, h->d_loss, 6 * 4, hipMemcpyDeviceToHost, st));
     MZ_TRY(h, hipStreamSynchronize(st));
+    return 0;
+}
+
+int mz_debug_unroll(mz_handle* h, int B, float* values, float* policies, float* rewards) {
+    if (!h) return -2;
+    if (B < 0 || B > h->bcap) return fail(h, "B exceeds the last learner batch");
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    const size_t n = (size_t)B * (h->conf.num_unroll_steps + 1);
+    if (values) MZ_TRY(h, hipMemcpy(values, h->d_pv, n * 4, hipMemcpyDeviceToHost));
+    if (policies) MZ_TRY(h, hipMemcpy(policies, h->d_pp, n * h->A * 4, hipMemcpyDeviceToHost));
+    if (rewards) MZ_TRY(h, hipMemcpy(rewards, h->d_pr, n * 4, hipMemcpyDeviceToHost));
     return 0;
 }
 

@@ -280,6 +280,7 @@ extern "C" __global__ __launch_bounds__(256) void mz_rsearch_nets(RSearchParams 
     const int net = blockIdx.y == 0 ? MZ_NET_PRED : MZ_NET_DYN;
     const RPlan& R = P.plans[net];
     const int NG = P.ng, t0 = blockIdx.x * NG, H = P.H, S = P.S;
+    rn_fill_ktabs(R, lds);
     for (int i = threadIdx.x; i < R.in_feat * NG; i += blockDim.x) {
         const int f = i / NG, g = i - f * NG, gg = t0 + g;
         float v = 0.0f;
@@ -306,5 +307,66 @@ extern "C" __global__ __launch_bounds__(256) void mz_rsearch_nets(RSearchParams 
             if (gg < P.G) P.hid[((size_t)gg * (S + 1) + P.s + 1) * H + f] = lds[R.out0_off + i];
         }
         if (threadIdx.x < NG && t0 + (int)threadIdx.x < P.G) P.o_r[t0 + threadIdx.x] = lds[R.out1_off + threadIdx.x];
+    }
+}
+
+// ================================================================ learner
+// Forward unroll of the learner (Learning.jl:347-370): representation, then
+// for i = 1..K prediction(h_{i-1}) -> step i (step 0 is the same prediction of
+// h0, written once for both), dynamics(2h ⊕ a_i/|A|) -> h_i, r_i; r_0 = 0.
+extern "C" __global__ __launch_bounds__(256) void mz_runroll_kernel(RUnrollParams U) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const RPlan& Rr = U.plans[MZ_NET_REPR];
+    const RPlan& Rp = U.plans[MZ_NET_PRED];
+    const RPlan& Rd = U.plans[MZ_NET_DYN];
+    const int NG = U.ng, t0 = blockIdx.x * NG, H = U.H, A = U.A, K1 = U.K + 1;
+    rn_fill_ktabs(Rr, lds);
+    for (int i = threadIdx.x; i < Rr.in_feat * NG; i += blockDim.x) {
+        const int f = i / NG, g = i - f * NG;
+        lds[Rr.in_off + i] = t0 + g < U.B ? U.obs[(size_t)(t0 + g) * U.obs_feat + f] : 0.0f;
+    }
+    __syncthreads();
+    rn_run(Rr, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                     // :347
+    for (int i = threadIdx.x; i < H * NG; i += blockDim.x) {
+        const int f = i / NG, g = i - f * NG;
+        if (t0 + g < U.B) U.hs[(size_t)(t0 + g) * H + f] = lds[Rr.out0_off + i];
+    }
+    if (threadIdx.x < NG && t0 + (int)threadIdx.x < U.B) U.pr[(size_t)(t0 + threadIdx.x) * K1] = 0.0f;
+    const int ns = U.K > 0 ? U.K : 1;              // K = 0: the prediction of h0 alone
+    for (int s = 1; s <= ns; ++s) {
+        __syncthreads();
+        rn_fill_ktabs(Rp, lds);
+        for (int i = threadIdx.x; i < H * NG; i += blockDim.x) {
+            const int f = i / NG, g = i - f * NG;
+            lds[Rp.in_off + i] = t0 + g < U.B ? U.hs[(size_t)(t0 + g) * H + f] : 0.0f;
+        }
+        __syncthreads();
+        rn_run(Rp, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                 // :351 / :356
+        for (int i = threadIdx.x; i < (1 + A) * NG; i += blockDim.x) {
+            const int r = i / NG, g = i - r * NG, b = t0 + g;
+            if (b >= U.B) continue;
+            const float v = r == 0 ? lds[Rp.out0_off + g] : lds[Rp.out1_off + (r - 1) * NG + g];
+            for (int j = s == 1 ? 0 : s; j <= (s <= U.K ? s : 0); ++j) {
+                if (r == 0) U.pv[(size_t)b * K1 + j] = v;
+                else U.pp[((size_t)b * K1 + j) * A + (r - 1)] = v;
+            }
+        }
+        if (s > U.K) break;
+        __syncthreads();
+        rn_fill_ktabs(Rd, lds);
+        for (int i = threadIdx.x; i < Rd.in_feat * NG; i += blockDim.x) {     // make_dynamics_input (:293-304)
+            const int f = i / NG, g = i - f * NG, b = t0 + g;
+            float v = 0.0f;
+            if (b < U.B) v = f < H ? U.hs[(size_t)b * H + f] * 2.0f : U.actions[(size_t)b * K1 + (s - 1)] / (float)A;
+            lds[Rd.in_off + i] = v;
+        }
+        __syncthreads();
+        rn_run(Rd, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                 // :362
+        for (int i = threadIdx.x; i < H * NG; i += blockDim.x) {
+            const int f = i / NG, g = i - f * NG;
+            if (t0 + g < U.B) U.hs[(size_t)(t0 + g) * H + f] = lds[Rd.out0_off + i];
+        }
+        if (threadIdx.x < NG && t0 + (int)threadIdx.x < U.B)
+            U.pr[(size_t)(t0 + threadIdx.x) * K1 + s] = lds[Rd.out1_off + threadIdx.x];
     }
 }

@@ -72,3 +72,17 @@ struct RSearchParams {
     const RPlan* plans;    // repr, pred, dyn
     const float* Wimg; const float* flat;
 };
+
+// Learner unroll with the ResNet networks (Learning.jl:347-370, Q10): per
+// tile of NG samples, representation, then K x (prediction(h), dynamics(2h ⊕
+// a/|A|)); h is handed between the nets through hs.  Raw outputs as the FC
+// unroll: value / reward already activated, policy logits.
+struct RUnrollParams {
+    int B, K, A, H, W, P, obs_feat, ng;
+    float bn_s;
+    const float* obs; const float* actions;
+    float* pv; float* pp; float* pr;   // (K+1, B), (A, K+1, B), (K+1, B)
+    float* hs;                         // [B][H] scratch
+    const RPlan* plans;
+    const float* Wimg; const float* flat;
+};

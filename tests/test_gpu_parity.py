@@ -154,7 +154,7 @@ def _random_batch(B, K, A, rng):
     tr = rng.uniform(-1, 1, (B, K + 1)).astype(np.float32)
     tpol = rng.random((B, K + 1, A)).astype(np.float32)
     tpol /= tpol.sum(-1, keepdims=True)
-    gs = rng.integers(1, K + 1, B).astype(np.float32)
+    gs = rng.integers(1, max(K, 1) + 1, B).astype(np.float32)
     return dict(observation=obs, actions=acts, target_values=tv, target_rewards=tr, target_policies=tpol,
                 gradient_scale=gs)
 
@@ -169,8 +169,11 @@ def test_learner_steps_bitexact(ttt, nets, B):
     for t in range(1, 13):
         batch = _random_batch(B, conf.num_unroll_steps, 9, rng)
         eta = cos_schedule(t)
+        want = ora.unroll(batch["observation"], batch["actions"])
         lg = eng.learner_step(batch, eta)
         lo = ora.learner_step(st, batch, eta)
+        for g, o in zip(eng.debug_unroll(B), want):          # the unroll's read-outs, bit for bit
+            assert np.array_equal(g, o), f"step {t} unroll differs"
         np.testing.assert_allclose(lg, lo, rtol=2e-5, atol=1e-6)
         for n in range(3):
             assert np.array_equal(eng.get_weights(n), ora.params[n]), f"step {t} net {n} params differ"

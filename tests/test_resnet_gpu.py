@@ -74,3 +74,35 @@ def test_resnet_search_bitexact(ttt, S, G, explore, temp, seed):
     _compare_trees(tree_g, tree_o, G)
     assert np.array_equal(cv, cv2) and np.array_equal(rv, rv2) and np.array_equal(act, act2)
     eng.close()
+
+
+@pytest.mark.parametrize("B,K", [(20, 5), (33, 3), (7, 0)])
+def test_resnet_learner_steps(ttt, B, K):
+    """ResNet learner (unroll on the network kernels + the shared loss/∇ = 2θ
+    kernel + ADAM): the unroll's read-outs bit-exact against ora_unroll, the
+    losses within the f64 cross-sample tolerance, parameters bit-exact."""
+    import dataclasses
+    from muzero_jl_amd import abi
+    from muzero_jl_amd.config import cos_schedule
+    from test_gpu_parity import _random_batch
+    conf = dataclasses.replace(ttt.conf, batch_size=B, num_unroll_steps=K)
+    o, nets = _resnet_oracle(conf, ttt.resnet_hyper, seed=B)
+    nets = _perturb_bn(conf, ttt.resnet_hyper, nets, seed=K)
+    eng = abi.Engine(conf, ttt.resnet_hyper, device=0, max_games=8, rng_seed=1)
+    for n, w in enumerate(nets):
+        o.set_weights(n, w)
+        eng.set_weights(n, w)
+    st = o.learner_state()
+    rng = np.random.default_rng(B + K)
+    for t in range(1, 5):
+        batch = _random_batch(B, K, 9, rng)
+        eta = cos_schedule(t)
+        want = o.unroll(batch["observation"], batch["actions"])
+        lg = eng.learner_step(batch, eta)
+        lo = o.learner_step(st, batch, eta)
+        for g, w in zip(eng.debug_unroll(B), want):
+            assert np.array_equal(g, w), f"step {t} unroll differs"
+        np.testing.assert_allclose(lg, lo, rtol=2e-5, atol=1e-6)
+        for n in range(3):
+            assert np.array_equal(eng.get_weights(n), o.params[n]), f"step {t} net {n} params differ"
+    eng.close()
