@@ -1,12 +1,17 @@
 """bench.py — MCTS node-expansions/s (+ learner steps/s) on MI355X.
 
-Workload (BASELINE.json configs[1]): TicTacToe FC net (games/tictactoe/
-params.jl hyper, 74,881 fp32 params, random glorot init), 512 concurrent
-games per GPU, 50 simulations per move.  One step = one batched run_mcts +
-select_action over the 512 games (a single search-kernel launch) from real
-TicTacToe positions already resident in HBM; each step uses a fresh RNG step
-key.  Multi-GPU: games shard across ranks (no data-path collective) ->
-"scaling": "weak"; the learner leg all-reduces its gradient bucket over RCCL.
+Workload (default, BASELINE.json configs[1]): TicTacToe FC net (games/
+tictactoe/params.jl hyper, 74,881 fp32 params, random glorot init), 512
+concurrent games per GPU, 50 simulations per move.  One step = one batched
+run_mcts + select_action over the 512 games (a single search-kernel launch)
+from real TicTacToe positions already resident in HBM; each step uses a fresh
+RNG step key.  `--net resnet` measures configs[2] instead: the ResNet path
+(Constructors.jl ResNetHP, 2 blocks x 64 filters) on 2048 games, the search
+being a root launch + 50 x (tree step, network launch) + a final tree step;
+its roofline is the network kernel's, timed by the engine's own HIP events on
+the launch stream.  Multi-GPU: games shard across ranks (no data-path
+collective) -> "scaling": "weak"; the learner leg all-reduces its gradient
+bucket over RCCL.
 
 Prints ONE JSON line on rank 0.
 """
@@ -29,24 +34,22 @@ import _mzpkg  # noqa: E402
 
 _mzpkg.load()
 from muzero_jl_amd.abi import Engine  # noqa: E402
-from muzero_jl_amd.config import cos_schedule, to_c_config, to_c_ffhp  # noqa: E402
+from muzero_jl_amd.config import cos_schedule, to_c_config, to_c_ffhp, to_c_resnet_hp  # noqa: E402
 from muzero_jl_amd.games import tictactoe as ttt  # noqa: E402
-from muzero_jl_amd.networks import init_nets  # noqa: E402
+from muzero_jl_amd.networks import init_nets, net_macs  # noqa: E402
 from muzero_jl_amd.selfplay import random_positions  # noqa: E402
 
 METRIC = "self-play MCTS node-expansions/sec + train steps/sec, TicTacToe FC net, 1-8 GPU"
-F_EXP = 2 * (22848 + 32768)          # FLOP per expansion: prediction + dynamics
-F_ROOT = 2 * (18048 + 22848)         # FLOP per root: representation + prediction
 PEAK_F32 = 157.3                     # TFLOP/s, MI355X_MICROARCH.md (f32 MFMA = f32 vector peak)
 
 
-def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0):
+def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0, resnet=False):
     """The oracle (C restatement of the reference semantics, 1 thread) on a
     bounded sample of the same workload: 32-game batches of the same
     positions, 50 sims/move, until `budget_s` of CPU time has been spent."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import Oracle
-    o = Oracle(to_c_config(conf), to_c_ffhp(hyper), seed=1)
+    o = Oracle(to_c_config(conf), to_c_resnet_hp(hyper) if resnet else to_c_ffhp(hyper), seed=1)
     for n, w in enumerate(nets):
         o.set_weights(n, w)
     n_games, t0, step = 0, time.perf_counter(), 0
@@ -66,7 +69,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--games", type=int, default=512)
+    ap.add_argument("--net", choices=["fc", "resnet"], default="fc")
+    ap.add_argument("--games", type=int, default=None, help="games per GPU (fc 512, resnet 2048)")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--learner-steps", type=int, default=50)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -84,9 +88,10 @@ def main():
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
 
+    resnet = args.net == "resnet"
     conf = dataclasses.replace(ttt.conf, num_iters=args.sims)
-    hyper = ttt.hyper
-    G, S = args.games, args.sims
+    hyper = ttt.resnet_hyper if resnet else ttt.hyper
+    G, S = args.games or (2048 if resnet else 512), args.sims
     nets = init_nets(conf, hyper, seed=1234)              # identical replicas on every rank
     eng = Engine(conf, hyper, device=local, max_games=G, rng_seed=1)
     for n, w in enumerate(nets):
@@ -123,6 +128,17 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if resnet:
+        # the dominant kernel is the network launch (S per search): time it
+        # with the engine's events on the launch stream over 3 more searches
+        eng.debug_enable(2)
+        eng.debug_kernel_time()
+        for k in range(3):
+            step(args.warmup + args.steps + k)
+        torch.cuda.synchronize()
+        t_ms, n_l = eng.debug_kernel_time()
+        eng.debug_enable(0)
+        kern_ms = t_ms / n_l
     assert np.all(legal[np.arange(G), d_act.cpu().numpy() - 1]), "illegal action selected"
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -166,11 +182,17 @@ def main():
     if rank == 0:
         total_exp = world * G * S * args.steps
         value = total_exp / elapsed
-        flop_launch = G * S * F_EXP + G * F_ROOT
+        f_exp = 2 * (net_macs(conf, hyper, 1) + net_macs(conf, hyper, 2))   # prediction + dynamics
+        f_root = 2 * (net_macs(conf, hyper, 0) + net_macs(conf, hyper, 1))  # representation + prediction
+        # FC: one launch is the whole search; ResNet: one network launch = one
+        # simulation's prediction + dynamics over the G games
+        flop_launch = G * f_exp if resnet else G * S * f_exp + G * f_root
         achieved = flop_launch / (kern_ms * 1e-3) / 1e12
         # HBM bytes per launch from the committed PMC summary of THIS kernel
         # variant (tools/pmc_summary.py; latest round wins), else null
         traffic, variant = None, eng.search_variant()
+        if resnet:
+            variant = "mz_rsearch_nets"
         for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
             with open(pmc) as f:
                 rec = json.load(f)
@@ -178,13 +200,15 @@ def main():
                 traffic = rec.get("hbm_bytes_per_launch")
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(conf, hyper, nets, obs, legal, tp, args.cpu_budget)
+            cpu = cpu_baseline(conf, hyper, nets, obs, legal, tp, args.cpu_budget, resnet)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "node-expansions/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: random-play TicTacToe positions, random glorot weights",
-            "config": {"workload": f"TicTacToe FC (params.jl hyper), {G} games/GPU x {S} sims/move (configs[1])",
+            "config": {"workload": (f"TicTacToe ResNet (2 blocks x 64 filters, 3x3), {G} games/GPU x {S} sims/move "
+                                    f"(configs[2])") if resnet else
+                                   f"TicTacToe FC (params.jl hyper), {G} games/GPU x {S} sims/move (configs[1])",
                        "games_per_gpu": G, "sims_per_move": S, "global_games": G * world,
                        "parallelism": f"games sharded x{world}, learner dp{world} (RCCL all-reduce)"},
             "learner_steps_per_s": round(learner_sps, 1),

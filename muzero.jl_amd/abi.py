@@ -51,6 +51,7 @@ SIGNATURES = {
     "mz_debug_enable": (ctypes.c_int, [_VP, ctypes.c_int]),
     "mz_debug_tree": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP]),
     "mz_debug_unroll": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP]),
+    "mz_debug_kernel_time": (ctypes.c_int, [_VP, _VP, _VP]),
     "mz_learner_step": (ctypes.c_int, [_VP, ctypes.POINTER(MzBatch), ctypes.c_double, _VP]),
     "mz_grad_count": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_size_t)]),
     "mz_learner_grad_dev": (ctypes.c_int, [_VP, ctypes.POINTER(MzBatch), _VP, _VP, _VP]),
@@ -191,6 +192,12 @@ class Engine:
         self._check(self.lib.mz_debug_tree(self.h, G, _p(eN), _p(eW), _p(eP), _p(eR), _p(eC), _p(ntp)),
                     "mz_debug_tree")
         return dict(N=eN, W=eW, P=eP, R=eR, C=eC, to_play=ntp)
+
+    def debug_kernel_time(self):
+        """(summed ms, launches) of the timed network launches since the last call."""
+        t, n = ctypes.c_double(), ctypes.c_int()
+        self._check(self.lib.mz_debug_kernel_time(self.h, ctypes.byref(t), ctypes.byref(n)), "mz_debug_kernel_time")
+        return t.value, n.value
 
     def debug_unroll(self, B):
         """Read-outs of the last learner unroll: values (B, K+1), policies

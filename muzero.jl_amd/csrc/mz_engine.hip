@@ -122,6 +122,8 @@ struct mz_handle {
     double* d_pbc = nullptr; double* d_sqrt = nullptr; float* d_aval = nullptr;
     double* d_pbterm = nullptr;             // pbc(Np) * (sqrt(Np) / (Nc + 1)), triangle
     char* d_tree = nullptr; size_t tree_game_bytes = 0; bool lds_tree = false; int dump_tree = 0;
+    int time_nets = 0;                      // mz_debug_enable flag 2: events around each ResNet nets launch
+    std::vector<hipEvent_t> tev; size_t tev_used = 0;
     bool use_res = false;                   // register-resident sim-plan kernel
     // small-batch kernel (mz_small.hip): schedule images + LDS layout
     bool small_ok = false;
@@ -893,6 +895,7 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
 void mz_engine_destroy(mz_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
     for (void* p : h->allocs) (void)hipFree(p);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -1122,9 +1125,21 @@ static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     for (int s = 0; s <= h->S; ++s) {
         P.s = s;
         MZ_TRY(h, hipLaunchKernel((const void*)mz_rsearch_tree, dim3(groups), dim3(256), args, 0, st));
-        if (s < h->S)
-            MZ_TRY(h, hipLaunchKernel((const void*)mz_rsearch_nets, dim3(tiles, 2), dim3(256), args,
-                                      rsearch_nets_lds(h), st));
+        if (s == h->S) break;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (h->time_nets) {
+            if (h->tev_used + 2 > h->tev.size())
+                for (int i = 0; i < 2; ++i) {
+                    hipEvent_t e;
+                    MZ_TRY(h, hipEventCreate(&e));
+                    h->tev.push_back(e);
+                }
+            e0 = h->tev[h->tev_used++]; e1 = h->tev[h->tev_used++];
+            MZ_TRY(h, hipEventRecord(e0, st));
+        }
+        MZ_TRY(h, hipLaunchKernel((const void*)mz_rsearch_nets, dim3(tiles, 2), dim3(256), args,
+                                  rsearch_nets_lds(h), st));
+        if (e1) MZ_TRY(h, hipEventRecord(e1, st));
     }
     h->last_variant = "mz_rsearch";
     return 0;
@@ -1228,6 +1243,7 @@ int mz_mcts_search(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
 int mz_debug_enable(mz_handle* h, int flags) {
     if (!h) return -2;
     h->dump_tree = flags & 1;
+    h->time_nets = (flags >> 1) & 1;
     return 0;
 }
 
@@ -1404,6 +1420,22 @@ int mz_learner_step(mz_handle* h, const mz_batch* b, double eta, float* losses_o
     if (rc) return rc;
     if (losses_out) MZ_TRY(h, hipMemcpyAsync(losses_out, h->d_loss, 6 * 4, hipMemcpyDeviceToHost, st));
     MZ_TRY(h, hipStreamSynchronize(st));
+    return 0;
+}
+
+int mz_debug_kernel_time(mz_handle* h, double* total_ms, int* launches) {
+    if (!h) return -2;
+    MZ_TRY(h, hipSetDevice(h->device));
+    double t = 0.0;
+    for (size_t i = 0; i + 1 < h->tev_used; i += 2) {
+        MZ_TRY(h, hipEventSynchronize(h->tev[i + 1]));
+        float ms = 0.0f;
+        MZ_TRY(h, hipEventElapsedTime(&ms, h->tev[i], h->tev[i + 1]));
+        t += ms;
+    }
+    if (total_ms) *total_ms = t;
+    if (launches) *launches = (int)(h->tev_used / 2);
+    h->tev_used = 0;
     return 0;
 }
 

@@ -117,6 +117,17 @@ def param_count(conf, hyper, net):
     return sum(i * o + o for _, i, o, _ in layer_specs(conf, hyper, net))
 
 
+def net_macs(conf, hyper, net):
+    """Multiply-accumulates of one forward of `net` for one item (the
+    algorithmic FLOP count is 2x this): Dense in*out, conv W*H*kw*kh*cin*cout
+    (same-padded, stride 1)."""
+    if isinstance(hyper, ResNetHP):
+        W, H, _ = conf.observation_shape
+        return sum(op["cin"] * op["cout"] * (op["kw"] * op["kh"] * W * H if op["kind"] == "conv" else 1)
+                   for op in resnet_specs(conf, hyper, net))
+    return sum(i * o for _, i, o, _ in layer_specs(conf, hyper, net))
+
+
 def glorot_uniform(rng, out, inp):
     """Flux 0.12 glorot_uniform: (rand(Float32, out, in) .- 0.5f0) .* sqrt(24f0 / (in + out))."""
     u = rng.random((inp, out), dtype=np.float32)          # column-major (out, in) == C (in, out)
