@@ -720,19 +720,24 @@ static RPlan rn_plan(const mz_handle* h, const std::vector<RSpec>& sp, int net, 
             else { L.out_off = ping[r.chain]; ping[r.chain] = ping[r.chain] == S1 ? S2 : S1; }
             cur[r.chain] = L.out_off;
         }
+        // A fragments [ob][q][j/4][lane][j%4] (NQ padded to NQ4 = 4⌈NQ/4⌉ with
+        // zeros): one 16-byte load gives a lane four k-steps of a quarter chain
         L.w_img = w_img;
-        const int nks = 4 * L.nq;
+        const int nq4 = (L.nq + 3) & ~3;
         for (int ob = 0; ob < L.n_ob; ++ob)
-            for (int ks = 0; ks < nks; ++ks)
-                for (int lane = 0; lane < 64; ++lane) {
-                    const int o = ob * 16 + (lane & 15), k = ks * 4 + (lane >> 4);
-                    int src = -1;
-                    if (o < r.cout && k < L.K)
-                        src = (int)(flat_off + r.woff + (r.conv ? (size_t)k + (size_t)L.K * o
-                                                                : (size_t)o + (size_t)r.cout * k));
-                    if (srcw) srcw->push_back(src);
-                }
-        w_img += L.n_ob * nks * 64;
+            for (int q = 0; q < 4; ++q)
+                for (int jc = 0; jc < nq4 / 4; ++jc)
+                    for (int lane = 0; lane < 64; ++lane)
+                        for (int jj = 0; jj < 4; ++jj) {
+                            const int j = 4 * jc + jj;
+                            const int o = ob * 16 + (lane & 15), k = (q * L.nq + j) * 4 + (lane >> 4);
+                            int src = -1;
+                            if (j < L.nq && o < r.cout && k < L.K)
+                                src = (int)(flat_off + r.woff + (r.conv ? (size_t)k + (size_t)L.K * o
+                                                                        : (size_t)o + (size_t)r.cout * k));
+                            if (srcw) srcw->push_back(src);
+                        }
+        w_img += L.n_ob * 4 * nq4 * 64;
         if (L.kk > 1) L.ktab = region(L.K);
     }
     if (net == MZ_NET_REPR) { R.out0_off = B0; R.out0_n = h->H; R.out1_n = 0; }
@@ -1056,7 +1061,7 @@ static int rnet_forward(mz_handle* h, int net, const float* x, int n, float* out
     Q.P = Q.W * Q.H; Q.n_items = n; Q.softmax1 = net == MZ_NET_PRED; Q.bn_s = h->bn_s;
     Q.plan = h->d_rplan + net; Q.Wimg = h->d_Wp; Q.flat = h->d_flat; Q.x = dx; Q.out0 = d0; Q.out1 = d1;
     void* args[] = {&Q};
-    hipError_t le = hipLaunchKernel((const void*)mz_rnet_forward_kernel, dim3((n + Q.ng - 1) / Q.ng), dim3(256),
+    hipError_t le = hipLaunchKernel((const void*)mz_rnet_forward_kernel, dim3((n + Q.ng - 1) / Q.ng), dim3(RN_THREADS),
                                     args, h->rn_lds[net], h->stream);
     (void)hipMemcpyAsync(out0, d0, (size_t)n * R.out0_n * 4, hipMemcpyDeviceToHost, h->stream);
     if (out1 && R.out1_n) (void)hipMemcpyAsync(out1, d1, (size_t)n * R.out1_n * 4, hipMemcpyDeviceToHost, h->stream);
@@ -1119,9 +1124,13 @@ static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     P.path = h->d_rpath; P.gst = h->d_rgst; P.x_pred = h->d_rxpred;
     P.o_v = h->d_rov; P.o_logit = h->d_rologit; P.o_r = h->d_ror;
     P.ng = h->rn_ng; P.bn_s = h->bn_s; P.plans = h->d_rplan; P.Wimg = h->d_Wp; P.flat = h->d_flat;
+#ifdef MZ_STAMPS
+    if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * std::max(h->max_games, 128)));
+    P.stamps = h->d_stamps;
+#endif
     void* args[] = {&P};
     const unsigned tiles = (unsigned)((G + P.ng - 1) / P.ng), groups = (unsigned)((G + 15) / 16);
-    MZ_TRY(h, hipLaunchKernel((const void*)mz_rsearch_root, dim3(tiles), dim3(256), args, rsearch_root_lds(h), st));
+    MZ_TRY(h, hipLaunchKernel((const void*)mz_rsearch_root, dim3(tiles), dim3(RN_THREADS), args, rsearch_root_lds(h), st));
     for (int s = 0; s <= h->S; ++s) {
         P.s = s;
         MZ_TRY(h, hipLaunchKernel((const void*)mz_rsearch_tree, dim3(groups), dim3(256), args, 0, st));
@@ -1137,7 +1146,7 @@ static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
             e0 = h->tev[h->tev_used++]; e1 = h->tev[h->tev_used++];
             MZ_TRY(h, hipEventRecord(e0, st));
         }
-        MZ_TRY(h, hipLaunchKernel((const void*)mz_rsearch_nets, dim3(tiles, 2), dim3(256), args,
+        MZ_TRY(h, hipLaunchKernel((const void*)mz_rsearch_nets, dim3(tiles, 2), dim3(RN_THREADS_NETS), args,
                                   rsearch_nets_lds(h), st));
         if (e1) MZ_TRY(h, hipEventRecord(e1, st));
     }
@@ -1322,7 +1331,7 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
     U.obs = b->observation; U.actions = b->actions; U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
     U.hs = h->d_rhs; U.plans = h->d_rplan; U.Wimg = h->d_Wp; U.flat = h->d_flat;
     void* args[] = {&U};
-    MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_kernel, dim3((B + U.ng - 1) / U.ng), dim3(256), args,
+    MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_kernel, dim3((B + U.ng - 1) / U.ng), dim3(RN_THREADS), args,
                               runroll_lds(h), st));
     return learner_losses(h, b, grad_dev, losses_dev, st, MZ_ACT_IDENTITY, MZ_ACT_IDENTITY);
 }

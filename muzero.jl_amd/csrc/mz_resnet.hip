@@ -1,6 +1,6 @@
 // mz_resnet.hip — the ResNet networks (row a14; Learning.jl:148-255, the
 // intended architecture of SURVEY §2.1 Q12) on f32 MFMA, one tile of NG games
-// per 256-thread workgroup, activations resident in LDS across all layers.
+// per RN_THREADS-thread workgroup, activations resident in LDS across all layers.
 //
 // A layer is a generalised Dense (mz_resnet_params.h).  Each wave takes
 // 16x16 output tiles (16 rows of W x 16 columns); a tile's K runs as four
@@ -20,101 +20,295 @@ __device__ __forceinline__ float rn_act(int act, float v) {
     return v;
 }
 
-// B(k, n) of one layer for this lane
-struct RnCol {
-    int n;        // column
-    bool ok;      // n < ncols
-    int p, g, w, h;
-};
-
-__device__ __forceinline__ float rn_b(const RLayer& L, const RnCol& c, int k, int ncols, int NG, int Wb, int P,
-                                      const float* lds) {
-    if (!c.ok || k >= L.K) return 0.0f;
-    if (L.kk == 1) return lds[L.in_off + k * ncols + c.n];
-    const int t = reinterpret_cast<const int*>(lds)[L.ktab + k];      // (ch << 8) | (dx+8) << 4 | (dy+8)
-    const int ch = t >> 8, dx = ((t >> 4) & 15) - 8, dy = (t & 15) - 8;
-    const int sx = c.w + dx, sy = c.h + dy;
-    if (sx < 0 || sx >= Wb || sy < 0 || sy >= P / Wb) return 0.0f;
-    return lds[L.in_off + ch * ncols + (sx + Wb * sy) * NG + c.g];
+// A fragments of 16 output rows (block ob) for chunk c = k-steps 4c..4c+3 of
+// the four quarter chains: a[q][jj] (image [ob][q][nq4/4][lane][4]).
+__device__ __forceinline__ void rn_load_a(float (&a)[4][4], const float* __restrict__ Wimg, const RLayer& L,
+                                          int ob, int c, int lane) {
+    const int nch = (L.nq + 3) >> 2;
+    const float* base = Wimg + L.w_img + (size_t)ob * (16 * nch * 64) + (size_t)lane * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(base + (size_t)((q * nch + c) * 64) * 4);
+        a[q][0] = v.x; a[q][1] = v.y; a[q][2] = v.z; a[q][3] = v.w;
+    }
 }
 
-__device__ void rn_layer(const RLayer& L, const float* __restrict__ Wimg, const float* __restrict__ flat,
-                         float* lds, int NG, int Wb, int P, float bn_s) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
-    const int ncols = L.spatial ? P * NG : NG;
-    const int n_nb = (ncols + 15) >> 4;
-    const int NQ = L.nq;
-    for (int t = wave; t < L.n_ob * n_nb; t += nwaves) {
-        const int ob = t / n_nb, nb = t - ob * n_nb;
-        RnCol c;
-        c.n = nb * 16 + (lane & 15);
-        c.ok = c.n < ncols;
-        c.p = c.n / NG; c.g = c.n - c.p * NG;
-        c.w = c.p % Wb; c.h = c.p / Wb;
-        const float* wb = Wimg + L.w_img + (size_t)ob * (4 * NQ * 64) + lane;
-        mz_f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
-        const int kl = lane >> 4;
-        for (int j = 0; j < NQ; ++j) {
-            const int k0 = (0 * NQ + j) * 4 + kl, k1 = (1 * NQ + j) * 4 + kl;
-            const int k2 = (2 * NQ + j) * 4 + kl, k3 = (3 * NQ + j) * 4 + kl;
-            const float b0 = rn_b(L, c, k0, ncols, NG, Wb, P, lds), b1 = rn_b(L, c, k1, ncols, NG, Wb, P, lds);
-            const float b2 = rn_b(L, c, k2, ncols, NG, Wb, P, lds), b3 = rn_b(L, c, k3, ncols, NG, Wb, P, lds);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[(0 * NQ + j) * 64], b0, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[(1 * NQ + j) * 64], b1, acc1, 0, 0, 0);
-            acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[(2 * NQ + j) * 64], b2, acc2, 0, 0, 0);
-            acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[(3 * NQ + j) * 64], b3, acc3, 0, 0, 0);
-        }
-        if (!c.ok) continue;
+// Epilogue of NB 16x16 accumulator sets (column blocks of one lane: n[i],
+// row block ob): ((p0+p1)+(p2+p3)) + b, BatchNorm in test mode, residual,
+// activation -> out[o][n].  The BatchNorm quotient (t − 0)/s uses r = 1/s:
+// q0 = t·r, e = fma(−q0, s, t), q0 + e·r is the IEEE quotient for every
+// float with |t| >= 2^-100 (exhaustive check: tools/check_bn_div.c,
+// tests/test_bn_div.py); below that, where e underflows, one wave-uniform
+// branch divides.
+// bias, γ, β of the 4 rows a lane holds in row block ob (issued before the
+// MFMAs of the unit so their latency hides under them)
+__device__ __forceinline__ void rn_load_ep(float (&ep)[3][4], const RLayer& L, const float* __restrict__ flat, int ob,
+                                           int kl) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int o = ob * 16 + kl * 4 + r;
-            if (o >= L.cout) continue;
-            float d = (acc0[r] + acc1[r]) + (acc2[r] + acc3[r]);
-            d = d + flat[L.boff + o];
-            if (L.bn) d = flat[L.bnoff + L.cout + o] * ((d - 0.0f) / bn_s) + flat[L.bnoff + o];
-            if (L.res_add) d = d + lds[L.res_off + o * ncols + c.n];
-            lds[L.out_off + o * ncols + c.n] = rn_act(L.act, d);
+    for (int r = 0; r < 4; ++r) {
+        const int o = ob * 16 + kl * 4 + r, oc = o < L.cout ? o : L.cout - 1;
+        ep[0][r] = flat[L.boff + oc];
+        ep[1][r] = L.bn ? flat[L.bnoff + L.cout + oc] : 0.0f;
+        ep[2][r] = L.bn ? flat[L.bnoff + oc] : 0.0f;
+    }
+}
+
+template <int NB>
+__device__ __forceinline__ void rn_epilogue(const RLayer& L, const mz_f32x4 (&acc)[NB][4], const float (&ep)[3][4],
+                                            float* lds, int ob, int kl, const int (&n)[NB], int ncols, float bn_s,
+                                            float bn_r) {
+    float d[NB][4];
+    bool tiny = false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float bias = ep[0][r];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            float t = (acc[i][0][r] + acc[i][1][r]) + (acc[i][2][r] + acc[i][3][r]);
+            t = t + bias;
+            d[i][r] = t;
+            tiny |= fabsf(t) < 0x1p-100f;
+        }
+    }
+    if (L.bn) {
+        float q[NB][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const float t = d[i][r] - 0.0f;
+                const float q0 = t * bn_r;
+                const float e = fmaf(-q0, bn_s, t);
+                q[i][r] = fmaf(e, bn_r, q0);
+            }
+        if (__builtin_expect(__ballot(tiny) != 0, 0)) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int i = 0; i < NB; ++i)
+                    if (fabsf(d[i][r]) < 0x1p-100f) q[i][r] = (d[i][r] - 0.0f) / bn_s;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int i = 0; i < NB; ++i) d[i][r] = ep[1][r] * q[i][r] + ep[2][r];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int o = ob * 16 + kl * 4 + r;
+        if (o >= L.cout) continue;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            if (n[i] >= ncols) continue;
+            float v = d[i][r];
+            if (L.res_add) v = v + lds[L.res_off + o * ncols + n[i]];
+            lds[L.out_off + o * ncols + n[i]] = rn_act(L.act, v);
         }
     }
 }
 
+// One layer, barrier-separated from its neighbours (Dense layers, kernels
+// > 1x1).  A wave owns a unit = one 16-row output block x NBW 16-column
+// blocks; each A fragment feeds NBW MFMAs and the four k-quarter chains of
+// every 16x16 tile run as four accumulators (canonical order: chain q takes
+// k = (q·NQ + j)·4 + (lane>>4) for j ascending).  The wave walks (unit, chunk
+// of 4 k-steps) pairs, the A fragments of the next pair loaded before the
+// MFMAs of the current one; a chunk's B operands are read from LDS in one
+// batch.  B(k, n): MODE 0 Dense / MODE 1 1x1 conv read x[k][n]; MODE 2
+// (kernel > 1x1) reads
+// through the k table: t = off·256 | (dx+8)·16 | (dy+8) with off = ch·ncols +
+// (dx + W·dy)·NG, zero outside the board.  Addresses are clamped in range and
+// out-of-range operands selected to 0 (no branches).
+template <int NBW, int MODE>
+__device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restrict__ Wimg,
+                                           const float* __restrict__ flat, float* lds, int NG, int Wb, int P,
+                                           float bn_s, float bn_r) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
+    const int ncols = MODE == 0 ? NG : P * NG;
+    const int n_nb = (ncols + 15) >> 4;
+    const int n_grp = (n_nb + NBW - 1) / NBW;
+    const int units = L.n_ob * n_grp;
+    const int NQ = L.nq, K = L.K, Hb = P / Wb, nch = (NQ + 3) >> 2;
+    const int kl = lane >> 4;
+    const int* tab = reinterpret_cast<const int*>(lds) + L.ktab;
+    int u = wave;
+    if (u >= units) return;
+    float an[4][4];
+    rn_load_a(an, Wimg, L, u / n_grp, 0, lane);
+    for (; u < units; u += nwaves) {
+        const int ob = u / n_grp, grp = u - ob * n_grp;
+        float ep[3][4];
+        rn_load_ep(ep, L, flat, ob, kl);
+        int cb[NBW], cw[NBW], chh[NBW];
+#pragma unroll
+        for (int i = 0; i < NBW; ++i) {
+            const int n = (grp * NBW + i) * 16 + (lane & 15);
+            const int nn = n < ncols ? n : ncols - 1;
+            cb[i] = L.in_off + nn;
+            if (MODE == 2) {
+                const int pp = nn / NG;
+                cw[i] = pp % Wb; chh[i] = pp / Wb;
+            }
+        }
+        // MODE 0/1: byte address of row q·NQ·4 + kl at each column block; the
+        // k-step adds a wave-uniform j·4·ncols; kq[q] = rows of quarter q left
+        // for this lane (k < K)
+        uint32_t bq[4][NBW];
+        int kq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            kq[q] = K - (q * NQ * 4 + kl);
+#pragma unroll
+            for (int i = 0; i < NBW; ++i) bq[q][i] = (uint32_t)(cb[i] + (q * NQ * 4 + kl) * ncols) * 4u;
+        }
+        mz_f32x4 acc[NBW][4];
+#pragma unroll
+        for (int i = 0; i < NBW; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[i][q] = mz_f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < nch; ++c) {
+            float ac[4][4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) ac[q][jj] = an[q][jj];
+            {                                           // prefetch the next (unit, chunk) or layer
+                const int un = c + 1 < nch ? u : u + nwaves, cn = c + 1 < nch ? c + 1 : 0;
+                if (un < units) rn_load_a(an, Wimg, L, un / n_grp, cn, lane);
+            }
+            float b[4][4][NBW];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int k = (q * NQ + 4 * c + jj) * 4 + kl;
+                    const bool kin = k < K && 4 * c + jj < NQ;
+                    const int kc = kin ? k : K - 1;
+                    if (MODE == 2) {
+                        const int t = tab[kc];
+                        const int off = t >> 8, dx = ((t >> 4) & 15) - 8, dy = (t & 15) - 8;
+#pragma unroll
+                        for (int i = 0; i < NBW; ++i) {
+                            const bool ok = kin && (unsigned)(cw[i] + dx) < (unsigned)Wb &&
+                                            (unsigned)(chh[i] + dy) < (unsigned)Hb;
+                            const float v = lds[ok ? cb[i] + off : cb[i]];
+                            b[jj][q][i] = ok ? v : 0.0f;
+                        }
+                    } else {
+                        const uint32_t so = (uint32_t)((4 * c + jj) * 4 * ncols) * 4u;
+                        const bool kv = 4 * (4 * c + jj) < kq[q];
+#pragma unroll
+                        for (int i = 0; i < NBW; ++i) {
+                            const float v = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(lds) +
+                                                                            bq[q][i] + so);
+                            b[jj][q][i] = kv ? v : 0.0f;
+                        }
+                    }
+                }
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                if (4 * c + jj >= NQ) break;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int i = 0; i < NBW; ++i)
+                        acc[i][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[q][jj], b[jj][q][i], acc[i][q], 0, 0, 0);
+            }
+        }
+        int nn[NBW];
+#pragma unroll
+        for (int i = 0; i < NBW; ++i) nn[i] = (grp * NBW + i) * 16 + (lane & 15);
+        rn_epilogue<NBW>(L, acc, ep, lds, ob, kl, nn, ncols, bn_s, bn_r);
+    }
+}
+
+__device__ __forceinline__ void rn_layer(const RLayer& L, const float* __restrict__ Wimg,
+                                         const float* __restrict__ flat, float* lds, int NG, int Wb, int P,
+                                         float bn_s, float bn_r) {
+#ifndef RN_NBW
+#define RN_NBW 3
+#endif
+    if (L.kk > 1) rn_layer_t<3, 2>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+    else if (L.spatial) rn_layer_t<RN_NBW, 1>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+    else rn_layer_t<1, 0>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+}
+
 // the k tables of the layers with a kernel > 1x1 (filled once per launch)
-__device__ void rn_fill_ktabs(const RPlan& R, float* lds) {
+__device__ void rn_fill_ktabs(const RPlan& R, float* lds, int NG, int Wb, int P) {
     for (int i = 0; i < R.n; ++i) {
         const RLayer& L = R.L[i];
         if (L.kk == 1) continue;
         int* tab = reinterpret_cast<int*>(lds) + L.ktab;
         for (int k = threadIdx.x; k < L.K; k += blockDim.x) {
-            const int ch = k / L.kk, r = k - ch * L.kk, j = r / L.kw, ii = r - j * L.kw;
+            const int c = k / L.kk, r = k - c * L.kk, j = r / L.kw, ii = r - j * L.kw;
             const int dx = (L.kw - 1 - ii) - L.pw, dy = (L.kh - 1 - j) - L.ph;
-            tab[k] = (ch << 8) | ((dx + 8) << 4) | (dy + 8);
+            const int off = c * P * NG + (dx + Wb * dy) * NG;
+            tab[k] = off * 256 | ((dx + 8) << 4) | (dy + 8);
         }
     }
 }
 
-__device__ void rn_run(const RPlan& R, const float* Wimg, const float* flat, float* lds, int NG, int Wb, int P,
-                       float bn_s) {
+// A net: its layers one by one, a workgroup barrier after each.
+__device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const float* flat, float* lds, int NG,
+                                       int Wb, int P, float bn_s, unsigned long long* st = nullptr) {
+    const float bn_r = 1.0f / bn_s;
+    const int wv = threadIdx.x >> 6;
+#ifdef MZ_STAMPS
+    if (st && (threadIdx.x & 63) == 0) st[wv * 64 + 63] = __builtin_amdgcn_s_memtime();
+#endif
     for (int i = 0; i < R.n; ++i) {
-        rn_layer(R.L[i], Wimg, flat, lds, NG, Wb, P, bn_s);
+        rn_layer(R.L[i], Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+#ifdef MZ_STAMPS
+        if (st && (threadIdx.x & 63) == 0) st[wv * 64 + 2 * i] = __builtin_amdgcn_s_memtime();
+#endif
         __syncthreads();
+#ifdef MZ_STAMPS
+        if (st && (threadIdx.x & 63) == 0) st[wv * 64 + 2 * i + 1] = __builtin_amdgcn_s_memtime();
+#endif
     }
+    (void)wv;
+}
+
+// Thread layout of the staging loops: game g = tid mod NG (NG a power of
+// two), features f0, f0 + fs, ... — per-game addresses are computed once and
+// the unrolled loop keeps several loads in flight.
+struct RnLane {
+    int g, f0, fs;
+};
+__device__ __forceinline__ RnLane rn_lane(int NG) {
+    const int lg = __ffs(NG) - 1;
+    return RnLane{(int)threadIdx.x & (NG - 1), (int)threadIdx.x >> lg, (int)blockDim.x >> lg};
+}
+// LDS tile dst[f][NG] <- val(f) for f < n
+template <class Fn>
+__device__ __forceinline__ void rn_stage(float* dst, int NG, int n, const RnLane& t, Fn val) {
+#pragma unroll 6
+    for (int f = t.f0; f < n; f += t.fs) dst[f * NG + t.g] = val(f);
+}
+// put(f, src[f][g]) for f < n
+template <class Fn>
+__device__ __forceinline__ void rn_unstage(const float* src, int NG, int n, const RnLane& t, Fn put) {
+#pragma unroll 6
+    for (int f = t.f0; f < n; f += t.fs) put(f, src[f * NG + t.g]);
 }
 
 // Batched forward of one net (mz_net_forward): x (in_feat, n) -> out0, out1.
-extern "C" __global__ __launch_bounds__(256) void mz_rnet_forward_kernel(RNetParams Q) {
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_rnet_forward_kernel(RNetParams Q) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const RPlan& R = *Q.plan;
     const int NG = Q.ng, t0 = blockIdx.x * NG;
-    rn_fill_ktabs(R, lds);
-    for (int i = threadIdx.x; i < R.in_feat * NG; i += blockDim.x) {
-        const int f = i / NG, g = i - f * NG;
-        lds[R.in_off + i] = t0 + g < Q.n_items ? Q.x[(size_t)(t0 + g) * R.in_feat + f] : 0.0f;
+    rn_fill_ktabs(R, lds, NG, Q.W, Q.P);
+    const RnLane t = rn_lane(NG);
+    const bool ok = t0 + t.g < Q.n_items;
+    {
+        const float* x = Q.x + (size_t)(ok ? t0 + t.g : 0) * R.in_feat;
+        rn_stage(lds + R.in_off, NG, R.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
     }
     __syncthreads();
     rn_run(R, Q.Wimg, Q.flat, lds, NG, Q.W, Q.P, Q.bn_s);
-    for (int i = threadIdx.x; i < R.out0_n * NG; i += blockDim.x) {
-        const int f = i / NG, g = i - f * NG;
-        if (t0 + g < Q.n_items) Q.out0[(size_t)(t0 + g) * R.out0_n + f] = lds[R.out0_off + i];
+    if (ok) {
+        float* o = Q.out0 + (size_t)(t0 + t.g) * R.out0_n;
+        rn_unstage(lds + R.out0_off, NG, R.out0_n, t, [&](int f, float v) { o[f] = v; });
     }
     if (R.out1_n && Q.out1) {
         const int g = threadIdx.x;
@@ -145,7 +339,7 @@ __device__ __forceinline__ TreeView rs_tree(const RSearchParams& P, int gg) {
 // Root (SelfPlay.jl:230-251): representation + prediction of NG games per
 // tile, h0 -> hidden slot 0, root expansion with the double softmax (Q3),
 // exploration noise, per-game state.
-extern "C" __global__ __launch_bounds__(256) void mz_rsearch_root(RSearchParams P) {
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_rsearch_root(RSearchParams P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const RPlan& Rr = P.plans[MZ_NET_REPR];
     const RPlan& Rp = P.plans[MZ_NET_PRED];
@@ -153,22 +347,19 @@ extern "C" __global__ __launch_bounds__(256) void mz_rsearch_root(RSearchParams 
     const int nplan = Rr.lds_floats > Rp.lds_floats ? Rr.lds_floats : Rp.lds_floats;
     float* stg = lds + nplan;                       // [16][16] softmax / noise staging
     float* noise = stg + 256;                       // [16][16]
-    rn_fill_ktabs(Rr, lds);
-    for (int i = threadIdx.x; i < Rr.in_feat * NG; i += blockDim.x) {
-        const int f = i / NG, g = i - f * NG;
-        lds[Rr.in_off + i] = t0 + g < P.G ? P.obs[(size_t)(t0 + g) * P.obs_feat + f] : 0.0f;
+    rn_fill_ktabs(Rr, lds, NG, P.W, P.P);
+    const RnLane t = rn_lane(NG);
+    const bool ok = t0 + t.g < P.G;
+    {
+        const float* x = P.obs + (size_t)(ok ? t0 + t.g : 0) * P.obs_feat;
+        rn_stage(lds + Rr.in_off, NG, Rr.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
     }
     __syncthreads();
     rn_run(Rr, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s);                    // :234
-    for (int i = threadIdx.x; i < H * NG; i += blockDim.x) {
-        const int f = i / NG, g = i - f * NG;
-        if (t0 + g < P.G) P.hid[(size_t)(t0 + g) * (P.S + 1) * H + f] = lds[Rr.out0_off + i];
-    }
+    float* h0 = P.hid + (size_t)(ok ? t0 + t.g : 0) * (P.S + 1) * H;
+    if (ok) rn_unstage(lds + Rr.out0_off, NG, H, t, [&](int f, float v) { h0[f] = v; });
     __syncthreads();
-    for (int i = threadIdx.x; i < H * NG; i += blockDim.x) {                  // prediction input = h0
-        const int f = i / NG, g = i - f * NG;
-        lds[Rp.in_off + i] = t0 + g < P.G ? P.hid[(size_t)(t0 + g) * (P.S + 1) * H + f] : 0.0f;
-    }
+    rn_stage(lds + Rp.in_off, NG, H, t, [&](int f) { return ok ? h0[f] : 0.0f; });   // prediction input = h0
     __syncthreads();
     rn_run(Rp, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s);                    // :239
     const int gl = threadIdx.x >> 4, a = threadIdx.x & 15, gg = t0 + gl;
@@ -275,38 +466,43 @@ extern "C" __global__ __launch_bounds__(256) void mz_rsearch_tree(RSearchParams 
 
 // Networks of simulation s: blockIdx.y = 0 prediction(parent h), 1 dynamics
 // (2h ⊕ a/|A|, Q1) writing h' into hidden slot s+1.
-extern "C" __global__ __launch_bounds__(256) void mz_rsearch_nets(RSearchParams P) {
+extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RSearchParams P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int net = blockIdx.y == 0 ? MZ_NET_PRED : MZ_NET_DYN;
     const RPlan& R = P.plans[net];
     const int NG = P.ng, t0 = blockIdx.x * NG, H = P.H, S = P.S;
-    rn_fill_ktabs(R, lds);
-    for (int i = threadIdx.x; i < R.in_feat * NG; i += blockDim.x) {
-        const int f = i / NG, g = i - f * NG, gg = t0 + g;
-        float v = 0.0f;
-        if (gg < P.G) {
-            const int* st = P.gst + (size_t)gg * RG_INTS;
-            if (net == MZ_NET_PRED) v = P.x_pred[(size_t)gg * H + f];
-            else if (f < H) v = P.hid[((size_t)gg * (S + 1) + st[RG_LEAF_E]) * H + f];
-            else v = P.aval_tab[st[RG_LEAF_A]];
-        }
-        lds[R.in_off + i] = v;
+    unsigned long long* st = nullptr;
+#ifdef MZ_STAMPS
+    if (P.stamps && blockIdx.x == 0 && P.s == 0) st = P.stamps + blockIdx.y * 512;
+    if (st && (threadIdx.x & 63) == 0) st[(threadIdx.x >> 6) * 64 + 60] = __builtin_amdgcn_s_memtime();
+#endif
+    rn_fill_ktabs(R, lds, NG, P.W, P.P);
+    const RnLane t = rn_lane(NG);
+    const int gg = t0 + t.g;
+    const bool ok = gg < P.G;
+    if (net == MZ_NET_PRED) {
+        const float* x = P.x_pred + (size_t)(ok ? gg : 0) * H;
+        rn_stage(lds + R.in_off, NG, H, t, [&](int f) { return ok ? x[f] : 0.0f; });
+    } else {
+        const int* st = P.gst + (size_t)(ok ? gg : 0) * RG_INTS;
+        const float* x = P.hid + ((size_t)(ok ? gg : 0) * (S + 1) + st[RG_LEAF_E]) * H;
+        const float av = P.aval_tab[st[RG_LEAF_A]];
+        rn_stage(lds + R.in_off, NG, R.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? x[f] : av; });
     }
     __syncthreads();
-    rn_run(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s);
+    rn_run(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st);
+#ifdef MZ_STAMPS
+    if (st && (threadIdx.x & 63) == 0) st[(threadIdx.x >> 6) * 64 + 61] = __builtin_amdgcn_s_memtime();
+#endif
+    if (!ok) return;
     if (net == MZ_NET_PRED) {
-        for (int i = threadIdx.x; i < (1 + P.A) * NG; i += blockDim.x) {
-            const int r = i / NG, g = i - r * NG, gg = t0 + g;
-            if (gg >= P.G) continue;
-            if (r == 0) P.o_v[gg] = lds[R.out0_off + g];
-            else P.o_logit[(size_t)gg * P.A + (r - 1)] = lds[R.out1_off + (r - 1) * NG + g];
-        }
+        if (t.f0 == 0) P.o_v[gg] = lds[R.out0_off + t.g];
+        float* o = P.o_logit + (size_t)gg * P.A;
+        rn_unstage(lds + R.out1_off, NG, P.A, t, [&](int f, float v) { o[f] = v; });
     } else {
-        for (int i = threadIdx.x; i < H * NG; i += blockDim.x) {
-            const int f = i / NG, g = i - f * NG, gg = t0 + g;
-            if (gg < P.G) P.hid[((size_t)gg * (S + 1) + P.s + 1) * H + f] = lds[R.out0_off + i];
-        }
-        if (threadIdx.x < NG && t0 + (int)threadIdx.x < P.G) P.o_r[t0 + threadIdx.x] = lds[R.out1_off + threadIdx.x];
+        float* o = P.hid + ((size_t)gg * (S + 1) + P.s + 1) * H;
+        rn_unstage(lds + R.out0_off, NG, H, t, [&](int f, float v) { o[f] = v; });
+        if (t.f0 == 0) P.o_r[gg] = lds[R.out1_off + t.g];
     }
 }
 
@@ -314,59 +510,53 @@ extern "C" __global__ __launch_bounds__(256) void mz_rsearch_nets(RSearchParams 
 // Forward unroll of the learner (Learning.jl:347-370): representation, then
 // for i = 1..K prediction(h_{i-1}) -> step i (step 0 is the same prediction of
 // h0, written once for both), dynamics(2h ⊕ a_i/|A|) -> h_i, r_i; r_0 = 0.
-extern "C" __global__ __launch_bounds__(256) void mz_runroll_kernel(RUnrollParams U) {
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_kernel(RUnrollParams U) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const RPlan& Rr = U.plans[MZ_NET_REPR];
     const RPlan& Rp = U.plans[MZ_NET_PRED];
     const RPlan& Rd = U.plans[MZ_NET_DYN];
     const int NG = U.ng, t0 = blockIdx.x * NG, H = U.H, A = U.A, K1 = U.K + 1;
-    rn_fill_ktabs(Rr, lds);
-    for (int i = threadIdx.x; i < Rr.in_feat * NG; i += blockDim.x) {
-        const int f = i / NG, g = i - f * NG;
-        lds[Rr.in_off + i] = t0 + g < U.B ? U.obs[(size_t)(t0 + g) * U.obs_feat + f] : 0.0f;
+    const RnLane t = rn_lane(NG);
+    const int b = t0 + t.g;
+    const bool ok = b < U.B;
+    const size_t bs = (size_t)(ok ? b : 0);
+    float* hs = U.hs + bs * H;
+    rn_fill_ktabs(Rr, lds, NG, U.W, U.P);
+    {
+        const float* x = U.obs + bs * U.obs_feat;
+        rn_stage(lds + Rr.in_off, NG, Rr.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
     }
     __syncthreads();
     rn_run(Rr, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                     // :347
-    for (int i = threadIdx.x; i < H * NG; i += blockDim.x) {
-        const int f = i / NG, g = i - f * NG;
-        if (t0 + g < U.B) U.hs[(size_t)(t0 + g) * H + f] = lds[Rr.out0_off + i];
-    }
-    if (threadIdx.x < NG && t0 + (int)threadIdx.x < U.B) U.pr[(size_t)(t0 + threadIdx.x) * K1] = 0.0f;
+    if (ok) rn_unstage(lds + Rr.out0_off, NG, H, t, [&](int f, float v) { hs[f] = v; });
+    if (ok && t.f0 == 0) U.pr[bs * K1] = 0.0f;
     const int ns = U.K > 0 ? U.K : 1;              // K = 0: the prediction of h0 alone
     for (int s = 1; s <= ns; ++s) {
         __syncthreads();
-        rn_fill_ktabs(Rp, lds);
-        for (int i = threadIdx.x; i < H * NG; i += blockDim.x) {
-            const int f = i / NG, g = i - f * NG;
-            lds[Rp.in_off + i] = t0 + g < U.B ? U.hs[(size_t)(t0 + g) * H + f] : 0.0f;
-        }
+        rn_fill_ktabs(Rp, lds, NG, U.W, U.P);
+        rn_stage(lds + Rp.in_off, NG, H, t, [&](int f) { return ok ? hs[f] : 0.0f; });
         __syncthreads();
         rn_run(Rp, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                 // :351 / :356
-        for (int i = threadIdx.x; i < (1 + A) * NG; i += blockDim.x) {
-            const int r = i / NG, g = i - r * NG, b = t0 + g;
-            if (b >= U.B) continue;
-            const float v = r == 0 ? lds[Rp.out0_off + g] : lds[Rp.out1_off + (r - 1) * NG + g];
+        if (ok) {
+            // step s (and step 0 from the same prediction of h0, Q10)
             for (int j = s == 1 ? 0 : s; j <= (s <= U.K ? s : 0); ++j) {
-                if (r == 0) U.pv[(size_t)b * K1 + j] = v;
-                else U.pp[((size_t)b * K1 + j) * A + (r - 1)] = v;
+                if (t.f0 == 0) U.pv[bs * K1 + j] = lds[Rp.out0_off + t.g];
+                float* o = U.pp + (bs * K1 + j) * A;
+                rn_unstage(lds + Rp.out1_off, NG, A, t, [&](int f, float v) { o[f] = v; });
             }
         }
         if (s > U.K) break;
         __syncthreads();
-        rn_fill_ktabs(Rd, lds);
-        for (int i = threadIdx.x; i < Rd.in_feat * NG; i += blockDim.x) {     // make_dynamics_input (:293-304)
-            const int f = i / NG, g = i - f * NG, b = t0 + g;
-            float v = 0.0f;
-            if (b < U.B) v = f < H ? U.hs[(size_t)b * H + f] * 2.0f : U.actions[(size_t)b * K1 + (s - 1)] / (float)A;
-            lds[Rd.in_off + i] = v;
+        rn_fill_ktabs(Rd, lds, NG, U.W, U.P);
+        {                                                                      // make_dynamics_input (:293-304)
+            const float av = ok ? U.actions[bs * K1 + (s - 1)] / (float)A : 0.0f;
+            rn_stage(lds + Rd.in_off, NG, Rd.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? hs[f] * 2.0f : av; });
         }
         __syncthreads();
         rn_run(Rd, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                 // :362
-        for (int i = threadIdx.x; i < H * NG; i += blockDim.x) {
-            const int f = i / NG, g = i - f * NG;
-            if (t0 + g < U.B) U.hs[(size_t)(t0 + g) * H + f] = lds[Rd.out0_off + i];
+        if (ok) {
+            rn_unstage(lds + Rd.out0_off, NG, H, t, [&](int f, float v) { hs[f] = v; });
+            if (t.f0 == 0) U.pr[bs * K1 + s] = lds[Rd.out1_off + t.g];
         }
-        if (threadIdx.x < NG && t0 + (int)threadIdx.x < U.B)
-            U.pr[(size_t)(t0 + threadIdx.x) * K1 + s] = lds[Rd.out1_off + threadIdx.x];
     }
 }

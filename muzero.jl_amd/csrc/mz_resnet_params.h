@@ -12,6 +12,12 @@
 #pragma once
 
 #define RN_MAX_LAYERS 96
+#ifndef RN_THREADS
+#define RN_THREADS 512           // root / unroll / forward kernels: 8 waves, 2 per SIMD
+#endif
+#ifndef RN_THREADS_NETS
+#define RN_THREADS_NETS 768      // search network launch: 12 waves, 3 per SIMD (one unit of a 64x144 conv each)
+#endif
 
 struct RLayer {
     int kk;              // kw * kh (1: Dense or 1x1 conv; > 1: im2col gather through the k table)
@@ -20,7 +26,7 @@ struct RLayer {
     int nq, n_ob;        // k-steps per quarter (ceil(K/16)), 16-row output blocks
     int spatial;         // columns = P·NG (conv) or NG (Dense)
     int act, bn, res_add;
-    int w_img;           // packed A fragments [n_ob][4·nq][64] in the image
+    int w_img;           // packed A fragments [n_ob][4][nq4/4][64][4] in the image (nq4 = 4⌈nq/4⌉)
     int boff, bnoff;     // absolute offsets in the flat parameters (bias; β then γ)
     int in_off, out_off, res_off;   // LDS offsets (floats)
     int ktab;            // LDS offset of the k table (kk > 1), else -1
@@ -70,6 +76,7 @@ struct RSearchParams {
     float* o_v; float* o_logit; float* o_r;   // [G], [G][A], [G]
     int ng; float bn_s;
     const RPlan* plans;    // repr, pred, dyn
+    unsigned long long* stamps;   // -DMZ_STAMPS builds: per-layer ticks of nets blocks (0,0), (0,1)
     const float* Wimg; const float* flat;
 };
 
