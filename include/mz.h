@@ -217,6 +217,58 @@ int mz_learner_grad_dev(mz_handle* h, const mz_batch* dev_batch, float* grad_dev
 int mz_learner_apply_dev(mz_handle* h, const float* grad_dev, float grad_scale,
                          double eta, void* stream);
 
+/* ---- Device self-play and replay shard ------------
+ * The loop body of play_game (SelfPlay.jl:330-382) and the replay buffer
+ * (ReplayBuffer.jl) kept in HBM: no host round trip per move or per batch. */
+enum { MZ_ENV_TICTACTOE = 0, MZ_ENV_CONNECT4 = 1 };
+
+/* Device self-play state for G <= max_games game slots: env boards
+ * (games/tictactoe/game.jl with quirk Q14, or the Connect4 env of BASELINE
+ * configs[3], rules in muzero.jl_amd/games/connect4.py), each slot's
+ * GameHistory (Constructors.jl:6-16) in HBM, and a replay shard: FIFO of
+ * replay_games >= G finished games (ReplayBuffer.jl:133-161, PER = false;
+ * the RemoteBufferChannel Dict keyed by game number).  Every slot starts a
+ * new game.  The conf must match the env (TicTacToe (3,3,3)/9 actions,
+ * Connect4 (6,7,3)/7 actions).  Calling it again discards the state.       */
+int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games);
+
+/* One move of every slot, on the device, stream-ordered: observation append
+ * and stacked observations (SelfPlay.jl:351-355, Q15), legal mask, to_play,
+ * the batched search (as mz_mcts_search_dev with exploration on), env step
+ * and GameHistory append (:359-379).  Games that end (terminal, or more than
+ * max_moves moves, :343) go to the replay shard in slot order (save_game)
+ * and their slot starts a new game.  rng_step = the global move counter.   */
+int mz_selfplay_move(mz_handle* h, uint32_t rng_step, uint32_t game_offset, float temperature,
+                     void* stream);
+
+/* The shard's counters {num_played_games, num_played_steps, total_samples}
+ * (ReplayBuffer.jl:133-161) and the games it holds; synchronises.          */
+int mz_replay_counts(mz_handle* h, int64_t* counts, int32_t* games_in_buffer);
+
+/* save_game of a host GameHistory of T moves (obs as 0/1 bytes (T, W*H*C),
+ * actions / rewards / to_play / root_values (T), child_visits (A, T)).     */
+int mz_replay_save_game(mz_handle* h, int32_t T, const uint8_t* obs, const int32_t* actions,
+                        const float* rewards, const int32_t* to_play, const float* child_visits,
+                        const float* root_values);
+
+/* get_batch with make_target (ReplayBuffer.jl:5-50, 73-107, 188-217) on the
+ * device: B samples drawn with the Philox streams of learner step `step`
+ * (engine seed; sample_n_games uniform with replacement, sample_position
+ * uniform, absorbing-state actions uniform).  Fills *batch with device
+ * arrays owned by the handle (valid until the next call; feed them to
+ * mz_learner_grad_dev) and, if index_batch != NULL, copies the (game
+ * number, 1-based position) pairs to it (B x 2, synchronises).             */
+int mz_replay_sample(mz_handle* h, int32_t B, uint32_t step, mz_batch* batch, int32_t* index_batch,
+                     void* stream);
+
+/* Debug/parity: game i of the shard (0 = oldest held), buffers sized for
+ * max_moves + 1 moves (layouts as mz_replay_save_game); any pointer may be
+ * NULL.  And the slots' games in progress: moves recorded, boards (G, W*H*C)
+ * as 0/1 bytes, player to move.  Both synchronise.                         */
+int mz_replay_get_game(mz_handle* h, int32_t i, int32_t* T, uint8_t* obs, int32_t* actions,
+                       float* rewards, int32_t* to_play, float* child_visits, float* root_values);
+int mz_selfplay_slots(mz_handle* h, int32_t* history_len, uint8_t* board, int32_t* player);
+
 /* Name of the search kernel variant the last search launched (for profiles):
  * mz_search_small{1,2,4} (T games per workgroup, G <= 4 x #CUs) or the
  * 16-game MFMA tile kernel mz_search_kernel_{lds,hbm}[_res].  Environment

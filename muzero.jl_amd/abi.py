@@ -16,6 +16,7 @@ from .config import (MzConfig, MzFFHP, MzResNetHP, ResNetHP, hidden_size, stacke
                      to_c_ffhp, to_c_resnet_hp)
 
 NET_REPR, NET_PRED, NET_DYN = 0, 1, 2
+ENV_TICTACTOE, ENV_CONNECT4 = 0, 1
 
 _lib = None
 
@@ -56,6 +57,13 @@ SIGNATURES = {
     "mz_grad_count": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_size_t)]),
     "mz_learner_grad_dev": (ctypes.c_int, [_VP, ctypes.POINTER(MzBatch), _VP, _VP, _VP]),
     "mz_learner_apply_dev": (ctypes.c_int, [_VP, _VP, ctypes.c_float, ctypes.c_double, _VP]),
+    "mz_selfplay_init": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "mz_selfplay_move": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float, _VP]),
+    "mz_replay_counts": (ctypes.c_int, [_VP, _VP, _VP]),
+    "mz_replay_save_game": (ctypes.c_int, [_VP, ctypes.c_int32, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "mz_replay_sample": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.POINTER(MzBatch), _VP, _VP]),
+    "mz_replay_get_game": (ctypes.c_int, [_VP, ctypes.c_int32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "mz_selfplay_slots": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
     "mz_search_variant": (ctypes.c_char_p, [_VP]),
     "mz_sync": (ctypes.c_int, [_VP]),
 }
@@ -79,6 +87,21 @@ def load_library(path=LIB_PATH):
 
 def _p(a):
     return None if a is None else a.ctypes.data_as(_VP)
+
+
+_hip = None
+
+
+def _copy_d2h(dst, src_ptr):
+    """hipMemcpy device -> host (the HIP runtime libmz is linked against)."""
+    global _hip
+    if _hip is None:
+        _hip = ctypes.CDLL("libamdhip64.so")
+        _hip.hipMemcpy.restype = ctypes.c_int
+        _hip.hipMemcpy.argtypes = [_VP, _VP, ctypes.c_size_t, ctypes.c_int]
+    rc = _hip.hipMemcpy(dst.ctypes.data_as(_VP), ctypes.c_void_p(src_ptr), dst.nbytes, 2)   # DeviceToHost
+    if rc != 0:
+        raise MzError(f"hipMemcpy failed ({rc})")
 
 
 class MzError(RuntimeError):
@@ -235,6 +258,80 @@ class Engine:
     def learner_apply_dev(self, grad_ptr, grad_scale, eta, stream=None):
         self._check(self.lib.mz_learner_apply_dev(self.h, grad_ptr, grad_scale, float(eta), stream),
                     "mz_learner_apply_dev")
+
+    # ---- device self-play + replay shard
+    def selfplay_init(self, env_kind, G, replay_games):
+        self._check(self.lib.mz_selfplay_init(self.h, env_kind, G, replay_games), "mz_selfplay_init")
+        self.sp_G = G
+        self.osz = int(np.prod(self.conf.observation_shape))
+
+    def selfplay_move(self, rng_step, game_offset=0, temperature=1.0, stream=None):
+        self._check(self.lib.mz_selfplay_move(self.h, rng_step, game_offset, temperature, stream),
+                    "mz_selfplay_move")
+
+    def replay_counts(self):
+        """({num_played_games, num_played_steps, total_samples}, games held)."""
+        c = np.zeros(3, np.int64)
+        n = ctypes.c_int32()
+        self._check(self.lib.mz_replay_counts(self.h, _p(c), ctypes.byref(n)), "mz_replay_counts")
+        return c, n.value
+
+    def replay_save_game(self, hist):
+        """save_game of a host GameHistory (selfplay.GameHistory)."""
+        a = hist.as_arrays()
+        obs = np.ascontiguousarray(a["observation"] != 0, np.uint8)
+        self._check(self.lib.mz_replay_save_game(
+            self.h, len(a["action"]), _p(obs), _p(np.ascontiguousarray(a["action"], np.int32)),
+            _p(np.ascontiguousarray(a["reward"], np.float32)), _p(np.ascontiguousarray(a["to_play"], np.int32)),
+            _p(np.ascontiguousarray(a["child_visits"], np.float32)),
+            _p(np.ascontiguousarray(a["root_values"], np.float32))), "mz_replay_save_game")
+
+    def replay_get_game(self, i):
+        """Game i of the shard (0 = oldest held) as a selfplay.GameHistory."""
+        from .selfplay import GameHistory
+        Tm = self.conf.max_moves + 1
+        T = ctypes.c_int32()
+        obs = np.zeros((Tm, self.osz), np.uint8)
+        act = np.zeros(Tm, np.int32)
+        rew = np.zeros(Tm, np.float32)
+        tp = np.zeros(Tm, np.int32)
+        cv = np.zeros((Tm, self.A), np.float32)
+        rv = np.zeros(Tm, np.float32)
+        self._check(self.lib.mz_replay_get_game(self.h, i, ctypes.byref(T), _p(obs), _p(act), _p(rew), _p(tp),
+                                                _p(cv), _p(rv)), "mz_replay_get_game")
+        n = T.value
+        return GameHistory(observation_history=[o.astype(np.float32) for o in obs[:n]],
+                           action_history=[int(x) for x in act[:n]], reward_history=[float(x) for x in rew[:n]],
+                           to_play_history=[int(x) for x in tp[:n]], child_visits=[c for c in cv[:n]],
+                           root_values=[float(x) for x in rv[:n]])
+
+    def replay_sample(self, B, step, stream=None, index=False):
+        """Device get_batch: returns (MzBatch of device pointers, index_batch (B, 2) or None)."""
+        b = MzBatch()
+        idx = np.zeros((B, 2), np.int32) if index else None
+        self._check(self.lib.mz_replay_sample(self.h, B, step, ctypes.byref(b), _p(idx) if index else None, stream),
+                    "mz_replay_sample")
+        return b, idx
+
+    def batch_to_host(self, b):
+        """Copy a device MzBatch (from replay_sample) into the host dict layout of ReplayBuffer.get_batch."""
+        B, K1, A = b.batch_size, self.conf.num_unroll_steps + 1, self.A
+        self.sync()
+        out = {}
+        for name, shape in (("observation", (B, self.obs_feat)), ("actions", (B, K1)), ("target_values", (B, K1)),
+                            ("target_rewards", (B, K1)), ("target_policies", (B, K1, A)), ("gradient_scale", (B,))):
+            a = np.empty(shape, np.float32)
+            _copy_d2h(a, getattr(b, name))
+            out[name] = a
+        return out
+
+    def selfplay_slots(self):
+        G = self.sp_G
+        ln = np.zeros(G, np.int32)
+        board = np.zeros((G, self.osz), np.uint8)
+        pl = np.zeros(G, np.int32)
+        self._check(self.lib.mz_selfplay_slots(self.h, _p(ln), _p(board), _p(pl)), "mz_selfplay_slots")
+        return ln, board, pl
 
     def search_variant(self):
         return self.lib.mz_search_variant(self.h).decode()

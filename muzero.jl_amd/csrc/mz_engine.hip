@@ -25,11 +25,17 @@ extern "C" __global__ void mz_search_kernel_hbm(SearchParams P);
 extern "C" __global__ void mz_search_kernel_lds_res(SearchParams P);
 #include "mz_small_params.h"
 #include "mz_resnet_params.h"
+#include "mz_selfplay_params.h"
 extern "C" __global__ void mz_rnet_forward_kernel(RNetParams Q);
 extern "C" __global__ void mz_rsearch_root(RSearchParams P);
 extern "C" __global__ void mz_rsearch_tree(RSearchParams P);
 extern "C" __global__ void mz_rsearch_nets(RSearchParams P);
 extern "C" __global__ void mz_runroll_kernel(RUnrollParams U);
+extern "C" __global__ void mz_sp_prepare(SpParams S);
+extern "C" __global__ void mz_sp_commit(SpParams S);
+extern "C" __global__ void mz_sp_order(SpParams S);
+extern "C" __global__ void mz_sp_store(SpParams S);
+extern "C" __global__ void mz_rp_sample(RpSampleParams Q);
 extern "C" __global__ void mz_search_small1(SmallParams P);
 extern "C" __global__ void mz_search_small2(SmallParams P);
 extern "C" __global__ void mz_search_small4(SmallParams P);
@@ -158,6 +164,18 @@ struct mz_handle {
     unsigned* d_counter = nullptr;          // last-block counter of mz_learner_grad_kernel
     float* d_lterm = nullptr;               // [2][B(K+1)] loss terms
     unsigned long long* d_stamps = nullptr;
+    // device self-play + replay shard (mz_selfplay.hip); own allocation list (re-init frees it)
+    int sp_env = -1, sp_G = 0, sp_T = 0, sp_osz = 0, sp_cap = 0;
+    uint8_t* d_sp_board = nullptr; int32_t* d_sp_player = nullptr; uint8_t* d_sp_over = nullptr;
+    SpHist sp_hist{}, sp_ring{};
+    long long* d_sp_counters = nullptr;
+    int32_t* d_sp_done = nullptr; int32_t* d_sp_rpos = nullptr;
+    float* d_sp_dpow = nullptr;
+    float *d_rs_obs = nullptr, *d_rs_act = nullptr, *d_rs_tv = nullptr, *d_rs_tr = nullptr, *d_rs_tp = nullptr,
+          *d_rs_gs = nullptr;
+    int32_t* d_rs_index = nullptr;
+    int rs_cap = 0;
+    std::vector<void*> sp_allocs;
     std::vector<void*> allocs;
 };
 
@@ -902,6 +920,7 @@ void mz_engine_destroy(mz_handle* h) {
     (void)hipSetDevice(h->device);
     for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
     for (void* p : h->allocs) (void)hipFree(p);
+    for (void* p : h->sp_allocs) (void)hipFree(p);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -1477,6 +1496,235 @@ int mz_debug_stamps(mz_handle* h, unsigned long long* out, int n_blocks) {
 const char* mz_search_variant(const mz_handle* h) {
     if (!h) return "";
     return h->last_variant.c_str();
+}
+
+// ------------------------------------------------ device self-play + replay
+}  // extern "C"
+
+template <typename T>
+static hipError_t spalloc(mz_handle* h, T** p, size_t n, bool zero = true) {
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T) + 16);
+    if (e == hipSuccess) {
+        h->sp_allocs.push_back(*p);
+        if (zero) e = hipMemset(*p, 0, n * sizeof(T) + 16);
+    }
+    return e;
+}
+
+static int sp_alloc_hist(mz_handle* h, SpHist& r, size_t n) {
+    const size_t T = (size_t)h->sp_T, A = (size_t)h->A;
+    MZ_TRY(h, spalloc(h, &r.obs, n * T * h->sp_osz));
+    MZ_TRY(h, spalloc(h, &r.act, n * T));
+    MZ_TRY(h, spalloc(h, &r.rew, n * T));
+    MZ_TRY(h, spalloc(h, &r.tp, n * T));
+    MZ_TRY(h, spalloc(h, &r.cv, n * T * A));
+    MZ_TRY(h, spalloc(h, &r.rv, n * T));
+    MZ_TRY(h, spalloc(h, &r.len, n));
+    return 0;
+}
+
+static SpParams sp_params(mz_handle* h) {
+    SpParams S;
+    std::memset(&S, 0, sizeof(S));
+    const mz_config& c = h->conf;
+    S.G = h->sp_G; S.env = h->sp_env; S.W = c.observation_shape[0]; S.H = c.observation_shape[1];
+    S.osz = h->sp_osz; S.P = h->plane; S.A = h->A; S.F = h->obs_feat; S.stacked = c.stacked_observations;
+    S.T = h->sp_T; S.max_moves = c.max_moves;
+    S.board = h->d_sp_board; S.player = h->d_sp_player; S.over = h->d_sp_over;
+    S.hist = h->sp_hist; S.ring = h->sp_ring; S.cap = h->sp_cap; S.counters = h->d_sp_counters;
+    S.obs = h->d_obs; S.legal = h->d_legal; S.tp = h->d_tp; S.cv = h->d_cv; S.rv = h->d_rv; S.act = h->d_act;
+    S.done = h->d_sp_done; S.ring_pos = h->d_sp_rpos;
+    return S;
+}
+
+extern "C" {
+
+int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games) {
+    if (!h) return -2;
+    const mz_config& c = h->conf;
+    const int W = c.observation_shape[0], H = c.observation_shape[1], C = c.observation_shape[2];
+    if (env_kind == MZ_ENV_TICTACTOE) {
+        if (W != 3 || H != 3 || C != 3 || h->A != 9) return fail(h, "TicTacToe needs observation_shape (3,3,3), 9 actions");
+    } else if (env_kind == MZ_ENV_CONNECT4) {
+        if (W != 6 || H != 7 || C != 3 || h->A != 7) return fail(h, "Connect4 needs observation_shape (6,7,3), 7 actions");
+    } else {
+        return fail(h, "unknown env_kind");
+    }
+    if (G < 1 || G > h->max_games) return fail(h, "G must be in 1..max_games");
+    if (replay_games < G) return fail(h, "replay_games must be >= G (one move can finish every slot)");
+    if (c.max_moves < 1) return fail(h, "max_moves must be >= 1");
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    for (void* p : h->sp_allocs) (void)hipFree(p);
+    h->sp_allocs.clear();
+    h->rs_cap = 0;
+    h->sp_env = env_kind; h->sp_G = G; h->sp_cap = replay_games;
+    h->sp_T = c.max_moves + 1; h->sp_osz = W * H * C;
+    MZ_TRY(h, spalloc(h, &h->d_sp_board, (size_t)G * h->sp_osz));
+    MZ_TRY(h, spalloc(h, &h->d_sp_player, (size_t)G));
+    MZ_TRY(h, spalloc(h, &h->d_sp_over, (size_t)G));
+    if (sp_alloc_hist(h, h->sp_hist, (size_t)G)) return -1;
+    if (sp_alloc_hist(h, h->sp_ring, (size_t)replay_games)) return -1;
+    MZ_TRY(h, spalloc(h, &h->d_sp_counters, 4));
+    MZ_TRY(h, spalloc(h, &h->d_sp_done, (size_t)G));
+    MZ_TRY(h, spalloc(h, &h->d_sp_rpos, (size_t)G));
+    // f32(discount^n) as Julia's Float32^Int (≈ f32(pow(f64))), n = 0..td+1
+    std::vector<float> dp(c.td_steps + 2);
+    for (int n = 0; n < (int)dp.size(); ++n) dp[n] = (float)std::pow((double)c.discount, (double)n);
+    MZ_TRY(h, spalloc(h, &h->d_sp_dpow, dp.size()));
+    MZ_TRY(h, hipMemcpy(h->d_sp_dpow, dp.data(), dp.size() * 4, hipMemcpyHostToDevice));
+    // every slot: new game (boards: empty plane set, player 1)
+    std::vector<uint8_t> b((size_t)G * h->sp_osz, 0);
+    const int cells = W * H;
+    for (int g = 0; g < G; ++g)
+        for (int k = 2 * cells; k < 3 * cells; ++k) b[(size_t)g * h->sp_osz + k] = 1;
+    std::vector<int32_t> pl(G, 1);
+    MZ_TRY(h, hipMemcpy(h->d_sp_board, b.data(), b.size(), hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(h->d_sp_player, pl.data(), (size_t)G * 4, hipMemcpyHostToDevice));
+    return 0;
+}
+
+int mz_selfplay_move(mz_handle* h, uint32_t rng_step, uint32_t game_offset, float temperature, void* stream) {
+    if (!h) return -2;
+    if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
+    MZ_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    SpParams S = sp_params(h);
+    const int G = h->sp_G;
+    const dim3 waves((G + 3) / 4);
+    hipLaunchKernelGGL(mz_sp_prepare, waves, dim3(256), 0, st, S);
+    MZ_TRY(h, hipGetLastError());
+    int rc = mz_mcts_search_dev(h, G, h->d_obs, h->d_legal, h->d_tp, 1, rng_step, game_offset, temperature, h->d_cv,
+                                h->d_rv, h->d_act, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(mz_sp_commit, waves, dim3(256), 0, st, S);
+    hipLaunchKernelGGL(mz_sp_order, dim3(1), dim3(1024), 0, st, S);
+    hipLaunchKernelGGL(mz_sp_store, dim3(G), dim3(256), 0, st, S);
+    MZ_TRY(h, hipGetLastError());
+    return 0;
+}
+
+int mz_replay_counts(mz_handle* h, int64_t* counts, int32_t* games_in_buffer) {
+    if (!h) return -2;
+    if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    long long c[3];
+    MZ_TRY(h, hipMemcpy(c, h->d_sp_counters, sizeof(c), hipMemcpyDeviceToHost));
+    if (counts) for (int i = 0; i < 3; ++i) counts[i] = c[i];
+    if (games_in_buffer) *games_in_buffer = (int32_t)std::min<long long>(c[0], h->sp_cap);
+    return 0;
+}
+
+int mz_replay_save_game(mz_handle* h, int32_t T, const uint8_t* obs, const int32_t* actions, const float* rewards,
+                        const int32_t* to_play, const float* child_visits, const float* root_values) {
+    if (!h) return -2;
+    if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
+    if (T < 1 || T > h->sp_T) return fail(h, "game length must be in 1..max_moves+1");
+    if (!obs || !actions || !rewards || !to_play || !child_visits || !root_values) return fail(h, "null array");
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    long long c[3];
+    MZ_TRY(h, hipMemcpy(c, h->d_sp_counters, sizeof(c), hipMemcpyDeviceToHost));
+    const long long num = c[0] + 1;
+    const int slot = (int)((num - 1) % h->sp_cap);
+    if (num > h->sp_cap) {                          // the FIFO evicts game num - cap (:156-160)
+        int32_t old = 0;
+        MZ_TRY(h, hipMemcpy(&old, h->sp_ring.len + slot, 4, hipMemcpyDeviceToHost));
+        c[2] -= old;
+    }
+    c[0] = num; c[1] += T; c[2] += T;
+    const size_t base = (size_t)slot * h->sp_T, A = (size_t)h->A;
+    const SpHist& r = h->sp_ring;
+    MZ_TRY(h, hipMemcpy(r.obs + base * h->sp_osz, obs, (size_t)T * h->sp_osz, hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(r.act + base, actions, (size_t)T * 4, hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(r.rew + base, rewards, (size_t)T * 4, hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(r.tp + base, to_play, (size_t)T * 4, hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(r.cv + base * A, child_visits, (size_t)T * A * 4, hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(r.rv + base, root_values, (size_t)T * 4, hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(r.len + slot, &T, 4, hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(h->d_sp_counters, c, sizeof(c), hipMemcpyHostToDevice));
+    return 0;
+}
+
+int mz_replay_sample(mz_handle* h, int32_t B, uint32_t step, mz_batch* batch, int32_t* index_batch, void* stream) {
+    if (!h || !batch) return -2;
+    if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
+    if (B < 1) return fail(h, "batch_size must be >= 1");
+    MZ_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    {
+        long long played = 0;                     // sample_n_games needs a non-empty buffer
+        MZ_TRY(h, hipStreamSynchronize(st));
+        MZ_TRY(h, hipMemcpy(&played, h->d_sp_counters, sizeof(played), hipMemcpyDeviceToHost));
+        if (played == 0) return fail(h, "replay buffer is empty");
+    }
+    const int K1 = h->conf.num_unroll_steps + 1, A = h->A;
+    if (B > h->rs_cap) {
+        MZ_TRY(h, spalloc(h, &h->d_rs_obs, (size_t)B * h->obs_feat, false));
+        MZ_TRY(h, spalloc(h, &h->d_rs_act, (size_t)B * K1, false));
+        MZ_TRY(h, spalloc(h, &h->d_rs_tv, (size_t)B * K1, false));
+        MZ_TRY(h, spalloc(h, &h->d_rs_tr, (size_t)B * K1, false));
+        MZ_TRY(h, spalloc(h, &h->d_rs_tp, (size_t)B * K1 * A, false));
+        MZ_TRY(h, spalloc(h, &h->d_rs_gs, (size_t)B, false));
+        MZ_TRY(h, spalloc(h, &h->d_rs_index, (size_t)B * 2, false));
+        h->rs_cap = B;
+    }
+    RpSampleParams Q;
+    std::memset(&Q, 0, sizeof(Q));
+    Q.B = B; Q.K = K1 - 1; Q.A = A; Q.osz = h->sp_osz; Q.P = h->plane; Q.F = h->obs_feat;
+    Q.stacked = h->conf.stacked_observations; Q.T = h->sp_T; Q.td = h->conf.td_steps; Q.cap = h->sp_cap;
+    Q.seed = h->seed; Q.step = step; Q.ring = h->sp_ring; Q.counters = h->d_sp_counters; Q.disc_pow = h->d_sp_dpow;
+    Q.obs = h->d_rs_obs; Q.actions = h->d_rs_act; Q.tv = h->d_rs_tv; Q.tr = h->d_rs_tr; Q.tpol = h->d_rs_tp;
+    Q.gscale = h->d_rs_gs; Q.index = h->d_rs_index;
+    hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, Q);
+    MZ_TRY(h, hipGetLastError());
+    batch->batch_size = B;
+    batch->observation = h->d_rs_obs; batch->actions = h->d_rs_act; batch->target_values = h->d_rs_tv;
+    batch->target_rewards = h->d_rs_tr; batch->target_policies = h->d_rs_tp; batch->gradient_scale = h->d_rs_gs;
+    if (index_batch) {
+        MZ_TRY(h, hipMemcpyAsync(index_batch, h->d_rs_index, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+        MZ_TRY(h, hipStreamSynchronize(st));
+    }
+    return 0;
+}
+
+int mz_replay_get_game(mz_handle* h, int32_t i, int32_t* T, uint8_t* obs, int32_t* actions, float* rewards,
+                       int32_t* to_play, float* child_visits, float* root_values) {
+    if (!h) return -2;
+    if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    long long c[3];
+    MZ_TRY(h, hipMemcpy(c, h->d_sp_counters, sizeof(c), hipMemcpyDeviceToHost));
+    const long long held = std::min<long long>(c[0], h->sp_cap);
+    if (i < 0 || i >= held) return fail(h, "game index out of range");
+    const long long num = c[0] - held + 1 + i;
+    const int slot = (int)((num - 1) % h->sp_cap);
+    const size_t base = (size_t)slot * h->sp_T, A = (size_t)h->A;
+    const SpHist& r = h->sp_ring;
+    int32_t len = 0;
+    MZ_TRY(h, hipMemcpy(&len, r.len + slot, 4, hipMemcpyDeviceToHost));
+    if (T) *T = len;
+    if (obs) MZ_TRY(h, hipMemcpy(obs, r.obs + base * h->sp_osz, (size_t)len * h->sp_osz, hipMemcpyDeviceToHost));
+    if (actions) MZ_TRY(h, hipMemcpy(actions, r.act + base, (size_t)len * 4, hipMemcpyDeviceToHost));
+    if (rewards) MZ_TRY(h, hipMemcpy(rewards, r.rew + base, (size_t)len * 4, hipMemcpyDeviceToHost));
+    if (to_play) MZ_TRY(h, hipMemcpy(to_play, r.tp + base, (size_t)len * 4, hipMemcpyDeviceToHost));
+    if (child_visits) MZ_TRY(h, hipMemcpy(child_visits, r.cv + base * A, (size_t)len * A * 4, hipMemcpyDeviceToHost));
+    if (root_values) MZ_TRY(h, hipMemcpy(root_values, r.rv + base, (size_t)len * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int mz_selfplay_slots(mz_handle* h, int32_t* history_len, uint8_t* board, int32_t* player) {
+    if (!h) return -2;
+    if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    const size_t G = (size_t)h->sp_G;
+    if (history_len) MZ_TRY(h, hipMemcpy(history_len, h->sp_hist.len, G * 4, hipMemcpyDeviceToHost));
+    if (board) MZ_TRY(h, hipMemcpy(board, h->d_sp_board, G * h->sp_osz, hipMemcpyDeviceToHost));
+    if (player) MZ_TRY(h, hipMemcpy(player, h->d_sp_player, G * 4, hipMemcpyDeviceToHost));
+    return 0;
 }
 
 int mz_sync(mz_handle* h) {

@@ -1,0 +1,288 @@
+// mz_selfplay.hip — device self-play loop body and device replay shard
+// (SURVEY §8f-1, §8f-2).  One move of G lockstep games (play_game's loop body,
+// SelfPlay.jl:343-380) is: mz_sp_prepare (observation append, stacked
+// observations, legal mask, to_play) -> the batched search -> mz_sp_commit
+// (env step, history append, finish test) -> mz_sp_order (ring slots of the
+// finished games in slot order, replay counters) -> mz_sp_store (finished
+// game -> replay ring, slot reset).  Nothing crosses PCIe.  mz_rp_sample is
+// get_batch + make_target on the ring, writing an mz_batch in HBM.
+//
+// Env rules: TicTacToe exactly as games/tictactoe/game.jl with quirk Q14 (the
+// win test looks at the plane of the player TO MOVE; reward ±1 by the mover's
+// id), Connect4 as games/connect4.py.  Host mirrors:
+// muzero.jl_amd/games/{tictactoe,connect4}.py, selfplay.py, replay_buffer.py.
+#include "mz_internal.h"
+#include "mz_selfplay_params.h"
+
+// ------------------------------------------------------------------- envs
+__constant__ int8_t c_ttt_lines[8][3] = {{0, 3, 6}, {1, 4, 7}, {2, 5, 8}, {0, 1, 2},
+                                          {3, 4, 5}, {6, 7, 8}, {0, 4, 8}, {6, 4, 2}};
+
+// TicTacToe (game.jl:102-115, Q14): a line on the plane of player p
+__device__ __forceinline__ bool ttt_line(const uint8_t* b, int p) {
+    const uint8_t* pl = b + 9 * (p - 1);
+    bool any = false;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) any |= pl[c_ttt_lines[l][0]] && pl[c_ttt_lines[l][1]] && pl[c_ttt_lines[l][2]];
+    return any;
+}
+
+__device__ __forceinline__ bool c4_wins(const uint8_t* stones, int w, int h, int W, int H) {
+    const int dw[4] = {1, 0, 1, 1}, dh[4] = {0, 1, 1, -1};
+    for (int d = 0; d < 4; ++d) {
+        int n = 1;
+        for (int s = 1; s >= -1; s -= 2) {
+            int ww = w + s * dw[d], hh = h + s * dh[d];
+            while (ww >= 0 && ww < W && hh >= 0 && hh < H && stones[ww + W * hh]) {
+                ++n;
+                ww += s * dw[d];
+                hh += s * dh[d];
+            }
+        }
+        if (n >= 4) return true;
+    }
+    return false;
+}
+
+// legal actions (1..A) as a bit mask
+__device__ uint32_t env_legal(const SpParams& S, int g) {
+    const uint8_t* b = S.board + (size_t)g * S.osz;
+    uint32_t m = 0;
+    if (S.env == MZ_ENV_TICTACTOE) {                    // game.jl:37-43
+        if (ttt_line(b, S.player[g])) return 0;
+        for (int c = 0; c < 9; ++c) m |= (uint32_t)b[18 + c] << c;
+    } else {
+        if (S.over[g]) return 0;
+        const int cells = S.W * S.H;
+        for (int h = 0; h < S.H; ++h) m |= (uint32_t)b[2 * cells + (S.W - 1) + S.W * h] << h;
+    }
+    return m;
+}
+
+// env(action) (game.jl:45-52) + is_terminated / reward (:85-100): returns the
+// reward recorded for the mover, sets *done
+__device__ float env_step(const SpParams& S, int g, int a, bool* done) {
+    uint8_t* b = S.board + (size_t)g * S.osz;
+    const int p = S.player[g];
+    if (S.env == MZ_ENV_TICTACTOE) {
+        const int c = a - 1;
+        b[18 + c] = 0;
+        b[9 * (p - 1) + c] = 1;
+        const int np = p % 2 + 1;
+        S.player[g] = np;
+        const bool win = ttt_line(b, np);
+        bool full = true;
+        for (int k = 0; k < 9; ++k) full &= b[18 + k] == 0;
+        *done = full || win;
+        return (*done && win) ? (p == 1 ? 1.0f : -1.0f) : 0.0f;
+    }
+    const int W = S.W, cells = S.W * S.H, h = a - 1;
+    int w = 0;
+    while (w < W && !b[2 * cells + w + W * h]) ++w;
+    const int cell = w + W * h;
+    b[2 * cells + cell] = 0;
+    b[(p - 1) * cells + cell] = 1;
+    const bool win = c4_wins(b + (p - 1) * cells, w, h, W, S.H);
+    bool full = true;
+    for (int k = 0; k < cells; ++k) full &= b[2 * cells + k] == 0;
+    *done = win || full;
+    S.over[g] = *done;
+    S.player[g] = 3 - p;
+    return win ? 1.0f : 0.0f;
+}
+
+__device__ void env_reset(const SpParams& S, int g, int lane) {
+    uint8_t* b = S.board + (size_t)g * S.osz;
+    const int cells = S.osz / 3;
+    for (int k = lane; k < S.osz; k += 64) b[k] = k >= 2 * cells;
+    if (lane == 0) { S.player[g] = 1; S.over[g] = 0; }
+}
+
+// get_stacked_observations (SelfPlay.jl:128-149, Q15) of record `obs`/`act`
+// at 1-based index (cur = observation `index`): [obs_t, (action plane = raw
+// id, obs_{t-1}) ...], zeros before the first move
+__device__ __forceinline__ void stacked_obs(float* out, const uint8_t* cur, const uint8_t* obs, const int32_t* act,
+                                            int index, int osz, int P, int stacked, int lane) {
+    for (int k = lane; k < osz; k += 64) out[k] = (float)cur[k];
+    int o = osz;
+    for (int past = index - 1; past >= index - stacked; --past) {
+        if (past >= 1) {
+            const float av = (float)act[past - 1];
+            for (int k = lane; k < P; k += 64) out[o + k] = av;
+            const uint8_t* po = obs + (size_t)(past - 1) * osz;
+            for (int k = lane; k < osz; k += 64) out[o + P + k] = (float)po[k];
+        } else {
+            for (int k = lane; k < P + osz; k += 64) out[o + k] = 0.0f;
+        }
+        o += P + osz;
+    }
+}
+
+// ------------------------------------------------------------ self-play move
+// one wave per game slot
+extern "C" __global__ __launch_bounds__(256) void mz_sp_prepare(SpParams S) {
+    const int g = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (g >= S.G) return;
+    const int t = S.hist.len[g];                                   // moves so far
+    uint8_t* ho = S.hist.obs + ((size_t)g * S.T + t) * S.osz;     // observation_history append (:352)
+    const uint8_t* b = S.board + (size_t)g * S.osz;
+    for (int k = lane; k < S.osz; k += 64) ho[k] = b[k];
+    stacked_obs(S.obs + (size_t)g * S.F, b, S.hist.obs + (size_t)g * S.T * S.osz, S.hist.act + (size_t)g * S.T,
+                t + 1, S.osz, S.P, S.stacked, lane);                // :355
+    if (lane == 0) {
+        const uint32_t m = env_legal(S, g);
+        for (int a = 0; a < S.A; ++a) S.legal[(size_t)g * S.A + a] = (m >> a) & 1u;
+        S.tp[g] = S.player[g];                                     // :351
+    }
+}
+
+extern "C" __global__ __launch_bounds__(256) void mz_sp_commit(SpParams S) {
+    const int g = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (g >= S.G) return;
+    const int t = S.hist.len[g];
+    const size_t r = (size_t)g * S.T + t;
+    for (int a = lane; a < S.A; a += 64) S.hist.cv[r * S.A + a] = S.cv[(size_t)g * S.A + a];   // :375-379
+    if (lane == 0) {
+        const int a = S.act[g];
+        const int mover = S.player[g];
+        bool done = false;
+        const float rew = env_step(S, g, a, &done);                // :366-368
+        S.hist.act[r] = a;
+        S.hist.rew[r] = rew;
+        S.hist.tp[r] = mover;
+        S.hist.rv[r] = S.rv[g];
+        S.hist.len[g] = t + 1;
+        S.done[g] = done || t + 1 > S.max_moves;                  // :343 (> max_moves)
+    }
+}
+
+// Ring slots of this move's finished games in slot order (the host driver
+// saves them in ascending slot order) and the replay counters (save_game,
+// ReplayBuffer.jl:133-161).  One workgroup.
+extern "C" __global__ __launch_bounds__(1024) void mz_sp_order(SpParams S) {
+    __shared__ int cnt[1024];
+    __shared__ long long red[3][1024];
+    const int tid = threadIdx.x, per = (S.G + 1023) / 1024;
+    const int g0 = tid * per, g1 = min(S.G, g0 + per);
+    int n = 0;
+    for (int g = g0; g < g1; ++g) n += S.done[g] != 0;
+    cnt[tid] = n;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {                           // inclusive scan
+        const int v = tid >= o ? cnt[tid - o] : 0;
+        __syncthreads();
+        cnt[tid] += v;
+        __syncthreads();
+    }
+    const long long played = S.counters[0];
+    long long rank = cnt[tid] - n, steps = 0, evicted = 0;
+    for (int g = g0; g < g1; ++g) {
+        if (!S.done[g]) { S.ring_pos[g] = -1; continue; }
+        const long long num = played + rank + 1;                   // game number (1-based)
+        const int slot = (int)((num - 1) % S.cap);
+        const int len = S.hist.len[g];
+        if (num > S.cap) evicted += S.ring.len[slot];              // the game it replaces
+        S.ring_pos[g] = slot;
+        steps += len;
+        ++rank;
+    }
+    red[0][tid] = n; red[1][tid] = steps; red[2][tid] = evicted;
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+        if (tid < o)
+            for (int k = 0; k < 3; ++k) red[k][tid] += red[k][tid + o];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        S.counters[0] = played + red[0][0];
+        S.counters[1] += red[1][0];
+        S.counters[2] += red[1][0] - red[2][0];
+    }
+}
+
+// finished game -> its ring slot; the slot starts a new game (one workgroup per slot)
+extern "C" __global__ __launch_bounds__(256) void mz_sp_store(SpParams S) {
+    const int g = blockIdx.x;
+    if (!S.done[g]) return;
+    const int slot = S.ring_pos[g], len = S.hist.len[g], tid = threadIdx.x;
+    const size_t src = (size_t)g * S.T, dst = (size_t)slot * S.T;
+    for (int k = tid; k < len * S.osz; k += blockDim.x) S.ring.obs[dst * S.osz + k] = S.hist.obs[src * S.osz + k];
+    for (int k = tid; k < len * S.A; k += blockDim.x) S.ring.cv[dst * S.A + k] = S.hist.cv[src * S.A + k];
+    for (int k = tid; k < len; k += blockDim.x) {
+        S.ring.act[dst + k] = S.hist.act[src + k];
+        S.ring.rew[dst + k] = S.hist.rew[src + k];
+        S.ring.tp[dst + k] = S.hist.tp[src + k];
+        S.ring.rv[dst + k] = S.hist.rv[src + k];
+    }
+    __syncthreads();                               // every thread has read len and done
+    if (tid == 0) { S.ring.len[slot] = len; S.hist.len[g] = 0; S.done[g] = 0; }
+    if (tid < 64) env_reset(S, g, tid);
+}
+
+// ------------------------------------------------------------- replay sample
+// compute_target_value (ReplayBuffer.jl:5-20, Q9), f32, 1-based index
+__device__ float rp_target_value(const RpSampleParams& Q, const float* rv, const int32_t* tp, const float* rew, int T,
+                                 int index) {
+    const int bi = index + Q.td;
+    if (bi >= T) return 0.0f;
+    const float r0 = rv[bi - 1];
+    const float last = tp[bi - 1] == tp[index - 1] ? r0 : -r0;
+    float value = last * Q.disc_pow[Q.td];
+    for (int i = 1; i <= Q.td + 1; ++i) {
+        const float r = rew[index + i - 2];
+        const float sr = tp[index - 1] == tp[index + i - 1] ? r : -r;
+        value = value + sr * Q.disc_pow[i];
+    }
+    return value;
+}
+
+// one wave per sample (get_batch, :188-217)
+extern "C" __global__ __launch_bounds__(256) void mz_rp_sample(RpSampleParams Q) {
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (b >= Q.B) return;
+    const long long played = Q.counters[0];
+    const int n = (int)(played < Q.cap ? played : Q.cap);
+    const long long oldest = played - n + 1;                       // game number of ids[0]
+    const uint32_t gi = mz_rng_below(mz_rng_u32(Q.seed, MZ_RNG_GAME, (uint32_t)b, Q.step, 0), (uint32_t)n);   // :102
+    const long long num = oldest + gi;
+    const int slot = (int)((num - 1) % Q.cap);
+    const size_t base = (size_t)slot * Q.T;
+    const int T = Q.ring.len[slot];
+    const int pos = (int)mz_rng_below(mz_rng_u32(Q.seed, MZ_RNG_POS, (uint32_t)b, Q.step, 0), (uint32_t)T) + 1;  // :80
+    const int K1 = Q.K + 1, A = Q.A;
+    const float* rv = Q.ring.rv + base;
+    const int32_t* tp = Q.ring.tp + base;
+    const float* rew = Q.ring.rew + base;
+    const int32_t* act = Q.ring.act + base;
+    const float* cv = Q.ring.cv + base * A;
+    const float uni = 1.0f / (float)A;
+    for (int k = lane; k < K1; k += 64) {                          // make_target (:25-50)
+        const int ci = pos + k;
+        float v = 0.0f, r = 0.0f, a;
+        if (ci < T) {
+            v = rp_target_value(Q, rv, tp, rew, T, ci);
+            r = rew[ci - 1];
+            a = (float)act[ci - 1];
+        } else if (ci == T) {
+            r = rew[ci - 1];
+            a = (float)act[ci - 1];
+        } else {                                                   // absorbing states
+            a = (float)(mz_rng_below(mz_rng_u32(Q.seed, MZ_RNG_ABSORB, (uint32_t)b, Q.step, (uint32_t)k), (uint32_t)A) + 1);
+        }
+        Q.tv[(size_t)b * K1 + k] = v;
+        Q.tr[(size_t)b * K1 + k] = r;
+        Q.actions[(size_t)b * K1 + k] = a;
+    }
+    for (int e = lane; e < K1 * A; e += 64) {
+        const int k = e / A, a = e - k * A, ci = pos + k;
+        Q.tpol[(size_t)b * K1 * A + e] = ci < T ? cv[(size_t)(ci - 1) * A + a] : uni;
+    }
+    stacked_obs(Q.obs + (size_t)b * Q.F, Q.ring.obs + (base + pos - 1) * Q.osz, Q.ring.obs + base * Q.osz, act, pos,
+                Q.osz, Q.P, Q.stacked, lane);
+    if (lane == 0) {
+        const int gs = T + 1 - pos;                                // :212 min(K, len(action_history)+1-pos)
+        Q.gscale[b] = (float)(Q.K < gs ? Q.K : gs);
+        Q.index[2 * b] = (int)num;
+        Q.index[2 * b + 1] = pos;
+    }
+}

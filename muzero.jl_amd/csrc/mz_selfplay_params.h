@@ -1,0 +1,49 @@
+// mz_selfplay_params.h — device self-play and the device
+// replay shard (§8f-2): parameters shared by the host (mz_engine.hip) and the
+// kernels (mz_selfplay.hip).
+//
+// Per game slot g (G slots played in lockstep, SelfPlay.jl:330-382):
+//   env      board[g][osz] (0/1 bytes: planes [p1, p2, empty], col-major cells),
+//            player[g] (1 or 2), over[g];
+//   history  GameHistory (Constructors.jl:6-16) of the game in progress, up to
+//            T = max_moves + 1 moves: obs[g][T][osz] bytes, act / rew / tp /
+//            rv [g][T], cv [g][T][A], len[g] = moves recorded.
+// Replay shard (ReplayBuffer.jl:133-161, PER = false): a FIFO ring of `cap`
+// finished games with the same per-game layout; game number n (1-based, the
+// Dict key of save_game) lives in ring slot (n - 1) mod cap.
+#pragma once
+#include <stdint.h>
+
+struct SpHist {                 // a set of game records: [n][T] ...
+    uint8_t* obs;               // [n][T][osz]
+    int32_t* act;               // [n][T] 1-based actions
+    float* rew;                 // [n][T]
+    int32_t* tp;                // [n][T] to_play before the move
+    float* cv;                  // [n][T][A] child visit distributions
+    float* rv;                  // [n][T] root values
+    int32_t* len;               // [n] moves
+};
+
+struct SpParams {
+    int G, env, W, H, osz, P, A, F, stacked, T, max_moves;
+    uint8_t* board; int32_t* player; uint8_t* over;
+    SpHist hist;                // [G] games in progress
+    SpHist ring;                // [cap] replay shard
+    int cap;
+    long long* counters;        // [0] num_played_games, [1] num_played_steps, [2] total_samples
+    // search io (device buffers of the engine)
+    float* obs; uint8_t* legal; int32_t* tp; const float* cv; const float* rv; const int32_t* act;
+    int32_t* done;              // [G] finished this move
+    int32_t* ring_pos;          // [G] ring slot of the finished game
+};
+
+// get_batch + make_target (ReplayBuffer.jl:5-50, 73-107, 188-217) on the shard
+struct RpSampleParams {
+    int B, K, A, osz, P, F, stacked, T, td, cap;
+    uint64_t seed; uint32_t step;
+    SpHist ring;
+    const long long* counters;
+    const float* disc_pow;      // [td + 2]: f32(discount^n) as Julia's Float32^Int
+    float* obs; float* actions; float* tv; float* tr; float* tpol; float* gscale;
+    int32_t* index;             // [B][2]: (game number, position) — index_batch
+};

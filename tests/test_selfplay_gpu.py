@@ -1,0 +1,148 @@
+"""Device self-play and replay shard through the C ABI,
+against the host driver (selfplay.BatchedSelfPlay over the same engine search
+and the numpy envs) and the host ReplayBuffer: finished games, games in
+progress, replay counters, FIFO eviction and get_batch/make_target samples,
+bit for bit; then a learner step fed straight from the device batch."""
+import dataclasses
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _env(kind):
+    from muzero_jl_amd import abi
+    from muzero_jl_amd.games import connect4, tictactoe
+    if kind == "ttt":
+        return tictactoe, tictactoe.BatchedTicTacToe, abi.ENV_TICTACTOE
+    return connect4, connect4.BatchedConnect4, abi.ENV_CONNECT4
+
+
+def _engines(mod, conf, hyper, G, seed=5):
+    from muzero_jl_amd import abi
+    from muzero_jl_amd.networks import init_nets
+    nets = init_nets(conf, hyper, seed=seed + 100)
+    out = []
+    for _ in range(2):
+        e = abi.Engine(conf, hyper, device=0, max_games=G, rng_seed=seed)
+        for n, w in enumerate(nets):
+            e.set_weights(n, w)
+        out.append(e)
+    return out
+
+
+def _same_game(dev, host, osz):
+    a, b = dev.as_arrays(), host.as_arrays()
+    assert np.array_equal(a["observation"].reshape(-1, osz), b["observation"].reshape(-1, osz))
+    for k in ("action", "reward", "to_play", "child_visits", "root_values"):
+        assert np.array_equal(a[k], b[k]), k
+
+
+def _play_both(kind, G, moves, cap, S=6, resnet=False, step0=100, temperature=1.0):
+    from muzero_jl_amd.selfplay import BatchedSelfPlay
+    mod, env_cls, env_kind = _env(kind)
+    conf = dataclasses.replace(mod.conf, num_iters=S, replay_buffer_size=cap)
+    hyper = mod.resnet_hyper if resnet else mod.hyper
+    eh, ed = _engines(mod, conf, hyper, G)
+    sp = BatchedSelfPlay(eh, env_cls, G, game_offset=7, step0=step0)
+    ed.selfplay_init(env_kind, G, cap)
+    for m in range(moves):
+        sp.play_move(temperature)
+        ed.selfplay_move(step0 + m, game_offset=7, temperature=temperature)
+    return conf, sp, eh, ed
+
+
+@pytest.mark.parametrize("kind,G,moves", [("ttt", 24, 13), ("c4", 12, 30)])
+def test_device_selfplay_matches_host(kind, G, moves):
+    conf, sp, eh, ed = _play_both(kind, G, moves, cap=8 * G)
+    osz = int(np.prod(conf.observation_shape))
+    counts, held = ed.replay_counts()
+    assert counts[0] == len(sp.finished) and held == len(sp.finished) and held > 0
+    assert counts[1] == sum(len(h.root_values) for h in sp.finished) == counts[2]
+    for i, h in enumerate(sp.finished):
+        _same_game(ed.replay_get_game(i), h, osz)
+    ln, board, player = ed.selfplay_slots()
+    assert np.array_equal(ln, [len(h.action_history) for h in sp.histories])
+    assert np.array_equal(board, sp.env.board.astype(np.uint8)) and np.array_equal(player, sp.env.player)
+    eh.close(); ed.close()
+
+
+def test_device_selfplay_resnet_matches_host():
+    conf, sp, eh, ed = _play_both("ttt", 16, 11, cap=64, S=4, resnet=True)
+    counts, held = ed.replay_counts()
+    assert counts[0] == len(sp.finished) > 0
+    for i, h in enumerate(sp.finished):
+        _same_game(ed.replay_get_game(i), h, 27)
+    eh.close(); ed.close()
+
+
+def test_replay_fifo_and_sample_match_host():
+    """cap = G: the FIFO evicts; counters, held games and samples follow the
+    host ReplayBuffer fed the same finished games in the same order."""
+    from muzero_jl_amd.replay_buffer import ReplayBuffer
+    G = 16
+    conf, sp, eh, ed = _play_both("ttt", G, 30, cap=G)
+    rb = ReplayBuffer(conf, seed=5)
+    for h in sp.finished:
+        rb.save_game(h)
+    counts, held = ed.replay_counts()
+    assert len(sp.finished) > G                                  # eviction happened
+    assert (counts[0], counts[1], counts[2]) == (rb.num_played_games, rb.num_played_steps, rb.total_samples)
+    assert held == len(rb) == G
+    for i, (gid, h) in enumerate(rb.buffer.items()):
+        _same_game(ed.replay_get_game(i), h, 27)
+    for step in (1, 2, 77):
+        B = 40
+        conf_b = dataclasses.replace(conf, batch_size=B)
+        rb.conf = conf_b
+        idx_h, bh = rb.get_batch(step)
+        b, idx_d = ed.replay_sample(B, step, index=True)
+        bd = ed.batch_to_host(b)
+        assert [tuple(x) for x in idx_d] == [tuple(x) for x in idx_h]
+        for k in bh:
+            assert np.array_equal(bd[k], bh[k]), (step, k)
+    eh.close(); ed.close()
+
+
+def test_learner_step_from_device_batch():
+    """mz_replay_sample -> mz_learner_grad_dev/apply: same losses and weights as
+    mz_learner_step on the host-assembled batch of the same samples."""
+    import torch
+    from muzero_jl_amd.config import cos_schedule
+    from muzero_jl_amd.replay_buffer import ReplayBuffer
+    G = 16
+    conf, sp, eh, ed = _play_both("ttt", G, 12, cap=64)
+    rb = ReplayBuffer(dataclasses.replace(conf, batch_size=32), seed=5)
+    for h in sp.finished:
+        rb.save_game(h)
+    for step in (1, 2, 3):
+        _, bh = rb.get_batch(step)
+        lh = eh.learner_step(bh, cos_schedule(step))
+        b, _ = ed.replay_sample(32, step)
+        grad = torch.empty(ed.grad_count(), dtype=torch.float32, device="cuda")
+        losses = torch.empty(8, dtype=torch.float32, device="cuda")
+        ed.learner_grad_dev([b.observation, b.actions, b.target_values, b.target_rewards, b.target_policies,
+                             b.gradient_scale], 32, grad.data_ptr(), losses.data_ptr())
+        ed.learner_apply_dev(grad.data_ptr(), 1.0, cos_schedule(step))
+        ed.sync()
+        assert np.array_equal(losses.cpu().numpy()[:6], lh)
+        for n in range(3):
+            assert np.array_equal(ed.get_weights(n), eh.get_weights(n))
+    eh.close(); ed.close()
+
+
+def test_selfplay_rejects_bad_setup(ttt):
+    from muzero_jl_amd import abi
+    from muzero_jl_amd.abi import MzError
+    e = abi.Engine(ttt.conf, ttt.hyper, device=0, max_games=8, rng_seed=1)
+    with pytest.raises(MzError, match="Connect4 needs"):
+        e.selfplay_init(abi.ENV_CONNECT4, 8, 8)
+    with pytest.raises(MzError, match="replay_games"):
+        e.selfplay_init(abi.ENV_TICTACTOE, 8, 4)
+    with pytest.raises(MzError, match="mz_selfplay_init first"):
+        e.selfplay_move(0)
+    e.selfplay_init(abi.ENV_TICTACTOE, 8, 8)
+    with pytest.raises(MzError, match="empty"):
+        e.replay_sample(4, 1)
+    e.close()
