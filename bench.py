@@ -33,8 +33,9 @@ import torch.distributed as dist  # noqa: E402
 import _mzpkg  # noqa: E402
 
 _mzpkg.load()
-from muzero_jl_amd.abi import Engine  # noqa: E402
+from muzero_jl_amd.abi import ENV_CONNECT4, ENV_TICTACTOE, Engine  # noqa: E402
 from muzero_jl_amd.config import cos_schedule, to_c_config, to_c_ffhp, to_c_resnet_hp  # noqa: E402
+from muzero_jl_amd.games import connect4 as c4  # noqa: E402
 from muzero_jl_amd.games import tictactoe as ttt  # noqa: E402
 from muzero_jl_amd.networks import init_nets, net_macs  # noqa: E402
 from muzero_jl_amd.selfplay import random_positions  # noqa: E402
@@ -64,13 +65,26 @@ def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0, resnet=False)
                        f"oracle/mz_oracle.c single thread, {dt:.1f} s")
 
 
+def workload(game, resnet, G, S):
+    if game is c4:
+        return (f"Connect4 6x7 {'ResNet-8 (4 blocks x 64 filters, 3x3)' if resnet else 'FC'}, {G} games/GPU x "
+                f"{S} sims/move" + (" (configs[3]: 4096 games = 512/GPU x 8)" if resnet else ""))
+    if resnet:
+        return f"TicTacToe ResNet (2 blocks x 64 filters, 3x3), {G} games/GPU x {S} sims/move (configs[2])"
+    return f"TicTacToe FC (params.jl hyper), {G} games/GPU x {S} sims/move (configs[1])"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--game", choices=["tictactoe", "connect4"], default="tictactoe")
     ap.add_argument("--net", choices=["fc", "resnet"], default="fc")
-    ap.add_argument("--games", type=int, default=None, help="games per GPU (fc 512, resnet 2048)")
+    ap.add_argument("--games", type=int, default=None,
+                    help="games per GPU (tictactoe: fc 512, resnet 2048; connect4: 512)")
+    ap.add_argument("--pipeline-moves", type=int, default=20,
+                    help="timed moves of the device self-play loop (0 = skip that leg)")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--learner-steps", type=int, default=50)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -89,19 +103,24 @@ def main():
     sp = stream.cuda_stream
 
     resnet = args.net == "resnet"
-    conf = dataclasses.replace(ttt.conf, num_iters=args.sims)
-    hyper = ttt.resnet_hyper if resnet else ttt.hyper
-    G, S = args.games or (2048 if resnet else 512), args.sims
+    game = c4 if args.game == "connect4" else ttt
+    env_cls = c4.BatchedConnect4 if game is c4 else ttt.BatchedTicTacToe
+    conf = dataclasses.replace(game.conf, num_iters=args.sims)
+    hyper = game.resnet_hyper if resnet else game.hyper
+    A = len(conf.action_space)
+    G = args.games or (2048 if resnet and game is ttt else 512)
+    S = args.sims
     nets = init_nets(conf, hyper, seed=1234)              # identical replicas on every rank
     eng = Engine(conf, hyper, device=local, max_games=G, rng_seed=1)
     for n, w in enumerate(nets):
         eng.set_weights(n, w)
 
-    obs, legal, tp = random_positions(ttt.BatchedTicTacToe, G, seed=100 + rank)
-    d_obs = torch.from_numpy(obs).to(dev)
-    d_legal = torch.from_numpy(legal.astype(np.uint8)).to(dev)
-    d_tp = torch.from_numpy(tp.astype(np.int32)).to(dev)
-    d_cv = torch.empty((G, 9), dtype=torch.float32, device=dev)
+    obs, legal, tp = random_positions(env_cls, G, seed=100 + rank, max_plies=6 if game is ttt else 16)
+    # raw pointers cross the ABI: row-major (C-contiguous) device copies
+    d_obs = torch.from_numpy(np.ascontiguousarray(obs, np.float32)).to(dev)
+    d_legal = torch.from_numpy(np.ascontiguousarray(legal, np.uint8)).to(dev)
+    d_tp = torch.from_numpy(np.ascontiguousarray(tp, np.int32)).to(dev)
+    d_cv = torch.empty((G, A), dtype=torch.float32, device=dev)
     d_rv = torch.empty(G, dtype=torch.float32, device=dev)
     d_act = torch.empty(G, dtype=torch.int32, device=dev)
 
@@ -139,28 +158,61 @@ def main():
         t_ms, n_l = eng.debug_kernel_time()
         eng.debug_enable(0)
         kern_ms = t_ms / n_l
-    assert np.all(legal[np.arange(G), d_act.cpu().numpy() - 1]), "illegal action selected"
+    acts = d_act.cpu().numpy()
+    bad = np.flatnonzero(~legal[np.arange(G), acts - 1])
+    assert len(bad) == 0, f"illegal action selected in games {bad[:8]} (actions {acts[bad[:8]]})"
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    # ---- learner leg: ref_semantics learner step at B = batch_size (32),
+    # ---- device self-play pipeline: the whole move loop on the
+    # device — observation/stacked planes, search, env step, GameHistory and
+    # replay-shard append — G games per rank, timed like the search leg
+    env_kind = ENV_CONNECT4 if game is c4 else ENV_TICTACTOE
+    eng.selfplay_init(env_kind, G, max(G, conf.replay_buffer_size))
+    mv = 1 << 20                                          # move counter (RNG step keys)
+    pipe = None
+    if args.pipeline_moves > 0:
+        for _ in range(3):
+            eng.selfplay_move(mv, game_offset=rank * G, stream=sp)
+            mv += 1
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tp0 = time.perf_counter()
+        for _ in range(args.pipeline_moves):
+            eng.selfplay_move(mv, game_offset=rank * G, stream=sp)
+            mv += 1
+        torch.cuda.synchronize()
+        tpl = torch.tensor([time.perf_counter() - tp0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tpl, op=dist.ReduceOp.MAX)
+        tpl = float(tpl.item())
+        pipe = {"moves_per_s": round(world * G * args.pipeline_moves / tpl, 1),
+                "node_expansions_per_s": round(world * G * S * args.pipeline_moves / tpl, 1),
+                "ms_per_move": round(tpl / args.pipeline_moves * 1e3, 4), "moves": args.pipeline_moves}
+    torch.cuda.synchronize()                              # (replay_counts syncs only libmz's own stream)
+    while eng.replay_counts()[1] == 0:                    # the learner needs finished games
+        eng.selfplay_move(mv, game_offset=rank * G, stream=sp)
+        mv += 1
+        torch.cuda.synchronize()
+    if pipe is not None:
+        pipe["replay"] = dict(zip(("num_played_games", "num_played_steps", "total_samples"),
+                                  (int(x) for x in eng.replay_counts()[0])))
+
+    # ---- learner leg: ref_semantics learner step at B = batch_size (32) on
+    # batches sampled on the device from this rank's replay shard (§8f-2),
     # gradient bucket all-reduced over RCCL when world > 1
-    B, K, A = conf.batch_size, conf.num_unroll_steps, 9
-    rng = np.random.default_rng(7 + rank)
-    tpol = rng.random((B, K + 1, A)).astype(np.float32)
-    tpol /= tpol.sum(-1, keepdims=True)
-    bt = [torch.from_numpy(x).to(dev) for x in (
-        (rng.random((B, 63)) < 0.4).astype(np.float32), rng.integers(1, 10, (B, K + 1)).astype(np.float32),
-        rng.uniform(-1, 1, (B, K + 1)).astype(np.float32), np.zeros((B, K + 1), np.float32), tpol,
-        rng.integers(1, K + 1, B).astype(np.float32))]
+    B, K = conf.batch_size, conf.num_unroll_steps
     grad = torch.empty(eng.grad_count(), dtype=torch.float32, device=dev)
     losses = torch.empty(8, dtype=torch.float32, device=dev)
 
     def lstep(k):
-        eng.learner_grad_dev([x.data_ptr() for x in bt], B, grad.data_ptr(), losses.data_ptr(), stream=sp)
+        b, _ = eng.replay_sample(B, k + 1, stream=sp)
+        eng.learner_grad_dev([b.observation, b.actions, b.target_values, b.target_rewards, b.target_policies,
+                              b.gradient_scale], B, grad.data_ptr(), losses.data_ptr(), stream=sp)
         if world > 1:
             dist.all_reduce(grad)
         eng.learner_apply_dev(grad.data_ptr(), 1.0 / world, cos_schedule(k + 1), stream=sp)
@@ -205,14 +257,15 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "node-expansions/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: random-play TicTacToe positions, random glorot weights",
-            "config": {"workload": (f"TicTacToe ResNet (2 blocks x 64 filters, 3x3), {G} games/GPU x {S} sims/move "
-                                    f"(configs[2])") if resnet else
-                                   f"TicTacToe FC (params.jl hyper), {G} games/GPU x {S} sims/move (configs[1])",
+            "data": f"synthetic: random-play {game.__name__.split('.')[-1]} positions, random glorot weights; "
+                    "learner batches sampled on the device from the self-play replay shard",
+            "config": {"workload": workload(game, resnet, G, S),
                        "games_per_gpu": G, "sims_per_move": S, "global_games": G * world,
                        "parallelism": f"games sharded x{world}, learner dp{world} (RCCL all-reduce)"},
             "learner_steps_per_s": round(learner_sps, 1),
-            "learner_config": {"batch_size": B, "num_unroll_steps": K, "mode": "ref_semantics"},
+            "learner_config": {"batch_size": B, "num_unroll_steps": K, "mode": "ref_semantics",
+                               "batch_source": "mz_replay_sample (device get_batch + make_target)"},
+            "selfplay_pipeline": pipe,
             "roofline": {"bound": "mfma", "achieved": round(achieved, 4), "peak": PEAK_F32, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_F32, 5), "traffic": traffic,
                          "kernel": variant, "kernel_ms": round(kern_ms, 4),

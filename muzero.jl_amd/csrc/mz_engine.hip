@@ -175,6 +175,7 @@ struct mz_handle {
           *d_rs_gs = nullptr;
     int32_t* d_rs_index = nullptr;
     int rs_cap = 0;
+    bool sp_has_games = false;              // the FIFO never empties once a game is in
     std::vector<void*> sp_allocs;
     std::vector<void*> allocs;
 };
@@ -1558,6 +1559,7 @@ int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games) {
     for (void* p : h->sp_allocs) (void)hipFree(p);
     h->sp_allocs.clear();
     h->rs_cap = 0;
+    h->sp_has_games = false;
     h->sp_env = env_kind; h->sp_G = G; h->sp_cap = replay_games;
     h->sp_T = c.max_moves + 1; h->sp_osz = W * H * C;
     MZ_TRY(h, spalloc(h, &h->d_sp_board, (size_t)G * h->sp_osz));
@@ -1653,11 +1655,12 @@ int mz_replay_sample(mz_handle* h, int32_t B, uint32_t step, mz_batch* batch, in
     if (B < 1) return fail(h, "batch_size must be >= 1");
     MZ_TRY(h, hipSetDevice(h->device));
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    {
-        long long played = 0;                     // sample_n_games needs a non-empty buffer
+    if (!h->sp_has_games) {                       // sample_n_games needs a non-empty buffer
+        long long played = 0;
         MZ_TRY(h, hipStreamSynchronize(st));
         MZ_TRY(h, hipMemcpy(&played, h->d_sp_counters, sizeof(played), hipMemcpyDeviceToHost));
         if (played == 0) return fail(h, "replay buffer is empty");
+        h->sp_has_games = true;
     }
     const int K1 = h->conf.num_unroll_steps + 1, A = h->A;
     if (B > h->rs_cap) {

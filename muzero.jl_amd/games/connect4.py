@@ -89,7 +89,7 @@ class BatchedConnect4:
 
     def legal_mask(self):
         top = self.board[:, 2 * CELLS + (W - 1) + W * np.arange(H)]       # top cell of each column empty
-        return top & ~self.over[:, None]
+        return np.ascontiguousarray(top & ~self.over[:, None])          # (G, A) row-major for the ABI
 
     def step(self, actions):
         """actions 1-based (G,); returns (reward for the mover, done)."""

@@ -130,13 +130,16 @@ class BatchedSelfPlay:
 
 
 def random_positions(env_cls, G, seed=0, max_plies=6):
-    """Real TicTacToe positions for benchmarking: random legal play from the
-    initial board for 0..max_plies plies; returns stacked observations
-    (G, F), legal masks (G, A) and to_play (G,).  Positions that ended are
-    replaced by the initial board."""
+    """Real positions for benchmarking (any env with [p1, p2, empty] board
+    planes, stacked_observations = 1): random legal play from the initial
+    board for 0..max_plies plies; returns stacked observations (G, F), legal
+    masks (G, A) and to_play (G,).  Positions that ended are replaced by the
+    initial board."""
     rng = np.random.default_rng(seed)
     env = env_cls(G)
-    prev_obs = np.zeros((G, 27), np.float32)
+    osz = env.board.shape[1]
+    plane = osz // 3
+    prev_obs = np.zeros((G, osz), np.float32)
     prev_act = np.zeros(G, np.int32)
     plies = rng.integers(0, max_plies + 1, G)
     alive = np.ones(G, bool)
@@ -145,12 +148,14 @@ def random_positions(env_cls, G, seed=0, max_plies=6):
         go = (plies > t) & alive & legal.any(1)
         if not go.any():
             break
-        choice = np.array([rng.choice(np.flatnonzero(legal[g])) + 1 if go[g] else 1 for g in range(G)], np.int32)
+        # games not playing this ply take their first legal move and are restored below
+        choice = np.array([rng.choice(np.flatnonzero(legal[g])) + 1 if go[g] else int(np.argmax(legal[g])) + 1
+                           for g in range(G)], np.int32)
         before = env.board.astype(np.float32)
-        board_save, player_save = env.board.copy(), env.player.copy()
+        saved = {k: v.copy() for k, v in vars(env).items() if isinstance(v, np.ndarray)}
         _, done = env.step(choice)
-        env.board[~go] = board_save[~go]
-        env.player[~go] = player_save[~go]
+        for k, v in saved.items():                       # games not playing this ply keep their state
+            getattr(env, k)[~go] = v[~go]
         prev_obs[go] = before[go]
         prev_act[go] = choice[go]
         ended = go & done
@@ -160,6 +165,6 @@ def random_positions(env_cls, G, seed=0, max_plies=6):
             prev_act[ended] = 0
             alive &= ~ended
     cur = env.board.astype(np.float32)
-    plane = np.repeat(prev_act[:, None].astype(np.float32), 9, axis=1)
-    obs = np.concatenate([cur, plane, prev_obs], axis=1)
+    planes = np.repeat(prev_act[:, None].astype(np.float32), plane, axis=1)
+    obs = np.concatenate([cur, planes, prev_obs], axis=1)
     return obs, env.legal_mask(), env.player.copy()

@@ -106,3 +106,62 @@ def test_resnet_learner_steps(ttt, B, K):
         for n in range(3):
             assert np.array_equal(eng.get_weights(n), o.params[n]), f"step {t} net {n} params differ"
     eng.close()
+
+
+@pytest.fixture(scope="module")
+def rn_c4():
+    """Connect4 ResNet-8 (configs[3]): a 6x7 board, tiles of 4 games."""
+    from muzero_jl_amd import abi
+    from muzero_jl_amd.games import connect4
+    conf, hyper = connect4.conf, connect4.resnet_hyper
+    o, nets = _resnet_oracle(conf, hyper, seed=21)
+    nets = _perturb_bn(conf, hyper, nets, seed=22)
+    eng = abi.Engine(conf, hyper, device=0, max_games=32, rng_seed=3)
+    for n, w in enumerate(nets):
+        o.set_weights(n, w)
+        eng.set_weights(n, w)
+    yield conf, hyper, o, eng
+    eng.close()
+
+
+@pytest.mark.parametrize("net", [0, 1, 2])
+def test_resnet_connect4_forward_bitexact(rn_c4, net):
+    conf, hyper, o, eng = rn_c4
+    rng = np.random.default_rng(net)
+    n = 9
+    if net == 0:
+        x = (rng.random((n, 294)) < 0.4).astype(np.float32)
+    elif net == 1:
+        x = rng.normal(0, 1, (n, o.H)).astype(np.float32)
+    else:
+        x = np.concatenate([rng.normal(0, 1, (n, o.H)), np.full((n, 42), 3 / 7)], 1).astype(np.float32)
+    want, got = o.forward(net, x), eng.forward(net, x)
+    if net == 0:
+        assert np.array_equal(got, want)
+    else:
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+
+
+def test_resnet_connect4_search_bitexact():
+    import dataclasses
+    from muzero_jl_amd import abi
+    from muzero_jl_amd.games import connect4
+    from muzero_jl_amd.selfplay import random_positions
+    from test_gpu_parity import _compare_trees
+    conf = dataclasses.replace(connect4.conf, num_iters=6)
+    hyper = connect4.resnet_hyper
+    o, nets = _resnet_oracle(conf, hyper, seed=23)
+    G = 9
+    eng = abi.Engine(conf, hyper, device=0, max_games=G, rng_seed=o.seed)
+    for n, w in enumerate(nets):
+        eng.set_weights(n, w)
+    obs, legal, tp = random_positions(connect4.BatchedConnect4, G, seed=5, max_plies=12)
+    eng.debug_enable(1)
+    cv, rv, act = eng.mcts_search(obs, legal, tp, exploration=True, rng_step=3, game_offset=0, temperature=1.0)
+    tree_g = eng.debug_tree(G)
+    cv2, rv2, act2, tree_o, _ = o.mcts_search(obs, legal, tp, exploration=True, rng_step=3, game_offset=0,
+                                              temperature=1.0, dump=True)
+    assert np.all(legal[np.arange(G), act - 1])
+    _compare_trees(tree_g, tree_o, G)
+    assert np.array_equal(cv, cv2) and np.array_equal(rv, rv2) and np.array_equal(act, act2)
+    eng.close()

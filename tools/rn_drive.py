@@ -39,7 +39,7 @@ def main():
         eng.set_weights(n, w)
     obs, legal, tp = random_positions(ttt.BatchedTicTacToe, G, seed=100)
     dev = torch.device("cuda", 0)
-    d = [torch.from_numpy(x).to(dev) for x in (obs, legal.astype(np.uint8), tp.astype(np.int32))]
+    d = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (obs, legal.astype(np.uint8), tp.astype(np.int32))]
     cv = torch.empty((G, 9), dtype=torch.float32, device=dev)
     rv = torch.empty(G, dtype=torch.float32, device=dev)
     act = torch.empty(G, dtype=torch.int32, device=dev)
