@@ -269,6 +269,16 @@ int mz_replay_get_game(mz_handle* h, int32_t i, int32_t* T, uint8_t* obs, int32_
                        float* rewards, int32_t* to_play, float* child_visits, float* root_values);
 int mz_selfplay_slots(mz_handle* h, int32_t* history_len, uint8_t* board, int32_t* player);
 
+/* ---- Checkpoints -------------------------------------------
+ * Replace serialize(joinpath(networks_path, "$(step)_<net>.bin"), net)
+ * (Learning.jl:424-431) and play.jl's deserialize: one safetensors file with
+ * the three nets' Flux.params arrays ("<net>.<i>", Julia column-major bytes,
+ * shape = the Julia shape reversed), the ADAM moments and βp state, and
+ * metadata (training_step, network kind, config).  Load checks every shape
+ * against this engine and restores weights + optimiser state (resume).      */
+int mz_checkpoint_save(mz_handle* h, const char* path, int64_t training_step);
+int mz_checkpoint_load(mz_handle* h, const char* path, int64_t* training_step);
+
 /* Name of the search kernel variant the last search launched (for profiles):
  * mz_search_small{1,2,4} (T games per workgroup, G <= 4 x #CUs) or the
  * 16-game MFMA tile kernel mz_search_kernel_{lds,hbm}[_res].  Environment

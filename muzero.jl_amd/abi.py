@@ -64,6 +64,8 @@ SIGNATURES = {
     "mz_replay_sample": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.POINTER(MzBatch), _VP, _VP]),
     "mz_replay_get_game": (ctypes.c_int, [_VP, ctypes.c_int32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "mz_selfplay_slots": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
+    "mz_checkpoint_save": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int64]),
+    "mz_checkpoint_load": (ctypes.c_int, [_VP, ctypes.c_char_p, _VP]),
     "mz_search_variant": (ctypes.c_char_p, [_VP]),
     "mz_sync": (ctypes.c_int, [_VP]),
 }
@@ -332,6 +334,16 @@ class Engine:
         pl = np.zeros(G, np.int32)
         self._check(self.lib.mz_selfplay_slots(self.h, _p(ln), _p(board), _p(pl)), "mz_selfplay_slots")
         return ln, board, pl
+
+    # ---- checkpoints
+    def checkpoint_save(self, path, training_step):
+        self._check(self.lib.mz_checkpoint_save(self.h, os.fsencode(path), int(training_step)), "mz_checkpoint_save")
+
+    def checkpoint_load(self, path):
+        """Restores weights + ADAM state; returns the checkpoint's training step."""
+        step = ctypes.c_int64()
+        self._check(self.lib.mz_checkpoint_load(self.h, os.fsencode(path), ctypes.byref(step)), "mz_checkpoint_load")
+        return step.value
 
     def search_variant(self):
         return self.lib.mz_search_variant(self.h).decode()

@@ -26,6 +26,7 @@ extern "C" __global__ void mz_search_kernel_lds_res(SearchParams P);
 #include "mz_small_params.h"
 #include "mz_resnet_params.h"
 #include "mz_selfplay_params.h"
+#include "mz_ckpt_iface.h"
 extern "C" __global__ void mz_rnet_forward_kernel(RNetParams Q);
 extern "C" __global__ void mz_rsearch_root(RSearchParams P);
 extern "C" __global__ void mz_rsearch_tree(RSearchParams P);
@@ -1501,6 +1502,102 @@ const char* mz_search_variant(const mz_handle* h) {
 
 // ------------------------------------------------ device self-play + replay
 }  // extern "C"
+
+// ------------------------------------------------ checkpoint interface (mz_ckpt_iface.h)
+static const char* kNetNames[3] = {"representation", "prediction", "dynamics"};
+
+std::vector<MzParamDesc> mz_param_table(const mz_handle* h) {
+    std::vector<MzParamDesc> t;
+    for (int net = 0; net < 3; ++net) {
+        int i = 0;
+        auto add = [&](std::vector<int64_t> shp, size_t off) {
+            size_t cnt = 1;
+            for (int64_t d : shp) cnt *= (size_t)d;
+            t.push_back(MzParamDesc{std::string(kNetNames[net]) + "." + std::to_string(i++), shp, off, cnt});
+        };
+        if (h->kind == 0) {                                   // Dense: W (out, in), b (out)
+            for (const LayerSpec& L : h->layers) {
+                if (L.net != net) continue;
+                add({L.out, L.in}, L.flux_w);
+                add({L.out}, L.flux_b);
+            }
+        } else {                                              // Conv: W (kw,kh,cin,cout), b, BatchNorm β, γ
+            size_t np = 0;
+            for (const RSpec& r : rn_specs(h->conf, h->rhp, net, &np)) {
+                const size_t base = h->flat_off[net];
+                if (r.conv) {
+                    add({r.kw, r.kh, r.cin, r.cout}, base + r.woff);
+                    add({r.cout}, base + r.boff);
+                    add({r.cout}, base + r.bnoff);
+                    add({r.cout}, base + r.bnoff + r.cout);
+                } else {
+                    add({r.cout, r.cin}, base + r.woff);
+                    add({r.cout}, base + r.boff);
+                }
+            }
+        }
+    }
+    return t;
+}
+
+size_t mz_flat_count(const mz_handle* h) { return h->nflat; }
+
+int mz_state_get(mz_handle* h, float* flat, float* m, float* v, double* beta_pow) {
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    if (flat) MZ_TRY(h, hipMemcpy(flat, h->d_flat, h->nflat * 4, hipMemcpyDeviceToHost));
+    if (m) MZ_TRY(h, hipMemcpy(m, h->d_m, h->nflat * 4, hipMemcpyDeviceToHost));
+    if (v) MZ_TRY(h, hipMemcpy(v, h->d_v, h->nflat * 4, hipMemcpyDeviceToHost));
+    if (beta_pow) { beta_pow[0] = h->bp1; beta_pow[1] = h->bp2; }
+    return 0;
+}
+
+int mz_state_set(mz_handle* h, const float* flat, const float* m, const float* v, const double* beta_pow) {
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, hipMemcpy(h->d_flat, flat, h->nflat * 4, hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(h->d_m, m, h->nflat * 4, hipMemcpyHostToDevice));
+    MZ_TRY(h, hipMemcpy(h->d_v, v, h->nflat * 4, hipMemcpyHostToDevice));
+    h->bp1 = beta_pow[0]; h->bp2 = beta_pow[1];
+    if (repack(h)) return -1;
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+std::string mz_net_kind(const mz_handle* h) { return h->kind == 0 ? "fc" : "resnet"; }
+
+std::string mz_describe(const mz_handle* h) {
+    const mz_config& c = h->conf;
+    std::string s = "{\"observation_shape\":[" + std::to_string(c.observation_shape[0]) + "," +
+                    std::to_string(c.observation_shape[1]) + "," + std::to_string(c.observation_shape[2]) + "]" +
+                    ",\"action_space_size\":" + std::to_string(c.action_space_size) +
+                    ",\"stacked_observations\":" + std::to_string(c.stacked_observations) +
+                    ",\"num_unroll_steps\":" + std::to_string(c.num_unroll_steps);
+    if (h->kind == 0) {
+        const mz_ffhp& p = h->hp;
+        s += ",\"width_hidden\":" + std::to_string(p.width_hidden) +
+             ",\"depth_representation\":" + std::to_string(p.depth_representation) +
+             ",\"depth_prediction\":" + std::to_string(p.depth_prediction) +
+             ",\"depth_dynamics\":" + std::to_string(p.depth_dynamics) +
+             ",\"depth_policy\":" + std::to_string(p.depth_policy) + ",\"depth_value\":" + std::to_string(p.depth_value) +
+             ",\"depth_reward\":" + std::to_string(p.depth_reward) +
+             ",\"depth_state_head\":" + std::to_string(p.depth_state_head) +
+             ",\"hidden_state_size\":" + std::to_string(p.hidden_state_size) +
+             ",\"reward_activation\":" + std::to_string(p.reward_activation);
+    } else {
+        const mz_resnet_hp& p = h->rhp;
+        s += ",\"num_blocks\":" + std::to_string(p.num_blocks) + ",\"num_filters\":" + std::to_string(p.num_filters) +
+             ",\"conv_kernel_size\":[" + std::to_string(p.conv_kernel_size[0]) + "," +
+             std::to_string(p.conv_kernel_size[1]) + "]" +
+             ",\"num_first_head_filters\":" + std::to_string(p.num_first_head_filters) +
+             ",\"num_second_head_filters\":" + std::to_string(p.num_second_head_filters) +
+             ",\"depth_value\":" + std::to_string(p.depth_value) + ",\"width_hidden\":" + std::to_string(p.width_hidden) +
+             ",\"reward_activation\":" + std::to_string(p.reward_activation);
+    }
+    return s + "}";
+}
+
+int mz_set_error(mz_handle* h, const std::string& msg) { return fail(h, msg); }
 
 template <typename T>
 static hipError_t spalloc(mz_handle* h, T** p, size_t n, bool zero = true) {
