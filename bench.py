@@ -35,6 +35,7 @@ import _mzpkg  # noqa: E402
 _mzpkg.load()
 from muzero_jl_amd.abi import ENV_CONNECT4, ENV_TICTACTOE, Engine  # noqa: E402
 from muzero_jl_amd.config import cos_schedule, to_c_config, to_c_ffhp, to_c_resnet_hp  # noqa: E402
+from muzero_jl_amd.games import atari_synth as atari  # noqa: E402
 from muzero_jl_amd.games import connect4 as c4  # noqa: E402
 from muzero_jl_amd.games import tictactoe as ttt  # noqa: E402
 from muzero_jl_amd.networks import init_nets, net_macs  # noqa: E402
@@ -44,10 +45,10 @@ METRIC = "self-play MCTS node-expansions/sec + train steps/sec, TicTacToe FC net
 PEAK_F32 = 157.3                     # TFLOP/s, MI355X_MICROARCH.md (f32 MFMA = f32 vector peak)
 
 
-def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0, resnet=False):
+def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0, resnet=False, batch=32):
     """The oracle (C restatement of the reference semantics, 1 thread) on a
-    bounded sample of the same workload: 32-game batches of the same
-    positions, 50 sims/move, until `budget_s` of CPU time has been spent."""
+    bounded sample of the same workload: `batch`-game batches of the same
+    positions, the same sims/move, until `budget_s` of CPU time has been spent."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import Oracle
     o = Oracle(to_c_config(conf), to_c_resnet_hp(hyper) if resnet else to_c_ffhp(hyper), seed=1)
@@ -55,17 +56,20 @@ def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0, resnet=False)
         o.set_weights(n, w)
     n_games, t0, step = 0, time.perf_counter(), 0
     while time.perf_counter() - t0 < budget_s:
-        i = (step * 32) % (obs.shape[0] - 32 + 1)
-        o.mcts_search(obs[i:i + 32], legal[i:i + 32], tp[i:i + 32], exploration=True, rng_step=step)
-        n_games += 32
+        i = (step * batch) % (obs.shape[0] - batch + 1)
+        o.mcts_search(obs[i:i + batch], legal[i:i + batch], tp[i:i + batch], exploration=True, rng_step=step)
+        n_games += batch
         step += 1
     dt = time.perf_counter() - t0
     return dict(value=n_games * conf.num_iters / dt, unit="node-expansions/s", cores=1, kind="port",
-                sample=f"{n_games} games x {conf.num_iters} sims (32-game batches of the bench positions), "
+                sample=f"{n_games} games x {conf.num_iters} sims ({batch}-game batches of the bench positions), "
                        f"oracle/mz_oracle.c single thread, {dt:.1f} s")
 
 
 def workload(game, resnet, G, S):
+    if game is atari:
+        return (f"synthetic Atari-like 84x84x4 observations, ResNet with the Learning.jl:175-187 downsampler "
+                f"(84->6, then 2 blocks x 64 filters), 18 actions, {G} games/GPU x {S} sims/move (configs[4])")
     if game is c4:
         return (f"Connect4 6x7 {'ResNet-8 (4 blocks x 64 filters, 3x3)' if resnet else 'FC'}, {G} games/GPU x "
                 f"{S} sims/move" + (" (configs[3]: 4096 games = 512/GPU x 8)" if resnet else ""))
@@ -79,13 +83,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--game", choices=["tictactoe", "connect4"], default="tictactoe")
+    ap.add_argument("--game", choices=["tictactoe", "connect4", "atari"], default="tictactoe")
     ap.add_argument("--net", choices=["fc", "resnet"], default="fc")
     ap.add_argument("--games", type=int, default=None,
-                    help="games per GPU (tictactoe: fc 512, resnet 2048; connect4: 512)")
+                    help="games per GPU (tictactoe: fc 512, resnet 2048; connect4, atari: 512)")
     ap.add_argument("--pipeline-moves", type=int, default=20,
                     help="timed moves of the device self-play loop (0 = skip that leg)")
-    ap.add_argument("--sims", type=int, default=50)
+    ap.add_argument("--sims", type=int, default=None, help="sims per move (default 50; atari 200)")
     ap.add_argument("--learner-steps", type=int, default=50)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -102,20 +106,25 @@ def main():
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
 
-    resnet = args.net == "resnet"
-    game = c4 if args.game == "connect4" else ttt
-    env_cls = c4.BatchedConnect4 if game is c4 else ttt.BatchedTicTacToe
-    conf = dataclasses.replace(game.conf, num_iters=args.sims)
+    game = {"connect4": c4, "atari": atari}.get(args.game, ttt)
+    resnet = args.net == "resnet" or game is atari          # configs[4] is the downsampling ResNet
+    S = args.sims or (200 if game is atari else 50)
+    conf = dataclasses.replace(game.conf, num_iters=S)
     hyper = game.resnet_hyper if resnet else game.hyper
     A = len(conf.action_space)
     G = args.games or (2048 if resnet and game is ttt else 512)
-    S = args.sims
     nets = init_nets(conf, hyper, seed=1234)              # identical replicas on every rank
     eng = Engine(conf, hyper, device=local, max_games=G, rng_seed=1)
     for n, w in enumerate(nets):
         eng.set_weights(n, w)
 
-    obs, legal, tp = random_positions(env_cls, G, seed=100 + rank, max_plies=6 if game is ttt else 16)
+    if game is atari:                                     # synthetic observations, every action legal, 1 player
+        obs = atari.observations(G, seed=rank)
+        legal = np.ones((G, A), bool)
+        tp = np.ones(G, np.int32)
+    else:
+        env_cls = c4.BatchedConnect4 if game is c4 else ttt.BatchedTicTacToe
+        obs, legal, tp = random_positions(env_cls, G, seed=100 + rank, max_plies=6 if game is ttt else 16)
     # raw pointers cross the ABI: row-major (C-contiguous) device copies
     d_obs = torch.from_numpy(np.ascontiguousarray(obs, np.float32)).to(dev)
     d_legal = torch.from_numpy(np.ascontiguousarray(legal, np.uint8)).to(dev)
@@ -170,11 +179,12 @@ def main():
     # ---- device self-play pipeline: the whole move loop on the
     # device — observation/stacked planes, search, env step, GameHistory and
     # replay-shard append — G games per rank, timed like the search leg
-    env_kind = ENV_CONNECT4 if game is c4 else ENV_TICTACTOE
-    eng.selfplay_init(env_kind, G, max(G, conf.replay_buffer_size))
-    mv = 1 << 20                                          # move counter (RNG step keys)
     pipe = None
-    if args.pipeline_moves > 0:
+    if game is not atari:                                 # (no Atari env: the search leg is configs[4]'s step)
+        env_kind = ENV_CONNECT4 if game is c4 else ENV_TICTACTOE
+        eng.selfplay_init(env_kind, G, max(G, conf.replay_buffer_size))
+    mv = 1 << 20                                          # move counter (RNG step keys)
+    if args.pipeline_moves > 0 and game is not atari:
         for _ in range(3):
             eng.selfplay_move(mv, game_offset=rank * G, stream=sp)
             mv += 1
@@ -194,7 +204,7 @@ def main():
                 "node_expansions_per_s": round(world * G * S * args.pipeline_moves / tpl, 1),
                 "ms_per_move": round(tpl / args.pipeline_moves * 1e3, 4), "moves": args.pipeline_moves}
     torch.cuda.synchronize()                              # (replay_counts syncs only libmz's own stream)
-    while eng.replay_counts()[1] == 0:                    # the learner needs finished games
+    while game is not atari and eng.replay_counts()[1] == 0:   # the learner needs finished games
         eng.selfplay_move(mv, game_offset=rank * G, stream=sp)
         mv += 1
         torch.cuda.synchronize()
@@ -209,10 +219,22 @@ def main():
     grad = torch.empty(eng.grad_count(), dtype=torch.float32, device=dev)
     losses = torch.empty(8, dtype=torch.float32, device=dev)
 
+    if game is atari:                                     # a synthetic batch resident in HBM
+        rng = np.random.default_rng(7 + rank)
+        tpol = rng.random((B, K + 1, A)).astype(np.float32)
+        sb = [atari.observations(B, seed=1000 + rank), rng.integers(1, A + 1, (B, K + 1)).astype(np.float32),
+              rng.uniform(-1, 1, (B, K + 1)).astype(np.float32), np.zeros((B, K + 1), np.float32),
+              tpol / tpol.sum(-1, keepdims=True), rng.integers(1, K + 1, B).astype(np.float32)]
+        sb = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in sb]
+
     def lstep(k):
-        b, _ = eng.replay_sample(B, k + 1, stream=sp)
-        eng.learner_grad_dev([b.observation, b.actions, b.target_values, b.target_rewards, b.target_policies,
-                              b.gradient_scale], B, grad.data_ptr(), losses.data_ptr(), stream=sp)
+        if game is atari:
+            ptrs = [x.data_ptr() for x in sb]
+        else:
+            b, _ = eng.replay_sample(B, k + 1, stream=sp)
+            ptrs = [b.observation, b.actions, b.target_values, b.target_rewards, b.target_policies,
+                    b.gradient_scale]
+        eng.learner_grad_dev(ptrs, B, grad.data_ptr(), losses.data_ptr(), stream=sp)
         if world > 1:
             dist.all_reduce(grad)
         eng.learner_apply_dev(grad.data_ptr(), 1.0 / world, cos_schedule(k + 1), stream=sp)
@@ -252,19 +274,23 @@ def main():
                 traffic = rec.get("hbm_bytes_per_launch")
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(conf, hyper, nets, obs, legal, tp, args.cpu_budget, resnet)
+            cpu = cpu_baseline(conf, hyper, nets, obs, legal, tp, args.cpu_budget, resnet,
+                               batch=1 if game is atari else 32)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "node-expansions/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": f"synthetic: random-play {game.__name__.split('.')[-1]} positions, random glorot weights; "
-                    "learner batches sampled on the device from the self-play replay shard",
+            "data": ("synthetic: 84x84x4 U[0,1) Philox observations, random glorot weights; synthetic learner "
+                     "batch resident in HBM" if game is atari else
+                     f"synthetic: random-play {game.__name__.split('.')[-1]} positions, random glorot weights; "
+                     "learner batches sampled on the device from the self-play replay shard"),
             "config": {"workload": workload(game, resnet, G, S),
                        "games_per_gpu": G, "sims_per_move": S, "global_games": G * world,
                        "parallelism": f"games sharded x{world}, learner dp{world} (RCCL all-reduce)"},
             "learner_steps_per_s": round(learner_sps, 1),
             "learner_config": {"batch_size": B, "num_unroll_steps": K, "mode": "ref_semantics",
-                               "batch_source": "mz_replay_sample (device get_batch + make_target)"},
+                               "batch_source": "synthetic device batch" if game is atari else
+                               "mz_replay_sample (device get_batch + make_target)"},
             "selfplay_pipeline": pipe,
             "roofline": {"bound": "mfma", "achieved": round(achieved, 4), "peak": PEAK_F32, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_F32, 5), "traffic": traffic,

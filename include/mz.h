@@ -95,7 +95,13 @@ typedef struct mz_resnet_hp {
     int32_t num_second_head_filters; /* 2: policy head 1x1 conv channels */
     int32_t num_first_head_filters;  /* 1: value / reward head 1x1 conv channels */
     float batch_norm_momentum;       /* 0.6 (unused in test mode) */
-    int32_t downsample;              /* false (the Atari downsampler is not built) */
+    int32_t downsample;              /* false; true = the Atari downsampler of Learning.jl:175-187
+                                        (BASELINE configs[4]): Conv(k, C=>C, stride 2), 2 blocks,
+                                        Conv(k, C=>2C, stride 2), 3 blocks, MeanPool((3,3), stride 2,
+                                        pad 1), 3 blocks, MeanPool, then the representation's
+                                        Conv(k, 2C=>nf) + blocks: 84x84 -> 6x6.  The hidden board
+                                        (representation_output_size) is then 6x6, and the
+                                        downsampler's params lead the representation's Flux.params */
     int32_t depth_policy;            /* hidden Dense layers (the reference reuses depth_value, kept) */
     int32_t depth_value;             /* hidden Dense layers of the value / reward / policy heads */
     int32_t width_hidden;            /* 64: Dense width of the heads */
@@ -113,7 +119,9 @@ typedef struct mz_handle mz_handle;
 int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device,
                      int max_games, uint64_t rng_seed, mz_handle** out);
 /* Same engine with the ResNet networks (ResNetHP, configs 3-5).  Hidden
- * state = (W, H, num_filters); the dynamics input is (W, H, num_filters+1). */
+ * state = (W, H, num_filters) on the observation board (W, H), or on the
+ * downsampled board with ResNetHP.downsample; the dynamics input is
+ * (W, H, num_filters+1).  action_space_size <= 32 (the FC engine: <= 16). */
 int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, int device,
                             int max_games, uint64_t rng_seed, mz_handle** out);
 void mz_engine_destroy(mz_handle* h);

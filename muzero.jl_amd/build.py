@@ -5,7 +5,7 @@ import subprocess
 from . import PKG_DIR, LIB_PATH
 
 SOURCES = ["mz_engine.hip", "mz_search.hip", "mz_small.hip", "mz_nets.hip", "mz_resnet.hip", "mz_selfplay.hip",
-           "mz_checkpoint.cpp"]
+           "mz_downsample.hip", "mz_checkpoint.cpp"]
 HEADERS = ["mz_internal.h", "mz_mlp_device.h", "mz_tree_device.h", "mz_small_params.h", "mz_resnet_params.h",
            "mz_selfplay_params.h", "mz_ckpt_iface.h"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",

@@ -36,11 +36,14 @@ def param_table(conf, hyper, net):
 
     if isinstance(hyper, ResNetHP):
         for op in resnet_specs(conf, hyper, net):
+            if op["kind"] == "pool":                      # MeanPool: no params
+                continue
             if op["kind"] == "conv":
                 add((op["kw"], op["kh"], op["cin"], op["cout"]))
                 add((op["cout"],))
-                add((op["cout"],))                        # BatchNorm β
-                add((op["cout"],))                        # BatchNorm γ
+                if op["bn"]:
+                    add((op["cout"],))                    # BatchNorm β
+                    add((op["cout"],))                    # BatchNorm γ
             else:
                 add((op["cout"], op["cin"]))
                 add((op["cout"],))

@@ -170,15 +170,13 @@ def to_c_ffhp(h: FeedForwardHP) -> MzFFHP:
 
 
 def to_c_resnet_hp(h: ResNetHP) -> MzResNetHP:
-    if h.downsample:
-        raise ValueError("ResNetHP.downsample: the Atari downsampler is not built")
     m = MzResNetHP()
     for f in ("num_blocks", "num_filters", "num_second_head_filters", "num_first_head_filters",
               "depth_policy", "depth_value", "width_hidden"):
         setattr(m, f, getattr(h, f))
     m.conv_kernel_size[0], m.conv_kernel_size[1] = h.conv_kernel_size
     m.batch_norm_momentum = h.batch_norm_momentum
-    m.downsample = 0
+    m.downsample = int(bool(h.downsample))
     act = h.reward_activation
     if callable(act):
         act = act.__name__
@@ -187,9 +185,12 @@ def to_c_resnet_hp(h: ResNetHP) -> MzResNetHP:
 
 
 def hidden_size(conf: Config, hyper) -> int:
-    """Hidden-state floats: FeedForwardHP.hidden_state_size, or W*H*num_filters."""
+    """Hidden-state floats: FeedForwardHP.hidden_state_size, or W*H*num_filters
+    on the hidden board (after the downsampler when ResNetHP.downsample)."""
     if isinstance(hyper, ResNetHP):
-        return conf.observation_shape[0] * conf.observation_shape[1] * hyper.num_filters
+        from .networks import resnet_board
+        W, H = resnet_board(conf, hyper)
+        return W * H * hyper.num_filters
     return hyper.hidden_state_size
 
 

@@ -30,6 +30,9 @@ extern "C" __global__ void mz_search_kernel_lds_res(SearchParams P);
 extern "C" __global__ void mz_rnet_forward_kernel(RNetParams Q);
 extern "C" __global__ void mz_rsearch_root(RSearchParams P);
 extern "C" __global__ void mz_rsearch_tree(RSearchParams P);
+extern "C" __global__ void mz_rsearch_root32(RSearchParams P);
+extern "C" __global__ void mz_downsample_kernel(DsParams Q);
+extern "C" __global__ void mz_rsearch_tree32(RSearchParams P);
 extern "C" __global__ void mz_rsearch_nets(RSearchParams P);
 extern "C" __global__ void mz_runroll_kernel(RUnrollParams U);
 extern "C" __global__ void mz_sp_prepare(SpParams S);
@@ -54,6 +57,10 @@ extern "C" __global__ void mz_learner_grad_kernel(int B, int K, int A, int v_act
                                                   float* pr, const float* tv, const float* tp, const float* gscale,
                                                   float* terms, const float* flat, const size_t* netoff, float* G,
                                                   double* part, unsigned* counter, float* out);
+extern "C" __global__ void mz_learner_grad_kernel32(int B, int K, int A, int v_act, int r_act, float* pv, float* pp,
+                                                    float* pr, const float* tv, const float* tp, const float* gscale,
+                                                    float* terms, const float* flat, const size_t* netoff, float* G,
+                                                    double* part, unsigned* counter, float* out);
 extern "C" __global__ void mz_adam_kernel(float* P, float* M, float* V, const float* G, float gscale, size_t n,
                                           double bp1, double bp2, double eta, float* Wp, float* Bp,
                                           const int* inv_tile, float* smw, float* smb, const int* inv_small);
@@ -100,6 +107,17 @@ struct mz_handle {
     mz_ffhp hp;
     int kind = 0;                           // 0 FeedForwardHP, 1 ResNetHP
     mz_resnet_hp rhp{};
+    // ResNet config of the networks after the downsampler (= conf without
+    // one): observation_shape = the representation tail's input board and
+    // channels, stacked_observations = 0 (ResNetHP.downsample, configs[4])
+    mz_config rconf{};
+    int ds = 0;                             // downsampler (mz_downsample.hip) on
+    DsPlan dsplan{};
+    DsPlan* d_dsplan = nullptr;
+    size_t ds_lds = 0, ds_n = 0;            // its LDS bytes, its parameter count (first in the repr net)
+    int rin_feat = 0;                       // representation tail input features (obs_feat without downsampler)
+    float* d_dsout = nullptr;               // [max_games][rin_feat] search roots' downsampled observations
+    float* d_dsb = nullptr; int dsb_cap = 0;   // [cap][rin_feat] scratch: learner batches, net_forward
     // ResNet networks (mz_resnet.hip): host plans, device copies, tile width
     std::vector<RPlan> rplan;               // [3]
     RPlan* d_rplan = nullptr;               // [3]
@@ -691,10 +709,10 @@ static std::vector<RSpec> rn_specs(const mz_config& c, const mz_resnet_hp& hp, i
 // reads B0 through the small buffers S0..S2; outputs O0 / O1.
 static RPlan rn_plan(const mz_handle* h, const std::vector<RSpec>& sp, int net, int NG, size_t flat_off,
                      int& w_img, std::vector<int>* srcw) {
-    const mz_config& c = h->conf;
+    const mz_config& c = h->rconf;
     const int W = c.observation_shape[0], Hh = c.observation_shape[1], P = W * Hh;
     const int nf = h->rhp.num_filters, hs = h->rhp.width_hidden;
-    const int in_feat = net == MZ_NET_REPR ? h->obs_feat : net == MZ_NET_PRED ? h->H : h->H + h->plane;
+    const int in_feat = net == MZ_NET_REPR ? h->rin_feat : net == MZ_NET_PRED ? h->H : h->H + h->plane;
     const int big = nf * P * NG;
     int off = 0;
     auto region = [&](int n) { int o = off; off += (n + 3) / 4 * 4; return o; };
@@ -807,7 +825,94 @@ static int alloc_learner(mz_handle* h) {
 }
 
 static size_t rsearch_root_lds(const mz_handle* h) {
-    return (size_t)std::max(h->rplan[0].lds_floats, h->rplan[1].lds_floats) * 4 + 512 * 4;
+    const int gw = h->A > 16 ? 32 : 16;     // softmax / noise staging [16][gw] x 2
+    return (size_t)std::max(h->rplan[0].lds_floats, h->rplan[1].lds_floats) * 4 + (size_t)2 * 16 * gw * 4;
+}
+
+// The downsampler of Learning.jl:175-187 (op for op as oracle/mz_oracle.c
+// onet_build_resnet with downsample, `size` read as conv_kernel_size):
+// Conv(k, C => C, stride 2), 2 blocks, Conv(k, C => 2C, stride 2), 3 blocks,
+// MeanPool((3,3), stride 2, pad 1), 3 blocks, MeanPool — then the tail
+// Conv(k, 2C => nf) + BatchNorm + blocks is the RPlan of rconf.  Parameters
+// (Flux.params order, first in the representation's flat vector): strided
+// conv W, b; block conv W, b, β, γ.  Returns the parameter count.
+static size_t ds_build(mz_handle* h, DsPlan& D) {
+    const mz_config& c = h->conf;
+    const int kw = h->rhp.conv_kernel_size[0], kh = h->rhp.conv_kernel_size[1];
+    int C = c.observation_shape[2] * (c.stacked_observations + 1) + c.stacked_observations;
+    int w = c.observation_shape[0], hh = c.observation_shape[1];
+    std::memset(&D, 0, sizeof(D));
+    D.in_feat = w * hh * C;
+    size_t n = 0;
+    int cur = -1;
+    auto s2 = [](int x, int k) { return (x + 2 * (k / 2) - k) / 2 + 1; };
+    auto conv = [&](int cin, int cout, int stride, int bn, int act) -> DsLayer& {
+        DsLayer& L = D.L[D.n++];
+        L.kind = DS_CONV; L.cin = cin; L.cout = cout; L.kw = kw; L.kh = kh; L.pw = kw / 2; L.ph = kh / 2;
+        L.stride = stride; L.Wi = w; L.Hi = hh;
+        L.Wo = stride == 2 ? s2(w, kw) : w; L.Ho = stride == 2 ? s2(hh, kh) : hh;
+        L.act = act; L.bn = bn;
+        L.woff = (int)n; n += (size_t)kw * kh * cin * cout;
+        L.boff = (int)n; n += (size_t)cout;
+        if (bn) { L.bnoff = (int)n; n += (size_t)2 * cout; }
+        D.w_floats = std::max(D.w_floats, kw * kh * cin * cout);
+        w = L.Wo; hh = L.Ho;
+        return L;
+    };
+    auto strided = [&](int cin, int cout) {
+        DsLayer& L = conv(cin, cout, 2, 0, MZ_ACT_IDENTITY);
+        L.in_buf = cur; L.out_buf = cur == 0 ? 1 : 0; cur = L.out_buf;
+    };
+    auto block = [&](int f) {
+        DsLayer& a = conv(f, f, 1, 1, MZ_ACT_RELU);
+        a.in_buf = cur; a.out_buf = 1 - cur;
+        DsLayer& b = conv(f, f, 1, 1, MZ_ACT_RELU);
+        b.in_buf = 1 - cur; b.out_buf = cur; b.res_add = 1; b.res_buf = cur;
+    };
+    auto pool = [&](int f) {
+        DsLayer& L = D.L[D.n++];
+        L.kind = DS_POOL; L.cin = f; L.cout = f; L.kw = 3; L.kh = 3; L.pw = 1; L.ph = 1; L.stride = 2;
+        L.Wi = w; L.Hi = hh; L.Wo = s2(w, 3); L.Ho = s2(hh, 3); L.act = MZ_ACT_IDENTITY;
+        L.in_buf = cur; L.out_buf = 1 - cur; cur = L.out_buf;
+        w = L.Wo; hh = L.Ho;
+    };
+    strided(C, C);
+    for (int i = 0; i < 2; ++i) block(C);
+    strided(C, 2 * C);
+    for (int i = 0; i < 3; ++i) block(2 * C);
+    pool(2 * C);
+    for (int i = 0; i < 3; ++i) block(2 * C);
+    pool(2 * C);
+    D.L[D.n - 1].out_buf = -1;                       // the last layer writes the output to HBM
+    D.out_feat = w * hh * 2 * C;
+    for (int i = 0; i < D.n; ++i) {
+        const DsLayer& L = D.L[i];
+        if (i > 0) D.buf_floats = std::max(D.buf_floats, L.cin * L.Wi * L.Hi);
+        D.buf_floats = std::max(D.buf_floats, L.cout * L.Wo * L.Ho);
+    }
+    D.buf_floats = (D.buf_floats + 3) & ~3;
+    D.w_floats = (D.w_floats + 3) & ~3;
+    h->rconf = c;
+    h->rconf.observation_shape[0] = w; h->rconf.observation_shape[1] = hh; h->rconf.observation_shape[2] = 2 * C;
+    h->rconf.stacked_observations = 0;
+    h->ds_lds = ((size_t)2 * D.buf_floats + D.w_floats + 512) * 4;
+    return n;
+}
+
+// run the downsampler over n items: x (in_feat, n) -> y (rin_feat, n)
+static int ds_launch(mz_handle* h, const float* x, float* y, int n, hipStream_t st) {
+    DsParams Q;
+    Q.n_items = n; Q.bn_s = h->bn_s; Q.plan = h->d_dsplan; Q.flat = h->d_flat; Q.x = x; Q.y = y;
+    void* args[] = {&Q};
+    MZ_TRY(h, hipLaunchKernel((const void*)mz_downsample_kernel, dim3(n), dim3(DS_THREADS), args, h->ds_lds, st));
+    return 0;
+}
+static int ensure_dsb(mz_handle* h, int n) {
+    if (n <= h->dsb_cap) return 0;
+    if (h->d_dsb) { (void)hipFree(h->d_dsb); h->d_dsb = nullptr; }
+    MZ_TRY(h, hipMalloc(&h->d_dsb, (size_t)n * h->rin_feat * 4));
+    h->dsb_cap = n;
+    return 0;
 }
 static size_t rsearch_nets_lds(const mz_handle* h) {
     return (size_t)std::max(h->rplan[1].lds_floats, h->rplan[2].lds_floats) * 4;
@@ -823,11 +928,10 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
     h->seed = rng_seed;
     auto bad = [&](const std::string& m) { g_create_error = m; delete h; return -2; };
     const mz_config& c = *conf;
-    if (c.action_space_size < 1 || c.action_space_size > 16)
-        return bad("action_space_size must be in 1..16 (16-lane select groups)");
+    if (c.action_space_size < 1 || c.action_space_size > 32)
+        return bad("action_space_size must be in 1..32 (16- or 32-lane select groups)");
     if (c.players < 1 || c.players > 2) return bad("players must be 1 or 2");
     if (c.num_iters < 1 || c.num_iters > 65000) return bad("num_iters out of range");
-    if (hyper->downsample) return bad("ResNetHP.downsample: the Atari downsampler is not built");
     if (hyper->conv_kernel_size[0] % 2 == 0 || hyper->conv_kernel_size[1] % 2 == 0 ||
         hyper->conv_kernel_size[0] > 15 || hyper->conv_kernel_size[1] > 15)
         return bad("conv_kernel_size must be odd and <= 15 (Learning.jl:164 asserts odd)");
@@ -836,13 +940,26 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
     if (hipSetDevice(device) != hipSuccess) return bad("hipSetDevice failed (no GPU?)");
     const int W = c.observation_shape[0], Hh = c.observation_shape[1], C = c.observation_shape[2];
     h->obs_feat = W * Hh * (C * (c.stacked_observations + 1) + c.stacked_observations);
-    h->plane = W * Hh;
-    h->H = W * Hh * hyper->num_filters; h->A = c.action_space_size; h->S = c.num_iters;
+    h->rconf = c;
+    h->A = c.action_space_size; h->S = c.num_iters;
+    if (hyper->downsample) {
+        h->ds = 1;
+        h->ds_n = ds_build(h, h->dsplan);
+        if (h->dsplan.L[0].kw * h->dsplan.L[0].kh * 2 * h->dsplan.L[0].cin > 256)
+            return bad("downsampler: conv_kernel_size x 2C input channels exceeds 256 taps");
+        if (h->ds_lds > kLdsMax) return bad("downsampler activations exceed the LDS");
+    }
+    const int rW = h->rconf.observation_shape[0], rH = h->rconf.observation_shape[1];
+    h->rin_feat = h->ds ? h->dsplan.out_feat : h->obs_feat;
+    h->plane = rW * rH;
+    h->H = rW * rH * hyper->num_filters;
     std::vector<RSpec> sp[3];
     size_t off = 0;
     for (int n = 0; n < 3; ++n) {
-        sp[n] = rn_specs(c, *hyper, n, &h->nparams[n]);
-        h->flat_off[n] = off; off += h->nparams[n];
+        sp[n] = rn_specs(h->rconf, *hyper, n, &h->nparams[n]);
+        h->flat_off[n] = off;
+        if (n == MZ_NET_REPR) h->nparams[n] += h->ds_n;     // downsampler params first
+        off += h->nparams[n];
     }
     h->nflat = off;
     // widest tile whose three plans fit the LDS
@@ -850,7 +967,8 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
         int wi = 0;
         bool fits = true;
         for (int n = 0; n < 3; ++n)
-            fits &= (size_t)rn_plan(h, sp[n], n, ng, h->flat_off[n], wi, nullptr).lds_floats * 4 <= kLdsMax;
+            fits &= (size_t)rn_plan(h, sp[n], n, ng, h->flat_off[n] + (n == 0 ? h->ds_n : 0), wi,
+                                    nullptr).lds_floats * 4 <= kLdsMax;
         if (fits) h->rn_ng = ng;
     }
     if (!h->rn_ng) return bad("ResNet activations exceed the LDS even for one game per tile");
@@ -862,7 +980,7 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
     int wi = 0;
     h->rplan.resize(3);
     for (int n = 0; n < 3; ++n) {
-        h->rplan[n] = rn_plan(h, sp[n], n, h->rn_ng, h->flat_off[n], wi, &sw);
+        h->rplan[n] = rn_plan(h, sp[n], n, h->rn_ng, h->flat_off[n] + (n == 0 ? h->ds_n : 0), wi, &sw);
         h->rn_lds[n] = (size_t)h->rplan[n].lds_floats * 4;
     }
     h->packed_w_n = sw.size(); h->packed_b_n = 0;
@@ -895,6 +1013,16 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
     CK(rsearch_root_lds(h) > kLdsMax ? fail(h, "ResNet root tile exceeds the LDS") : 0);
     CK(hipFuncSetAttribute((const void*)mz_rsearch_root, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)rsearch_root_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(root)"));
+    CK(hipFuncSetAttribute((const void*)mz_rsearch_root32, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)rsearch_root_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(root32)"));
+    if (h->ds) {
+        CK(hipFuncSetAttribute((const void*)mz_downsample_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)h->ds_lds) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(downsample)"));
+        CK(al(&h->d_dsplan, 1));
+        CK(hipMemcpy(h->d_dsplan, &h->dsplan, sizeof(DsPlan), hipMemcpyHostToDevice) == hipSuccess
+               ? 0 : fail(h, "copy"));
+        CK(al(&h->d_dsout, (size_t)max_games * h->rin_feat));
+    }
     CK(hipFuncSetAttribute((const void*)mz_runroll_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)lmax) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll)"));
     CK(hipFuncSetAttribute((const void*)mz_rsearch_nets, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -923,6 +1051,7 @@ void mz_engine_destroy(mz_handle* h) {
     for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
     for (void* p : h->allocs) (void)hipFree(p);
     for (void* p : h->sp_allocs) (void)hipFree(p);
+    if (h->d_dsb) (void)hipFree(h->d_dsb);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -1072,15 +1201,24 @@ int mz_weights_get(mz_handle* h, int net, float* flat, size_t n) {
 
 static int rnet_forward(mz_handle* h, int net, const float* x, int n, float* out0, float* out1) {
     const RPlan& R = h->rplan[net];
+    const bool ds = h->ds && net == MZ_NET_REPR;
+    const int xin = ds ? h->obs_feat : R.in_feat;     // the raw observation goes through the downsampler
     float *dx = nullptr, *d0 = nullptr, *d1 = nullptr;
-    MZ_TRY(h, hipMalloc(&dx, (size_t)n * R.in_feat * 4));
+    MZ_TRY(h, hipMalloc(&dx, (size_t)n * xin * 4));
     MZ_TRY(h, hipMalloc(&d0, (size_t)n * R.out0_n * 4));
     MZ_TRY(h, hipMalloc(&d1, (size_t)n * std::max(R.out1_n, 1) * 4));
-    (void)hipMemcpyAsync(dx, x, (size_t)n * R.in_feat * 4, hipMemcpyHostToDevice, h->stream);
+    (void)hipMemcpyAsync(dx, x, (size_t)n * xin * 4, hipMemcpyHostToDevice, h->stream);
+    if (ds) {
+        if (ensure_dsb(h, n) || ds_launch(h, dx, h->d_dsb, n, h->stream)) {
+            (void)hipFree(dx); (void)hipFree(d0); (void)hipFree(d1);
+            return -1;
+        }
+    }
     RNetParams Q;
-    Q.ng = h->rn_ng; Q.W = h->conf.observation_shape[0]; Q.H = h->conf.observation_shape[1];
+    Q.ng = h->rn_ng; Q.W = h->rconf.observation_shape[0]; Q.H = h->rconf.observation_shape[1];
     Q.P = Q.W * Q.H; Q.n_items = n; Q.softmax1 = net == MZ_NET_PRED; Q.bn_s = h->bn_s;
-    Q.plan = h->d_rplan + net; Q.Wimg = h->d_Wp; Q.flat = h->d_flat; Q.x = dx; Q.out0 = d0; Q.out1 = d1;
+    Q.plan = h->d_rplan + net; Q.Wimg = h->d_Wp; Q.flat = h->d_flat; Q.x = ds ? h->d_dsb : dx; Q.out0 = d0;
+    Q.out1 = d1;
     void* args[] = {&Q};
     hipError_t le = hipLaunchKernel((const void*)mz_rnet_forward_kernel, dim3((n + Q.ng - 1) / Q.ng), dim3(RN_THREADS),
                                     args, h->rn_lds[net], h->stream);
@@ -1133,8 +1271,8 @@ static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
                    float* root_value, int32_t* action_out, hipStream_t st) {
     RSearchParams P;
     std::memset(&P, 0, sizeof(P));
-    P.G = G; P.S = h->S; P.A = h->A; P.H = h->H; P.W = h->conf.observation_shape[0];
-    P.P = h->plane; P.players = h->conf.players; P.obs_feat = h->obs_feat; P.exploration = exploration;
+    P.G = G; P.S = h->S; P.A = h->A; P.H = h->H; P.W = h->rconf.observation_shape[0];
+    P.P = h->plane; P.players = h->conf.players; P.obs_feat = h->rin_feat; P.exploration = exploration;
     P.rng_step = rng_step; P.game_offset = game_offset; P.seed = h->seed; P.temperature = temperature;
     P.discount = h->conf.discount; P.dirichlet_alpha = h->conf.dirichlet_alpha;
     P.exploration_eps = h->conf.exploration_eps;
@@ -1149,12 +1287,19 @@ static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * std::max(h->max_games, 128)));
     P.stamps = h->d_stamps;
 #endif
+    if (h->ds) {                                    // representation: downsampler, then the tail in the root
+        if (ds_launch(h, obs, h->d_dsout, G, st)) return -1;
+        P.obs = h->d_dsout;
+    }
     void* args[] = {&P};
-    const unsigned tiles = (unsigned)((G + P.ng - 1) / P.ng), groups = (unsigned)((G + 15) / 16);
-    MZ_TRY(h, hipLaunchKernel((const void*)mz_rsearch_root, dim3(tiles), dim3(RN_THREADS), args, rsearch_root_lds(h), st));
+    const int gw = h->A > 16 ? 32 : 16;             // lanes per game in the tree kernels
+    const unsigned tiles = (unsigned)((G + P.ng - 1) / P.ng), groups = (unsigned)((G + 256 / gw - 1) / (256 / gw));
+    const void* kroot = gw == 32 ? (const void*)mz_rsearch_root32 : (const void*)mz_rsearch_root;
+    const void* ktree = gw == 32 ? (const void*)mz_rsearch_tree32 : (const void*)mz_rsearch_tree;
+    MZ_TRY(h, hipLaunchKernel(kroot, dim3(tiles), dim3(RN_THREADS), args, rsearch_root_lds(h), st));
     for (int s = 0; s <= h->S; ++s) {
         P.s = s;
-        MZ_TRY(h, hipLaunchKernel((const void*)mz_rsearch_tree, dim3(groups), dim3(256), args, 0, st));
+        MZ_TRY(h, hipLaunchKernel(ktree, dim3(groups), dim3(256), args, 0, st));
         if (s == h->S) break;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->time_nets) {
@@ -1348,8 +1493,12 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     RUnrollParams U;
     U.B = B; U.K = h->conf.num_unroll_steps; U.A = h->A; U.H = h->H;
-    U.W = h->conf.observation_shape[0]; U.P = h->plane; U.obs_feat = h->obs_feat; U.ng = h->rn_ng; U.bn_s = h->bn_s;
-    U.obs = b->observation; U.actions = b->actions; U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
+    U.W = h->rconf.observation_shape[0]; U.P = h->plane; U.obs_feat = h->rin_feat; U.ng = h->rn_ng; U.bn_s = h->bn_s;
+    U.obs = b->observation; U.actions = b->actions;
+    if (h->ds) {                                    // representation (:347): downsampler, then the tail
+        if (ensure_dsb(h, B) || ds_launch(h, b->observation, h->d_dsb, B, st)) return -1;
+        U.obs = h->d_dsb;
+    } U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
     U.hs = h->d_rhs; U.plans = h->d_rplan; U.Wimg = h->d_Wp; U.flat = h->d_flat;
     void* args[] = {&U};
     MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_kernel, dim3((B + U.ng - 1) / U.ng), dim3(RN_THREADS), args,
@@ -1407,8 +1556,9 @@ static int learner_losses(mz_handle* h, const mz_batch* b, float* grad_dev, floa
     const int B = b->batch_size, K = h->conf.num_unroll_steps, A = h->A;
     float* lo = losses_dev ? losses_dev : h->d_loss;
     float* g = grad_dev ? grad_dev : h->d_grad;
-    const int nlb = (B * (K + 1) + MZ_THREADS / 16 - 1) / (MZ_THREADS / 16);
-    hipLaunchKernelGGL(mz_learner_grad_kernel, dim3(nlb + 3 * MZ_L2_BLOCKS), dim3(MZ_THREADS), 0, st, B, K, A,
+    const int gw = A > 16 ? 32 : 16;            // lanes per (sample, step) group
+    const int nlb = (B * (K + 1) + MZ_THREADS / gw - 1) / (MZ_THREADS / gw);
+    hipLaunchKernelGGL(gw == 32 ? mz_learner_grad_kernel32 : mz_learner_grad_kernel, dim3(nlb + 3 * MZ_L2_BLOCKS), dim3(MZ_THREADS), 0, st, B, K, A,
                        v_act, r_act, h->d_pv, h->d_pp, h->d_pr, b->target_values, b->target_policies,
                        b->gradient_scale, h->d_lterm, h->d_flat, h->d_netoff, g, h->d_sq, h->d_counter, lo);
     MZ_TRY(h, hipGetLastError());
@@ -1523,8 +1673,16 @@ std::vector<MzParamDesc> mz_param_table(const mz_handle* h) {
             }
         } else {                                              // Conv: W (kw,kh,cin,cout), b, BatchNorm β, γ
             size_t np = 0;
-            for (const RSpec& r : rn_specs(h->conf, h->rhp, net, &np)) {
-                const size_t base = h->flat_off[net];
+            if (net == MZ_NET_REPR && h->ds)                  // the downsampler's convs first (MeanPool: none)
+                for (int i = 0; i < h->dsplan.n; ++i) {
+                    const DsLayer& L = h->dsplan.L[i];
+                    if (L.kind != DS_CONV) continue;
+                    add({L.kw, L.kh, L.cin, L.cout}, h->flat_off[net] + L.woff);
+                    add({L.cout}, h->flat_off[net] + L.boff);
+                    if (L.bn) { add({L.cout}, h->flat_off[net] + L.bnoff); add({L.cout}, h->flat_off[net] + L.bnoff + L.cout); }
+                }
+            for (const RSpec& r : rn_specs(h->rconf, h->rhp, net, &np)) {
+                const size_t base = h->flat_off[net] + (net == MZ_NET_REPR ? h->ds_n : 0);
                 if (r.conv) {
                     add({r.kw, r.kh, r.cin, r.cout}, base + r.woff);
                     add({r.cout}, base + r.boff);
@@ -1592,6 +1750,7 @@ std::string mz_describe(const mz_handle* h) {
              ",\"num_first_head_filters\":" + std::to_string(p.num_first_head_filters) +
              ",\"num_second_head_filters\":" + std::to_string(p.num_second_head_filters) +
              ",\"depth_value\":" + std::to_string(p.depth_value) + ",\"width_hidden\":" + std::to_string(p.width_hidden) +
+             ",\"downsample\":" + std::to_string(p.downsample) +
              ",\"reward_activation\":" + std::to_string(p.reward_activation);
     }
     return s + "}";

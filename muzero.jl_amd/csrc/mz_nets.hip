@@ -111,7 +111,8 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_unroll_kernel(Unroll
 // out: [0] value, [1] reward (0, intermediate_rewards = false), [2] policy,
 // [3..5] Σθ² of repr / pred / dyn.
 #define MZ_L2_BLOCKS 32
-extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_grad_kernel(
+template <int GW>
+__device__ __forceinline__ void learner_grad_body(
     int B, int K, int A, int v_act, int r_act, float* pv, float* pp, float* pr, const float* tv, const float* tp,
     const float* gscale, float* terms, const float* flat, const size_t* netoff, float* G, double* part,
     unsigned* counter, float* out) {
@@ -120,27 +121,27 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_grad_kernel(
     __shared__ bool last;
     const int tid = threadIdx.x;
     const int n = B * (K + 1);
-    const int nlb = (n + MZ_THREADS / 16 - 1) / (MZ_THREADS / 16);
+    const int nlb = (n + MZ_THREADS / GW - 1) / (MZ_THREADS / GW);
     float* vsq = terms;
     float* cet = terms + n;
     if ((int)blockIdx.x < nlb) {
-        const int t = blockIdx.x * (MZ_THREADS / 16) + (tid >> 4), a = tid & 15;
-        float* st = stg + (tid & ~15);
-        if (t < n) {                            // whole 16-lane groups are in or out
+        const int t = blockIdx.x * (MZ_THREADS / GW) + tid / GW, a = tid % GW;
+        float* st = stg + (tid & ~(GW - 1));
+        if (t < n) {                            // whole GW-lane groups are in or out
             const bool in = a < A;
             float* yh = pp + (size_t)t * A;
             const float x = in ? yh[a] : -INFINITY;
-            const float m = g16_max(x);
+            const float m = gmax<GW>(x);
             const float e = in ? det_expf(x - m) : 0.0f;
-            const float s = g16_seqsum(e, A, st, a);
+            const float s = gseqsum<GW>(e, A, st, a);
             const float p = in ? e / s : -INFINITY;
             if (in) yh[a] = p;
-            const float m2 = g16_max(p);
+            const float m2 = gmax<GW>(p);
             const float e2 = in ? det_expf(p - m2) : 0.0f;
-            const float se = g16_seqsum(e2, A, st, a);
+            const float se = gseqsum<GW>(e2, A, st, a);
             const float ls = det_logf(se);
             const float term = in ? tp[(size_t)t * A + a] * ((p - m2) - ls) : 0.0f;
-            const float ce = g16_seqsum(term, A, st, a);
+            const float ce = gseqsum<GW>(term, A, st, a);
             if (a == 0) {
                 const float v = mz_post_act(v_act, pv[t]);
                 pv[t] = v;
@@ -206,6 +207,16 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_grad_kernel(
             s += __hip_atomic_load(part + tid * MZ_L2_BLOCKS + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         out[3 + tid] = (float)s;
     }
+}
+#define MZ_LG_ARGS int B, int K, int A, int v_act, int r_act, float* pv, float* pp, float* pr, const float* tv, \
+    const float* tp, const float* gscale, float* terms, const float* flat, const size_t* netoff, float* G, \
+    double* part, unsigned* counter, float* out
+#define MZ_LG_CALL B, K, A, v_act, r_act, pv, pp, pr, tv, tp, gscale, terms, flat, netoff, G, part, counter, out
+extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_grad_kernel(MZ_LG_ARGS) {
+    learner_grad_body<16>(MZ_LG_CALL);
+}
+extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_grad_kernel32(MZ_LG_ARGS) {
+    learner_grad_body<32>(MZ_LG_CALL);
 }
 
 // Flux 0.12 apply!(ADAM) + WeightDecay(0) + `x .-= Δ` (Learning.jl:395-397).

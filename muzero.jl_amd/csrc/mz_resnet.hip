@@ -338,15 +338,16 @@ __device__ __forceinline__ TreeView rs_tree(const RSearchParams& P, int gg) {
 
 // Root (SelfPlay.jl:230-251): representation + prediction of NG games per
 // tile, h0 -> hidden slot 0, root expansion with the double softmax (Q3),
-// exploration noise, per-game state.
-extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_rsearch_root(RSearchParams P) {
+// exploration noise, per-game state.  GW lanes per game (A <= GW).
+template <int GW>
+__device__ __forceinline__ void rsearch_root_body(const RSearchParams& P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const RPlan& Rr = P.plans[MZ_NET_REPR];
     const RPlan& Rp = P.plans[MZ_NET_PRED];
     const int NG = P.ng, t0 = blockIdx.x * NG, H = P.H, A = P.A;
     const int nplan = Rr.lds_floats > Rp.lds_floats ? Rr.lds_floats : Rp.lds_floats;
-    float* stg = lds + nplan;                       // [16][16] softmax / noise staging
-    float* noise = stg + 256;                       // [16][16]
+    float* stg = lds + nplan;                       // [16][GW] softmax / noise staging
+    float* noise = stg + 16 * GW;                   // [16][GW]
     rn_fill_ktabs(Rr, lds, NG, P.W, P.P);
     const RnLane t = rn_lane(NG);
     const bool ok = t0 + t.g < P.G;
@@ -362,19 +363,19 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_rsearch_root(RSearch
     rn_stage(lds + Rp.in_off, NG, H, t, [&](int f) { return ok ? h0[f] : 0.0f; });   // prediction input = h0
     __syncthreads();
     rn_run(Rp, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s);                    // :239
-    const int gl = threadIdx.x >> 4, a = threadIdx.x & 15, gg = t0 + gl;
+    const int gl = threadIdx.x / GW, a = threadIdx.x % GW, gg = t0 + gl;
     const bool active = gl < NG && gg < P.G;
     if (active) {
         uint32_t legal = 0;
         for (int b = 0; b < A; ++b) if (P.legal[(size_t)gg * A + b]) legal |= 1u << b;
         const uint32_t gid = P.game_offset + (uint32_t)gg;
         TreeView tree = rs_tree(P, gg);
-        const float prior = double_softmax_prior(a < A ? lds[Rp.out1_off + a * NG + gl] : 0.0f, a, A, legal,
-                                                 stg + 16 * gl);
+        const float prior = double_softmax_prior<GW>(a < A ? lds[Rp.out1_off + a * NG + gl] : 0.0f, a, A, legal,
+                                                     stg + GW * gl);
         init_edges(tree, 0, a, A, prior);                                       // :245
         if (P.exploration) {                                                    // :247-249
-            const float nz = root_noise_lane(legal, a, A, P.seed, gid, P.rng_step, P.dirichlet_alpha,
-                                             noise + 16 * gl);
+            const float nz = root_noise_lane<GW>(legal, a, A, P.seed, gid, P.rng_step, P.dirichlet_alpha,
+                                                 noise + GW * gl);
             if (a < A && ((legal >> a) & 1u))
                 tree.p(a) = tree.p(a) * (1.0f - P.exploration_eps) + nz * P.exploration_eps;
         }
@@ -388,15 +389,18 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_rsearch_root(RSearch
         }
     }
 }
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_rsearch_root(RSearchParams P) { rsearch_root_body<16>(P); }
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_rsearch_root32(RSearchParams P) { rsearch_root_body<32>(P); }
 
 // Tree step s: expand + backup of simulation s-1 (s > 0), then select +
 // gather for simulation s (s < S), or the search statistics and the action
-// (s == S).  16 lanes per game, 16 games per workgroup.
-extern "C" __global__ __launch_bounds__(256) void mz_rsearch_tree(RSearchParams P) {
+// (s == S).  GW lanes per game, 256 / GW games per workgroup.
+template <int GW>
+__device__ __forceinline__ void rsearch_tree_body(const RSearchParams& P) {
     __shared__ float stg[256];
-    const int gl = threadIdx.x >> 4, a = threadIdx.x & 15, lane = threadIdx.x & 63;
-    const int gg = blockIdx.x * 16 + gl;
-    if (gg >= P.G) return;                          // whole 16-lane groups leave together
+    const int gl = threadIdx.x / GW, a = threadIdx.x % GW, lane = threadIdx.x & 63;
+    const int gg = blockIdx.x * (256 / GW) + gl;
+    if (gg >= P.G) return;                          // whole GW-lane groups leave together
     const int A = P.A, H = P.H, S = P.S, PS = 2 * (S + 2);
     int* st = P.gst + (size_t)gg * RG_INTS;
     int* path = P.path + (size_t)gg * PS;
@@ -405,8 +409,8 @@ extern "C" __global__ __launch_bounds__(256) void mz_rsearch_tree(RSearchParams 
     const uint32_t gid = P.game_offset + (uint32_t)gg;
     if (P.s > 0) {
         const int e_new = P.s;                      // the node simulation s-1 expanded (:280)
-        const float prior = double_softmax_prior(a < A ? P.o_logit[(size_t)gg * A + a] : 0.0f, a, A, legal,
-                                                 stg + 16 * gl);
+        const float prior = double_softmax_prior<GW>(a < A ? P.o_logit[(size_t)gg * A + a] : 0.0f, a, A, legal,
+                                                     stg + GW * gl);
         init_edges(tree, e_new, a, A, prior);
         const int tl = st[RG_VTP], depth = st[RG_DEPTH];
         if (a == 0) {
@@ -421,8 +425,8 @@ extern "C" __global__ __launch_bounds__(256) void mz_rsearch_tree(RSearchParams 
         int rN = st[RG_ROOTN];
         float rW = __int_as_float(st[RG_ROOTW]);
         float mmin = __int_as_float(st[RG_MMIN]), mmax = __int_as_float(st[RG_MMAX]);
-        backup_path(tree, path, depth, P.o_v[gg], tl, A, P.players, P.discount, rN, rW, st[RG_ROOT_TP], mmin,
-                    mmax, a);                                                   // :281
+        backup_path<GW>(tree, path, depth, P.o_v[gg], tl, A, P.players, P.discount, rN, rW, st[RG_ROOT_TP], mmin,
+                        mmax, a);                                               // :281
         __builtin_amdgcn_wave_barrier();
         if (a == 0) {
             st[RG_ROOTN] = rN; st[RG_ROOTW] = __float_as_int(rW);
@@ -432,7 +436,7 @@ extern "C" __global__ __launch_bounds__(256) void mz_rsearch_tree(RSearchParams 
         __builtin_amdgcn_wave_barrier();
     }
     if (P.s < S) {
-        const SelectOut so = select_path<false>(tree, path, st[RG_ROOTN], st[RG_ROOT_TP], legal,
+        const SelectOut so = select_path<false, GW>(tree, path, st[RG_ROOTN], st[RG_ROOT_TP], legal,
                                                 __int_as_float(st[RG_MMIN]), __int_as_float(st[RG_MMAX]), a, lane,
                                                 A, P.players, P.discount, nullptr, P.pbc_tab, P.sqrt_tab, P.seed,
                                                 gid, P.rng_step, P.s);                    // :256-268
@@ -442,7 +446,7 @@ extern "C" __global__ __launch_bounds__(256) void mz_rsearch_tree(RSearchParams 
         // parent h -> prediction input; h *= 2 in place (Q1), read by the dynamics launch
         float* hp = P.hid + ((size_t)gg * (S + 1) + so.leaf_e) * H;
         float* xp = P.x_pred + (size_t)gg * H;
-        for (int k = a; k < H; k += 16) {
+        for (int k = a; k < H; k += GW) {
             const float hv = hp[k];
             xp[k] = hv;
             hp[k] = hv * 2.0f;
@@ -450,11 +454,11 @@ extern "C" __global__ __launch_bounds__(256) void mz_rsearch_tree(RSearchParams 
     } else {                                        // store_search_stats! (:115-122) + select_action (:293-306)
         const bool lg = a < A && ((legal >> a) & 1u);
         const int Nc = lg ? (int)(tree.nc(a) & 0xffffu) : 0;
-        const int sum = g16_isum(Nc);
+        const int sum = gisum<GW>(Nc);
         if (a < A) P.child_visits[(size_t)gg * A + a] = lg ? (float)((double)Nc / (double)sum) : 0.0f;
-        int cnt[16];
+        int cnt[GW];
 #pragma unroll
-        for (int b = 0; b < 16; ++b) cnt[b] = __shfl(Nc, b, 16);
+        for (int b = 0; b < GW; ++b) cnt[b] = __shfl(Nc, b, GW);
         if (a == 0) {
             const int rN = st[RG_ROOTN];
             P.root_value[gg] = rN == 0 ? 0.0f : __int_as_float(st[RG_ROOTW]) / (float)rN;
@@ -463,6 +467,8 @@ extern "C" __global__ __launch_bounds__(256) void mz_rsearch_tree(RSearchParams 
         }
     }
 }
+extern "C" __global__ __launch_bounds__(256) void mz_rsearch_tree(RSearchParams P) { rsearch_tree_body<16>(P); }
+extern "C" __global__ __launch_bounds__(256) void mz_rsearch_tree32(RSearchParams P) { rsearch_tree_body<32>(P); }
 
 // Networks of simulation s: blockIdx.y = 0 prediction(parent h), 1 dynamics
 // (2h ⊕ a/|A|, Q1) writing h' into hidden slot s+1.

@@ -93,3 +93,37 @@ struct RUnrollParams {
     const RPlan* plans;
     const float* Wimg; const float* flat;
 };
+
+// Downsampler of the ResNet representation (ResNetHP.downsample,
+// Learning.jl:175-187; BASELINE configs[4]): stride-2 convs without
+// BatchNorm, residual blocks and MeanPool((3,3), stride 2, pad 1) taking the
+// (84, 84, C) observation to (6, 6, 2C), which the representation's tail
+// (conv 2C -> nf + blocks, an RPlan) reads.  One workgroup per item; the
+// activations ping-pong between two LDS buffers [c][h][w] (the column-major
+// (W, H, C) order), the first layer reads the observation from HBM.
+#define DS_MAX_LAYERS 32
+#define DS_THREADS 512
+enum { DS_CONV = 0, DS_POOL = 1 };
+struct DsLayer {
+    int kind, cin, cout, kw, kh, pw, ph, stride;
+    int Wi, Hi, Wo, Ho;
+    int act, bn, res_add;
+    int woff, boff, bnoff;   // absolute offsets in the flat parameters (conv)
+    int in_buf, out_buf;     // LDS buffer 0 / 1, or -1 = the observation (in) / the output (out)
+    int res_buf;             // residual buffer (res_add)
+};
+struct DsPlan {
+    int n;
+    DsLayer L[DS_MAX_LAYERS];
+    int buf_floats;          // floats per activation buffer
+    int w_floats;            // largest conv weight block (K x cout)
+    int in_feat, out_feat;   // W*H*C of the observation / of the output
+};
+struct DsParams {
+    int n_items;
+    float bn_s;
+    const DsPlan* plan;
+    const float* flat;
+    const float* x;          // (in_feat, n_items) column-major
+    float* y;                // (out_feat, n_items)
+};

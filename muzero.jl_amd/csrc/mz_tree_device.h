@@ -14,7 +14,9 @@
 //   nr[e]  f32  reward of expanded node e (node.reward)
 //   ntp[e] i8   to_play of expanded node e
 // The same code runs on an LDS or an HBM copy.
-// Threads are grouped 16 lanes per game (lane a = child slot a, A <= 16).
+// Threads are grouped GW lanes per game (lane a = child slot a, A <= GW):
+// GW = 16 (one DPP row; every FC kernel and A <= 16) or 32 (two rows, A <= 32,
+// e.g. the 18 Atari actions of BASELINE configs[4]).
 #pragma once
 #include "mz_internal.h"
 
@@ -83,58 +85,85 @@ __device__ __forceinline__ int g16_isum(int v) {
     return v;
 }
 
-// sequential (ascending) f32 sum of lanes 0..n-1 of the 16-lane group; every
+// GW-lane group versions: the 16-lane DPP reduction, then for GW = 32 one
+// exchange with the other row of the pair (ds_swizzle-free __shfl_xor).
+template <int GW> __device__ __forceinline__ float gmax(float v) {
+    v = g16_max(v);
+    if constexpr (GW == 32) { const float t = __shfl_xor(v, 16, 32); v = v > t ? v : t; }
+    return v;
+}
+template <int GW> __device__ __forceinline__ float gmin(float v) {
+    v = g16_min(v);
+    if constexpr (GW == 32) { const float t = __shfl_xor(v, 16, 32); v = v < t ? v : t; }
+    return v;
+}
+template <int GW> __device__ __forceinline__ uint32_t gor(uint32_t v) {
+    v = g16_or(v);
+    if constexpr (GW == 32) v |= (uint32_t)__shfl_xor((int)v, 16, 32);
+    return v;
+}
+template <int GW> __device__ __forceinline__ int gisum(int v) {
+#pragma unroll
+    for (int o = GW / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, GW);
+    return v;
+}
+
+// sequential (ascending) f32 sum of lanes 0..n-1 of the GW-lane group; every
 // lane returns the same value (the oracle's `s = s + y[i]` loop order).  The
-// values are staged through this group's 16-float LDS slot `st` (same wave:
-// LDS ops complete in order) and read back as four broadcast b128 loads.
-__device__ __forceinline__ float g16_seqsum(float v, int n, float* st, int a) {
+// values are staged through this group's GW-float LDS slot `st` (same wave:
+// LDS ops complete in order) and read back as GW/4 broadcast b128 loads.
+template <int GW>
+__device__ __forceinline__ float gseqsum(float v, int n, float* st, int a) {
     st[a] = v;
     __builtin_amdgcn_wave_barrier();
-    float x[16];
+    float x[GW];
 #pragma unroll
-    for (int b = 0; b < 16; b += 4) {
+    for (int b = 0; b < GW; b += 4) {
         const float4 q = *reinterpret_cast<const float4*>(st + b);
         x[b] = q.x; x[b + 1] = q.y; x[b + 2] = q.z; x[b + 3] = q.w;
     }
     __builtin_amdgcn_wave_barrier();
     float s = 0.0f;
 #pragma unroll
-    for (int b = 0; b < 16; ++b) if (b < n) s = s + x[b];
+    for (int b = 0; b < GW; ++b) if (b < n) s = s + x[b];
     return s;
 }
+__device__ __forceinline__ float g16_seqsum(float v, int n, float* st, int a) { return gseqsum<16>(v, n, st, a); }
 
 __device__ __forceinline__ int nth_set_bit(uint32_t m, int k) {
     for (int i = 0; i < k; ++i) m &= m - 1;
     return __builtin_ctz(m);
 }
 
-// expand_node! (SelfPlay.jl:88-96) priors for the 16-lane group: the policy
+// expand_node! (SelfPlay.jl:88-96) priors for the GW-lane group: the policy
 // head's softmax over all A logits (Learning.jl:114), then the softmax over
 // the legal entries (:89, Q3).  `logit` is this lane's logit (a < A).
+template <int GW = 16>
 __device__ __forceinline__ float double_softmax_prior(float logit, int a, int A, uint32_t legal, float* st) {
     const bool in = a < A;
     const float x = in ? logit : -INFINITY;
-    const float m = g16_max(x);
+    const float m = gmax<GW>(x);
     const float ex = in ? det_expf(x - m) : 0.0f;
-    const float s = g16_seqsum(ex, A, st, a);
+    const float s = gseqsum<GW>(ex, A, st, a);
     const float prob = in ? ex / s : 0.0f;
     const bool lg = in && ((legal >> a) & 1u);
-    const float m2 = g16_max(lg ? prob : -INFINITY);
+    const float m2 = gmax<GW>(lg ? prob : -INFINITY);
     const float e2 = lg ? det_expf(prob - m2) : 0.0f;
-    const float s2 = g16_seqsum(e2, A, st, a);   // illegal lanes add +0: same as the legal-only sum
+    const float s2 = gseqsum<GW>(e2, A, st, a);  // illegal lanes add +0: same as the legal-only sum
     return lg ? e2 / s2 : 0.0f;
 }
 
-// add_exploration_noise! (SelfPlay.jl:102-109) noise for the 16-lane group,
+// add_exploration_noise! (SelfPlay.jl:102-109) noise for the GW-lane group,
 // lane-parallel: legal lane a draws Dirichlet component rank(a) from its own
 // stream (mz_dirichlet_gamma); the f32 sum runs in ascending action order
 // (illegal lanes add +0, exact); returns the normalised noise (0 if illegal).
+template <int GW = 16>
 __device__ __forceinline__ float root_noise_lane(uint32_t legal, int a, int A, uint64_t seed, uint32_t gid,
                                                  uint32_t step, float alpha, float* st) {
     const bool lg = a < A && ((legal >> a) & 1u);
     const int r = __builtin_popcount(legal & ((1u << a) - 1u));
     const float gm = lg ? mz_dirichlet_gamma(seed, gid, step, r, alpha) : 0.0f;
-    const float sum = g16_seqsum(gm, A, st, a);
+    const float sum = gseqsum<GW>(gm, A, st, a);
     const float inv = 1.0f / sum;
     return lg ? gm * inv : 0.0f;
 }
@@ -174,7 +203,7 @@ __device__ __forceinline__ float g16_vmax(float v) {
     return v;
 }
 
-// select_child loop (SelfPlay.jl:256-268) for the game of this 16-lane group.
+// select_child loop (SelfPlay.jl:256-268) for the game of this GW-lane group.
 // pUCT (ucb_score :171-184) in f64 with one rounding to f32 (Q5); ties by
 // exact equality, broken by the Philox TIE stream keyed (sim, depth) — the
 // draw only matters (and is only computed) when there is more than one tie.
@@ -182,9 +211,9 @@ __device__ __forceinline__ float g16_vmax(float v) {
 // entry when TAB, else the pbc/sqrt entries and an f64 division), a
 // branch-free score (illegal lanes score a clamped real edge and are masked
 // to -inf), a DPP max, a ballot, and the chosen edge's record by DPP.  The
-// path stays in registers while depth < 16 (lane d keeps level d) and is
+// path stays in registers while depth < GW (lane d keeps level d) and is
 // written to `path` once at the end; deeper levels are stored directly.
-template <bool TAB>
+template <bool TAB, int GW = 16>
 __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, int root_N, int root_tp,
                                                  uint32_t legal, float mmin, float mmax, int a, int lane,
                                                  int A, int players, float discount, const double* pbterm,
@@ -218,9 +247,10 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
         const float vs = Nc > 0 ? (norm ? vn : ed.w) : 0.0f;
         const float us = (float)(prior_score + (double)vs);
         const float u = lg ? us : -INFINITY;
-        const float m = g16_vmax(u);
+        float m = g16_vmax(u);
+        if constexpr (GW == 32) { const float t = __shfl_xor(m, 16, 32); m = m > t ? m : t; }
         const uint64_t bal = __builtin_amdgcn_ballot_w64(lg && u == m);
-        const uint32_t mask = (uint32_t)(bal >> (lane & 48)) & 0xffffu;
+        const uint32_t mask = GW == 16 ? (uint32_t)(bal >> (lane & 48)) & 0xffffu : (uint32_t)(bal >> (lane & 32));
         depth += 1;
         int ach = __builtin_ctz(mask);
         // ties (rare): one wave-uniform test, then the Philox draw per group
@@ -232,12 +262,12 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
             }
         }
         const int ei = e * A + ach;
-        const uint32_t ncc = g16_or(a == ach ? nc : 0u);   // the chosen lane's nc, via DPP
+        const uint32_t ncc = gor<GW>(a == ach ? nc : 0u);  // the chosen lane's nc, via DPP
         const int Cch = (int)(ncc >> 16);
-        const bool keep = a == depth;                     // depth < 16: lane `depth` keeps the level
+        const bool keep = a == depth;                     // depth < GW: lane `depth` keeps the level
         pe = keep ? ei : pe;
         pc = keep ? Cch - 1 : pc;
-        if (depth >= 16 && a == 0) { path[2 * depth] = ei; path[2 * depth + 1] = Cch - 1; }
+        if (depth >= GW && a == 0) { path[2 * depth] = ei; path[2 * depth + 1] = Cch - 1; }
         vtp = vtp >= players ? 1 : vtp + 1;             // mod1(vtp + 1, |players|), :267
         if (Cch == 0) { out = SelectOut{e, ach, vtp, depth}; break; }
         e = Cch - 1; Np = (int)(ncc & 0xffffu);
@@ -246,7 +276,7 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
     return out;
 }
 
-// backpropagate! (SelfPlay.jl:190-217), quirk Q7, for the 16-lane group.
+// backpropagate! (SelfPlay.jl:190-217), quirk Q7, for the GW-lane group.
 // Node d of the path (0 = root ... depth = the just-expanded leaf with
 // to_play tl) receives v_in(d): v_in(depth) = the leaf value; otherwise
 // v_in(d) = v_out(d+1) with v_out(k) = (tp_k == tl) ? -R_k : R_k + γ v_in(k).
@@ -256,6 +286,7 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
 // alternates with depth): all levels update in parallel, bit-exactly.  The
 // min-max fold is order-independent (exact comparisons).  1-player games
 // have no resets and run the sequential loop on lane 0.
+template <int GW = 16>
 __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, int depth, float value, int tl,
                                             int A, int players, float discount, int& root_N, float& root_W,
                                             int root_tp, float& mmin, float& mmax, int a) {
@@ -283,8 +314,8 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
                 else { root_N = N; root_W = W; }
             }
         }
-        root_N = __shfl(root_N, 0, 16); root_W = __shfl(root_W, 0, 16);
-        mmin = __shfl(mmin, 0, 16); mmax = __shfl(mmax, 0, 16);
+        root_N = __shfl(root_N, 0, GW); root_W = __shfl(root_W, 0, GW);
+        mmin = __shfl(mmin, 0, GW); mmax = __shfl(mmax, 0, GW);
         return;
     }
     // two players: to_play alternates with depth (node k has mod1(root_tp + k),
@@ -295,7 +326,7 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
     // then the edge record and the children's R / to_play.
     float lmin = INFINITY, lmax = -INFINITY;
     int rN = root_N; float rW = root_W;
-    for (int base = 0; base <= depth; base += 16) {
+    for (int base = 0; base <= depth; base += GW) {
         const int d = base + a;
         if (d <= depth) {
             const int i = d > 0 ? path[2 * d] : 0;
@@ -327,18 +358,22 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
             } else { rN = N; rW = W; }
         }
     }
-    lmin = g16_min(lmin);
-    lmax = g16_max(lmax);
+    lmin = gmin<GW>(lmin);
+    lmax = gmax<GW>(lmax);
     mmin = mmin < lmin ? mmin : lmin;
     mmax = mmax > lmax ? mmax : lmax;
-    // lane 0 of the group (level 0 = the root) to all 16 lanes: DPP row broadcast
-    root_N = __builtin_amdgcn_update_dpp(0, rN, 0x150, 0xF, 0xF, false);
-    root_W = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, rW), 0x150, 0xF, 0xF, false));
+    // lane 0 of the group (level 0 = the root) to all GW lanes: DPP row broadcast
+    if constexpr (GW == 16) {
+        root_N = __builtin_amdgcn_update_dpp(0, rN, 0x150, 0xF, 0xF, false);
+        root_W = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, rW), 0x150, 0xF, 0xF, false));
+    } else {
+        root_N = __shfl(rN, 0, GW); root_W = __shfl(rW, 0, GW);
+    }
 }
 
 // select_action (SelfPlay.jl:293-306): same rule as the oracle.
 __device__ int select_action_dev(const int* cnt, uint32_t legal, int A, float temperature, uint32_t r) {
-    int acts[16], c[16], n = 0;
+    int acts[MZ_MAX_ACTIONS], c[MZ_MAX_ACTIONS], n = 0;
     for (int a = 0; a < A; ++a) if ((legal >> a) & 1u) { acts[n] = a; c[n] = cnt[a]; ++n; }
     if (temperature == 0.0f) {
         int best = 0;
@@ -355,7 +390,7 @@ __device__ int select_action_dev(const int* cnt, uint32_t legal, int A, float te
         return acts[n - 1];
     }
     float e = 1.0f / temperature;
-    float w[16], s = 0.0f;
+    float w[MZ_MAX_ACTIONS], s = 0.0f;
     for (int i = 0; i < n; ++i) {
         w[i] = c[i] > 0 ? (float)det_exp(det_log((double)c[i]) * (double)e) : 0.0f;
         s = s + w[i];
@@ -367,8 +402,9 @@ __device__ int select_action_dev(const int* cnt, uint32_t legal, int A, float te
 }
 
 // Copy one game's tree to the global debug buffers (parity tests only).
+template <int GW = 16>
 __device__ __forceinline__ void dump_tree(const TreeView& t, const TreeView& dst, int n_edges, int n_nodes,
-                                          int lane16) {
-    for (int i = lane16; i < n_edges; i += 16) dst.e[i] = t.e[i];
-    for (int i = lane16; i < n_nodes; i += 16) { dst.nr[i] = t.nr[i]; dst.ntp[i] = t.ntp[i]; }
+                                          int lane) {
+    for (int i = lane; i < n_edges; i += GW) dst.e[i] = t.e[i];
+    for (int i = lane; i < n_nodes; i += GW) { dst.nr[i] = t.nr[i]; dst.ntp[i] = t.ntp[i]; }
 }

@@ -49,22 +49,43 @@ def _act(a):
     return {"tanh": ACT_TANH, "relu": ACT_RELU, "identity": ACT_IDENTITY}[a]
 
 
+def _s2(n, k):
+    return (n + 2 * (k // 2) - k) // 2 + 1
+
+
+def resnet_board(conf, hyper):
+    """(W, H) of the hidden state: the observation board, or after the
+    downsampler (two stride-2 convs, two MeanPool(3, stride 2, pad 1);
+    84 -> 42 -> 21 -> 11 -> 6) — representation_output_size, which
+    prediction / dynamics read (Learning.jl:173, 194, 229)."""
+    W, H = conf.observation_shape[0], conf.observation_shape[1]
+    if getattr(hyper, "downsample", False):
+        kw, kh = hyper.conv_kernel_size
+        W, H = _s2(_s2(W, kw), kw), _s2(_s2(H, kh), kh)
+        W, H = _s2(_s2(W, 3), 3), _s2(_s2(H, 3), 3)
+    return W, H
+
+
 def resnet_specs(conf, hyper, net):
     """Intended ResNet architecture (Learning.jl:148-255 with Q12 fixed), in
-    the oracle's op order (oracle/mz_oracle.c onet_build_resnet)."""
-    W, H, C = conf.observation_shape
+    the oracle's op order (oracle/mz_oracle.c onet_build_resnet).  Conv ops
+    carry their output board (W, H), input board (Wi, Hi) and stride; "pool"
+    ops are the downsampler's MeanPool((3,3), stride 2, pad 1) (no params)."""
+    C = conf.observation_shape[2]
+    W, H = resnet_board(conf, hyper)
     nf, nb, hs, A = hyper.num_filters, hyper.num_blocks, hyper.width_hidden, len(conf.action_space)
     P, nvf, npf = W * H, hyper.num_first_head_filters, hyper.num_second_head_filters
     ops = []
 
-    def conv(ch, cin, cout, k, act=ACT_RELU):
-        ops.append(dict(chain=ch, kind="conv", cin=cin, cout=cout, kw=k[0], kh=k[1], W=W, H=H, bn=True,
-                        act=act, res_save=False, res_add=False))
+    def conv(ch, cin, cout, k, act=ACT_RELU, board=(W, H), stride=1, bn=True, inb=None):
+        ops.append(dict(chain=ch, kind="conv", cin=cin, cout=cout, kw=k[0], kh=k[1], W=board[0], H=board[1],
+                        Wi=(inb or board)[0], Hi=(inb or board)[1], stride=stride, bn=bn, act=act,
+                        res_save=False, res_add=False))
 
-    def block(ch, n, k):                                   # resnet_block (:148-158)
-        conv(ch, n, n, k)
+    def block(ch, n, k, board=(W, H)):                     # resnet_block (:148-158)
+        conv(ch, n, n, k, board=board)
         ops[-1]["res_save"] = True
-        conv(ch, n, n, k)
+        conv(ch, n, n, k, board=board)
         ops[-1]["res_add"] = True
 
     def dense(ch, i, o, act):
@@ -73,7 +94,26 @@ def resnet_specs(conf, hyper, net):
     k1 = (1, 1)
     if net == NET_REPR:                                    # :160-191
         k = tuple(hyper.conv_kernel_size)
-        conv(0, C * (conf.stacked_observations + 1) + conf.stacked_observations, nf, k)
+        cin = C * (conf.stacked_observations + 1) + conf.stacked_observations
+        if getattr(hyper, "downsample", False):            # :175-187 (`size` read as ksize)
+            b0 = tuple(conf.observation_shape[:2])
+            b1 = (_s2(b0[0], k[0]), _s2(b0[1], k[1]))
+            conv(0, cin, cin, k, act=ACT_IDENTITY, board=b1, stride=2, bn=False, inb=b0)
+            for _ in range(2):
+                block(0, cin, k, b1)
+            b2 = (_s2(b1[0], k[0]), _s2(b1[1], k[1]))
+            conv(0, cin, 2 * cin, k, act=ACT_IDENTITY, board=b2, stride=2, bn=False, inb=b1)
+            for _ in range(3):
+                block(0, 2 * cin, k, b2)
+            b3 = (_s2(b2[0], 3), _s2(b2[1], 3))
+            ops.append(dict(chain=0, kind="pool", cin=2 * cin, cout=2 * cin, kw=3, kh=3, W=b3[0], H=b3[1],
+                            Wi=b2[0], Hi=b2[1], stride=2, act=ACT_IDENTITY, res_save=False, res_add=False))
+            for _ in range(3):
+                block(0, 2 * cin, k, b3)
+            ops.append(dict(chain=0, kind="pool", cin=2 * cin, cout=2 * cin, kw=3, kh=3, W=W, H=H,
+                            Wi=b3[0], Hi=b3[1], stride=2, act=ACT_IDENTITY, res_save=False, res_add=False))
+            cin = 2 * cin
+        conv(0, cin, nf, k)
         for _ in range(nb):
             block(0, nf, k)
     elif net == NET_PRED:                                  # :193-226
@@ -106,6 +146,8 @@ def resnet_specs(conf, hyper, net):
 
 
 def _op_params(op):
+    if op["kind"] == "pool":
+        return 0
     if op["kind"] == "dense":
         return op["cin"] * op["cout"] + op["cout"]
     return op["kw"] * op["kh"] * op["cin"] * op["cout"] + op["cout"] + (2 * op["cout"] if op["bn"] else 0)
@@ -120,11 +162,15 @@ def param_count(conf, hyper, net):
 def net_macs(conf, hyper, net):
     """Multiply-accumulates of one forward of `net` for one item (the
     algorithmic FLOP count is 2x this): Dense in*out, conv W*H*kw*kh*cin*cout
-    (same-padded, stride 1)."""
+    over its output board, MeanPool W*H*kw*kh*c additions (counted as MACs)."""
     if isinstance(hyper, ResNetHP):
-        W, H, _ = conf.observation_shape
-        return sum(op["cin"] * op["cout"] * (op["kw"] * op["kh"] * W * H if op["kind"] == "conv" else 1)
-                   for op in resnet_specs(conf, hyper, net))
+        def macs(op):
+            if op["kind"] == "dense":
+                return op["cin"] * op["cout"]
+            if op["kind"] == "pool":
+                return op["W"] * op["H"] * op["kw"] * op["kh"] * op["cin"]
+            return op["cin"] * op["cout"] * op["kw"] * op["kh"] * op["W"] * op["H"]
+        return sum(macs(op) for op in resnet_specs(conf, hyper, net))
     return sum(i * o for _, i, o, _ in layer_specs(conf, hyper, net))
 
 
@@ -148,14 +194,17 @@ def init_net(conf, hyper, net, seed=0):
     parts = []
     if isinstance(hyper, ResNetHP):
         for op in resnet_specs(conf, hyper, net):
+            if op["kind"] == "pool":
+                continue
             if op["kind"] == "dense":
                 parts.append(glorot_uniform(rng, op["cout"], op["cin"]).reshape(-1))
                 parts.append(np.zeros(op["cout"], np.float32))
             else:
                 parts.append(glorot_uniform_conv(rng, op["kw"], op["kh"], op["cin"], op["cout"]))
                 parts.append(np.zeros(op["cout"], np.float32))
-                parts.append(np.zeros(op["cout"], np.float32))       # β
-                parts.append(np.ones(op["cout"], np.float32))        # γ
+                if op["bn"]:
+                    parts.append(np.zeros(op["cout"], np.float32))   # β
+                    parts.append(np.ones(op["cout"], np.float32))    # γ
         return np.concatenate(parts)
     for _, i, o, _ in layer_specs(conf, hyper, net):
         parts.append(glorot_uniform(rng, o, i).reshape(-1))
@@ -173,6 +222,9 @@ def unflatten_resnet(conf, hyper, net, flat):
     out, off = [], 0
     for op in resnet_specs(conf, hyper, net):
         op = dict(op)
+        if op["kind"] == "pool":
+            out.append(op)
+            continue
         if op["kind"] == "dense":
             i, o = op["cin"], op["cout"]
             op["w"] = flat[off: off + i * o].reshape(i, o).T
@@ -184,7 +236,7 @@ def unflatten_resnet(conf, hyper, net, flat):
             off += n
         op["b"] = flat[off: off + op["cout"]]
         off += op["cout"]
-        if op["kind"] == "conv":
+        if op["kind"] == "conv" and op["bn"]:
             op["beta"] = flat[off: off + op["cout"]]
             op["gamma"] = flat[off + op["cout"]: off + 2 * op["cout"]]
             off += 2 * op["cout"]

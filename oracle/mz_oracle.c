@@ -47,7 +47,9 @@ typedef struct { int32_t kind; mz_ffhp ff; mz_resnet_hp rn; } ora_nethp;   /* ki
 typedef struct {
     int in, out, act;          /* Dense: features; Conv: channels */
     size_t woff, boff;
-    int conv, kw, kh, pw, ph, W, H;   /* Conv (stride 1, zero pad, kernel flipped) over W x H */
+    int conv, kw, kh, pw, ph, W, H;   /* Conv (zero pad, kernel flipped); output board W x H */
+    int sw, sh, Wi, Hi;        /* stride and input board (stride 1: Wi x Hi = W x H) */
+    int pool;                  /* MeanPool(kw x kh, stride, pad) of `in` = `out` channels, no params */
     int bn; size_t bnoff;      /* BatchNorm(out) after the affine: β at bnoff, γ at bnoff + out */
     int res_save, res_add;     /* block input saved here / added before the activation */
 } OLayer;
@@ -59,7 +61,7 @@ typedef struct {
     int maxact;          /* largest activation (floats) */
 } ONet;
 
-static int olayer_insize(const OLayer* l) { return l->conv ? l->in * l->W * l->H : l->in; }
+static int olayer_insize(const OLayer* l) { return l->conv ? l->in * l->Wi * l->Hi : l->in; }
 static int olayer_outsize(const OLayer* l) { return l->conv ? l->out * l->W * l->H : l->out; }
 
 static OLayer* onet_add(ONet* net, int part, int in, int out, int act) {
@@ -77,6 +79,7 @@ static OLayer* onet_conv(ONet* net, int part, int in, int out, int kw, int kh, i
     memset(l, 0, sizeof(*l));
     l->conv = 1; l->in = in; l->out = out; l->act = act;
     l->kw = kw; l->kh = kh; l->pw = kw / 2; l->ph = kh / 2; l->W = W; l->H = H;
+    l->sw = 1; l->sh = 1; l->Wi = W; l->Hi = H;
     l->woff = net->nparams; net->nparams += (size_t)kw * kh * in * out;
     l->boff = net->nparams; net->nparams += (size_t)out;
     if (bn) { l->bn = 1; l->bnoff = net->nparams; net->nparams += (size_t)2 * out; }
@@ -91,9 +94,52 @@ static void onet_resblock(ONet* net, int part, int n, int k, int W, int H) {
     b->res_add = 1;
 }
 
+/* Conv(k, in => out, stride = 2, pad = k .÷ 2) without BatchNorm or
+ * activation (the downsampler's strided convs, Learning.jl:177,179) from a
+ * Wi x Hi board to ((Wi + 2pw - kw) ÷ 2 + 1) x (...) */
+static OLayer* onet_conv_s2(ONet* net, int in, int out, int kw, int kh, int Wi, int Hi) {
+    const int W = (Wi + 2 * (kw / 2) - kw) / 2 + 1, H = (Hi + 2 * (kh / 2) - kh) / 2 + 1;
+    OLayer* l = onet_conv(net, 0, in, out, kw, kh, W, H, 0, MZ_ACT_IDENTITY);
+    l->sw = 2; l->sh = 2; l->Wi = Wi; l->Hi = Hi;
+    return l;
+}
+
+/* MeanPool((3,3), stride = 2, pad = 1) (Learning.jl:181,183; the reference
+ * writes MeanPool(3, ...), which Flux 0.12 only accepts as a tuple) */
+static void onet_meanpool(ONet* net, int ch, int Wi, int Hi) {
+    OLayer* l = &net->L[0][net->n[0]++];
+    memset(l, 0, sizeof(*l));
+    l->conv = 1; l->pool = 1; l->in = ch; l->out = ch; l->act = MZ_ACT_IDENTITY;
+    l->kw = 3; l->kh = 3; l->pw = 1; l->ph = 1; l->sw = 2; l->sh = 2; l->Wi = Wi; l->Hi = Hi;
+    l->W = (Wi + 2 - 3) / 2 + 1; l->H = (Hi + 2 - 3) / 2 + 1;
+}
+
+/* Board of the hidden state: the observation board, or with ResNetHP
+ * downsample the board after the downsampler (two stride-2 convs and two
+ * stride-2 pools: 84 -> 42 -> 21 -> 11 -> 6), which the reference computes
+ * as representation_output_size (Learning.jl:173, taken from the wrong chain,
+ * Q12) and prediction / dynamics read (:194, :229). */
+static void rn_board(const mz_config* c, const mz_resnet_hp* hp, int* W, int* H) {
+    int w = c->observation_shape[0], h = c->observation_shape[1];
+    if (hp->downsample) {
+        const int kw = hp->conv_kernel_size[0], kh = hp->conv_kernel_size[1];
+        for (int i = 0; i < 2; ++i) { w = (w + 2 * (kw / 2) - kw) / 2 + 1; h = (h + 2 * (kh / 2) - kh) / 2 + 1; }
+        for (int i = 0; i < 2; ++i) { w = (w + 2 - 3) / 2 + 1; h = (h + 2 - 3) / 2 + 1; }
+    }
+    *W = w; *H = h;
+}
+
 static int nethp_hidden(const mz_config* c, const ora_nethp* hp) {
     if (hp->kind == 0) return hp->ff.hidden_state_size;
-    return c->observation_shape[0] * c->observation_shape[1] * hp->rn.num_filters;
+    int W, H; rn_board(c, &hp->rn, &W, &H);
+    return W * H * hp->rn.num_filters;
+}
+
+/* plane of the dynamics action input: the hidden state's board */
+static int hid_plane(const mz_config* c, const ora_nethp* hp) {
+    if (hp->kind == 0) return c->observation_shape[0] * c->observation_shape[1];
+    int W, H; rn_board(c, &hp->rn, &W, &H);
+    return W * H;
 }
 
 static void onet_finish(ONet* net) {
@@ -108,12 +154,29 @@ static void onet_finish(ONet* net) {
 
 /* init_representation / init_prediction / init_dynamics for ResNetHP */
 static void onet_build_resnet(ONet* net, int which, const mz_config* c, const mz_resnet_hp* hp) {
-    int W = c->observation_shape[0], H = c->observation_shape[1], C = c->observation_shape[2];
+    int W, H, C = c->observation_shape[2];
+    rn_board(c, hp, &W, &H);
     int nf = hp->num_filters, nb = hp->num_blocks, hs = hp->width_hidden, A = c->action_space_size;
     int P = W * H, nvf = hp->num_first_head_filters, npf = hp->num_second_head_filters;
     if (which == MZ_NET_REPR) {                                           /* :160-191 */
         int cin = C * (c->stacked_observations + 1) + c->stacked_observations;   /* Q12: the stacked input */
         int kw = hp->conv_kernel_size[0], kh = hp->conv_kernel_size[1];
+        if (hp->downsample) {                                             /* :175-187 */
+            /* `size` (undefined there) read as conv_kernel_size; indim[3] as
+             * the stacked input's channels cin */
+            int w = c->observation_shape[0], h = c->observation_shape[1];
+            OLayer* l = onet_conv_s2(net, cin, cin, kw, kh, w, h);        /* :177 */
+            w = l->W; h = l->H;
+            for (int i = 0; i < 2; ++i) onet_resblock(net, 0, cin, kw, w, h);
+            l = onet_conv_s2(net, cin, 2 * cin, kw, kh, w, h);            /* :179 */
+            w = l->W; h = l->H;
+            for (int i = 0; i < 3; ++i) onet_resblock(net, 0, 2 * cin, kw, w, h);
+            onet_meanpool(net, 2 * cin, w, h);                            /* :181 */
+            w = net->L[0][net->n[0] - 1].W; h = net->L[0][net->n[0] - 1].H;
+            for (int i = 0; i < 3; ++i) onet_resblock(net, 0, 2 * cin, kw, w, h);
+            onet_meanpool(net, 2 * cin, w, h);                            /* :183 */
+            cin = 2 * cin;                                                /* :184: Conv(ksize, 2C => nf) */
+        }
         onet_conv(net, 0, cin, nf, kw, kh, W, H, 1, MZ_ACT_RELU);
         for (int i = 0; i < nb; ++i) onet_resblock(net, 0, nf, kw, W, H);
     } else if (which == MZ_NET_PRED) {                                    /* :193-226 */
@@ -212,21 +275,24 @@ static void dense_fwd(const OLayer* l, const float* P, const float* x, float* y)
         y[o] = act_apply(l->act, mz_dot(P + l->woff, l->out, l->in, o, x) + P[l->boff + o]);
 }
 
-/* Flux Conv (stride 1, zero padding, kernel flipped) on a (W, H, cin)
- * column-major activation: the im2col row of position (w, h) is, for k = i +
- * kw*j + kw*kh*c (the weight's column-major order), x[w + (kw-1-i) - pw,
- * h + (kh-1-j) - ph, c].  Then bias, BatchNorm, the saved block input, act. */
+/* Flux Conv (zero padding, kernel flipped) on a (Wi, Hi, cin) column-major
+ * activation: the im2col row of output position (w, h) is, for k = i +
+ * kw*j + kw*kh*c (the weight's column-major order), x[sw*w + (kw-1-i) - pw,
+ * sh*h + (kh-1-j) - ph, c] (0 outside the board).  Then bias, BatchNorm, the
+ * saved block input, act. */
 static void conv_fwd(const OLayer* l, const float* P, const float* x, float* y, const float* res) {
     const int W = l->W, H = l->H, Pn = W * H, K = l->kw * l->kh * l->in;
+    const int Wi = l->Wi, Hi = l->Hi, Pi = Wi * Hi;
     float* col = (float*)malloc(sizeof(float) * (size_t)K);
     for (int hh = 0; hh < H; ++hh)
         for (int ww = 0; ww < W; ++ww) {
             for (int c = 0; c < l->in; ++c)
                 for (int j = 0; j < l->kh; ++j)
                     for (int i = 0; i < l->kw; ++i) {
-                        const int sx = ww + (l->kw - 1 - i) - l->pw, sy = hh + (l->kh - 1 - j) - l->ph;
+                        const int sx = l->sw * ww + (l->kw - 1 - i) - l->pw;
+                        const int sy = l->sh * hh + (l->kh - 1 - j) - l->ph;
                         const int k = i + l->kw * j + l->kw * l->kh * c;
-                        col[k] = (sx >= 0 && sx < W && sy >= 0 && sy < H) ? x[sx + W * sy + Pn * c] : 0.0f;
+                        col[k] = (sx >= 0 && sx < Wi && sy >= 0 && sy < Hi) ? x[sx + Wi * sy + Pi * c] : 0.0f;
                     }
             const int p = ww + W * hh;
             for (int o = 0; o < l->out; ++o) {
@@ -237,6 +303,25 @@ static void conv_fwd(const OLayer* l, const float* P, const float* x, float* y, 
             }
         }
     free(col);
+}
+
+/* NNlib meanpool (0.7): the in-board window entries summed in f32, rows of
+ * the window (j) outer and columns (i) inner, times Float32(1/prod(k)) —
+ * padded entries count in the divisor (the window is never flipped). */
+static void pool_fwd(const OLayer* l, const float* x, float* y) {
+    const int W = l->W, H = l->H, Wi = l->Wi, Hi = l->Hi;
+    const float inv = 1.0f / (float)(l->kw * l->kh);
+    for (int c = 0; c < l->in; ++c)
+        for (int hh = 0; hh < H; ++hh)
+            for (int ww = 0; ww < W; ++ww) {
+                float m = 0.0f;
+                for (int j = 0; j < l->kh; ++j)
+                    for (int i = 0; i < l->kw; ++i) {
+                        const int sx = l->sw * ww + i - l->pw, sy = l->sh * hh + j - l->ph;
+                        if (sx >= 0 && sx < Wi && sy >= 0 && sy < Hi) m = m + x[sx + Wi * sy + Wi * Hi * c];
+                    }
+                y[ww + W * hh + W * H * c] = inv * m;
+            }
 }
 
 /* NNlib softmax over n entries: max, exp(x - max), sequential sum, divide. */
@@ -257,7 +342,8 @@ static void run_chain(const ONet* net, int part, const float* P, const float* x,
         const OLayer* l = &net->L[part][i];
         float* dst = (i & 1) ? b : a;
         if (l->res_save) memcpy(res, cur, sizeof(float) * (size_t)olayer_insize(l));
-        if (l->conv) conv_fwd(l, P, cur, dst, res);
+        if (l->pool) pool_fwd(l, cur, dst);
+        else if (l->conv) conv_fwd(l, P, cur, dst, res);
         else dense_fwd(l, P, cur, dst);
         cur = dst;
     }
@@ -283,6 +369,8 @@ static void net_forward1(const ONet* net, const float* P, const float* x, float*
     }
     free(t);
 }
+
+EXPORT int ora_hidden_size(const mz_config* c, const ora_nethp* hp) { return nethp_hidden(c, hp); }
 
 EXPORT size_t ora_param_count(const mz_config* c, const ora_nethp* hp, int which) {
     ONet n; onet_build(&n, which, c, hp); return n.nparams;
@@ -475,7 +563,7 @@ static int run_mcts(OCtx* X, const float* obs, const uint8_t* legal, int to_play
          * action plane Float32(a / |A|) with a 1-based. */
         for (int i = 0; i < H; ++i) ph[i] = ph[i] * 2.0f;
         memcpy(sa, ph, sizeof(float) * H);
-        int plane = c->observation_shape[0] * c->observation_shape[1];
+        int plane = hid_plane(c, X->hp);
         float aval = (float)((double)(action + 1) / (double)A);
         for (int i = 0; i < plane; ++i) sa[H + i] = aval;
         int slot = it + 1;
@@ -802,7 +890,7 @@ EXPORT void ora_unroll(const mz_config* c, const ora_nethp* hp, const float* Pre
     onet_build(&nr, MZ_NET_REPR, c, hp); onet_build(&np, MZ_NET_PRED, c, hp); onet_build(&nd, MZ_NET_DYN, c, hp);
     int H = nethp_hidden(c, hp), A = c->action_space_size, K = c->num_unroll_steps;
     int in = olayer_insize(&nr.L[0][0]);
-    int plane = c->observation_shape[0] * c->observation_shape[1];
+    int plane = hid_plane(c, hp);
     float* h = (float*)malloc(sizeof(float) * (size_t)H);
     float* sa = (float*)malloc(sizeof(float) * (size_t)(H + plane));
     float v, pol[MAXA];

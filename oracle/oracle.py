@@ -34,6 +34,8 @@ def lib():
         L = ctypes.CDLL(LIB)
         L.ora_param_count.restype = ctypes.c_size_t
         L.ora_param_count.argtypes = [_VP, _VP, ctypes.c_int]
+        L.ora_hidden_size.restype = ctypes.c_int
+        L.ora_hidden_size.argtypes = [_VP, _VP]
         L.ora_net_forward.argtypes = [_VP, _VP, ctypes.c_int, _VP, _VP, ctypes.c_int, _VP, _VP]
         L.ora_mcts_search.restype = ctypes.c_int
         L.ora_mcts_search.argtypes = [_VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_int, _VP, _VP, _VP,
@@ -103,10 +105,10 @@ class Oracle:
         self.chp = nethp(chp)
         self.seed = seed
         self.A = cconf.action_space_size
-        if self.chp.kind == 1:
-            self.H = cconf.observation_shape[0] * cconf.observation_shape[1] * chp.num_filters
-        else:
-            self.H = chp.hidden_state_size
+        self.H = self.L.ora_hidden_size(ctypes.byref(self.cconf), ctypes.byref(self.chp))
+        # board of the dynamics action plane: the hidden state's
+        self.plane = self.H // chp.num_filters if self.chp.kind == 1 else \
+            cconf.observation_shape[0] * cconf.observation_shape[1]
         self.S = cconf.num_iters
         self.K = cconf.num_unroll_steps
         self.params = [np.zeros(self.param_count(i), np.float32) for i in range(3)]

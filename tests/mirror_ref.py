@@ -118,7 +118,7 @@ class Mirror:
         if exploration:
             self.add_noise(root, gid, step)
         mm = [f32(np.inf), f32(-np.inf)]
-        plane = self.c.observation_shape[0] * self.c.observation_shape[1]
+        plane = self.o.plane                                     # the hidden state's board
         for it in range(self.c.num_iters):
             node, vtp, path, depth, action = root, to_play, [root], 0, 0
             while node.children is not None:

@@ -35,12 +35,16 @@ def _perturb_bn(conf, hyper, nets, seed=1):
         flat = flat.copy()
         off = 0
         for op in resnet_specs(conf, hyper, n):
+            if op["kind"] == "pool":
+                continue
             if op["kind"] == "dense":
                 off += op["cin"] * op["cout"] + op["cout"]
                 continue
             off += op["kw"] * op["kh"] * op["cin"] * op["cout"]
             flat[off: off + op["cout"]] = rng.normal(0, 0.1, op["cout"]).astype(np.float32)        # bias
             off += op["cout"]
+            if not op["bn"]:
+                continue
             flat[off: off + op["cout"]] = rng.normal(0, 0.1, op["cout"]).astype(np.float32)        # β
             flat[off + op["cout"]: off + 2 * op["cout"]] = rng.uniform(0.5, 1.5, op["cout"]).astype(np.float32)
             off += 2 * op["cout"]
@@ -54,7 +58,6 @@ def _torch_forward(conf, hyper, net, flat, x):
     import torch.nn.functional as F
     from muzero_jl_amd.config import ACT_RELU, ACT_TANH
     from muzero_jl_amd.networks import unflatten_resnet
-    W, H, _ = conf.observation_shape
     ops = unflatten_resnet(conf, hyper, net, flat)
 
     def act(t, a):
@@ -63,16 +66,20 @@ def _torch_forward(conf, hyper, net, flat, x):
     def chain(t, ch):
         res = None
         for op in [o for o in ops if o["chain"] == ch]:
-            if op["kind"] == "conv":
+            if op["kind"] == "pool":                   # MeanPool((3,3), stride 2, pad 1), padding counted
+                t = F.avg_pool2d(t, 3, stride=2, padding=1, count_include_pad=True)
+            elif op["kind"] == "conv":
                 if t.dim() == 2:                       # (n, W*H*C) column-major -> (n, C, H, W)
-                    t = t.reshape(t.shape[0], op["cin"], H, W)
+                    t = t.reshape(t.shape[0], op["cin"], op["Hi"], op["Wi"])
                 if op["res_save"]:
                     res = t
                 w = torch.flip(torch.from_numpy(np.ascontiguousarray(op["w"])), dims=[2, 3])
-                y = F.conv2d(t, w, torch.from_numpy(op["b"].copy()), padding=(op["kh"] // 2, op["kw"] // 2))
-                y = F.batch_norm(y, torch.zeros(op["cout"]), torch.ones(op["cout"]),
-                                 torch.from_numpy(op["gamma"].copy()), torch.from_numpy(op["beta"].copy()),
-                                 training=False, eps=1e-5)
+                y = F.conv2d(t, w, torch.from_numpy(op["b"].copy()), stride=op["stride"],
+                             padding=(op["kh"] // 2, op["kw"] // 2))
+                if op["bn"]:
+                    y = F.batch_norm(y, torch.zeros(op["cout"]), torch.ones(op["cout"]),
+                                     torch.from_numpy(op["gamma"].copy()), torch.from_numpy(op["beta"].copy()),
+                                     training=False, eps=1e-5)
                 if op["res_add"]:
                     y = y + res
                 t = act(y, op["act"])
@@ -130,5 +137,63 @@ def test_resnet_oracle_search_matches_mirror(ttt):
     o, _ = _resnet_oracle(conf, ttt.resnet_hyper, seed=3)
     obs, legal, tp = random_positions(3, 17)
     cv, rv, act, _, _ = o.mcts_search(obs, legal, tp, exploration=True, rng_step=2, game_offset=5, dump=True)
+    cv2, rv2, act2, _ = Mirror(o, conf).search(obs, legal, tp, True, 5, 2)
+    assert np.array_equal(cv, cv2) and np.array_equal(rv, rv2) and np.array_equal(act, act2)
+
+
+def test_downsample_param_counts_and_board():
+    """configs[4]: the downsampler of Learning.jl:175-187 takes 84x84x4 to 6x6x8."""
+    from muzero_jl_amd.games import atari_synth as at
+    from muzero_jl_amd.networks import param_count, resnet_board, resnet_specs
+    assert resnet_board(at.conf, at.resnet_hyper) == (6, 6)
+    ops = resnet_specs(at.conf, at.resnet_hyper, 0)
+    assert [(o["Wi"], o["W"]) for o in ops if o["kind"] != "dense" and o["stride"] == 2] == \
+        [(84, 42), (42, 21), (21, 11), (11, 6)]
+    o, _ = _resnet_oracle(at.conf, at.resnet_hyper)
+    assert [param_count(at.conf, at.resnet_hyper, n) for n in range(3)] == [o.param_count(n) for n in range(3)]
+    assert o.H == 6 * 6 * 64
+
+
+@pytest.mark.parametrize("net", [0, 1, 2])
+def test_downsample_oracle_matches_torch(net):
+    """The downsampling representation (stride-2 convs without BatchNorm,
+    MeanPool with the padding counted) and the 6x6 prediction / dynamics with
+    18 actions, oracle vs torch fp32 at 1e-5."""
+    from muzero_jl_amd.games import atari_synth as at
+    conf, hyper = at.conf, at.resnet_hyper
+    o, nets = _resnet_oracle(conf, hyper)
+    nets = _perturb_bn(conf, hyper, nets)
+    for n, w in enumerate(nets):
+        o.set_weights(n, w)
+    rng = np.random.default_rng(net)
+    n = 2
+    if net == 0:
+        x = at.observations(n, seed=net)
+    elif net == 1:
+        x = rng.normal(0, 1, (n, o.H)).astype(np.float32)
+    else:
+        x = np.concatenate([rng.normal(0, 1, (n, o.H)), np.full((n, 36), 5 / 18)], 1).astype(np.float32)
+    ref = _torch_forward(conf, hyper, net, nets[net], x)
+    got = o.forward(net, x)
+    if net == 0:
+        np.testing.assert_allclose(got, ref, **TOL)
+    else:
+        np.testing.assert_allclose(got[0], ref[0], **TOL)
+        np.testing.assert_allclose(got[1], ref[1], **TOL)
+
+
+def test_downsample_oracle_search_matches_mirror():
+    """configs[4] search semantics (one player, 18 actions, 6x6 hidden board)
+    in the oracle vs the independent mirror."""
+    from mirror_ref import Mirror
+    from muzero_jl_amd.games import atari_synth as at
+    conf = dataclasses.replace(at.conf, num_iters=6)
+    o, _ = _resnet_oracle(conf, at.resnet_hyper, seed=3)
+    G = 2
+    obs = at.observations(G, seed=1)
+    legal = np.ones((G, 18), bool)
+    legal[1, 5:9] = False
+    tp = np.ones(G, np.int32)
+    cv, rv, act = o.mcts_search(obs, legal, tp, exploration=True, rng_step=2, game_offset=5)
     cv2, rv2, act2, _ = Mirror(o, conf).search(obs, legal, tp, True, 5, 2)
     assert np.array_equal(cv, cv2) and np.array_equal(rv, rv2) and np.array_equal(act, act2)
