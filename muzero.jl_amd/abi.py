@@ -78,6 +78,15 @@ def load_library(path=LIB_PATH):
     if not os.path.exists(path):
         raise RuntimeError(f"libmz.so not built at {path}: run __graft_entry__.build() "
                            "(there is no CPU fallback for the engine)")
+    # torch's wheel ships its own libamdhip64.so.7 with the same soname as
+    # /opt/rocm's: whichever loads first serves the whole process.  Loading
+    # torch first (when present) makes libmz bind to torch's copy, so the
+    # engine and torch streams / device tensors share one HIP runtime in any
+    # import order; torch cannot initialise on the other copy.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
@@ -98,7 +107,9 @@ def _copy_d2h(dst, src_ptr):
     """hipMemcpy device -> host (the HIP runtime libmz is linked against)."""
     global _hip
     if _hip is None:
-        _hip = ctypes.CDLL("libamdhip64.so")
+        # by soname: the copy already loaded for libmz (torch's or /opt/rocm's,
+        # whichever came first); a plain "libamdhip64.so" can load a second runtime
+        _hip = ctypes.CDLL("libamdhip64.so.7")
         _hip.hipMemcpy.restype = ctypes.c_int
         _hip.hipMemcpy.argtypes = [_VP, _VP, ctypes.c_size_t, ctypes.c_int]
     rc = _hip.hipMemcpy(dst.ctypes.data_as(_VP), ctypes.c_void_p(src_ptr), dst.nbytes, 2)   # DeviceToHost

@@ -33,6 +33,8 @@ extern "C" __global__ void mz_rsearch_tree(RSearchParams P);
 extern "C" __global__ void mz_rsearch_root32(RSearchParams P);
 extern "C" __global__ void mz_downsample_kernel(DsParams Q);
 extern "C" __global__ void mz_rsearch_tree32(RSearchParams P);
+extern "C" __global__ void mz_rsearch_tree_lds(RSearchParams P);
+extern "C" __global__ void mz_rsearch_tree_lds32(RSearchParams P);
 extern "C" __global__ void mz_rsearch_nets(RSearchParams P);
 extern "C" __global__ void mz_runroll_kernel(RUnrollParams U);
 extern "C" __global__ void mz_sp_prepare(SpParams S);
@@ -146,6 +148,7 @@ struct mz_handle {
     int* d_plan_sim_res = nullptr;          // register-resident image of the sim plan (or null)
     double* d_pbc = nullptr; double* d_sqrt = nullptr; float* d_aval = nullptr;
     double* d_pbterm = nullptr;             // pbc(Np) * (sqrt(Np) / (Nc + 1)), triangle
+    size_t rtree_lds = 0;                                    // LDS of the LDS-cached ResNet tree step (0 = HBM kernel)
     char* d_tree = nullptr; size_t tree_game_bytes = 0; bool lds_tree = false; int dump_tree = 0;
     int time_nets = 0;                      // mz_debug_enable flag 2: events around each ResNet nets launch
     std::vector<hipEvent_t> tev; size_t tev_used = 0;
@@ -1032,8 +1035,18 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
         const size_t G = (size_t)max_games, S = (size_t)h->S, A = (size_t)h->A, H = (size_t)h->H;
         h->tree_game_bytes = tree_game_bytes(h->S, h->A);
         CK(alloc_search_tables(h));
-        CK(al(&h->d_tree, G * h->tree_game_bytes));
+        // +64: the tree step copies the to_play bytes as dwords (up to 3 bytes past them)
+        CK(al(&h->d_tree, G * h->tree_game_bytes + 64));
         CK(al(&h->d_hid, G * (S + 1) * H));
+        {
+            const int gw = h->A > 16 ? 32 : 16;
+            const RsTreeLds L = rs_tree_lds(h->S, h->tree_game_bytes, gw);
+            h->rtree_lds = (size_t)L.total <= kLdsMax && !std::getenv("MZ_RTREE_HBM") ? (size_t)L.total : 0;
+            if (h->rtree_lds)
+                CK(hipFuncSetAttribute(gw == 32 ? (const void*)mz_rsearch_tree_lds32 : (const void*)mz_rsearch_tree_lds,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->rtree_lds) == hipSuccess
+                       ? 0 : fail(h, "hipFuncSetAttribute(tree_lds)"));
+        }
         CK(al(&h->d_rpath, G * 2 * (S + 2))); CK(al(&h->d_rgst, G * RG_INTS));
         CK(al(&h->d_rxpred, G * H)); CK(al(&h->d_rov, G)); CK(al(&h->d_rologit, G * A)); CK(al(&h->d_ror, G));
         CK(al(&h->d_obs, G * h->obs_feat)); CK(al(&h->d_legal, G * A)); CK(al(&h->d_tp, G));
@@ -1295,11 +1308,15 @@ static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     const int gw = h->A > 16 ? 32 : 16;             // lanes per game in the tree kernels
     const unsigned tiles = (unsigned)((G + P.ng - 1) / P.ng), groups = (unsigned)((G + 256 / gw - 1) / (256 / gw));
     const void* kroot = gw == 32 ? (const void*)mz_rsearch_root32 : (const void*)mz_rsearch_root;
-    const void* ktree = gw == 32 ? (const void*)mz_rsearch_tree32 : (const void*)mz_rsearch_tree;
+    // tree step: LDS-cached (one wave per 64/gw games) unless the tree exceeds the LDS
+    const bool tl = h->rtree_lds != 0;
+    const void* ktree = tl ? (gw == 32 ? (const void*)mz_rsearch_tree_lds32 : (const void*)mz_rsearch_tree_lds)
+                           : (gw == 32 ? (const void*)mz_rsearch_tree32 : (const void*)mz_rsearch_tree);
+    const unsigned tgrid = tl ? (unsigned)((G + 64 / gw - 1) / (64 / gw)) : groups;
     MZ_TRY(h, hipLaunchKernel(kroot, dim3(tiles), dim3(RN_THREADS), args, rsearch_root_lds(h), st));
     for (int s = 0; s <= h->S; ++s) {
         P.s = s;
-        MZ_TRY(h, hipLaunchKernel(ktree, dim3(groups), dim3(256), args, 0, st));
+        MZ_TRY(h, hipLaunchKernel(ktree, dim3(tgrid), dim3(tl ? 64 : 256), args, tl ? h->rtree_lds : 0, st));
         if (s == h->S) break;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->time_nets) {

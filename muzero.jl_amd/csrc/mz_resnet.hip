@@ -470,6 +470,197 @@ __device__ __forceinline__ void rsearch_tree_body(const RSearchParams& P) {
 extern "C" __global__ __launch_bounds__(256) void mz_rsearch_tree(RSearchParams P) { rsearch_tree_body<16>(P); }
 extern "C" __global__ __launch_bounds__(256) void mz_rsearch_tree32(RSearchParams P) { rsearch_tree_body<32>(P); }
 
+// Copy n units of `size` bytes (4 or 16) from global `src` to LDS `dst` with
+// LDS-DMA (global_load_lds): per instruction the wave moves 64 units to the
+// wave-uniform base dst + 64·c, lane l's unit landing at base + l·size.
+// Issue only; the caller waits (vmcnt) before reading.
+template <int SZ>
+__device__ __forceinline__ void glds_copy(const void* src, void* dst, int n, int lane) {
+    const char* s = reinterpret_cast<const char*>(src);
+    char* d = reinterpret_cast<char*>(dst);
+    for (int c = 0; c < n; c += 64)
+        if (c + lane < n) {
+            auto* g = (__attribute__((address_space(1))) void*)(s + (size_t)(c + lane) * SZ);
+            auto* l = (__attribute__((address_space(3))) void*)(d + (size_t)c * SZ);
+            if constexpr (SZ == 16) __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
+            else __builtin_amdgcn_global_load_lds(g, l, 4, 0, 0);
+        }
+}
+
+// The tree step of rsearch_tree_body with each game's tree cached in LDS for
+// the launch.  A launch walks up to depth levels of select and of backup, one
+// dependent access each; on the HBM tree every one of them is a cache miss
+// (the previous launch wrote the records), so a deep 1-player search (BASELINE
+// configs[4]: mean depth 49) spent ~2 µs per level.  Here one wave (64/GW
+// games) first copies, by LDS-DMA, each game's existing nodes (edge records,
+// rewards, to_play), its path and the pUCT tables into LDS, all in flight at
+// once; expand, backup, select and the search statistics then run on LDS
+// exactly as in rsearch_tree_body.  HBM stays the tree's home between
+// launches: the records this step changed — the new node's A edges, the path
+// edges backup updated, the new node's reward and to_play — are written back.
+#ifdef MZ_STAMPS   // diagnostic build only: phase ticks of workgroup 0 at every 4th simulation
+#define RT_STAMP(k)                                                                                   \
+    do {                                                                                              \
+        if (blockIdx.x == 0 && threadIdx.x == 0 && (P.s & 3) == 0)                                    \
+            P.stamps[1024 + (P.s >> 2) * 16 + (k)] = __builtin_amdgcn_s_memtime();                    \
+    } while (0)
+#else
+#define RT_STAMP(k) do {} while (0)
+#endif
+template <int GW>
+__device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    RT_STAMP(0);
+    constexpr int NGW = 64 / GW;
+    const int gl = threadIdx.x / GW, a = threadIdx.x % GW, lane = threadIdx.x & 63;
+    const int gg = blockIdx.x * NGW + gl;
+    const int A = P.A, H = P.H, S = P.S, PS = 2 * (S + 2), s = P.s;
+    const int E = (S + 1) * A, NN = S + 1;
+    const RsTreeLds L = rs_tree_lds(S, P.tree_game_bytes, GW);
+    char* lb = reinterpret_cast<char*>(lds);
+    double* pbc = reinterpret_cast<double*>(lb);
+    double* sqt = pbc + (S + 2);
+    // per-game state and network outputs: plain loads, issued before the copies
+    const bool live = gg < P.G;
+    const int gc = live ? gg : P.G - 1;
+    int* st = P.gst + (size_t)gc * RG_INTS;
+    const int4 st0 = reinterpret_cast<const int4*>(st)[0], st1 = reinterpret_cast<const int4*>(st)[1];
+    const int4 st2 = reinterpret_cast<const int4*>(st)[2];
+    const float logit = s > 0 && a < A ? P.o_logit[(size_t)gc * A + a] : 0.0f;
+    const float o_r = s > 0 ? P.o_r[gc] : 0.0f, o_v = s > 0 ? P.o_v[gc] : 0.0f;
+    // LDS-DMA: tables, then per game the existing nodes 0..n_old-1 and the path
+    const int n_old = s > 0 ? s : 1;
+    glds_copy<4>(P.pbc_tab, pbc, 2 * (S + 2), lane);
+    glds_copy<4>(P.sqrt_tab, sqt, 2 * (S + 2), lane);
+    for (int g = 0; g < NGW; ++g) {
+        const int gq = blockIdx.x * NGW + g;
+        if (gq >= P.G) break;
+        const char* src = P.tree + (size_t)gq * P.tree_game_bytes;
+        char* dst = lb + L.tables + g * L.game;
+        glds_copy<16>(src, dst, n_old * A, lane);                                    // edge records
+        glds_copy<4>(src + 16 * (size_t)E, dst + 16 * (size_t)E, n_old, lane);        // nr
+        glds_copy<4>(src + 16 * (size_t)E + 4 * (size_t)NN, dst + 16 * (size_t)E + 4 * (size_t)NN,
+                     (n_old + 3) / 4, lane);                                           // ntp (bytes, as dwords)
+        glds_copy<4>(P.path + (size_t)gq * PS, dst + L.path, PS, lane);
+    }
+    RT_STAMP(1);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    RT_STAMP(2);
+    if (!live) return;                              // whole GW-lane groups leave together
+    char* gb = lb + L.tables + gl * L.game;
+    TreeView tree = tree_view(gb, E, NN);
+    TreeView gt = rs_tree(P, gg);
+    int* path = reinterpret_cast<int*>(gb + L.path);
+    float* stg = reinterpret_cast<float*>(gb + L.stg);
+    const uint32_t legal = (uint32_t)st0.x;
+    const int root_tp = st0.y;
+    const uint32_t gid = P.game_offset + (uint32_t)gg;
+    int rN = st0.z;
+    float rW = __int_as_float(st0.w), mmin = __int_as_float(st1.x), mmax = __int_as_float(st1.y);
+    if (s > 0) {
+        const int e_new = s;                        // the node simulation s-1 expanded (:280)
+        const float prior = double_softmax_prior<GW>(logit, a, A, legal, stg);
+        init_edges(tree, e_new, a, A, prior);
+        const int tl = st2.x, depth = st2.y;
+        if (a == 0) {
+            const int li = st1.z * A + st1.w;
+            tree.nc(li) = (tree.nc(li) & 0xffffu) | ((uint32_t)(e_new + 1) << 16);
+            tree.nr[e_new] = o_r;
+            tree.ntp[e_new] = (int8_t)tl;
+            path[2 * depth + 1] = e_new;
+            gt.nr[e_new] = o_r;
+            gt.ntp[e_new] = (int8_t)tl;
+        }
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        RT_STAMP(3);
+        if (P.players == 1)
+            backup_path_1p<GW>(tree, path, depth, o_v, P.discount, rN, rW, mmin, mmax, a,
+                               reinterpret_cast<float*>(gb + L.rr), reinterpret_cast<float*>(gb + L.vin));
+        else
+            backup_path<GW>(tree, path, depth, o_v, tl, A, P.players, P.discount, rN, rW, root_tp, mmin, mmax,
+                            a);                                                 // :281
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        RT_STAMP(4);
+        // write-back: the new node's edges, then the path edges (the leaf edge last level)
+        if (a < A) gt.e[e_new * A + a] = tree.e[e_new * A + a];
+        for (int d = 1 + a; d <= depth; d += GW) {
+            const int i = path[2 * d];
+            gt.e[i] = tree.e[i];
+        }
+        if (a == 0) {
+            st[RG_ROOTN] = rN; st[RG_ROOTW] = __float_as_int(rW);
+            st[RG_MMIN] = __float_as_int(mmin); st[RG_MMAX] = __float_as_int(mmax);
+        }
+        RT_STAMP(5);
+    }
+    if (s < S) {
+        const SelectOut so = select_path<false, GW>(tree, P.path + (size_t)gg * PS, rN, root_tp, legal, mmin, mmax,
+                                                    a, lane, A, P.players, P.discount, nullptr, pbc, sqt, P.seed,
+                                                    gid, P.rng_step, s);                   // :256-268
+        RT_STAMP(6);
+        if (a == 0) {
+            st[RG_LEAF_E] = so.leaf_e; st[RG_LEAF_A] = so.leaf_a; st[RG_VTP] = so.vtp; st[RG_DEPTH] = so.depth;
+        }
+        // parent h -> prediction input; h *= 2 in place (Q1), read by the dynamics launch.
+        // 16-byte pieces, RT_GU per lane loaded before any is stored (the stores
+        // could alias the loads, so a one-at-a-time loop waits a full memory
+        // round trip per piece)
+        float* hp = P.hid + ((size_t)gg * (S + 1) + so.leaf_e) * H;
+        float* xp = P.x_pred + (size_t)gg * H;
+        if ((H & 3) == 0) {
+            constexpr int RT_GU = 8;
+            float4* hp4 = reinterpret_cast<float4*>(hp);
+            float4* xp4 = reinterpret_cast<float4*>(xp);
+            const int H4 = H >> 2;
+            for (int k0 = 0; k0 < H4; k0 += RT_GU * GW) {
+                float4 v[RT_GU];
+#pragma unroll
+                for (int u = 0; u < RT_GU; ++u) {
+                    const int k = k0 + u * GW + a;
+                    if (k < H4) v[u] = hp4[k];
+                }
+#pragma unroll
+                for (int u = 0; u < RT_GU; ++u) {
+                    const int k = k0 + u * GW + a;
+                    if (k < H4) {
+                        xp4[k] = v[u];
+                        hp4[k] = make_float4(v[u].x * 2.0f, v[u].y * 2.0f, v[u].z * 2.0f, v[u].w * 2.0f);
+                    }
+                }
+            }
+        } else {
+            for (int k = a; k < H; k += GW) {
+                const float hv = hp[k];
+                xp[k] = hv;
+                hp[k] = hv * 2.0f;
+            }
+        }
+        RT_STAMP(7);
+    } else {                                        // store_search_stats! (:115-122) + select_action (:293-306)
+        const bool lg = a < A && ((legal >> a) & 1u);
+        const int Nc = lg ? (int)(tree.nc(a) & 0xffffu) : 0;
+        const int sum = gisum<GW>(Nc);
+        if (a < A) P.child_visits[(size_t)gg * A + a] = lg ? (float)((double)Nc / (double)sum) : 0.0f;
+        int cnt[GW];
+#pragma unroll
+        for (int b = 0; b < GW; ++b) cnt[b] = __shfl(Nc, b, GW);
+        if (a == 0) {
+            P.root_value[gg] = rN == 0 ? 0.0f : rW / (float)rN;
+            const uint32_t r = mz_rng_u32(P.seed, MZ_RNG_ACTION, gid, P.rng_step, 0);
+            P.action_out[gg] = select_action_dev(cnt, legal, A, P.temperature, r) + 1;
+        }
+    }
+}
+extern "C" __global__ __launch_bounds__(64) void mz_rsearch_tree_lds(RSearchParams P) {
+    rsearch_tree_lds_body<16>(P);
+}
+extern "C" __global__ __launch_bounds__(64) void mz_rsearch_tree_lds32(RSearchParams P) {
+    rsearch_tree_lds_body<32>(P);
+}
+
 // Networks of simulation s: blockIdx.y = 0 prediction(parent h), 1 dynamics
 // (2h ⊕ a/|A|, Q1) writing h' into hidden slot s+1.
 extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RSearchParams P) {

@@ -80,6 +80,26 @@ struct RSearchParams {
     const float* Wimg; const float* flat;
 };
 
+// LDS layout of the LDS-cached tree step (mz_rsearch_tree_lds*): one wave per
+// workgroup, 64/GW games.  Shared: the pUCT tables pbc[S+2], sqrt[S+2] (f64).
+// Per game: the tree copy (tree_game_bytes, +16 for the dword copy of the
+// to_play bytes), the path [2(S+2)] ints, rr / vin [S+2] floats (1-player
+// backup), the GW-float softmax staging slot.
+struct RsTreeLds { int tables, game, tree, path, rr, vin, stg, total; };
+__host__ __device__ __forceinline__ int rs_align16(size_t x) { return (int)((x + 15) & ~(size_t)15); }
+__host__ __device__ __forceinline__ RsTreeLds rs_tree_lds(int S, size_t tree_game_bytes, int GW) {
+    RsTreeLds L;
+    L.tables = rs_align16((size_t)16 * (S + 2));
+    L.tree = 0;
+    L.path = rs_align16(tree_game_bytes + 16);
+    L.rr = L.path + rs_align16((size_t)8 * (S + 2));
+    L.vin = L.rr + rs_align16((size_t)4 * (S + 2));
+    L.stg = L.vin + rs_align16((size_t)4 * (S + 2));
+    L.game = L.stg + rs_align16((size_t)4 * GW);
+    L.total = L.tables + (64 / GW) * L.game;
+    return L;
+}
+
 // Learner unroll with the ResNet networks (Learning.jl:347-370, Q10): per
 // tile of NG samples, representation, then K x (prediction(h), dynamics(2h ⊕
 // a/|A|)); h is handed between the nets through hs.  Raw outputs as the FC

@@ -86,20 +86,36 @@ __device__ __forceinline__ int g16_isum(int v) {
 }
 
 // GW-lane group versions: the 16-lane DPP reduction, then for GW = 32 one
-// exchange with the other row of the pair (ds_swizzle-free __shfl_xor).
+// exchange with the other row of the pair.  The row pair of a GW = 32 group (rows 0/1 or 2/3) exchanges through
+// v_permlane16_swap (gfx950, VALU): with both operands equal the two results
+// are {own row, partner row} in row order, in every lane of the pair.
+__device__ __forceinline__ void row_pair(uint32_t v, uint32_t& x, uint32_t& y) {
+    const auto s = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    x = (uint32_t)s[0]; y = (uint32_t)s[1];
+}
 template <int GW> __device__ __forceinline__ float gmax(float v) {
     v = g16_max(v);
-    if constexpr (GW == 32) { const float t = __shfl_xor(v, 16, 32); v = v > t ? v : t; }
+    if constexpr (GW == 32) {
+        uint32_t x, y;
+        row_pair(__builtin_bit_cast(uint32_t, v), x, y);
+        const float fx = __builtin_bit_cast(float, x), fy = __builtin_bit_cast(float, y);
+        v = fx > fy ? fx : fy;
+    }
     return v;
 }
 template <int GW> __device__ __forceinline__ float gmin(float v) {
     v = g16_min(v);
-    if constexpr (GW == 32) { const float t = __shfl_xor(v, 16, 32); v = v < t ? v : t; }
+    if constexpr (GW == 32) {
+        uint32_t x, y;
+        row_pair(__builtin_bit_cast(uint32_t, v), x, y);
+        const float fx = __builtin_bit_cast(float, x), fy = __builtin_bit_cast(float, y);
+        v = fx < fy ? fx : fy;
+    }
     return v;
 }
 template <int GW> __device__ __forceinline__ uint32_t gor(uint32_t v) {
     v = g16_or(v);
-    if constexpr (GW == 32) v |= (uint32_t)__shfl_xor((int)v, 16, 32);
+    if constexpr (GW == 32) { uint32_t x, y; row_pair(v, x, y); v = x | y; }
     return v;
 }
 template <int GW> __device__ __forceinline__ int gisum(int v) {
@@ -227,18 +243,20 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
     int pe = 0, pc = 0;
     SelectOut out;
     for (;;) {
+        // the parent's pUCT table entries depend only on Np: read them with the record
+        double pbn = 0.0, sqn = 0.0;
+        if constexpr (!TAB) { pbn = pbc_tab[Np]; sqn = sqrt_tab[Np]; }
         float4 ed = t.e[e * A + ac];
         // keep the whole record one load and the score branch-free: without
         // these the compiler sinks the ev load and the division into an
         // Nc > 0 branch (a second LDS round trip and two exec branches)
-        asm volatile("" : "+v"(ed.x), "+v"(ed.y), "+v"(ed.z), "+v"(ed.w));
+        asm volatile("" : "+v"(ed.x), "+v"(ed.y), "+v"(ed.z), "+v"(ed.w), "+v"(pbn), "+v"(sqn));
         const uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
         const int Nc = (int)(nc & 0xffffu);
         double pb_c;
         if constexpr (TAB) {
             pb_c = pbterm[pbterm_index(Np, Nc < Np ? Nc : Np)];
         } else {
-            const double pbn = pbc_tab[Np], sqn = sqrt_tab[Np];
             pb_c = pbn * (sqn / (double)(Nc + 1));
         }
         const double prior_score = pb_c * (double)ed.z;
@@ -248,7 +266,12 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
         const float us = (float)(prior_score + (double)vs);
         const float u = lg ? us : -INFINITY;
         float m = g16_vmax(u);
-        if constexpr (GW == 32) { const float t = __shfl_xor(m, 16, 32); m = m > t ? m : t; }
+        if constexpr (GW == 32) {
+            uint32_t x, y;
+            row_pair(__builtin_bit_cast(uint32_t, m), x, y);
+            const float fx = __builtin_bit_cast(float, x), fy = __builtin_bit_cast(float, y);
+            m = fx > fy ? fx : fy;
+        }
         const uint64_t bal = __builtin_amdgcn_ballot_w64(lg && u == m);
         const uint32_t mask = GW == 16 ? (uint32_t)(bal >> (lane & 48)) & 0xffffu : (uint32_t)(bal >> (lane & 32));
         depth += 1;
@@ -369,6 +392,66 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
     } else {
         root_N = __shfl(rN, 0, GW); root_W = __shfl(rW, 0, GW);
     }
+}
+
+// backpropagate! (SelfPlay.jl:190-217) for 1-player games, lane-parallel.
+// Without to_play resets the incoming value is the linear chain v_in(depth)
+// = leaf value, v_in(d-1) = R_d + γ·v_in(d), which the sequential loop
+// evaluates node by node.  Here the lanes first stage R_d (node d's reward)
+// in `rr`, every lane runs the same f32 chain over the staged values (two
+// ops per level, no memory on the critical path) and lane 0 stores v_in(d)
+// in `vin`; then each lane updates its own levels as the sequential loop
+// would (W + v, N + 1, q = W/N, R + γq).  Same f32 operations, same results;
+// `rr`/`vin` hold depth + 1 floats (LDS, this group's own).
+template <int GW>
+__device__ __forceinline__ void backup_path_1p(const TreeView& t, const int* path, int depth, float value,
+                                               float discount, int& root_N, float& root_W, float& mmin,
+                                               float& mmax, int a, float* rr, float* vin) {
+    for (int d = 1 + a; d <= depth; d += GW) rr[d] = t.nr[path[2 * d + 1]];
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    float v = value;
+    if (a == 0) vin[depth] = v;
+    int d = depth;
+    for (; d >= 4; d -= 4) {                         // four staged rewards per LDS wait
+        const float r0 = rr[d], r1 = rr[d - 1], r2 = rr[d - 2], r3 = rr[d - 3];
+        const float v0 = r0 + discount * v;
+        const float v1 = r1 + discount * v0;
+        const float v2 = r2 + discount * v1;
+        v = r3 + discount * v2;
+        if (a == 0) { vin[d - 1] = v0; vin[d - 2] = v1; vin[d - 3] = v2; vin[d - 4] = v; }
+    }
+    for (; d >= 1; --d) {
+        v = rr[d] + discount * v;
+        if (a == 0) vin[d - 1] = v;
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    float lmin = INFINITY, lmax = -INFINITY;
+    int rN = root_N; float rW = root_W;
+    for (int d0 = a; d0 <= depth; d0 += GW) {
+        const int i = d0 > 0 ? path[2 * d0] : 0;
+        const float4 ed = t.e[i];
+        const float vi = vin[d0];
+        uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
+        int N; float W, R;
+        if (d0 > 0) { N = (int)(nc & 0xffffu); W = ed.y; R = rr[d0]; }
+        else { N = root_N; W = root_W; R = 0.0f; }
+        W = W + vi; N += 1;
+        const float q = W / (float)N;
+        const float upd = R + discount * q;
+        lmin = lmin < upd ? lmin : upd;
+        lmax = lmax > upd ? lmax : upd;
+        if (d0 > 0) {
+            nc = (nc & 0xffff0000u) | (uint32_t)N;
+            t.nc(i) = nc; t.w(i) = W; t.ev(i) = R + discount * q;
+        } else { rN = N; rW = W; }
+    }
+    lmin = gmin<GW>(lmin);
+    lmax = gmax<GW>(lmax);
+    mmin = mmin < lmin ? mmin : lmin;
+    mmax = mmax > lmax ? mmax : lmax;
+    root_N = __shfl(rN, 0, GW); root_W = __shfl(rW, 0, GW);
 }
 
 // select_action (SelfPlay.jl:293-306): same rule as the oracle.
