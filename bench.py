@@ -229,12 +229,12 @@ def main():
 
     def lstep(k):
         if game is atari:
-            ptrs = [x.data_ptr() for x in sb]
-        else:
-            b, _ = eng.replay_sample(B, k + 1, stream=sp)
-            ptrs = [b.observation, b.actions, b.target_values, b.target_rewards, b.target_policies,
-                    b.gradient_scale]
-        eng.learner_grad_dev(ptrs, B, grad.data_ptr(), losses.data_ptr(), stream=sp)
+            eng.learner_grad_dev([x.data_ptr() for x in sb], B, grad.data_ptr(), losses.data_ptr(), stream=sp)
+        elif world == 1:                                  # get_batch + unroll, losses + ADAM: two launches
+            eng.learner_train_dev(B, k + 1, cos_schedule(k + 1), losses.data_ptr(), stream=sp)
+            return
+        else:                                             # get_batch fused into the unroll; ∇ exchanged
+            eng.learner_grad_sampled_dev(B, k + 1, grad.data_ptr(), losses.data_ptr(), stream=sp)
         if world > 1:
             dist.all_reduce(grad)
         eng.learner_apply_dev(grad.data_ptr(), 1.0 / world, cos_schedule(k + 1), stream=sp)
@@ -290,7 +290,10 @@ def main():
             "learner_steps_per_s": round(learner_sps, 1),
             "learner_config": {"batch_size": B, "num_unroll_steps": K, "mode": "ref_semantics",
                                "batch_source": "synthetic device batch" if game is atari else
-                               "mz_replay_sample (device get_batch + make_target)"},
+                               ("mz_learner_train_dev: device get_batch + make_target fused into the unroll, "
+                                "ADAM fused into the loss kernel" if world == 1 else
+                                "mz_learner_grad_sampled_dev (device get_batch fused into the unroll) + RCCL "
+                                "all-reduce + mz_learner_apply_dev")},
             "selfplay_pipeline": pipe,
             "roofline": {"bound": "mfma", "achieved": round(achieved, 4), "peak": PEAK_F32, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_F32, 5), "traffic": traffic,

@@ -269,6 +269,21 @@ int mz_replay_save_game(mz_handle* h, int32_t T, const uint8_t* obs, const int32
 int mz_replay_sample(mz_handle* h, int32_t B, uint32_t step, mz_batch* batch, int32_t* index_batch,
                      void* stream);
 
+/* One learner iteration on a batch drawn from this GPU's replay shard:
+ * get_batch (as mz_replay_sample(step)) + learning! (Learning.jl:327-404).
+ * The sampling runs inside the FC unroll kernel (its own launch otherwise).
+ * _grad_sampled_dev: results of mz_replay_sample + mz_learner_grad_dev (for
+ * a gradient exchange before mz_learner_apply_dev).  _train_dev (one GPU,
+ * world = 1): also the ADAM step with learning rate eta, fused into the loss
+ * kernel — results of the three calls with grad_scale 1.  The batch arrays
+ * are left in the handle's mz_replay_sample buffers.  Replaces, per step,
+ * the learner's fetch of the buffer + get_batch + learning! iteration
+ * (Learning.jl:329-404).                                                    */
+int mz_learner_grad_sampled_dev(mz_handle* h, int32_t B, uint32_t step, float* grad_dev,
+                                float* losses_dev, void* stream);
+int mz_learner_train_dev(mz_handle* h, int32_t B, uint32_t step, double eta, float* losses_dev,
+                         void* stream);
+
 /* Debug/parity: game i of the shard (0 = oldest held), buffers sized for
  * max_moves + 1 moves (layouts as mz_replay_save_game); any pointer may be
  * NULL.  And the slots' games in progress: moves recorded, boards (G, W*H*C)

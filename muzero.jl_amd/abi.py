@@ -62,6 +62,8 @@ SIGNATURES = {
     "mz_replay_counts": (ctypes.c_int, [_VP, _VP, _VP]),
     "mz_replay_save_game": (ctypes.c_int, [_VP, ctypes.c_int32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "mz_replay_sample": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.POINTER(MzBatch), _VP, _VP]),
+    "mz_learner_grad_sampled_dev": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, _VP, _VP, _VP]),
+    "mz_learner_train_dev": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.c_double, _VP, _VP]),
     "mz_replay_get_game": (ctypes.c_int, [_VP, ctypes.c_int32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "mz_selfplay_slots": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
     "mz_checkpoint_save": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int64]),
@@ -325,6 +327,16 @@ class Engine:
         self._check(self.lib.mz_replay_sample(self.h, B, step, ctypes.byref(b), _p(idx) if index else None, stream),
                     "mz_replay_sample")
         return b, idx
+
+    def learner_grad_sampled_dev(self, B, step, grad_ptr, losses_ptr=None, stream=None):
+        """replay_sample(B, step) + learner_grad_dev, the sampling fused into the unroll kernel."""
+        self._check(self.lib.mz_learner_grad_sampled_dev(self.h, B, step, grad_ptr, losses_ptr, stream),
+                    "mz_learner_grad_sampled_dev")
+
+    def learner_train_dev(self, B, step, eta, losses_ptr=None, stream=None):
+        """One GPU: replay_sample + learner_grad_dev + learner_apply_dev(scale 1) in two launches."""
+        self._check(self.lib.mz_learner_train_dev(self.h, B, step, float(eta), losses_ptr, stream),
+                    "mz_learner_train_dev")
 
     def batch_to_host(self, b):
         """Copy a device MzBatch (from replay_sample) into the host dict layout of ReplayBuffer.get_batch."""

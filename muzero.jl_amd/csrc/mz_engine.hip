@@ -54,15 +54,14 @@ extern "C" __global__ void mz_forward_kernel(const int* plan, const float* Wp, c
                                              int in_off, int in_feat, const float* x, int n, int out0_off, int o0,
                                              float* out0, int out1_off, int o1, float* out1, int sm1, int act0,
                                              int act1);
-#define MZ_L2_BLOCKS 32
 extern "C" __global__ void mz_learner_grad_kernel(int B, int K, int A, int v_act, int r_act, float* pv, float* pp,
                                                   float* pr, const float* tv, const float* tp, const float* gscale,
-                                                  float* terms, const float* flat, const size_t* netoff, float* G,
-                                                  double* part, unsigned* counter, float* out);
+                                                  float* terms, float* flat, const size_t* netoff, float* G,
+                                                  double* part, unsigned* counter, float* out, LgAdam ad);
 extern "C" __global__ void mz_learner_grad_kernel32(int B, int K, int A, int v_act, int r_act, float* pv, float* pp,
                                                     float* pr, const float* tv, const float* tp, const float* gscale,
-                                                    float* terms, const float* flat, const size_t* netoff, float* G,
-                                                    double* part, unsigned* counter, float* out);
+                                                    float* terms, float* flat, const size_t* netoff, float* G,
+                                                    double* part, unsigned* counter, float* out, LgAdam ad);
 extern "C" __global__ void mz_adam_kernel(float* P, float* M, float* V, const float* G, float gscale, size_t n,
                                           double bp1, double bp2, double eta, float* Wp, float* Bp,
                                           const int* inv_tile, float* smw, float* smb, const int* inv_small);
@@ -1499,7 +1498,7 @@ static size_t runroll_lds(const mz_handle* h) {
 }
 
 static int learner_losses(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, hipStream_t st,
-                          int v_act, int r_act);
+                          int v_act, int r_act, bool fuse_adam = false, double eta = 0.0);
 
 // ResNet learner: the unroll on the network kernels, then the shared loss /
 // ∇ = 2θ kernel (the plans' outputs are already activated)
@@ -1523,14 +1522,24 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
     return learner_losses(h, b, grad_dev, losses_dev, st, MZ_ACT_IDENTITY, MZ_ACT_IDENTITY);
 }
 
+static int fc_unroll(mz_handle* h, const mz_batch* b, hipStream_t st, const RpSampleParams* rp);
+
 // forward unroll + losses + ∇ = 2θ into grad_dev (device batch pointers)
 int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, void* stream) {
     if (!h || !b) return -2;
     if (h->kind == 1) return rlearner_grad(h, b, grad_dev, losses_dev, stream);
-    const int B = b->batch_size, K = h->conf.num_unroll_steps, A = h->A;
-    if (B < 1) return fail(h, "batch_size must be >= 1");
-    if (ensure_batch(h, B)) return -1;
+    if (b->batch_size < 1) return fail(h, "batch_size must be >= 1");
+    if (ensure_batch(h, b->batch_size)) return -1;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    if (fc_unroll(h, b, st, nullptr)) return -1;
+    return learner_losses(h, b, grad_dev, losses_dev, st, h->lay.v_act, h->lay.r_act);
+}
+
+// FC learner unroll of batch b (Learning.jl:327-343); rp != nullptr: the
+// batch is drawn from the replay shard by get_batch (mz_rp_sample's body),
+// inside the small unroll kernel when it applies, else by its own launch
+static int fc_unroll(mz_handle* h, const mz_batch* b, hipStream_t st, const RpSampleParams* rp) {
+    const int B = b->batch_size, K = h->conf.num_unroll_steps, A = h->A;
     const int ti_u = B <= 4 * h->n_cu ? 0 : 1;
     // one item per thread in the unroll's per-step loops; a/|A| staging of 64 floats
     const bool small_unroll = h->small_ok && (ti_u + 1) * h->H <= 256 && (ti_u + 1) * h->plane <= 256 &&
@@ -1553,10 +1562,16 @@ int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float*
         if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * std::max(h->max_games, B)));
         U.stamps = h->d_stamps;
 #endif
+        U.sample = rp != nullptr;
+        if (rp) U.rp = *rp; else std::memset(&U.rp, 0, sizeof(U.rp));
         void* args[] = {&U};
         MZ_TRY(h, hipLaunchKernel(ti == 0 ? (const void*)mz_unroll_small1 : (const void*)mz_unroll_small2,
                                   dim3((B + T - 1) / T), dim3(SM_THREADS), args, unroll_small_lds(h, ti), st));
     } else {
+        if (rp) {
+            hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, *rp);
+            MZ_TRY(h, hipGetLastError());
+        }
         UnrollParams U;
         U.B = B; U.K = K; U.A = A; U.H = h->H; U.plane = h->plane; U.obs_feat = h->obs_feat;
         U.obs = b->observation; U.actions = b->actions; U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
@@ -1564,21 +1579,36 @@ int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float*
         hipLaunchKernelGGL(mz_unroll_kernel, dim3((B + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
                            (size_t)h->lay.total * 4, st, U);
     }
-    return learner_losses(h, b, grad_dev, losses_dev, st, h->lay.v_act, h->lay.r_act);
+    MZ_TRY(h, hipGetLastError());
+    return 0;
 }
 
-// losses + ∇ = 2θ from the unroll outputs in d_pv / d_pp / d_pr
+static LgAdam adam_args(mz_handle* h, int on, double eta) {
+    return LgAdam{on, h->d_m, h->d_v, h->bp1, h->bp2, eta, h->d_Wp, h->d_Bp, h->d_inv_tile, h->d_sm_w,
+                  h->d_sm_bias, h->d_inv_small};
+}
+// after an ADAM update: βp .= βp .* β
+static void adam_advance(mz_handle* h) {
+    h->bp1 = h->bp1 * 0.9;
+    h->bp2 = h->bp2 * 0.999;
+}
+
+// losses + ∇ = 2θ from the unroll outputs in d_pv / d_pp / d_pr; with
+// fuse_adam (world = 1) the ∇ is not stored: each parameter slice's block
+// applies the ADAM update (learning rate eta) right after reading θ for Σθ²
 static int learner_losses(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, hipStream_t st,
-                          int v_act, int r_act) {
+                          int v_act, int r_act, bool fuse_adam, double eta) {
     const int B = b->batch_size, K = h->conf.num_unroll_steps, A = h->A;
     float* lo = losses_dev ? losses_dev : h->d_loss;
     float* g = grad_dev ? grad_dev : h->d_grad;
     const int gw = A > 16 ? 32 : 16;            // lanes per (sample, step) group
     const int nlb = (B * (K + 1) + MZ_THREADS / gw - 1) / (MZ_THREADS / gw);
+    const LgAdam ad = adam_args(h, fuse_adam ? 1 : 0, eta);
     hipLaunchKernelGGL(gw == 32 ? mz_learner_grad_kernel32 : mz_learner_grad_kernel, dim3(nlb + 3 * MZ_L2_BLOCKS), dim3(MZ_THREADS), 0, st, B, K, A,
                        v_act, r_act, h->d_pv, h->d_pp, h->d_pr, b->target_values, b->target_policies,
-                       b->gradient_scale, h->d_lterm, h->d_flat, h->d_netoff, g, h->d_sq, h->d_counter, lo);
+                       b->gradient_scale, h->d_lterm, h->d_flat, h->d_netoff, g, h->d_sq, h->d_counter, lo, ad);
     MZ_TRY(h, hipGetLastError());
+    if (fuse_adam) adam_advance(h);
     return 0;
 }
 
@@ -1589,8 +1619,7 @@ int mz_learner_apply_dev(mz_handle* h, const float* grad_dev, float grad_scale, 
     hipLaunchKernelGGL(mz_adam_kernel, dim3(128), dim3(MZ_THREADS), 0, st, h->d_flat, h->d_m, h->d_v, g,
                        grad_scale, h->nflat, h->bp1, h->bp2, eta, h->d_Wp, h->d_Bp, h->d_inv_tile, h->d_sm_w,
                        h->d_sm_bias, h->d_inv_small);
-    h->bp1 = h->bp1 * 0.9;                  // βp .= βp .* β
-    h->bp2 = h->bp2 * 0.999;
+    adam_advance(h);
     MZ_TRY(h, hipGetLastError());
     return 0;
 }
@@ -1922,12 +1951,11 @@ int mz_replay_save_game(mz_handle* h, int32_t T, const uint8_t* obs, const int32
     return 0;
 }
 
-int mz_replay_sample(mz_handle* h, int32_t B, uint32_t step, mz_batch* batch, int32_t* index_batch, void* stream) {
-    if (!h || !batch) return -2;
+// get_batch parameters for B samples at learner step `step` into the
+// engine's batch arrays (allocated on first use); batch = those arrays
+static int rs_params(mz_handle* h, int32_t B, uint32_t step, hipStream_t st, RpSampleParams* Qo, mz_batch* batch) {
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
     if (B < 1) return fail(h, "batch_size must be >= 1");
-    MZ_TRY(h, hipSetDevice(h->device));
-    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     if (!h->sp_has_games) {                       // sample_n_games needs a non-empty buffer
         long long played = 0;
         MZ_TRY(h, hipStreamSynchronize(st));
@@ -1953,16 +1981,61 @@ int mz_replay_sample(mz_handle* h, int32_t B, uint32_t step, mz_batch* batch, in
     Q.seed = h->seed; Q.step = step; Q.ring = h->sp_ring; Q.counters = h->d_sp_counters; Q.disc_pow = h->d_sp_dpow;
     Q.obs = h->d_rs_obs; Q.actions = h->d_rs_act; Q.tv = h->d_rs_tv; Q.tr = h->d_rs_tr; Q.tpol = h->d_rs_tp;
     Q.gscale = h->d_rs_gs; Q.index = h->d_rs_index;
-    hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, Q);
-    MZ_TRY(h, hipGetLastError());
+    *Qo = Q;
     batch->batch_size = B;
     batch->observation = h->d_rs_obs; batch->actions = h->d_rs_act; batch->target_values = h->d_rs_tv;
     batch->target_rewards = h->d_rs_tr; batch->target_policies = h->d_rs_tp; batch->gradient_scale = h->d_rs_gs;
+    return 0;
+}
+
+int mz_replay_sample(mz_handle* h, int32_t B, uint32_t step, mz_batch* batch, int32_t* index_batch, void* stream) {
+    if (!h || !batch) return -2;
+    MZ_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    RpSampleParams Q;
+    if (rs_params(h, B, step, st, &Q, batch)) return -1;
+    hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, Q);
+    MZ_TRY(h, hipGetLastError());
     if (index_batch) {
         MZ_TRY(h, hipMemcpyAsync(index_batch, h->d_rs_index, (size_t)B * 8, hipMemcpyDeviceToHost, st));
         MZ_TRY(h, hipStreamSynchronize(st));
     }
     return 0;
+}
+
+// Learner iteration on a batch drawn from this GPU's replay shard
+// (get_batch + learning!, ReplayBuffer.jl:188-217, Learning.jl:327-404) with
+// the sampling fused into the FC unroll kernel: results are those of
+// mz_replay_sample(step) + mz_learner_grad_dev (+ mz_learner_apply_dev with
+// grad_scale 1 for mz_learner_train_dev, whose ADAM update is fused into the
+// loss kernel: one GPU, no gradient exchange).
+static int learner_sampled(mz_handle* h, int32_t B, uint32_t step, float* grad_dev, float* losses_dev,
+                           hipStream_t st, bool train, double eta) {
+    MZ_TRY(h, hipSetDevice(h->device));
+    RpSampleParams Q;
+    mz_batch b;
+    if (rs_params(h, B, step, st, &Q, &b)) return -1;
+    if (ensure_batch(h, B)) return -1;
+    if (h->kind == 1) {                             // ResNet: sample, then the network unroll
+        hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, Q);
+        MZ_TRY(h, hipGetLastError());
+        if (!train) return rlearner_grad(h, &b, grad_dev, losses_dev, st);
+        if (rlearner_grad(h, &b, nullptr, losses_dev, st)) return -1;
+        return mz_learner_apply_dev(h, nullptr, 1.0f, eta, st);
+    }
+    if (fc_unroll(h, &b, st, &Q)) return -1;
+    return learner_losses(h, &b, grad_dev, losses_dev, st, h->lay.v_act, h->lay.r_act, train, eta);
+}
+
+int mz_learner_grad_sampled_dev(mz_handle* h, int32_t B, uint32_t step, float* grad_dev, float* losses_dev,
+                                void* stream) {
+    if (!h) return -2;
+    return learner_sampled(h, B, step, grad_dev, losses_dev, stream ? (hipStream_t)stream : h->stream, false, 0.0);
+}
+
+int mz_learner_train_dev(mz_handle* h, int32_t B, uint32_t step, double eta, float* losses_dev, void* stream) {
+    if (!h) return -2;
+    return learner_sampled(h, B, step, nullptr, losses_dev, stream ? (hipStream_t)stream : h->stream, true, eta);
 }
 
 int mz_replay_get_game(mz_handle* h, int32_t i, int32_t* T, uint8_t* obs, int32_t* actions, float* rewards,

@@ -18,6 +18,7 @@
 
 #define MZ_TILE 16          // games (or samples) per workgroup tile = MFMA N
 #define MZ_THREADS 256      // 4 wavefronts
+#define MZ_L2_BLOCKS 32     // Σθ² / ∇ (/ fused ADAM) blocks per net in mz_learner_grad_kernel*
 #define MZ_MAX_STAGES 64
 
 // One Dense layer inside a plan.  All offsets are in floats.
@@ -103,6 +104,15 @@ struct UnrollParams {
     const float* Wp; const float* Bp;
     const int* plan_repr; const int* plan_sim;
     ActLayout lay;
+};
+
+// ADAM state and image scatter maps for mz_adam_kernel / the fused update of
+// mz_learner_grad_kernel* (on = 1: update in place with G = 2θ, world = 1).
+struct LgAdam {
+    int on;
+    float* M; float* V;
+    double bp1, bp2, eta;
+    float* Wp; float* Bp; const int* inv_tile; float* smw; float* smb; const int* inv_small;
 };
 
 __host__ __device__ inline int mz_round16(int x) { return (x + 15) & ~15; }

@@ -107,15 +107,67 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_unroll_kernel(Unroll
 //    and ∇ = 2θ written for it (Q11: only sum(sqnorm, params) depends on θ);
 //  * the last block to finish folds each sample's steps in ascending k, the
 //    cross-sample sums in f64 (tolerance-checked, not bitwise), and the Σθ²
-//    partials in ascending order, then resets the counter.
+//    partials in a fixed order (one wave per net), then resets the counter.
 // out: [0] value, [1] reward (0, intermediate_rewards = false), [2] policy,
 // [3..5] Σθ² of repr / pred / dyn.
-#define MZ_L2_BLOCKS 32
+
+// Flux 0.12 apply!(ADAM) + WeightDecay(0) + `x .-= Δ` (Learning.jl:395-397)
+// for parameter i with gradient g.  bp = (β1^t, β2^t) of the current step.
+// The new value is also scattered into the search / unroll images through
+// the inverse maps (each parameter has one position in each image), so the
+// images never need a repack after a learner step.
+__device__ __forceinline__ void mz_scatter(float x, int code, float* w, float* b) {
+    if (code >= 0) w[code] = x;
+    else if (code <= -2) b[-code - 2] = x;
+}
+// adam_update of P[i0 + u·stride] (u < 4, u·stride < rem) with g = 2·x[u]
+// (x[u] = the current value): all loads first, then the four updates
+__device__ __forceinline__ void adam_update4(const LgAdam& ad, float* P, size_t i0, size_t stride, size_t rem,
+                                             const float (&x)[4]) {
+    const double b1 = 0.9, b2 = 0.999, eps = 1e-8;
+    float mo[4], vo[4];
+    int it[4], is[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const size_t i = i0 + u * stride;
+        const bool in = u * stride < rem;
+        mo[u] = in ? ad.M[i] : 0.0f; vo[u] = in ? ad.V[i] : 0.0f;
+        it[u] = in ? ad.inv_tile[i] : -1; is[u] = in ? ad.inv_small[i] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        if (u * stride >= rem) continue;
+        const size_t i = i0 + u * stride;
+        const float g = x[u] * 2.0f;
+        const float m = (float)(b1 * (double)mo[u] + (1.0 - b1) * (double)g);
+        const float g2 = g * g;
+        const float v = (float)(b2 * (double)vo[u] + (1.0 - b2) * (double)g2);
+        ad.M[i] = m; ad.V[i] = v;
+        const float d = (float)((double)m / (1.0 - ad.bp1) / (sqrt((double)v / (1.0 - ad.bp2)) + eps) * ad.eta);
+        const float xn = x[u] - d;
+        P[i] = xn;
+        mz_scatter(xn, it[u], ad.Wp, ad.Bp);
+        mz_scatter(xn, is[u], ad.smw, ad.smb);
+    }
+}
+__device__ __forceinline__ void adam_update(const LgAdam& ad, float* P, size_t i, float g) {
+    const double b1 = 0.9, b2 = 0.999, eps = 1e-8;
+    const float m = (float)(b1 * (double)ad.M[i] + (1.0 - b1) * (double)g);
+    const float g2 = g * g;
+    const float v = (float)(b2 * (double)ad.V[i] + (1.0 - b2) * (double)g2);
+    ad.M[i] = m; ad.V[i] = v;
+    const float d = (float)((double)m / (1.0 - ad.bp1) / (sqrt((double)v / (1.0 - ad.bp2)) + eps) * ad.eta);
+    const float x = P[i] - d;
+    P[i] = x;
+    mz_scatter(x, ad.inv_tile[i], ad.Wp, ad.Bp);
+    mz_scatter(x, ad.inv_small[i], ad.smw, ad.smb);
+}
+#define MZ_FOLD_K1 8    // K + 1 up to this: the fold stages the step terms in LDS
 template <int GW>
 __device__ __forceinline__ void learner_grad_body(
     int B, int K, int A, int v_act, int r_act, float* pv, float* pp, float* pr, const float* tv, const float* tp,
-    const float* gscale, float* terms, const float* flat, const size_t* netoff, float* G, double* part,
-    unsigned* counter, float* out) {
+    const float* gscale, float* terms, float* flat, const size_t* netoff, float* G, double* part,
+    unsigned* counter, float* out, LgAdam ad) {
     __shared__ double red_v[MZ_THREADS], red_p[MZ_THREADS], red_c[MZ_THREADS];
     __shared__ float stg[MZ_THREADS];
     __shared__ bool last;
@@ -156,10 +208,24 @@ __device__ __forceinline__ void learner_grad_body(
         const int net = nb / MZ_L2_BLOCKS, blk = nb % MZ_L2_BLOCKS;
         const size_t off = netoff[net], cnt = netoff[3 + net];
         double s = 0.0;
-        for (size_t i = (size_t)blk * blockDim.x + tid; i < cnt; i += (size_t)MZ_L2_BLOCKS * blockDim.x) {
-            const float x = flat[off + i];
-            s += (double)x * (double)x;
-            G[off + i] = x * 2.0f;
+        // elements i, i + stride, ... as one thread's ascending f64 sum; four per
+        // pass with every load issued before any store (the fused ADAM's f64
+        // chains then overlap)
+        const size_t stride = (size_t)MZ_L2_BLOCKS * blockDim.x;
+        for (size_t i = (size_t)blk * blockDim.x + tid; i < cnt; i += 4 * stride) {
+            float x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = i + u * stride < cnt ? flat[off + i + u * stride] : 0.0f;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + u * stride < cnt) s += (double)x[u] * (double)x[u];
+            if (ad.on) {                        // = mz_adam_kernel with G = 2θ, gscale 1
+                adam_update4(ad, flat, off + i, stride, cnt - i, x);
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (i + u * stride < cnt) G[off + i + u * stride] = x[u] * 2.0f;
+            }
         }
         red_v[tid] = s;
         __syncthreads();
@@ -179,15 +245,40 @@ __device__ __forceinline__ void learner_grad_body(
     if (!last) return;
     __threadfence();
     double sv = 0.0, sg = 0.0, sc = 0.0;
-    for (int j = tid; j < B; j += blockDim.x) {
-        float s = 0.0f, c = 0.0f;
-        for (int k = 0; k <= K; ++k) {
-            s = s + __hip_atomic_load(vsq + (size_t)j * (K + 1) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            c = c + (-__hip_atomic_load(cet + (size_t)j * (K + 1) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    // per sample j (thread j mod blockDim): its K+1 steps in ascending k.  The
+    // terms of blockDim samples at a time are first staged in LDS by all
+    // threads (one load each, all in flight), so no thread walks a chain of
+    // dependent global loads
+    __shared__ float fv[MZ_THREADS * MZ_FOLD_K1], fc[MZ_THREADS * MZ_FOLD_K1];
+    const int K1 = K + 1;
+    for (int j0 = 0; j0 < B; j0 += blockDim.x) {
+        const int nj = B - j0 < (int)blockDim.x ? B - j0 : (int)blockDim.x;
+        const bool staged = K1 <= MZ_FOLD_K1;
+        if (staged) {
+            for (int e = tid; e < nj * K1; e += blockDim.x) {
+                fv[e] = __hip_atomic_load(vsq + (size_t)j0 * K1 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                fc[e] = __hip_atomic_load(cet + (size_t)j0 * K1 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
         }
-        sv += (double)(s / gscale[j]);
-        sc += (double)c;                        // Σ_k ce_k
-        sg += 1.0 / (double)gscale[j];          // Σ_j 1/g_j
+        if (tid < nj) {
+            const int j = j0 + tid;
+            float s = 0.0f, c = 0.0f;
+            for (int k = 0; k < K1; ++k) {
+                const float vk = staged ? fv[tid * K1 + k]
+                                        : __hip_atomic_load(vsq + (size_t)j * K1 + k, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+                const float ck = staged ? fc[tid * K1 + k]
+                                        : __hip_atomic_load(cet + (size_t)j * K1 + k, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+                s = s + vk;
+                c = c + (-ck);
+            }
+            sv += (double)(s / gscale[j]);
+            sc += (double)c;                    // Σ_k ce_k
+            sg += 1.0 / (double)gscale[j];      // Σ_j 1/g_j
+        }
+        if (staged) __syncthreads();
     }
     red_v[tid] = sv; red_p[tid] = sg; red_c[tid] = sc;
     __syncthreads();
@@ -201,17 +292,19 @@ __device__ __forceinline__ void learner_grad_body(
         out[2] = (float)(red_c[0] * red_p[0] / ((double)B * (double)B));  // mean over (1,B,B), Q11
         *counter = 0u;
     }
-    if (tid < 3) {
+    if (tid < 192) {                            // wave w folds net w's partials: fixed pairs, then a fixed tree
+        const int net = tid >> 6, j = tid & 63;
         double s = 0.0;
-        for (int b = 0; b < MZ_L2_BLOCKS; ++b)
-            s += __hip_atomic_load(part + tid * MZ_L2_BLOCKS + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        out[3 + tid] = (float)s;
+        for (int b = j; b < MZ_L2_BLOCKS; b += 64)
+            s += __hip_atomic_load(part + net * MZ_L2_BLOCKS + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+        if (j == 0) out[3 + net] = (float)s;
     }
 }
 #define MZ_LG_ARGS int B, int K, int A, int v_act, int r_act, float* pv, float* pp, float* pr, const float* tv, \
-    const float* tp, const float* gscale, float* terms, const float* flat, const size_t* netoff, float* G, \
-    double* part, unsigned* counter, float* out
-#define MZ_LG_CALL B, K, A, v_act, r_act, pv, pp, pr, tv, tp, gscale, terms, flat, netoff, G, part, counter, out
+    const float* tp, const float* gscale, float* terms, float* flat, const size_t* netoff, float* G, \
+    double* part, unsigned* counter, float* out, LgAdam ad
+#define MZ_LG_CALL B, K, A, v_act, r_act, pv, pp, pr, tv, tp, gscale, terms, flat, netoff, G, part, counter, out, ad
 extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_grad_kernel(MZ_LG_ARGS) {
     learner_grad_body<16>(MZ_LG_CALL);
 }
@@ -219,33 +312,14 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_grad_kernel3
     learner_grad_body<32>(MZ_LG_CALL);
 }
 
-// Flux 0.12 apply!(ADAM) + WeightDecay(0) + `x .-= Δ` (Learning.jl:395-397).
-// grad = G[i] * gscale (gscale = 1/world after an all-reduce sum; exact for
-// power-of-two world sizes).  bp = (β1^t, β2^t) of the current step.  The
-// new value is also scattered into the search / unroll images through the
-// inverse maps (each parameter has one position in each image), so the
-// images never need a repack after a learner step.
-__device__ __forceinline__ void mz_scatter(float x, int code, float* w, float* b) {
-    if (code >= 0) w[code] = x;
-    else if (code <= -2) b[-code - 2] = x;
-}
-
+// ADAM over all parameters (adam_update): grad = G[i] * gscale (gscale =
+// 1/world after an all-reduce sum; exact for power-of-two world sizes).
 extern "C" __global__ void mz_adam_kernel(float* P, float* M, float* V, const float* G, float gscale,
                                           size_t n, double bp1, double bp2, double eta, float* Wp, float* Bp,
                                           const int* inv_tile, float* smw, float* smb, const int* inv_small) {
-    const double b1 = 0.9, b2 = 0.999, eps = 1e-8;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        const float g = G[i] * gscale;
-        const float m = (float)(b1 * (double)M[i] + (1.0 - b1) * (double)g);
-        const float g2 = g * g;
-        const float v = (float)(b2 * (double)V[i] + (1.0 - b2) * (double)g2);
-        M[i] = m; V[i] = v;
-        const float d = (float)((double)m / (1.0 - bp1) / (sqrt((double)v / (1.0 - bp2)) + eps) * eta);
-        const float x = P[i] - d;
-        P[i] = x;
-        mz_scatter(x, inv_tile[i], Wp, Bp);
-        mz_scatter(x, inv_small[i], smw, smb);
-    }
+    const LgAdam ad{1, M, V, bp1, bp2, eta, Wp, Bp, inv_tile, smw, smb, inv_small};
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        adam_update(ad, P, i, G[i] * gscale);
 }
 
 // Rebuild the MFMA weight image from the Flux-order flat parameters:

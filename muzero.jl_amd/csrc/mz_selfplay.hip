@@ -13,6 +13,7 @@
 // muzero.jl_amd/games/{tictactoe,connect4}.py, selfplay.py, replay_buffer.py.
 #include "mz_internal.h"
 #include "mz_selfplay_params.h"
+#include "mz_replay_device.h"
 
 // ------------------------------------------------------------------- envs
 __constant__ int8_t c_ttt_lines[8][3] = {{0, 3, 6}, {1, 4, 7}, {2, 5, 8}, {0, 1, 2},
@@ -96,26 +97,6 @@ __device__ void env_reset(const SpParams& S, int g, int lane) {
     const int cells = S.osz / 3;
     for (int k = lane; k < S.osz; k += 64) b[k] = k >= 2 * cells;
     if (lane == 0) { S.player[g] = 1; S.over[g] = 0; }
-}
-
-// get_stacked_observations (SelfPlay.jl:128-149, Q15) of record `obs`/`act`
-// at 1-based index (cur = observation `index`): [obs_t, (action plane = raw
-// id, obs_{t-1}) ...], zeros before the first move
-__device__ __forceinline__ void stacked_obs(float* out, const uint8_t* cur, const uint8_t* obs, const int32_t* act,
-                                            int index, int osz, int P, int stacked, int lane) {
-    for (int k = lane; k < osz; k += 64) out[k] = (float)cur[k];
-    int o = osz;
-    for (int past = index - 1; past >= index - stacked; --past) {
-        if (past >= 1) {
-            const float av = (float)act[past - 1];
-            for (int k = lane; k < P; k += 64) out[o + k] = av;
-            const uint8_t* po = obs + (size_t)(past - 1) * osz;
-            for (int k = lane; k < osz; k += 64) out[o + P + k] = (float)po[k];
-        } else {
-            for (int k = lane; k < P + osz; k += 64) out[o + k] = 0.0f;
-        }
-        o += P + osz;
-    }
 }
 
 // ------------------------------------------------------------ self-play move
@@ -220,69 +201,9 @@ extern "C" __global__ __launch_bounds__(256) void mz_sp_store(SpParams S) {
 }
 
 // ------------------------------------------------------------- replay sample
-// compute_target_value (ReplayBuffer.jl:5-20, Q9), f32, 1-based index
-__device__ float rp_target_value(const RpSampleParams& Q, const float* rv, const int32_t* tp, const float* rew, int T,
-                                 int index) {
-    const int bi = index + Q.td;
-    if (bi >= T) return 0.0f;
-    const float r0 = rv[bi - 1];
-    const float last = tp[bi - 1] == tp[index - 1] ? r0 : -r0;
-    float value = last * Q.disc_pow[Q.td];
-    for (int i = 1; i <= Q.td + 1; ++i) {
-        const float r = rew[index + i - 2];
-        const float sr = tp[index - 1] == tp[index + i - 1] ? r : -r;
-        value = value + sr * Q.disc_pow[i];
-    }
-    return value;
-}
-
-// one wave per sample (get_batch, :188-217)
+// one wave per sample (get_batch, :188-217); the body is shared with the
+// fused sample + unroll kernel (mz_replay_device.h)
 extern "C" __global__ __launch_bounds__(256) void mz_rp_sample(RpSampleParams Q) {
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (b >= Q.B) return;
-    const long long played = Q.counters[0];
-    const int n = (int)(played < Q.cap ? played : Q.cap);
-    const long long oldest = played - n + 1;                       // game number of ids[0]
-    const uint32_t gi = mz_rng_below(mz_rng_u32(Q.seed, MZ_RNG_GAME, (uint32_t)b, Q.step, 0), (uint32_t)n);   // :102
-    const long long num = oldest + gi;
-    const int slot = (int)((num - 1) % Q.cap);
-    const size_t base = (size_t)slot * Q.T;
-    const int T = Q.ring.len[slot];
-    const int pos = (int)mz_rng_below(mz_rng_u32(Q.seed, MZ_RNG_POS, (uint32_t)b, Q.step, 0), (uint32_t)T) + 1;  // :80
-    const int K1 = Q.K + 1, A = Q.A;
-    const float* rv = Q.ring.rv + base;
-    const int32_t* tp = Q.ring.tp + base;
-    const float* rew = Q.ring.rew + base;
-    const int32_t* act = Q.ring.act + base;
-    const float* cv = Q.ring.cv + base * A;
-    const float uni = 1.0f / (float)A;
-    for (int k = lane; k < K1; k += 64) {                          // make_target (:25-50)
-        const int ci = pos + k;
-        float v = 0.0f, r = 0.0f, a;
-        if (ci < T) {
-            v = rp_target_value(Q, rv, tp, rew, T, ci);
-            r = rew[ci - 1];
-            a = (float)act[ci - 1];
-        } else if (ci == T) {
-            r = rew[ci - 1];
-            a = (float)act[ci - 1];
-        } else {                                                   // absorbing states
-            a = (float)(mz_rng_below(mz_rng_u32(Q.seed, MZ_RNG_ABSORB, (uint32_t)b, Q.step, (uint32_t)k), (uint32_t)A) + 1);
-        }
-        Q.tv[(size_t)b * K1 + k] = v;
-        Q.tr[(size_t)b * K1 + k] = r;
-        Q.actions[(size_t)b * K1 + k] = a;
-    }
-    for (int e = lane; e < K1 * A; e += 64) {
-        const int k = e / A, a = e - k * A, ci = pos + k;
-        Q.tpol[(size_t)b * K1 * A + e] = ci < T ? cv[(size_t)(ci - 1) * A + a] : uni;
-    }
-    stacked_obs(Q.obs + (size_t)b * Q.F, Q.ring.obs + (base + pos - 1) * Q.osz, Q.ring.obs + base * Q.osz, act, pos,
-                Q.osz, Q.P, Q.stacked, lane);
-    if (lane == 0) {
-        const int gs = T + 1 - pos;                                // :212 min(K, len(action_history)+1-pos)
-        Q.gscale[b] = (float)(Q.K < gs ? Q.K : gs);
-        Q.index[2 * b] = (int)num;
-        Q.index[2 * b + 1] = pos;
-    }
+    if (b < Q.B) rp_sample_one(Q, b, lane);
 }

@@ -22,6 +22,7 @@
 #include "mz_tree_device.h"
 
 #include "mz_small_params.h"
+#include "mz_replay_device.h"
 
 #ifdef MZ_STAMPS
 #define SM_STAMP(i)                                                              \
@@ -416,6 +417,8 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
     float wr[SM_MAX_SIM][16];
     sm_load<SM_MAX_SIM>(0, P.n_root, P.w_root, wr);
     sm_load<SM_MAX_SIM>(P.n_root, P.n_sim, P.w_sim, wr);   // sim stages the representation leaves free
+    if (P.sample && (tid >> 6) < T && tile0 + (tid >> 6) < P.B)   // get_batch of this tile's samples
+        rp_sample_one(P.rp, tile0 + (tid >> 6), tid & 63);
     for (int i = tid; i < P.act_total; i += SM_THREADS) act[i] = 0.0f;
     for (int i = tid; i < nrec * SM_REC_INTS; i += SM_THREADS) rec[i] = P.rec[i];
     __syncthreads();

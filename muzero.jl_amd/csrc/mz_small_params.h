@@ -2,6 +2,7 @@
 // kernel (mz_small.hip), shared with the host schedule builder.
 #pragma once
 #include "mz_internal.h"
+#include "mz_selfplay_params.h"
 
 #define SM_THREADS 512
 #define SM_SLOTS 2
@@ -55,5 +56,10 @@ struct SmallUnrollParams {
     int x_rep, x_pred, x_dyn, h_out, v_out, p_out, r_out;
     int v_act, r_act;
     unsigned long long* stamps;   // -DMZ_STAMPS builds: [blocks][8] phase ticks (else unused)
+    // fused get_batch (mz_learner_*_sampled): wave w < T of the workgroup first
+    // draws sample tile0 + w from the replay shard into rp's batch arrays (obs
+    // and actions are the arrays above), under the weight-image loads
+    int sample;
+    RpSampleParams rp;
 };
 

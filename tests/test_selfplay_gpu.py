@@ -146,3 +146,48 @@ def test_selfplay_rejects_bad_setup(ttt):
     with pytest.raises(MzError, match="empty"):
         e.replay_sample(4, 1)
     e.close()
+
+
+def _device_pair(kind, G, moves, cap, resnet=False):
+    """Two engines with the same weights whose device self-play fills
+    identical replay shards."""
+    mod, _, env_kind = _env(kind)
+    conf = dataclasses.replace(mod.conf, num_iters=6, replay_buffer_size=cap)
+    e1, e2 = _engines(mod, conf, mod.resnet_hyper if resnet else mod.hyper, G)
+    for e in (e1, e2):
+        e.selfplay_init(env_kind, G, cap)
+        for m in range(moves):
+            e.selfplay_move(100 + m, game_offset=7)
+    return e1, e2
+
+
+@pytest.mark.parametrize("kind,resnet,B", [("ttt", False, 32), ("ttt", False, 40), ("c4", False, 24),
+                                           ("ttt", False, 1100), ("ttt", True, 32)])
+def test_fused_learner_matches_separate_calls(kind, resnet, B):
+    """mz_learner_train_dev (sampling fused into the unroll, ADAM into the loss
+    kernel) and mz_learner_grad_sampled_dev + apply == mz_replay_sample +
+    mz_learner_grad_dev + mz_learner_apply_dev, bit for bit: losses, weights."""
+    import torch
+    from muzero_jl_amd.config import cos_schedule
+    e1, e2 = _device_pair(kind, 16, 14 if kind == "ttt" else 30, cap=64, resnet=resnet)
+    assert e1.replay_counts()[0][0] > 0
+    grad = torch.empty(e1.grad_count(), dtype=torch.float32, device="cuda")
+    l1 = torch.empty(8, dtype=torch.float32, device="cuda")
+    l2 = torch.empty(8, dtype=torch.float32, device="cuda")
+    for step in (1, 2, 3, 4):
+        eta = cos_schedule(step)
+        b, _ = e1.replay_sample(B, step)
+        e1.learner_grad_dev([b.observation, b.actions, b.target_values, b.target_rewards, b.target_policies,
+                             b.gradient_scale], B, grad.data_ptr(), l1.data_ptr())
+        e1.learner_apply_dev(grad.data_ptr(), 1.0, eta)
+        if step % 2:
+            e2.learner_train_dev(B, step, eta, l2.data_ptr())
+        else:
+            g2 = torch.empty_like(grad)
+            e2.learner_grad_sampled_dev(B, step, g2.data_ptr(), l2.data_ptr())
+            e2.learner_apply_dev(g2.data_ptr(), 1.0, eta)
+        e1.sync(); e2.sync()
+        assert np.array_equal(l1.cpu().numpy()[:6], l2.cpu().numpy()[:6]), step
+        for n in range(3):
+            assert np.array_equal(e1.get_weights(n), e2.get_weights(n)), (step, n)
+    e1.close(); e2.close()
