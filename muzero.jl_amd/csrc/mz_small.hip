@@ -179,8 +179,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     int* sg_vtp = si + 128;
     int* sg_depth = si + 144;
     float* sg_stage = reinterpret_cast<float*>(si + 160);       // [4][16]
-    float* sg_val = reinterpret_cast<float*>(si + 224);         // [4] leaf value (read-out activation applied)
-    float* sg_rew = reinterpret_cast<float*>(si + 228);         // [4] leaf reward
+    // si + 224 .. 231: unused (formerly the leaf value / reward read-outs)
     float* sg_noise = reinterpret_cast<float*>(si + 232);       // [4][16] root exploration noise
     int* sg_path = si + 296;                                      // [T][2(S+2)]
     // select / gather tables in LDS (they sit on the per-level critical path)
@@ -313,44 +312,44 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act);
         SM_STAMP(3);
         const int e_new = s + 1;
+        // expand (wave 2) runs beside the read-outs + backup (wave 0): they
+        // touch disjoint LDS — the new slot's edges vs the path edges, the
+        // leaf edge's child link and the new slot's reward / to_play
         if (tid < 64) {
-            // ---- expand slot s+1 (:280)
-            if (tree_thread) {
-                const float prior = double_softmax_prior(a < A ? act[P.p_out + a * T + g] : 0.0f, a, A, legal,
-                                                         sg_stage + 16 * g);
-                if (active) init_edges(tree, e_new, a, A, prior);
+            // ---- value / reward read-out activations, then backpropagate! (:190-217)
+            if (active) {
+                const float val = mz_post_act(P.v_act, act[P.v_out + g]);
+                const float rew = mz_post_act(P.r_act, act[P.r_out + g]);
+                const int tl = sg_vtp[g];
+                const int depth = sg_depth[g];
+                if (a == 0) {
+                    const int li = sg_leaf_e[g] * A + sg_leaf_a[g];
+                    tree.nc(li) = (tree.nc(li) & 0xffffu) | ((uint32_t)(e_new + 1) << 16);
+                    tree.nr[e_new] = rew;
+                    tree.ntp[e_new] = (int8_t)tl;
+                    path[2 * depth + 1] = e_new;
+                }
+                __builtin_amdgcn_wave_barrier();
+                int rN = sg_rootN[g];
+                float rW = sg_rootW[g], mmin = sg_mmin[g], mmax = sg_mmax[g];
+                backup_path(tree, path, depth, val, tl, A, P.players, P.discount, rN, rW, sg_root_tp[g], mmin,
+                            mmax, a);
+                if (a == 0) { sg_rootN[g] = rN; sg_rootW[g] = rW; sg_mmin[g] = mmin; sg_mmax[g] = mmax; }
             }
-        } else if (tid < 64 + T) {
-            // wave 1: the value / reward read-out activations (f64 tanh) off
-            // wave 0's critical path
-            const int gl = tid - 64;
-            sg_val[gl] = mz_post_act(P.v_act, act[P.v_out + gl]);
-            sg_rew[gl] = mz_post_act(P.r_act, act[P.r_out + gl]);
-        } else if (tid >= 128) {
-            for (int i = tid - 128; i < T * H; i += SM_THREADS - 128)     // store h'
+        } else if (tid >= 128 && tid < 128 + 16 * T) {
+            // ---- expand slot s+1 (:280): wave 2 lanes 16 g2 + a2 (g2, a2 as wave 0's g, a)
+            const int g2 = (tid - 128) >> 4;
+            const bool active2 = tile0 + g2 < P.G;
+            TreeView tree2 = tree_view(lds_tree + (size_t)g2 * P.tree_game_bytes, E, NN);
+            const float prior = double_softmax_prior(a < A ? act[P.p_out + a * T + g2] : 0.0f, a, A, sg_legal[g2],
+                                                     sg_stage + 16 * g2);
+            if (active2) init_edges(tree2, e_new, a, A, prior);
+        } else if (tid >= 192) {
+            for (int i = tid - 192; i < T * H; i += SM_THREADS - 192)     // store h'
                 hid[((size_t)(i / H) * NN + e_new) * H + (i % H)] = act[P.h_out + (i % H) * T + i / H];
         }
         __syncthreads();
         SM_STAMP(4);
-        // ---- backpropagate! (:190-217); no barrier after: only wave 0 reads the tree
-        if (active) {
-            const int tl = sg_vtp[g];
-            const int depth = sg_depth[g];
-            if (a == 0) {
-                const int li = sg_leaf_e[g] * A + sg_leaf_a[g];
-                tree.nc(li) = (tree.nc(li) & 0xffffu) | ((uint32_t)(e_new + 1) << 16);
-                tree.nr[e_new] = sg_rew[g];
-                tree.ntp[e_new] = (int8_t)tl;
-                path[2 * depth + 1] = e_new;
-            }
-            __builtin_amdgcn_wave_barrier();
-            int rN = sg_rootN[g];
-            float rW = sg_rootW[g], mmin = sg_mmin[g], mmax = sg_mmax[g];
-            backup_path(tree, path, depth, sg_val[g], tl, A, P.players, P.discount, rN, rW, sg_root_tp[g], mmin,
-                        mmax, a);
-            if (a == 0) { sg_rootN[g] = rN; sg_rootW[g] = rW; sg_mmin[g] = mmin; sg_mmax[g] = mmax; }
-        }
-        __builtin_amdgcn_wave_barrier();
         SM_STAMP(5);
     }
     __syncthreads();
