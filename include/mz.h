@@ -249,6 +249,27 @@ int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games);
 int mz_selfplay_move(mz_handle* h, uint32_t rng_step, uint32_t game_offset, float temperature,
                      void* stream);
 
+/* Evaluation play (competitive_play!, SelfPlay.jl:421-435; play_game with
+ * an opponent, :330-382; select_opponent_action, :311-325).  mode
+ * MZ_SP_EVAL: finished games are not saved (competitive_play! keeps no
+ * buffer) but tallied for mz_eval_results; with opponent MZ_OPP_RANDOM the
+ * player != muzero_player (1 or 2) plays a uniform legal action (the Philox
+ * OPPONENT stream keyed (game id, rng_step)) instead of the search's, the
+ * intended reading of :321 (the reference reads `las`, defined only in the
+ * "human" branch); MZ_OPP_SELF: MuZero plays both sides.  Pass
+ * temperature 0 to mz_selfplay_move for competitive play.  MZ_SP_TRAIN
+ * (default): self_play! (:384-419).  Applies to the following moves; the
+ * games in progress continue.                                              */
+enum { MZ_SP_TRAIN = 0, MZ_SP_EVAL = 1 };
+enum { MZ_OPP_SELF = 0, MZ_OPP_RANDOM = 1 };
+int mz_selfplay_mode(mz_handle* h, int mode, int opponent, int muzero_player);
+
+/* Evaluation tally since mz_selfplay_init: {games finished, MuZero wins,
+ * opponent wins, draws}; the winner is read from the last move's reward
+ * (TicTacToe with quirk Q14: the player to move after it; Connect4: the
+ * mover).  Synchronises.                                                    */
+int mz_eval_results(mz_handle* h, int64_t* out4);
+
 /* The shard's counters {num_played_games, num_played_steps, total_samples}
  * (ReplayBuffer.jl:133-161) and the games it holds; synchronises.          */
 int mz_replay_counts(mz_handle* h, int64_t* counts, int32_t* games_in_buffer);

@@ -17,6 +17,8 @@ from .config import (MzConfig, MzFFHP, MzResNetHP, ResNetHP, hidden_size, stacke
 
 NET_REPR, NET_PRED, NET_DYN = 0, 1, 2
 ENV_TICTACTOE, ENV_CONNECT4 = 0, 1
+SP_TRAIN, SP_EVAL = 0, 1
+OPP_SELF, OPP_RANDOM = 0, 1
 
 _lib = None
 
@@ -59,6 +61,8 @@ SIGNATURES = {
     "mz_learner_apply_dev": (ctypes.c_int, [_VP, _VP, ctypes.c_float, ctypes.c_double, _VP]),
     "mz_selfplay_init": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "mz_selfplay_move": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float, _VP]),
+    "mz_selfplay_mode": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "mz_eval_results": (ctypes.c_int, [_VP, _VP]),
     "mz_replay_counts": (ctypes.c_int, [_VP, _VP, _VP]),
     "mz_replay_save_game": (ctypes.c_int, [_VP, ctypes.c_int32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "mz_replay_sample": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.POINTER(MzBatch), _VP, _VP]),
@@ -144,6 +148,7 @@ class Engine:
         if rc != 0:
             raise MzError(f"mz_engine_create: {lib.mz_create_error().decode()}")
         self.h = h
+        self.rng_seed = rng_seed
         self.max_games = max_games
         self.A = len(conf.action_space)
         self.H = hidden_size(conf, hyper)
@@ -283,6 +288,16 @@ class Engine:
     def selfplay_move(self, rng_step, game_offset=0, temperature=1.0, stream=None):
         self._check(self.lib.mz_selfplay_move(self.h, rng_step, game_offset, temperature, stream),
                     "mz_selfplay_move")
+
+    def selfplay_mode(self, mode, opponent=OPP_SELF, muzero_player=1):
+        """SP_TRAIN (self_play!) or SP_EVAL (competitive_play!: games tallied, not saved)."""
+        self._check(self.lib.mz_selfplay_mode(self.h, mode, opponent, muzero_player), "mz_selfplay_mode")
+
+    def eval_results(self):
+        """(games finished, MuZero wins, opponent wins, draws) since selfplay_init."""
+        out = np.zeros(4, np.int64)
+        self._check(self.lib.mz_eval_results(self.h, _p(out)), "mz_eval_results")
+        return tuple(int(x) for x in out)
 
     def replay_counts(self):
         """({num_played_games, num_played_steps, total_samples}, games held)."""

@@ -191,6 +191,8 @@ struct mz_handle {
     SpHist sp_hist{}, sp_ring{};
     long long* d_sp_counters = nullptr;
     int32_t* d_sp_done = nullptr; int32_t* d_sp_rpos = nullptr;
+    int sp_eval = 0, sp_opp = MZ_OPP_SELF, sp_mzp = 1;    // mz_selfplay_mode
+    long long* d_eval = nullptr;                          // [4] evaluation tally
     float* d_sp_dpow = nullptr;
     float *d_rs_obs = nullptr, *d_rs_act = nullptr, *d_rs_tv = nullptr, *d_rs_tr = nullptr, *d_rs_tp = nullptr,
           *d_rs_gs = nullptr;
@@ -1837,6 +1839,8 @@ static SpParams sp_params(mz_handle* h) {
     S.hist = h->sp_hist; S.ring = h->sp_ring; S.cap = h->sp_cap; S.counters = h->d_sp_counters;
     S.obs = h->d_obs; S.legal = h->d_legal; S.tp = h->d_tp; S.cv = h->d_cv; S.rv = h->d_rv; S.act = h->d_act;
     S.done = h->d_sp_done; S.ring_pos = h->d_sp_rpos;
+    S.eval = h->sp_eval; S.opponent = h->sp_opp; S.muzero_player = h->sp_mzp;
+    S.seed = h->seed; S.eval_counts = h->d_eval;
     return S;
 }
 
@@ -1872,6 +1876,8 @@ int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games) {
     MZ_TRY(h, spalloc(h, &h->d_sp_counters, 4));
     MZ_TRY(h, spalloc(h, &h->d_sp_done, (size_t)G));
     MZ_TRY(h, spalloc(h, &h->d_sp_rpos, (size_t)G));
+    MZ_TRY(h, spalloc(h, &h->d_eval, 4));
+    h->sp_eval = 0; h->sp_opp = MZ_OPP_SELF; h->sp_mzp = 1;
     // f32(discount^n) as Julia's Float32^Int (≈ f32(pow(f64))), n = 0..td+1
     std::vector<float> dp(c.td_steps + 2);
     for (int n = 0; n < (int)dp.size(); ++n) dp[n] = (float)std::pow((double)c.discount, (double)n);
@@ -1894,6 +1900,7 @@ int mz_selfplay_move(mz_handle* h, uint32_t rng_step, uint32_t game_offset, floa
     MZ_TRY(h, hipSetDevice(h->device));
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     SpParams S = sp_params(h);
+    S.step = rng_step; S.game_offset = game_offset;
     const int G = h->sp_G;
     const dim3 waves((G + 3) / 4);
     hipLaunchKernelGGL(mz_sp_prepare, waves, dim3(256), 0, st, S);
@@ -1905,6 +1912,27 @@ int mz_selfplay_move(mz_handle* h, uint32_t rng_step, uint32_t game_offset, floa
     hipLaunchKernelGGL(mz_sp_order, dim3(1), dim3(1024), 0, st, S);
     hipLaunchKernelGGL(mz_sp_store, dim3(G), dim3(256), 0, st, S);
     MZ_TRY(h, hipGetLastError());
+    return 0;
+}
+
+int mz_selfplay_mode(mz_handle* h, int mode, int opponent, int muzero_player) {
+    if (!h) return -2;
+    if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
+    if (mode != MZ_SP_TRAIN && mode != MZ_SP_EVAL) return fail(h, "mode must be MZ_SP_TRAIN or MZ_SP_EVAL");
+    if (opponent != MZ_OPP_SELF && opponent != MZ_OPP_RANDOM) return fail(h, "opponent must be MZ_OPP_SELF or MZ_OPP_RANDOM");
+    if (muzero_player != 1 && muzero_player != 2) return fail(h, "muzero_player must be 1 or 2");
+    h->sp_eval = mode == MZ_SP_EVAL; h->sp_opp = opponent; h->sp_mzp = muzero_player;
+    return 0;
+}
+
+int mz_eval_results(mz_handle* h, int64_t* out4) {
+    if (!h || !out4) return -2;
+    if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    long long c[4];
+    MZ_TRY(h, hipMemcpy(c, h->d_eval, sizeof(c), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 4; ++i) out4[i] = c[i];
     return 0;
 }
 

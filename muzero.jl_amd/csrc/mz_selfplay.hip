@@ -92,6 +92,15 @@ __device__ float env_step(const SpParams& S, int g, int a, bool* done) {
     return win ? 1.0f : 0.0f;
 }
 
+// Winner of a finished game from its last move (0 = draw / unfinished).
+// TicTacToe (Q14): the win test after a move looks at the plane of the player
+// now to move, so a nonzero reward means THAT player (3 - mover) holds a line;
+// Connect4: a nonzero reward is the mover's own four in a row.
+__device__ __forceinline__ int game_winner(const SpParams& S, float last_reward, int last_mover) {
+    if (last_reward == 0.0f) return 0;
+    return S.env == MZ_ENV_TICTACTOE ? 3 - last_mover : last_mover;
+}
+
 __device__ void env_reset(const SpParams& S, int g, int lane) {
     uint8_t* b = S.board + (size_t)g * S.osz;
     const int cells = S.osz / 3;
@@ -124,8 +133,19 @@ extern "C" __global__ __launch_bounds__(256) void mz_sp_commit(SpParams S) {
     const size_t r = (size_t)g * S.T + t;
     for (int a = lane; a < S.A; a += 64) S.hist.cv[r * S.A + a] = S.cv[(size_t)g * S.A + a];   // :375-379
     if (lane == 0) {
-        const int a = S.act[g];
+        int a = S.act[g];
         const int mover = S.player[g];
+        if (S.eval && S.opponent == MZ_OPP_RANDOM && mover != S.muzero_player) {   // :319-321
+            uint32_t legal = 0;
+            for (int b = 0; b < S.A; ++b) legal |= (uint32_t)(S.legal[(size_t)g * S.A + b] != 0) << b;
+            const int n = __builtin_popcount(legal);
+            if (n > 0) {
+                const uint32_t r = mz_rng_u32(S.seed, MZ_RNG_OPPONENT, S.game_offset + (uint32_t)g, S.step, 0);
+                uint32_t m = legal;
+                for (int k = (int)mz_rng_below(r, (uint32_t)n); k > 0; --k) m &= m - 1;
+                a = __builtin_ctz(m) + 1;
+            }
+        }
         bool done = false;
         const float rew = env_step(S, g, a, &done);                // :366-368
         S.hist.act[r] = a;
@@ -154,6 +174,20 @@ extern "C" __global__ __launch_bounds__(1024) void mz_sp_order(SpParams S) {
         __syncthreads();
         cnt[tid] += v;
         __syncthreads();
+    }
+    if (S.eval) {                                                   // tally; nothing is saved
+        long long t[4] = {0, 0, 0, 0};
+        for (int g = g0; g < g1; ++g) {
+            S.ring_pos[g] = -1;
+            if (!S.done[g]) continue;
+            const size_t last = (size_t)g * S.T + S.hist.len[g] - 1;
+            const int w = game_winner(S, S.hist.rew[last], S.hist.tp[last]);
+            t[0] += 1;
+            t[w == 0 ? 3 : w == S.muzero_player ? 1 : 2] += 1;
+        }
+        for (int k = 0; k < 4; ++k)                                 // integer sums: any order is exact
+            if (t[k]) atomicAdd(reinterpret_cast<unsigned long long*>(S.eval_counts + k), (unsigned long long)t[k]);
+        return;
     }
     const long long played = S.counters[0];
     long long rank = cnt[tid] - n, steps = 0, evicted = 0;
@@ -186,7 +220,13 @@ extern "C" __global__ __launch_bounds__(256) void mz_sp_store(SpParams S) {
     const int g = blockIdx.x;
     if (!S.done[g]) return;
     const int slot = S.ring_pos[g], len = S.hist.len[g], tid = threadIdx.x;
-    const size_t src = (size_t)g * S.T, dst = (size_t)slot * S.T;
+    const size_t src = (size_t)g * S.T, dst = (size_t)(slot < 0 ? 0 : slot) * S.T;
+    if (slot < 0) {                                // evaluation: the slot just restarts
+        __syncthreads();
+        if (tid == 0) { S.hist.len[g] = 0; S.done[g] = 0; }
+        if (tid < 64) env_reset(S, g, tid);
+        return;
+    }
     for (int k = tid; k < len * S.osz; k += blockDim.x) S.ring.obs[dst * S.osz + k] = S.hist.obs[src * S.osz + k];
     for (int k = tid; k < len * S.A; k += blockDim.x) S.ring.cv[dst * S.A + k] = S.hist.cv[src * S.A + k];
     for (int k = tid; k < len; k += blockDim.x) {

@@ -35,6 +35,14 @@ struct SpParams {
     float* obs; uint8_t* legal; int32_t* tp; const float* cv; const float* rv; const int32_t* act;
     int32_t* done;              // [G] finished this move
     int32_t* ring_pos;          // [G] ring slot of the finished game
+    // evaluation play (competitive_play!, SelfPlay.jl:421-435): finished games
+    // are tallied, not saved; with opponent = MZ_OPP_RANDOM the moves of the
+    // player != muzero_player are uniform legal actions (select_opponent_action
+    // :311-325) from the Philox OPPONENT stream keyed (game id, move step)
+    int eval, opponent, muzero_player;
+    uint32_t step, game_offset;
+    uint64_t seed;
+    long long* eval_counts;     // [4] games, muzero wins, opponent wins, draws
 };
 
 // get_batch + make_target (ReplayBuffer.jl:5-50, 73-107, 188-217) on the shard

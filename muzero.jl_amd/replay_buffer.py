@@ -15,28 +15,7 @@ import numpy as np
 from .selfplay import GameHistory, get_stacked_observations
 
 MZ_RNG_GAME, MZ_RNG_POS, MZ_RNG_ABSORB = 4, 5, 6
-_M = 0xFFFFFFFF
-
-
-def _philox(c0, c1, c2, c3, k0, k1):
-    """Philox4x32-10 (include/mz_detmath.h mz_philox), pure Python."""
-    for _ in range(10):
-        p0 = 0xD2511F53 * c0
-        p1 = 0xCD9E8D57 * c2
-        hi0, lo0 = (p0 >> 32) & _M, p0 & _M
-        hi1, lo1 = (p1 >> 32) & _M, p1 & _M
-        c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
-        k0 = (k0 + 0x9E3779B9) & _M
-        k1 = (k1 + 0xBB67AE85) & _M
-    return c0, c1, c2, c3
-
-
-def rng_u32(seed, purpose, ident, step, idx):
-    return _philox(idx & _M, ident & _M, step & _M, purpose, seed & _M, (seed >> 32) & _M)[0]
-
-
-def rng_below(r, n):
-    return (r * n) >> 32
+from .rng import _M, _philox, rng_below, rng_u32  # noqa: F401  (re-exported)
 
 
 def disc_pow(g, n):

@@ -14,6 +14,18 @@ from typing import List, Optional
 import numpy as np
 
 from .config import stacked_features
+from .rng import rng_below, rng_u32
+
+MZ_RNG_OPPONENT = 7                                               # include/mz_detmath.h
+
+
+def game_winner(env_name, last_reward, last_mover):
+    """Winner of a finished game from its last move (0 = draw).  TicTacToe with
+    Q14: the win test after a move looks at the plane of the player then to
+    move, so a nonzero reward means 3 - mover holds a line; Connect4: the mover."""
+    if last_reward == 0.0:
+        return 0
+    return 3 - last_mover if env_name == "tictactoe" else last_mover
 
 
 def visit_softmax_temperature_fn(trained_steps: int) -> float:   # SelfPlay.jl:48-56
@@ -62,7 +74,13 @@ def get_stacked_observations(obs_hist, action_hist, index, num_stacked, plane):
 class BatchedSelfPlay:
     """G TicTacToe games played in lockstep on one engine (one GPU)."""
 
-    def __init__(self, engine, env_cls, G, game_offset=0, step0=0):
+    def __init__(self, engine, env_cls, G, game_offset=0, step0=0, opponent="self", muzero_player=1):
+        """opponent "self" (self_play!, SelfPlay.jl:384-419) or "random": the
+        player != muzero_player plays a uniform legal action
+        (select_opponent_action, :311-325) — competitive_play! (:421-435)."""
+        assert opponent in ("self", "random") and muzero_player in (1, 2)
+        self.opponent = opponent
+        self.muzero_player = muzero_player
         self.eng = engine
         self.conf = engine.conf
         self.G = G
@@ -97,6 +115,12 @@ class BatchedSelfPlay:
                 raise NotImplementedError("temperature_threshold with mixed move counts")
         cv, rv, act = self.eng.mcts_search(obs, legal, tp, exploration=True, rng_step=self.step,
                                            game_offset=self.game_offset, temperature=temps)  # :359-360
+        if self.opponent == "random":                                         # :357-362, :321
+            for g in np.flatnonzero(tp != self.muzero_player):
+                acts = np.flatnonzero(legal[g])
+                if len(acts):
+                    r = rng_u32(self.eng.rng_seed, MZ_RNG_OPPONENT, self.game_offset + int(g), self.step, 0)
+                    act[g] = acts[rng_below(r, len(acts))] + 1
         reward, done = self.env.step(act)                                     # :366-368
         for g, h in enumerate(self.histories):                                # :375-379
             h.child_visits.append(cv[g])

@@ -191,3 +191,41 @@ def test_fused_learner_matches_separate_calls(kind, resnet, B):
         for n in range(3):
             assert np.array_equal(e1.get_weights(n), e2.get_weights(n)), (step, n)
     e1.close(); e2.close()
+
+
+@pytest.mark.parametrize("kind,opp,mzp", [("ttt", "random", 1), ("ttt", "random", 2), ("c4", "random", 2),
+                                          ("ttt", "self", 1)])
+def test_evaluation_play_matches_host(kind, opp, mzp):
+    """competitive_play! on the device (mz_selfplay_mode(SP_EVAL)): random
+    opponent moves, temperature 0, games tallied instead of saved — the same
+    games as the host driver (BatchedSelfPlay(opponent=...)) move for move."""
+    from muzero_jl_amd import abi
+    from muzero_jl_amd.selfplay import BatchedSelfPlay, game_winner
+    mod, env_cls, env_kind = _env(kind)
+    G = 16
+    conf = dataclasses.replace(mod.conf, num_iters=6, replay_buffer_size=64)
+    eh, ed = _engines(mod, conf, mod.hyper, G)
+    sp = BatchedSelfPlay(eh, env_cls, G, game_offset=7, step0=100, opponent=opp, muzero_player=mzp)
+    ed.selfplay_init(env_kind, G, 64)
+    ed.selfplay_mode(abi.SP_EVAL, abi.OPP_RANDOM if opp == "random" else abi.OPP_SELF, mzp)
+    for m in range(14 if kind == "ttt" else 30):
+        sp.play_move(0.0)
+        ed.selfplay_move(100 + m, game_offset=7, temperature=0.0)
+    name = "tictactoe" if kind == "ttt" else "connect4"
+    t = [0, 0, 0, 0]
+    for h in sp.finished:
+        w = game_winner(name, h.reward_history[-1], h.to_play_history[-1])
+        t[0] += 1
+        t[3 if w == 0 else 1 if w == mzp else 2] += 1
+    assert t[0] > 0 and ed.eval_results() == tuple(t)
+    assert ed.replay_counts()[0][0] == 0                      # competitive_play! saves nothing
+    ln, board, player = ed.selfplay_slots()
+    assert np.array_equal(ln, [len(h.action_history) for h in sp.histories])
+    assert np.array_equal(board, sp.env.board.astype(np.uint8)) and np.array_equal(player, sp.env.player)
+    ed.selfplay_mode(abi.SP_TRAIN)                             # back to self_play!: finished games are saved
+    for m in range(12):
+        ed.selfplay_move(200 + m, game_offset=7)
+    assert ed.replay_counts()[0][0] > 0
+    with pytest.raises(abi.MzError, match="muzero_player"):
+        ed.selfplay_mode(abi.SP_EVAL, abi.OPP_RANDOM, 3)
+    eh.close(); ed.close()
