@@ -195,7 +195,8 @@ int mz_debug_unroll(mz_handle* h, int B, float* values, float* policies, float* 
  * column-major as in the reference:
  *   observation (W,H,Cs,B), actions (K+1,B) as float action ids,
  *   target_values (K+1,B), target_rewards (K+1,B), target_policies (A,K+1,B),
- *   gradient_scale (B).  PER weights are not supported (PER=false).        */
+ *   gradient_scale (B), weights (B): PER importance-sampling weights
+ *   (weight_batch, ReplayBuffer.jl:211-215), NULL = all 1 (PER = false).     */
 typedef struct mz_batch {
     int32_t batch_size;
     const float* observation;
@@ -204,6 +205,7 @@ typedef struct mz_batch {
     const float* target_rewards;
     const float* target_policies;
     const float* gradient_scale;
+    const float* weights;
 } mz_batch;
 
 /* Learner step in ref_semantics (Learning.jl:327-413, quirks Q10/Q11):
@@ -304,6 +306,22 @@ int mz_learner_grad_sampled_dev(mz_handle* h, int32_t B, uint32_t step, float* g
                                 float* losses_dev, void* stream);
 int mz_learner_train_dev(mz_handle* h, int32_t B, uint32_t step, double eta, float* losses_dev,
                          void* stream);
+
+/* PER (conf.PER, ReplayBuffer.jl:133-145, 168-183; Learning.jl:400-404).
+ * With PER the shard keeps per-position priorities (initialised by
+ * save_game: |root_value − target_value|^PER_alpha, game priority = max),
+ * get_batch samples games and positions by priority and fills
+ * batch->weights, and the learner weights its losses.  The fused learner
+ * calls (mz_learner_train_dev / _grad_sampled_dev) then update the sampled
+ * positions' priorities from the unroll's values; after mz_replay_sample +
+ * mz_learner_grad_dev call mz_replay_update_priorities (it uses the batch of
+ * the last sample and the last unroll).  The reference's update_priorities!
+ * cannot run (`minimum(a, b)`, a K+2-element slice); this is its intended
+ * reading: positions pos..min(pos+K, len), samples in batch order.          */
+int mz_replay_update_priorities(mz_handle* h, void* stream);
+/* Debug/parity: priorities of game i of the shard (0 = oldest held), T of
+ * them, and its game priority; synchronises.                                */
+int mz_replay_get_priorities(mz_handle* h, int32_t i, float* priorities, float* game_priority);
 
 /* Debug/parity: game i of the shard (0 = oldest held), buffers sized for
  * max_moves + 1 moves (layouts as mz_replay_save_game); any pointer may be

@@ -31,7 +31,7 @@ _VP = ctypes.c_void_p
 class MzBatch(ctypes.Structure):
     _fields_ = [("batch_size", ctypes.c_int32), ("observation", _VP), ("actions", _VP),
                 ("target_values", _VP), ("target_rewards", _VP), ("target_policies", _VP),
-                ("gradient_scale", _VP)]
+                ("gradient_scale", _VP), ("weights", _VP)]
 
 
 # exported symbol -> (restype, argtypes); tests check every one is present
@@ -68,6 +68,8 @@ SIGNATURES = {
     "mz_replay_sample": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.POINTER(MzBatch), _VP, _VP]),
     "mz_learner_grad_sampled_dev": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, _VP, _VP, _VP]),
     "mz_learner_train_dev": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.c_double, _VP, _VP]),
+    "mz_replay_update_priorities": (ctypes.c_int, [_VP, _VP]),
+    "mz_replay_get_priorities": (ctypes.c_int, [_VP, ctypes.c_int32, _VP, _VP]),
     "mz_replay_get_game": (ctypes.c_int, [_VP, ctypes.c_int32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "mz_selfplay_slots": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
     "mz_checkpoint_save": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int64]),
@@ -255,12 +257,15 @@ class Engine:
     # ---- learner
     def learner_step(self, batch, eta):
         """batch: dict with observation (B, F), actions (B, K+1), target_values (B, K+1),
-        target_rewards (B, K+1), target_policies (B, K+1, A), gradient_scale (B)."""
+        target_rewards (B, K+1), target_policies (B, K+1, A), gradient_scale (B) and,
+        with PER, weights (B)."""
         arrs = {k: np.ascontiguousarray(batch[k], dtype=np.float32) for k in
                 ("observation", "actions", "target_values", "target_rewards", "target_policies", "gradient_scale")}
+        w = batch.get("weights")
+        w = None if w is None else np.ascontiguousarray(w, dtype=np.float32)
         b = MzBatch(arrs["observation"].shape[0], _p(arrs["observation"]), _p(arrs["actions"]),
                     _p(arrs["target_values"]), _p(arrs["target_rewards"]), _p(arrs["target_policies"]),
-                    _p(arrs["gradient_scale"]))
+                    _p(arrs["gradient_scale"]), _p(w))
         losses = np.empty(6, np.float32)
         self._check(self.lib.mz_learner_step(self.h, ctypes.byref(b), float(eta), _p(losses)), "mz_learner_step")
         return losses
@@ -363,7 +368,23 @@ class Engine:
             a = np.empty(shape, np.float32)
             _copy_d2h(a, getattr(b, name))
             out[name] = a
+        if b.weights:                                   # PER importance weights
+            a = np.empty(B, np.float32)
+            _copy_d2h(a, b.weights)
+            out["weights"] = a
         return out
+
+    def replay_update_priorities(self, stream=None):
+        """PER update_priorities! of the last sampled batch from the last unroll's values."""
+        self._check(self.lib.mz_replay_update_priorities(self.h, stream), "mz_replay_update_priorities")
+
+    def replay_get_priorities(self, i):
+        """(priorities (T,), game priority) of shard game i (0 = oldest held)."""
+        T = self.replay_get_game(i).as_arrays()["action"].shape[0]
+        pr = np.zeros(T, np.float32)
+        gp = np.zeros(1, np.float32)
+        self._check(self.lib.mz_replay_get_priorities(self.h, i, _p(pr), _p(gp)), "mz_replay_get_priorities")
+        return pr, float(gp[0])
 
     def selfplay_slots(self):
         G = self.sp_G

@@ -42,6 +42,13 @@ extern "C" __global__ void mz_sp_commit(SpParams S);
 extern "C" __global__ void mz_sp_order(SpParams S);
 extern "C" __global__ void mz_sp_store(SpParams S);
 extern "C" __global__ void mz_rp_sample(RpSampleParams Q);
+extern "C" __global__ void mz_rp_per_init(SpHist ring, int slot, int len, int Tmax, int td, const float* disc_pow,
+                                          int alpha);
+extern "C" __global__ void mz_rp_per_prep(SpHist ring, const long long* counters, int cap, float* cum, float* prob,
+                                          long long* total);
+extern "C" __global__ void mz_rp_per_norm(float* w, int B);
+extern "C" __global__ void mz_rp_per_update(SpHist ring, const long long* counters, int cap, int Tmax, int B, int K,
+                                            int alpha, const int32_t* index, const float* pv, const float* tv);
 extern "C" __global__ void mz_search_small1(SmallParams P);
 extern "C" __global__ void mz_search_small2(SmallParams P);
 extern "C" __global__ void mz_search_small4(SmallParams P);
@@ -57,11 +64,11 @@ extern "C" __global__ void mz_forward_kernel(const int* plan, const float* Wp, c
 extern "C" __global__ void mz_learner_grad_kernel(int B, int K, int A, int v_act, int r_act, float* pv, float* pp,
                                                   float* pr, const float* tv, const float* tp, const float* gscale,
                                                   float* terms, float* flat, const size_t* netoff, float* G,
-                                                  double* part, unsigned* counter, float* out, LgAdam ad);
+                                                  double* part, unsigned* counter, float* out, const float* wts, LgAdam ad);
 extern "C" __global__ void mz_learner_grad_kernel32(int B, int K, int A, int v_act, int r_act, float* pv, float* pp,
                                                     float* pr, const float* tv, const float* tp, const float* gscale,
                                                     float* terms, float* flat, const size_t* netoff, float* G,
-                                                    double* part, unsigned* counter, float* out, LgAdam ad);
+                                                    double* part, unsigned* counter, float* out, const float* wts, LgAdam ad);
 extern "C" __global__ void mz_adam_kernel(float* P, float* M, float* V, const float* G, float gscale, size_t n,
                                           double bp1, double bp2, double eta, float* Wp, float* Bp,
                                           const int* inv_tile, float* smw, float* smb, const int* inv_small);
@@ -148,6 +155,10 @@ struct mz_handle {
     double* d_pbc = nullptr; double* d_sqrt = nullptr; float* d_aval = nullptr;
     double* d_pbterm = nullptr;             // pbc(Np) * (sqrt(Np) / (Nc + 1)), triangle
     size_t rtree_lds = 0;                                    // LDS of the LDS-cached ResNet tree step (0 = HBM kernel)
+    float* d_bw = nullptr;                                   // host batch PER weights (mz_learner_step)
+    float* d_rs_w = nullptr; float* d_per_cum = nullptr; float* d_per_p = nullptr;   // PER sampling
+    long long* d_per_total = nullptr;
+    int rs_last_B = 0;                                       // batch size of the last get_batch
     char* d_tree = nullptr; size_t tree_game_bytes = 0; bool lds_tree = false; int dump_tree = 0;
     int time_nets = 0;                      // mz_debug_enable flag 2: events around each ResNet nets launch
     std::vector<hipEvent_t> tev; size_t tev_used = 0;
@@ -1490,6 +1501,7 @@ static int ensure_batch(mz_handle* h, int B) {
                       (size_t)B * (K + 1)};
     for (int i = 0; i < 9; ++i) MZ_TRY(h, dalloc(h, bufs[i], sizes[i]));
     MZ_TRY(h, dalloc(h, &h->d_lterm, (size_t)2 * B * (K + 1)));
+    MZ_TRY(h, dalloc(h, &h->d_bw, (size_t)B));
     if (h->kind == 1) MZ_TRY(h, dalloc(h, &h->d_rhs, (size_t)B * h->H));
     h->bcap = B;
     return 0;
@@ -1608,7 +1620,7 @@ static int learner_losses(mz_handle* h, const mz_batch* b, float* grad_dev, floa
     const LgAdam ad = adam_args(h, fuse_adam ? 1 : 0, eta);
     hipLaunchKernelGGL(gw == 32 ? mz_learner_grad_kernel32 : mz_learner_grad_kernel, dim3(nlb + 3 * MZ_L2_BLOCKS), dim3(MZ_THREADS), 0, st, B, K, A,
                        v_act, r_act, h->d_pv, h->d_pp, h->d_pr, b->target_values, b->target_policies,
-                       b->gradient_scale, h->d_lterm, h->d_flat, h->d_netoff, g, h->d_sq, h->d_counter, lo, ad);
+                       b->gradient_scale, h->d_lterm, h->d_flat, h->d_netoff, g, h->d_sq, h->d_counter, lo, b->weights, ad);
     MZ_TRY(h, hipGetLastError());
     if (fuse_adam) adam_advance(h);
     return 0;
@@ -1639,9 +1651,11 @@ int mz_learner_step(mz_handle* h, const mz_batch* b, double eta, float* losses_o
     MZ_TRY(h, hipMemcpyAsync(h->d_btr, b->target_rewards, (size_t)B * (K + 1) * 4, hipMemcpyHostToDevice, st));
     MZ_TRY(h, hipMemcpyAsync(h->d_btp, b->target_policies, (size_t)B * (K + 1) * A * 4, hipMemcpyHostToDevice, st));
     MZ_TRY(h, hipMemcpyAsync(h->d_bgs, b->gradient_scale, (size_t)B * 4, hipMemcpyHostToDevice, st));
+    if (b->weights) MZ_TRY(h, hipMemcpyAsync(h->d_bw, b->weights, (size_t)B * 4, hipMemcpyHostToDevice, st));
     mz_batch db = *b;
     db.observation = h->d_bobs; db.actions = h->d_bact; db.target_values = h->d_btv;
     db.target_rewards = h->d_btr; db.target_policies = h->d_btp; db.gradient_scale = h->d_bgs;
+    db.weights = b->weights ? h->d_bw : nullptr;
     int rc = mz_learner_grad_dev(h, &db, h->d_grad, h->d_loss, st);
     if (rc) return rc;
     rc = mz_learner_apply_dev(h, h->d_grad, 1.0f, eta, st);
@@ -1825,6 +1839,8 @@ static int sp_alloc_hist(mz_handle* h, SpHist& r, size_t n) {
     MZ_TRY(h, spalloc(h, &r.cv, n * T * A));
     MZ_TRY(h, spalloc(h, &r.rv, n * T));
     MZ_TRY(h, spalloc(h, &r.len, n));
+    MZ_TRY(h, spalloc(h, &r.prio, n * T));
+    MZ_TRY(h, spalloc(h, &r.gprio, n));
     return 0;
 }
 
@@ -1841,6 +1857,7 @@ static SpParams sp_params(mz_handle* h) {
     S.done = h->d_sp_done; S.ring_pos = h->d_sp_rpos;
     S.eval = h->sp_eval; S.opponent = h->sp_opp; S.muzero_player = h->sp_mzp;
     S.seed = h->seed; S.eval_counts = h->d_eval;
+    S.per = c.PER != 0; S.per_alpha = c.PER_alpha; S.td = c.td_steps; S.disc_pow = h->d_sp_dpow;
     return S;
 }
 
@@ -1877,6 +1894,9 @@ int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games) {
     MZ_TRY(h, spalloc(h, &h->d_sp_done, (size_t)G));
     MZ_TRY(h, spalloc(h, &h->d_sp_rpos, (size_t)G));
     MZ_TRY(h, spalloc(h, &h->d_eval, 4));
+    MZ_TRY(h, spalloc(h, &h->d_per_cum, (size_t)h->sp_cap));
+    MZ_TRY(h, spalloc(h, &h->d_per_p, (size_t)h->sp_cap));
+    MZ_TRY(h, spalloc(h, &h->d_per_total, 1));
     h->sp_eval = 0; h->sp_opp = MZ_OPP_SELF; h->sp_mzp = 1;
     // f32(discount^n) as Julia's Float32^Int (≈ f32(pow(f64))), n = 0..td+1
     std::vector<float> dp(c.td_steps + 2);
@@ -1976,6 +1996,12 @@ int mz_replay_save_game(mz_handle* h, int32_t T, const uint8_t* obs, const int32
     MZ_TRY(h, hipMemcpy(r.rv + base, root_values, (size_t)T * 4, hipMemcpyHostToDevice));
     MZ_TRY(h, hipMemcpy(r.len + slot, &T, 4, hipMemcpyHostToDevice));
     MZ_TRY(h, hipMemcpy(h->d_sp_counters, c, sizeof(c), hipMemcpyHostToDevice));
+    if (h->conf.PER) {                              // initial priorities (:136-143)
+        hipLaunchKernelGGL(mz_rp_per_init, dim3(1), dim3(64), 0, h->stream, h->sp_ring, slot, (int)T, h->sp_T,
+                           h->conf.td_steps, (const float*)h->d_sp_dpow, h->conf.PER_alpha);
+        MZ_TRY(h, hipGetLastError());
+        MZ_TRY(h, hipStreamSynchronize(h->stream));
+    }
     return 0;
 }
 
@@ -2000,6 +2026,7 @@ static int rs_params(mz_handle* h, int32_t B, uint32_t step, hipStream_t st, RpS
         MZ_TRY(h, spalloc(h, &h->d_rs_tp, (size_t)B * K1 * A, false));
         MZ_TRY(h, spalloc(h, &h->d_rs_gs, (size_t)B, false));
         MZ_TRY(h, spalloc(h, &h->d_rs_index, (size_t)B * 2, false));
+        MZ_TRY(h, spalloc(h, &h->d_rs_w, (size_t)B, false));
         h->rs_cap = B;
     }
     RpSampleParams Q;
@@ -2009,10 +2036,36 @@ static int rs_params(mz_handle* h, int32_t B, uint32_t step, hipStream_t st, RpS
     Q.seed = h->seed; Q.step = step; Q.ring = h->sp_ring; Q.counters = h->d_sp_counters; Q.disc_pow = h->d_sp_dpow;
     Q.obs = h->d_rs_obs; Q.actions = h->d_rs_act; Q.tv = h->d_rs_tv; Q.tr = h->d_rs_tr; Q.tpol = h->d_rs_tp;
     Q.gscale = h->d_rs_gs; Q.index = h->d_rs_index;
+    Q.per = h->conf.PER != 0;
+    if (Q.per) {                                  // game probabilities of the held games (:91-99)
+        Q.per_cum = h->d_per_cum; Q.per_p = h->d_per_p; Q.per_total = h->d_per_total; Q.weights = h->d_rs_w;
+        hipLaunchKernelGGL(mz_rp_per_prep, dim3(1), dim3(64), 0, st, h->sp_ring, (const long long*)h->d_sp_counters,
+                           h->sp_cap, h->d_per_cum, h->d_per_p, h->d_per_total);
+        MZ_TRY(h, hipGetLastError());
+    }
     *Qo = Q;
     batch->batch_size = B;
     batch->observation = h->d_rs_obs; batch->actions = h->d_rs_act; batch->target_values = h->d_rs_tv;
     batch->target_rewards = h->d_rs_tr; batch->target_policies = h->d_rs_tp; batch->gradient_scale = h->d_rs_gs;
+    batch->weights = Q.per ? h->d_rs_w : nullptr;
+    return 0;
+}
+
+// PER: weight_batch ./= maximum(weight_batch) after the sampling launch
+static int per_norm(mz_handle* h, int B, hipStream_t st) {
+    if (!h->conf.PER) return 0;
+    hipLaunchKernelGGL(mz_rp_per_norm, dim3(1), dim3(256), 0, st, h->d_rs_w, B);
+    MZ_TRY(h, hipGetLastError());
+    return 0;
+}
+
+// PER: update_priorities! of the last sampled batch from the last unroll's values
+static int per_update(mz_handle* h, int B, hipStream_t st) {
+    if (!h->conf.PER) return 0;
+    hipLaunchKernelGGL(mz_rp_per_update, dim3(1), dim3(64), 0, st, h->sp_ring, (const long long*)h->d_sp_counters,
+                       h->sp_cap, h->sp_T, B, h->conf.num_unroll_steps, h->conf.PER_alpha, h->d_rs_index, h->d_pv,
+                       h->d_rs_tv);
+    MZ_TRY(h, hipGetLastError());
     return 0;
 }
 
@@ -2024,6 +2077,8 @@ int mz_replay_sample(mz_handle* h, int32_t B, uint32_t step, mz_batch* batch, in
     if (rs_params(h, B, step, st, &Q, batch)) return -1;
     hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, Q);
     MZ_TRY(h, hipGetLastError());
+    if (per_norm(h, B, st)) return -1;
+    h->rs_last_B = B;
     if (index_batch) {
         MZ_TRY(h, hipMemcpyAsync(index_batch, h->d_rs_index, (size_t)B * 8, hipMemcpyDeviceToHost, st));
         MZ_TRY(h, hipStreamSynchronize(st));
@@ -2044,15 +2099,46 @@ static int learner_sampled(mz_handle* h, int32_t B, uint32_t step, float* grad_d
     mz_batch b;
     if (rs_params(h, B, step, st, &Q, &b)) return -1;
     if (ensure_batch(h, B)) return -1;
+    h->rs_last_B = B;
     if (h->kind == 1) {                             // ResNet: sample, then the network unroll
         hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, Q);
         MZ_TRY(h, hipGetLastError());
-        if (!train) return rlearner_grad(h, &b, grad_dev, losses_dev, st);
-        if (rlearner_grad(h, &b, nullptr, losses_dev, st)) return -1;
-        return mz_learner_apply_dev(h, nullptr, 1.0f, eta, st);
+        if (per_norm(h, B, st)) return -1;
+        if (rlearner_grad(h, &b, train ? nullptr : grad_dev, losses_dev, st)) return -1;
+        if (per_update(h, B, st)) return -1;                       // Learning.jl:400-404
+        return train ? mz_learner_apply_dev(h, nullptr, 1.0f, eta, st) : 0;
     }
     if (fc_unroll(h, &b, st, &Q)) return -1;
-    return learner_losses(h, &b, grad_dev, losses_dev, st, h->lay.v_act, h->lay.r_act, train, eta);
+    if (per_norm(h, B, st)) return -1;
+    if (learner_losses(h, &b, grad_dev, losses_dev, st, h->lay.v_act, h->lay.r_act, train, eta)) return -1;
+    return per_update(h, B, st);                                   // Learning.jl:400-404
+}
+
+int mz_replay_update_priorities(mz_handle* h, void* stream) {
+    if (!h) return -2;
+    if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
+    if (!h->conf.PER) return fail(h, "PER is off in the config");
+    if (h->rs_last_B <= 0) return fail(h, "no batch sampled yet");
+    MZ_TRY(h, hipSetDevice(h->device));
+    return per_update(h, h->rs_last_B, stream ? (hipStream_t)stream : h->stream);
+}
+
+int mz_replay_get_priorities(mz_handle* h, int32_t i, float* priorities, float* game_priority) {
+    if (!h) return -2;
+    if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    long long played = 0;
+    MZ_TRY(h, hipMemcpy(&played, h->d_sp_counters, sizeof(played), hipMemcpyDeviceToHost));
+    const long long n = std::min<long long>(played, h->sp_cap);
+    if (i < 0 || i >= n) return fail(h, "game index out of range");
+    const int slot = (int)((played - n + i) % h->sp_cap);
+    int32_t T = 0;
+    MZ_TRY(h, hipMemcpy(&T, h->sp_ring.len + slot, 4, hipMemcpyDeviceToHost));
+    if (priorities)
+        MZ_TRY(h, hipMemcpy(priorities, h->sp_ring.prio + (size_t)slot * h->sp_T, (size_t)T * 4, hipMemcpyDeviceToHost));
+    if (game_priority) MZ_TRY(h, hipMemcpy(game_priority, h->sp_ring.gprio + slot, 4, hipMemcpyDeviceToHost));
+    return 0;
 }
 
 int mz_learner_grad_sampled_dev(mz_handle* h, int32_t B, uint32_t step, float* grad_dev, float* losses_dev,

@@ -167,7 +167,7 @@ template <int GW>
 __device__ __forceinline__ void learner_grad_body(
     int B, int K, int A, int v_act, int r_act, float* pv, float* pp, float* pr, const float* tv, const float* tp,
     const float* gscale, float* terms, float* flat, const size_t* netoff, float* G, double* part,
-    unsigned* counter, float* out, LgAdam ad) {
+    unsigned* counter, float* out, const float* wts, LgAdam ad) {
     __shared__ double red_v[MZ_THREADS], red_p[MZ_THREADS], red_c[MZ_THREADS];
     __shared__ float stg[MZ_THREADS];
     __shared__ bool last;
@@ -274,9 +274,10 @@ __device__ __forceinline__ void learner_grad_body(
                 s = s + vk;
                 c = c + (-ck);
             }
-            sv += (double)(s / gscale[j]);
+            const float w = wts ? wts[j] : 1.0f;   // PER importance weights (Learning.jl:271-285)
+            sv += (double)((s / gscale[j]) * w);
             sc += (double)c;                    // Σ_k ce_k
-            sg += 1.0 / (double)gscale[j];      // Σ_j 1/g_j
+            sg += (double)w / (double)gscale[j];   // Σ_j w_j/g_j
         }
         if (staged) __syncthreads();
     }
@@ -303,8 +304,8 @@ __device__ __forceinline__ void learner_grad_body(
 }
 #define MZ_LG_ARGS int B, int K, int A, int v_act, int r_act, float* pv, float* pp, float* pr, const float* tv, \
     const float* tp, const float* gscale, float* terms, float* flat, const size_t* netoff, float* G, \
-    double* part, unsigned* counter, float* out, LgAdam ad
-#define MZ_LG_CALL B, K, A, v_act, r_act, pv, pp, pr, tv, tp, gscale, terms, flat, netoff, G, part, counter, out, ad
+    double* part, unsigned* counter, float* out, const float* wts, LgAdam ad
+#define MZ_LG_CALL B, K, A, v_act, r_act, pv, pp, pr, tv, tp, gscale, terms, flat, netoff, G, part, counter, out, wts, ad
 extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_grad_kernel(MZ_LG_ARGS) {
     learner_grad_body<16>(MZ_LG_CALL);
 }

@@ -27,19 +27,66 @@ __device__ __forceinline__ void stacked_obs(float* out, const uint8_t* cur, cons
 }
 
 // compute_target_value (ReplayBuffer.jl:5-20, Q9), f32, 1-based index
-__device__ __forceinline__ float rp_target_value(const RpSampleParams& Q, const float* rv, const int32_t* tp, const float* rew, int T,
-                                 int index) {
-    const int bi = index + Q.td;
+__device__ __forceinline__ float rp_target_value(int td, const float* disc_pow, const float* rv, const int32_t* tp,
+                                                 const float* rew, int T, int index) {
+    const int bi = index + td;
     if (bi >= T) return 0.0f;
     const float r0 = rv[bi - 1];
     const float last = tp[bi - 1] == tp[index - 1] ? r0 : -r0;
-    float value = last * Q.disc_pow[Q.td];
-    for (int i = 1; i <= Q.td + 1; ++i) {
+    float value = last * disc_pow[td];
+    for (int i = 1; i <= td + 1; ++i) {
         const float r = rew[index + i - 2];
         const float sr = tp[index - 1] == tp[index + i - 1] ? r : -r;
-        value = value + sr * Q.disc_pow[i];
+        value = value + sr * disc_pow[i];
     }
     return value;
+}
+
+// PER priority |x|^alpha (Julia Float32^Int): f64 repeated multiplication,
+// rounded once to f32 (the host mirror's per_priority is the same loop)
+__device__ __forceinline__ float per_priority(float x, int alpha) {
+    const double ax = (double)fabsf(x);
+    double r = 1.0;
+    for (int i = 0; i < alpha; ++i) r = r * ax;
+    return (float)r;
+}
+
+// uniform double in [0, 1) from a Philox draw: 24 bits, exact
+__device__ __forceinline__ double per_uniform(uint32_t r) { return (double)(r >> 8) * 5.9604644775390625e-08; }
+
+// Categorical(p) with f32 probabilities p[i] = w[i] / S (S = ascending f32
+// sum of w): i = first index whose ascending f32 running sum is >= u (the
+// last index if none); *prob = p[i].  Sequential, one lane.
+__device__ __forceinline__ int per_categorical(const float* w, int n, double u, float* prob) {
+    float S = 0.0f;
+    for (int i = 0; i < n; ++i) S = S + w[i];
+    int i = 0;
+    float p = w[0] / S, c = p;
+    while ((double)c < u && i < n - 1) {
+        ++i;
+        p = w[i] / S;
+        c = c + p;
+    }
+    *prob = p;
+    return i;
+}
+
+// save_game's initial priorities for ring slot `slot` of length len (PER,
+// ReplayBuffer.jl:136-143): |root_value_i − target_value_i|^alpha, game
+// priority = max.  Lanes over positions, lane 0 folds the max.
+__device__ __forceinline__ void per_init_slot(SpHist& ring, int slot, int len, int Tmax, int td,
+                                              const float* disc_pow, int alpha, int lane, int nlanes) {
+    const size_t base = (size_t)slot * Tmax;
+    for (int k = lane; k < len; k += nlanes)
+        ring.prio[base + k] = per_priority(ring.rv[base + k] -
+                                           rp_target_value(td, disc_pow, ring.rv + base, ring.tp + base,
+                                                           ring.rew + base, len, k + 1), alpha);
+}
+__device__ __forceinline__ void per_game_max(SpHist& ring, int slot, int len, int Tmax) {
+    const float* pr = ring.prio + (size_t)slot * Tmax;
+    float m = pr[0];
+    for (int k = 1; k < len; ++k) m = pr[k] > m ? pr[k] : m;
+    ring.gprio[slot] = m;
 }
 
 // get_batch's sample b (sample_n_games :102, sample_position :80,
@@ -49,12 +96,35 @@ __device__ __forceinline__ void rp_sample_one(const RpSampleParams& Q, int b, in
     const long long played = Q.counters[0];
     const int n = (int)(played < Q.cap ? played : Q.cap);
     const long long oldest = played - n + 1;                       // game number of ids[0]
-    const uint32_t gi = mz_rng_below(mz_rng_u32(Q.seed, MZ_RNG_GAME, (uint32_t)b, Q.step, 0), (uint32_t)n);   // :102
+    const uint32_t rg = mz_rng_u32(Q.seed, MZ_RNG_GAME, (uint32_t)b, Q.step, 0);
+    const uint32_t rp = mz_rng_u32(Q.seed, MZ_RNG_POS, (uint32_t)b, Q.step, 0);
+    uint32_t gi;
+    float gprob = 0.0f;
+    if (Q.per) {                                                   // Categorical(game_probs), :96-103
+        const double u = per_uniform(rg);
+        int lo = 0, hi = n - 1;                                    // first i with cum[i] >= u, else n-1
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((double)Q.per_cum[mid] >= u) hi = mid; else lo = mid + 1;
+        }
+        gi = (uint32_t)lo;
+        gprob = Q.per_p[lo];
+    } else {
+        gi = mz_rng_below(rg, (uint32_t)n);                        // :102
+    }
     const long long num = oldest + gi;
     const int slot = (int)((num - 1) % Q.cap);
     const size_t base = (size_t)slot * Q.T;
     const int T = Q.ring.len[slot];
-    const int pos = (int)mz_rng_below(mz_rng_u32(Q.seed, MZ_RNG_POS, (uint32_t)b, Q.step, 0), (uint32_t)T) + 1;  // :80
+    int pos;
+    if (Q.per) {                                                   // Categorical(position_probs), :75-78
+        float pprob = 0.0f;
+        pos = per_categorical(Q.ring.prio + base, T, per_uniform(rp), &pprob) + 1;
+        if (lane == 0)                                             // :213
+            Q.weights[b] = 1.0f / ((float)*Q.per_total * gprob * pprob);
+    } else {
+        pos = (int)mz_rng_below(rp, (uint32_t)T) + 1;              // :80
+    }
     const int K1 = Q.K + 1, A = Q.A;
     const float* rv = Q.ring.rv + base;
     const int32_t* tp = Q.ring.tp + base;
@@ -66,7 +136,7 @@ __device__ __forceinline__ void rp_sample_one(const RpSampleParams& Q, int b, in
         const int ci = pos + k;
         float v = 0.0f, r = 0.0f, a;
         if (ci < T) {
-            v = rp_target_value(Q, rv, tp, rew, T, ci);
+            v = rp_target_value(Q.td, Q.disc_pow, rv, tp, rew, T, ci);
             r = rew[ci - 1];
             a = (float)act[ci - 1];
         } else if (ci == T) {

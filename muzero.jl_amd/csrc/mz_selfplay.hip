@@ -236,8 +236,92 @@ extern "C" __global__ __launch_bounds__(256) void mz_sp_store(SpParams S) {
         S.ring.rv[dst + k] = S.hist.rv[src + k];
     }
     __syncthreads();                               // every thread has read len and done
+    if (S.per) {                                   // save_game's initial priorities (:136-143)
+        SpHist ring = S.ring;
+        per_init_slot(ring, slot, len, S.T, S.td, S.disc_pow, S.per_alpha, tid, blockDim.x);
+        __syncthreads();
+        if (tid == 0) per_game_max(ring, slot, len, S.T);
+    }
     if (tid == 0) { S.ring.len[slot] = len; S.hist.len[g] = 0; S.done[g] = 0; }
     if (tid < 64) env_reset(S, g, tid);
+}
+
+// ------------------------------------------------------------------- PER
+// initial priorities of one ring slot written by mz_replay_save_game
+extern "C" __global__ void mz_rp_per_init(SpHist ring, int slot, int len, int Tmax, int td, const float* disc_pow,
+                                          int alpha) {
+    per_init_slot(ring, slot, len, Tmax, td, disc_pow, alpha, threadIdx.x, blockDim.x);
+    __syncthreads();
+    if (threadIdx.x == 0) per_game_max(ring, slot, len, Tmax);
+}
+
+// sample_n_games' game probabilities (:91-99): the held games oldest first
+// (the Dict's game-number order), p_i = gprio_i / S with S the ascending f32
+// sum, cum_i the ascending f32 running sum of p; total_samples = Σ len.  One
+// lane: the f32 sums are sequential by definition.
+extern "C" __global__ void mz_rp_per_prep(SpHist ring, const long long* counters, int cap, float* cum, float* prob,
+                                          long long* total) {
+    if (threadIdx.x != 0) return;
+    const long long played = counters[0];
+    const int n = (int)(played < cap ? played : cap);
+    const long long oldest = played - n + 1;
+    float S = 0.0f;
+    long long tot = 0;
+    for (int i = 0; i < n; ++i) {
+        const int slot = (int)((oldest + i - 1) % cap);
+        S = S + ring.gprio[slot];
+        tot += ring.len[slot];
+    }
+    float c = 0.0f;
+    for (int i = 0; i < n; ++i) {
+        const float p = ring.gprio[(int)((oldest + i - 1) % cap)] / S;
+        c = c + p;
+        prob[i] = p;
+        cum[i] = c;
+    }
+    *total = tot;
+}
+
+// weight_batch ./= maximum(weight_batch) (:215)
+extern "C" __global__ void mz_rp_per_norm(float* w, int B) {
+    __shared__ float red[256];
+    const int tid = threadIdx.x;
+    float m = -INFINITY;
+    for (int i = tid; i < B; i += blockDim.x) m = w[i] > m ? w[i] : m;
+    red[tid] = m;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if (tid < o) red[tid] = red[tid + o] > red[tid] ? red[tid + o] : red[tid];
+        __syncthreads();
+    }
+    const float mx = red[0];
+    for (int i = tid; i < B; i += blockDim.x) w[i] = w[i] / mx;
+}
+
+// update_priorities! (ReplayBuffer.jl:168-183, Learning.jl:400-404) in its
+// intended reading (the reference's `minimum(a, b)` and its K+2-element slice
+// cannot run): for sample i in batch order, if game index[i] is still held,
+// positions pos..min(pos+K, len) get |pv − tv|^alpha of steps 0.., then the
+// game priority is their max.  Samples run in order (later ones overwrite),
+// lanes over the steps of one sample.
+extern "C" __global__ void mz_rp_per_update(SpHist ring, const long long* counters, int cap, int Tmax, int B, int K,
+                                            int alpha, const int32_t* index, const float* pv, const float* tv) {
+    const int lane = threadIdx.x;
+    const long long played = counters[0];
+    const long long held_from = played - (played < cap ? played : cap) + 1;
+    for (int i = 0; i < B; ++i) {
+        const long long num = index[2 * i];
+        const int pos = index[2 * i + 1];
+        if (num < held_from) continue;                     // evicted since it was sampled
+        const int slot = (int)((num - 1) % cap), len = ring.len[slot];
+        const int end = pos + K < len ? pos + K : len;     // 1-based, inclusive
+        float* pr = ring.prio + (size_t)slot * Tmax;
+        for (int k = pos + lane; k <= end; k += blockDim.x)
+            pr[k - 1] = per_priority(pv[(size_t)i * (K + 1) + (k - pos)] - tv[(size_t)i * (K + 1) + (k - pos)], alpha);
+        __syncthreads();
+        if (lane == 0) per_game_max(ring, slot, len, Tmax);
+        __syncthreads();
+    }
 }
 
 // ------------------------------------------------------------- replay sample

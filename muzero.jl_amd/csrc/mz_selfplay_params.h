@@ -22,6 +22,8 @@ struct SpHist {                 // a set of game records: [n][T] ...
     float* cv;                  // [n][T][A] child visit distributions
     float* rv;                  // [n][T] root values
     int32_t* len;               // [n] moves
+    float* prio;                // [n][T] PER position priorities (ring only, conf.PER)
+    float* gprio;               // [n] PER game priority = max(prio) (ring only)
 };
 
 struct SpParams {
@@ -43,6 +45,9 @@ struct SpParams {
     uint32_t step, game_offset;
     uint64_t seed;
     long long* eval_counts;     // [4] games, muzero wins, opponent wins, draws
+    // PER (conf.PER): initial priorities of a stored game (save_game, ReplayBuffer.jl:133-145)
+    int per, per_alpha, td;
+    const float* disc_pow;
 };
 
 // get_batch + make_target (ReplayBuffer.jl:5-50, 73-107, 188-217) on the shard
@@ -54,4 +59,12 @@ struct RpSampleParams {
     const float* disc_pow;      // [td + 2]: f32(discount^n) as Julia's Float32^Int
     float* obs; float* actions; float* tv; float* tr; float* tpol; float* gscale;
     int32_t* index;             // [B][2]: (game number, position) — index_batch
+    // PER (conf.PER): sample_n_games / sample_position by priority (:73-107)
+    // from the cumulative game probabilities of mz_rp_per_prep; raw IS weights
+    // 1/(total_samples·p_game·p_pos), normalised by mz_rp_per_norm (:211-215)
+    int per;
+    const float* per_cum;       // [n held] cumulative f32 game probabilities (oldest first)
+    const float* per_p;         // [n held] game probabilities
+    const long long* per_total; // total_samples of the held games
+    float* weights;             // [B]
 };

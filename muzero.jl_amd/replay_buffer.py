@@ -2,7 +2,7 @@
 
 FIFO buffer of GameHistory keyed by game id (save_game, :133-161; the
 RemoteBufferChannel Dict semantics, src/RemoteBufferChannel.jl), uniform
-sampling (PER=false, params.jl:11) with the engine's Philox streams instead of
+or prioritized (PER, :73-107, 133-145, 168-183) sampling with the engine's Philox streams instead of
 Julia's global RNG (quirk Q6), n-step value targets with the reference's
 exact indexing (quirk Q9), and batch assembly in the reference's column-major
 tuple layout (get_batch, :188-217).  One buffer per GPU shard.
@@ -67,6 +67,40 @@ def make_target(conf, h, state_index, seed=0, sample=0, step=0):
     return tv, tr, tp, ta
 
 
+def per_priority(x, alpha):
+    """|x|^PER_alpha as Julia's Float32^Int, restated as f64 repeated
+    multiplication rounded once to f32 (the kernels' per_priority)."""
+    ax = abs(float(np.float32(x)))
+    r = 1.0
+    for _ in range(alpha):
+        r = r * ax
+    return np.float32(r)
+
+
+def per_uniform(r):
+    """uniform in [0, 1) from a Philox draw (24 bits, exact)."""
+    return (r >> 8) * 5.9604644775390625e-08
+
+
+def per_categorical(w, u):
+    """Categorical over p_i = w_i / S (S = ascending f32 sum): the first index
+    whose ascending f32 running sum of p is >= u (else the last); returns
+    (index, p_index).  The restatement of rand(rng, Categorical(p)) used by
+    sample_n_games / sample_position with PER (ReplayBuffer.jl:75-78, 96-103)."""
+    f32 = np.float32
+    S = f32(0.0)
+    for x in w:
+        S = f32(S + f32(x))
+    i = 0
+    p = f32(f32(w[0]) / S)
+    c = p
+    while float(c) < u and i < len(w) - 1:
+        i += 1
+        p = f32(f32(w[i]) / S)
+        c = f32(c + p)
+    return i, p
+
+
 class ReplayBuffer:
     """Per-GPU buffer: Dict{game_id => GameHistory} with FIFO eviction."""
 
@@ -81,8 +115,13 @@ class ReplayBuffer:
     def __len__(self):
         return len(self.buffer)
 
-    def save_game(self, history: GameHistory):                  # :133-161 (PER=false)
+    def save_game(self, history: GameHistory):                  # :133-161
         n = len(history.root_values)
+        if self.conf.PER:                                       # initial priorities :136-143
+            history.priorities = np.array([per_priority(np.float32(history.root_values[i]) -
+                                                        compute_target_value(self.conf, history, i + 1),
+                                                        self.conf.PER_alpha) for i in range(n)], np.float32)
+            history.game_priority = np.float32(history.priorities.max())
         self.num_played_games += 1
         self.num_played_steps += n
         self.total_samples += n
@@ -110,15 +149,49 @@ class ReplayBuffer:
         tp = np.zeros((B, K + 1, A), np.float32)
         gs = np.zeros(B, np.float32)
         index_batch = []
+        per = bool(c.PER)
+        if per:                                                 # :190, :91-99
+            total = sum(len(h.root_values) for h in self.buffer.values())
+            gprio = [self.buffer[i].game_priority for i in ids]
+            wts = np.zeros(B, np.float32)
         for b in range(B):
-            gi = rng_below(rng_u32(self.seed, MZ_RNG_GAME, b, step, 0), n)       # sample_n_games :102
+            rg = rng_u32(self.seed, MZ_RNG_GAME, b, step, 0)
+            rp = rng_u32(self.seed, MZ_RNG_POS, b, step, 0)
+            if per:
+                gi, gprob = per_categorical(gprio, per_uniform(rg))                # sample_n_games :96-103
+            else:
+                gi = rng_below(rg, n)                                              # sample_n_games :102
             h = self.buffer[ids[gi]]
             T = len(h.root_values)
-            pos = rng_below(rng_u32(self.seed, MZ_RNG_POS, b, step, 0), T) + 1   # sample_position :80
+            if per:                                                                # sample_position :75-78
+                pi, pprob = per_categorical(h.priorities, per_uniform(rp))
+                pos = pi + 1
+                wts[b] = np.float32(1.0) / np.float32(np.float32(np.float32(total) * gprob) * pprob)   # :213
+            else:
+                pos = rng_below(rp, T) + 1                                         # sample_position :80
             tv[b], tr[b], tp[b], acts[b] = make_target(c, h, pos, self.seed, b, step)
             obs[b] = get_stacked_observations(h.observation_history, h.action_history, pos,
                                               c.stacked_observations, plane)
             gs[b] = min(K, len(h.action_history) + 1 - pos)                        # :212
             index_batch.append((ids[gi], pos))
-        return index_batch, dict(observation=obs, actions=acts, target_values=tv, target_rewards=tr,
-                                 target_policies=tp, gradient_scale=gs)
+        out = dict(observation=obs, actions=acts, target_values=tv, target_rewards=tr,
+                   target_policies=tp, gradient_scale=gs)
+        if per:
+            out["weights"] = (wts / wts.max()).astype(np.float32)                 # :215
+        return index_batch, out
+
+    def update_priorities(self, index_batch, predicted_values, target_values):
+        """update_priorities! (ReplayBuffer.jl:168-183, Learning.jl:400-404) in its
+        intended reading: sample i (batch order) sets positions pos..min(pos+K, len)
+        of its game, if still held, to |v̂ − v|^alpha of steps 0.., then the game
+        priority to their max.  predicted / target values: (B, K+1)."""
+        K, alpha = self.conf.num_unroll_steps, self.conf.PER_alpha
+        for i, (gid, pos) in enumerate(index_batch):
+            if gid not in self.buffer:
+                continue
+            h = self.buffer[gid]
+            end = min(pos + K, len(h.priorities))
+            for k in range(pos, end + 1):
+                h.priorities[k - 1] = per_priority(np.float32(predicted_values[i][k - pos]) -
+                                                   np.float32(target_values[i][k - pos]), alpha)
+            h.game_priority = np.float32(h.priorities.max())

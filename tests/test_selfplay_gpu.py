@@ -229,3 +229,104 @@ def test_evaluation_play_matches_host(kind, opp, mzp):
     with pytest.raises(abi.MzError, match="muzero_player"):
         ed.selfplay_mode(abi.SP_EVAL, abi.OPP_RANDOM, 3)
     eh.close(); ed.close()
+
+
+def _per_engines(G, moves, cap, host=True):
+    from muzero_jl_amd.selfplay import BatchedSelfPlay
+    mod, env_cls, env_kind = _env("ttt")
+    conf = dataclasses.replace(mod.conf, num_iters=6, replay_buffer_size=cap, PER=True, PER_alpha=1)
+    e1, e2 = _engines(mod, conf, mod.hyper, G)
+    sp = BatchedSelfPlay(e1, env_cls, G, game_offset=7, step0=100) if host else None
+    e2.selfplay_init(env_kind, G, cap)
+    if not host:
+        e1.selfplay_init(env_kind, G, cap)
+    for m in range(moves):
+        if host:
+            sp.play_move()
+        else:
+            e1.selfplay_move(100 + m, game_offset=7)
+        e2.selfplay_move(100 + m, game_offset=7)
+    return conf, sp, e1, e2
+
+
+def _np_losses(pv, pp, tv, tpol, gs, w):
+    """Learning.jl:261-288 with PER weights, in f64 (ref_semantics: the
+    policy term is Q11's mean_j(CE_j)·mean_i(w_i/g_i) broadcast)."""
+    B = pv.shape[0]
+    vl = np.mean(((pv.astype(np.float64) - tv) ** 2).sum(1) / gs * w)
+    lp = np.log(np.exp(pp.astype(np.float64)).sum(-1, keepdims=True))
+    ce = -(tpol * (pp - lp)).sum((1, 2))
+    return vl, ce.sum() * (w / gs.astype(np.float64)).sum() / (B * B)
+
+
+def test_per_replay_matches_host():
+    """PER on the device shard == the host ReplayBuffer mirror: initial
+    priorities (save_game), prioritized get_batch with its importance weights,
+    the weighted losses, and update_priorities! after each learner step."""
+    import torch
+    from muzero_jl_amd.replay_buffer import ReplayBuffer
+    conf, sp, eh, ed = _per_engines(16, 30, cap=24)
+    rb = ReplayBuffer(conf, seed=5)
+    for h in sp.finished:
+        rb.save_game(h)
+    assert ed.replay_counts()[1] == len(rb) == 24 and len(sp.finished) > 24     # the FIFO evicted
+
+    def same_priorities():
+        for i, (gid, h) in enumerate(rb.buffer.items()):
+            pr, gp = ed.replay_get_priorities(i)
+            assert np.array_equal(pr, h.priorities) and np.float32(gp) == h.game_priority, i
+
+    same_priorities()
+    B = 40
+    rb.conf = dataclasses.replace(conf, batch_size=B)
+    grad = torch.empty(ed.grad_count(), dtype=torch.float32, device="cuda")
+    losses = torch.empty(8, dtype=torch.float32, device="cuda")
+    for step in (1, 2, 3):
+        idx_h, bh = rb.get_batch(step)
+        b, idx_d = ed.replay_sample(B, step, index=True)
+        bd = ed.batch_to_host(b)
+        assert [tuple(x) for x in idx_d] == [tuple(x) for x in idx_h]
+        for k in bh:
+            assert np.array_equal(bd[k], bh[k]), (step, k)
+        assert bh["weights"].max() == 1.0
+        ed.learner_grad_dev([b.observation, b.actions, b.target_values, b.target_rewards, b.target_policies,
+                             b.gradient_scale, b.weights], B, grad.data_ptr(), losses.data_ptr())
+        pv, pp, _ = ed.debug_unroll(B)
+        lo = losses.cpu().numpy()
+        vl, pl = _np_losses(pv, pp, bh["target_values"], bh["target_policies"], bh["gradient_scale"],
+                            bh["weights"])
+        np.testing.assert_allclose([lo[0], lo[2]], [vl, pl], rtol=1e-4, atol=1e-6)
+        ed.replay_update_priorities()
+        rb.update_priorities(idx_h, pv, bh["target_values"])
+        same_priorities()
+    eh.close(); ed.close()
+
+
+def test_per_fused_learner_matches_separate_calls():
+    """With PER, mz_learner_train_dev (weights, losses, priority update fused)
+    == replay_sample + grad_dev(weights) + update_priorities + apply."""
+    import torch
+    from muzero_jl_amd.config import cos_schedule
+    conf, _, e1, e2 = _per_engines(16, 20, cap=64, host=False)
+    B = 32
+    grad = torch.empty(e1.grad_count(), dtype=torch.float32, device="cuda")
+    l1 = torch.empty(8, dtype=torch.float32, device="cuda")
+    l2 = torch.empty(8, dtype=torch.float32, device="cuda")
+    for step in (1, 2, 3):
+        eta = cos_schedule(step)
+        b, _ = e1.replay_sample(B, step)
+        e1.learner_grad_dev([b.observation, b.actions, b.target_values, b.target_rewards, b.target_policies,
+                             b.gradient_scale, b.weights], B, grad.data_ptr(), l1.data_ptr())
+        e1.replay_update_priorities()
+        e1.learner_apply_dev(grad.data_ptr(), 1.0, eta)
+        e2.learner_train_dev(B, step, eta, l2.data_ptr())
+        e1.sync(); e2.sync()
+        assert np.array_equal(l1.cpu().numpy()[:6], l2.cpu().numpy()[:6]), step
+        held = e1.replay_counts()[1]
+        for i in range(held):
+            p1, g1 = e1.replay_get_priorities(i)
+            p2, g2 = e2.replay_get_priorities(i)
+            assert np.array_equal(p1, p2) and g1 == g2
+        for n in range(3):
+            assert np.array_equal(e1.get_weights(n), e2.get_weights(n)), (step, n)
+    e1.close(); e2.close()
