@@ -98,9 +98,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU over RCCL ("nccl").  MZ_DIST_BACKEND=gloo with more ranks
+    # than GPUs rehearses the N > 1 path on a one-GPU box (ranks share device
+    # local % #GPUs; gloo all-reduces the CUDA gradient through the host)
+    backend = os.environ.get("MZ_DIST_BACKEND", "nccl")
+    local = local % torch.cuda.device_count() if backend != "nccl" else local
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     stream = torch.cuda.Stream(device=dev)        # non-null stream shared with libmz (events see it)
     torch.cuda.set_stream(stream)
