@@ -298,8 +298,8 @@ def main():
             "learner_steps_per_s": round(learner_sps, 1),
             "learner_config": {"batch_size": B, "num_unroll_steps": K, "mode": "ref_semantics",
                                "batch_source": "synthetic device batch" if game is atari else
-                               ("mz_learner_train_dev: device get_batch + make_target fused into the unroll, "
-                                "ADAM fused into the loss kernel" if world == 1 else
+                               ("mz_learner_train_dev: one launch — device get_batch + make_target + unroll + "
+                                "losses, ADAM into the second image set" if world == 1 else
                                 "mz_learner_grad_sampled_dev (device get_batch fused into the unroll) + RCCL "
                                 "all-reduce + mz_learner_apply_dev")},
             "selfplay_pipeline": pipe,

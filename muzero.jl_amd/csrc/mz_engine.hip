@@ -54,6 +54,8 @@ extern "C" __global__ void mz_search_small2(SmallParams P);
 extern "C" __global__ void mz_search_small4(SmallParams P);
 extern "C" __global__ void mz_unroll_small1(SmallUnrollParams P);
 extern "C" __global__ void mz_unroll_small2(SmallUnrollParams P);
+extern "C" __global__ void mz_learn_small1(SmallUnrollParams P, LearnParams L);
+extern "C" __global__ void mz_learn_small2(SmallUnrollParams P, LearnParams L);
 extern "C" __global__ void mz_search_kernel_hbm_res(SearchParams P);
 
 extern "C" __global__ void mz_unroll_kernel(UnrollParams P);
@@ -169,6 +171,10 @@ struct mz_handle {
     int sm_n_sim = 0, sm_n_root = 0;
     float* d_sm_w = nullptr;                // [n_sim + n_root][2][256][16] weight image (sim then root)
     float* d_sm_bias = nullptr;             // [n_sim + n_root][2][64]
+    // FC engines: a second image set (tile16 W/B, small W/bias) that the one-launch
+    // learner step (mz_learn_small*) writes while its unroll reads the current set;
+    // the host swaps the sets after the launch
+    float* d_Wp2 = nullptr; float* d_Bp2 = nullptr; float* d_sm_w2 = nullptr; float* d_sm_bias2 = nullptr;
     int* d_sm_srcw = nullptr; int* d_sm_srcb = nullptr;
     size_t sm_w_n = 0, sm_b_n = 0;
     int* d_sm_rec[3] = {nullptr, nullptr, nullptr};   // per T in {1,2,4}
@@ -626,6 +632,17 @@ static int repack(mz_handle* h, hipStream_t st = nullptr) {
                            h->d_flat, h->d_sm_srcw, h->d_sm_w, h->sm_w_n);
         hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->sm_b_n + T - 1) / T)), dim3(T), 0, st,
                            h->d_flat, h->d_sm_srcb, h->d_sm_bias, h->sm_b_n);
+    }
+    if (h->d_sm_w2) {                            // the second image set (one-launch learner step)
+        hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_w_n + T - 1) / T)), dim3(T), 0, st,
+                           h->d_flat, h->d_srcW, h->d_Wp2, h->packed_w_n);
+        if (h->packed_b_n)
+            hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_b_n + T - 1) / T)), dim3(T), 0, st,
+                               h->d_flat, h->d_srcB, h->d_Bp2, h->packed_b_n);
+        hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->sm_w_n + T - 1) / T)), dim3(T), 0, st,
+                           h->d_flat, h->d_sm_srcw, h->d_sm_w2, h->sm_w_n);
+        hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->sm_b_n + T - 1) / T)), dim3(T), 0, st,
+                           h->d_flat, h->d_sm_srcb, h->d_sm_bias2, h->sm_b_n);
     }
     MZ_TRY(h, hipGetLastError());
     return 0;
@@ -1147,6 +1164,15 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
     CK(al(&h->d_flat, h->nflat));
     CK(al(&h->d_Wp, h->packed_w_n));
     CK(al(&h->d_Bp, h->packed_b_n));
+    if (h->small_ok) {
+        CK(al(&h->d_Wp2, h->packed_w_n)); CK(al(&h->d_Bp2, h->packed_b_n));
+        CK(al(&h->d_sm_w2, h->sm_w_n)); CK(al(&h->d_sm_bias2, h->sm_b_n));
+        const void* kl[2] = {(const void*)mz_learn_small1, (const void*)mz_learn_small2};
+        for (int ti = 0; ti < 2; ++ti)
+            CK(hipFuncSetAttribute(kl[ti], hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)unroll_small_lds(h, ti)) == hipSuccess
+                   ? 0 : fail(h, "hipFuncSetAttribute(learn_small)"));
+    }
     CK(hipMemset(h->d_flat, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
     CK(repack(h));
     // tables: libm log2/sqrt on the host, the values the oracle computes inline
@@ -1537,6 +1563,9 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
 }
 
 static int fc_unroll(mz_handle* h, const mz_batch* b, hipStream_t st, const RpSampleParams* rp);
+static int small_unroll_ti(const mz_handle* h, int B);
+static int small_unroll_params(mz_handle* h, const mz_batch* b, int ti, const RpSampleParams* rp,
+                               SmallUnrollParams* Uo);
 
 // forward unroll + losses + ∇ = 2θ into grad_dev (device batch pointers)
 int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, void* stream) {
@@ -1554,30 +1583,13 @@ int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float*
 // inside the small unroll kernel when it applies, else by its own launch
 static int fc_unroll(mz_handle* h, const mz_batch* b, hipStream_t st, const RpSampleParams* rp) {
     const int B = b->batch_size, K = h->conf.num_unroll_steps, A = h->A;
-    const int ti_u = B <= 4 * h->n_cu ? 0 : 1;
-    // one item per thread in the unroll's per-step loops; a/|A| staging of 64 floats
-    const bool small_unroll = h->small_ok && (ti_u + 1) * h->H <= 256 && (ti_u + 1) * h->plane <= 256 &&
-                              (ti_u + 1) * (A + 2) <= SM_THREADS && (ti_u + 1) * (K + 1) <= 64;
-    if (small_unroll) {
+    const int ti_u = small_unroll_ti(h, B);
+    if (ti_u >= 0) {
         // the search's stage schedule and register images, T samples per
         // workgroup (ADAM keeps the images current)
         const int ti = ti_u, T = ti + 1;
-        const int* lay = h->sm_lay[ti];
         SmallUnrollParams U;
-        U.B = B; U.K = K; U.A = A; U.H = h->H; U.plane = h->plane; U.obs_feat = h->obs_feat;
-        U.obs = b->observation; U.actions = b->actions; U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
-        U.n_sim = h->sm_n_sim; U.n_root = h->sm_n_root; U.w_sim = h->d_sm_w;
-        U.w_root = h->d_sm_w + (size_t)h->sm_n_sim * SM_SLOTS * 256 * 16;
-        U.bias = h->d_sm_bias; U.rec = h->d_sm_rec[ti]; U.act_total = lay[0];
-        U.x_rep = lay[1]; U.x_pred = lay[2]; U.x_dyn = lay[3]; U.h_out = lay[4]; U.v_out = lay[5];
-        U.p_out = lay[6]; U.r_out = lay[7]; U.v_act = h->lay.v_act; U.r_act = h->lay.r_act;
-        U.stamps = nullptr;
-#ifdef MZ_STAMPS
-        if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * std::max(h->max_games, B)));
-        U.stamps = h->d_stamps;
-#endif
-        U.sample = rp != nullptr;
-        if (rp) U.rp = *rp; else std::memset(&U.rp, 0, sizeof(U.rp));
+        if (small_unroll_params(h, b, ti, rp, &U)) return -1;
         void* args[] = {&U};
         MZ_TRY(h, hipLaunchKernel(ti == 0 ? (const void*)mz_unroll_small1 : (const void*)mz_unroll_small2,
                                   dim3((B + T - 1) / T), dim3(SM_THREADS), args, unroll_small_lds(h, ti), st));
@@ -1594,6 +1606,43 @@ static int fc_unroll(mz_handle* h, const mz_batch* b, hipStream_t st, const RpSa
                            (size_t)h->lay.total * 4, st, U);
     }
     MZ_TRY(h, hipGetLastError());
+    return 0;
+}
+
+// T = 2 when B exceeds 4 samples per CU; -1 if the small unroll cannot hold the nets
+static int small_unroll_ti(const mz_handle* h, int B) {
+    const int K = h->conf.num_unroll_steps, A = h->A;
+    const int ti_u = B <= 4 * h->n_cu ? 0 : 1;
+    // one item per thread in the unroll's per-step loops; a/|A| staging of 64 floats
+    const bool ok = h->small_ok && (ti_u + 1) * h->H <= 256 && (ti_u + 1) * h->plane <= 256 &&
+                    (ti_u + 1) * (A + 2) <= SM_THREADS && (ti_u + 1) * (K + 1) <= 64;
+    return ok ? ti_u : -1;
+}
+
+// parameters of mz_unroll_small* / mz_learn_small* for batch b (T = ti + 1
+// samples per workgroup, the search's stage schedule and register images)
+static int small_unroll_params(mz_handle* h, const mz_batch* b, int ti, const RpSampleParams* rp,
+                               SmallUnrollParams* Uo) {
+    const int B = b->batch_size, K = h->conf.num_unroll_steps, A = h->A;
+    {
+        const int* lay = h->sm_lay[ti];
+        SmallUnrollParams U;
+        U.B = B; U.K = K; U.A = A; U.H = h->H; U.plane = h->plane; U.obs_feat = h->obs_feat;
+        U.obs = b->observation; U.actions = b->actions; U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
+        U.n_sim = h->sm_n_sim; U.n_root = h->sm_n_root; U.w_sim = h->d_sm_w;
+        U.w_root = h->d_sm_w + (size_t)h->sm_n_sim * SM_SLOTS * 256 * 16;
+        U.bias = h->d_sm_bias; U.rec = h->d_sm_rec[ti]; U.act_total = lay[0];
+        U.x_rep = lay[1]; U.x_pred = lay[2]; U.x_dyn = lay[3]; U.h_out = lay[4]; U.v_out = lay[5];
+        U.p_out = lay[6]; U.r_out = lay[7]; U.v_act = h->lay.v_act; U.r_act = h->lay.r_act;
+        U.stamps = nullptr;
+#ifdef MZ_STAMPS
+        if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * std::max(h->max_games, B)));
+        U.stamps = h->d_stamps;
+#endif
+        U.sample = rp != nullptr;
+        if (rp) U.rp = *rp; else std::memset(&U.rp, 0, sizeof(U.rp));
+        *Uo = U;
+    }
     return 0;
 }
 
@@ -2107,6 +2156,26 @@ static int learner_sampled(mz_handle* h, int32_t B, uint32_t step, float* grad_d
         if (rlearner_grad(h, &b, train ? nullptr : grad_dev, losses_dev, st)) return -1;
         if (per_update(h, B, st)) return -1;                       // Learning.jl:400-404
         return train ? mz_learner_apply_dev(h, nullptr, 1.0f, eta, st) : 0;
+    }
+    const int ti = small_unroll_ti(h, B);
+    if (train && ti >= 0 && !h->conf.PER && h->A <= 16 && h->d_sm_w2 && !std::getenv("MZ_LEARN_2LAUNCH")) {
+        // one launch: unroll + losses ‖ Σθ² + ADAM into the second image set, then swap the sets
+        SmallUnrollParams U;
+        if (small_unroll_params(h, &b, ti, &Q, &U)) return -1;
+        LearnParams L;
+        L.nU = (B + ti) / (ti + 1);
+        L.tv = b.target_values; L.tp = b.target_policies; L.gscale = b.gradient_scale;
+        L.terms = h->d_lterm; L.flat = h->d_flat; L.netoff = h->d_netoff; L.part = h->d_sq; L.counter = h->d_counter;
+        L.out = losses_dev ? losses_dev : h->d_loss;
+        L.ad = LgAdam{1, h->d_m, h->d_v, h->bp1, h->bp2, eta, h->d_Wp2, h->d_Bp2, h->d_inv_tile, h->d_sm_w2,
+                      h->d_sm_bias2, h->d_inv_small};
+        void* args[] = {&U, &L};
+        MZ_TRY(h, hipLaunchKernel(ti == 0 ? (const void*)mz_learn_small1 : (const void*)mz_learn_small2,
+                                  dim3(L.nU + LEARN_L2_GROUPS), dim3(SM_THREADS), args, unroll_small_lds(h, ti), st));
+        std::swap(h->d_Wp, h->d_Wp2); std::swap(h->d_Bp, h->d_Bp2);
+        std::swap(h->d_sm_w, h->d_sm_w2); std::swap(h->d_sm_bias, h->d_sm_bias2);
+        adam_advance(h);
+        return 0;
     }
     if (fc_unroll(h, &b, st, &Q)) return -1;
     if (per_norm(h, B, st)) return -1;

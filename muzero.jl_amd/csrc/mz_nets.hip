@@ -4,6 +4,7 @@
 // ADAM (Flux 0.12 ADAMW()[1]) and re-packing of the MFMA weight image.
 #include "mz_mlp_device.h"
 #include "mz_tree_device.h"
+#include "mz_learner_device.h"
 
 // One plan over tiles of 16 samples: x (in_feat, n) column-major in HBM ->
 // LDS -> plan -> out0 (o0 rows) / out1 (o1 rows, softmaxed if sm1).
@@ -96,81 +97,19 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_unroll_kernel(Unroll
     }
 }
 
-// One launch after the unroll (Learning.jl:261-288, 380-393 in ref_semantics):
-//  * blocks [0, nlb): one 16-lane group per (sample, step) t, lane a = action
-//    a: read-outs on the raw unroll outputs — policy = softmax of the logits
-//    (max, det_expf, ascending sum, divide), value / reward = their
-//    activations — then the step's terms: squared value error and the
-//    logitcrossentropy of the probabilities (Q11's double softmax), every
-//    sum in ascending action order (g16_seqsum);
-//  * blocks [nlb, nlb + 3·MZ_L2_BLOCKS): θ² of a fixed slice summed in f64,
-//    and ∇ = 2θ written for it (Q11: only sum(sqnorm, params) depends on θ);
-//  * the last block to finish folds each sample's steps in ascending k, the
-//    cross-sample sums in f64 (tolerance-checked, not bitwise), and the Σθ²
-//    partials in a fixed order (one wave per net), then resets the counter.
-// out: [0] value, [1] reward (0, intermediate_rewards = false), [2] policy,
-// [3..5] Σθ² of repr / pred / dyn.
-
-// Flux 0.12 apply!(ADAM) + WeightDecay(0) + `x .-= Δ` (Learning.jl:395-397)
-// for parameter i with gradient g.  bp = (β1^t, β2^t) of the current step.
-// The new value is also scattered into the search / unroll images through
-// the inverse maps (each parameter has one position in each image), so the
-// images never need a repack after a learner step.
-__device__ __forceinline__ void mz_scatter(float x, int code, float* w, float* b) {
-    if (code >= 0) w[code] = x;
-    else if (code <= -2) b[-code - 2] = x;
-}
-// adam_update of P[i0 + u·stride] (u < 4, u·stride < rem) with g = 2·x[u]
-// (x[u] = the current value): all loads first, then the four updates
-__device__ __forceinline__ void adam_update4(const LgAdam& ad, float* P, size_t i0, size_t stride, size_t rem,
-                                             const float (&x)[4]) {
-    const double b1 = 0.9, b2 = 0.999, eps = 1e-8;
-    float mo[4], vo[4];
-    int it[4], is[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const size_t i = i0 + u * stride;
-        const bool in = u * stride < rem;
-        mo[u] = in ? ad.M[i] : 0.0f; vo[u] = in ? ad.V[i] : 0.0f;
-        it[u] = in ? ad.inv_tile[i] : -1; is[u] = in ? ad.inv_small[i] : -1;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        if (u * stride >= rem) continue;
-        const size_t i = i0 + u * stride;
-        const float g = x[u] * 2.0f;
-        const float m = (float)(b1 * (double)mo[u] + (1.0 - b1) * (double)g);
-        const float g2 = g * g;
-        const float v = (float)(b2 * (double)vo[u] + (1.0 - b2) * (double)g2);
-        ad.M[i] = m; ad.V[i] = v;
-        const float d = (float)((double)m / (1.0 - ad.bp1) / (sqrt((double)v / (1.0 - ad.bp2)) + eps) * ad.eta);
-        const float xn = x[u] - d;
-        P[i] = xn;
-        mz_scatter(xn, it[u], ad.Wp, ad.Bp);
-        mz_scatter(xn, is[u], ad.smw, ad.smb);
-    }
-}
-__device__ __forceinline__ void adam_update(const LgAdam& ad, float* P, size_t i, float g) {
-    const double b1 = 0.9, b2 = 0.999, eps = 1e-8;
-    const float m = (float)(b1 * (double)ad.M[i] + (1.0 - b1) * (double)g);
-    const float g2 = g * g;
-    const float v = (float)(b2 * (double)ad.V[i] + (1.0 - b2) * (double)g2);
-    ad.M[i] = m; ad.V[i] = v;
-    const float d = (float)((double)m / (1.0 - ad.bp1) / (sqrt((double)v / (1.0 - ad.bp2)) + eps) * ad.eta);
-    const float x = P[i] - d;
-    P[i] = x;
-    mz_scatter(x, ad.inv_tile[i], ad.Wp, ad.Bp);
-    mz_scatter(x, ad.inv_small[i], ad.smw, ad.smb);
-}
-#define MZ_FOLD_K1 8    // K + 1 up to this: the fold stages the step terms in LDS
+// One launch after the unroll (Learning.jl:261-288, 380-393 in ref_semantics;
+// pieces in mz_learner_device.h):
+//  * blocks [0, nlb): one GW-lane group per (sample, step), lg_step_terms;
+//  * blocks [nlb, nlb + 3·MZ_L2_BLOCKS): lg_l2_slice (Σθ², ∇ = 2θ or the
+//    fused ADAM);
+//  * the last block out folds (lg_fold).
 template <int GW>
 __device__ __forceinline__ void learner_grad_body(
     int B, int K, int A, int v_act, int r_act, float* pv, float* pp, float* pr, const float* tv, const float* tp,
     const float* gscale, float* terms, float* flat, const size_t* netoff, float* G, double* part,
     unsigned* counter, float* out, const float* wts, LgAdam ad) {
-    __shared__ double red_v[MZ_THREADS], red_p[MZ_THREADS], red_c[MZ_THREADS];
+    __shared__ double red[MZ_THREADS];
     __shared__ float stg[MZ_THREADS];
-    __shared__ bool last;
     const int tid = threadIdx.x;
     const int n = B * (K + 1);
     const int nlb = (n + MZ_THREADS / GW - 1) / (MZ_THREADS / GW);
@@ -178,129 +117,16 @@ __device__ __forceinline__ void learner_grad_body(
     float* cet = terms + n;
     if ((int)blockIdx.x < nlb) {
         const int t = blockIdx.x * (MZ_THREADS / GW) + tid / GW, a = tid % GW;
-        float* st = stg + (tid & ~(GW - 1));
-        if (t < n) {                            // whole GW-lane groups are in or out
-            const bool in = a < A;
-            float* yh = pp + (size_t)t * A;
-            const float x = in ? yh[a] : -INFINITY;
-            const float m = gmax<GW>(x);
-            const float e = in ? det_expf(x - m) : 0.0f;
-            const float s = gseqsum<GW>(e, A, st, a);
-            const float p = in ? e / s : -INFINITY;
-            if (in) yh[a] = p;
-            const float m2 = gmax<GW>(p);
-            const float e2 = in ? det_expf(p - m2) : 0.0f;
-            const float se = gseqsum<GW>(e2, A, st, a);
-            const float ls = det_logf(se);
-            const float term = in ? tp[(size_t)t * A + a] * ((p - m2) - ls) : 0.0f;
-            const float ce = gseqsum<GW>(term, A, st, a);
-            if (a == 0) {
-                const float v = mz_post_act(v_act, pv[t]);
-                pv[t] = v;
-                pr[t] = mz_post_act(r_act, pr[t]);
-                const float d = v - tv[t];
-                vsq[t] = d * d;
-                cet[t] = ce;
-            }
-        }
+        if (t < n)                              // whole GW-lane groups are in or out
+            lg_step_terms<GW>(t, a, A, v_act, r_act, pv, pp, pr, tv, tp, vsq, cet, stg + (tid & ~(GW - 1)));
     } else {
         const int nb = blockIdx.x - nlb;
         const int net = nb / MZ_L2_BLOCKS, blk = nb % MZ_L2_BLOCKS;
-        const size_t off = netoff[net], cnt = netoff[3 + net];
-        double s = 0.0;
-        // elements i, i + stride, ... as one thread's ascending f64 sum; four per
-        // pass with every load issued before any store (the fused ADAM's f64
-        // chains then overlap)
-        const size_t stride = (size_t)MZ_L2_BLOCKS * blockDim.x;
-        for (size_t i = (size_t)blk * blockDim.x + tid; i < cnt; i += 4 * stride) {
-            float x[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) x[u] = i + u * stride < cnt ? flat[off + i + u * stride] : 0.0f;
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (i + u * stride < cnt) s += (double)x[u] * (double)x[u];
-            if (ad.on) {                        // = mz_adam_kernel with G = 2θ, gscale 1
-                adam_update4(ad, flat, off + i, stride, cnt - i, x);
-            } else {
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (i + u * stride < cnt) G[off + i + u * stride] = x[u] * 2.0f;
-            }
-        }
-        red_v[tid] = s;
-        __syncthreads();
-        for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-            if (tid < o) red_v[tid] += red_v[tid + o];
-            __syncthreads();
-        }
-        if (tid == 0) part[net * MZ_L2_BLOCKS + blk] = red_v[0];
+        red[tid] = lg_l2_slice(net, blk, tid, netoff, flat, G, ad);
+        lg_tree256(red, tid);
+        if (tid == 0) part[net * MZ_L2_BLOCKS + blk] = red[0];
     }
-    // the last block out folds
-    __syncthreads();
-    if (tid == 0) {
-        __threadfence();
-        last = atomicAdd(counter, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    double sv = 0.0, sg = 0.0, sc = 0.0;
-    // per sample j (thread j mod blockDim): its K+1 steps in ascending k.  The
-    // terms of blockDim samples at a time are first staged in LDS by all
-    // threads (one load each, all in flight), so no thread walks a chain of
-    // dependent global loads
-    __shared__ float fv[MZ_THREADS * MZ_FOLD_K1], fc[MZ_THREADS * MZ_FOLD_K1];
-    const int K1 = K + 1;
-    for (int j0 = 0; j0 < B; j0 += blockDim.x) {
-        const int nj = B - j0 < (int)blockDim.x ? B - j0 : (int)blockDim.x;
-        const bool staged = K1 <= MZ_FOLD_K1;
-        if (staged) {
-            for (int e = tid; e < nj * K1; e += blockDim.x) {
-                fv[e] = __hip_atomic_load(vsq + (size_t)j0 * K1 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                fc[e] = __hip_atomic_load(cet + (size_t)j0 * K1 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __syncthreads();
-        }
-        if (tid < nj) {
-            const int j = j0 + tid;
-            float s = 0.0f, c = 0.0f;
-            for (int k = 0; k < K1; ++k) {
-                const float vk = staged ? fv[tid * K1 + k]
-                                        : __hip_atomic_load(vsq + (size_t)j * K1 + k, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT);
-                const float ck = staged ? fc[tid * K1 + k]
-                                        : __hip_atomic_load(cet + (size_t)j * K1 + k, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT);
-                s = s + vk;
-                c = c + (-ck);
-            }
-            const float w = wts ? wts[j] : 1.0f;   // PER importance weights (Learning.jl:271-285)
-            sv += (double)((s / gscale[j]) * w);
-            sc += (double)c;                    // Σ_k ce_k
-            sg += (double)w / (double)gscale[j];   // Σ_j w_j/g_j
-        }
-        if (staged) __syncthreads();
-    }
-    red_v[tid] = sv; red_p[tid] = sg; red_c[tid] = sc;
-    __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-        if (tid < o) { red_v[tid] += red_v[tid + o]; red_p[tid] += red_p[tid + o]; red_c[tid] += red_c[tid + o]; }
-        __syncthreads();
-    }
-    if (tid == 0) {
-        out[0] = (float)(red_v[0] / (double)B);
-        out[1] = 0.0f;                          // intermediate_rewards = false (:276-280)
-        out[2] = (float)(red_c[0] * red_p[0] / ((double)B * (double)B));  // mean over (1,B,B), Q11
-        *counter = 0u;
-    }
-    if (tid < 192) {                            // wave w folds net w's partials: fixed pairs, then a fixed tree
-        const int net = tid >> 6, j = tid & 63;
-        double s = 0.0;
-        for (int b = j; b < MZ_L2_BLOCKS; b += 64)
-            s += __hip_atomic_load(part + net * MZ_L2_BLOCKS + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-        if (j == 0) out[3 + net] = (float)s;
-    }
+    lg_fold(B, K, vsq, cet, gscale, wts, part, counter, out);
 }
 #define MZ_LG_ARGS int B, int K, int A, int v_act, int r_act, float* pv, float* pp, float* pr, const float* tv, \
     const float* tp, const float* gscale, float* terms, float* flat, const size_t* netoff, float* G, \

@@ -23,6 +23,7 @@
 
 #include "mz_small_params.h"
 #include "mz_replay_device.h"
+#include "mz_learner_device.h"
 
 #ifdef MZ_STAMPS
 #define SM_STAMP(i)                                                              \
@@ -412,12 +413,14 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
     const int pl_t = tid - 256;                                       // a/|A| plane: threads 256..
     const int pl_gl = pl_t >= 0 ? pl_t / P.plane : 0, pl_k = pl_t - pl_gl * P.plane;
     const int o_gl = tid / (A + 2), o_c = tid - o_gl * (A + 2);      // raw outputs: tid < T*(A+2)
-    // weight-image loads first: in flight under the setup copies
+    // get_batch of this tile's samples on waves 0..T-1, BEFORE their weight
+    // loads: a wave's loads complete in order (vmcnt), so behind 56 image
+    // loads the sampler's dependent chain would start only once they land
+    if (P.sample && (tid >> 6) < T && tile0 + (tid >> 6) < P.B)
+        rp_sample_one(P.rp, tile0 + (tid >> 6), tid & 63);
     float wr[SM_MAX_SIM][16];
     sm_load<SM_MAX_SIM>(0, P.n_root, P.w_root, wr);
     sm_load<SM_MAX_SIM>(P.n_root, P.n_sim, P.w_sim, wr);   // sim stages the representation leaves free
-    if (P.sample && (tid >> 6) < T && tile0 + (tid >> 6) < P.B)   // get_batch of this tile's samples
-        rp_sample_one(P.rp, tile0 + (tid >> 6), tid & 63);
     for (int i = tid; i < P.act_total; i += SM_THREADS) act[i] = 0.0f;
     for (int i = tid; i < nrec * SM_REC_INTS; i += SM_THREADS) rec[i] = P.rec[i];
     __syncthreads();
@@ -488,4 +491,59 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
 
 extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small1(SmallUnrollParams P) { unroll_body<1>(P); }
 extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small2(SmallUnrollParams P) { unroll_body<2>(P); }
+
+// One learner iteration in one launch (LearnParams): unroll (+ get_batch) and
+// each tile's loss terms ‖ Σθ² + ADAM into the second image set; last block
+// folds.  Same results as mz_unroll_small* + mz_learner_grad_kernel (fused
+// ADAM): the loss terms, the θ² slices (256-thread groups) and the fold are
+// the same code on the same decomposition.
+template <int T>
+__device__ __forceinline__ void learn_body(const SmallUnrollParams& P, const LearnParams& L) {
+    __shared__ float stg[SM_THREADS];
+    __shared__ double red[SM_THREADS];
+    const int tid = threadIdx.x;
+    const int K1 = P.K + 1, n = P.B * K1;
+    float* vsq = L.terms;
+    float* cet = L.terms + n;
+#ifdef MZ_STAMPS
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+#endif
+    if ((int)blockIdx.x < L.nU) {
+        unroll_body<T>(P);
+#ifdef MZ_STAMPS
+        const unsigned long long t_unroll = __builtin_amdgcn_s_memtime();
+#endif
+        __syncthreads();                               // the tile's raw outputs -> its loss groups
+        const int g16 = tid >> 4, a = tid & 15, gl = g16 / K1, k = g16 - gl * K1;
+        const int b = blockIdx.x * T + gl;
+        if (gl < T && b < P.B)
+            lg_step_terms<16>(b * K1 + k, a, P.A, P.v_act, P.r_act, P.pv, P.pp, P.pr, L.tv, L.tp, vsq, cet,
+                              stg + (tid & ~15));
+#ifdef MZ_STAMPS   // slot 6: unroll start -> end, slot 7: loss terms (wave 0)
+        if (tid == 0 && P.stamps) {
+            P.stamps[blockIdx.x * 8 + 6] = t_unroll - t_start;
+            P.stamps[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memtime() - t_unroll;
+        }
+#endif
+    } else {
+        const int half = tid >> 8, t256 = tid & (MZ_THREADS - 1);
+        const int vb = ((int)blockIdx.x - L.nU) * 2 + half;
+        const int net = vb / MZ_L2_BLOCKS, blk = vb % MZ_L2_BLOCKS;
+        red[tid] = lg_l2_slice(net, blk, t256, L.netoff, L.flat, nullptr, L.ad);
+        __syncthreads();
+        for (int o = MZ_THREADS / 2; o > 0; o >>= 1) {            // lg_tree256 on each half
+            if (t256 < o) red[tid] += red[tid + o];
+            __syncthreads();
+        }
+        if (t256 == 0) L.part[net * MZ_L2_BLOCKS + blk] = red[tid];
+    }
+    lg_fold(P.B, P.K, vsq, cet, L.gscale, nullptr, L.part, L.counter, L.out);
+}
+
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_small1(SmallUnrollParams P, LearnParams L) {
+    learn_body<1>(P, L);
+}
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_small2(SmallUnrollParams P, LearnParams L) {
+    learn_body<2>(P, L);
+}
 

@@ -63,3 +63,17 @@ struct SmallUnrollParams {
     RpSampleParams rp;
 };
 
+// One-launch learner step (mz_learn_small*, mz_learner_train_dev on one GPU,
+// PER off): blocks [0, nU) are the unroll workgroups of SmallUnrollParams,
+// which then compute their samples' loss terms; blocks [nU, nU + 48) run the
+// Σθ² slices with ADAM (two 256-thread slices each) writing the new values into
+// the engine's second image set, so the unroll blocks' weight loads never
+// race them; the last block folds the losses.
+struct LearnParams {
+    int nU;
+    const float* tv; const float* tp; const float* gscale;
+    float* terms; float* flat; const size_t* netoff; double* part; unsigned* counter; float* out;
+    LgAdam ad;
+};
+#define LEARN_L2_GROUPS (3 * MZ_L2_BLOCKS / 2)
+
