@@ -330,3 +330,27 @@ def test_per_fused_learner_matches_separate_calls():
         for n in range(3):
             assert np.array_equal(e1.get_weights(n), e2.get_weights(n)), (step, n)
     e1.close(); e2.close()
+
+
+def test_per_host_save_game_priorities():
+    """mz_replay_save_game with PER: the initial priorities of host-played games
+    (save_game, ReplayBuffer.jl:136-143) equal the host mirror's."""
+    from muzero_jl_amd import abi
+    from muzero_jl_amd.replay_buffer import ReplayBuffer
+    from muzero_jl_amd.selfplay import BatchedSelfPlay
+    mod, env_cls, env_kind = _env("ttt")
+    conf = dataclasses.replace(mod.conf, num_iters=4, replay_buffer_size=8, PER=True, PER_alpha=2)
+    e1, e2 = _engines(mod, conf, mod.hyper, 8)
+    sp = BatchedSelfPlay(e1, env_cls, 8, step0=3)
+    for _ in range(24):
+        sp.play_move()
+    e2.selfplay_init(env_kind, 8, 8)
+    rb = ReplayBuffer(conf, seed=1)
+    for h in sp.finished:
+        e2.replay_save_game(h)
+        rb.save_game(h)
+    assert len(rb) == e2.replay_counts()[1] > 0
+    for i, h in enumerate(rb.buffer.values()):
+        pr, gp = e2.replay_get_priorities(i)
+        assert np.array_equal(pr, h.priorities) and np.float32(gp) == h.game_priority
+    e1.close(); e2.close()
