@@ -319,8 +319,19 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         if (tid < 64) {
             // ---- value / reward read-out activations, then backpropagate! (:190-217)
             if (active) {
-                const float val = mz_post_act(P.v_act, act[P.v_out + g]);
-                const float rew = mz_post_act(P.r_act, act[P.r_out + g]);
+                // one activation per lane (even lanes the value, odd the reward, both
+                // f64 tanh chains run at once), then each quad's lanes 0 / 1 to all
+                // four by DPP quad_perm [0,0,0,0] / [1,1,1,1]
+                const bool odd = (a & 1) != 0;
+                const float ro = mz_post_act(odd ? P.r_act : P.v_act, act[(odd ? P.r_out : P.v_out) + g]);
+                const float val = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                    0, __builtin_bit_cast(int, ro), 0x00, 0xF, 0xF, false));
+                const float rew = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                    0, __builtin_bit_cast(int, ro), 0x55, 0xF, 0xF, false));
+#ifdef MZ_STAMPS
+                if (threadIdx.x == 0) asm volatile("" :: "v"(val), "v"(rew));
+#endif
+                SM_STAMP(5);                    // stamp build: slot 5 = the read-out activations
                 const int tl = sg_vtp[g];
                 const int depth = sg_depth[g];
                 if (a == 0) {
@@ -351,7 +362,6 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         }
         __syncthreads();
         SM_STAMP(4);
-        SM_STAMP(5);
     }
     __syncthreads();
 
