@@ -100,13 +100,16 @@ __device__ __forceinline__ void lg_step_terms(int t, int a, int A, int v_act, in
     const float ls = det_logf(se);
     const float term = in ? tp[(size_t)t * A + a] * ((p - m2) - ls) : 0.0f;
     const float ce = gseqsum<GW>(term, A, st, a);
-    if (a == 0) {
-        const float v = mz_post_act(v_act, pv[t]);
-        pv[t] = v;
-        pr[t] = mz_post_act(r_act, pr[t]);
-        const float d = v - tv[t];
-        vsq[t] = d * d;
-        cet[t] = ce;
+    if (a < 2) {                                // lane 0 the value, lane 1 the reward read-out, at once
+        const float y = mz_post_act(a == 0 ? v_act : r_act, a == 0 ? pv[t] : pr[t]);
+        if (a == 0) {
+            pv[t] = y;
+            const float d = y - tv[t];
+            vsq[t] = d * d;
+            cet[t] = ce;
+        } else {
+            pr[t] = y;
+        }
     }
 }
 
