@@ -227,6 +227,22 @@ int mz_learner_grad_dev(mz_handle* h, const mz_batch* dev_batch, float* grad_dev
 int mz_learner_apply_dev(mz_handle* h, const float* grad_dev, float grad_scale,
                          double eta, void* stream);
 
+/* ---- Data-parallel learner over RCCL -------------------------
+ * For hosts without torch.distributed (the Julia binding): one RCCL
+ * communicator per handle, one handle per GPU.  Rank 0 calls
+ * mz_dp_unique_id and hands the 128-byte id to every rank out of band (the
+ * RemoteChannel / Distributed.jl of the reference host); each rank calls
+ * mz_dp_init.  mz_dp_allreduce sums the gradient bucket (mz_grad_count
+ * floats, grad_dev or the handle's gradient if NULL) in place over RCCL on
+ * `stream`; mz_learner_train_dp = mz_learner_grad_sampled_dev + that
+ * all-reduce + mz_learner_apply_dev(1/world).  librccl.so.1 is loaded on
+ * first use (the copy already in the process if any).                      */
+#define MZ_DP_ID_BYTES 128
+int mz_dp_unique_id(uint8_t* id);
+int mz_dp_init(mz_handle* h, int rank, int world, const uint8_t* id);
+int mz_dp_allreduce(mz_handle* h, float* grad_dev, void* stream);
+int mz_learner_train_dp(mz_handle* h, int32_t B, uint32_t step, double eta, float* losses_dev, void* stream);
+
 /* ---- Device self-play and replay shard ------------
  * The loop body of play_game (SelfPlay.jl:330-382) and the replay buffer
  * (ReplayBuffer.jl) kept in HBM: no host round trip per move or per batch. */

@@ -61,6 +61,10 @@ SIGNATURES = {
     "mz_learner_apply_dev": (ctypes.c_int, [_VP, _VP, ctypes.c_float, ctypes.c_double, _VP]),
     "mz_selfplay_init": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "mz_selfplay_move": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float, _VP]),
+    "mz_dp_unique_id": (ctypes.c_int, [_VP]),
+    "mz_dp_init": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP]),
+    "mz_dp_allreduce": (ctypes.c_int, [_VP, _VP, _VP]),
+    "mz_learner_train_dp": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.c_double, _VP, _VP]),
     "mz_selfplay_mode": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "mz_eval_results": (ctypes.c_int, [_VP, _VP]),
     "mz_replay_counts": (ctypes.c_int, [_VP, _VP, _VP]),
@@ -357,6 +361,28 @@ class Engine:
         """One GPU: replay_sample + learner_grad_dev + learner_apply_dev(scale 1) in two launches."""
         self._check(self.lib.mz_learner_train_dev(self.h, B, step, float(eta), losses_ptr, stream),
                     "mz_learner_train_dev")
+
+    # ---- data-parallel learner over RCCL through the C ABI (SURVEY §8e)
+    @staticmethod
+    def dp_unique_id():
+        """128-byte RCCL id (rank 0; hand it to every rank out of band)."""
+        lib = load_library()
+        buf = (ctypes.c_uint8 * 128)()
+        if lib.mz_dp_unique_id(buf) != 0:
+            raise MzError("mz_dp_unique_id failed (librccl.so.1)")
+        return bytes(buf)
+
+    def dp_init(self, rank, world, uid):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        self._check(self.lib.mz_dp_init(self.h, rank, world, buf), "mz_dp_init")
+
+    def dp_allreduce(self, grad_ptr=None, stream=None):
+        self._check(self.lib.mz_dp_allreduce(self.h, grad_ptr, stream), "mz_dp_allreduce")
+
+    def learner_train_dp(self, B, step, eta, losses_ptr=None, stream=None):
+        """grad_sampled_dev + RCCL all-reduce + apply(1/world) in one call."""
+        self._check(self.lib.mz_learner_train_dp(self.h, B, step, float(eta), losses_ptr, stream),
+                    "mz_learner_train_dp")
 
     def batch_to_host(self, b):
         """Copy a device MzBatch (from replay_sample) into the host dict layout of ReplayBuffer.get_batch."""

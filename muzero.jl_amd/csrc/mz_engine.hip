@@ -5,6 +5,7 @@
 // image, owns every device buffer of one engine (one handle per GPU), and
 // launches the search / forward / learner kernels on the handle's stream.
 #include <hip/hip_runtime.h>
+#include <dlfcn.h>
 
 #include <cmath>
 #include <cstdio>
@@ -161,6 +162,7 @@ struct mz_handle {
     float* d_rs_w = nullptr; float* d_per_cum = nullptr; float* d_per_p = nullptr;   // PER sampling
     long long* d_per_total = nullptr;
     int rs_last_B = 0;                                       // batch size of the last get_batch
+    void* dp_comm = nullptr; int dp_world = 0, dp_rank = 0;  // mz_dp_init: RCCL communicator
     char* d_tree = nullptr; size_t tree_game_bytes = 0; bool lds_tree = false; int dump_tree = 0;
     int time_nets = 0;                      // mz_debug_enable flag 2: events around each ResNet nets launch
     std::vector<hipEvent_t> tev; size_t tev_used = 0;
@@ -1087,6 +1089,38 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
     return 0;
 }
 
+// ---- RCCL, loaded on first use (dlopen: libmz has no link dependency on it;
+// RTLD_NOLOAD first so a process that already holds an RCCL — torch's — shares it)
+struct RcclApi {
+    bool ok = false;
+    int (*get_id)(void*) = nullptr;                                    // ncclGetUniqueId(ncclUniqueId*)
+    int (*init_rank)(void**, int, const void*, int) = nullptr;         // ncclCommInitRank(comm*, n, id (by value), rank)
+    int (*allreduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
+    int (*destroy)(void*) = nullptr;
+    const char* (*err)(int) = nullptr;
+};
+static RcclApi& rccl() {
+    static RcclApi api;
+    static bool tried = false;
+    if (tried) return api;
+    tried = true;
+    void* lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!lib) lib = dlopen("librccl.so.1", RTLD_NOW);
+    if (!lib) lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+    if (!lib) return api;
+    api.get_id = reinterpret_cast<int (*)(void*)>(dlsym(lib, "ncclGetUniqueId"));
+    api.allreduce = reinterpret_cast<int (*)(const void*, void*, size_t, int, int, void*, hipStream_t)>(
+        dlsym(lib, "ncclAllReduce"));
+    api.destroy = reinterpret_cast<int (*)(void*)>(dlsym(lib, "ncclCommDestroy"));
+    api.err = reinterpret_cast<const char* (*)(int)>(dlsym(lib, "ncclGetErrorString"));
+    api.ok = api.get_id && api.allreduce && api.destroy && dlsym(lib, "ncclCommInitRank");
+    return api;
+}
+static void dp_destroy(mz_handle* h) {
+    if (h->dp_comm && rccl().ok) (void)rccl().destroy(h->dp_comm);
+    h->dp_comm = nullptr; h->dp_world = 0;
+}
+
 void mz_engine_destroy(mz_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
@@ -1095,6 +1129,7 @@ void mz_engine_destroy(mz_handle* h) {
     for (void* p : h->sp_allocs) (void)hipFree(p);
     if (h->d_dsb) (void)hipFree(h->d_dsb);
     if (h->stream) (void)hipStreamDestroy(h->stream);
+    dp_destroy(h);
     delete h;
 }
 
@@ -2214,6 +2249,55 @@ int mz_learner_grad_sampled_dev(mz_handle* h, int32_t B, uint32_t step, float* g
                                 void* stream) {
     if (!h) return -2;
     return learner_sampled(h, B, step, grad_dev, losses_dev, stream ? (hipStream_t)stream : h->stream, false, 0.0);
+}
+
+// ---- data-parallel learner over RCCL through the C ABI
+#define MZ_DP_ID_BYTES 128   // sizeof(ncclUniqueId)
+int mz_dp_unique_id(uint8_t* id) {
+    if (!id) return -2;
+    if (!rccl().ok) return -1;
+    return rccl().get_id(id) == 0 ? 0 : -1;
+}
+
+int mz_dp_init(mz_handle* h, int rank, int world, const uint8_t* id) {
+    if (!h || !id) return -2;
+    if (world < 1 || rank < 0 || rank >= world) return fail(h, "rank / world out of range");
+    if (!rccl().ok) return fail(h, "librccl.so.1 not found");
+    MZ_TRY(h, hipSetDevice(h->device));
+    dp_destroy(h);
+    // ncclCommInitRank(ncclComm_t*, int nranks, ncclUniqueId commId (128 bytes by value), int rank):
+    // called through a prototype that passes the id by value
+    struct Id { uint8_t b[MZ_DP_ID_BYTES]; };
+    Id v;
+    std::memcpy(v.b, id, MZ_DP_ID_BYTES);
+    static void* lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    auto init = reinterpret_cast<int (*)(void**, int, Id, int)>(dlsym(lib ? lib : RTLD_DEFAULT, "ncclCommInitRank"));
+    if (!init) return fail(h, "ncclCommInitRank not found");
+    void* comm = nullptr;
+    const int rc = init(&comm, world, v, rank);
+    if (rc != 0) return fail(h, std::string("ncclCommInitRank: ") + (rccl().err ? rccl().err(rc) : "error"));
+    h->dp_comm = comm; h->dp_world = world; h->dp_rank = rank;
+    return 0;
+}
+
+int mz_dp_allreduce(mz_handle* h, float* grad_dev, void* stream) {
+    if (!h) return -2;
+    if (!h->dp_comm) return fail(h, "mz_dp_init first");
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    float* g = grad_dev ? grad_dev : h->d_grad;
+    // ncclFloat32 = 7, ncclSum = 0
+    const int rc = rccl().allreduce(g, g, h->nflat, 7, 0, h->dp_comm, st);
+    if (rc != 0) return fail(h, std::string("ncclAllReduce: ") + (rccl().err ? rccl().err(rc) : "error"));
+    return 0;
+}
+
+int mz_learner_train_dp(mz_handle* h, int32_t B, uint32_t step, double eta, float* losses_dev, void* stream) {
+    if (!h) return -2;
+    if (!h->dp_comm) return fail(h, "mz_dp_init first");
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    if (learner_sampled(h, B, step, nullptr, losses_dev, st, false, 0.0)) return -1;
+    if (mz_dp_allreduce(h, nullptr, st)) return -1;
+    return mz_learner_apply_dev(h, nullptr, 1.0f / (float)h->dp_world, eta, st);
 }
 
 int mz_learner_train_dev(mz_handle* h, int32_t B, uint32_t step, double eta, float* losses_dev, void* stream) {

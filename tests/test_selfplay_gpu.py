@@ -354,3 +354,27 @@ def test_per_host_save_game_priorities():
         pr, gp = e2.replay_get_priorities(i)
         assert np.array_equal(pr, h.priorities) and np.float32(gp) == h.game_priority
     e1.close(); e2.close()
+
+
+def test_dp_rccl_world1_matches_single_gpu():
+    """The C-ABI data-parallel learner (mz_dp_unique_id / mz_dp_init /
+    mz_learner_train_dp: grad + RCCL all-reduce + apply(1/world)) on a
+    one-rank communicator equals mz_learner_train_dev, bit for bit."""
+    import torch
+    from muzero_jl_amd import abi
+    from muzero_jl_amd.config import cos_schedule
+    e1, e2 = _device_pair("ttt", 16, 14, cap=64)
+    with pytest.raises(abi.MzError, match="mz_dp_init first"):
+        e2.dp_allreduce()
+    e2.dp_init(0, 1, abi.Engine.dp_unique_id())
+    l1 = torch.empty(8, dtype=torch.float32, device="cuda")
+    l2 = torch.empty(8, dtype=torch.float32, device="cuda")
+    for step in (1, 2, 3):
+        eta = cos_schedule(step)
+        e1.learner_train_dev(32, step, eta, l1.data_ptr())
+        e2.learner_train_dp(32, step, eta, l2.data_ptr())
+        e1.sync(); e2.sync()
+        assert np.array_equal(l1.cpu().numpy()[:6], l2.cpu().numpy()[:6]), step
+        for n in range(3):
+            assert np.array_equal(e1.get_weights(n), e2.get_weights(n)), (step, n)
+    e1.close(); e2.close()
