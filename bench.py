@@ -45,25 +45,38 @@ METRIC = "self-play MCTS node-expansions/sec + train steps/sec, TicTacToe FC net
 PEAK_F32 = 157.3                     # TFLOP/s, MI355X_MICROARCH.md (f32 MFMA = f32 vector peak)
 
 
-def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0, resnet=False, batch=32):
-    """The oracle (C restatement of the reference semantics, 1 thread) on a
-    bounded sample of the same workload: `batch`-game batches of the same
-    positions, the same sims/move, until `budget_s` of CPU time has been spent."""
+def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0, resnet=False, batch=32, threads=1):
+    """The oracle (C restatement of the reference semantics) on a bounded
+    sample of the same workload: `batch`-game batches of the same positions,
+    the same sims/move, for `budget_s` of wall time on `threads` host threads
+    (one Oracle instance each; ctypes releases the GIL during the search)."""
+    import threading
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import Oracle
-    o = Oracle(to_c_config(conf), to_c_resnet_hp(hyper) if resnet else to_c_ffhp(hyper), seed=1)
-    for n, w in enumerate(nets):
-        o.set_weights(n, w)
-    n_games, t0, step = 0, time.perf_counter(), 0
-    while time.perf_counter() - t0 < budget_s:
-        i = (step * batch) % (obs.shape[0] - batch + 1)
-        o.mcts_search(obs[i:i + batch], legal[i:i + batch], tp[i:i + batch], exploration=True, rng_step=step)
-        n_games += batch
-        step += 1
+    counts = [0] * threads
+
+    def worker(w):
+        o = Oracle(to_c_config(conf), to_c_resnet_hp(hyper) if resnet else to_c_ffhp(hyper), seed=1)
+        for n, wt in enumerate(nets):
+            o.set_weights(n, wt)
+        step = w
+        while time.perf_counter() - t0 < budget_s:
+            i = (step * batch) % (obs.shape[0] - batch + 1)
+            o.mcts_search(obs[i:i + batch], legal[i:i + batch], tp[i:i + batch], exploration=True, rng_step=step)
+            counts[w] += batch
+            step += threads
+
+    t0 = time.perf_counter()
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
     dt = time.perf_counter() - t0
-    return dict(value=n_games * conf.num_iters / dt, unit="node-expansions/s", cores=1, kind="port",
+    n_games = sum(counts)
+    return dict(value=n_games * conf.num_iters / dt, unit="node-expansions/s", cores=threads, kind="port",
                 sample=f"{n_games} games x {conf.num_iters} sims ({batch}-game batches of the bench positions), "
-                       f"oracle/mz_oracle.c single thread, {dt:.1f} s")
+                       f"oracle/mz_oracle.c on {threads} host thread{'s' if threads > 1 else ''}, {dt:.1f} s")
 
 
 def workload(game, resnet, G, S):
@@ -92,6 +105,8 @@ def main():
     ap.add_argument("--sims", type=int, default=None, help="sims per move (default 50; atari 200)")
     ap.add_argument("--learner-steps", type=int, default=50)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="host threads of the oracle baseline (the box's CPU share for one GPU is 16)")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -280,10 +295,13 @@ def main():
                 rec = json.load(f)
             if rec.get("kernel") == variant:
                 traffic = rec.get("hbm_bytes_per_launch")
-        cpu = None
+        cpu = cpu1 = None
         if world == 1 and not args.no_cpu:
+            nt = max(1, min(args.cpu_threads, os.cpu_count() or 1))
             cpu = cpu_baseline(conf, hyper, nets, obs, legal, tp, args.cpu_budget, resnet,
-                               batch=1 if game is atari else 32)
+                               batch=1 if game is atari else 32, threads=nt)
+            cpu1 = cpu_baseline(conf, hyper, nets, obs, legal, tp, args.cpu_budget, resnet,
+                                batch=1 if game is atari else 32, threads=1)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "node-expansions/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -308,6 +326,7 @@ def main():
                          "kernel": variant, "kernel_ms": round(kern_ms, 4),
                          "flop_per_launch": flop_launch},
             "cpu_baseline": cpu,
+            "cpu_baseline_1thread": cpu1,    # the reference's single self-play worker (main.jl:2)
         }
         print(json.dumps(out), flush=True)
     if world > 1:
