@@ -54,6 +54,7 @@ def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0, resnet=False,
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import Oracle
     counts = [0] * threads
+    batch = min(batch, obs.shape[0])     # fewer bench games than one batch: search them all, count what ran
 
     def worker(w):
         o = Oracle(to_c_config(conf), to_c_resnet_hp(hyper) if resnet else to_c_ffhp(hyper), seed=1)
