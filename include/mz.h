@@ -12,7 +12,11 @@
  *   - host buffers are caller-owned and borrowed for the duration of the call;
  *     `_dev` variants take device pointers and a hipStream_t (as void*);
  *   - one handle per GPU, one host thread per handle; calls are synchronous
- *     at return (the `_dev` variants are stream-ordered instead);
+ *     at return (the `_dev` variants are stream-ordered instead); a
+ *     host-synchronous call (weights, state, checkpoints, replay / debug
+ *     read-outs, the host-buffer search and learner step) first waits for all
+ *     of the process's work on the device, so `_dev` work queued on a caller
+ *     stream is complete before it reads or overwrites engine memory;
  *   - action ids are 1-based (Julia convention), arrays are column-major with
  *     the reference's shapes (W,H,C,N): feature index = w + W*h + W*H*c.
  */
@@ -346,6 +350,33 @@ int mz_replay_get_priorities(mz_handle* h, int32_t i, float* priorities, float* 
 int mz_replay_get_game(mz_handle* h, int32_t i, int32_t* T, uint8_t* obs, int32_t* actions,
                        float* rewards, int32_t* to_play, float* child_visits, float* root_values);
 int mz_selfplay_slots(mz_handle* h, int32_t* history_len, uint8_t* board, int32_t* player);
+
+/* ---- Actor–learner loop (self_play! ‖ learning!) -----
+ * The reference runs self_play! (SelfPlay.jl:384-419) and learning!
+ * (Learning.jl:306-438) as two processes coupled by RemoteChannels (quirk
+ * Q16): self-play take!s the training step once per game, the learner put!s
+ * it once per step, and every checkpoint_interval steps the learner queues
+ * its nets on remote_NNs (capacity 1, starting with the initial nets) which
+ * self-play then take!s — the actors run one checkpoint behind.  On the
+ * device, for the G lockstep slots of mz_selfplay_init:
+ *   mz_train_init: the actors' weight set and the queue start as copies of
+ *     the engine's current (initial) nets; learner step t = 0; B = batch.
+ *   mz_train_run: `moves` times: one self-play move of every slot with the
+ *     ACTORS' nets (mz_selfplay_move, move key move0 + m, temperature
+ *     visit_softmax_temperature_fn(t)); then one learner step per game saved
+ *     by that move (mz_learner_train_dev with step t+1, eta = Cos(t+1)) while
+ *     t <= training_steps; after step t with t % checkpoint_interval == 0 and
+ *     t > 1 the actors take the queued nets and the learner's nets are queued.
+ *     Reads the shard's game counter back once per move (one sync).
+ *     state_out[4] = {t, num_played_games, actor refreshes, learner steps of
+ *     this call}; losses_dev (device, 6 floats, or NULL) = the last step's.
+ *   mz_train_weights_get: the learner's, actors' or queued nets (Flux order).
+ * One GPU (world = 1).  oracle/mz_oracle.c ora_train_loop restates it.      */
+enum { MZ_TRAIN_LEARNER = 0, MZ_TRAIN_ACTOR = 1, MZ_TRAIN_QUEUED = 2 };
+int mz_train_init(mz_handle* h, int32_t batch_size);
+int mz_train_run(mz_handle* h, int32_t moves, uint32_t move0, uint32_t game_offset, int64_t* state_out,
+                 float* losses_dev, void* stream);
+int mz_train_weights_get(mz_handle* h, int which, int net, float* flat, size_t n);
 
 /* ---- Checkpoints -------------------------------------------
  * Replace serialize(joinpath(networks_path, "$(step)_<net>.bin"), net)

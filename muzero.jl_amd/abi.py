@@ -18,6 +18,7 @@ from .config import (MzConfig, MzFFHP, MzResNetHP, ResNetHP, hidden_size, stacke
 NET_REPR, NET_PRED, NET_DYN = 0, 1, 2
 ENV_TICTACTOE, ENV_CONNECT4 = 0, 1
 SP_TRAIN, SP_EVAL = 0, 1
+TRAIN_LEARNER, TRAIN_ACTOR, TRAIN_QUEUED = 0, 1, 2
 OPP_SELF, OPP_RANDOM = 0, 1
 
 _lib = None
@@ -76,6 +77,9 @@ SIGNATURES = {
     "mz_replay_get_priorities": (ctypes.c_int, [_VP, ctypes.c_int32, _VP, _VP]),
     "mz_replay_get_game": (ctypes.c_int, [_VP, ctypes.c_int32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "mz_selfplay_slots": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
+    "mz_train_init": (ctypes.c_int, [_VP, ctypes.c_int32]),
+    "mz_train_run": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, _VP, _VP, _VP]),
+    "mz_train_weights_get": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP, ctypes.c_size_t]),
     "mz_checkpoint_save": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int64]),
     "mz_checkpoint_load": (ctypes.c_int, [_VP, ctypes.c_char_p, _VP]),
     "mz_search_variant": (ctypes.c_char_p, [_VP]),
@@ -297,6 +301,26 @@ class Engine:
     def selfplay_move(self, rng_step, game_offset=0, temperature=1.0, stream=None):
         self._check(self.lib.mz_selfplay_move(self.h, rng_step, game_offset, temperature, stream),
                     "mz_selfplay_move")
+
+    def train_init(self, batch_size):
+        """Actor–learner loop (self_play! ‖ learning!, Q16): actors and the
+        queued nets start from the current weights (mz_train_init)."""
+        self._check(self.lib.mz_train_init(self.h, batch_size), "mz_train_init")
+
+    def train_run(self, moves, move0=0, game_offset=0, losses_ptr=None, stream=None):
+        """`moves` self-play moves with the actors' nets, one learner step per
+        finished game, actor refresh every checkpoint_interval steps; returns
+        (t, num_played_games, actor refreshes, learner steps of this call)."""
+        st = np.zeros(4, np.int64)
+        self._check(self.lib.mz_train_run(self.h, moves, move0, game_offset, _p(st), losses_ptr, stream),
+                    "mz_train_run")
+        return tuple(int(x) for x in st)
+
+    def train_weights(self, which, net):
+        """Flux-order weights of the learner / actors / queued nets."""
+        out = np.empty(self.param_count(net), np.float32)
+        self._check(self.lib.mz_train_weights_get(self.h, which, net, _p(out), out.size), "mz_train_weights_get")
+        return out
 
     def selfplay_mode(self, mode, opponent=OPP_SELF, muzero_player=1):
         """SP_TRAIN (self_play!) or SP_EVAL (competitive_play!: games tallied, not saved)."""

@@ -1,6 +1,11 @@
-"""Build libmz.so (hand-written HIP for gfx950) in-tree with hipcc."""
+"""Build libmz.so (hand-written HIP for gfx950) in-tree with hipcc.
+
+Each source compiles to its own object in parallel (a source is rebuilt when
+it, or any header, is newer than its object); the objects link into
+muzero.jl_amd/lib/libmz.so."""
 import os
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 from . import PKG_DIR, LIB_PATH
 
@@ -8,7 +13,7 @@ SOURCES = ["mz_engine.hip", "mz_search.hip", "mz_small.hip", "mz_nets.hip", "mz_
            "mz_downsample.hip", "mz_checkpoint.cpp"]
 HEADERS = ["mz_internal.h", "mz_mlp_device.h", "mz_tree_device.h", "mz_small_params.h", "mz_resnet_params.h",
            "mz_selfplay_params.h", "mz_ckpt_iface.h", "mz_replay_device.h", "mz_learner_device.h"]
-FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
          # the numerics contract (include/mz_detmath.h): no FP contraction, IEEE
          # division/sqrt, f32 denormals kept (hipcc defaults for the last two)
          "-ffp-contract=off", "-fno-fast-math", "-Wno-unused-result",
@@ -18,21 +23,38 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
          "-fno-slp-vectorize"]
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, jobs=None):
     csrc = os.path.join(PKG_DIR, "csrc")
     inc = os.path.join(os.path.dirname(PKG_DIR), "include")
-    srcs = [os.path.join(csrc, s) for s in SOURCES]
-    deps = srcs + [os.path.join(csrc, h) for h in HEADERS] + \
+    objdir = os.path.join(os.path.dirname(LIB_PATH), "obj")
+    srcs = [os.path.join(csrc, s) for s in SOURCES if os.path.exists(os.path.join(csrc, s))]
+    hdrs = [os.path.join(csrc, h) for h in HEADERS if os.path.exists(os.path.join(csrc, h))] + \
         [os.path.join(inc, f) for f in ("mz.h", "mz_detmath.h")]
-    if not force and os.path.exists(LIB_PATH):
-        t = os.path.getmtime(LIB_PATH)
-        if all(os.path.getmtime(d) <= t for d in deps):
-            return LIB_PATH
-    os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
+    hdr_t = max(os.path.getmtime(d) for d in hdrs)
+    os.makedirs(objdir, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc] + FLAGS + ["-o", LIB_PATH + ".tmp"] + srcs
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(objdir, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or not os.path.exists(o) or os.path.getmtime(o) < max(hdr_t, os.path.getmtime(s)):
+            todo.append((s, o))
+
+    def compile_one(so):
+        s, o = so
+        cmd = [hipcc] + FLAGS + ["-c", "-o", o + ".tmp", s]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(o + ".tmp", o)
+
+    if todo:
+        with ThreadPoolExecutor(jobs or min(len(todo), os.cpu_count() or 4, 16)) as ex:
+            list(ex.map(compile_one, todo))
+    if todo or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(os.path.getmtime(o) for o in objs):
+        cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB_PATH + ".tmp"] + objs
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(LIB_PATH + ".tmp", LIB_PATH)
     return LIB_PATH

@@ -210,6 +210,7 @@ struct mz_handle {
     SpHist sp_hist{}, sp_ring{};
     long long* d_sp_counters = nullptr;
     int32_t* d_sp_done = nullptr; int32_t* d_sp_rpos = nullptr;
+    float* d_sp_temp = nullptr;             // [G] per-slot temperatures (temperature_threshold)
     int sp_eval = 0, sp_opp = MZ_OPP_SELF, sp_mzp = 1;    // mz_selfplay_mode
     long long* d_eval = nullptr;                          // [4] evaluation tally
     float* d_sp_dpow = nullptr;
@@ -218,6 +219,15 @@ struct mz_handle {
     int32_t* d_rs_index = nullptr;
     int rs_cap = 0;
     bool sp_has_games = false;              // the FIFO never empties once a game is in
+    // actor–learner loop (mz_train_*): the actors' weight set (flat + the
+    // search images), the queued nets (remote_NNs, flat), the learner step t
+    struct WSet { float* flat = nullptr; float* Wp = nullptr; float* Bp = nullptr; float* smw = nullptr;
+                  float* smb = nullptr; };
+    WSet tr_actor;
+    float* d_tr_queued = nullptr;
+    int tr_B = 0;
+    int64_t tr_t = 0, tr_games = 0, tr_refresh = 0;
+    long long* h_tr_cnt = nullptr;          // pinned: num_played_games read back once per move
     std::vector<void*> sp_allocs;
     std::vector<void*> allocs;
 };
@@ -232,6 +242,13 @@ struct mz_handle {
     } while (0)
 
 static int fail(mz_handle* h, const std::string& m) { h->err = m; return -2; }
+
+// Host-synchronous entry points (weights, state, replay read-outs, debug
+// copies) wait for ALL of this process's work on the device, not only the
+// handle's stream: `_dev` calls may have queued work on a caller stream
+// (torch's, created non-blocking like the handle's), which a blocking
+// hipMemcpy would not wait for.
+static hipError_t sync_device(mz_handle* h) { (void)h; return hipDeviceSynchronize(); }
 
 template <typename T>
 static hipError_t dalloc(mz_handle* h, T** p, size_t n) {
@@ -1091,10 +1108,12 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
 
 // ---- RCCL, loaded on first use (dlopen: libmz has no link dependency on it;
 // RTLD_NOLOAD first so a process that already holds an RCCL — torch's — shares it)
+// ncclUniqueId: a 128-byte struct that ncclCommInitRank takes BY VALUE
+struct RcclId { uint8_t b[MZ_DP_ID_BYTES]; };
 struct RcclApi {
     bool ok = false;
     int (*get_id)(void*) = nullptr;                                    // ncclGetUniqueId(ncclUniqueId*)
-    int (*init_rank)(void**, int, const void*, int) = nullptr;         // ncclCommInitRank(comm*, n, id (by value), rank)
+    int (*init_rank)(void**, int, RcclId, int) = nullptr;              // ncclCommInitRank(comm*, n, id, rank)
     int (*allreduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
     int (*destroy)(void*) = nullptr;
     const char* (*err)(int) = nullptr;
@@ -1113,7 +1132,8 @@ static RcclApi& rccl() {
         dlsym(lib, "ncclAllReduce"));
     api.destroy = reinterpret_cast<int (*)(void*)>(dlsym(lib, "ncclCommDestroy"));
     api.err = reinterpret_cast<const char* (*)(int)>(dlsym(lib, "ncclGetErrorString"));
-    api.ok = api.get_id && api.allreduce && api.destroy && dlsym(lib, "ncclCommInitRank");
+    api.init_rank = reinterpret_cast<int (*)(void**, int, RcclId, int)>(dlsym(lib, "ncclCommInitRank"));
+    api.ok = api.get_id && api.init_rank && api.allreduce && api.destroy;
     return api;
 }
 static void dp_destroy(mz_handle* h) {
@@ -1128,6 +1148,7 @@ void mz_engine_destroy(mz_handle* h) {
     for (void* p : h->allocs) (void)hipFree(p);
     for (void* p : h->sp_allocs) (void)hipFree(p);
     if (h->d_dsb) (void)hipFree(h->d_dsb);
+    if (h->h_tr_cnt) (void)hipHostFree(h->h_tr_cnt);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     dp_destroy(h);
     delete h;
@@ -1269,9 +1290,10 @@ int mz_weights_set(mz_handle* h, int net, const float* flat, size_t n) {
     if (net < 0 || net > 2) return fail(h, "bad net id");
     if (n != h->nparams[net]) return fail(h, "weights_set: wrong parameter count");
     MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, sync_device(h));                  // no search / learner launch still reads the old weights
     MZ_TRY(h, hipMemcpyAsync(h->d_flat + h->flat_off[net], flat, n * 4, hipMemcpyHostToDevice, h->stream));
     if (repack(h)) return -1;
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     return 0;
 }
 
@@ -1280,8 +1302,9 @@ int mz_weights_get(mz_handle* h, int net, float* flat, size_t n) {
     if (net < 0 || net > 2) return fail(h, "bad net id");
     if (n != h->nparams[net]) return fail(h, "weights_get: wrong parameter count");
     MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, sync_device(h));                  // learner steps queued on any stream have landed
     MZ_TRY(h, hipMemcpyAsync(flat, h->d_flat + h->flat_off[net], n * 4, hipMemcpyDeviceToHost, h->stream));
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     return 0;
 }
 
@@ -1310,7 +1333,7 @@ static int rnet_forward(mz_handle* h, int net, const float* x, int n, float* out
                                     args, h->rn_lds[net], h->stream);
     (void)hipMemcpyAsync(out0, d0, (size_t)n * R.out0_n * 4, hipMemcpyDeviceToHost, h->stream);
     if (out1 && R.out1_n) (void)hipMemcpyAsync(out1, d1, (size_t)n * R.out1_n * 4, hipMemcpyDeviceToHost, h->stream);
-    hipError_t se = hipStreamSynchronize(h->stream);
+    hipError_t se = sync_device(h);
     (void)hipFree(dx); (void)hipFree(d0); (void)hipFree(d1);
     MZ_TRY(h, le);
     MZ_TRY(h, se);
@@ -1323,6 +1346,7 @@ int mz_net_forward(mz_handle* h, int net, const float* x, int n, float* out0, fl
     if (n < 0) return fail(h, "negative batch");
     if (n == 0) return 0;
     MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, sync_device(h));                  // weights written by `_dev` calls on other streams
     if (h->kind == 1) return rnet_forward(h, net, x, n, out0, out1);
     const int H = h->H, A = h->A;
     const int in_feat = net == MZ_NET_REPR ? h->obs_feat : net == MZ_NET_PRED ? H : H + h->plane;
@@ -1344,7 +1368,7 @@ int mz_net_forward(mz_handle* h, int net, const float* x, int n, float* out0, fl
     hipError_t le = hipGetLastError();
     (void)hipMemcpyAsync(out0, d0, (size_t)n * o0 * 4, hipMemcpyDeviceToHost, h->stream);
     if (out1 && net != MZ_NET_REPR) (void)hipMemcpyAsync(out1, d1, (size_t)n * o1 * 4, hipMemcpyDeviceToHost, h->stream);
-    hipError_t se = hipStreamSynchronize(h->stream);
+    hipError_t se = sync_device(h);
     (void)hipFree(dx); (void)hipFree(d0); (void)hipFree(d1);
     MZ_TRY(h, le);
     MZ_TRY(h, se);
@@ -1354,9 +1378,10 @@ int mz_net_forward(mz_handle* h, int net, const float* x, int n, float* out0, fl
 // ResNet search: root launch, S x (tree step, networks), final tree step
 static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_mask, const int32_t* to_play,
                    int exploration, uint32_t rng_step, uint32_t game_offset, float temperature, float* child_visits,
-                   float* root_value, int32_t* action_out, hipStream_t st) {
+                   float* root_value, int32_t* action_out, hipStream_t st, const float* temp_g) {
     RSearchParams P;
     std::memset(&P, 0, sizeof(P));
+    P.temp_g = temp_g;
     P.G = G; P.S = h->S; P.A = h->A; P.H = h->H; P.W = h->rconf.observation_shape[0];
     P.P = h->plane; P.players = h->conf.players; P.obs_feat = h->rin_feat; P.exploration = exploration;
     P.rng_step = rng_step; P.game_offset = game_offset; P.seed = h->seed; P.temperature = temperature;
@@ -1410,17 +1435,21 @@ static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     return 0;
 }
 
-int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* legal_mask, const int32_t* to_play,
-                       int exploration, uint32_t rng_step, uint32_t game_offset, float temperature,
-                       float* child_visits, float* root_value, int32_t* action_out, void* stream) {
+// the batched search; temp_g: per-game temperatures (device, G) or NULL =
+// `temperature` for every game
+static int search_dev(mz_handle* h, int G, const float* obs, const uint8_t* legal_mask, const int32_t* to_play,
+                      int exploration, uint32_t rng_step, uint32_t game_offset, float temperature,
+                      float* child_visits, float* root_value, int32_t* action_out, void* stream,
+                      const float* temp_g) {
     if (!h) return -2;
     if (G < 0 || G > h->max_games) return fail(h, "G exceeds max_games");
     if (G == 0) return 0;
     if (h->kind == 1)
         return rsearch(h, G, obs, legal_mask, to_play, exploration, rng_step, game_offset, temperature,
-                       child_visits, root_value, action_out, stream ? (hipStream_t)stream : h->stream);
+                       child_visits, root_value, action_out, stream ? (hipStream_t)stream : h->stream, temp_g);
     SearchParams P;
     std::memset(&P, 0, sizeof(P));
+    P.temp_g = temp_g;
     P.G = G; P.S = h->S; P.A = h->A; P.H = h->H; P.players = h->conf.players; P.obs_feat = h->obs_feat;
     P.plane = h->plane; P.exploration = exploration; P.rng_step = rng_step; P.game_offset = game_offset;
     P.seed = h->seed; P.temperature = temperature; P.discount = h->conf.discount;
@@ -1443,6 +1472,7 @@ int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* leg
         const int ti = T == 1 ? 0 : T == 2 ? 1 : 2;
         SmallParams Q;
         std::memset(&Q, 0, sizeof(Q));
+        Q.temp_g = temp_g;
         Q.G = G; Q.S = h->S; Q.A = h->A; Q.H = h->H; Q.players = h->conf.players; Q.obs_feat = h->obs_feat;
         Q.plane = h->plane; Q.exploration = exploration; Q.rng_step = rng_step; Q.game_offset = game_offset;
         Q.seed = h->seed; Q.temperature = temperature; Q.discount = h->conf.discount;
@@ -1478,6 +1508,13 @@ int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* leg
     return 0;
 }
 
+int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* legal_mask, const int32_t* to_play,
+                       int exploration, uint32_t rng_step, uint32_t game_offset, float temperature,
+                       float* child_visits, float* root_value, int32_t* action_out, void* stream) {
+    return search_dev(h, G, obs, legal_mask, to_play, exploration, rng_step, game_offset, temperature, child_visits,
+                      root_value, action_out, stream, nullptr);
+}
+
 int mz_mcts_search(mz_handle* h, int G, const float* obs, const uint8_t* legal_mask, const int32_t* to_play,
                    int exploration, uint32_t rng_step, uint32_t game_offset, float temperature, float* child_visits,
                    float* root_value, int32_t* action_out) {
@@ -1492,6 +1529,7 @@ int mz_mcts_search(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
         if (to_play[g] < 1 || to_play[g] > h->conf.players) return fail(h, "to_play out of range");
     }
     MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, sync_device(h));                  // `_dev` work on other streams first
     MZ_TRY(h, hipMemcpyAsync(h->d_obs, obs, (size_t)G * h->obs_feat * 4, hipMemcpyHostToDevice, h->stream));
     MZ_TRY(h, hipMemcpyAsync(h->d_legal, legal_mask, (size_t)G * A, hipMemcpyHostToDevice, h->stream));
     MZ_TRY(h, hipMemcpyAsync(h->d_tp, to_play, (size_t)G * 4, hipMemcpyHostToDevice, h->stream));
@@ -1501,7 +1539,7 @@ int mz_mcts_search(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     MZ_TRY(h, hipMemcpyAsync(child_visits, h->d_cv, (size_t)G * A * 4, hipMemcpyDeviceToHost, h->stream));
     MZ_TRY(h, hipMemcpyAsync(root_value, h->d_rv, (size_t)G * 4, hipMemcpyDeviceToHost, h->stream));
     MZ_TRY(h, hipMemcpyAsync(action_out, h->d_act, (size_t)G * 4, hipMemcpyDeviceToHost, h->stream));
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     return 0;
 }
 
@@ -1517,7 +1555,7 @@ int mz_debug_tree(mz_handle* h, int G, int32_t* eN, float* eW, float* eP, float*
     if (G < 0 || G > h->max_games) return fail(h, "G exceeds max_games");
     if (h->lds_tree && !h->dump_tree) return fail(h, "mz_debug_tree needs mz_debug_enable(h, 1) before the search");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     const int S = h->S, A = h->A, NN = S + 1, E = NN * A;
     const size_t gb = h->tree_game_bytes;
     std::vector<char> buf((size_t)G * gb);
@@ -1728,6 +1766,7 @@ int mz_learner_step(mz_handle* h, const mz_batch* b, double eta, float* losses_o
     MZ_TRY(h, hipSetDevice(h->device));
     if (B < 1) return fail(h, "batch_size must be >= 1");
     if (ensure_batch(h, B)) return -1;
+    MZ_TRY(h, sync_device(h));                  // `_dev` work on other streams first
     hipStream_t st = h->stream;
     MZ_TRY(h, hipMemcpyAsync(h->d_bobs, b->observation, (size_t)B * h->obs_feat * 4, hipMemcpyHostToDevice, st));
     MZ_TRY(h, hipMemcpyAsync(h->d_bact, b->actions, (size_t)B * (K + 1) * 4, hipMemcpyHostToDevice, st));
@@ -1769,7 +1808,7 @@ int mz_debug_unroll(mz_handle* h, int B, float* values, float* policies, float* 
     if (!h) return -2;
     if (B < 0 || B > h->bcap) return fail(h, "B exceeds the last learner batch");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     const size_t n = (size_t)B * (h->conf.num_unroll_steps + 1);
     if (values) MZ_TRY(h, hipMemcpy(values, h->d_pv, n * 4, hipMemcpyDeviceToHost));
     if (policies) MZ_TRY(h, hipMemcpy(policies, h->d_pp, n * h->A * 4, hipMemcpyDeviceToHost));
@@ -1782,7 +1821,7 @@ int mz_debug_stamps(mz_handle* h, unsigned long long* out, int n_blocks) {
     if (!h) return -2;
 #ifdef MZ_STAMPS
     if (!h->d_stamps) return fail(h, "no stamps recorded");
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     MZ_TRY(h, hipMemcpy(out, h->d_stamps, (size_t)n_blocks * 8 * 8, hipMemcpyDeviceToHost));
     return 0;
 #else
@@ -1848,7 +1887,7 @@ size_t mz_flat_count(const mz_handle* h) { return h->nflat; }
 
 int mz_state_get(mz_handle* h, float* flat, float* m, float* v, double* beta_pow) {
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     if (flat) MZ_TRY(h, hipMemcpy(flat, h->d_flat, h->nflat * 4, hipMemcpyDeviceToHost));
     if (m) MZ_TRY(h, hipMemcpy(m, h->d_m, h->nflat * 4, hipMemcpyDeviceToHost));
     if (v) MZ_TRY(h, hipMemcpy(v, h->d_v, h->nflat * 4, hipMemcpyDeviceToHost));
@@ -1858,13 +1897,13 @@ int mz_state_get(mz_handle* h, float* flat, float* m, float* v, double* beta_pow
 
 int mz_state_set(mz_handle* h, const float* flat, const float* m, const float* v, const double* beta_pow) {
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     MZ_TRY(h, hipMemcpy(h->d_flat, flat, h->nflat * 4, hipMemcpyHostToDevice));
     MZ_TRY(h, hipMemcpy(h->d_m, m, h->nflat * 4, hipMemcpyHostToDevice));
     MZ_TRY(h, hipMemcpy(h->d_v, v, h->nflat * 4, hipMemcpyHostToDevice));
     h->bp1 = beta_pow[0]; h->bp2 = beta_pow[1];
     if (repack(h)) return -1;
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     return 0;
 }
 
@@ -1962,11 +2001,12 @@ int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games) {
     if (replay_games < G) return fail(h, "replay_games must be >= G (one move can finish every slot)");
     if (c.max_moves < 1) return fail(h, "max_moves must be >= 1");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     for (void* p : h->sp_allocs) (void)hipFree(p);
     h->sp_allocs.clear();
     h->rs_cap = 0;
     h->sp_has_games = false;
+    h->tr_B = 0;                                // a new shard: mz_train_init again
     h->sp_env = env_kind; h->sp_G = G; h->sp_cap = replay_games;
     h->sp_T = c.max_moves + 1; h->sp_osz = W * H * C;
     MZ_TRY(h, spalloc(h, &h->d_sp_board, (size_t)G * h->sp_osz));
@@ -1977,6 +2017,7 @@ int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games) {
     MZ_TRY(h, spalloc(h, &h->d_sp_counters, 4));
     MZ_TRY(h, spalloc(h, &h->d_sp_done, (size_t)G));
     MZ_TRY(h, spalloc(h, &h->d_sp_rpos, (size_t)G));
+    MZ_TRY(h, spalloc(h, &h->d_sp_temp, (size_t)G));
     MZ_TRY(h, spalloc(h, &h->d_eval, 4));
     MZ_TRY(h, spalloc(h, &h->d_per_cum, (size_t)h->sp_cap));
     MZ_TRY(h, spalloc(h, &h->d_per_p, (size_t)h->sp_cap));
@@ -2005,12 +2046,16 @@ int mz_selfplay_move(mz_handle* h, uint32_t rng_step, uint32_t game_offset, floa
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     SpParams S = sp_params(h);
     S.step = rng_step; S.game_offset = game_offset;
+    // temperature_threshold (SelfPlay.jl:344-346): per-slot temperatures
+    const bool thr = h->conf.temperature_threshold >= 0;
+    S.temperature = temperature; S.temp_threshold = h->conf.temperature_threshold;
+    S.temp_g = thr ? h->d_sp_temp : nullptr;
     const int G = h->sp_G;
     const dim3 waves((G + 3) / 4);
     hipLaunchKernelGGL(mz_sp_prepare, waves, dim3(256), 0, st, S);
     MZ_TRY(h, hipGetLastError());
-    int rc = mz_mcts_search_dev(h, G, h->d_obs, h->d_legal, h->d_tp, 1, rng_step, game_offset, temperature, h->d_cv,
-                                h->d_rv, h->d_act, st);
+    int rc = search_dev(h, G, h->d_obs, h->d_legal, h->d_tp, 1, rng_step, game_offset, temperature, h->d_cv,
+                        h->d_rv, h->d_act, st, S.temp_g);
     if (rc) return rc;
     hipLaunchKernelGGL(mz_sp_commit, waves, dim3(256), 0, st, S);
     hipLaunchKernelGGL(mz_sp_order, dim3(1), dim3(1024), 0, st, S);
@@ -2033,7 +2078,7 @@ int mz_eval_results(mz_handle* h, int64_t* out4) {
     if (!h || !out4) return -2;
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     long long c[4];
     MZ_TRY(h, hipMemcpy(c, h->d_eval, sizeof(c), hipMemcpyDeviceToHost));
     for (int i = 0; i < 4; ++i) out4[i] = c[i];
@@ -2044,7 +2089,7 @@ int mz_replay_counts(mz_handle* h, int64_t* counts, int32_t* games_in_buffer) {
     if (!h) return -2;
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     long long c[3];
     MZ_TRY(h, hipMemcpy(c, h->d_sp_counters, sizeof(c), hipMemcpyDeviceToHost));
     if (counts) for (int i = 0; i < 3; ++i) counts[i] = c[i];
@@ -2059,7 +2104,7 @@ int mz_replay_save_game(mz_handle* h, int32_t T, const uint8_t* obs, const int32
     if (T < 1 || T > h->sp_T) return fail(h, "game length must be in 1..max_moves+1");
     if (!obs || !actions || !rewards || !to_play || !child_visits || !root_values) return fail(h, "null array");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     long long c[3];
     MZ_TRY(h, hipMemcpy(c, h->d_sp_counters, sizeof(c), hipMemcpyDeviceToHost));
     const long long num = c[0] + 1;
@@ -2084,7 +2129,7 @@ int mz_replay_save_game(mz_handle* h, int32_t T, const uint8_t* obs, const int32
         hipLaunchKernelGGL(mz_rp_per_init, dim3(1), dim3(64), 0, h->stream, h->sp_ring, slot, (int)T, h->sp_T,
                            h->conf.td_steps, (const float*)h->d_sp_dpow, h->conf.PER_alpha);
         MZ_TRY(h, hipGetLastError());
-        MZ_TRY(h, hipStreamSynchronize(h->stream));
+        MZ_TRY(h, sync_device(h));
     }
     return 0;
 }
@@ -2231,7 +2276,7 @@ int mz_replay_get_priorities(mz_handle* h, int32_t i, float* priorities, float* 
     if (!h) return -2;
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     long long played = 0;
     MZ_TRY(h, hipMemcpy(&played, h->d_sp_counters, sizeof(played), hipMemcpyDeviceToHost));
     const long long n = std::min<long long>(played, h->sp_cap);
@@ -2265,16 +2310,10 @@ int mz_dp_init(mz_handle* h, int rank, int world, const uint8_t* id) {
     if (!rccl().ok) return fail(h, "librccl.so.1 not found");
     MZ_TRY(h, hipSetDevice(h->device));
     dp_destroy(h);
-    // ncclCommInitRank(ncclComm_t*, int nranks, ncclUniqueId commId (128 bytes by value), int rank):
-    // called through a prototype that passes the id by value
-    struct Id { uint8_t b[MZ_DP_ID_BYTES]; };
-    Id v;
+    RcclId v;
     std::memcpy(v.b, id, MZ_DP_ID_BYTES);
-    static void* lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
-    auto init = reinterpret_cast<int (*)(void**, int, Id, int)>(dlsym(lib ? lib : RTLD_DEFAULT, "ncclCommInitRank"));
-    if (!init) return fail(h, "ncclCommInitRank not found");
     void* comm = nullptr;
-    const int rc = init(&comm, world, v, rank);
+    const int rc = rccl().init_rank(&comm, world, v, rank);
     if (rc != 0) return fail(h, std::string("ncclCommInitRank: ") + (rccl().err ? rccl().err(rc) : "error"));
     h->dp_comm = comm; h->dp_world = world; h->dp_rank = rank;
     return 0;
@@ -2310,7 +2349,7 @@ int mz_replay_get_game(mz_handle* h, int32_t i, int32_t* T, uint8_t* obs, int32_
     if (!h) return -2;
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     long long c[3];
     MZ_TRY(h, hipMemcpy(c, h->d_sp_counters, sizeof(c), hipMemcpyDeviceToHost));
     const long long held = std::min<long long>(c[0], h->sp_cap);
@@ -2335,11 +2374,130 @@ int mz_selfplay_slots(mz_handle* h, int32_t* history_len, uint8_t* board, int32_
     if (!h) return -2;
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    MZ_TRY(h, sync_device(h));
     const size_t G = (size_t)h->sp_G;
     if (history_len) MZ_TRY(h, hipMemcpy(history_len, h->sp_hist.len, G * 4, hipMemcpyDeviceToHost));
     if (board) MZ_TRY(h, hipMemcpy(board, h->d_sp_board, G * h->sp_osz, hipMemcpyDeviceToHost));
     if (player) MZ_TRY(h, hipMemcpy(player, h->d_sp_player, G * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+// ---- actor–learner loop (self_play! ‖ learning!, Q16)
+// The actors search with their own weight set; the learner trains the
+// engine's weights.  The set is swapped in around each self-play move (the
+// search kernels read the images the handle points at).
+static void wset_swap(mz_handle* h, mz_handle::WSet& w) {
+    std::swap(h->d_flat, w.flat); std::swap(h->d_Wp, w.Wp); std::swap(h->d_Bp, w.Bp);
+    std::swap(h->d_sm_w, w.smw); std::swap(h->d_sm_bias, w.smb);
+}
+// flat -> the set's search images (the repack of the handle's current images)
+static int wset_repack(mz_handle* h, mz_handle::WSet& w, hipStream_t st) {
+    const int T = 256;
+    hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_w_n + T - 1) / T)), dim3(T), 0, st,
+                       w.flat, h->d_srcW, w.Wp, h->packed_w_n);
+    if (h->packed_b_n)
+        hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->packed_b_n + T - 1) / T)), dim3(T), 0, st,
+                           w.flat, h->d_srcB, w.Bp, h->packed_b_n);
+    if (h->small_ok) {
+        hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->sm_w_n + T - 1) / T)), dim3(T), 0, st,
+                           w.flat, h->d_sm_srcw, w.smw, h->sm_w_n);
+        hipLaunchKernelGGL(mz_repack_kernel, dim3((unsigned)((h->sm_b_n + T - 1) / T)), dim3(T), 0, st,
+                           w.flat, h->d_sm_srcb, w.smb, h->sm_b_n);
+    }
+    MZ_TRY(h, hipGetLastError());
+    return 0;
+}
+// ParameterSchedulers 0.2.3 Cos(λ0 = 1e-4, λ1 = 1e-1, period = 10) under
+// Stateful, step t >= 1 (Learning.jl:319, 382)
+static double cos_schedule(int64_t t) {
+    const double l0 = 1e-4, l1 = 1e-1, range = std::fabs(l0 - l1), off = std::min(l0, l1);
+    const double a = 6.283185307179586 * (double)(t - 1) / 10.0;
+    return range * (1.0 + std::cos(a)) / 2.0 + off;
+}
+
+int mz_train_init(mz_handle* h, int32_t B) {
+    if (!h) return -2;
+    if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
+    if (B < 1) return fail(h, "batch_size must be >= 1");
+    if (h->dp_world > 1) return fail(h, "mz_train_run is the single-GPU loop (world = 1)");
+    if (h->conf.checkpoint_interval < 1) return fail(h, "checkpoint_interval must be >= 1");
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, sync_device(h));
+    mz_handle::WSet& w = h->tr_actor;
+    if (!w.flat) {
+        MZ_TRY(h, dalloc(h, &w.flat, h->nflat));
+        MZ_TRY(h, dalloc(h, &w.Wp, h->packed_w_n));
+        if (h->packed_b_n) MZ_TRY(h, dalloc(h, &w.Bp, h->packed_b_n));
+        if (h->small_ok) { MZ_TRY(h, dalloc(h, &w.smw, h->sm_w_n)); MZ_TRY(h, dalloc(h, &w.smb, h->sm_b_n)); }
+        MZ_TRY(h, dalloc(h, &h->d_tr_queued, h->nflat));
+        MZ_TRY(h, hipHostMalloc(reinterpret_cast<void**>(&h->h_tr_cnt), 4 * sizeof(long long)));
+    }
+    // actors and the queue start from the learner's current (initial) nets (main.jl:23)
+    MZ_TRY(h, hipMemcpyAsync(w.flat, h->d_flat, h->nflat * 4, hipMemcpyDeviceToDevice, h->stream));
+    MZ_TRY(h, hipMemcpyAsync(h->d_tr_queued, h->d_flat, h->nflat * 4, hipMemcpyDeviceToDevice, h->stream));
+    if (wset_repack(h, w, h->stream)) return -1;
+    MZ_TRY(h, hipMemcpyAsync(h->h_tr_cnt, h->d_sp_counters, sizeof(long long), hipMemcpyDeviceToHost, h->stream));
+    MZ_TRY(h, hipStreamSynchronize(h->stream));
+    h->tr_B = B; h->tr_t = 0; h->tr_refresh = 0;
+    h->tr_games = h->h_tr_cnt[0];
+    return 0;
+}
+
+int mz_train_run(mz_handle* h, int32_t moves, uint32_t move0, uint32_t game_offset, int64_t* state_out,
+                 float* losses_dev, void* stream) {
+    if (!h) return -2;
+    if (!h->tr_B) return fail(h, "mz_train_init first");
+    if (moves < 0) return fail(h, "moves must be >= 0");
+    MZ_TRY(h, hipSetDevice(h->device));
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    int64_t steps = 0;
+    for (int32_t mv = 0; mv < moves; ++mv) {
+        // 1. self-play move with the actors' nets (SelfPlay.jl:343-380); temperature
+        //    visit_softmax_temperature_fn(t) (:48-56, 396-397)
+        const float temp = h->tr_t < 500000 ? 1.0f : h->tr_t < 750000 ? 0.5f : 0.25f;
+        wset_swap(h, h->tr_actor);
+        const int rc = mz_selfplay_move(h, move0 + (uint32_t)mv, game_offset, temp, st);
+        wset_swap(h, h->tr_actor);
+        if (rc) return rc;
+        // 2. games saved this move (save_game in slot order, inside the move)
+        MZ_TRY(h, hipMemcpyAsync(h->h_tr_cnt, h->d_sp_counters, sizeof(long long), hipMemcpyDeviceToHost, st));
+        MZ_TRY(h, hipStreamSynchronize(st));
+        const int64_t nfin = h->h_tr_cnt[0] - h->tr_games;
+        h->tr_games = h->h_tr_cnt[0];
+        // 3. one learner step per saved game while t <= training_steps (Learning.jl:327),
+        //    get_batch keyed by the step number, eta = Cos(step)
+        for (int64_t k = 0; k < nfin && h->tr_t <= h->conf.training_steps; ++k) {
+            const int64_t t = h->tr_t + 1;
+            if (mz_learner_train_dev(h, h->tr_B, (uint32_t)t, cos_schedule(t), losses_dev, st)) return -1;
+            h->tr_t = t;
+            ++steps;
+            // 4. checkpoint: the actors take the queued nets, the learner's nets are queued
+            //    (SelfPlay.jl:399-401 / Learning.jl:416-418: one checkpoint behind)
+            if (t % h->conf.checkpoint_interval == 0 && t > 1) {
+                MZ_TRY(h, hipMemcpyAsync(h->tr_actor.flat, h->d_tr_queued, h->nflat * 4, hipMemcpyDeviceToDevice, st));
+                if (wset_repack(h, h->tr_actor, st)) return -1;
+                MZ_TRY(h, hipMemcpyAsync(h->d_tr_queued, h->d_flat, h->nflat * 4, hipMemcpyDeviceToDevice, st));
+                ++h->tr_refresh;
+            }
+        }
+    }
+    if (state_out) {
+        state_out[0] = h->tr_t; state_out[1] = h->tr_games; state_out[2] = h->tr_refresh; state_out[3] = steps;
+    }
+    return 0;
+}
+
+int mz_train_weights_get(mz_handle* h, int which, int net, float* flat, size_t n) {
+    if (!h) return -2;
+    if (which == MZ_TRAIN_LEARNER) return mz_weights_get(h, net, flat, n);
+    if (!h->tr_B) return fail(h, "mz_train_init first");
+    if (which != MZ_TRAIN_ACTOR && which != MZ_TRAIN_QUEUED) return fail(h, "which: learner, actor or queued");
+    if (net < 0 || net > 2) return fail(h, "bad net id");
+    if (n != h->nparams[net]) return fail(h, "wrong parameter count");
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_TRY(h, sync_device(h));
+    const float* src = which == MZ_TRAIN_ACTOR ? h->tr_actor.flat : h->d_tr_queued;
+    MZ_TRY(h, hipMemcpy(flat, src + h->flat_off[net], n * 4, hipMemcpyDeviceToHost));
     return 0;
 }
 

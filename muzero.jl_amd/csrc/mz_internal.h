@@ -71,6 +71,7 @@ struct SearchParams {
     uint32_t rng_step, game_offset;
     uint64_t seed;
     float temperature, discount, dirichlet_alpha, exploration_eps;
+    const float* temp_g;   // per-game temperatures (self-play temperature_threshold) or NULL
     // inputs
     const float* obs; const uint8_t* legal; const int32_t* to_play;
     // outputs

@@ -55,14 +55,16 @@ __device__ __forceinline__ float per_priority(float x, int alpha) {
 __device__ __forceinline__ double per_uniform(uint32_t r) { return (double)(r >> 8) * 5.9604644775390625e-08; }
 
 // Categorical(p) with f32 probabilities p[i] = w[i] / S (S = ascending f32
-// sum of w): i = first index whose ascending f32 running sum is >= u (the
-// last index if none); *prob = p[i].  Sequential, one lane.
+// sum of w): i = first index whose ascending f32 running sum is > u (the
+// last index if none) — Distributions 0.25 rand(::DiscreteNonParametric)
+// advances while cp <= draw, so a zero-probability entry is never drawn;
+// *prob = p[i].  Sequential, one lane.
 __device__ __forceinline__ int per_categorical(const float* w, int n, double u, float* prob) {
     float S = 0.0f;
     for (int i = 0; i < n; ++i) S = S + w[i];
     int i = 0;
     float p = w[0] / S, c = p;
-    while ((double)c < u && i < n - 1) {
+    while ((double)c <= u && i < n - 1) {
         ++i;
         p = w[i] / S;
         c = c + p;
@@ -102,10 +104,10 @@ __device__ __forceinline__ void rp_sample_one(const RpSampleParams& Q, int b, in
     float gprob = 0.0f;
     if (Q.per) {                                                   // Categorical(game_probs), :96-103
         const double u = per_uniform(rg);
-        int lo = 0, hi = n - 1;                                    // first i with cum[i] >= u, else n-1
+        int lo = 0, hi = n - 1;                                    // first i with cum[i] > u, else n-1
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
-            if ((double)Q.per_cum[mid] >= u) hi = mid; else lo = mid + 1;
+            if ((double)Q.per_cum[mid] > u) hi = mid; else lo = mid + 1;
         }
         gi = (uint32_t)lo;
         gprob = Q.per_p[lo];

@@ -37,9 +37,11 @@ __device__ __forceinline__ void rn_load_a(float (&a)[4][4], const float* __restr
 // row block ob): ((p0+p1)+(p2+p3)) + b, BatchNorm in test mode, residual,
 // activation -> out[o][n].  The BatchNorm quotient (t − 0)/s uses r = 1/s:
 // q0 = t·r, e = fma(−q0, s, t), q0 + e·r is the IEEE quotient for every
-// float with |t| >= 2^-100 (exhaustive check: tools/check_bn_div.c,
-// tests/test_bn_div.py); below that, where e underflows, one wave-uniform
-// branch divides.
+// finite float with |t| >= 2^-100 (exhaustive check: tools/check_bn_div.c,
+// tests/test_bn_div.py); below that, where e underflows, and for ±inf / NaN
+// (q0 = ±inf makes e NaN, where IEEE gives ±inf: hidden states overflow once
+// Q1's in-place doubling has run ~128 levels deep, configs[4]), one
+// wave-uniform branch divides.
 // bias, γ, β of the 4 rows a lane holds in row block ob (issued before the
 // MFMAs of the unit so their latency hides under them)
 __device__ __forceinline__ void rn_load_ep(float (&ep)[3][4], const RLayer& L, const float* __restrict__ flat, int ob,
@@ -67,7 +69,7 @@ __device__ __forceinline__ void rn_epilogue(const RLayer& L, const mz_f32x4 (&ac
             float t = (acc[i][0][r] + acc[i][1][r]) + (acc[i][2][r] + acc[i][3][r]);
             t = t + bias;
             d[i][r] = t;
-            tiny |= fabsf(t) < 0x1p-100f;
+            tiny |= !(fabsf(t) >= 0x1p-100f) || fabsf(t) == INFINITY;   // tiny, ±inf or NaN
         }
     }
     if (L.bn) {
@@ -86,7 +88,8 @@ __device__ __forceinline__ void rn_epilogue(const RLayer& L, const mz_f32x4 (&ac
             for (int r = 0; r < 4; ++r)
 #pragma unroll
                 for (int i = 0; i < NB; ++i)
-                    if (fabsf(d[i][r]) < 0x1p-100f) q[i][r] = (d[i][r] - 0.0f) / bn_s;
+                    if (!(fabsf(d[i][r]) >= 0x1p-100f) || fabsf(d[i][r]) == INFINITY)
+                        q[i][r] = (d[i][r] - 0.0f) / bn_s;
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -463,7 +466,7 @@ __device__ __forceinline__ void rsearch_tree_body(const RSearchParams& P) {
             const int rN = st[RG_ROOTN];
             P.root_value[gg] = rN == 0 ? 0.0f : __int_as_float(st[RG_ROOTW]) / (float)rN;
             const uint32_t r = mz_rng_u32(P.seed, MZ_RNG_ACTION, gid, P.rng_step, 0);
-            P.action_out[gg] = select_action_dev(cnt, legal, A, P.temperature, r) + 1;
+            P.action_out[gg] = select_action_dev(cnt, legal, A, P.temp_g ? P.temp_g[gg] : P.temperature, r) + 1;
         }
     }
 }
@@ -650,7 +653,7 @@ __device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
         if (a == 0) {
             P.root_value[gg] = rN == 0 ? 0.0f : rW / (float)rN;
             const uint32_t r = mz_rng_u32(P.seed, MZ_RNG_ACTION, gid, P.rng_step, 0);
-            P.action_out[gg] = select_action_dev(cnt, legal, A, P.temperature, r) + 1;
+            P.action_out[gg] = select_action_dev(cnt, legal, A, P.temp_g ? P.temp_g[gg] : P.temperature, r) + 1;
         }
     }
 }

@@ -65,6 +65,7 @@ struct RSearchParams {
     uint32_t rng_step, game_offset;
     uint64_t seed;
     float temperature, discount, dirichlet_alpha, exploration_eps;
+    const float* temp_g;   // per-game temperatures (self-play temperature_threshold) or NULL
     const float* obs; const uint8_t* legal; const int32_t* to_play;
     float* child_visits; float* root_value; int32_t* action_out;
     const double* pbc_tab; const double* sqrt_tab; const float* aval_tab;

@@ -204,7 +204,7 @@ __device__ __forceinline__ void search_body(const SearchParams& P) {
             const int rN = sg_rootN[g];
             P.root_value[gg] = rN == 0 ? 0.0f : sg_rootW[g] / (float)rN;
             const uint32_t r = mz_rng_u32(P.seed, MZ_RNG_ACTION, gid, P.rng_step, 0);
-            P.action_out[gg] = select_action_dev(cnt, legal, A, P.temperature, r) + 1;
+            P.action_out[gg] = select_action_dev(cnt, legal, A, P.temp_g ? P.temp_g[gg] : P.temperature, r) + 1;
         }
         if (LDS_TREE && P.dump_tree) dump_tree(tree, gtree, E, NN, a);
     }

@@ -123,6 +123,8 @@ extern "C" __global__ __launch_bounds__(256) void mz_sp_prepare(SpParams S) {
         const uint32_t m = env_legal(S, g);
         for (int a = 0; a < S.A; ++a) S.legal[(size_t)g * S.A + a] = (m >> a) & 1u;
         S.tp[g] = S.player[g];                                     // :351
+        if (S.temp_g)                                              // :344-346
+            S.temp_g[g] = S.temp_threshold >= 0 && t >= S.temp_threshold ? 0.0f : S.temperature;
     }
 }
 

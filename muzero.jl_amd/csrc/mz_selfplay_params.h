@@ -48,6 +48,9 @@ struct SpParams {
     // PER (conf.PER): initial priorities of a stored game (save_game, ReplayBuffer.jl:133-145)
     int per, per_alpha, td;
     const float* disc_pow;
+    // temperature_threshold (SelfPlay.jl:344-346): a game with >= temp_threshold
+    // moves recorded plays at temperature 0 (-1 = nothing: every slot at `temperature`)
+    float temperature; int temp_threshold; float* temp_g;   // temp_g [G]
 };
 
 // get_batch + make_target (ReplayBuffer.jl:5-50, 73-107, 188-217) on the shard

@@ -378,7 +378,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
             const int rN = sg_rootN[g];
             P.root_value[gg] = rN == 0 ? 0.0f : sg_rootW[g] / (float)rN;
             const uint32_t r = mz_rng_u32(P.seed, MZ_RNG_ACTION, gid, P.rng_step, 0);
-            P.action_out[gg] = sm_select_action(cnt, legal, A, P.temperature, r) + 1;
+            P.action_out[gg] = sm_select_action(cnt, legal, A, P.temp_g ? P.temp_g[gg] : P.temperature, r) + 1;
         }
         if (P.dump_tree) {
             TreeView dst = tree_view(P.tree + (size_t)gg * P.tree_game_bytes, E, NN);

@@ -84,7 +84,9 @@ def per_uniform(r):
 
 def per_categorical(w, u):
     """Categorical over p_i = w_i / S (S = ascending f32 sum): the first index
-    whose ascending f32 running sum of p is >= u (else the last); returns
+    whose ascending f32 running sum of p is > u (else the last; Distributions
+    0.25 advances while cp <= draw, so zero-probability entries are never
+    drawn); returns
     (index, p_index).  The restatement of rand(rng, Categorical(p)) used by
     sample_n_games / sample_position with PER (ReplayBuffer.jl:75-78, 96-103)."""
     f32 = np.float32
@@ -94,7 +96,7 @@ def per_categorical(w, u):
     i = 0
     p = f32(f32(w[0]) / S)
     c = p
-    while float(c) < u and i < len(w) - 1:
+    while float(c) <= u and i < len(w) - 1:
         i += 1
         p = f32(f32(w[i]) / S)
         c = f32(c + p)

@@ -107,14 +107,18 @@ class BatchedSelfPlay:
             h.observation_history.append(self.env.board[g].astype(np.float32))  # :352
         obs = self._stacked()                                                 # :355
         legal = self.env.legal_mask()
-        temps = temperature
-        if c.temperature_threshold is not None:
-            # per-game threshold (:344-346) needs per-game temperatures: split by group
-            moves = np.array([len(h.action_history) for h in self.histories])
-            if np.any(moves >= c.temperature_threshold):
-                raise NotImplementedError("temperature_threshold with mixed move counts")
         cv, rv, act = self.eng.mcts_search(obs, legal, tp, exploration=True, rng_step=self.step,
-                                           game_offset=self.game_offset, temperature=temps)  # :359-360
+                                           game_offset=self.game_offset, temperature=temperature)  # :359-360
+        if c.temperature_threshold is not None:
+            # :344-346: a game with >= temperature_threshold moves plays at temperature 0.
+            # A game's search depends only on its own inputs and Philox keys (game id,
+            # step), so the batch is searched again at 0 and those games take that action.
+            moves = np.array([len(h.action_history) for h in self.histories])
+            cold = moves >= c.temperature_threshold
+            if cold.any() and temperature != 0.0:
+                _, _, act0 = self.eng.mcts_search(obs, legal, tp, exploration=True, rng_step=self.step,
+                                                  game_offset=self.game_offset, temperature=0.0)
+                act = np.where(cold, act0, act)
         if self.opponent == "random":                                         # :357-362, :321
             for g in np.flatnonzero(tp != self.muzero_player):
                 acts = np.flatnonzero(legal[g])

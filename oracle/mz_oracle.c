@@ -915,39 +915,73 @@ EXPORT void ora_unroll(const mz_config* c, const ora_nethp* hp, const float* Pre
     free(h); free(sa);
 }
 
-/* loss (:261-288) data terms; l2 = sum(sqnorm, params) per net in f64. */
-EXPORT void ora_losses(const mz_config* c, int B, const float* pv, const float* pp, const float* tv,
-                       const float* tp, const float* gscale, float* value_loss, float* policy_loss) {
-    int A = c->action_space_size, K = c->num_unroll_steps;
-    /* value: mse(agg = mean((sum(x, dims=1) ./ g) .* 1)) */
-    float vs = 0.0f;
-    for (int j = 0; j < B; ++j) {
-        float s = 0.0f;
-        for (int k = 0; k <= K; ++k) {
-            float d = pv[(size_t)j * (K + 1) + k] - tv[(size_t)j * (K + 1) + k];
-            s = s + d * d;
-        }
-        vs = vs + s / gscale[j];
+/* loss (:261-288) data terms.  Julia's Float32 `sum`/`mean` are pairwise and
+ * not reproducible offline; the restatement fixes one order, the
+ * engine's lg_fold (muzero.jl_amd/csrc/mz_learner_device.h): each sample's
+ * K+1 step terms in ascending k in f32, then the cross-sample sums in f64 —
+ * 64 lanes (sample j on lane j mod 64, ascending j), folded by the xor
+ * butterfly (offsets 32..1) into lane 0.  Both sides therefore round once
+ * from a near-exact f64 sum.                                                 */
+static double fold64(const double* lanes) {
+    double x[64], y[64];
+    memcpy(x, lanes, sizeof(x));
+    for (int o = 32; o >= 1; o >>= 1) {
+        for (int l = 0; l < 64; ++l) y[l] = x[l] + x[l ^ o];
+        memcpy(x, y, sizeof(x));
     }
-    *value_loss = vs / (float)B;
-    /* policy: (1,1,B) ./ (1,B) broadcast to (1,B,B) then mean (Q11) */
-    float ce[4096];
-    for (int j = 0; j < B; ++j) {
-        float s = 0.0f;
-        for (int k = 0; k <= K; ++k)
-            s = s + policy_ce(pp + ((size_t)j * (K + 1) + k) * A, tp + ((size_t)j * (K + 1) + k) * A, A);
-        ce[j] = s;
-    }
-    float ps = 0.0f;
-    for (int j = 0; j < B; ++j)
-        for (int k = 0; k < B; ++k) ps = ps + ce[k] / gscale[j];
-    *policy_loss = ps / (float)((size_t)B * B);
+    return x[0];
 }
 
+EXPORT void ora_losses_w(const mz_config* c, int B, const float* pv, const float* pp, const float* tv,
+                         const float* tp, const float* gscale, const float* wts, float* value_loss,
+                         float* policy_loss) {
+    int A = c->action_space_size, K = c->num_unroll_steps;
+    double sv[64] = {0}, sc[64] = {0}, sg[64] = {0};
+    for (int j = 0; j < B; ++j) {
+        float s = 0.0f, ce = 0.0f;
+        for (int k = 0; k <= K; ++k) {
+            float d = pv[(size_t)j * (K + 1) + k] - tv[(size_t)j * (K + 1) + k];
+            s = s + d * d;                                           /* mse, :273 */
+            ce = ce + policy_ce(pp + ((size_t)j * (K + 1) + k) * A, tp + ((size_t)j * (K + 1) + k) * A, A);
+        }
+        float w = wts ? wts[j] : 1.0f;                               /* PER weight_batch, :271-285 */
+        sv[j & 63] += (double)((s / gscale[j]) * w);
+        sc[j & 63] += (double)ce;                                    /* Σ_k CE_k */
+        sg[j & 63] += (double)w / (double)gscale[j];
+    }
+    /* value: mean((sum(x, dims=1) ./ g) .* w) */
+    *value_loss = (float)(fold64(sv) / (double)B);
+    /* policy: (1,1,B) ./ (1,B) broadcast to (1,B,B) then mean (Q11):
+     * Σ_j CE_j · Σ_i w_i/g_i / B² */
+    *policy_loss = (float)(fold64(sc) * fold64(sg) / ((double)B * (double)B));
+}
+
+EXPORT void ora_losses(const mz_config* c, int B, const float* pv, const float* pp, const float* tv,
+                       const float* tp, const float* gscale, float* value_loss, float* policy_loss) {
+    ora_losses_w(c, B, pv, pp, tv, tp, gscale, NULL, value_loss, policy_loss);
+}
+
+/* sum(sqnorm, params) (:287) in f64, in the engine's fixed order
+ * (lg_l2_slice + lg_tree256 + lg_fold): 32 slices of 256 threads, thread t
+ * of slice b summing elements b·256 + t + j·8192 in ascending j, a pairwise
+ * tree over the 256 threads (offsets 128..1), then the 32 slice sums on
+ * lanes 0..31 of the 64-lane butterfly.                                      */
 EXPORT double ora_sqnorm(const float* P, size_t n) {
-    double s = 0.0;
-    for (size_t i = 0; i < n; ++i) s += (double)P[i] * (double)P[i];
-    return s;
+    enum { NB = 32, NT = 256 };
+    const size_t stride = (size_t)NB * NT;
+    double part[64] = {0};
+    for (int b = 0; b < NB; ++b) {
+        double red[NT];
+        for (int t = 0; t < NT; ++t) {
+            double s = 0.0;
+            for (size_t i = (size_t)b * NT + t; i < n; i += stride) s += (double)P[i] * (double)P[i];
+            red[t] = s;
+        }
+        for (int o = NT / 2; o > 0; o >>= 1)
+            for (int t = 0; t < o; ++t) red[t] += red[t + o];
+        part[b] = red[0];
+    }
+    return fold64(part);
 }
 
 /* Flux 0.12 ADAMW() = Optimiser(ADAM(η, (0.9, 0.999)), WeightDecay(0));
@@ -997,6 +1031,150 @@ EXPORT void ora_learner_step(const mz_config* c, const ora_nethp* hp, float* Pre
     ora_adam_2theta(Pdyn, m_all + n0 + n1, v_all + n0 + n1, n2, bp, eta);
     bp[0] = bp[0] * 0.9; bp[1] = bp[1] * 0.999;
     free(pv); free(pr); free(pp);
+}
+
+/* ================================================== actor–learner loop
+ * self_play! (SelfPlay.jl:384-419) ‖ learning! (Learning.jl:306-438), the
+ * coupling of quirk Q16 restated deterministically for G lockstep self-play
+ * slots — the schedule of the engine's mz_train_run:
+ *   1. one move of every slot (play_game's loop body, SelfPlay.jl:343-380)
+ *      with the ACTOR's nets: move key move0 + m, game id game_offset + g,
+ *      temperature visit_softmax_temperature_fn(t) (:48-56, t = learner steps
+ *      so far), 0 once a game has temperature_threshold moves (:344-346);
+ *   2. the games that ended are saved in slot order (save_game,
+ *      ReplayBuffer.jl:133-161, FIFO of `cap` games) and their slots restart;
+ *   3. one learner step per saved game (self_play! take!s training_step once
+ *      per game, :396; learning! put!s once per step, Learning.jl:411) while
+ *      t <= training_steps (:327): get_batch keyed by step t+1, the
+ *      ref_semantics step with eta = Cos(t+1); t += 1;
+ *   4. after step t with t % checkpoint_interval == 0 && t > 1 the actor
+ *      takes the queued nets and the learner's nets of step t are queued
+ *      (remote_NNs is a capacity-1 channel that starts with the initial nets,
+ *      only fetch()ed by self-play, :392, 399-401; Learning.jl:416-418): the
+ *      actor runs one checkpoint behind.
+ * TicTacToe only (the oracle's env).  P{l,a,q}[3]: learner / actor / queued
+ * nets, updated in place; the learner's ADAM state m, v, bp as in
+ * ora_learner_step.  Outputs: t (in/out), counters {num_played_games,
+ * num_played_steps, total_samples}, the held games (oldest first: T, obs
+ * (27,T), actions, rewards, to_play, child visits (A,T), root values; each
+ * sized for max_moves + 1 moves), the slots' move counts / boards / players,
+ * the last step's losses.                                                   */
+static double ora_temp_fn(int64_t t) { return t < 500000 ? 1.0 : t < 750000 ? 0.5 : 0.25; }
+
+EXPORT int ora_train_loop(const mz_config* cin, const ora_nethp* hp, float* Pl0, float* Pl1, float* Pl2,
+                          float* Pa0, float* Pa1, float* Pa2, float* Pq0, float* Pq1, float* Pq2,
+                          float* m_all, float* v_all, double* bp, uint64_t seed, int G, int cap, int moves,
+                          uint32_t move0, uint32_t game_offset, int64_t* t_io, int64_t* counters,
+                          int32_t* held_T, float* held_obs, int32_t* held_act, float* held_rew,
+                          int32_t* held_tp, float* held_cv, float* held_rv, int32_t* slot_len,
+                          uint8_t* slot_board, int32_t* slot_player, float* losses) {
+    mz_config c = *cin;
+    const int A = c.action_space_size, Tm = c.max_moves + 1, OS = 27, B = c.batch_size, K = c.num_unroll_steps;
+    if (c.observation_shape[0] * c.observation_shape[1] * c.observation_shape[2] != OS || A != 9) return -1;
+    const size_t n0 = ora_param_count(&c, hp, MZ_NET_REPR), n1 = ora_param_count(&c, hp, MZ_NET_PRED),
+                 n2 = ora_param_count(&c, hp, MZ_NET_DYN);
+    OCtx X; ctx_init(&X, &c, hp, Pa0, Pa1, Pa2, seed);
+    /* games in progress and the ring, (27,T) float observations as OHist wants */
+    float* s_obs = calloc((size_t)G * Tm * OS, 4); int32_t* s_act = calloc((size_t)G * Tm, 4);
+    float* s_rew = calloc((size_t)G * Tm, 4); int32_t* s_tp = calloc((size_t)G * Tm, 4);
+    float* s_cv = calloc((size_t)G * Tm * A, 4); float* s_rv = calloc((size_t)G * Tm, 4);
+    int* s_len = calloc(G, sizeof(int));
+    OTTT* env = malloc(sizeof(OTTT) * G);
+    for (int g = 0; g < G; ++g) ttt_reset(&env[g]);
+    float* r_obs = calloc((size_t)cap * Tm * OS, 4); int32_t* r_act = calloc((size_t)cap * Tm, 4);
+    float* r_rew = calloc((size_t)cap * Tm, 4); int32_t* r_tp = calloc((size_t)cap * Tm, 4);
+    float* r_cv = calloc((size_t)cap * Tm * A, 4); float* r_rv = calloc((size_t)cap * Tm, 4);
+    int* r_len = calloc(cap, sizeof(int));
+    int64_t played = 0, steps = 0, samples = 0, t = *t_io;
+    int osz = c.observation_shape[0] * c.observation_shape[1] *
+              (c.observation_shape[2] * (c.stacked_observations + 1) + c.stacked_observations);
+    float* b_obs = malloc(sizeof(float) * (size_t)B * osz); float* b_act = malloc(sizeof(float) * B * (K + 1));
+    float* b_tv = malloc(sizeof(float) * B * (K + 1)); float* b_tr = malloc(sizeof(float) * B * (K + 1));
+    float* b_tp = malloc(sizeof(float) * (size_t)B * (K + 1) * A); float* b_gs = malloc(sizeof(float) * B);
+    int32_t* b_idx = malloc(sizeof(int32_t) * 2 * B);
+    OHist* hist = malloc(sizeof(OHist) * cap);
+    float stacked[1024];
+    int* fin = malloc(sizeof(int) * G);
+    for (int mv = 0; mv < moves; ++mv) {
+        const uint32_t step = move0 + (uint32_t)mv;
+        int nfin = 0;
+        for (int g = 0; g < G; ++g) {                                   /* 1. one move per slot */
+            const int T = s_len[g];
+            float* oh = s_obs + (size_t)g * Tm * OS;
+            for (int i = 0; i < OS; ++i) oh[(size_t)T * OS + i] = (float)env[g].b[i];   /* :352 */
+            ora_stacked_obs(&c, oh, s_act + (size_t)g * Tm, T + 1, stacked);           /* :355 */
+            uint8_t legal[MAXA]; ttt_legal(&env[g], legal);
+            const int p = env[g].player;                                /* :351 */
+            float temp = (float)ora_temp_fn(t);
+            if (c.temperature_threshold >= 0 && T >= c.temperature_threshold) temp = 0.0f;   /* :344-346 */
+            const uint32_t gid = game_offset + (uint32_t)g;
+            int root = run_mcts(&X, stacked, legal, p, 1, gid, step, NULL);               /* :359 */
+            int a = select_action(&X, root, temp, gid, step) + 1;       /* :360 */
+            ttt_step(&env[g], a);                                       /* :366 */
+            float r = ttt_reward(&env[g], p);                           /* :367 */
+            int done = ttt_terminated(&env[g]);                         /* :368 */
+            search_stats(&X, root, s_cv + ((size_t)g * Tm + T) * A, s_rv + (size_t)g * Tm + T);   /* :375 */
+            s_act[(size_t)g * Tm + T] = a; s_rew[(size_t)g * Tm + T] = r; s_tp[(size_t)g * Tm + T] = p;
+            s_len[g] = T + 1;
+            if (done || s_len[g] > c.max_moves) fin[nfin++] = g;        /* :343 */
+        }
+        for (int k = 0; k < nfin; ++k) {                                /* 2. save_game, slot order */
+            const int g = fin[k], T = s_len[g];
+            played += 1; steps += T; samples += T;
+            const int slot = (int)((played - 1) % cap);
+            if (played > cap) samples -= r_len[slot];                   /* FIFO eviction, :158 */
+            r_len[slot] = T;
+            memcpy(r_obs + (size_t)slot * Tm * OS, s_obs + (size_t)g * Tm * OS, sizeof(float) * (size_t)T * OS);
+            memcpy(r_act + (size_t)slot * Tm, s_act + (size_t)g * Tm, 4 * (size_t)T);
+            memcpy(r_rew + (size_t)slot * Tm, s_rew + (size_t)g * Tm, 4 * (size_t)T);
+            memcpy(r_tp + (size_t)slot * Tm, s_tp + (size_t)g * Tm, 4 * (size_t)T);
+            memcpy(r_cv + (size_t)slot * Tm * A, s_cv + (size_t)g * Tm * A, 4 * (size_t)T * A);
+            memcpy(r_rv + (size_t)slot * Tm, s_rv + (size_t)g * Tm, 4 * (size_t)T);
+            s_len[g] = 0; ttt_reset(&env[g]);
+        }
+        for (int k = 0; k < nfin; ++k) {                                /* 3. one learner step per game */
+            if (t > c.training_steps) break;                            /* while t <= training_steps */
+            const int nh = (int)(played < cap ? played : cap);
+            const int64_t oldest = played - nh + 1;
+            for (int i = 0; i < nh; ++i) {
+                const int slot = (int)((oldest + i - 1) % cap);
+                hist[i] = (OHist){r_len[slot], r_obs + (size_t)slot * Tm * OS, r_act + (size_t)slot * Tm,
+                                  r_rew + (size_t)slot * Tm, r_tp + (size_t)slot * Tm,
+                                  r_cv + (size_t)slot * Tm * A, r_rv + (size_t)slot * Tm};
+            }
+            const uint32_t st = (uint32_t)(t + 1);
+            ora_get_batch(&c, hist, nh, (int)oldest, seed, st, b_obs, b_act, b_tv, b_tr, b_tp, b_gs, b_idx);
+            ora_learner_step(&c, hp, Pl0, Pl1, Pl2, m_all, v_all, bp, B, b_obs, b_act, b_tv, b_tp, b_gs,
+                             ora_cos_schedule(1e-4, 1e-1, 10, (int)st), losses);
+            t = st;
+            if (t % c.checkpoint_interval == 0 && t > 1) {              /* 4. actor <- queued, queue <- learner */
+                memcpy(Pa0, Pq0, 4 * n0); memcpy(Pa1, Pq1, 4 * n1); memcpy(Pa2, Pq2, 4 * n2);
+                memcpy(Pq0, Pl0, 4 * n0); memcpy(Pq1, Pl1, 4 * n1); memcpy(Pq2, Pl2, 4 * n2);
+            }
+        }
+    }
+    *t_io = t;
+    counters[0] = played; counters[1] = steps; counters[2] = samples;
+    const int nh = (int)(played < cap ? played : cap);
+    for (int i = 0; i < nh; ++i) {                                      /* held games, oldest first */
+        const int slot = (int)((played - nh + i) % cap), T = r_len[slot];
+        held_T[i] = T;
+        memcpy(held_obs + (size_t)i * Tm * OS, r_obs + (size_t)slot * Tm * OS, sizeof(float) * (size_t)T * OS);
+        memcpy(held_act + (size_t)i * Tm, r_act + (size_t)slot * Tm, 4 * (size_t)T);
+        memcpy(held_rew + (size_t)i * Tm, r_rew + (size_t)slot * Tm, 4 * (size_t)T);
+        memcpy(held_tp + (size_t)i * Tm, r_tp + (size_t)slot * Tm, 4 * (size_t)T);
+        memcpy(held_cv + (size_t)i * Tm * A, r_cv + (size_t)slot * Tm * A, 4 * (size_t)T * A);
+        memcpy(held_rv + (size_t)i * Tm, r_rv + (size_t)slot * Tm, 4 * (size_t)T);
+    }
+    for (int g = 0; g < G; ++g) {
+        slot_len[g] = s_len[g]; slot_player[g] = env[g].player;
+        memcpy(slot_board + (size_t)g * OS, env[g].b, OS);
+    }
+    ctx_free(&X);
+    free(s_obs); free(s_act); free(s_rew); free(s_tp); free(s_cv); free(s_rv); free(s_len); free(env);
+    free(r_obs); free(r_act); free(r_rew); free(r_tp); free(r_cv); free(r_rv); free(r_len);
+    free(b_obs); free(b_act); free(b_tv); free(b_tr); free(b_tp); free(b_gs); free(b_idx); free(hist); free(fin);
+    return nh;
 }
 
 /* ======================================================== detmath exports

@@ -59,6 +59,11 @@ def lib():
         L.ora_cos_schedule.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int]
         L.ora_learner_step.argtypes = [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_int, _VP, _VP, _VP,
                                        _VP, _VP, ctypes.c_double, _VP]
+        L.ora_losses_w.argtypes = [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]
+        L.ora_train_loop.restype = ctypes.c_int
+        L.ora_train_loop.argtypes = [_VP, _VP] + [_VP] * 9 + [_VP, _VP, _VP, ctypes.c_uint64, ctypes.c_int,
+                                                           ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
+                                                           ctypes.c_uint32] + [_VP] * 13
         for n, r, a in [("ora_det_expf", ctypes.c_float, [ctypes.c_float]),
                         ("ora_det_tanhf", ctypes.c_float, [ctypes.c_float]),
                         ("ora_det_logf", ctypes.c_float, [ctypes.c_float]),
@@ -205,6 +210,44 @@ class Oracle:
                                 _p(a["target_values"]), _p(a["target_policies"]), _p(a["gradient_scale"]),
                                 eta, _p(losses))
         return losses
+
+
+def train_loop(ora, G, cap, moves, move0=0, game_offset=0, state=None):
+    """ora_train_loop (oracle/mz_oracle.c): the actor–learner schedule of
+    mz_train_run from fresh slots — ora.params are the learner's nets (updated
+    in place); returns dict(t, counters, held games, slots, actor / queued
+    nets, losses, state)."""
+    c, h = ora._c()
+    conf = ora.cconf
+    A, Tm = ora.A, conf.max_moves + 1
+    st = state or ora.learner_state()
+    actor = [p.copy() for p in ora.params]
+    queued = [p.copy() for p in ora.params]
+    t = np.zeros(1, np.int64)
+    counters = np.zeros(3, np.int64)
+    hT = np.zeros(cap, np.int32)
+    hobs = np.zeros((cap, Tm, 27), np.float32)
+    hact = np.zeros((cap, Tm), np.int32)
+    hrew = np.zeros((cap, Tm), np.float32)
+    htp = np.zeros((cap, Tm), np.int32)
+    hcv = np.zeros((cap, Tm, A), np.float32)
+    hrv = np.zeros((cap, Tm), np.float32)
+    slen = np.zeros(G, np.int32)
+    sboard = np.zeros((G, 27), np.uint8)
+    splayer = np.zeros(G, np.int32)
+    losses = np.zeros(6, np.float32)
+    P = ora.params
+    nh = ora.L.ora_train_loop(c, h, _p(P[0]), _p(P[1]), _p(P[2]), _p(actor[0]), _p(actor[1]), _p(actor[2]),
+                              _p(queued[0]), _p(queued[1]), _p(queued[2]), _p(st["m"]), _p(st["v"]), _p(st["bp"]),
+                              ora.seed, G, cap, moves, move0, game_offset, _p(t), _p(counters), _p(hT), _p(hobs),
+                              _p(hact), _p(hrew), _p(htp), _p(hcv), _p(hrv), _p(slen), _p(sboard), _p(splayer),
+                              _p(losses))
+    assert nh >= 0, "ora_train_loop: TicTacToe only"
+    held = [dict(observation=hobs[i, :hT[i]].copy(), action=hact[i, :hT[i]].copy(), reward=hrew[i, :hT[i]].copy(),
+                 to_play=htp[i, :hT[i]].copy(), child_visits=hcv[i, :hT[i]].copy(), root_values=hrv[i, :hT[i]].copy())
+            for i in range(nh)]
+    return dict(t=int(t[0]), counters=counters, held=held, slot_len=slen, slot_board=sboard, slot_player=splayer,
+                actor=actor, queued=queued, losses=losses, state=st)
 
 
 def histories_to_c(histories):

@@ -80,3 +80,14 @@ def test_prioritized_batch_weights_and_update(ttt):
         g2, p2 = idx[last]
         assert h.priorities[pos - 1] == per_priority(pv[last][pos - p2] - b["target_values"][last][pos - p2], 1)
         assert h.game_priority == h.priorities.max()
+
+
+def test_per_categorical_tie_rule():
+    """Distributions 0.25 rand(::DiscreteNonParametric) advances while
+    cp <= draw: an exact tie moves on, and a zero-probability entry is never
+    drawn, even at draw 0."""
+    w = np.array([0.0, 0.0, 2.0, 2.0], np.float32)
+    assert per_categorical(w, 0.0) == (2, np.float32(0.5))          # leading zeros skipped at u = 0
+    assert per_categorical(w, 0.5)[0] == 3                          # cp = 0.5 <= 0.5: the tie advances
+    assert per_categorical(w, 0.49)[0] == 2
+    assert per_categorical(np.array([1.0, 0.0], np.float32), 0.9999)[0] == 0

@@ -39,10 +39,10 @@ def _same_game(dev, host, osz):
         assert np.array_equal(a[k], b[k]), k
 
 
-def _play_both(kind, G, moves, cap, S=6, resnet=False, step0=100, temperature=1.0):
+def _play_both(kind, G, moves, cap, S=6, resnet=False, step0=100, temperature=1.0, thr=None):
     from muzero_jl_amd.selfplay import BatchedSelfPlay
     mod, env_cls, env_kind = _env(kind)
-    conf = dataclasses.replace(mod.conf, num_iters=S, replay_buffer_size=cap)
+    conf = dataclasses.replace(mod.conf, num_iters=S, replay_buffer_size=cap, temperature_threshold=thr)
     hyper = mod.resnet_hyper if resnet else mod.hyper
     eh, ed = _engines(mod, conf, hyper, G)
     sp = BatchedSelfPlay(eh, env_cls, G, game_offset=7, step0=step0)
@@ -65,6 +65,25 @@ def test_device_selfplay_matches_host(kind, G, moves):
     ln, board, player = ed.selfplay_slots()
     assert np.array_equal(ln, [len(h.action_history) for h in sp.histories])
     assert np.array_equal(board, sp.env.board.astype(np.uint8)) and np.array_equal(player, sp.env.player)
+    eh.close(); ed.close()
+
+
+@pytest.mark.parametrize("kind,resnet", [("ttt", False), ("ttt", True), ("c4", False)])
+def test_temperature_threshold_matches_host(kind, resnet):
+    """conf.temperature_threshold (SelfPlay.jl:344-346): once a game has
+    recorded that many moves it plays at temperature 0 — per slot on the
+    device (mz_sp_prepare writes each slot's temperature), per game on the
+    host; finished games and games in progress agree move for move."""
+    G, thr = 16, 2
+    conf, sp, eh, ed = _play_both(kind, G, 14, cap=8 * G, S=5, resnet=resnet, thr=thr)
+    osz = int(np.prod(conf.observation_shape))
+    counts, held = ed.replay_counts()
+    assert counts[0] == len(sp.finished) > 0
+    for i, h in enumerate(sp.finished):
+        _same_game(ed.replay_get_game(i), h, osz)
+    ln, board, _ = ed.selfplay_slots()
+    assert np.array_equal(ln, [len(h.action_history) for h in sp.histories])
+    assert np.array_equal(board, sp.env.board.astype(np.uint8))
     eh.close(); ed.close()
 
 
