@@ -80,6 +80,25 @@ def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0, resnet=False,
                        f"oracle/mz_oracle.c on {threads} host thread{'s' if threads > 1 else ''}, {dt:.1f} s")
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summaries
+    (profiles/pmc_*.json of tools/pmc_summary.py, profiles/pmc2_*.json of
+    tools/pmc_kernels.py: FETCH_SIZE x2 for the 16 B/lane image reads, per
+    MI355X_MICROARCH.md, + WRITE_SIZE); the latest round wins; None if none."""
+    traffic = None
+    for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+        with open(pmc) as f:
+            rec = json.load(f)
+        if rec.get("kernel") == kernel:
+            traffic = rec.get("hbm_bytes_per_launch")
+    for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc2_*.json"))):
+        with open(pmc) as f:
+            rec = json.load(f).get("kernels", {}).get(kernel)
+        if rec and "hbm_bytes_per_launch_fetch_x2" in rec:
+            traffic = rec["hbm_bytes_per_launch_fetch_x2"]
+    return traffic
+
+
 def workload(game, resnet, G, S):
     if game is atari:
         return (f"synthetic Atari-like 84x84x4 observations, ResNet with the Learning.jl:175-187 downsampler "
@@ -89,7 +108,8 @@ def workload(game, resnet, G, S):
                 f"{S} sims/move" + (" (configs[3]: 4096 games = 512/GPU x 8)" if resnet else ""))
     if resnet:
         return f"TicTacToe ResNet (2 blocks x 64 filters, 3x3), {G} games/GPU x {S} sims/move (configs[2])"
-    return f"TicTacToe FC (params.jl hyper), {G} games/GPU x {S} sims/move (configs[1])"
+    cfg = "configs[0]-style single game" if G == 1 else "configs[1]" if (G, S) == (512, 50) else "TicTacToe FC"
+    return f"TicTacToe FC (params.jl hyper), {G} games/GPU x {S} sims/move ({cfg})"
 
 
 def main():
@@ -105,6 +125,8 @@ def main():
                     help="timed moves of the device self-play loop (0 = skip that leg)")
     ap.add_argument("--sims", type=int, default=None, help="sims per move (default 50; atari 200)")
     ap.add_argument("--learner-steps", type=int, default=50)
+    ap.add_argument("--train-moves", type=int, default=20,
+                    help="timed moves of the actor-learner loop mz_train_run (0 = skip that leg)")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host threads of the oracle baseline (the box's CPU share for one GPU is 16)")
@@ -204,8 +226,8 @@ def main():
     # device — observation/stacked planes, search, env step, GameHistory and
     # replay-shard append — G games per rank, timed like the search leg
     pipe = None
+    env_kind = ENV_CONNECT4 if game is c4 else ENV_TICTACTOE
     if game is not atari:                                 # (no Atari env: the search leg is configs[4]'s step)
-        env_kind = ENV_CONNECT4 if game is c4 else ENV_TICTACTOE
         eng.selfplay_init(env_kind, G, max(G, conf.replay_buffer_size))
     mv = 1 << 20                                          # move counter (RNG step keys)
     if args.pipeline_moves > 0 and game is not atari:
@@ -276,6 +298,54 @@ def main():
     if world > 1:
         dist.all_reduce(tl, op=dist.ReduceOp.MAX)
     learner_sps = args.learner_steps / float(tl.item())
+    # per-step device time: events around each step on the launch stream, in
+    # a separate loop (recording events between steps adds host work)
+    nev = 20
+    lev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nev)]
+    for k in range(nev):
+        lev[k][0].record(stream)
+        lstep(5 + args.learner_steps + k)
+        lev[k][1].record(stream)
+    torch.cuda.synchronize()
+    lstep_ms = float(np.mean([a.elapsed_time(b) for a, b in lev]))
+    # the learner's dominant kernel: FC world 1 = the whole step is one launch
+    # (mz_learn_small*), timed by the events around it; ResNet = the unroll
+    # (mz_runroll_kernel), timed by the engine's events on its launch stream
+    if resnet:
+        eng.debug_enable(4)
+        eng.debug_kernel_time()
+        for k in range(5):
+            lstep(5 + args.learner_steps + nev + k)
+        torch.cuda.synchronize()
+        t_ms, n_l = eng.debug_kernel_time()
+        eng.debug_enable(0)
+        lkern, lkern_ms = "mz_runroll_kernel", t_ms / n_l
+    else:
+        lkern = "mz_learn_small1" if world == 1 else None
+        lkern_ms = lstep_ms
+
+    # ---- actor-learner loop (row a12, self_play! || learning!, Q16): self-play
+    # moves with the actors' nets and one learner step per finished game, the
+    # actors refreshed one checkpoint behind (mz_train_run, one GPU)
+    train = None
+    if args.train_moves > 0 and world == 1 and game is not atari:
+        eng.selfplay_init(env_kind, G, max(G, conf.replay_buffer_size))
+        eng.train_init(B)
+        eng.train_run(3, move0=mv, game_offset=rank * G, stream=sp)
+        mv += 3
+        torch.cuda.synchronize()
+        tt0 = time.perf_counter()
+        st0 = eng.train_run(args.train_moves, move0=mv, game_offset=rank * G, stream=sp)
+        torch.cuda.synchronize()
+        ttr = time.perf_counter() - tt0
+        mv += args.train_moves
+        train = {"moves": args.train_moves, "ms_per_move": round(ttr / args.train_moves * 1e3, 4),
+                 "node_expansions_per_s": round(G * S * args.train_moves / ttr, 1),
+                 "learner_steps": st0[3], "learner_steps_per_s": round(st0[3] / ttr, 1),
+                 "games_finished": st0[1], "actor_refreshes": st0[2],
+                 "schedule": "mz_train_run: one self-play move of all games with the actors' nets, then one "
+                             "learner step (B = batch_size, device get_batch) per finished game; actors take "
+                             "the queued nets every checkpoint_interval steps"}
 
     if rank == 0:
         total_exp = world * G * S * args.steps
@@ -288,14 +358,28 @@ def main():
         achieved = flop_launch / (kern_ms * 1e-3) / 1e12
         # HBM bytes per launch from the committed PMC summary of THIS kernel
         # variant (tools/pmc_summary.py; latest round wins), else null
-        traffic, variant = None, eng.search_variant()
-        if resnet:
-            variant = "mz_rsearch_nets"
-        for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
-            with open(pmc) as f:
-                rec = json.load(f)
-            if rec.get("kernel") == variant:
-                traffic = rec.get("hbm_bytes_per_launch")
+        variant = "mz_rsearch_nets" if resnet else eng.search_variant()
+        traffic = pmc_traffic(variant)
+        # learner roofline (north_star: HBM GB/s and MFMA utilisation of the
+        # learner): algorithmic FLOP of the unroll (2·B·(repr +
+        # (K+1)·pred + K·dyn) MACs) + ADAM (~10 FLOP/param, FC one-launch step);
+        # algorithmic bytes of the ADAM step = 28 B/param (θ, m, v read and
+        # written, the image scatter), measured traffic from the PMC summary
+        lroof = None
+        if lkern is not None:
+            nparam = sum(int(x.size) for x in nets)
+            f_unroll = 2 * B * (net_macs(conf, hyper, 0) + (K + 1) * net_macs(conf, hyper, 1) +
+                                K * net_macs(conf, hyper, 2))
+            lflop = f_unroll + (0 if resnet else 10 * nparam)
+            lbytes = 0 if resnet else 28 * nparam
+            lach = lflop / (lkern_ms * 1e-3) / 1e12
+            ltraffic = pmc_traffic(lkern)
+            hbm_gbs = (ltraffic if ltraffic else lbytes) / (lkern_ms * 1e-3) / 1e9
+            lroof = {"bound": "mfma", "achieved": round(lach, 4), "peak": PEAK_F32, "unit": "TFLOP/s",
+                     "frac": round(lach / PEAK_F32, 5), "traffic": ltraffic, "kernel": lkern,
+                     "kernel_ms": round(lkern_ms, 5), "flop_per_launch": lflop,
+                     "hbm_bytes_algorithmic": lbytes, "hbm_GBps": round(hbm_gbs, 2),
+                     "hbm_frac": round(hbm_gbs / 8000.0, 5)}
         cpu = cpu1 = None
         if world == 1 and not args.no_cpu:
             nt = max(1, min(args.cpu_threads, os.cpu_count() or 1))
@@ -315,6 +399,9 @@ def main():
                        "games_per_gpu": G, "sims_per_move": S, "global_games": G * world,
                        "parallelism": f"games sharded x{world}, learner dp{world} (RCCL all-reduce)"},
             "learner_steps_per_s": round(learner_sps, 1),
+            "learner_step_ms": round(lstep_ms, 5),
+            "learner_roofline": lroof,
+            "train_loop": train,
             "learner_config": {"batch_size": B, "num_unroll_steps": K, "mode": "ref_semantics",
                                "batch_source": "synthetic device batch" if game is atari else
                                ("mz_learner_train_dev: one launch — device get_batch + make_target + unroll + "

@@ -171,7 +171,8 @@ int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* leg
 
 /* Debug/parity: flags & 1 = keep a copy of every search's final tree in HBM
  * (the LDS-resident tree is otherwise discarded at kernel exit); flags & 2 =
- * time the ResNet search's network launches (mz_debug_kernel_time). */
+ * time the ResNet search's network launches, flags & 4 = the ResNet
+ * learner's unroll launches (mz_debug_kernel_time). */
 int mz_debug_enable(mz_handle* h, int flags);
 
 /* Debug/parity: copy the last search's tree statistics to host.  Per game,
@@ -183,9 +184,10 @@ int mz_debug_tree(mz_handle* h, int G, int32_t* edge_N, float* edge_W, float* ed
                   float* edge_R, int32_t* edge_child, int32_t* node_to_play);
 
 /* Measurement: with mz_debug_enable(h, 2) every network launch of the
- * ResNet search (mz_rsearch_nets, its dominant kernel) is bracketed by HIP
- * events on its stream; this returns the summed duration and the launch
- * count since the previous call, and resets them.                         */
+ * ResNet search (mz_rsearch_nets, its dominant kernel), with flag 4 every
+ * learner unroll launch (mz_runroll_kernel), is bracketed by HIP events on
+ * its stream; this returns the summed duration and the launch count since
+ * the previous call, and resets them.                                      */
 int mz_debug_kernel_time(mz_handle* h, double* total_ms, int* launches);
 
 /* Debug/parity: the last learner unroll's read-outs (Learning.jl:347-370)

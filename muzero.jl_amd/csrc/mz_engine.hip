@@ -38,6 +38,8 @@ extern "C" __global__ void mz_rsearch_tree_lds(RSearchParams P);
 extern "C" __global__ void mz_rsearch_tree_lds32(RSearchParams P);
 extern "C" __global__ void mz_rsearch_nets(RSearchParams P);
 extern "C" __global__ void mz_runroll_kernel(RUnrollParams U);
+extern "C" __global__ void mz_runroll_chain(RUnrollParams U);
+extern "C" __global__ void mz_runroll_pred(RUnrollParams U);
 extern "C" __global__ void mz_sp_prepare(SpParams S);
 extern "C" __global__ void mz_sp_commit(SpParams S);
 extern "C" __global__ void mz_sp_order(SpParams S);
@@ -133,6 +135,11 @@ struct mz_handle {
     std::vector<RPlan> rplan;               // [3]
     RPlan* d_rplan = nullptr;               // [3]
     int rn_ng = 0;
+    // the learner unroll's chain (mz_runroll_chain): the same nets on narrow tiles
+    std::vector<RPlan> rplan_l;
+    RPlan* d_rplan_l = nullptr;
+    int rn_ng_l = 0;
+    size_t rn_lds_l = 0;
     size_t rn_lds[3] = {0, 0, 0};
     float bn_s = 1.0f;
     int* d_rpath = nullptr; int* d_rgst = nullptr;          // ResNet search: [G][2(S+2)], [G][RG_INTS]
@@ -165,6 +172,7 @@ struct mz_handle {
     void* dp_comm = nullptr; int dp_world = 0, dp_rank = 0;  // mz_dp_init: RCCL communicator
     char* d_tree = nullptr; size_t tree_game_bytes = 0; bool lds_tree = false; int dump_tree = 0;
     int time_nets = 0;                      // mz_debug_enable flag 2: events around each ResNet nets launch
+    int time_unroll = 0;                    // flag 4: events around each ResNet learner unroll launch
     std::vector<hipEvent_t> tev; size_t tev_used = 0;
     bool use_res = false;                   // register-resident sim-plan kernel
     // small-batch kernel (mz_small.hip): schedule images + LDS layout
@@ -242,6 +250,7 @@ struct mz_handle {
     } while (0)
 
 static int fail(mz_handle* h, const std::string& m) { h->err = m; return -2; }
+static int timing_events(mz_handle* h, hipEvent_t* e0, hipEvent_t* e1);
 
 // Host-synchronous entry points (weights, state, replay read-outs, debug
 // copies) wait for ALL of this process's work on the device, not only the
@@ -1035,6 +1044,18 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
         h->rn_lds[n] = (size_t)h->rplan[n].lds_floats * 4;
     }
     h->packed_w_n = sw.size(); h->packed_b_n = 0;
+    {   // learner chain tiles: MZ_RN_NG_LEARN (power of two), default 1 (tools/rn_learner_ab.sh)
+        const char* e = std::getenv("MZ_RN_NG_LEARN");
+        int ngl = e ? std::atoi(e) : 1;
+        if (ngl < 1 || ngl > h->rn_ng || (ngl & (ngl - 1))) ngl = 1;
+        h->rn_ng_l = ngl;
+        int wl = 0;
+        h->rplan_l.resize(3);
+        for (int n = 0; n < 3; ++n) {
+            h->rplan_l[n] = rn_plan(h, sp[n], n, ngl, h->flat_off[n] + (n == 0 ? h->ds_n : 0), wl, nullptr);
+            h->rn_lds_l = std::max(h->rn_lds_l, (size_t)h->rplan_l[n].lds_floats * 4);
+        }
+    }
     h->inv_tile.assign(h->nflat, -1);
     for (size_t i = 0; i < sw.size(); ++i) if (sw[i] >= 0) h->inv_tile[(size_t)sw[i]] = (int)i;
     h->inv_small.assign(h->nflat, -1);
@@ -1049,6 +1070,9 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
     CK(al_i(&h->d_inv_small, h->inv_small));
     CK(al(&h->d_rplan, 3));
     CK(hipMemcpy(h->d_rplan, h->rplan.data(), 3 * sizeof(RPlan), hipMemcpyHostToDevice) == hipSuccess
+           ? 0 : fail(h, "copy"));
+    CK(al(&h->d_rplan_l, 3));
+    CK(hipMemcpy(h->d_rplan_l, h->rplan_l.data(), 3 * sizeof(RPlan), hipMemcpyHostToDevice) == hipSuccess
            ? 0 : fail(h, "copy"));
     CK(al(&h->d_flat, h->nflat));
     CK(al(&h->d_Wp, h->packed_w_n));
@@ -1076,6 +1100,10 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
     }
     CK(hipFuncSetAttribute((const void*)mz_runroll_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)lmax) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll)"));
+    CK(hipFuncSetAttribute((const void*)mz_runroll_pred, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)lmax) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_pred)"));
+    CK(hipFuncSetAttribute((const void*)mz_runroll_chain, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)h->rn_lds_l) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_chain)"));
     CK(hipFuncSetAttribute((const void*)mz_rsearch_nets, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)rsearch_nets_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(nets)"));
     // search buffers (trees and hidden states in HBM)
@@ -1547,6 +1575,7 @@ int mz_debug_enable(mz_handle* h, int flags) {
     if (!h) return -2;
     h->dump_tree = flags & 1;
     h->time_nets = (flags >> 1) & 1;
+    h->time_unroll = (flags >> 2) & 1;
     return 0;
 }
 
@@ -1601,7 +1630,7 @@ static int ensure_batch(mz_handle* h, int B) {
     for (int i = 0; i < 9; ++i) MZ_TRY(h, dalloc(h, bufs[i], sizes[i]));
     MZ_TRY(h, dalloc(h, &h->d_lterm, (size_t)2 * B * (K + 1)));
     MZ_TRY(h, dalloc(h, &h->d_bw, (size_t)B));
-    if (h->kind == 1) MZ_TRY(h, dalloc(h, &h->d_rhs, (size_t)B * h->H));
+    if (h->kind == 1) MZ_TRY(h, dalloc(h, &h->d_rhs, (size_t)B * std::max(K, 1) * h->H));
     h->bcap = B;
     return 0;
 }
@@ -1615,7 +1644,8 @@ static int learner_losses(mz_handle* h, const mz_batch* b, float* grad_dev, floa
 
 // ResNet learner: the unroll on the network kernels, then the shared loss /
 // ∇ = 2θ kernel (the plans' outputs are already activated)
-static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, void* stream) {
+static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, void* stream,
+                         bool fuse_adam = false, double eta = 0.0) {
     const int B = b->batch_size;
     if (B < 1) return fail(h, "batch_size must be >= 1");
     if (ensure_batch(h, B)) return -1;
@@ -1629,10 +1659,25 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
         U.obs = h->d_dsb;
     } U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
     U.hs = h->d_rhs; U.plans = h->d_rplan; U.Wimg = h->d_Wp; U.flat = h->d_flat;
+    U.plans_l = h->d_rplan_l; U.ng_l = h->rn_ng_l;
     void* args[] = {&U};
-    MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_kernel, dim3((B + U.ng - 1) / U.ng), dim3(RN_THREADS), args,
-                              runroll_lds(h), st));
-    return learner_losses(h, b, grad_dev, losses_dev, st, MZ_ACT_IDENTITY, MZ_ACT_IDENTITY);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (h->time_unroll) {
+        if (timing_events(h, &e0, &e1)) return -1;
+        MZ_TRY(h, hipEventRecord(e0, st));
+    }
+    if (std::getenv("MZ_RUNROLL_FUSED")) {          // the one-kernel unroll (pred inside the chain)
+        MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_kernel, dim3((B + U.ng - 1) / U.ng), dim3(RN_THREADS),
+                                  args, runroll_lds(h), st));
+    } else {                                        // chain on narrow tiles, then the B·K predictions
+        const int KH = std::max(U.K, 1);
+        MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_chain, dim3((B + U.ng_l - 1) / U.ng_l), dim3(RN_THREADS),
+                                  args, h->rn_lds_l, st));
+        MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred, dim3((B * KH + U.ng - 1) / U.ng), dim3(RN_THREADS),
+                                  args, runroll_lds(h), st));
+    }
+    if (e1) MZ_TRY(h, hipEventRecord(e1, st));
+    return learner_losses(h, b, grad_dev, losses_dev, st, MZ_ACT_IDENTITY, MZ_ACT_IDENTITY, fuse_adam, eta);
 }
 
 static int fc_unroll(mz_handle* h, const mz_batch* b, hipStream_t st, const RpSampleParams* rp);
@@ -1785,6 +1830,18 @@ int mz_learner_step(mz_handle* h, const mz_batch* b, double eta, float* losses_o
     if (rc) return rc;
     if (losses_out) MZ_TRY(h, hipMemcpyAsync(losses_out, h->d_loss, 6 * 4, hipMemcpyDeviceToHost, st));
     MZ_TRY(h, hipStreamSynchronize(st));
+    return 0;
+}
+
+// the next (start, stop) event pair of the measurement list (mz_debug_kernel_time)
+static int timing_events(mz_handle* h, hipEvent_t* e0, hipEvent_t* e1) {
+    if (h->tev_used + 2 > h->tev.size())
+        for (int i = 0; i < 2; ++i) {
+            hipEvent_t e;
+            MZ_TRY(h, hipEventCreate(&e));
+            h->tev.push_back(e);
+        }
+    *e0 = h->tev[h->tev_used++]; *e1 = h->tev[h->tev_used++];
     return 0;
 }
 
@@ -2233,9 +2290,9 @@ static int learner_sampled(mz_handle* h, int32_t B, uint32_t step, float* grad_d
         hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, Q);
         MZ_TRY(h, hipGetLastError());
         if (per_norm(h, B, st)) return -1;
-        if (rlearner_grad(h, &b, train ? nullptr : grad_dev, losses_dev, st)) return -1;
-        if (per_update(h, B, st)) return -1;                       // Learning.jl:400-404
-        return train ? mz_learner_apply_dev(h, nullptr, 1.0f, eta, st) : 0;
+        // one GPU: ADAM fused into the loss / Σθ² kernel (as the FC path)
+        if (rlearner_grad(h, &b, train ? nullptr : grad_dev, losses_dev, st, train, eta)) return -1;
+        return per_update(h, B, st);                               // Learning.jl:400-404
     }
     const int ti = small_unroll_ti(h, B);
     if (train && ti >= 0 && !h->conf.PER && h->A <= 16 && h->d_sm_w2 && !std::getenv("MZ_LEARN_2LAUNCH")) {

@@ -225,15 +225,28 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
     }
 }
 
+template <bool NARROW>
 __device__ __forceinline__ void rn_layer(const RLayer& L, const float* __restrict__ Wimg,
                                          const float* __restrict__ flat, float* lds, int NG, int Wb, int P,
                                          float bn_s, float bn_r) {
 #ifndef RN_NBW
 #define RN_NBW 3
 #endif
-    if (L.kk > 1) rn_layer_t<3, 2>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
-    else if (L.spatial) rn_layer_t<RN_NBW, 1>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
-    else rn_layer_t<1, 0>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+    // narrow tiles (the learner chain's, a few items on a small board) have
+    // fewer than 3 column blocks: a unit of exactly that many (no MFMAs on
+    // columns past the tile)
+    const int n_nb = NARROW && L.spatial ? (P * NG + 15) >> 4 : 3;
+    if (L.kk > 1) {
+        if (n_nb == 1) rn_layer_t<1, 2>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+        else if (n_nb == 2) rn_layer_t<2, 2>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+        else rn_layer_t<3, 2>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+    } else if (L.spatial) {
+        if (n_nb == 1) rn_layer_t<1, 1>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+        else if (n_nb == 2) rn_layer_t<2, 1>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+        else rn_layer_t<RN_NBW, 1>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+    } else {
+        rn_layer_t<1, 0>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+    }
 }
 
 // the k tables of the layers with a kernel > 1x1 (filled once per launch)
@@ -252,6 +265,9 @@ __device__ void rn_fill_ktabs(const RPlan& R, float* lds, int NG, int Wb, int P)
 }
 
 // A net: its layers one by one, a workgroup barrier after each.
+// NARROW: also the 1- / 2-column-block units (the learner chain's narrow
+// tiles); the wide-tile kernels keep the 3-block units only
+template <bool NARROW = false>
 __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const float* flat, float* lds, int NG,
                                        int Wb, int P, float bn_s, unsigned long long* st = nullptr) {
     const float bn_r = 1.0f / bn_s;
@@ -260,7 +276,7 @@ __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const 
     if (st && (threadIdx.x & 63) == 0) st[wv * 64 + 63] = __builtin_amdgcn_s_memtime();
 #endif
     for (int i = 0; i < R.n; ++i) {
-        rn_layer(R.L[i], Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+        rn_layer<NARROW>(R.L[i], Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
 #ifdef MZ_STAMPS
         if (st && (threadIdx.x & 63) == 0) st[wv * 64 + 2 * i] = __builtin_amdgcn_s_memtime();
 #endif
@@ -757,6 +773,82 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_kernel(RUnro
         if (ok) {
             rn_unstage(lds + Rd.out0_off, NG, H, t, [&](int f, float v) { hs[f] = v; });
             if (t.f0 == 0) U.pr[bs * K1 + s] = lds[Rd.out1_off + t.g];
+        }
+    }
+}
+
+// Learner unroll, split form (the same read-outs as mz_runroll_kernel, bit for
+// bit: every tile column is an independent fma chain, so the tile width does
+// not change a result).  The unroll's only sequential part is representation
+// (:347) then K dynamics steps (:355-362); the K predictions (:351, :356) only
+// read h_0 .. h_{K-1}.  mz_runroll_chain runs the chain on narrow tiles of
+// ng_l samples — B / ng_l workgroups instead of B / 16, a narrower MFMA
+// column range per layer, so a short per-layer critical path — and stores
+// h_s to hs[b][s]; mz_runroll_pred then runs the B·K predictions as one wide
+// launch on tiles of ng items.
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrollParams U) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const RPlan& Rr = U.plans_l[MZ_NET_REPR];
+    const RPlan& Rd = U.plans_l[MZ_NET_DYN];
+    const int NG = U.ng_l, t0 = blockIdx.x * NG, H = U.H, A = U.A, K = U.K, K1 = K + 1;
+    const RnLane t = rn_lane(NG);
+    const int b = t0 + t.g;
+    const bool ok = b < U.B;
+    const size_t bs = (size_t)(ok ? b : 0);
+    const int KH = K > 0 ? K : 1;
+    float* hs = U.hs + bs * KH * H;                 // [K][H]: h_s, s = 0 .. K-1
+    rn_fill_ktabs(Rr, lds, NG, U.W, U.P);
+    {
+        const float* x = U.obs + bs * U.obs_feat;
+        rn_stage(lds + Rr.in_off, NG, Rr.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
+    }
+    __syncthreads();
+    rn_run<true>(Rr, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                     // :347
+    if (ok) rn_unstage(lds + Rr.out0_off, NG, H, t, [&](int f, float v) { hs[f] = v; });
+    if (ok && t.f0 == 0) U.pr[bs * K1] = 0.0f;                                 // :352 zeros
+    for (int s = 1; s <= K; ++s) {
+        __syncthreads();
+        rn_fill_ktabs(Rd, lds, NG, U.W, U.P);
+        {                                                                      // make_dynamics_input (:293-304)
+            const float av = ok ? U.actions[bs * K1 + (s - 1)] / (float)A : 0.0f;
+            const float* hp = hs + (size_t)(s - 1) * H;
+            rn_stage(lds + Rd.in_off, NG, Rd.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? hp[f] * 2.0f : av; });
+        }
+        __syncthreads();
+        rn_run<true>(Rd, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                 // :362
+        if (ok) {
+            if (s < K) rn_unstage(lds + Rd.out0_off, NG, H, t, [&](int f, float v) { hs[(size_t)s * H + f] = v; });
+            if (t.f0 == 0) U.pr[bs * K1 + s] = lds[Rd.out1_off + t.g];
+        }
+    }
+}
+
+// prediction(h_s) for items i = b·KH + s (KH = max(K, 1)): step s + 1's value
+// and policy, and step 0's too for s = 0 (Q10: :351 and :356 at i = 1 both
+// predict from h_0)
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred(RUnrollParams U) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const RPlan& Rp = U.plans[MZ_NET_PRED];
+    const int NG = U.ng, H = U.H, A = U.A, K = U.K, K1 = K + 1, KH = K > 0 ? K : 1;
+    const int n_items = U.B * KH, t0 = blockIdx.x * NG;
+    const RnLane t = rn_lane(NG);
+    const int it = t0 + t.g;
+    const bool ok = it < n_items;
+    const size_t ic = (size_t)(ok ? it : 0);
+    rn_fill_ktabs(Rp, lds, NG, U.W, U.P);
+    {
+        const float* x = U.hs + ic * H;
+        rn_stage(lds + Rp.in_off, NG, H, t, [&](int f) { return ok ? x[f] : 0.0f; });
+    }
+    __syncthreads();
+    rn_run(Rp, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                     // :351 / :356
+    if (ok) {
+        const size_t b = ic / KH;
+        const int s = (int)(ic - b * KH);
+        for (int j = s == 0 ? 0 : s + 1; j <= (s + 1 <= K ? s + 1 : 0); ++j) {
+            if (t.f0 == 0) U.pv[b * K1 + j] = lds[Rp.out0_off + t.g];
+            float* o = U.pp + (b * K1 + j) * A;
+            rn_unstage(lds + Rp.out1_off, NG, A, t, [&](int f, float v) { o[f] = v; });
         }
     }
 }

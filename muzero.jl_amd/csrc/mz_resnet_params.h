@@ -110,9 +110,13 @@ struct RUnrollParams {
     float bn_s;
     const float* obs; const float* actions;
     float* pv; float* pp; float* pr;   // (K+1, B), (A, K+1, B), (K+1, B)
-    float* hs;                         // [B][H] scratch
+    float* hs;                         // [B][H] scratch (mz_runroll_kernel); [B][K][H] h_0..h_{K-1} (split form)
     const RPlan* plans;
     const float* Wimg; const float* flat;
+    // split form: mz_runroll_chain (representation + the K dynamics steps, the
+    // sequential part) on tiles of ng_l samples with plans_l, then
+    // mz_runroll_pred (the K predictions, independent) on tiles of ng items
+    const RPlan* plans_l; int ng_l;
 };
 
 // Downsampler of the ResNet representation (ResNetHP.downsample,

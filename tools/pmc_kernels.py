@@ -1,0 +1,53 @@
+"""Per-kernel medians of rocprofv3 --pmc counters (one pass per directory).
+
+usage: python tools/pmc_kernels.py <out.json> <command> <dir> [<dir> ...] -- <kernel> [<kernel> ...]
+
+Writes {kernel: {counter: median per dispatch, ..., "dispatches": n}} plus
+derived figures when the counters are present: HBM bytes per launch
+(FETCH_SIZE, WRITE_SIZE are KB; the raw sum and the sum with FETCH_SIZE x2 —
+gfx950 reports half of 16 B/lane streaming reads, MI355X_MICROARCH.md HBM
+section), VALU instructions per MFMA, the share of wave cycles parked
+(SQ_WAIT_ANY / SQ_WAVE_CYCLES) and MFMA busy per busy cycle."""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+
+def main():
+    argv = sys.argv[1:]
+    cut = argv.index("--")
+    out, command, dirs, kernels = argv[0], argv[1], argv[2:cut], argv[cut + 1:]
+    vals = {k: {} for k in kernels}
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    for k in kernels:
+                        if row["Kernel_Name"].startswith(k):
+                            vals[k].setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    res = {"command": command, "kernels": {}}
+    for k, cs in vals.items():
+        if not cs:
+            continue
+        r = {c: statistics.median(v) for c, v in sorted(cs.items())}
+        r["dispatches"] = max(len(v) for v in cs.values())
+        if "FETCH_SIZE" in r and "WRITE_SIZE" in r:
+            r["hbm_bytes_per_launch_raw"] = (r["FETCH_SIZE"] + r["WRITE_SIZE"]) * 1024.0
+            r["hbm_bytes_per_launch_fetch_x2"] = (2 * r["FETCH_SIZE"] + r["WRITE_SIZE"]) * 1024.0
+        if r.get("SQ_INSTS_MFMA"):
+            r["valu_per_mfma"] = r.get("SQ_INSTS_VALU", 0.0) / r["SQ_INSTS_MFMA"]
+        if r.get("SQ_WAVE_CYCLES"):
+            r["wait_any_frac"] = r.get("SQ_WAIT_ANY", 0.0) / r["SQ_WAVE_CYCLES"]
+        if r.get("SQ_BUSY_CYCLES") and "SQ_VALU_MFMA_BUSY_CYCLES" in r:
+            r["mfma_busy_per_busy_cycle"] = r["SQ_VALU_MFMA_BUSY_CYCLES"] / r["SQ_BUSY_CYCLES"]
+        res["kernels"][k] = r
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
