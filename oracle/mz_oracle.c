@@ -1010,16 +1010,17 @@ EXPORT double ora_cos_schedule(double l0, double l1, int period, int t) {
 
 /* One full ref_semantics learner step: forward unroll + losses + ADAM on
  * all three nets; bp is advanced (βp .= βp .* β).                          */
-EXPORT void ora_learner_step(const mz_config* c, const ora_nethp* hp, float* Prep, float* Ppred, float* Pdyn,
-                             float* m_all, float* v_all, double* bp, int B, const float* obs,
-                             const float* actions, const float* tv, const float* tp, const float* gscale,
-                             double eta, float* losses) {
+/* ... with PER importance weights wts (B) or NULL (Learning.jl:271-285) */
+EXPORT void ora_learner_step_w(const mz_config* c, const ora_nethp* hp, float* Prep, float* Ppred, float* Pdyn,
+                               float* m_all, float* v_all, double* bp, int B, const float* obs,
+                               const float* actions, const float* tv, const float* tp, const float* gscale,
+                               const float* wts, double eta, float* losses) {
     int A = c->action_space_size, K = c->num_unroll_steps;
     float* pv = (float*)malloc(sizeof(float) * (size_t)B * (K + 1));
     float* pr = (float*)malloc(sizeof(float) * (size_t)B * (K + 1));
     float* pp = (float*)malloc(sizeof(float) * (size_t)B * (K + 1) * A);
     ora_unroll(c, hp, Prep, Ppred, Pdyn, B, obs, actions, pv, pp, pr);
-    ora_losses(c, B, pv, pp, tv, tp, gscale, &losses[0], &losses[2]);
+    ora_losses_w(c, B, pv, pp, tv, tp, gscale, wts, &losses[0], &losses[2]);
     losses[1] = 0.0f;                                  /* intermediate_rewards = false */
     size_t n0 = ora_param_count(c, hp, MZ_NET_REPR), n1 = ora_param_count(c, hp, MZ_NET_PRED),
            n2 = ora_param_count(c, hp, MZ_NET_DYN);
@@ -1031,6 +1032,171 @@ EXPORT void ora_learner_step(const mz_config* c, const ora_nethp* hp, float* Pre
     ora_adam_2theta(Pdyn, m_all + n0 + n1, v_all + n0 + n1, n2, bp, eta);
     bp[0] = bp[0] * 0.9; bp[1] = bp[1] * 0.999;
     free(pv); free(pr); free(pp);
+}
+EXPORT void ora_learner_step(const mz_config* c, const ora_nethp* hp, float* Prep, float* Ppred, float* Pdyn,
+                             float* m_all, float* v_all, double* bp, int B, const float* obs,
+                             const float* actions, const float* tv, const float* tp, const float* gscale,
+                             double eta, float* losses) {
+    ora_learner_step_w(c, hp, Prep, Ppred, Pdyn, m_all, v_all, bp, B, obs, actions, tv, tp, gscale, NULL, eta,
+                       losses);
+}
+
+/* ==================================================================== PER
+ * Prioritized replay (conf.PER; ReplayBuffer.jl:73-107, 133-145, 168-183,
+ * 188-217; Learning.jl:261-288, 400-404).  The reference's PER path cannot
+ * run (update_priorities! calls minimum(a, b) and assigns a K+2-element slice
+ * from K+1 priorities); this restates its intended reading.  Julia's
+ * rand(rng, Categorical(p)) draws from MersenneTwister (not reproducible
+ * offline): the restatement draws u from the Philox GAME / POS streams and
+ * applies Distributions 0.25's rand(::DiscreteNonParametric) rule — the first
+ * index whose ascending running sum of p exceeds u (advance while cp <= u).  */
+
+/* |x|^alpha as Julia's Float32^Int: f64 repeated multiplication, rounded once */
+EXPORT float ora_per_priority(float x, int alpha) {
+    double ax = fabs((double)x), r = 1.0;
+    for (int i = 0; i < alpha; ++i) r = r * ax;
+    return (float)r;
+}
+/* uniform in [0, 1) from a Philox draw: 24 bits, exact */
+static double per_uniform(uint32_t r) { return (double)(r >> 8) * 5.9604644775390625e-08; }
+/* Categorical(w ./ sum(w)) (:76, :98): p_i = w_i / S with S the ascending f32
+ * sum; the first i whose ascending f32 running sum of p exceeds u (else the
+ * last); *prob = p_i */
+EXPORT int ora_per_categorical(const float* w, int n, double u, float* prob) {
+    float S = 0.0f;
+    for (int i = 0; i < n; ++i) S = S + w[i];
+    int i = 0;
+    float p = w[0] / S, c = p;
+    while ((double)c <= u && i < n - 1) { ++i; p = w[i] / S; c = c + p; }
+    *prob = p;
+    return i;
+}
+/* save_game's priorities (:136-143): |root_value_i − target_value_i|^alpha,
+ * game priority = their max */
+EXPORT void ora_per_init(const mz_config* c, const OHist* h, float* prio, float* gprio) {
+    float m = 0.0f;
+    for (int i = 0; i < h->T; ++i) {
+        prio[i] = ora_per_priority(h->root_values[i] - ora_compute_target_value(c, h, i + 1), c->PER_alpha);
+        m = i == 0 || prio[i] > m ? prio[i] : m;
+    }
+    *gprio = m;
+}
+/* get_batch with PER (:188-217): games by priority (sample_n_games :91-99),
+ * positions by priority (sample_position :75-78), importance weights
+ * 1/(total_samples · p_game · p_pos) in f32 (:213), normalised by their
+ * maximum (:215).  prio is [n][Tmax] (game i = hist[i], oldest first).     */
+EXPORT void ora_get_batch_per(const mz_config* c, const OHist* hist, const float* prio, const float* gprio, int n,
+                              int Tmax, int first_id, uint64_t seed, uint32_t step, float* obs, float* actions,
+                              float* values, float* rewards, float* policies, float* gscale, float* weights,
+                              int32_t* idx_out) {
+    int A = c->action_space_size, K = c->num_unroll_steps, B = c->batch_size;
+    int osz = c->observation_shape[0] * c->observation_shape[1] *
+              (c->observation_shape[2] * (c->stacked_observations + 1) + c->stacked_observations);
+    long long total = 0;
+    for (int i = 0; i < n; ++i) total += hist[i].T;
+    float wmax = -INFINITY;
+    for (int b = 0; b < B; ++b) {
+        float gp, pp;
+        int gi = ora_per_categorical(gprio, n, per_uniform(mz_rng_u32(seed, MZ_RNG_GAME, (uint32_t)b, step, 0)), &gp);
+        const OHist* h = &hist[gi];
+        int pos = ora_per_categorical(prio + (size_t)gi * Tmax, h->T,
+                                      per_uniform(mz_rng_u32(seed, MZ_RNG_POS, (uint32_t)b, step, 0)), &pp) + 1;
+        weights[b] = 1.0f / ((float)total * gp * pp);
+        wmax = weights[b] > wmax ? weights[b] : wmax;
+        make_target(c, h, pos, seed, (uint32_t)b, step, values + (size_t)b * (K + 1),
+                    rewards + (size_t)b * (K + 1), policies + (size_t)b * (K + 1) * A,
+                    actions + (size_t)b * (K + 1));
+        ora_stacked_obs(c, h->obs, h->actions, pos, obs + (size_t)b * osz);
+        int gs = h->T + 1 - pos;
+        gscale[b] = (float)(K < gs ? K : gs);
+        idx_out[2 * b] = first_id + gi; idx_out[2 * b + 1] = pos;
+    }
+    for (int b = 0; b < B; ++b) weights[b] = weights[b] / wmax;
+}
+/* update_priorities! (:168-183) after a learner step (Learning.jl:400-404):
+ * sample i in batch order, if its game is still held, sets positions
+ * pos..min(pos+K, len) to |v̂ − v|^alpha of steps 0.., then the game priority
+ * to the new maximum (later samples overwrite earlier ones).               */
+EXPORT void ora_update_priorities(const mz_config* c, float* prio, float* gprio, const int32_t* lens, int n,
+                                  int Tmax, int first_id, int B, const int32_t* idx, const float* pv, const float* tv) {
+    int K = c->num_unroll_steps;
+    for (int i = 0; i < B; ++i) {
+        int gi = idx[2 * i] - first_id, pos = idx[2 * i + 1];
+        if (gi < 0 || gi >= n) continue;
+        int len = lens[gi], end = pos + K < len ? pos + K : len;
+        float* pr = prio + (size_t)gi * Tmax;
+        for (int k = pos; k <= end; ++k)
+            pr[k - 1] = ora_per_priority(pv[(size_t)i * (K + 1) + (k - pos)] - tv[(size_t)i * (K + 1) + (k - pos)],
+                                         c->PER_alpha);
+        float m = pr[0];
+        for (int k = 1; k < len; ++k) m = pr[k] > m ? pr[k] : m;
+        gprio[gi] = m;
+    }
+}
+
+/* ======================================================= evaluation play
+ * competitive_play! (SelfPlay.jl:421-435) = play_game (:330-382) with an
+ * opponent at temperature 0, games not saved, for G lockstep slots (the
+ * engine's MZ_SP_EVAL mode): the player muzero_player searches (run_mcts +
+ * select_action); the other player is "random" — select_opponent_action
+ * (:311-325) read as intended (the reference reads `las`, defined only in the
+ * "human" branch): a uniform legal action, the rank drawn from the Philox
+ * OPPONENT stream keyed (game id, move) — or MuZero too (opponent "self").
+ * Each finished game is tallied {games, MuZero wins, opponent wins, draws}:
+ * with quirk Q14 a nonzero last reward means the player then to move holds a
+ * line (winner = 3 − mover).  TicTacToe only.                               */
+EXPORT int ora_eval_play(const mz_config* c, const ora_nethp* hp, const float* Prep, const float* Ppred,
+                         const float* Pdyn, uint64_t seed, int G, int moves, uint32_t move0, uint32_t game_offset,
+                         int random_opponent, int muzero_player, float temperature, int64_t* tally,
+                         int32_t* slot_len, uint8_t* slot_board, int32_t* slot_player) {
+    const int A = c->action_space_size, Tm = c->max_moves + 1, OS = 27;
+    if (A != 9) return -1;
+    OCtx X; ctx_init(&X, c, hp, Prep, Ppred, Pdyn, seed);
+    float* s_obs = calloc((size_t)G * Tm * OS, 4); int32_t* s_act = calloc((size_t)G * Tm, 4);
+    int* s_len = calloc(G, sizeof(int));
+    OTTT* env = malloc(sizeof(OTTT) * G);
+    for (int g = 0; g < G; ++g) ttt_reset(&env[g]);
+    float stacked[1024];
+    for (int k = 0; k < 4; ++k) tally[k] = 0;
+    for (int mv = 0; mv < moves; ++mv) {
+        const uint32_t step = move0 + (uint32_t)mv;
+        for (int g = 0; g < G; ++g) {
+            const int T = s_len[g];
+            float* oh = s_obs + (size_t)g * Tm * OS;
+            for (int i = 0; i < OS; ++i) oh[(size_t)T * OS + i] = (float)env[g].b[i];
+            uint8_t legal[MAXA]; ttt_legal(&env[g], legal);
+            const int p = env[g].player;
+            const uint32_t gid = game_offset + (uint32_t)g;
+            int a;
+            if (!random_opponent || p == muzero_player) {               /* :357-358 */
+                ora_stacked_obs(c, oh, s_act + (size_t)g * Tm, T + 1, stacked);
+                int root = run_mcts(&X, stacked, legal, p, 1, gid, step, NULL);
+                a = select_action(&X, root, temperature, gid, step) + 1;
+            } else {                                                    /* :360, :321 */
+                int acts[MAXA], n = 0;
+                for (int b = 0; b < A; ++b) if (legal[b]) acts[n++] = b;
+                a = acts[mz_rng_below(mz_rng_u32(seed, MZ_RNG_OPPONENT, gid, step, 0), (uint32_t)n)] + 1;
+            }
+            ttt_step(&env[g], a);
+            float r = ttt_reward(&env[g], p);
+            int done = ttt_terminated(&env[g]);
+            s_act[(size_t)g * Tm + T] = a;
+            s_len[g] = T + 1;
+            if (done || s_len[g] > c->max_moves) {
+                int w = r == 0.0f ? 0 : 3 - p;
+                tally[0] += 1;
+                tally[w == 0 ? 3 : w == muzero_player ? 1 : 2] += 1;
+                s_len[g] = 0; ttt_reset(&env[g]);
+            }
+        }
+    }
+    for (int g = 0; g < G; ++g) {
+        slot_len[g] = s_len[g]; slot_player[g] = env[g].player;
+        memcpy(slot_board + (size_t)g * OS, env[g].b, OS);
+    }
+    ctx_free(&X);
+    free(s_obs); free(s_act); free(s_len); free(env);
+    return 0;
 }
 
 /* ================================================== actor–learner loop

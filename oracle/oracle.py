@@ -59,6 +59,21 @@ def lib():
         L.ora_cos_schedule.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int]
         L.ora_learner_step.argtypes = [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_int, _VP, _VP, _VP,
                                        _VP, _VP, ctypes.c_double, _VP]
+        L.ora_per_priority.restype = ctypes.c_float
+        L.ora_per_priority.argtypes = [ctypes.c_float, ctypes.c_int]
+        L.ora_per_categorical.restype = ctypes.c_int
+        L.ora_per_categorical.argtypes = [_VP, ctypes.c_int, ctypes.c_double, _VP]
+        L.ora_per_init.argtypes = [_VP, ctypes.POINTER(OHist), _VP, _VP]
+        L.ora_get_batch_per.argtypes = [_VP, _VP, _VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                        ctypes.c_uint32] + [_VP] * 8
+        L.ora_update_priorities.argtypes = [_VP, _VP, _VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, _VP, _VP, _VP]
+        L.ora_learner_step_w.argtypes = [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_int, _VP, _VP, _VP,
+                                         _VP, _VP, _VP, ctypes.c_double, _VP]
+        L.ora_eval_play.restype = ctypes.c_int
+        L.ora_eval_play.argtypes = [_VP, _VP, _VP, _VP, _VP, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                    _VP, _VP, _VP, _VP]
         L.ora_losses_w.argtypes = [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]
         L.ora_train_loop.restype = ctypes.c_int
         L.ora_train_loop.argtypes = [_VP, _VP] + [_VP] * 9 + [_VP, _VP, _VP, ctypes.c_uint64, ctypes.c_int,
@@ -195,6 +210,34 @@ class Oracle:
                           _p(pv), _p(pp), _p(pr))
         return pv, pp, pr
 
+    def learner_step_w(self, state, batch, eta, weights=None):
+        """ora_learner_step_w: the ref_semantics step with PER importance weights."""
+        c, h = self._c()
+        a = {k: np.ascontiguousarray(batch[k], np.float32) for k in
+             ("observation", "actions", "target_values", "target_policies", "gradient_scale")}
+        w = None if weights is None else np.ascontiguousarray(weights, np.float32)
+        losses = np.empty(6, np.float32)
+        B = a["observation"].shape[0]
+        self.L.ora_learner_step_w(c, h, _p(self.params[0]), _p(self.params[1]), _p(self.params[2]), _p(state["m"]),
+                                  _p(state["v"]), _p(state["bp"]), B, _p(a["observation"]), _p(a["actions"]),
+                                  _p(a["target_values"]), _p(a["target_policies"]), _p(a["gradient_scale"]), _p(w),
+                                  eta, _p(losses))
+        return losses
+
+    def eval_play(self, G, moves, move0=0, game_offset=0, random_opponent=True, muzero_player=1, temperature=0.0):
+        """ora_eval_play: competitive_play! for G lockstep TicTacToe slots ->
+        (tally {games, MuZero wins, opponent wins, draws}, slot lens, boards, players)."""
+        c, h = self._c()
+        tally = np.zeros(4, np.int64)
+        ln = np.zeros(G, np.int32)
+        board = np.zeros((G, 27), np.uint8)
+        player = np.zeros(G, np.int32)
+        rc = self.L.ora_eval_play(c, h, _p(self.params[0]), _p(self.params[1]), _p(self.params[2]), self.seed, G,
+                                  moves, move0, game_offset, int(random_opponent), muzero_player, temperature,
+                                  _p(tally), _p(ln), _p(board), _p(player))
+        assert rc == 0, "ora_eval_play: TicTacToe only"
+        return tuple(int(x) for x in tally), ln, board, player
+
     def learner_state(self):
         n = sum(p.size for p in self.params)
         return dict(m=np.zeros(n, np.float32), v=np.zeros(n, np.float32), bp=np.array([0.9, 0.999]))
@@ -248,6 +291,55 @@ def train_loop(ora, G, cap, moves, move0=0, game_offset=0, state=None):
             for i in range(nh)]
     return dict(t=int(t[0]), counters=counters, held=held, slot_len=slen, slot_board=sboard, slot_player=splayer,
                 actor=actor, queued=queued, losses=losses, state=st)
+
+
+class PerReplay:
+    """The oracle's PER shard (ora_per_init / ora_get_batch_per /
+    ora_update_priorities) over a list of held games (oldest first), game
+    numbers first_id.. — the reference's intended PER reading."""
+
+    def __init__(self, ora, histories, first_id):
+        self.o = ora
+        self.hist = histories
+        self.first_id = first_id
+        self.arr, self.keep = histories_to_c(histories)
+        self.Tmax = ora.cconf.max_moves + 1
+        n = len(histories)
+        self.lens = np.array([len(h["action"]) for h in histories], np.int32)
+        self.prio = np.zeros((n, self.Tmax), np.float32)
+        self.gprio = np.zeros(n, np.float32)
+        c, _ = ora._c()
+        for i in range(n):
+            ora.L.ora_per_init(c, ctypes.byref(self.arr[i]), _p(self.prio[i]),
+                               self.gprio[i:i + 1].ctypes.data_as(ctypes.c_void_p))
+
+    def get_batch(self, step, B):
+        import dataclasses  # noqa: F401
+        o = self.o
+        cc = type(o.cconf)()
+        ctypes.pointer(cc)[0] = o.cconf
+        cc.batch_size = B
+        K, A = o.K, o.A
+        osz = self.hist[0]["observation"].shape[1]
+        feat = (osz // 3) * (3 * (cc.stacked_observations + 1) + cc.stacked_observations)
+        out = dict(observation=np.zeros((B, feat), np.float32), actions=np.zeros((B, K + 1), np.float32),
+                   target_values=np.zeros((B, K + 1), np.float32), target_rewards=np.zeros((B, K + 1), np.float32),
+                   target_policies=np.zeros((B, K + 1, A), np.float32), gradient_scale=np.zeros(B, np.float32),
+                   weights=np.zeros(B, np.float32))
+        idx = np.zeros((B, 2), np.int32)
+        o.L.ora_get_batch_per(ctypes.byref(cc), self.arr, _p(self.prio), _p(self.gprio), len(self.hist), self.Tmax,
+                              self.first_id, o.seed, step, _p(out["observation"]), _p(out["actions"]),
+                              _p(out["target_values"]), _p(out["target_rewards"]), _p(out["target_policies"]),
+                              _p(out["gradient_scale"]), _p(out["weights"]), _p(idx))
+        return idx, out
+
+    def update_priorities(self, idx, pv, tv):
+        c, _ = self.o._c()
+        B = idx.shape[0]
+        self.o.L.ora_update_priorities(c, _p(self.prio), _p(self.gprio), _p(self.lens), len(self.hist), self.Tmax,
+                                       self.first_id, B, _p(np.ascontiguousarray(idx, np.int32)),
+                                       _p(np.ascontiguousarray(pv, np.float32)),
+                                       _p(np.ascontiguousarray(tv, np.float32)))
 
 
 def histories_to_c(histories):

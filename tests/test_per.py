@@ -91,3 +91,25 @@ def test_per_categorical_tie_rule():
     assert per_categorical(w, 0.5)[0] == 3                          # cp = 0.5 <= 0.5: the tie advances
     assert per_categorical(w, 0.49)[0] == 2
     assert per_categorical(np.array([1.0, 0.0], np.float32), 0.9999)[0] == 0
+
+
+def test_oracle_per_categorical_matches_mirror():
+    """The oracle's restatement of Categorical sampling (ora_per_categorical)
+    and of the priority power agree with the host mirror on random weights,
+    ties and zero entries."""
+    import ctypes
+    from oracle import lib
+    L = lib()
+    rng = np.random.default_rng(3)
+    for n in (1, 2, 5, 17):
+        for _ in range(50):
+            w = rng.random(n).astype(np.float32) * (rng.random(n) < 0.8)
+            if w.sum() == 0:
+                w[0] = 1.0
+            u = float(rng.integers(0, 1 << 24)) * 5.9604644775390625e-08
+            pr = np.zeros(1, np.float32)
+            k = L.ora_per_categorical(w.ctypes.data_as(ctypes.c_void_p), n, u, pr.ctypes.data_as(ctypes.c_void_p))
+            assert (k, pr[0]) == per_categorical(w, u)
+    for x in (-1.5, 0.0, 0.3, 7.25):
+        for a in (1, 2, 3):
+            assert np.float32(L.ora_per_priority(x, a)) == per_priority(np.float32(x), a)
