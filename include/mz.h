@@ -223,6 +223,18 @@ typedef struct mz_batch {
  * Single-GPU form; data-parallel training uses the split form below.      */
 int mz_learner_step(mz_handle* h, const mz_batch* batch, double eta, float* losses_out);
 
+/* Learner mode.  MZ_LEARN_REF_SEMANTICS (default): the reference as written
+ * — its pullbacks see only sum(sqnorm, params), so ∇ = 2θ (quirk Q11), and
+ * the reported policy loss is Q11's broadcast.  MZ_LEARN_CORRECTED (FC nets):
+ * the loss Learning.jl:261-288 means, differentiated through the unroll
+ * (real backpropagation on MFMA, mz_backprop.hip), as a per-sample mean so a
+ * data-parallel all-reduce-mean equals the global batch:
+ *   L = (1/B) Σ_b (w_b/g_b) [Σ_k (v−z)² + Σ_k CE(logits, π) + ir·Σ_k (r−u)²] + Σθ²
+ * (CE = logitcrossentropy on the policy head's logits).  Every learner entry
+ * point follows the mode; losses_out = {value, reward, policy, Σθ² ×3}.    */
+enum { MZ_LEARN_REF_SEMANTICS = 0, MZ_LEARN_CORRECTED = 1 };
+int mz_learner_set_mode(mz_handle* h, int mode);
+
 /* Split learner step for data-parallel training: (1) forward + losses +
  * gradient into grad_dev (device, mz_grad_count floats), (2) the caller
  * all-reduces (sum) grad_dev across ranks, (3) apply ADAM with scale

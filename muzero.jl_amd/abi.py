@@ -19,6 +19,7 @@ NET_REPR, NET_PRED, NET_DYN = 0, 1, 2
 ENV_TICTACTOE, ENV_CONNECT4 = 0, 1
 SP_TRAIN, SP_EVAL = 0, 1
 TRAIN_LEARNER, TRAIN_ACTOR, TRAIN_QUEUED = 0, 1, 2
+LEARN_REF_SEMANTICS, LEARN_CORRECTED = 0, 1
 OPP_SELF, OPP_RANDOM = 0, 1
 
 _lib = None
@@ -77,6 +78,7 @@ SIGNATURES = {
     "mz_replay_get_priorities": (ctypes.c_int, [_VP, ctypes.c_int32, _VP, _VP]),
     "mz_replay_get_game": (ctypes.c_int, [_VP, ctypes.c_int32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "mz_selfplay_slots": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
+    "mz_learner_set_mode": (ctypes.c_int, [_VP, ctypes.c_int]),
     "mz_train_init": (ctypes.c_int, [_VP, ctypes.c_int32]),
     "mz_train_run": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, _VP, _VP, _VP]),
     "mz_train_weights_get": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP, ctypes.c_size_t]),
@@ -301,6 +303,10 @@ class Engine:
     def selfplay_move(self, rng_step, game_offset=0, temperature=1.0, stream=None):
         self._check(self.lib.mz_selfplay_move(self.h, rng_step, game_offset, temperature, stream),
                     "mz_selfplay_move")
+
+    def learner_set_mode(self, mode):
+        """LEARN_REF_SEMANTICS (∇ = 2θ, quirk Q11) or LEARN_CORRECTED (backprop)."""
+        self._check(self.lib.mz_learner_set_mode(self.h, mode), "mz_learner_set_mode")
 
     def train_init(self, batch_size):
         """Actor–learner loop (self_play! ‖ learning!, Q16): actors and the

@@ -10,9 +10,10 @@ from concurrent.futures import ThreadPoolExecutor
 from . import PKG_DIR, LIB_PATH
 
 SOURCES = ["mz_engine.hip", "mz_search.hip", "mz_small.hip", "mz_nets.hip", "mz_resnet.hip", "mz_selfplay.hip",
-           "mz_downsample.hip", "mz_checkpoint.cpp"]
+           "mz_downsample.hip", "mz_checkpoint.cpp", "mz_backprop.hip"]
 HEADERS = ["mz_internal.h", "mz_mlp_device.h", "mz_tree_device.h", "mz_small_params.h", "mz_resnet_params.h",
-           "mz_selfplay_params.h", "mz_ckpt_iface.h", "mz_replay_device.h", "mz_learner_device.h"]
+           "mz_selfplay_params.h", "mz_ckpt_iface.h", "mz_replay_device.h", "mz_learner_device.h",
+           "mz_backprop_params.h"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
          # the numerics contract (include/mz_detmath.h): no FP contraction, IEEE
          # division/sqrt, f32 denormals kept (hipcc defaults for the last two)

@@ -1,0 +1,244 @@
+// mz_backprop.hip — the corrected-gradient learner (mz_learner_set_mode
+// MZ_LEARN_CORRECTED, FC nets): backpropagation through the K-step unroll of
+// Learning.jl:347-370 on f32 MFMA.  See mz_backprop_params.h for the loss.
+//
+//   mz_bp_tile  one workgroup (4 waves) per tile of 16 samples: the forward
+//               list of layer applications (each a 16-sample MFMA GEMM,
+//               y = act(W x + b), wave w owning output row blocks w, w+4, ..),
+//               the heads' loss gradients, then the list in reverse: dZ =
+//               dY ⊙ act'(y) in place, dX += Wᵀ dZ (MFMA, K = out).
+//   mz_bp_dw    one wave per 16x16 block of a layer's dW: Σ over tiles, the
+//               layer's applications and the 16 samples of dZ ⊗ x (MFMA with
+//               K = samples), + 2θ (∂Σθ²/∂θ); one wave per bias block.
+//   mz_bp_fold  Σθ² per net and the reported losses (deterministic f64 trees).
+// The ADAM step that follows is mz_adam_kernel (gradient scale 1/world).
+#include "mz_internal.h"
+#include "mz_backprop_params.h"
+
+typedef float bp_f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bp_act(int act, float v) {
+    return act == MZ_ACT_RELU ? mz_relu(v) : act == MZ_ACT_TANH ? det_tanhf(v) : v;
+}
+
+// y = act(W x + b) for the tile (all 256 threads; rows in blocks of 16 per wave)
+__device__ __forceinline__ void bp_dense_fwd(const BpApp& P, const float* __restrict__ flat, float* T) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
+    const float* W = flat + P.w_off;
+    const float* X = T + P.x;
+    float* Y = T + P.y;
+    const int nob = (P.out + 15) >> 4, nk = (P.in + 3) >> 2;
+    for (int ob = wave; ob < nob; ob += 4) {
+        const int o = ob * 16 + m;
+        const bool oin = o < P.out;
+        bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+        for (int kk = 0; kk < nk; ++kk) {
+            const int i = kk * 4 + kq;
+            const bool iin = i < P.in;
+            const float a = oin && iin ? W[o + (size_t)P.out * i] : 0.0f;
+            const float b = iin ? X[i * 16 + m] : 0.0f;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int oo = ob * 16 + kq * 4 + r;
+            if (oo < P.out) Y[oo * 16 + m] = bp_act(P.act, acc[r] + flat[P.b_off + oo]);
+        }
+    }
+}
+
+// G[x] += Wᵀ G[y] (G[y] holds dZ)
+__device__ __forceinline__ void bp_dense_dx(const BpApp& P, const float* __restrict__ flat, float* G) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
+    const float* W = flat + P.w_off;
+    const float* DZ = G + P.y;
+    float* DX = G + P.x;
+    const int nib = (P.in + 15) >> 4, nk = (P.out + 3) >> 2;
+    for (int ib = wave; ib < nib; ib += 4) {
+        const int i = ib * 16 + m;
+        const bool iin = i < P.in;
+        bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+        for (int kk = 0; kk < nk; ++kk) {
+            const int o = kk * 4 + kq;
+            const bool oin = o < P.out;
+            const float a = oin && iin ? W[o + (size_t)P.out * i] : 0.0f;
+            const float b = oin ? DZ[o * 16 + m] : 0.0f;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int ii = ib * 16 + kq * 4 + r;
+            if (ii < P.in) DX[ii * 16 + m] += acc[r];
+        }
+    }
+}
+
+extern "C" __global__ __launch_bounds__(256) void mz_bp_tile(BpParams Q) {
+    const int tid = threadIdx.x, t0 = blockIdx.x * 16, K1 = Q.K + 1;
+    float* T = Q.act + (size_t)blockIdx.x * Q.tile_floats;
+    float* G = Q.grad + (size_t)blockIdx.x * Q.tile_floats;
+    for (int e = tid; e < Q.tile_floats; e += 256) G[e] = 0.0f;
+    for (int e = tid; e < 16 * K1 * 3; e += 256) {
+        const int b = t0 + e / (K1 * 3);
+        if (b < Q.B) Q.terms[(size_t)t0 * K1 * 3 + e] = 0.0f;
+    }
+    for (int e = tid; e < 16 * K1; e += 256) {                // rewards: 0 at step 0 (and without heads)
+        const int b = t0 + e / K1;
+        if (b < Q.B) Q.pr[(size_t)t0 * K1 + e] = 0.0f;
+    }
+    for (int e = tid; e < Q.obs_feat * 16; e += 256) {       // observation_batch (:347)
+        const int f = e >> 4, s = e & 15, b = t0 + s;
+        T[Q.obs_t + e] = b < Q.B ? Q.obs[(size_t)b * Q.obs_feat + f] : 0.0f;
+    }
+    __syncthreads();
+    // ---- forward: representation, K dynamics steps, K+1 predictions (Q10)
+    for (int a = 0; a < Q.n_app; ++a) {
+        const BpApp P = Q.apps[a];
+        if (P.op == BP_DENSE) {
+            bp_dense_fwd(P, Q.flat, T);
+        } else {                                              // make_dynamics_input (:293-304)
+            for (int e = tid; e < P.out * 16; e += 256) {
+                const int i = e >> 4, s = e & 15, b = t0 + s;
+                float v;
+                if (i < P.in) v = T[P.x + e] * 2.0f;
+                else v = b < Q.B ? Q.actions[(size_t)b * K1 + P.step] / (float)Q.A : 0.0f;
+                T[P.y + e] = v;
+            }
+        }
+        __syncthreads();
+    }
+    // ---- heads: dL/dy of the value / policy / reward outputs, loss terms
+    for (int e = tid; e < Q.n_head * 16; e += 256) {
+        const BpHead hd = Q.heads[e >> 4];
+        const int s = e & 15, b = t0 + s, k = hd.step;
+        if (b >= Q.B) continue;
+        const float w = Q.weights ? Q.weights[b] : 1.0f;
+        const float c = w / (Q.gscale[b] * (float)Q.B);
+        const size_t bk = (size_t)b * K1 + k;
+        if (hd.kind == BP_HEAD_V || hd.kind == BP_HEAD_R) {
+            const bool v = hd.kind == BP_HEAD_V;
+            const float y = T[hd.y + s];
+            const float d = y - (v ? Q.tv[bk] : Q.tr[bk]);
+            const bool on = v || Q.intermediate_rewards;
+            (v ? Q.pv : Q.pr)[bk] = y;
+            G[hd.y + s] = on ? c * 2.0f * d : 0.0f;
+            Q.terms[bk * 3 + (v ? 0 : 2)] = on ? d * d : 0.0f;
+        } else {                                              // logitcrossentropy on the logits
+            const float* l = T + hd.y + s;
+            const float* pi = Q.tp + bk * Q.A;
+            float mx = l[0];
+            for (int a = 1; a < Q.A; ++a) mx = fmaxf(mx, l[a * 16]);
+            float S = 0.0f, sp = 0.0f;
+            for (int a = 0; a < Q.A; ++a) { S += det_expf(l[a * 16] - mx); sp += pi[a]; }
+            const float lS = det_logf(S);
+            float ce = 0.0f;
+            for (int a = 0; a < Q.A; ++a) {
+                const float z = l[a * 16] - mx;
+                ce -= pi[a] * (z - lS);
+                const float pa = det_expf(z) / S;
+                G[hd.y + s + a * 16] = c * (pa * sp - pi[a]);
+                Q.pp[bk * Q.A + a] = pa;
+            }
+            Q.terms[bk * 3 + 1] = ce;
+        }
+    }
+    __syncthreads();
+    // ---- backward, reverse order
+    for (int a = Q.n_app - 1; a >= 0; --a) {
+        const BpApp P = Q.apps[a];
+        if (P.op == BP_DENSE) {
+            for (int e = tid; e < P.out * 16; e += 256) {     // dZ = dY ⊙ act'(y), in place
+                const float g = G[P.y + e], y = T[P.y + e];
+                G[P.y + e] = P.act == MZ_ACT_RELU ? (y > 0.0f ? g : 0.0f)
+                           : P.act == MZ_ACT_TANH ? g * (1.0f - y * y) : g;
+            }
+            __syncthreads();
+            bp_dense_dx(P, Q.flat, G);
+        } else {                                              // ∂(2h)/∂h
+            for (int e = tid; e < P.in * 16; e += 256) G[P.x + e] += 2.0f * G[P.y + e];
+        }
+        __syncthreads();
+    }
+}
+
+extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
+    const BpJob J = Q.jobs[blockIdx.x];
+    const BpLayer L = Q.layers[J.layer];
+    const int lane = threadIdx.x, m = lane & 15, kq = lane >> 4;
+    if (J.ib < 0) {                                           // db = Σ dZ, + 2b
+        const int o = J.ob * 16 + lane;
+        if (lane >= 16 || o >= L.out) return;
+        float s = 0.0f;
+        for (int t = 0; t < Q.tiles; ++t)
+            for (int u = 0; u < L.n_use; ++u) {
+                const float* dz = Q.grad + (size_t)t * Q.tile_floats + Q.uses[L.use0 + u].y + o * 16;
+                for (int j = 0; j < 16; ++j) s += dz[j];
+            }
+        Q.out[L.b_off + o] = s + 2.0f * Q.flat[L.b_off + o];
+        return;
+    }
+    const int o = J.ob * 16 + m, i = J.ib * 16 + m;
+    const bool oin = o < L.out, iin = i < L.in;
+    bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < Q.tiles; ++t) {
+        const float* gt = Q.grad + (size_t)t * Q.tile_floats;
+        const float* at = Q.act + (size_t)t * Q.tile_floats;
+        for (int u = 0; u < L.n_use; ++u) {
+            const BpUse U = Q.uses[L.use0 + u];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {                     // K = the 16 samples, 4 per MFMA
+                const float a = oin ? gt[U.y + o * 16 + 4 * c + kq] : 0.0f;
+                const float b = iin ? at[U.x + i * 16 + 4 * c + kq] : 0.0f;
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int oo = J.ob * 16 + kq * 4 + r;
+        if (oo < L.out && iin) {
+            const size_t p = (size_t)L.w_off + oo + (size_t)L.out * i;
+            Q.out[p] = acc[r] + 2.0f * Q.flat[p];
+        }
+    }
+}
+
+// blocks 0..2: Σθ² of each net; block 3: the losses (per sample in ascending
+// k, then a 256-thread f64 tree over samples)
+extern "C" __global__ __launch_bounds__(256) void mz_bp_fold(BpFoldParams Q) {
+    __shared__ double red[3][256];
+    const int tid = threadIdx.x;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    if (blockIdx.x < 3) {
+        const size_t off = Q.netoff[blockIdx.x], n = Q.netoff[3 + blockIdx.x];
+        for (size_t i = tid; i < n; i += 256) s0 += (double)Q.flat[off + i] * (double)Q.flat[off + i];
+    } else {
+        const int K1 = Q.K + 1;
+        for (int b = tid; b < Q.B; b += 256) {
+            float v = 0.0f, p = 0.0f, r = 0.0f;
+            for (int k = 0; k < K1; ++k) {
+                const float* t = Q.terms + ((size_t)b * K1 + k) * 3;
+                v += t[0]; p += t[1]; r += t[2];
+            }
+            const double c = (double)(Q.weights ? Q.weights[b] : 1.0f) / (double)Q.gscale[b];
+            s0 += c * v; s1 += c * r; s2 += c * p;
+        }
+    }
+    red[0][tid] = s0; red[1][tid] = s1; red[2][tid] = s2;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) { red[0][tid] += red[0][tid + o]; red[1][tid] += red[1][tid + o]; red[2][tid] += red[2][tid + o]; }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        if (blockIdx.x < 3) {
+            Q.losses[3 + blockIdx.x] = (float)red[0][0];
+        } else {
+            Q.losses[0] = (float)(red[0][0] / Q.B);
+            Q.losses[1] = (float)(red[1][0] / Q.B);
+            Q.losses[2] = (float)(red[2][0] / Q.B);
+        }
+    }
+}

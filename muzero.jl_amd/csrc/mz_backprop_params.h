@@ -1,0 +1,74 @@
+// mz_backprop_params.h — the corrected-gradient learner (MZ_LEARN_CORRECTED):
+// real backpropagation through the K-step unroll of the FC nets.
+//
+// The reference differentiates only sum(sqnorm, params) (quirk Q11: the
+// predictions are computed outside the Zygote.pullback closures,
+// Learning.jl:347-393), so every gradient is 2θ.  The corrected mode
+// differentiates the loss it meant to (Learning.jl:261-288) through the same
+// forward (Q10 alignment, make_dynamics_input's 2h, :293-304), as a
+// per-sample mean so a data-parallel all-reduce-mean equals the global batch:
+//   L = (1/B) Σ_b (w_b / g_b) [ Σ_{k=0..K} (v_bk − z_bk)²
+//                              + Σ_{k=0..K} CE(ℓ_bk, π_bk)
+//                              + intermediate_rewards · Σ_{k=1..K} (r_bk − u_bk)² ]
+//       + Σθ²
+// with v = tanh(value head), ℓ the policy head's logits (logitcrossentropy
+// on logits, not on the softmax of a softmax, Q3), r the reward head after
+// reward_activation, w the PER weights (1 without PER), g gradient_scale.
+//
+// The unrolled graph is a host-built list of layer applications on tiles of
+// 16 samples (one MFMA N-tile): dense layers y = act(W x + b) and the
+// concatenation sa = [2h ; a/|A| plane].  Activations and gradients live in
+// per-tile arenas in HBM ([rows][16] f32 per tensor).
+#pragma once
+#include <stdint.h>
+
+enum { BP_DENSE = 0, BP_CONCAT = 1 };
+enum { BP_HEAD_V = 0, BP_HEAD_P = 1, BP_HEAD_R = 2 };
+
+struct BpApp {
+    int op;               // BP_DENSE / BP_CONCAT
+    int w_off, b_off;     // dense: flat offsets of W (out,in) column-major and b
+    int in, out, act;     // dense: dims, activation; concat: in = H (hidden), out = H + plane
+    int x, y;             // arena offsets (floats) of the input / output tensor
+    int step;             // concat: action column k (actions[b][k]); dense: layer id
+};
+
+struct BpHead {
+    int kind;             // BP_HEAD_V / P / R
+    int y;                // arena offset of the head's output tensor
+    int step;             // unroll step k (targets column)
+};
+
+struct BpUse { int x, y; };   // one application of a dense layer: input / output arena offsets
+
+struct BpLayer {
+    int w_off, b_off, in, out;
+    int use0, n_use;      // uses[use0 .. use0 + n_use)
+};
+
+struct BpJob { int layer, ob, ib; };   // one 16x16 block of dW (ib = -1: the bias block of row block ob)
+
+struct BpParams {
+    int B, K, A, H, plane, obs_feat, tile_floats, n_app, n_head, obs_t, intermediate_rewards;
+    const BpApp* apps; const BpHead* heads;
+    float* act; float* grad;              // arenas [tiles][tile_floats]
+    const float* flat;
+    const float* obs; const float* actions; const float* tv; const float* tr; const float* tp;
+    const float* gscale; const float* weights;
+    float* terms;                         // [B][K+1][3]: (v−z)², CE, (r−u)²
+    float* pv; float* pp; float* pr;      // the read-outs (K+1,B) / (A,K+1,B) / (K+1,B), as the unroll's
+};
+
+struct BpDwParams {
+    int tiles, tile_floats, n_job;
+    const BpJob* jobs; const BpLayer* layers; const BpUse* uses;
+    const float* act; const float* grad; const float* flat;
+    float* out;                           // Flux-order gradient (data term + 2θ)
+};
+
+struct BpFoldParams {
+    int B, K;
+    const float* terms; const float* gscale; const float* weights;
+    const float* flat; const size_t* netoff;
+    float* losses;                        // {value, reward, policy, Σθ² repr, pred, dyn}
+};

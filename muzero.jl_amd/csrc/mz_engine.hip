@@ -26,6 +26,7 @@ extern "C" __global__ void mz_search_kernel_hbm(SearchParams P);
 extern "C" __global__ void mz_search_kernel_lds_res(SearchParams P);
 #include "mz_small_params.h"
 #include "mz_resnet_params.h"
+#include "mz_backprop_params.h"
 #include "mz_selfplay_params.h"
 #include "mz_ckpt_iface.h"
 extern "C" __global__ void mz_rnet_forward_kernel(RNetParams Q);
@@ -39,6 +40,9 @@ extern "C" __global__ void mz_rsearch_tree_lds32(RSearchParams P);
 extern "C" __global__ void mz_rsearch_nets(RSearchParams P);
 extern "C" __global__ void mz_runroll_kernel(RUnrollParams U);
 extern "C" __global__ void mz_runroll_chain(RUnrollParams U);
+extern "C" __global__ void mz_bp_tile(BpParams Q);
+extern "C" __global__ void mz_bp_dw(BpDwParams Q);
+extern "C" __global__ void mz_bp_fold(BpFoldParams Q);
 extern "C" __global__ void mz_runroll_pred(RUnrollParams U);
 extern "C" __global__ void mz_sp_prepare(SpParams S);
 extern "C" __global__ void mz_sp_commit(SpParams S);
@@ -236,6 +240,13 @@ struct mz_handle {
     int tr_B = 0;
     int64_t tr_t = 0, tr_games = 0, tr_refresh = 0;
     long long* h_tr_cnt = nullptr;          // pinned: num_played_games read back once per move
+    // corrected-gradient learner (mz_backprop.hip): the unrolled graph and its arenas
+    int learn_mode = MZ_LEARN_REF_SEMANTICS;
+    bool bp_built = false;
+    int bp_n_app = 0, bp_n_head = 0, bp_n_job = 0, bp_tile_floats = 0, bp_obs_t = 0, bp_tiles_cap = 0;
+    BpApp* d_bp_apps = nullptr; BpHead* d_bp_heads = nullptr; BpLayer* d_bp_layers = nullptr;
+    BpUse* d_bp_uses = nullptr; BpJob* d_bp_jobs = nullptr;
+    float* d_bp_act = nullptr; float* d_bp_grad = nullptr; float* d_bp_terms = nullptr;
     std::vector<void*> sp_allocs;
     std::vector<void*> allocs;
 };
@@ -1681,6 +1692,7 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
 }
 
 static int fc_unroll(mz_handle* h, const mz_batch* b, hipStream_t st, const RpSampleParams* rp);
+static int bp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, hipStream_t st);
 static int small_unroll_ti(const mz_handle* h, int B);
 static int small_unroll_params(mz_handle* h, const mz_batch* b, int ti, const RpSampleParams* rp,
                                SmallUnrollParams* Uo);
@@ -1690,6 +1702,8 @@ int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float*
     if (!h || !b) return -2;
     if (h->kind == 1) return rlearner_grad(h, b, grad_dev, losses_dev, stream);
     if (b->batch_size < 1) return fail(h, "batch_size must be >= 1");
+    if (h->learn_mode == MZ_LEARN_CORRECTED)
+        return bp_grad(h, b, grad_dev, losses_dev, stream ? (hipStream_t)stream : h->stream);
     if (ensure_batch(h, b->batch_size)) return -1;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     if (fc_unroll(h, b, st, nullptr)) return -1;
@@ -1790,6 +1804,117 @@ static int learner_losses(mz_handle* h, const mz_batch* b, float* grad_dev, floa
                        b->gradient_scale, h->d_lterm, h->d_flat, h->d_netoff, g, h->d_sq, h->d_counter, lo, b->weights, ad);
     MZ_TRY(h, hipGetLastError());
     if (fuse_adam) adam_advance(h);
+    return 0;
+}
+
+// ---- corrected-gradient learner (MZ_LEARN_CORRECTED, FC nets; mz_backprop.hip)
+// The unrolled graph of Learning.jl:347-370: representation(obs); K dynamics
+// steps on sa_k = [2h_{k-1} ; a_{k-1}/|A|] (the state head skipped at k = K,
+// whose h_K no prediction reads; the reward heads only with
+// intermediate_rewards); K+1 predictions on h_0, h_0, h_1 .. h_{K-1} (Q10).
+static int build_bp(mz_handle* h) {
+    const int K = h->conf.num_unroll_steps, H = h->H;
+    std::vector<BpApp> apps;
+    std::vector<BpHead> heads;
+    int off = 0;
+    auto tensor = [&](int rows) { int o = off; off += ((rows + 3) & ~3) * 16; return o; };
+    const int obs_t = tensor(h->obs_feat);
+    auto dense = [&](int li, int x) {
+        const LayerSpec& L = h->layers[li];
+        BpApp a{};
+        a.op = BP_DENSE; a.w_off = (int)L.flux_w; a.b_off = (int)L.flux_b; a.in = L.in; a.out = L.out;
+        a.act = L.act; a.x = x; a.y = tensor(L.out); a.step = li;
+        apps.push_back(a);
+        return a.y;
+    };
+    auto chain = [&](int net, int ch, int x) {
+        for (int li : h->chains[net][ch]) x = dense(li, x);
+        return x;
+    };
+    std::vector<int> hs(K + 1, -1);
+    hs[0] = chain(MZ_NET_REPR, CH_TRUNK, obs_t);                                // :347
+    for (int k = 1; k <= K; ++k) {                                              // :355-362
+        BpApp c{};
+        c.op = BP_CONCAT; c.in = H; c.out = H + h->plane; c.x = hs[k - 1]; c.y = tensor(c.out); c.step = k - 1;
+        apps.push_back(c);
+        const int t = chain(MZ_NET_DYN, CH_TRUNK, c.y);
+        if (k < K) hs[k] = chain(MZ_NET_DYN, CH_HEAD1, t);
+        if (h->conf.intermediate_rewards) heads.push_back(BpHead{BP_HEAD_R, chain(MZ_NET_DYN, CH_HEAD2, t), k});
+    }
+    for (int k = 0; k <= K; ++k) {                                              // :351, :356 (Q10)
+        const int t = chain(MZ_NET_PRED, CH_TRUNK, hs[k <= 1 ? 0 : k - 1]);
+        heads.push_back(BpHead{BP_HEAD_V, chain(MZ_NET_PRED, CH_HEAD1, t), k});
+        heads.push_back(BpHead{BP_HEAD_P, chain(MZ_NET_PRED, CH_HEAD2, t), k});
+    }
+    // dW: every layer's applications, one wave per 16x16 block (+ one per bias block)
+    std::vector<BpLayer> layers(h->layers.size());
+    std::vector<BpUse> uses;
+    std::vector<BpJob> jobs;
+    for (size_t li = 0; li < h->layers.size(); ++li) {
+        const LayerSpec& L = h->layers[li];
+        BpLayer& bl = layers[li];
+        bl.w_off = (int)L.flux_w; bl.b_off = (int)L.flux_b; bl.in = L.in; bl.out = L.out;
+        bl.use0 = (int)uses.size();
+        for (const BpApp& a : apps) if (a.op == BP_DENSE && a.step == (int)li) uses.push_back(BpUse{a.x, a.y});
+        bl.n_use = (int)uses.size() - bl.use0;
+        for (int ob = 0; ob < (L.out + 15) / 16; ++ob) {
+            for (int ib = 0; ib < (L.in + 15) / 16; ++ib) jobs.push_back(BpJob{(int)li, ob, ib});
+            jobs.push_back(BpJob{(int)li, ob, -1});
+        }
+    }
+    auto up = [&](auto** d, const auto& v) -> int {
+        MZ_TRY(h, dalloc(h, d, v.size()));
+        MZ_TRY(h, hipMemcpy(*d, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice));
+        return 0;
+    };
+    if (up(&h->d_bp_apps, apps) || up(&h->d_bp_heads, heads) || up(&h->d_bp_layers, layers) ||
+        up(&h->d_bp_uses, uses) || up(&h->d_bp_jobs, jobs))
+        return -1;
+    h->bp_n_app = (int)apps.size(); h->bp_n_head = (int)heads.size(); h->bp_n_job = (int)jobs.size();
+    h->bp_tile_floats = off; h->bp_obs_t = obs_t;
+    h->bp_built = true;
+    return 0;
+}
+
+// corrected step: gradient (data term + 2θ) into grad_dev, losses, read-outs
+static int bp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, hipStream_t st) {
+    const int B = b->batch_size, K = h->conf.num_unroll_steps;
+    if (!h->bp_built && build_bp(h)) return -1;
+    if (ensure_batch(h, B)) return -1;
+    const int tiles = (B + 15) / 16;
+    if (tiles > h->bp_tiles_cap) {
+        MZ_TRY(h, dalloc(h, &h->d_bp_act, (size_t)tiles * h->bp_tile_floats));
+        MZ_TRY(h, dalloc(h, &h->d_bp_grad, (size_t)tiles * h->bp_tile_floats));
+        MZ_TRY(h, dalloc(h, &h->d_bp_terms, (size_t)tiles * 16 * (K + 1) * 3));
+        h->bp_tiles_cap = tiles;
+    }
+    BpParams Q;
+    Q.B = B; Q.K = K; Q.A = h->A; Q.H = h->H; Q.plane = h->plane; Q.obs_feat = h->obs_feat;
+    Q.tile_floats = h->bp_tile_floats; Q.n_app = h->bp_n_app; Q.n_head = h->bp_n_head; Q.obs_t = h->bp_obs_t;
+    Q.intermediate_rewards = h->conf.intermediate_rewards;
+    Q.apps = h->d_bp_apps; Q.heads = h->d_bp_heads; Q.act = h->d_bp_act; Q.grad = h->d_bp_grad; Q.flat = h->d_flat;
+    Q.obs = b->observation; Q.actions = b->actions; Q.tv = b->target_values; Q.tr = b->target_rewards;
+    Q.tp = b->target_policies; Q.gscale = b->gradient_scale; Q.weights = b->weights; Q.terms = h->d_bp_terms;
+    Q.pv = h->d_pv; Q.pp = h->d_pp; Q.pr = h->d_pr;
+    hipLaunchKernelGGL(mz_bp_tile, dim3(tiles), dim3(256), 0, st, Q);
+    BpDwParams D;
+    D.tiles = tiles; D.tile_floats = h->bp_tile_floats; D.n_job = h->bp_n_job; D.jobs = h->d_bp_jobs;
+    D.layers = h->d_bp_layers; D.uses = h->d_bp_uses; D.act = h->d_bp_act; D.grad = h->d_bp_grad; D.flat = h->d_flat;
+    D.out = grad_dev ? grad_dev : h->d_grad;
+    hipLaunchKernelGGL(mz_bp_dw, dim3(h->bp_n_job), dim3(64), 0, st, D);
+    BpFoldParams F;
+    F.B = B; F.K = K; F.terms = h->d_bp_terms; F.gscale = b->gradient_scale; F.weights = b->weights;
+    F.flat = h->d_flat; F.netoff = h->d_netoff; F.losses = losses_dev ? losses_dev : h->d_loss;
+    hipLaunchKernelGGL(mz_bp_fold, dim3(4), dim3(256), 0, st, F);
+    MZ_TRY(h, hipGetLastError());
+    return 0;
+}
+
+int mz_learner_set_mode(mz_handle* h, int mode) {
+    if (!h) return -2;
+    if (mode != MZ_LEARN_REF_SEMANTICS && mode != MZ_LEARN_CORRECTED) return fail(h, "unknown learner mode");
+    if (mode == MZ_LEARN_CORRECTED && h->kind != 0) return fail(h, "the corrected learner supports the FC nets");
+    h->learn_mode = mode;
     return 0;
 }
 
@@ -2293,6 +2418,14 @@ static int learner_sampled(mz_handle* h, int32_t B, uint32_t step, float* grad_d
         // one GPU: ADAM fused into the loss / Σθ² kernel (as the FC path)
         if (rlearner_grad(h, &b, train ? nullptr : grad_dev, losses_dev, st, train, eta)) return -1;
         return per_update(h, B, st);                               // Learning.jl:400-404
+    }
+    if (h->learn_mode == MZ_LEARN_CORRECTED) {     // sample, backprop, (ADAM)
+        hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, Q);
+        MZ_TRY(h, hipGetLastError());
+        if (per_norm(h, B, st)) return -1;
+        if (bp_grad(h, &b, train ? nullptr : grad_dev, losses_dev, st)) return -1;
+        if (per_update(h, B, st)) return -1;                       // Learning.jl:400-404
+        return train ? mz_learner_apply_dev(h, nullptr, 1.0f, eta, st) : 0;
     }
     const int ti = small_unroll_ti(h, B);
     if (train && ti >= 0 && !h->conf.PER && h->A <= 16 && h->d_sm_w2 && !std::getenv("MZ_LEARN_2LAUNCH")) {

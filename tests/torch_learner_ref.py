@@ -1,0 +1,77 @@
+"""Independent torch autograd reference of the corrected-gradient learner
+(MZ_LEARN_CORRECTED; include/mz.h): the FC nets of Learning.jl:87-142 built
+from the Flux-order flat vectors, the unroll of Learning.jl:347-370 (Q10
+alignment: predictions on h0, h0, h1 .. h_{K-1}; make_dynamics_input's 2h and
+a/|A| plane, :293-304) and the per-sample-mean loss
+
+  L = (1/B) Σ_b (w_b/g_b) [Σ_k (v−z)² + Σ_k CE(logits, π) + ir·Σ_{k>=1} (r−u)²] + Σθ²
+
+differentiated by torch.autograd (float64 by default)."""
+import numpy as np
+import torch
+
+
+def corrected_loss_and_grads(conf, hyper, nets, batch, weights=None, dtype=torch.float64):
+    from muzero_jl_amd.networks import unflatten
+    K, A = conf.num_unroll_steps, len(conf.action_space)
+    params = [torch.tensor(np.asarray(f), dtype=dtype, requires_grad=True) for f in nets]
+
+    def layers(net):
+        # the same slicing as networks.unflatten, on the autograd leaves
+        out, off = [], 0
+        for ch, W, b, act in unflatten(conf, hyper, net, np.asarray(nets[net])):
+            o, i = W.shape
+            Wt = params[net][off: off + i * o].reshape(i, o).T
+            off += i * o
+            bt = params[net][off: off + o]
+            off += o
+            out.append((ch, Wt, bt, act))
+        return out
+
+    L = [layers(n) for n in range(3)]
+
+    def chain(net, ch, x):
+        for c, W, b, act in L[net]:
+            if c != ch:
+                continue
+            x = x @ W.T + b
+            x = torch.relu(x) if act == 1 else torch.tanh(x) if act == 2 else x
+        return x
+
+    obs = torch.tensor(batch["observation"], dtype=dtype)
+    acts = torch.tensor(batch["actions"], dtype=dtype)
+    tv = torch.tensor(batch["target_values"], dtype=dtype)
+    tr = torch.tensor(batch["target_rewards"], dtype=dtype)
+    tp = torch.tensor(batch["target_policies"], dtype=dtype)
+    gs = torch.tensor(batch["gradient_scale"], dtype=dtype)
+    w = torch.ones_like(gs) if weights is None else torch.tensor(weights, dtype=dtype)
+    B = obs.shape[0]
+    plane = conf.observation_shape[0] * conf.observation_shape[1]
+    hs = [chain(0, 0, obs)]
+    rewards = [torch.zeros(B, dtype=dtype)]
+    for k in range(1, K + 1):
+        sa = torch.cat([2 * hs[k - 1], (acts[:, k - 1:k] / A).repeat(1, plane)], 1)
+        t = chain(2, 0, sa)
+        hs.append(chain(2, 1, t))
+        rewards.append(chain(2, 2, t)[:, 0])
+    vals, logits = [], []
+    for k in range(K + 1):
+        t = chain(1, 0, hs[0 if k <= 1 else k - 1])
+        vals.append(chain(1, 1, t)[:, 0])
+        logits.append(chain(1, 2, t))
+    v = torch.stack(vals, 1)
+    lg = torch.stack(logits, 1)
+    r = torch.stack(rewards, 1)
+    c = w / gs / B
+    vloss = (c * ((v - tv) ** 2).sum(1)).sum()
+    ce = -(tp * torch.log_softmax(lg, -1)).sum(-1)
+    ploss = (c * ce.sum(1)).sum()
+    rloss = (c * ((r[:, 1:] - tr[:, 1:]) ** 2).sum(1)).sum() if conf.intermediate_rewards else 0 * vloss
+    data = vloss + ploss + rloss
+    l2 = [(p ** 2).sum() for p in params]
+    total = data + sum(l2)
+    grads = torch.autograd.grad(total, params)
+    vloss, ploss, rloss = vloss.detach(), ploss.detach(), rloss.detach()
+    return dict(grads=[g.detach().numpy() for g in grads], value=float(vloss), policy=float(ploss),
+                reward=float(rloss), l2=[float(x.detach()) for x in l2], values=v.detach().numpy(),
+                policies=torch.softmax(lg, -1).detach().numpy(), rewards=r.detach().numpy())
