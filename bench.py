@@ -324,6 +324,38 @@ def main():
         lkern = "mz_learn_small1" if world == 1 else None
         lkern_ms = lstep_ms
 
+    # ---- corrected-gradient learner (MZ_LEARN_CORRECTED, FC nets): real
+    # backprop through the unroll on MFMA; with world > 1 the exchanged
+    # gradient is data-dependent
+    corrected = None
+    if not resnet and args.learner_steps > 0:
+        from muzero_jl_amd.abi import LEARN_CORRECTED, LEARN_REF_SEMANTICS
+        eng.learner_set_mode(LEARN_CORRECTED)
+        for k in range(3):
+            lstep(1000 + k)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tc0 = time.perf_counter()
+        ncs = max(10, args.learner_steps // 2)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for k in range(ncs):
+            lstep(1003 + k)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        tcs = torch.tensor([time.perf_counter() - tc0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tcs, op=dist.ReduceOp.MAX)
+        f_fb = 3 * 2 * B * (net_macs(conf, hyper, 0) + (K + 1) * net_macs(conf, hyper, 1) +
+                            K * net_macs(conf, hyper, 2))     # forward + backward (dX, dW) ≈ 3x forward
+        cms = ev0.elapsed_time(ev1) / ncs
+        corrected = {"learner_steps_per_s": round(ncs / float(tcs.item()), 1), "step_ms": round(cms, 5),
+                     "flop_per_step": f_fb, "tflops": round(f_fb / (cms * 1e-3) / 1e12, 4),
+                     "frac": round(f_fb / (cms * 1e-3) / 1e12 / PEAK_F32, 5),
+                     "kernels": "mz_rp_sample + mz_bp_tile + mz_bp_dw + mz_bp_fold + mz_adam_kernel"}
+        eng.learner_set_mode(LEARN_REF_SEMANTICS)
+
     # ---- actor-learner loop (row a12, self_play! || learning!, Q16): self-play
     # moves with the actors' nets and one learner step per finished game, the
     # actors refreshed one checkpoint behind (mz_train_run, one GPU)
@@ -401,6 +433,7 @@ def main():
             "learner_steps_per_s": round(learner_sps, 1),
             "learner_step_ms": round(lstep_ms, 5),
             "learner_roofline": lroof,
+            "learner_corrected": corrected,
             "train_loop": train,
             "learner_config": {"batch_size": B, "num_unroll_steps": K, "mode": "ref_semantics",
                                "batch_source": "synthetic device batch" if game is atari else

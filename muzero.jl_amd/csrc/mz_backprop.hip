@@ -5,8 +5,9 @@
 //   mz_bp_tile  one workgroup (4 waves) per tile of 16 samples: the forward
 //               list of layer applications (each a 16-sample MFMA GEMM,
 //               y = act(W x + b), wave w owning output row blocks w, w+4, ..),
-//               the heads' loss gradients, then the list in reverse: dZ =
-//               dY ⊙ act'(y) in place, dX += Wᵀ dZ (MFMA, K = out).
+//               the heads' loss gradients, then the list in reverse: dX +=
+//               Wᵀ dZ (MFMA, K = out) with dZ = dY ⊙ act'(y) formed as the
+//               operand is loaded (the dW kernel forms it the same way).
 //   mz_bp_dw    one wave per 16x16 block of a layer's dW: Σ over tiles, the
 //               layer's applications and the 16 samples of dZ ⊗ x (MFMA with
 //               K = samples), + 2θ (∂Σθ²/∂θ); one wave per bias block.
@@ -21,6 +22,32 @@ __device__ __forceinline__ float bp_act(int act, float v) {
     return act == MZ_ACT_RELU ? mz_relu(v) : act == MZ_ACT_TANH ? det_tanhf(v) : v;
 }
 
+// dZ = dY ⊙ act'(y) (act' from the output y: relu y > 0, tanh 1 − y²)
+__device__ __forceinline__ float bp_dz(int act, float g, float y) {
+    return act == MZ_ACT_RELU ? (y > 0.0f ? g : 0.0f) : act == MZ_ACT_TANH ? g * (1.0f - y * y) : g;
+}
+
+// One 16-row block of a 16-sample MFMA GEMM, C[r][s] = Σ_k A(r, k) B(k, s),
+// its operands gathered BP_KC k-steps at a time (all loads of a chunk in
+// flight before its MFMAs: one memory latency per chunk, not per k-step)
+#define BP_KC 16
+template <class FA, class FB>
+__device__ __forceinline__ bp_f32x4 bp_gemm_block(int nk, int kq, FA fa, FB fb) {
+    bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < nk; k0 += BP_KC) {
+        float a[BP_KC], b[BP_KC];
+#pragma unroll
+        for (int j = 0; j < BP_KC; ++j) {
+            const int k = (k0 + j) * 4 + kq;
+            a[j] = k0 + j < nk ? fa(k) : 0.0f;
+            b[j] = k0 + j < nk ? fb(k) : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < BP_KC; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+    }
+    return acc;
+}
+
 // y = act(W x + b) for the tile (all 256 threads; rows in blocks of 16 per wave)
 __device__ __forceinline__ void bp_dense_fwd(const BpApp& P, const float* __restrict__ flat, float* T) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
@@ -31,15 +58,9 @@ __device__ __forceinline__ void bp_dense_fwd(const BpApp& P, const float* __rest
     for (int ob = wave; ob < nob; ob += 4) {
         const int o = ob * 16 + m;
         const bool oin = o < P.out;
-        bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-        for (int kk = 0; kk < nk; ++kk) {
-            const int i = kk * 4 + kq;
-            const bool iin = i < P.in;
-            const float a = oin && iin ? W[o + (size_t)P.out * i] : 0.0f;
-            const float b = iin ? X[i * 16 + m] : 0.0f;
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
-        }
+        const bp_f32x4 acc = bp_gemm_block(nk, kq,
+            [&](int i) { return oin && i < P.in ? W[o + (size_t)P.out * i] : 0.0f; },
+            [&](int i) { return i < P.in ? X[i * 16 + m] : 0.0f; });
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int oo = ob * 16 + kq * 4 + r;
@@ -48,25 +69,21 @@ __device__ __forceinline__ void bp_dense_fwd(const BpApp& P, const float* __rest
     }
 }
 
-// G[x] += Wᵀ G[y] (G[y] holds dZ)
-__device__ __forceinline__ void bp_dense_dx(const BpApp& P, const float* __restrict__ flat, float* G) {
+// G[x] += Wᵀ dZ with dZ = G[y] ⊙ act'(y) formed as the operand is loaded
+__device__ __forceinline__ void bp_dense_dx(const BpApp& P, const float* __restrict__ flat, const float* T,
+                                            float* G) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
     const float* W = flat + P.w_off;
-    const float* DZ = G + P.y;
+    const float* DY = G + P.y;
+    const float* Y = T + P.y;
     float* DX = G + P.x;
     const int nib = (P.in + 15) >> 4, nk = (P.out + 3) >> 2;
     for (int ib = wave; ib < nib; ib += 4) {
         const int i = ib * 16 + m;
         const bool iin = i < P.in;
-        bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-        for (int kk = 0; kk < nk; ++kk) {
-            const int o = kk * 4 + kq;
-            const bool oin = o < P.out;
-            const float a = oin && iin ? W[o + (size_t)P.out * i] : 0.0f;
-            const float b = oin ? DZ[o * 16 + m] : 0.0f;
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
-        }
+        const bp_f32x4 acc = bp_gemm_block(nk, kq,
+            [&](int o) { return iin && o < P.out ? W[o + (size_t)P.out * i] : 0.0f; },
+            [&](int o) { return o < P.out ? bp_dz(P.act, DY[o * 16 + m], Y[o * 16 + m]) : 0.0f; });
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int ii = ib * 16 + kq * 4 + r;
@@ -149,13 +166,7 @@ extern "C" __global__ __launch_bounds__(256) void mz_bp_tile(BpParams Q) {
     for (int a = Q.n_app - 1; a >= 0; --a) {
         const BpApp P = Q.apps[a];
         if (P.op == BP_DENSE) {
-            for (int e = tid; e < P.out * 16; e += 256) {     // dZ = dY ⊙ act'(y), in place
-                const float g = G[P.y + e], y = T[P.y + e];
-                G[P.y + e] = P.act == MZ_ACT_RELU ? (y > 0.0f ? g : 0.0f)
-                           : P.act == MZ_ACT_TANH ? g * (1.0f - y * y) : g;
-            }
-            __syncthreads();
-            bp_dense_dx(P, Q.flat, G);
+            bp_dense_dx(P, Q.flat, T, G);
         } else {                                              // ∂(2h)/∂h
             for (int e = tid; e < P.in * 16; e += 256) G[P.x + e] += 2.0f * G[P.y + e];
         }
@@ -173,8 +184,8 @@ extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
         float s = 0.0f;
         for (int t = 0; t < Q.tiles; ++t)
             for (int u = 0; u < L.n_use; ++u) {
-                const float* dz = Q.grad + (size_t)t * Q.tile_floats + Q.uses[L.use0 + u].y + o * 16;
-                for (int j = 0; j < 16; ++j) s += dz[j];
+                const size_t e = (size_t)t * Q.tile_floats + Q.uses[L.use0 + u].y + o * 16;
+                for (int j = 0; j < 16; ++j) s += bp_dz(L.act, Q.grad[e + j], Q.act[e + j]);
             }
         Q.out[L.b_off + o] = s + 2.0f * Q.flat[L.b_off + o];
         return;
@@ -189,7 +200,8 @@ extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
             const BpUse U = Q.uses[L.use0 + u];
 #pragma unroll
             for (int c = 0; c < 4; ++c) {                     // K = the 16 samples, 4 per MFMA
-                const float a = oin ? gt[U.y + o * 16 + 4 * c + kq] : 0.0f;
+                const int e = U.y + o * 16 + 4 * c + kq;
+                const float a = oin ? bp_dz(L.act, gt[e], at[e]) : 0.0f;
                 const float b = iin ? at[U.x + i * 16 + 4 * c + kq] : 0.0f;
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
             }
@@ -211,9 +223,15 @@ extern "C" __global__ __launch_bounds__(256) void mz_bp_fold(BpFoldParams Q) {
     __shared__ double red[3][256];
     const int tid = threadIdx.x;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    if (blockIdx.x < 3) {
+    if (blockIdx.x < 3) {                       // 8 loads in flight per thread, then their squares in order
         const size_t off = Q.netoff[blockIdx.x], n = Q.netoff[3 + blockIdx.x];
-        for (size_t i = tid; i < n; i += 256) s0 += (double)Q.flat[off + i] * (double)Q.flat[off + i];
+        for (size_t i0 = tid; i0 < n; i0 += 8 * 256) {
+            float x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = i0 + u * 256 < n ? Q.flat[off + i0 + u * 256] : 0.0f;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s0 += (double)x[u] * (double)x[u];
+        }
     } else {
         const int K1 = Q.K + 1;
         for (int b = tid; b < Q.B; b += 256) {

@@ -42,7 +42,7 @@ struct BpHead {
 struct BpUse { int x, y; };   // one application of a dense layer: input / output arena offsets
 
 struct BpLayer {
-    int w_off, b_off, in, out;
+    int w_off, b_off, in, out, act;
     int use0, n_use;      // uses[use0 .. use0 + n_use)
 };
 

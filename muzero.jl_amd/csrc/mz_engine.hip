@@ -1853,7 +1853,7 @@ static int build_bp(mz_handle* h) {
     for (size_t li = 0; li < h->layers.size(); ++li) {
         const LayerSpec& L = h->layers[li];
         BpLayer& bl = layers[li];
-        bl.w_off = (int)L.flux_w; bl.b_off = (int)L.flux_b; bl.in = L.in; bl.out = L.out;
+        bl.w_off = (int)L.flux_w; bl.b_off = (int)L.flux_b; bl.in = L.in; bl.out = L.out; bl.act = L.act;
         bl.use0 = (int)uses.size();
         for (const BpApp& a : apps) if (a.op == BP_DENSE && a.step == (int)li) uses.push_back(BpUse{a.x, a.y});
         bl.n_use = (int)uses.size() - bl.use0;
