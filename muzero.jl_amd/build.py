@@ -24,10 +24,12 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
          "-fno-slp-vectorize"]
 
 
-def build(force=False, verbose=False, jobs=None):
+def build(force=False, verbose=False, jobs=None, out=None, objdir=None, extra=()):
+    """out / objdir / extra: a variant library (A/B experiments, tools/ab_default.sh)."""
     csrc = os.path.join(PKG_DIR, "csrc")
     inc = os.path.join(os.path.dirname(PKG_DIR), "include")
-    objdir = os.path.join(os.path.dirname(LIB_PATH), "obj")
+    lib_path = out or LIB_PATH
+    objdir = objdir or os.path.join(os.path.dirname(LIB_PATH), "obj")
     srcs = [os.path.join(csrc, s) for s in SOURCES if os.path.exists(os.path.join(csrc, s))]
     hdrs = [os.path.join(csrc, h) for h in HEADERS if os.path.exists(os.path.join(csrc, h))] + \
         [os.path.join(inc, f) for f in ("mz.h", "mz_detmath.h")]
@@ -43,7 +45,7 @@ def build(force=False, verbose=False, jobs=None):
 
     def compile_one(so):
         s, o = so
-        cmd = [hipcc] + FLAGS + ["-c", "-o", o + ".tmp", s]
+        cmd = [hipcc] + FLAGS + list(extra) + ["-c", "-o", o + ".tmp", s]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
@@ -52,10 +54,10 @@ def build(force=False, verbose=False, jobs=None):
     if todo:
         with ThreadPoolExecutor(jobs or min(len(todo), os.cpu_count() or 4, 16)) as ex:
             list(ex.map(compile_one, todo))
-    if todo or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(os.path.getmtime(o) for o in objs):
-        cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB_PATH + ".tmp"] + objs
+    if todo or not os.path.exists(lib_path) or os.path.getmtime(lib_path) < max(os.path.getmtime(o) for o in objs):
+        cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib_path + ".tmp"] + objs
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
-        os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+        os.replace(lib_path + ".tmp", lib_path)
+    return lib_path

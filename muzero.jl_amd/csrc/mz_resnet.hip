@@ -475,14 +475,12 @@ __device__ __forceinline__ void rsearch_tree_body(const RSearchParams& P) {
         const int Nc = lg ? (int)(tree.nc(a) & 0xffffu) : 0;
         const int sum = gisum<GW>(Nc);
         if (a < A) P.child_visits[(size_t)gg * A + a] = lg ? (float)((double)Nc / (double)sum) : 0.0f;
-        int cnt[GW];
-#pragma unroll
-        for (int b = 0; b < GW; ++b) cnt[b] = __shfl(Nc, b, GW);
+        const uint32_t r = mz_rng_u32(P.seed, MZ_RNG_ACTION, gid, P.rng_step, 0);
+        const int act = select_action_dev<GW>(Nc, legal, A, P.temp_g ? P.temp_g[gg] : P.temperature, r);
         if (a == 0) {
             const int rN = st[RG_ROOTN];
             P.root_value[gg] = rN == 0 ? 0.0f : __int_as_float(st[RG_ROOTW]) / (float)rN;
-            const uint32_t r = mz_rng_u32(P.seed, MZ_RNG_ACTION, gid, P.rng_step, 0);
-            P.action_out[gg] = select_action_dev(cnt, legal, A, P.temp_g ? P.temp_g[gg] : P.temperature, r) + 1;
+            P.action_out[gg] = act + 1;
         }
     }
 }
@@ -663,13 +661,11 @@ __device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
         const int Nc = lg ? (int)(tree.nc(a) & 0xffffu) : 0;
         const int sum = gisum<GW>(Nc);
         if (a < A) P.child_visits[(size_t)gg * A + a] = lg ? (float)((double)Nc / (double)sum) : 0.0f;
-        int cnt[GW];
-#pragma unroll
-        for (int b = 0; b < GW; ++b) cnt[b] = __shfl(Nc, b, GW);
+        const uint32_t r = mz_rng_u32(P.seed, MZ_RNG_ACTION, gid, P.rng_step, 0);
+        const int act = select_action_dev<GW>(Nc, legal, A, P.temp_g ? P.temp_g[gg] : P.temperature, r);
         if (a == 0) {
             P.root_value[gg] = rN == 0 ? 0.0f : rW / (float)rN;
-            const uint32_t r = mz_rng_u32(P.seed, MZ_RNG_ACTION, gid, P.rng_step, 0);
-            P.action_out[gg] = select_action_dev(cnt, legal, A, P.temp_g ? P.temp_g[gg] : P.temperature, r) + 1;
+            P.action_out[gg] = act + 1;
         }
     }
 }

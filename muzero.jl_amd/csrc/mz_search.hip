@@ -197,14 +197,12 @@ __device__ __forceinline__ void search_body(const SearchParams& P) {
         const int Nc = lg ? (int)(tree.nc(a) & 0xffffu) : 0;
         const int sum = g16_isum(Nc);
         if (a < A) P.child_visits[(size_t)gg * A + a] = lg ? (float)((double)Nc / (double)sum) : 0.0f;
-        int cnt[16];
-#pragma unroll
-        for (int b = 0; b < 16; ++b) cnt[b] = __shfl(Nc, b, 16);
+        const uint32_t r = mz_rng_u32(P.seed, MZ_RNG_ACTION, gid, P.rng_step, 0);
+        const int act = select_action_dev<16>(Nc, legal, A, P.temp_g ? P.temp_g[gg] : P.temperature, r);
         if (a == 0) {
             const int rN = sg_rootN[g];
             P.root_value[gg] = rN == 0 ? 0.0f : sg_rootW[g] / (float)rN;
-            const uint32_t r = mz_rng_u32(P.seed, MZ_RNG_ACTION, gid, P.rng_step, 0);
-            P.action_out[gg] = select_action_dev(cnt, legal, A, P.temp_g ? P.temp_g[gg] : P.temperature, r) + 1;
+            P.action_out[gg] = act + 1;
         }
         if (LDS_TREE && P.dump_tree) dump_tree(tree, gtree, E, NN, a);
     }

@@ -60,16 +60,37 @@ __device__ __forceinline__ void sm_chain(const float (&w)[16], const float (&x)[
     }
 }
 
+// The search's first stage reads its inputs straight from the hidden-state
+// store (no gather copy, no barrier): prediction's input x_pred = the parent's
+// h, dynamics' x_dyn = 2h ⊕ a/|A| (make_state_action, SelfPlay.jl:7-14; Q1's
+// in-place doubling of the parent is written back after the networks).
+struct SmFusedIn {
+    const float* hid; const int* leaf_e; const int* leaf_a; const float* aval;
+    int NN, H, plane, x_pred, x_dyn;
+};
+
 // One stage.  R = this thread's record of stage K; the record of stage K+1
 // (constant for the whole kernel) is fetched while stage K computes.
-template <int T>
-__device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int4* rec_next, float* lds) {
+template <int T, bool FI = false>
+__device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int4* rec_next, float* lds,
+                                         const SmFusedIn* fi = nullptr) {
     const int q = (threadIdx.x >> 4) & 3, i = threadIdx.x & 15;
     // x[q*kq + i] of the T games (rows beyond kq meet zero weights; the 64-row
     // input buffers are zero beyond K, so every step is exact)
     const float* xp = lds + R.x + (q * R.y + i) * T;
     float x[T];
-    if constexpr (T == 1) {
+    if constexpr (FI) {
+        const int k = q * R.y + i;
+        const bool pred = R.x == fi->x_pred, dyn = R.x == fi->x_dyn;
+#pragma unroll
+        for (int g = 0; g < T; ++g) {
+            const float* hp = fi->hid + ((size_t)g * fi->NN + fi->leaf_e[g]) * fi->H;
+            const float hv = k < fi->H ? hp[k] : 0.0f;
+            x[g] = pred ? hv
+                 : dyn ? (k < fi->H ? hv * 2.0f : k < fi->H + fi->plane ? fi->aval[fi->leaf_a[g]] : 0.0f)
+                 : xp[g];
+        }
+    } else if constexpr (T == 1) {
         x[0] = xp[0];
     } else if constexpr (T == 2) {
         const float2 v = *reinterpret_cast<const float2*>(xp);
@@ -111,18 +132,21 @@ __device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int
 
 // rec: this thread's record of stage 0 ([stage][slot][row] int4, stride 128)
 template <int T, int NMAX, int K = 0>
-__device__ __forceinline__ void sm_run_k(int n, const float (&wr)[NMAX][16], int4 R, const int4* rec, float* lds) {
+__device__ __forceinline__ void sm_run_k(int n, const float (&wr)[NMAX][16], int4 R, const int4* rec, float* lds,
+                                         const SmFusedIn* fi) {
     if constexpr (K < NMAX) {
         if (K < n) {
-            const int4 Rn = sm_stage<T>(wr[K], R, rec + (K + 1) * (SM_SLOTS * 64), lds);
-            sm_run_k<T, NMAX, K + 1>(n, wr, Rn, rec, lds);
+            const int4 Rn = K == 0 && fi ? sm_stage<T, true>(wr[K], R, rec + (K + 1) * (SM_SLOTS * 64), lds, fi)
+                                         : sm_stage<T>(wr[K], R, rec + (K + 1) * (SM_SLOTS * 64), lds);
+            sm_run_k<T, NMAX, K + 1>(n, wr, Rn, rec, lds, fi);
         }
     }
 }
 
 template <int T, int NMAX>
-__device__ __forceinline__ void sm_run(int n, const float (&wr)[NMAX][16], const int4* rec, float* lds) {
-    sm_run_k<T, NMAX>(n, wr, rec[0], rec, lds);
+__device__ __forceinline__ void sm_run(int n, const float (&wr)[NMAX][16], const int4* rec, float* lds,
+                                       const SmFusedIn* fi = nullptr) {
+    sm_run_k<T, NMAX>(n, wr, rec[0], rec, lds, fi);
 }
 
 // Weights of this thread's (slot, row, quarter) for stages 0..n-1 from the
@@ -146,11 +170,6 @@ __device__ __forceinline__ void sm_load(int k0, int k1, const float* W, float (&
             }
         }
     }
-}
-
-// once-per-move helpers kept out of line
-__device__ __noinline__ int sm_select_action(const int* cnt, uint32_t legal, int A, float temperature, uint32_t r) {
-    return select_action_dev(cnt, legal, A, temperature, r);
 }
 
 
@@ -269,6 +288,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     __syncthreads();
     SM_STAMP(0);
 
+    const SmFusedIn fin{hid, sg_leaf_e, sg_leaf_a, l_aval, NN, H, P.plane, P.x_pred, P.x_dyn};
     // Per simulation, three workgroup barriers besides the 8 network stages:
     // wave 0 owns the trees (T <= 4 games x 16 lanes), so select -> gather and
     // backup -> next select need only wave-local ordering.
@@ -290,27 +310,12 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
                 st_acc[7] += (unsigned long long)md;
             }
 #endif
-            // ---- gather: parent h -> prediction input; h *= 2 in place (Q1) -> dynamics input
-            for (int i = tid; i < T * H; i += 64) {
-                const int gl = i / H, k = i - gl * H;
-                if (tile0 + gl >= P.G) continue;              // inactive game of a partial tile
-                float* hp = hid + ((size_t)gl * NN + sg_leaf_e[gl]) * H + k;
-                const float hv = *hp;
-                const float h2 = hv * 2.0f;
-                *hp = h2;
-                act[P.x_pred + k * T + gl] = hv;
-                act[P.x_dyn + k * T + gl] = h2;
-            }
-            for (int i = tid; i < T * P.plane; i += 64) {
-                const int gl = i / P.plane, k = i - gl * P.plane;
-                if (tile0 + gl >= P.G) continue;
-                act[P.x_dyn + (H + k) * T + gl] = l_aval[sg_leaf_a[gl]];
-            }
         }
         __syncthreads();
         SM_STAMP(2);
-        // ---- prediction(parent.h) ‖ dynamics(2h ⊕ a/|A|)
-        sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act);
+        // ---- prediction(parent.h) ‖ dynamics(2h ⊕ a/|A|): the first stage
+        // reads the parent's h from the hidden-state store (gather fused)
+        sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act, &fin);
         SM_STAMP(3);
         const int e_new = s + 1;
         // expand (wave 2) runs beside the read-outs + backup (wave 0): they
@@ -357,8 +362,14 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
                                                      sg_stage + 16 * g2);
             if (active2) init_edges(tree2, e_new, a, A, prior);
         } else if (tid >= 192) {
-            for (int i = tid - 192; i < T * H; i += SM_THREADS - 192)     // store h'
-                hid[((size_t)(i / H) * NN + e_new) * H + (i % H)] = act[P.h_out + (i % H) * T + i / H];
+            for (int i = tid - 192; i < T * H; i += SM_THREADS - 192) {   // store h'; parent h *= 2 (Q1)
+                const int gl = i / H, k = i - gl * H;
+                hid[((size_t)gl * NN + e_new) * H + k] = act[P.h_out + k * T + gl];
+                if (tile0 + gl < P.G) {
+                    float* hp = hid + ((size_t)gl * NN + sg_leaf_e[gl]) * H + k;
+                    *hp = *hp * 2.0f;
+                }
+            }
         }
         __syncthreads();
         SM_STAMP(4);
@@ -371,14 +382,12 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         const int Nc = lg ? (int)(tree.nc(a) & 0xffffu) : 0;
         const int sum = g16_isum(Nc);
         if (a < A) P.child_visits[(size_t)gg * A + a] = lg ? (float)((double)Nc / (double)sum) : 0.0f;
-        int cnt[16];
-#pragma unroll
-        for (int b = 0; b < 16; ++b) cnt[b] = __shfl(Nc, b, 16);
+        const uint32_t r = mz_rng_u32(P.seed, MZ_RNG_ACTION, gid, P.rng_step, 0);
+        const int act = select_action_dev<16>(Nc, legal, A, P.temp_g ? P.temp_g[gg] : P.temperature, r);
         if (a == 0) {
             const int rN = sg_rootN[g];
             P.root_value[gg] = rN == 0 ? 0.0f : sg_rootW[g] / (float)rN;
-            const uint32_t r = mz_rng_u32(P.seed, MZ_RNG_ACTION, gid, P.rng_step, 0);
-            P.action_out[gg] = sm_select_action(cnt, legal, A, P.temp_g ? P.temp_g[gg] : P.temperature, r) + 1;
+            P.action_out[gg] = act + 1;
         }
         if (P.dump_tree) {
             TreeView dst = tree_view(P.tree + (size_t)gg * P.tree_game_bytes, E, NN);

@@ -201,7 +201,11 @@ struct SelectOut { int leaf_e, leaf_a, vtp, depth; };
 // (the f64 subexpression of ucb_score, SelfPlay.jl:172-174) for Nc < Np <=
 // S+1 as a triangle, so select replaces an f64 division by one LDS read.
 __host__ __device__ __forceinline__ int pbterm_index(int Np, int Nc) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return (int)(__umul24((unsigned)Np, (unsigned)(Np + 1)) >> 1) + Nc;   // full-rate 24-bit multiply
+#else
     return (int)(((unsigned)Np * (unsigned)(Np + 1)) >> 1) + Nc;
+#endif
 }
 __host__ __device__ __forceinline__ size_t pbterm_count(int S) { return (size_t)(S + 2) * (S + 3) / 2; }
 
@@ -246,7 +250,7 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
         // the parent's pUCT table entries depend only on Np: read them with the record
         double pbn = 0.0, sqn = 0.0;
         if constexpr (!TAB) { pbn = pbc_tab[Np]; sqn = sqrt_tab[Np]; }
-        float4 ed = t.e[e * A + ac];
+        float4 ed = t.e[(int)__umul24((unsigned)e, (unsigned)A) + ac];
         // keep the whole record one load and the score branch-free: without
         // these the compiler sinks the ev load and the division into an
         // Nc > 0 branch (a second LDS round trip and two exec branches)
@@ -260,6 +264,9 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
             pb_c = pbn * (sqn / (double)(Nc + 1));
         }
         const double prior_score = pb_c * (double)ed.z;
+        // normalize (:33-39), the IEEE division: a reciprocal per walk plus a
+        // Markstein correction is exact on [2^-60, 2^60] but needs a per-level
+        // range test and branch, which measured slower
         float vn = (ed.w - mmin) / den;                  // discarded unless norm and Nc > 0
         asm volatile("" : "+v"(vn));
         const float vs = Nc > 0 ? (norm ? vn : ed.w) : 0.0f;
@@ -284,7 +291,7 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
                 ach = nth_set_bit(mask, (int)mz_rng_below(r, (uint32_t)nt));
             }
         }
-        const int ei = e * A + ach;
+        const int ei = (int)__umul24((unsigned)e, (unsigned)A) + ach;
         const uint32_t ncc = gor<GW>(a == ach ? nc : 0u);  // the chosen lane's nc, via DPP
         const int Cch = (int)(ncc >> 16);
         const bool keep = a == depth;                     // depth < GW: lane `depth` keeps the level
@@ -454,34 +461,64 @@ __device__ __forceinline__ void backup_path_1p(const TreeView& t, const int* pat
     root_N = __shfl(rN, 0, GW); root_W = __shfl(rW, 0, GW);
 }
 
-// select_action (SelfPlay.jl:293-306): same rule as the oracle.
-__device__ int select_action_dev(const int* cnt, uint32_t legal, int A, float temperature, uint32_t r) {
-    int acts[MZ_MAX_ACTIONS], c[MZ_MAX_ACTIONS], n = 0;
-    for (int a = 0; a < A; ++a) if ((legal >> a) & 1u) { acts[n] = a; c[n] = cnt[a]; ++n; }
-    if (temperature == 0.0f) {
-        int best = 0;
-        for (int i = 1; i < n; ++i) if (c[i] > c[best]) best = i;
-        return acts[best];
+// select_action (SelfPlay.jl:293-306) for a GW-lane group, called by every
+// lane of the group with its own child's count Nc (lane a = action a): the
+// oracle's rule (legal actions in ascending order).  The N^(1/T) weights are
+// computed lane-parallel; the ordered scans read the lanes by shuffle with
+// static indices, so nothing lands in a scratch frame.  Every lane returns
+// the action.
+template <int GW>
+__device__ __forceinline__ int select_action_dev(int Nc, uint32_t legal, int A, float temperature, uint32_t r) {
+    const int a = (int)(threadIdx.x % GW);
+    legal &= A >= 32 ? 0xffffffffu : (1u << A) - 1u;
+    const bool lg = (legal >> a) & 1u;
+    const int n = __builtin_popcount(legal);
+    const int last = 31 - __builtin_clz(legal);
+    if (isinf(temperature)) return nth_set_bit(legal, (int)mz_rng_below(r, (uint32_t)n));
+    // the weight each lane contributes: N (T = 0 and T = 1) or f32(N^(1/T))
+    const bool gen = temperature != 0.0f && temperature != 1.0f;
+    const float wl = gen ? (lg && Nc > 0 ? (float)det_exp(det_log((double)Nc) * (double)(1.0f / temperature)) : 0.0f)
+                         : 0.0f;
+    const int c = lg ? Nc : 0;
+    if (temperature == 0.0f) {                        // argmax, the first maximum
+        int best = -1, bc = 0;
+#pragma unroll
+        for (int b = 0; b < GW; ++b) {
+            const int cb = __shfl(c, b, GW);
+            if (((legal >> b) & 1u) && (best < 0 || cb > bc)) { best = b; bc = cb; }
+        }
+        return best;
     }
-    if (isinf(temperature)) return acts[mz_rng_below(r, (uint32_t)n)];
-    if (temperature == 1.0f) {
+    if (!gen) {                                       // T = 1: ∝ N, the integer counts exactly
         uint32_t tot = 0;
-        for (int i = 0; i < n; ++i) tot += (uint32_t)c[i];
-        if (tot == 0) return acts[mz_rng_below(r, (uint32_t)n)];
-        uint32_t tt = mz_rng_below(r, tot), cum = 0;
-        for (int i = 0; i < n; ++i) { cum += (uint32_t)c[i]; if (cum > tt) return acts[i]; }
-        return acts[n - 1];
+#pragma unroll
+        for (int b = 0; b < GW; ++b) tot += (uint32_t)__shfl(c, b, GW);
+        if (tot == 0) return nth_set_bit(legal, (int)mz_rng_below(r, (uint32_t)n));
+        const uint32_t tt = mz_rng_below(r, tot);
+        uint32_t cum = 0;
+        int pick = -1;
+#pragma unroll
+        for (int b = 0; b < GW; ++b) {
+            cum += (uint32_t)__shfl(c, b, GW);
+            if (((legal >> b) & 1u) && pick < 0 && cum > tt) pick = b;
+        }
+        return pick >= 0 ? pick : last;
     }
-    float e = 1.0f / temperature;
-    float w[MZ_MAX_ACTIONS], s = 0.0f;
-    for (int i = 0; i < n; ++i) {
-        w[i] = c[i] > 0 ? (float)det_exp(det_log((double)c[i]) * (double)e) : 0.0f;
-        s = s + w[i];
+    float s = 0.0f;                                   // ∝ N^(1/T): f32 sum in ascending order
+#pragma unroll
+    for (int b = 0; b < GW; ++b) {
+        const float wb = __shfl(wl, b, GW);
+        if ((legal >> b) & 1u) s = s + wb;
     }
-    float u = (float)(r >> 8) * 5.9604644775390625e-08f * s;
+    const float u = (float)(r >> 8) * 5.9604644775390625e-08f * s;
     float cum = 0.0f;
-    for (int i = 0; i < n; ++i) { cum = cum + w[i]; if (cum > u) return acts[i]; }
-    return acts[n - 1];
+    int pick = -1;
+#pragma unroll
+    for (int b = 0; b < GW; ++b) {
+        const float wb = __shfl(wl, b, GW);
+        if (((legal >> b) & 1u) && pick < 0) { cum = cum + wb; if (cum > u) pick = b; }
+    }
+    return pick >= 0 ? pick : last;
 }
 
 // Copy one game's tree to the global debug buffers (parity tests only).
