@@ -81,10 +81,14 @@ def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0, resnet=False,
 
 
 def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summaries
+    """HBM bytes per launch of `kernel` ("a+b": the sum over a launch pair)
+    from the committed PMC summaries
     (profiles/pmc_*.json of tools/pmc_summary.py, profiles/pmc2_*.json of
     tools/pmc_kernels.py: FETCH_SIZE x2 for the 16 B/lane image reads, per
     MI355X_MICROARCH.md, + WRITE_SIZE); the latest round wins; None if none."""
+    if "+" in kernel:
+        parts = [pmc_traffic(k) for k in kernel.split("+")]
+        return None if any(p is None for p in parts) else sum(parts)
     traffic = None
     for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
         with open(pmc) as f:
@@ -310,7 +314,7 @@ def main():
     lstep_ms = float(np.mean([a.elapsed_time(b) for a, b in lev]))
     # the learner's dominant kernel: FC world 1 = the whole step is one launch
     # (mz_learn_small*), timed by the events around it; ResNet = the unroll
-    # (mz_runroll_kernel), timed by the engine's events on its launch stream
+    # (mz_runroll_chain + mz_runroll_pred), timed by the engine's events on its launch stream
     if resnet:
         eng.debug_enable(4)
         eng.debug_kernel_time()
@@ -319,7 +323,7 @@ def main():
         torch.cuda.synchronize()
         t_ms, n_l = eng.debug_kernel_time()
         eng.debug_enable(0)
-        lkern, lkern_ms = "mz_runroll_kernel", t_ms / n_l
+        lkern, lkern_ms = "mz_runroll_chain+mz_runroll_pred", t_ms / n_l
     else:
         lkern = "mz_learn_small1" if world == 1 else None
         lkern_ms = lstep_ms
