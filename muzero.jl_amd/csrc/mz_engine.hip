@@ -148,7 +148,9 @@ struct mz_handle {
     float bn_s = 1.0f;
     int* d_rpath = nullptr; int* d_rgst = nullptr;          // ResNet search: [G][2(S+2)], [G][RG_INTS]
     float* d_rxpred = nullptr; float* d_rov = nullptr; float* d_rologit = nullptr; float* d_ror = nullptr;
-    float* d_rhs = nullptr;                 // [bcap][H] learner unroll scratch (h between the nets)
+    float* d_rhs = nullptr;                 // [bcap][K][H] learner unroll scratch (h between the nets)
+    float* d_rts = nullptr;                 // [bcap][K][H] dynamics trunk outputs (the reward heads' input)
+    int rn_dyn_split = 0;                   // first reward-head layer of the dynamics plan
     int device = 0, max_games = 0;
     uint64_t seed = 0;
     std::string err;
@@ -1055,6 +1057,9 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
         h->rn_lds[n] = (size_t)h->rplan[n].lds_floats * 4;
     }
     h->packed_w_n = sw.size(); h->packed_b_n = 0;
+    h->rn_dyn_split = (int)sp[MZ_NET_DYN].size();     // the reward head: the dynamics layers of chain 2
+    for (size_t i = 0; i < sp[MZ_NET_DYN].size(); ++i)
+        if (sp[MZ_NET_DYN][i].chain == 2) { h->rn_dyn_split = (int)i; break; }
     {   // learner chain tiles: MZ_RN_NG_LEARN (power of two), default 1 (tools/rn_learner_ab.sh)
         const char* e = std::getenv("MZ_RN_NG_LEARN");
         int ngl = e ? std::atoi(e) : 1;
@@ -1641,7 +1646,10 @@ static int ensure_batch(mz_handle* h, int B) {
     for (int i = 0; i < 9; ++i) MZ_TRY(h, dalloc(h, bufs[i], sizes[i]));
     MZ_TRY(h, dalloc(h, &h->d_lterm, (size_t)2 * B * (K + 1)));
     MZ_TRY(h, dalloc(h, &h->d_bw, (size_t)B));
-    if (h->kind == 1) MZ_TRY(h, dalloc(h, &h->d_rhs, (size_t)B * std::max(K, 1) * h->H));
+    if (h->kind == 1) {
+        MZ_TRY(h, dalloc(h, &h->d_rhs, (size_t)B * std::max(K, 1) * h->H));
+        MZ_TRY(h, dalloc(h, &h->d_rts, (size_t)B * std::max(K, 1) * h->H));
+    }
     h->bcap = B;
     return 0;
 }
@@ -1671,6 +1679,12 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
     } U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
     U.hs = h->d_rhs; U.plans = h->d_rplan; U.Wimg = h->d_Wp; U.flat = h->d_flat;
     U.plans_l = h->d_rplan_l; U.ng_l = h->rn_ng_l;
+    U.dyn_split = h->rn_dyn_split; U.ts = h->d_rts;
+    U.stamps = nullptr;
+#ifdef MZ_STAMPS
+    if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * std::max(h->max_games, 128)));
+    U.stamps = h->d_stamps;
+#endif
     void* args[] = {&U};
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->time_unroll) {
@@ -1684,7 +1698,8 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
         const int KH = std::max(U.K, 1);
         MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_chain, dim3((B + U.ng_l - 1) / U.ng_l), dim3(RN_THREADS),
                                   args, h->rn_lds_l, st));
-        MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred, dim3((B * KH + U.ng - 1) / U.ng), dim3(RN_THREADS),
+        MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred, dim3((B * KH + U.ng - 1) / U.ng, U.K > 0 ? 2 : 1),
+                                  dim3(RN_THREADS),
                                   args, runroll_lds(h), st));
     }
     if (e1) MZ_TRY(h, hipEventRecord(e1, st));

@@ -122,11 +122,35 @@ __device__ __forceinline__ void rn_epilogue(const RLayer& L, const mz_f32x4 (&ac
 // through the k table: t = off·256 | (dx+8)·16 | (dy+8) with off = ch·ncols +
 // (dx + W·dy)·NG, zero outside the board.  Addresses are clamped in range and
 // out-of-range operands selected to 0 (no branches).
-template <int NBW, int MODE>
+// Operands of a wave's first unit of a layer, loaded before the barrier that
+// ends the previous layer (rn_run<.., PF = true>): its first chunk of A
+// fragments and its epilogue parameters.  Without this every layer starts
+// with a dependent round trip to L2 for the plan, then one for the weights.
+struct RnPf {
+    float an[4][4];
+    float ep[3][4];
+};
+
+template <int NBW, int MODE, bool PF = false>
 __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restrict__ Wimg,
                                            const float* __restrict__ flat, float* lds, int NG, int Wb, int P,
-                                           float bn_s, float bn_r) {
+                                           float bn_s, float bn_r, const RnPf* pf = nullptr,
+                                           unsigned long long* dbg = nullptr) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
+#ifdef MZ_STAMPS   // diagnostic build: phases of wave 0's first unit (waits forced, so approximate)
+#define RN_DBG(k)                                                                                     \
+    do {                                                                                              \
+        if (dbg && threadIdx.x == 0 && u == 0) dbg[k] = __builtin_amdgcn_s_memtime();                 \
+    } while (0)
+#define RN_DBG_WAIT(k)                                                                                \
+    do {                                                                                              \
+        if (dbg && u == 0) { __builtin_amdgcn_s_waitcnt(0); RN_DBG(k); }                              \
+    } while (0)
+#else
+#define RN_DBG(k) do {} while (0)
+#define RN_DBG_WAIT(k) do {} while (0)
+#endif
+    (void)dbg;
     const int ncols = MODE == 0 ? NG : P * NG;
     const int n_nb = (ncols + 15) >> 4;
     const int n_grp = (n_nb + NBW - 1) / NBW;
@@ -136,12 +160,27 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
     const int* tab = reinterpret_cast<const int*>(lds) + L.ktab;
     int u = wave;
     if (u >= units) return;
+    RN_DBG(0);
     float an[4][4];
-    rn_load_a(an, Wimg, L, u / n_grp, 0, lane);
+    if constexpr (PF) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) an[q][jj] = pf->an[q][jj];
+    } else {
+        rn_load_a(an, Wimg, L, u / n_grp, 0, lane);
+    }
     for (; u < units; u += nwaves) {
         const int ob = u / n_grp, grp = u - ob * n_grp;
         float ep[3][4];
-        rn_load_ep(ep, L, flat, ob, kl);
+        if (PF && u == wave) {
+#pragma unroll
+            for (int e = 0; e < 3; ++e)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ep[e][r] = pf->ep[e][r];
+        } else {
+            rn_load_ep(ep, L, flat, ob, kl);
+        }
         int cb[NBW], cw[NBW], chh[NBW];
 #pragma unroll
         for (int i = 0; i < NBW; ++i) {
@@ -169,6 +208,7 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
         for (int i = 0; i < NBW; ++i)
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[i][q] = mz_f32x4{0.f, 0.f, 0.f, 0.f};
+        RN_DBG_WAIT(1);                                 // operands of the first chunk in registers
         for (int c = 0; c < nch; ++c) {
             float ac[4][4];
 #pragma unroll
@@ -218,34 +258,68 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
                         acc[i][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[q][jj], b[jj][q][i], acc[i][q], 0, 0, 0);
             }
         }
+#ifdef MZ_STAMPS
+        if (dbg && u == 0) {
+#pragma unroll
+            for (int i = 0; i < NBW; ++i)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) asm volatile("s_nop 7" :: "v"(acc[i][q]));
+        }
+#endif
+        RN_DBG_WAIT(2);                                 // chunks done (MFMA results consumed)
         int nn[NBW];
 #pragma unroll
         for (int i = 0; i < NBW; ++i) nn[i] = (grp * NBW + i) * 16 + (lane & 15);
         rn_epilogue<NBW>(L, acc, ep, lds, ob, kl, nn, ncols, bn_s, bn_r);
+        RN_DBG_WAIT(3);                                 // epilogue stored
     }
 }
 
-template <bool NARROW>
-__device__ __forceinline__ void rn_layer(const RLayer& L, const float* __restrict__ Wimg,
-                                         const float* __restrict__ flat, float* lds, int NG, int Wb, int P,
-                                         float bn_s, float bn_r) {
 #ifndef RN_NBW
 #define RN_NBW 3
 #endif
-    // narrow tiles (the learner chain's, a few items on a small board) have
-    // fewer than 3 column blocks: a unit of exactly that many (no MFMAs on
-    // columns past the tile)
-    const int n_nb = NARROW && L.spatial ? (P * NG + 15) >> 4 : 3;
+// Column blocks per unit of layer L (the rn_layer_t instance rn_layer picks):
+// narrow tiles (the learner chain's, a few items on a small board) have fewer
+// than 3 column blocks, so a unit of exactly that many (no MFMAs on columns
+// past the tile)
+template <bool NARROW>
+__device__ __forceinline__ int rn_nbw(const RLayer& L, int NG, int P) {
+    if (!L.spatial) return 1;
+    const int n_nb = NARROW ? (P * NG + 15) >> 4 : 3;
+    return n_nb == 1 ? 1 : n_nb == 2 ? 2 : L.kk > 1 ? 3 : RN_NBW;
+}
+
+template <bool NARROW, bool PF = false>
+__device__ __forceinline__ void rn_layer(const RLayer& L, const float* __restrict__ Wimg,
+                                         const float* __restrict__ flat, float* lds, int NG, int Wb, int P,
+                                         float bn_s, float bn_r, const RnPf* pf = nullptr,
+                                         unsigned long long* dbg = nullptr) {
+    const int n_nb = NARROW && L.spatial ? (P * NG + 15) >> 4 : 3;     // as rn_nbw
     if (L.kk > 1) {
-        if (n_nb == 1) rn_layer_t<1, 2>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
-        else if (n_nb == 2) rn_layer_t<2, 2>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
-        else rn_layer_t<3, 2>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+        if (n_nb == 1) rn_layer_t<1, 2, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+        else if (n_nb == 2) rn_layer_t<2, 2, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+        else rn_layer_t<3, 2, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
     } else if (L.spatial) {
-        if (n_nb == 1) rn_layer_t<1, 1>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
-        else if (n_nb == 2) rn_layer_t<2, 1>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
-        else rn_layer_t<RN_NBW, 1>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+        if (n_nb == 1) rn_layer_t<1, 1, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+        else if (n_nb == 2) rn_layer_t<2, 1, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+        else rn_layer_t<RN_NBW, 1, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
     } else {
-        rn_layer_t<1, 0>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+        rn_layer_t<1, 0, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+    }
+}
+
+// This wave's first-unit operands of layer L (no-op for a wave without one)
+template <bool NARROW>
+__device__ __forceinline__ void rn_prefetch(const RLayer& L, const float* __restrict__ Wimg,
+                                            const float* __restrict__ flat, int NG, int P, RnPf& pf) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ncols = L.spatial ? P * NG : NG;
+    const int nbw = rn_nbw<NARROW>(L, NG, P);
+    const int n_grp = (((ncols + 15) >> 4) + nbw - 1) / nbw;
+    if (wave < L.n_ob * n_grp) {
+        const int ob = wave / n_grp;
+        rn_load_a(pf.an, Wimg, L, ob, 0, lane);
+        rn_load_ep(pf.ep, L, flat, ob, lane >> 4);
     }
 }
 
@@ -267,23 +341,53 @@ __device__ void rn_fill_ktabs(const RPlan& R, float* lds, int NG, int Wb, int P)
 // A net: its layers one by one, a workgroup barrier after each.
 // NARROW: also the 1- / 2-column-block units (the learner chain's narrow
 // tiles); the wide-tile kernels keep the 3-block units only
-template <bool NARROW = false>
+// PF: the next layer's plan entry, first A chunk and epilogue parameters are
+// loaded before each layer barrier (kernels with the register room: 512
+// threads).  Layers [i0, i1) (i1 < 0: to the end).
+template <bool NARROW = false, bool PF = false>
 __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const float* flat, float* lds, int NG,
-                                       int Wb, int P, float bn_s, unsigned long long* st = nullptr) {
+                                       int Wb, int P, float bn_s, unsigned long long* st = nullptr, int i0 = 0,
+                                       int i1 = -1) {
     const float bn_r = 1.0f / bn_s;
     const int wv = threadIdx.x >> 6;
+    if (i1 < 0) i1 = R.n;
 #ifdef MZ_STAMPS
     if (st && (threadIdx.x & 63) == 0) st[wv * 64 + 63] = __builtin_amdgcn_s_memtime();
 #endif
-    for (int i = 0; i < R.n; ++i) {
-        rn_layer<NARROW>(R.L[i], Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+    if constexpr (PF) {
+        if (i0 >= i1) return;
+        RnPf pf;
+        RLayer L = R.L[i0];
+        rn_prefetch<NARROW>(L, Wimg, flat, NG, P, pf);
+        for (int i = i0; i < i1; ++i) {
+            RLayer Ln;
+            if (i + 1 < i1) Ln = R.L[i + 1];
+            unsigned long long* dbg = nullptr;
 #ifdef MZ_STAMPS
-        if (st && (threadIdx.x & 63) == 0) st[wv * 64 + 2 * i] = __builtin_amdgcn_s_memtime();
+            if (st && i - i0 < 31) dbg = st + 1024 + 8 * (i - i0);
 #endif
-        __syncthreads();
+            rn_layer<NARROW, true>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, &pf, dbg);
+            if (i + 1 < i1) rn_prefetch<NARROW>(Ln, Wimg, flat, NG, P, pf);
 #ifdef MZ_STAMPS
-        if (st && (threadIdx.x & 63) == 0) st[wv * 64 + 2 * i + 1] = __builtin_amdgcn_s_memtime();
+            if (st && (threadIdx.x & 63) == 0 && i - i0 < 31) st[wv * 64 + 2 * (i - i0)] = __builtin_amdgcn_s_memtime();
 #endif
+            __syncthreads();
+#ifdef MZ_STAMPS
+            if (st && (threadIdx.x & 63) == 0 && i - i0 < 31) st[wv * 64 + 2 * (i - i0) + 1] = __builtin_amdgcn_s_memtime();
+#endif
+            L = Ln;
+        }
+    } else {
+        for (int i = i0; i < i1; ++i) {
+            rn_layer<NARROW>(R.L[i], Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+#ifdef MZ_STAMPS
+            if (st && (threadIdx.x & 63) == 0 && i - i0 < 31) st[wv * 64 + 2 * (i - i0)] = __builtin_amdgcn_s_memtime();
+#endif
+            __syncthreads();
+#ifdef MZ_STAMPS
+            if (st && (threadIdx.x & 63) == 0 && i - i0 < 31) st[wv * 64 + 2 * (i - i0) + 1] = __builtin_amdgcn_s_memtime();
+#endif
+        }
     }
     (void)wv;
 }
@@ -776,11 +880,15 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_kernel(RUnro
 // Learner unroll, split form (the same read-outs as mz_runroll_kernel, bit for
 // bit: every tile column is an independent fma chain, so the tile width does
 // not change a result).  The unroll's only sequential part is representation
-// (:347) then K dynamics steps (:355-362); the K predictions (:351, :356) only
-// read h_0 .. h_{K-1}.  mz_runroll_chain runs the chain on narrow tiles of
-// ng_l samples — B / ng_l workgroups instead of B / 16, a narrower MFMA
-// column range per layer, so a short per-layer critical path — and stores
-// h_s to hs[b][s]; mz_runroll_pred then runs the B·K predictions as one wide
+// (:347) then the K dynamics steps' state path (:355-362: the trunk and the
+// state head, h_{s-1} -> h_s); the K predictions (:351, :356) only read h_0 ..
+// h_{K-1} and the K reward heads only the dynamics trunk outputs.
+// mz_runroll_chain runs that path on narrow tiles of ng_l samples — B / ng_l
+// workgroups instead of B / 16, a narrower MFMA column range per layer, so a
+// short per-layer critical path, with each layer's plan entry and first
+// operands loaded under the previous one — and stores h_s to hs[b][s] and the
+// trunk output of step s to ts[b][s-1]; mz_runroll_pred then runs the B·K
+// predictions (blockIdx.y = 0) and the B·K reward heads (y = 1) as one wide
 // launch on tiles of ng items.
 extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrollParams U) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -792,14 +900,22 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrol
     const bool ok = b < U.B;
     const size_t bs = (size_t)(ok ? b : 0);
     const int KH = K > 0 ? K : 1;
+    const int split = U.dyn_split;                 // first reward-head layer of the dynamics plan
+    const int trunk = Rd.L[split].in_off;          // the trunk output the reward head reads
     float* hs = U.hs + bs * KH * H;                 // [K][H]: h_s, s = 0 .. K-1
+    float* ts = U.ts + bs * KH * H;                 // [K][H]: trunk output of step s + 1
+    unsigned long long* st_r = nullptr;
+    unsigned long long* st_d = nullptr;
+#ifdef MZ_STAMPS
+    if (U.stamps && blockIdx.x == 0) { st_r = U.stamps; st_d = U.stamps + 512; }
+#endif
     rn_fill_ktabs(Rr, lds, NG, U.W, U.P);
     {
         const float* x = U.obs + bs * U.obs_feat;
         rn_stage(lds + Rr.in_off, NG, Rr.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
     }
     __syncthreads();
-    rn_run<true>(Rr, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                     // :347
+    rn_run<true, true>(Rr, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, st_r);         // :347
     if (ok) rn_unstage(lds + Rr.out0_off, NG, H, t, [&](int f, float v) { hs[f] = v; });
     if (ok && t.f0 == 0) U.pr[bs * K1] = 0.0f;                                 // :352 zeros
     for (int s = 1; s <= K; ++s) {
@@ -811,40 +927,46 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrol
             rn_stage(lds + Rd.in_off, NG, Rd.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? hp[f] * 2.0f : av; });
         }
         __syncthreads();
-        rn_run<true>(Rd, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                 // :362
+        rn_run<true, true>(Rd, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, s == 1 ? st_d : nullptr, 0, split);  // :362
         if (ok) {
             if (s < K) rn_unstage(lds + Rd.out0_off, NG, H, t, [&](int f, float v) { hs[(size_t)s * H + f] = v; });
-            if (t.f0 == 0) U.pr[bs * K1 + s] = lds[Rd.out1_off + t.g];
+            rn_unstage(lds + trunk, NG, H, t, [&](int f, float v) { ts[(size_t)(s - 1) * H + f] = v; });
         }
     }
 }
 
-// prediction(h_s) for items i = b·KH + s (KH = max(K, 1)): step s + 1's value
-// and policy, and step 0's too for s = 0 (Q10: :351 and :356 at i = 1 both
-// predict from h_0)
+// blockIdx.y = 0: prediction(h_s) for items i = b·KH + s (KH = max(K, 1)):
+// step s + 1's value and policy, and step 0's too for s = 0 (Q10: :351 and
+// :356 at i = 1 both predict from h_0).  y = 1: the dynamics reward head on
+// the trunk output of step s + 1 (items b·K + s): r_{s+1}.
 extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred(RUnrollParams U) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const RPlan& Rp = U.plans[MZ_NET_PRED];
+    const bool rew = blockIdx.y == 1;
+    const RPlan& R = U.plans[rew ? MZ_NET_DYN : MZ_NET_PRED];
     const int NG = U.ng, H = U.H, A = U.A, K = U.K, K1 = K + 1, KH = K > 0 ? K : 1;
     const int n_items = U.B * KH, t0 = blockIdx.x * NG;
+    const int i0 = rew ? U.dyn_split : 0;
     const RnLane t = rn_lane(NG);
     const int it = t0 + t.g;
     const bool ok = it < n_items;
     const size_t ic = (size_t)(ok ? it : 0);
-    rn_fill_ktabs(Rp, lds, NG, U.W, U.P);
+    rn_fill_ktabs(R, lds, NG, U.W, U.P);
     {
-        const float* x = U.hs + ic * H;
-        rn_stage(lds + Rp.in_off, NG, H, t, [&](int f) { return ok ? x[f] : 0.0f; });
+        const float* x = (rew ? U.ts : U.hs) + ic * H;
+        rn_stage(lds + (rew ? R.L[i0].in_off : R.in_off), NG, H, t, [&](int f) { return ok ? x[f] : 0.0f; });
     }
     __syncthreads();
-    rn_run(Rp, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                     // :351 / :356
-    if (ok) {
-        const size_t b = ic / KH;
-        const int s = (int)(ic - b * KH);
-        for (int j = s == 0 ? 0 : s + 1; j <= (s + 1 <= K ? s + 1 : 0); ++j) {
-            if (t.f0 == 0) U.pv[b * K1 + j] = lds[Rp.out0_off + t.g];
-            float* o = U.pp + (b * K1 + j) * A;
-            rn_unstage(lds + Rp.out1_off, NG, A, t, [&](int f, float v) { o[f] = v; });
-        }
+    rn_run<false, true>(R, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, nullptr, i0);   // :351 / :356, :362
+    if (!ok) return;
+    const size_t b = ic / KH;
+    const int s = (int)(ic - b * KH);
+    if (rew) {
+        if (t.f0 == 0) U.pr[b * K1 + s + 1] = lds[R.out1_off + t.g];
+        return;
+    }
+    for (int j = s == 0 ? 0 : s + 1; j <= (s + 1 <= K ? s + 1 : 0); ++j) {
+        if (t.f0 == 0) U.pv[b * K1 + j] = lds[R.out0_off + t.g];
+        float* o = U.pp + (b * K1 + j) * A;
+        rn_unstage(lds + R.out1_off, NG, A, t, [&](int f, float v) { o[f] = v; });
     }
 }

@@ -117,6 +117,9 @@ struct RUnrollParams {
     // sequential part) on tiles of ng_l samples with plans_l, then
     // mz_runroll_pred (the K predictions, independent) on tiles of ng items
     const RPlan* plans_l; int ng_l;
+    int dyn_split;                     // first reward-head layer of the dynamics plans
+    float* ts;                         // [B][K][H] dynamics trunk outputs (split form: the reward heads' input)
+    unsigned long long* stamps;        // -DMZ_STAMPS builds: per-layer ticks of chain block 0 (repr, dyn s = 1)
 };
 
 // Downsampler of the ResNet representation (ResNetHP.downsample,
