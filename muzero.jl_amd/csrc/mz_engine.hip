@@ -44,6 +44,7 @@ extern "C" __global__ void mz_bp_tile(BpParams Q);
 extern "C" __global__ void mz_bp_dw(BpDwParams Q);
 extern "C" __global__ void mz_bp_fold(BpFoldParams Q);
 extern "C" __global__ void mz_runroll_pred(RUnrollParams U);
+extern "C" __global__ void mz_runroll_pred_n(RUnrollParams U);
 extern "C" __global__ void mz_sp_prepare(SpParams S);
 extern "C" __global__ void mz_sp_commit(SpParams S);
 extern "C" __global__ void mz_sp_order(SpParams S);
@@ -151,6 +152,8 @@ struct mz_handle {
     float* d_rhs = nullptr;                 // [bcap][K][H] learner unroll scratch (h between the nets)
     float* d_rts = nullptr;                 // [bcap][K][H] dynamics trunk outputs (the reward heads' input)
     int rn_dyn_split = 0;                   // first reward-head layer of the dynamics plan
+    std::vector<int> rtab;                  // offset tables of the narrow (chain) plans
+    int* d_rtab = nullptr;
     int device = 0, max_games = 0;
     uint64_t seed = 0;
     std::string err;
@@ -780,8 +783,35 @@ static std::vector<RSpec> rn_specs(const mz_config& c, const mz_resnet_hp& hp, i
 // block B0 -> B1 -> B0 (residual in place); head 1 reads B0 (the dynamics
 // state head runs its tower in B2 / B1, B2 aliasing the dead input X); head 2
 // reads B0 through the small buffers S0..S2; outputs O0 / O1.
+// Offset table of a narrow plan's layer L with a kernel > 1x1 (MODE 4 of
+// rn_layer_t): for quarter q, chunk c, column n < ncols_t and bank slot
+// sl = ((n >> 2) & 3) ^ σ(kl), the byte addresses of B(k, n), k = (q·nq + 4c +
+// jj)·4 + kl, jj = 0..3 — the same operand MODE 2 gathers through the k table —
+// or of the zero float for taps off the board, padded steps and columns past
+// the tile.  One 16-byte read gives a lane a chunk's four addresses.
+static void rn_otab_fill(std::vector<int>& t, const RLayer& L, int NG, int W, int P, int ncols_t, int zero_off) {
+    static const int sinv[4] = {0, 2, 3, 1};                      // σ^-1, σ = (0, 3, 1, 2)
+    const int nch = ((L.nq + 3) & ~3) / 4;
+    for (int q = 0; q < 4; ++q)
+        for (int c = 0; c < nch; ++c)
+            for (int n = 0; n < ncols_t; ++n)
+                for (int sl = 0; sl < 4; ++sl)
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const int kl = sinv[sl ^ ((n >> 2) & 3)], j = 4 * c + jj, k = (q * L.nq + j) * 4 + kl;
+                        int a = zero_off;
+                        if (j < L.nq && k < L.K && n < P * NG) {
+                            const int ci = k / L.kk, r = k - ci * L.kk, jy = r / L.kw, ix = r - jy * L.kw;
+                            const int dx = (L.kw - 1 - ix) - L.pw, dy = (L.kh - 1 - jy) - L.ph;
+                            const int p = n / NG, g = n - p * NG, px = p % W + dx, py = p / W + dy;
+                            if (px >= 0 && px < W && py >= 0 && py < P / W)
+                                a = L.in_off + ci * P * NG + (px + W * py) * NG + g;
+                        }
+                        t.push_back(a * 4);
+                    }
+}
+
 static RPlan rn_plan(const mz_handle* h, const std::vector<RSpec>& sp, int net, int NG, size_t flat_off,
-                     int& w_img, std::vector<int>* srcw) {
+                     int& w_img, std::vector<int>* srcw, bool sep_b2 = false, std::vector<int>* otab = nullptr) {
     const mz_config& c = h->rconf;
     const int W = c.observation_shape[0], Hh = c.observation_shape[1], P = W * Hh;
     const int nf = h->rhp.num_filters, hs = h->rhp.width_hidden;
@@ -791,9 +821,11 @@ static RPlan rn_plan(const mz_handle* h, const std::vector<RSpec>& sp, int net, 
     auto region = [&](int n) { int o = off; off += (n + 3) / 4 * 4; return o; };
     RPlan R;
     std::memset(&R, 0, sizeof(R));
-    const int X = region(std::max(in_feat * NG, net == MZ_NET_DYN ? big : 0));
+    // the dynamics state head's B2 aliases the dead input X, or (sep_b2, when the
+    // LDS allows) has its own region, so that its layout can be k-blocked
+    const int X = region(std::max(in_feat * NG, net == MZ_NET_DYN && !sep_b2 ? big : 0));
     const int B0 = region(big), B1 = region(big);
-    const int B2 = X;                                                // dynamics state head (X is dead by then)
+    const int B2 = net == MZ_NET_DYN && sep_b2 ? region(big) : X;
     int headc = 0;
     for (const RSpec& r : sp) if (r.chain && r.conv && r.cout != nf) headc = std::max(headc, r.cout * P * NG);
     const int S0 = region(std::max(headc, hs * NG)), S1 = region(hs * NG), S2 = region(hs * NG);
@@ -849,12 +881,73 @@ static RPlan rn_plan(const mz_handle* h, const std::vector<RSpec>& sp, int net, 
                             if (srcw) srcw->push_back(src);
                         }
         w_img += L.n_ob * 4 * nq4 * 64;
-        if (L.kk > 1) L.ktab = region(L.K);
+        // epilogue image: per output row o, {bias, γ, β, 0} (a lane's four rows
+        // are four 16-byte loads; ADAM scatters into it through the same inverse map)
+        L.ep_img = w_img;
+        for (int o = 0; o < L.n_ob * 16; ++o) {
+            const bool in = o < r.cout;
+            const int e[4] = {in ? (int)(flat_off + r.boff + o) : -1,
+                              in && r.bn ? (int)(flat_off + r.bnoff + r.cout + o) : -1,
+                              in && r.bn ? (int)(flat_off + r.bnoff + o) : -1, -1};
+            if (srcw) for (int x = 0; x < 4; ++x) srcw->push_back(e[x]);
+        }
+        w_img += L.n_ob * 16 * 4;
+        if (L.kk > 1 && !otab) L.ktab = region(L.K);
+    }
+    // layouts, per LDS region: k-blocked when every layer that reads the region
+    // as its B operand is a 1x1 conv / Dense with K % 64 == 0 (a region's
+    // layout never changes, so in-place residual blocks and aliased regions
+    // stay consistent); the final outputs are checked plain below
+    auto capable = [&](const RLayer& L) { return L.kk == 1 && L.K % 64 == 0; };
+    auto kb = [&](int off) {
+        bool any = false, all = true;
+        for (int j = 0; j < R.n; ++j)
+            if (R.L[j].in_off == off) { any = true; all &= capable(R.L[j]); }
+        return (int)(any && all);
+    };
+    R.in_kb = kb(X);
+    for (int j = 0; j < R.n; ++j) {
+        R.L[j].in_kb = kb(R.L[j].in_off);
+        R.L[j].out_kb = kb(R.L[j].out_off);
+        R.L[j].res_kb = R.L[j].res_add ? kb(R.L[j].res_off) : 0;
     }
     if (net == MZ_NET_REPR) { R.out0_off = B0; R.out0_n = h->H; R.out1_n = 0; }
     else if (net == MZ_NET_PRED) { R.out0_off = O0; R.out0_n = 1; R.out1_off = O1; R.out1_n = h->A; }
     else { R.out0_off = B2; R.out0_n = h->H; R.out1_off = O1; R.out1_n = 1; }
+    if (otab) {   // narrow plans: offset tables for the kernels > 1x1 (shared by layers of the same input / shape)
+        const int n_nb = (P * NG + 15) >> 4, nbw = n_nb == 1 ? 1 : n_nb == 2 ? 2 : 3;
+        const int ncols_t = (n_nb + nbw - 1) / nbw * nbw * 16;
+        const int zero = region(4);
+        std::vector<int> t;
+        std::vector<std::pair<std::vector<int>, int>> seen;      // (in_off, K, kw, kh) -> table offset in t
+        for (int i = 0; i < R.n; ++i) {
+            RLayer& L = R.L[i];
+            if (L.kk == 1) continue;
+            const std::vector<int> key = {L.in_off, L.K, L.kw, L.kh};
+            int at = -1;
+            for (auto& e : seen) if (e.first == key) at = e.second;
+            if (at < 0) { at = (int)t.size(); seen.push_back({key, at}); rn_otab_fill(t, L, NG, W, P, ncols_t, zero); }
+            L.ktab = at;                                           // relative until the region is placed
+            L.otab = 1;
+        }
+        if (!t.empty() && (size_t)(off + t.size() + 16 * 16 * 4) * 4 <= kLdsMax) {
+            R.tab_lds = region((int)t.size());
+            R.tab_n = (int)t.size();
+            R.tab_src = (int)otab->size();
+            R.zero_off = zero;
+            otab->insert(otab->end(), t.begin(), t.end());
+            for (int i = 0; i < R.n; ++i) if (R.L[i].otab) R.L[i].ktab += R.tab_lds;
+        } else {                                                   // does not fit: the k-table gather (MODE 2)
+            for (int i = 0; i < R.n; ++i) if (R.L[i].otab) { R.L[i].otab = 0; R.L[i].ktab = -1; }
+        }
+        for (int i = 0; i < R.n; ++i)                              // k tables for the layers that still need one
+            if (R.L[i].kk > 1 && !R.L[i].otab && R.L[i].ktab < 0) R.L[i].ktab = region(R.L[i].K);
+    }
+    region(16 * 16 * 4);           // slack: past-the-tile lanes of k-blocked reads (MODE 3) read up to 15 columns on
     R.lds_floats = off;
+    R.out0_kb = kb(R.out0_off);
+    for (int j = 0; j < R.n; ++j) R.k[j] = rn_rk_pack(R.L[j]);
+    if ((R.out0_kb && net == MZ_NET_PRED) || (R.out1_n && kb(R.out1_off))) R.n = -1;   // (never: read as plain)
     return R;
 }
 
@@ -1053,7 +1146,12 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
     int wi = 0;
     h->rplan.resize(3);
     for (int n = 0; n < 3; ++n) {
-        h->rplan[n] = rn_plan(h, sp[n], n, h->rn_ng, h->flat_off[n] + (n == 0 ? h->ds_n : 0), wi, &sw);
+        {
+            int wt = wi;
+            const bool sep = (size_t)rn_plan(h, sp[n], n, h->rn_ng, 0, wt, nullptr, true).lds_floats * 4 <= kLdsMax;
+            h->rplan[n] = rn_plan(h, sp[n], n, h->rn_ng, h->flat_off[n] + (n == 0 ? h->ds_n : 0), wi, &sw, sep);
+        }
+        CK(h->rplan[n].n < 0 ? fail(h, "ResNet plan: a k-blocked output buffer") : 0);
         h->rn_lds[n] = (size_t)h->rplan[n].lds_floats * 4;
     }
     h->packed_w_n = sw.size(); h->packed_b_n = 0;
@@ -1068,7 +1166,11 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
         int wl = 0;
         h->rplan_l.resize(3);
         for (int n = 0; n < 3; ++n) {
-            h->rplan_l[n] = rn_plan(h, sp[n], n, ngl, h->flat_off[n] + (n == 0 ? h->ds_n : 0), wl, nullptr);
+            int wt = wl;
+            const bool sep = (size_t)rn_plan(h, sp[n], n, ngl, 0, wt, nullptr, true).lds_floats * 4 <= kLdsMax;
+            h->rplan_l[n] = rn_plan(h, sp[n], n, ngl, h->flat_off[n] + (n == 0 ? h->ds_n : 0), wl, nullptr, sep,
+                                    &h->rtab);
+            CK(h->rplan_l[n].n < 0 ? fail(h, "ResNet plan: a k-blocked output buffer") : 0);
             h->rn_lds_l = std::max(h->rn_lds_l, (size_t)h->rplan_l[n].lds_floats * 4);
         }
     }
@@ -1087,6 +1189,7 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
     CK(al(&h->d_rplan, 3));
     CK(hipMemcpy(h->d_rplan, h->rplan.data(), 3 * sizeof(RPlan), hipMemcpyHostToDevice) == hipSuccess
            ? 0 : fail(h, "copy"));
+    if (!h->rtab.empty()) CK(al_i(&h->d_rtab, h->rtab));
     CK(al(&h->d_rplan_l, 3));
     CK(hipMemcpy(h->d_rplan_l, h->rplan_l.data(), 3 * sizeof(RPlan), hipMemcpyHostToDevice) == hipSuccess
            ? 0 : fail(h, "copy"));
@@ -1118,6 +1221,8 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
                            (int)lmax) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll)"));
     CK(hipFuncSetAttribute((const void*)mz_runroll_pred, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)lmax) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_pred)"));
+    CK(hipFuncSetAttribute((const void*)mz_runroll_pred_n, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)h->rn_lds_l) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_pred_n)"));
     CK(hipFuncSetAttribute((const void*)mz_runroll_chain, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)h->rn_lds_l) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_chain)"));
     CK(hipFuncSetAttribute((const void*)mz_rsearch_nets, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1679,7 +1784,7 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
     } U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
     U.hs = h->d_rhs; U.plans = h->d_rplan; U.Wimg = h->d_Wp; U.flat = h->d_flat;
     U.plans_l = h->d_rplan_l; U.ng_l = h->rn_ng_l;
-    U.dyn_split = h->rn_dyn_split; U.ts = h->d_rts;
+    U.dyn_split = h->rn_dyn_split; U.ts = h->d_rts; U.otab = h->d_rtab;
     U.stamps = nullptr;
 #ifdef MZ_STAMPS
     if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * std::max(h->max_games, 128)));
@@ -1698,9 +1803,15 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
         const int KH = std::max(U.K, 1);
         MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_chain, dim3((B + U.ng_l - 1) / U.ng_l), dim3(RN_THREADS),
                                   args, h->rn_lds_l, st));
-        MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred, dim3((B * KH + U.ng - 1) / U.ng, U.K > 0 ? 2 : 1),
-                                  dim3(RN_THREADS),
-                                  args, runroll_lds(h), st));
+        // the B·K predictions and reward heads: narrow tiles unless MZ_RN_PRED_WIDE
+        static const bool wide = std::getenv("MZ_RN_PRED_WIDE") != nullptr;
+        if (wide)
+            MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred, dim3((B * KH + U.ng - 1) / U.ng, U.K > 0 ? 2 : 1),
+                                      dim3(RN_THREADS), args, runroll_lds(h), st));
+        else
+            MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred_n,
+                                      dim3((B * KH + U.ng_l - 1) / U.ng_l, U.K > 0 ? 2 : 1), dim3(RN_THREADS), args,
+                                      h->rn_lds_l, st));
     }
     if (e1) MZ_TRY(h, hipEventRecord(e1, st));
     return learner_losses(h, b, grad_dev, losses_dev, st, MZ_ACT_IDENTITY, MZ_ACT_IDENTITY, fuse_adam, eta);

@@ -44,21 +44,54 @@ __device__ __forceinline__ void rn_load_a(float (&a)[4][4], const float* __restr
 // wave-uniform branch divides.
 // bias, γ, β of the 4 rows a lane holds in row block ob (issued before the
 // MFMAs of the unit so their latency hides under them)
-__device__ __forceinline__ void rn_load_ep(float (&ep)[3][4], const RLayer& L, const float* __restrict__ flat, int ob,
-                                           int kl) {
+// (from the layer's epilogue image: four 16-byte loads; rows past cout and the
+// BatchNorm entries of layers without one read 0)
+__device__ __forceinline__ void rn_load_ep(float (&ep)[3][4], const RLayer& L, const float* __restrict__ Wimg,
+                                           int ob, int kl) {
+    const float4* e = reinterpret_cast<const float4*>(Wimg + L.ep_img) + ob * 16 + kl * 4;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const int o = ob * 16 + kl * 4 + r, oc = o < L.cout ? o : L.cout - 1;
-        ep[0][r] = flat[L.boff + oc];
-        ep[1][r] = L.bn ? flat[L.bnoff + L.cout + oc] : 0.0f;
-        ep[2][r] = L.bn ? flat[L.bnoff + oc] : 0.0f;
+        const float4 v = e[r];
+        ep[0][r] = v.x; ep[1][r] = v.y; ep[2][r] = v.z;
     }
+}
+// A layer's packed entry by scalar load (constant address space: the plans
+// are never written by the kernels)
+__device__ __forceinline__ RLayer rn_layer_at(const RPlan& R, int i) {
+#ifdef __HIP_DEVICE_COMPILE__
+    typedef const __attribute__((address_space(4))) int4* cp4;
+    const cp4 k = (cp4)(&R.k[0]);
+    const int4 a = k[2 * i], b = k[2 * i + 1];
+    const RK x = {{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
+    return rn_rk_decode(x);
+#else
+    return rn_rk_decode(R.k[i]);
+#endif
+}
+
+// LDS index of output row o = ob·16 + kl·4 + r, column n, in layout kb
+__device__ __forceinline__ int rn_out_idx(int kb, int ob, int kl, int r, int n, int ncols) {
+    return kb ? (ob * ncols + n) * 16 + 4 * (((n >> 2) & 3) ^ rn_kb_sigma(r)) + kl   // rn_kb_off(o, n)
+              : (ob * 16 + kl * 4 + r) * ncols + n;
+}
+// the residual operands of a unit, read before its MFMAs (their LDS latency
+// then hides under the chunks); 0 for rows / columns past the layer
+template <int NB>
+__device__ __forceinline__ void rn_load_res(const RLayer& L, const float* lds, float (&res)[NB][4], int ob, int kl,
+                                            const int (&n)[NB], int ncols) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            const bool in = ob * 16 + kl * 4 + r < L.cout && n[i] < ncols;
+            res[i][r] = L.res_add && in ? lds[L.res_off + rn_out_idx(L.res_kb, ob, kl, r, n[i], ncols)] : 0.0f;
+        }
 }
 
 template <int NB>
 __device__ __forceinline__ void rn_epilogue(const RLayer& L, const mz_f32x4 (&acc)[NB][4], const float (&ep)[3][4],
                                             float* lds, int ob, int kl, const int (&n)[NB], int ncols, float bn_s,
-                                            float bn_r) {
+                                            float bn_r, const float (&res)[NB][4]) {
     float d[NB][4];
     bool tiny = false;
 #pragma unroll
@@ -104,8 +137,8 @@ __device__ __forceinline__ void rn_epilogue(const RLayer& L, const mz_f32x4 (&ac
         for (int i = 0; i < NB; ++i) {
             if (n[i] >= ncols) continue;
             float v = d[i][r];
-            if (L.res_add) v = v + lds[L.res_off + o * ncols + n[i]];
-            lds[L.out_off + o * ncols + n[i]] = rn_act(L.act, v);
+            if (L.res_add) v = v + res[i][r];
+            lds[L.out_off + rn_out_idx(L.out_kb, ob, kl, r, n[i], ncols)] = rn_act(L.act, v);
         }
     }
 }
@@ -151,7 +184,8 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
 #define RN_DBG_WAIT(k) do {} while (0)
 #endif
     (void)dbg;
-    const int ncols = MODE == 0 ? NG : P * NG;
+    // MODE 3: a 1x1 conv / Dense reading a k-blocked input (K % 64 == 0)
+    const int ncols = MODE == 0 ? NG : MODE == 3 ? (L.spatial ? P * NG : NG) : P * NG;
     const int n_nb = (ncols + 15) >> 4;
     const int n_grp = (n_nb + NBW - 1) / NBW;
     const int units = L.n_ob * n_grp;
@@ -179,7 +213,7 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
 #pragma unroll
                 for (int r = 0; r < 4; ++r) ep[e][r] = pf->ep[e][r];
         } else {
-            rn_load_ep(ep, L, flat, ob, kl);
+            rn_load_ep(ep, L, Wimg, ob, kl);
         }
         int cb[NBW], cw[NBW], chh[NBW];
 #pragma unroll
@@ -195,6 +229,9 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
         // MODE 0/1: byte address of row q·NQ·4 + kl at each column block; the
         // k-step adds a wave-uniform j·4·ncols; kq[q] = rows of quarter q left
         // for this lane (k < K)
+        // MODE 3: byte address of this lane's 16-byte piece of chunk 0 of quarter
+        // q (the four k-steps (q·NQ + 4c + jj)·4 + kl, jj = 0..3; chunk c adds
+        // a wave-uniform c·ncols·64 bytes)
         uint32_t bq[4][NBW];
         int kq[4];
 #pragma unroll
@@ -208,7 +245,97 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
         for (int i = 0; i < NBW; ++i)
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[i][q] = mz_f32x4{0.f, 0.f, 0.f, 0.f};
+        int nn[NBW];
+#pragma unroll
+        for (int i = 0; i < NBW; ++i) nn[i] = (grp * NBW + i) * 16 + (lane & 15);
+        // one-column-block units (the learner chain's) read their residual
+        // operands up front; wider units in the epilogue (register budget of the
+        // 12-wave network kernel)
+        float res[NBW][4];
+        if constexpr (NBW == 1) rn_load_res<NBW>(L, lds, res, ob, kl, nn, ncols);
         RN_DBG_WAIT(1);                                 // operands of the first chunk in registers
+        if constexpr (MODE == 4) {
+            // offset table (narrow plans): per quarter one 16-byte read of the
+            // chunk's four B addresses, then the four B reads; no address VALU
+            const int nch4 = ((NQ + 3) & ~3) / 4, ncols_t = n_grp * NBW * 16;
+            const int n0 = grp * NBW * 16 + (lane & 15);
+            const int* tb = reinterpret_cast<const int*>(lds) + L.ktab + n0 * 16 +
+                            4 * (((n0 >> 2) & 3) ^ rn_kb_sigma(kl));
+            constexpr int QG = NBW == 1 ? 4 : 2;
+            for (int c = 0; c < nch4; ++c) {
+                float ac[4][4];                         // this chunk's A; the next one's loads fly under it
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) ac[q][jj] = an[q][jj];
+                {
+                    const int un = c + 1 < nch4 ? u : u + nwaves, cn = c + 1 < nch4 ? c + 1 : 0;
+                    if (un < units) rn_load_a(an, Wimg, L, un / n_grp, cn, lane);
+                }
+#pragma unroll
+                for (int qp = 0; qp < 4; qp += QG) {
+                    int4 o[QG][NBW];
+#pragma unroll
+                    for (int h = 0; h < QG; ++h)
+#pragma unroll
+                        for (int i = 0; i < NBW; ++i)
+                            o[h][i] = *reinterpret_cast<const int4*>(tb + ((qp + h) * nch4 + c) * ncols_t * 16 + 256 * i);
+                    float bv[QG][NBW][4];
+#pragma unroll
+                    for (int h = 0; h < QG; ++h)
+#pragma unroll
+                        for (int i = 0; i < NBW; ++i) {
+                            const char* lb = reinterpret_cast<const char*>(lds);
+                            bv[h][i][0] = *reinterpret_cast<const float*>(lb + o[h][i].x);
+                            bv[h][i][1] = *reinterpret_cast<const float*>(lb + o[h][i].y);
+                            bv[h][i][2] = *reinterpret_cast<const float*>(lb + o[h][i].z);
+                            bv[h][i][3] = *reinterpret_cast<const float*>(lb + o[h][i].w);
+                        }
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+                        for (int h = 0; h < QG; ++h)
+#pragma unroll
+                            for (int i = 0; i < NBW; ++i)
+                                acc[i][qp + h] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[qp + h][jj], bv[h][i][jj],
+                                                                                      acc[i][qp + h], 0, 0, 0);
+                }
+            }
+        } else if constexpr (MODE == 3) {
+            // k-blocked input: per quarter one 16-byte LDS read per column block
+            // (unclamped columns: past-the-tile lanes read spare LDS, their
+            // results are discarded); A used in place, the next chunk's fetched
+            // after this chunk's MFMAs (1x1 convs over 64 channels have one)
+            const int n0 = grp * NBW * 16 + (lane & 15);
+            const uint32_t b0 = (uint32_t)(L.in_off + n0 * 16 + 4 * (((n0 >> 2) & 3) ^ rn_kb_sigma(kl))) * 4u;
+            for (int c = 0; c < nch; ++c) {
+                constexpr int QG = NBW == 1 ? 4 : 2;
+#pragma unroll
+                for (int qp = 0; qp < 4; qp += QG) {
+                    float4 v[QG][NBW];
+#pragma unroll
+                    for (int h = 0; h < QG; ++h) {
+                        const char* base = reinterpret_cast<const char*>(lds) + b0 +
+                                           (uint32_t)(((qp + h) * NQ / 4 + c) * ncols) * 64u;
+#pragma unroll
+                        for (int i = 0; i < NBW; ++i) v[h][i] = *reinterpret_cast<const float4*>(base + 1024 * i);
+                    }
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+                        for (int h = 0; h < QG; ++h)
+#pragma unroll
+                            for (int i = 0; i < NBW; ++i) {
+                                const float bv = jj == 0 ? v[h][i].x : jj == 1 ? v[h][i].y : jj == 2 ? v[h][i].z
+                                                                                                    : v[h][i].w;
+                                acc[i][qp + h] = __builtin_amdgcn_mfma_f32_16x16x4f32(an[qp + h][jj], bv,
+                                                                                      acc[i][qp + h], 0, 0, 0);
+                            }
+                }
+                const int un = c + 1 < nch ? u : u + nwaves, cn = c + 1 < nch ? c + 1 : 0;
+                if (un < units) rn_load_a(an, Wimg, L, un / n_grp, cn, lane);
+            }
+        } else
         for (int c = 0; c < nch; ++c) {
             float ac[4][4];
 #pragma unroll
@@ -267,10 +394,8 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
         }
 #endif
         RN_DBG_WAIT(2);                                 // chunks done (MFMA results consumed)
-        int nn[NBW];
-#pragma unroll
-        for (int i = 0; i < NBW; ++i) nn[i] = (grp * NBW + i) * 16 + (lane & 15);
-        rn_epilogue<NBW>(L, acc, ep, lds, ob, kl, nn, ncols, bn_s, bn_r);
+        if constexpr (NBW != 1) rn_load_res<NBW>(L, lds, res, ob, kl, nn, ncols);
+        rn_epilogue<NBW>(L, acc, ep, lds, ob, kl, nn, ncols, bn_s, bn_r, res);
         RN_DBG_WAIT(3);                                 // epilogue stored
     }
 }
@@ -295,7 +420,16 @@ __device__ __forceinline__ void rn_layer(const RLayer& L, const float* __restric
                                          float bn_s, float bn_r, const RnPf* pf = nullptr,
                                          unsigned long long* dbg = nullptr) {
     const int n_nb = NARROW && L.spatial ? (P * NG + 15) >> 4 : 3;     // as rn_nbw
-    if (L.kk > 1) {
+    if (NARROW && L.otab) {                                           // kernel > 1x1 through the offset table
+        if (n_nb == 1) rn_layer_t<1, 4, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+        else if (n_nb == 2) rn_layer_t<2, 4, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+        else rn_layer_t<3, 4, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+    } else if (L.in_kb) {                                             // 1x1 conv / Dense, K % 64 == 0
+        if (!L.spatial) rn_layer_t<1, 3, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+        else if (n_nb == 1) rn_layer_t<1, 3, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+        else if (n_nb == 2) rn_layer_t<2, 3, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+        else rn_layer_t<RN_NBW, 3, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+    } else if (L.kk > 1) {
         if (n_nb == 1) rn_layer_t<1, 2, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
         else if (n_nb == 2) rn_layer_t<2, 2, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
         else rn_layer_t<3, 2, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
@@ -319,7 +453,7 @@ __device__ __forceinline__ void rn_prefetch(const RLayer& L, const float* __rest
     if (wave < L.n_ob * n_grp) {
         const int ob = wave / n_grp;
         rn_load_a(pf.an, Wimg, L, ob, 0, lane);
-        rn_load_ep(pf.ep, L, flat, ob, lane >> 4);
+        rn_load_ep(pf.ep, L, Wimg, ob, lane >> 4);
     }
 }
 
@@ -327,7 +461,7 @@ __device__ __forceinline__ void rn_prefetch(const RLayer& L, const float* __rest
 __device__ void rn_fill_ktabs(const RPlan& R, float* lds, int NG, int Wb, int P) {
     for (int i = 0; i < R.n; ++i) {
         const RLayer& L = R.L[i];
-        if (L.kk == 1) continue;
+        if (L.kk == 1 || L.otab) continue;
         int* tab = reinterpret_cast<int*>(lds) + L.ktab;
         for (int k = threadIdx.x; k < L.K; k += blockDim.x) {
             const int c = k / L.kk, r = k - c * L.kk, j = r / L.kw, ii = r - j * L.kw;
@@ -357,11 +491,11 @@ __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const 
     if constexpr (PF) {
         if (i0 >= i1) return;
         RnPf pf;
-        RLayer L = R.L[i0];
+        RLayer L = rn_layer_at(R, i0);
         rn_prefetch<NARROW>(L, Wimg, flat, NG, P, pf);
         for (int i = i0; i < i1; ++i) {
             RLayer Ln;
-            if (i + 1 < i1) Ln = R.L[i + 1];
+            if (i + 1 < i1) Ln = rn_layer_at(R, i + 1);
             unsigned long long* dbg = nullptr;
 #ifdef MZ_STAMPS
             if (st && i - i0 < 31) dbg = st + 1024 + 8 * (i - i0);
@@ -379,7 +513,7 @@ __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const 
         }
     } else {
         for (int i = i0; i < i1; ++i) {
-            rn_layer<NARROW>(R.L[i], Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+            rn_layer<NARROW>(rn_layer_at(R, i), Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
 #ifdef MZ_STAMPS
             if (st && (threadIdx.x & 63) == 0 && i - i0 < 31) st[wv * 64 + 2 * (i - i0)] = __builtin_amdgcn_s_memtime();
 #endif
@@ -414,6 +548,25 @@ __device__ __forceinline__ void rn_unstage(const float* src, int NG, int n, cons
 #pragma unroll 6
     for (int f = t.f0; f < n; f += t.fs) put(f, src[f * NG + t.g]);
 }
+// The same for a buffer that conv layers read (feature f = p + P·c is row c,
+// column p·NG + g), plain or k-blocked (mz_resnet_params.h)
+__device__ __forceinline__ int rn_conv_idx(int kb, int f, int g, int NG, int P) {
+    if (!kb) return f * NG + g;
+    const int c = f / P, p = f - c * P;
+    return rn_kb_off(c, p * NG + g, P * NG);
+}
+template <class Fn>
+__device__ __forceinline__ void rn_stage_l(float* dst, int kb, int NG, int P, int n, const RnLane& t, Fn val) {
+    if (!kb) { rn_stage(dst, NG, n, t, val); return; }
+#pragma unroll 4
+    for (int f = t.f0; f < n; f += t.fs) dst[rn_conv_idx(1, f, t.g, NG, P)] = val(f);
+}
+template <class Fn>
+__device__ __forceinline__ void rn_unstage_l(const float* src, int kb, int NG, int P, int n, const RnLane& t, Fn put) {
+    if (!kb) { rn_unstage(src, NG, n, t, put); return; }
+#pragma unroll 4
+    for (int f = t.f0; f < n; f += t.fs) put(f, src[rn_conv_idx(1, f, t.g, NG, P)]);
+}
 
 // Batched forward of one net (mz_net_forward): x (in_feat, n) -> out0, out1.
 extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_rnet_forward_kernel(RNetParams Q) {
@@ -425,13 +578,13 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_rnet_forward_kernel(
     const bool ok = t0 + t.g < Q.n_items;
     {
         const float* x = Q.x + (size_t)(ok ? t0 + t.g : 0) * R.in_feat;
-        rn_stage(lds + R.in_off, NG, R.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
+        rn_stage_l(lds + R.in_off, R.in_kb, NG, Q.P, R.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
     }
     __syncthreads();
     rn_run(R, Q.Wimg, Q.flat, lds, NG, Q.W, Q.P, Q.bn_s);
     if (ok) {
         float* o = Q.out0 + (size_t)(t0 + t.g) * R.out0_n;
-        rn_unstage(lds + R.out0_off, NG, R.out0_n, t, [&](int f, float v) { o[f] = v; });
+        rn_unstage_l(lds + R.out0_off, R.out0_kb, NG, Q.P, R.out0_n, t, [&](int f, float v) { o[f] = v; });
     }
     if (R.out1_n && Q.out1) {
         const int g = threadIdx.x;
@@ -476,14 +629,14 @@ __device__ __forceinline__ void rsearch_root_body(const RSearchParams& P) {
     const bool ok = t0 + t.g < P.G;
     {
         const float* x = P.obs + (size_t)(ok ? t0 + t.g : 0) * P.obs_feat;
-        rn_stage(lds + Rr.in_off, NG, Rr.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
+        rn_stage_l(lds + Rr.in_off, Rr.in_kb, NG, P.P, Rr.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
     }
     __syncthreads();
     rn_run(Rr, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s);                    // :234
     float* h0 = P.hid + (size_t)(ok ? t0 + t.g : 0) * (P.S + 1) * H;
-    if (ok) rn_unstage(lds + Rr.out0_off, NG, H, t, [&](int f, float v) { h0[f] = v; });
+    if (ok) rn_unstage_l(lds + Rr.out0_off, Rr.out0_kb, NG, P.P, H, t, [&](int f, float v) { h0[f] = v; });
     __syncthreads();
-    rn_stage(lds + Rp.in_off, NG, H, t, [&](int f) { return ok ? h0[f] : 0.0f; });   // prediction input = h0
+    rn_stage_l(lds + Rp.in_off, Rp.in_kb, NG, P.P, H, t, [&](int f) { return ok ? h0[f] : 0.0f; });   // prediction input = h0
     __syncthreads();
     rn_run(Rp, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s);                    // :239
     const int gl = threadIdx.x / GW, a = threadIdx.x % GW, gg = t0 + gl;
@@ -798,12 +951,12 @@ extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RS
     const bool ok = gg < P.G;
     if (net == MZ_NET_PRED) {
         const float* x = P.x_pred + (size_t)(ok ? gg : 0) * H;
-        rn_stage(lds + R.in_off, NG, H, t, [&](int f) { return ok ? x[f] : 0.0f; });
+        rn_stage_l(lds + R.in_off, R.in_kb, NG, P.P, H, t, [&](int f) { return ok ? x[f] : 0.0f; });
     } else {
         const int* st = P.gst + (size_t)(ok ? gg : 0) * RG_INTS;
         const float* x = P.hid + ((size_t)(ok ? gg : 0) * (S + 1) + st[RG_LEAF_E]) * H;
         const float av = P.aval_tab[st[RG_LEAF_A]];
-        rn_stage(lds + R.in_off, NG, R.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? x[f] : av; });
+        rn_stage_l(lds + R.in_off, R.in_kb, NG, P.P, R.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? x[f] : av; });
     }
     __syncthreads();
     rn_run(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st);
@@ -817,7 +970,7 @@ extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RS
         rn_unstage(lds + R.out1_off, NG, P.A, t, [&](int f, float v) { o[f] = v; });
     } else {
         float* o = P.hid + ((size_t)gg * (S + 1) + P.s + 1) * H;
-        rn_unstage(lds + R.out0_off, NG, H, t, [&](int f, float v) { o[f] = v; });
+        rn_unstage_l(lds + R.out0_off, R.out0_kb, NG, P.P, H, t, [&](int f, float v) { o[f] = v; });
         if (t.f0 == 0) P.o_r[gg] = lds[R.out1_off + t.g];
     }
 }
@@ -840,17 +993,17 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_kernel(RUnro
     rn_fill_ktabs(Rr, lds, NG, U.W, U.P);
     {
         const float* x = U.obs + bs * U.obs_feat;
-        rn_stage(lds + Rr.in_off, NG, Rr.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
+        rn_stage_l(lds + Rr.in_off, Rr.in_kb, NG, U.P, Rr.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
     }
     __syncthreads();
     rn_run(Rr, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                     // :347
-    if (ok) rn_unstage(lds + Rr.out0_off, NG, H, t, [&](int f, float v) { hs[f] = v; });
+    if (ok) rn_unstage_l(lds + Rr.out0_off, Rr.out0_kb, NG, U.P, H, t, [&](int f, float v) { hs[f] = v; });
     if (ok && t.f0 == 0) U.pr[bs * K1] = 0.0f;
     const int ns = U.K > 0 ? U.K : 1;              // K = 0: the prediction of h0 alone
     for (int s = 1; s <= ns; ++s) {
         __syncthreads();
         rn_fill_ktabs(Rp, lds, NG, U.W, U.P);
-        rn_stage(lds + Rp.in_off, NG, H, t, [&](int f) { return ok ? hs[f] : 0.0f; });
+        rn_stage_l(lds + Rp.in_off, Rp.in_kb, NG, U.P, H, t, [&](int f) { return ok ? hs[f] : 0.0f; });
         __syncthreads();
         rn_run(Rp, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                 // :351 / :356
         if (ok) {
@@ -866,12 +1019,12 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_kernel(RUnro
         rn_fill_ktabs(Rd, lds, NG, U.W, U.P);
         {                                                                      // make_dynamics_input (:293-304)
             const float av = ok ? U.actions[bs * K1 + (s - 1)] / (float)A : 0.0f;
-            rn_stage(lds + Rd.in_off, NG, Rd.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? hs[f] * 2.0f : av; });
+            rn_stage_l(lds + Rd.in_off, Rd.in_kb, NG, U.P, Rd.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? hs[f] * 2.0f : av; });
         }
         __syncthreads();
         rn_run(Rd, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                 // :362
         if (ok) {
-            rn_unstage(lds + Rd.out0_off, NG, H, t, [&](int f, float v) { hs[f] = v; });
+            rn_unstage_l(lds + Rd.out0_off, Rd.out0_kb, NG, U.P, H, t, [&](int f, float v) { hs[f] = v; });
             if (t.f0 == 0) U.pr[bs * K1 + s] = lds[Rd.out1_off + t.g];
         }
     }
@@ -910,13 +1063,19 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrol
     if (U.stamps && blockIdx.x == 0) { st_r = U.stamps; st_d = U.stamps + 512; }
 #endif
     rn_fill_ktabs(Rr, lds, NG, U.W, U.P);
+    if (Rr.tab_n) {                                 // the representation's offset tables (+ the zero float)
+        const int4* src = reinterpret_cast<const int4*>(U.otab + Rr.tab_src);
+        int4* dst = reinterpret_cast<int4*>(reinterpret_cast<int*>(lds) + Rr.tab_lds);
+        for (int i = threadIdx.x; i < Rr.tab_n / 4; i += blockDim.x) dst[i] = src[i];
+        if (threadIdx.x == 0) lds[Rr.zero_off] = 0.0f;
+    }
     {
         const float* x = U.obs + bs * U.obs_feat;
-        rn_stage(lds + Rr.in_off, NG, Rr.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
+        rn_stage_l(lds + Rr.in_off, Rr.in_kb, NG, U.P, Rr.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
     }
     __syncthreads();
     rn_run<true, true>(Rr, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, st_r);         // :347
-    if (ok) rn_unstage(lds + Rr.out0_off, NG, H, t, [&](int f, float v) { hs[f] = v; });
+    if (ok) rn_unstage_l(lds + Rr.out0_off, Rr.out0_kb, NG, U.P, H, t, [&](int f, float v) { hs[f] = v; });
     if (ok && t.f0 == 0) U.pr[bs * K1] = 0.0f;                                 // :352 zeros
     for (int s = 1; s <= K; ++s) {
         __syncthreads();
@@ -924,13 +1083,14 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrol
         {                                                                      // make_dynamics_input (:293-304)
             const float av = ok ? U.actions[bs * K1 + (s - 1)] / (float)A : 0.0f;
             const float* hp = hs + (size_t)(s - 1) * H;
-            rn_stage(lds + Rd.in_off, NG, Rd.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? hp[f] * 2.0f : av; });
+            rn_stage_l(lds + Rd.in_off, Rd.in_kb, NG, U.P, Rd.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? hp[f] * 2.0f : av; });
         }
         __syncthreads();
         rn_run<true, true>(Rd, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, s == 1 ? st_d : nullptr, 0, split);  // :362
         if (ok) {
-            if (s < K) rn_unstage(lds + Rd.out0_off, NG, H, t, [&](int f, float v) { hs[(size_t)s * H + f] = v; });
-            rn_unstage(lds + trunk, NG, H, t, [&](int f, float v) { ts[(size_t)(s - 1) * H + f] = v; });
+            if (s < K) rn_unstage_l(lds + Rd.out0_off, Rd.out0_kb, NG, U.P, H, t,
+                                    [&](int f, float v) { hs[(size_t)s * H + f] = v; });
+            rn_unstage_l(lds + trunk, Rd.L[split].in_kb, NG, U.P, H, t, [&](int f, float v) { ts[(size_t)(s - 1) * H + f] = v; });
         }
     }
 }
@@ -939,11 +1099,12 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrol
 // step s + 1's value and policy, and step 0's too for s = 0 (Q10: :351 and
 // :356 at i = 1 both predict from h_0).  y = 1: the dynamics reward head on
 // the trunk output of step s + 1 (items b·K + s): r_{s+1}.
-extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred(RUnrollParams U) {
+template <bool NARROW>
+__device__ __forceinline__ void runroll_pred_body(const RUnrollParams& U) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const bool rew = blockIdx.y == 1;
-    const RPlan& R = U.plans[rew ? MZ_NET_DYN : MZ_NET_PRED];
-    const int NG = U.ng, H = U.H, A = U.A, K = U.K, K1 = K + 1, KH = K > 0 ? K : 1;
+    const RPlan& R = (NARROW ? U.plans_l : U.plans)[rew ? MZ_NET_DYN : MZ_NET_PRED];
+    const int NG = NARROW ? U.ng_l : U.ng, H = U.H, A = U.A, K = U.K, K1 = K + 1, KH = K > 0 ? K : 1;
     const int n_items = U.B * KH, t0 = blockIdx.x * NG;
     const int i0 = rew ? U.dyn_split : 0;
     const RnLane t = rn_lane(NG);
@@ -953,10 +1114,11 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred(RUnroll
     rn_fill_ktabs(R, lds, NG, U.W, U.P);
     {
         const float* x = (rew ? U.ts : U.hs) + ic * H;
-        rn_stage(lds + (rew ? R.L[i0].in_off : R.in_off), NG, H, t, [&](int f) { return ok ? x[f] : 0.0f; });
+        rn_stage_l(lds + (rew ? R.L[i0].in_off : R.in_off), rew ? R.L[i0].in_kb : R.in_kb, NG, U.P, H, t,
+                   [&](int f) { return ok ? x[f] : 0.0f; });
     }
     __syncthreads();
-    rn_run<false, true>(R, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, nullptr, i0);   // :351 / :356, :362
+    rn_run<NARROW, true>(R, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, nullptr, i0);   // :351 / :356, :362
     if (!ok) return;
     const size_t b = ic / KH;
     const int s = (int)(ic - b * KH);
@@ -970,3 +1132,7 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred(RUnroll
         rn_unstage(lds + R.out1_off, NG, A, t, [&](int f, float v) { o[f] = v; });
     }
 }
+// wide tiles of ng items (plans), or one item per workgroup on the narrow
+// (chain) plans — B·K workgroups, a short per-layer critical path
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred(RUnrollParams U) { runroll_pred_body<false>(U); }
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred_n(RUnrollParams U) { runroll_pred_body<true>(U); }

@@ -19,6 +19,18 @@
 #define RN_THREADS_NETS 768      // search network launch: 12 waves, 3 per SIMD (one unit of a 64x144 conv each)
 #endif
 
+// Activation buffer layouts.  Plain: x[k][n] at k·ncols + n (k = feature /
+// channel, n = column).  K-blocked (for readers whose MFMA B operands walk k in
+// steps of 4: 1x1 convs and Dense layers with K % 64 == 0): with k = 4m + kl,
+// element (k, n) sits at ((m >> 2)·ncols + n)·16 + 4·(((n >> 2) & 3) ^ σ(kl)) +
+// (m & 3), σ = (0, 3, 1, 2), so the four k-steps 4M..4M+3 a lane (kl = lane >>
+// 4, n = lane & 15) feeds to consecutive MFMAs are one 16-byte LDS read, and the
+// σ swizzle keeps each ds_read_b128 lane group on distinct banks.
+__host__ __device__ __forceinline__ int rn_kb_sigma(int kl) { return (0x2130 >> (4 * kl)) & 3; }
+__host__ __device__ __forceinline__ int rn_kb_off(int k, int n, int ncols) {
+    return ((k >> 4) * ncols + n) * 16 + 4 * (((n >> 2) & 3) ^ rn_kb_sigma(k & 3)) + ((k >> 2) & 3);
+}
+
 struct RLayer {
     int kk;              // kw * kh (1: Dense or 1x1 conv; > 1: im2col gather through the k table)
     int kw, kh, pw, ph;
@@ -30,15 +42,62 @@ struct RLayer {
     int boff, bnoff;     // absolute offsets in the flat parameters (bias; β then γ)
     int in_off, out_off, res_off;   // LDS offsets (floats)
     int ktab;            // LDS offset of the k table (kk > 1), else -1
+    int in_kb, out_kb, res_kb;   // input / output / residual buffer in the k-blocked layout (rn_kb_off)
+    int ep_img;          // epilogue image [n_ob·16 rows][bias, γ, β, 0] in the weight image (after the A fragments)
+    int otab;            // kernel > 1x1 read through a per-lane offset table at LDS int offset ktab (narrow plans)
 };
+
+// What the layer loop reads per layer, packed into 8 words so a layer's entry
+// is one scalar load (rn_rk_decode): flags, K | cout, nq | n_ob, in | out, res |
+// ktab (16-bit LDS offsets), w_img, ep_img
+struct RK { int w[8]; };
+enum { RK_KK = 1, RK_SPATIAL = 2, RK_BN = 16, RK_RES = 32, RK_IN_KB = 64, RK_OUT_KB = 128, RK_RES_KB = 256,
+       RK_OTAB = 512 };
+__host__ __device__ __forceinline__ RK rn_rk_pack(const RLayer& L) {
+    RK k;
+    k.w[0] = (L.kk > 1 ? RK_KK : 0) | (L.spatial ? RK_SPATIAL : 0) | (L.act << 2) | (L.bn ? RK_BN : 0) |
+             (L.res_add ? RK_RES : 0) | (L.in_kb ? RK_IN_KB : 0) | (L.out_kb ? RK_OUT_KB : 0) |
+             (L.res_kb ? RK_RES_KB : 0) | (L.otab ? RK_OTAB : 0);
+    k.w[1] = L.K | (L.cout << 16);
+    k.w[2] = L.nq | (L.n_ob << 16);
+    k.w[3] = L.in_off | (L.out_off << 16);
+    k.w[4] = (L.res_off & 0xffff) | (L.ktab << 16);
+    k.w[5] = L.w_img;
+    k.w[6] = L.ep_img;
+    k.w[7] = 0;
+    return k;
+}
+// the fields rn_layer_t reads (kk only as "> 1"; kw/kh/pw/ph, boff/bnoff unused there)
+__host__ __device__ __forceinline__ RLayer rn_rk_decode(const RK& k) {
+    RLayer L;
+    L.kk = (k.w[0] & RK_KK) ? 2 : 1; L.kw = L.kh = L.pw = L.ph = 0;
+    L.spatial = (k.w[0] & RK_SPATIAL) != 0; L.act = (k.w[0] >> 2) & 3; L.bn = (k.w[0] & RK_BN) != 0;
+    L.res_add = (k.w[0] & RK_RES) != 0; L.in_kb = (k.w[0] & RK_IN_KB) != 0; L.out_kb = (k.w[0] & RK_OUT_KB) != 0;
+    L.res_kb = (k.w[0] & RK_RES_KB) != 0; L.otab = (k.w[0] & RK_OTAB) != 0;
+    L.K = k.w[1] & 0xffff; L.cout = (int)((unsigned)k.w[1] >> 16);
+    L.nq = k.w[2] & 0xffff; L.n_ob = (int)((unsigned)k.w[2] >> 16);
+    L.in_off = k.w[3] & 0xffff; L.out_off = (int)((unsigned)k.w[3] >> 16);
+    L.res_off = k.w[4] & 0xffff; L.ktab = k.w[4] >> 16;
+    L.w_img = k.w[5]; L.ep_img = k.w[6];
+    L.boff = L.bnoff = 0;
+    return L;
+}
 
 struct RPlan {
     int n;
     RLayer L[RN_MAX_LAYERS];
+    RK k[RN_MAX_LAYERS];               // the same layers packed (rn_rk_pack)
     int in_off, in_feat;               // input buffer (features x NG)
+    int in_kb;                         // the staged input is k-blocked (its first readers are 1x1 / Dense, K % 64 == 0)
     int out0_off, out0_n;              // out0: h (REPR, DYN) or value (PRED)
+    int out0_kb;                       // out0 k-blocked (h of the dynamics, when its state head reads it so)
     int out1_off, out1_n;              // out1: policy logits (PRED) or reward (DYN), n = 0 if none
     int lds_floats;                    // LDS per workgroup (floats), k tables included
+    // narrow (learner chain) plans: the B-operand byte offsets of the layers with a
+    // kernel > 1x1 ([q][chunk][column][slot][4 k-steps], rn_otab_fill), copied
+    // from the engine's table buffer at tab_src to LDS at tab_lds (tab_n ints) by
+    // the kernel; zero_off = an LDS float kept 0 (out-of-board taps, padding)
+    int tab_src, tab_lds, tab_n, zero_off;
 };
 
 struct RNetParams {
@@ -117,6 +176,7 @@ struct RUnrollParams {
     // sequential part) on tiles of ng_l samples with plans_l, then
     // mz_runroll_pred (the K predictions, independent) on tiles of ng items
     const RPlan* plans_l; int ng_l;
+    const int* otab;                   // the narrow plans' offset tables (RPlan.tab_src)
     int dyn_split;                     // first reward-head layer of the dynamics plans
     float* ts;                         // [B][K][H] dynamics trunk outputs (split form: the reward heads' input)
     unsigned long long* stamps;        // -DMZ_STAMPS builds: per-layer ticks of chain block 0 (repr, dyn s = 1)
