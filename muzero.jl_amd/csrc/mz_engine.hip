@@ -45,6 +45,8 @@ extern "C" __global__ void mz_bp_dw(BpDwParams Q);
 extern "C" __global__ void mz_bp_fold(BpFoldParams Q);
 extern "C" __global__ void mz_runroll_pred(RUnrollParams U);
 extern "C" __global__ void mz_runroll_pred_n(RUnrollParams U);
+extern "C" __global__ void mz_runroll_pred_n1(RUnrollParams U);
+extern "C" __global__ void mz_runroll_chain1(RUnrollParams U);
 extern "C" __global__ void mz_sp_prepare(SpParams S);
 extern "C" __global__ void mz_sp_commit(SpParams S);
 extern "C" __global__ void mz_sp_order(SpParams S);
@@ -1221,8 +1223,10 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
                            (int)lmax) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll)"));
     CK(hipFuncSetAttribute((const void*)mz_runroll_pred, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)lmax) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_pred)"));
-    CK(hipFuncSetAttribute((const void*)mz_runroll_pred_n, hipFuncAttributeMaxDynamicSharedMemorySize,
-                           (int)h->rn_lds_l) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_pred_n)"));
+    for (const void* k : {(const void*)mz_runroll_pred_n, (const void*)mz_runroll_pred_n1,
+                          (const void*)mz_runroll_chain1})
+        CK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->rn_lds_l) == hipSuccess
+               ? 0 : fail(h, "hipFuncSetAttribute(runroll narrow)"));
     CK(hipFuncSetAttribute((const void*)mz_runroll_chain, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)h->rn_lds_l) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_chain)"));
     CK(hipFuncSetAttribute((const void*)mz_rsearch_nets, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1801,7 +1805,10 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
                                   args, runroll_lds(h), st));
     } else {                                        // chain on narrow tiles, then the B·K predictions
         const int KH = std::max(U.K, 1);
-        MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_chain, dim3((B + U.ng_l - 1) / U.ng_l), dim3(RN_THREADS),
+        // tiles of one column block: the 1-block instances (a fifth of the code)
+        const bool nb1 = (U.P * U.ng_l + 15) / 16 == 1;
+        MZ_TRY(h, hipLaunchKernel(nb1 ? (const void*)mz_runroll_chain1 : (const void*)mz_runroll_chain,
+                                  dim3((B + U.ng_l - 1) / U.ng_l), dim3(RN_THREADS),
                                   args, h->rn_lds_l, st));
         // the B·K predictions and reward heads: narrow tiles unless MZ_RN_PRED_WIDE
         static const bool wide = std::getenv("MZ_RN_PRED_WIDE") != nullptr;
@@ -1809,7 +1816,7 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
             MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred, dim3((B * KH + U.ng - 1) / U.ng, U.K > 0 ? 2 : 1),
                                       dim3(RN_THREADS), args, runroll_lds(h), st));
         else
-            MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred_n,
+            MZ_TRY(h, hipLaunchKernel(nb1 ? (const void*)mz_runroll_pred_n1 : (const void*)mz_runroll_pred_n,
                                       dim3((B * KH + U.ng_l - 1) / U.ng_l, U.K > 0 ? 2 : 1), dim3(RN_THREADS), args,
                                       h->rn_lds_l, st));
     }

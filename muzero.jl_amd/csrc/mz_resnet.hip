@@ -414,32 +414,31 @@ __device__ __forceinline__ int rn_nbw(const RLayer& L, int NG, int P) {
     return n_nb == 1 ? 1 : n_nb == 2 ? 2 : L.kk > 1 ? 3 : RN_NBW;
 }
 
-template <bool NARROW, bool PF = false>
+// NBWMAX = 1: a narrow kernel instance for tiles of one column block (the host
+// launches it only then): the 1-block units alone, a fifth of the code
+template <bool NARROW, bool PF = false, int NBWMAX = 3>
 __device__ __forceinline__ void rn_layer(const RLayer& L, const float* __restrict__ Wimg,
                                          const float* __restrict__ flat, float* lds, int NG, int Wb, int P,
                                          float bn_s, float bn_r, const RnPf* pf = nullptr,
                                          unsigned long long* dbg = nullptr) {
-    const int n_nb = NARROW && L.spatial ? (P * NG + 15) >> 4 : 3;     // as rn_nbw
+    const int n_nb = NBWMAX == 1 ? 1 : NARROW && L.spatial ? (P * NG + 15) >> 4 : 3;     // as rn_nbw
+#define RN_L(NB, M) rn_layer_t<NB, M, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg)
     if (NARROW && L.otab) {                                           // kernel > 1x1 through the offset table
-        if (n_nb == 1) rn_layer_t<1, 4, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
-        else if (n_nb == 2) rn_layer_t<2, 4, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
-        else rn_layer_t<3, 4, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+        if (n_nb == 1) RN_L(1, 4);
+        else if constexpr (NBWMAX > 1) { if (n_nb == 2) RN_L(2, 4); else RN_L(3, 4); }
     } else if (L.in_kb) {                                             // 1x1 conv / Dense, K % 64 == 0
-        if (!L.spatial) rn_layer_t<1, 3, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
-        else if (n_nb == 1) rn_layer_t<1, 3, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
-        else if (n_nb == 2) rn_layer_t<2, 3, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
-        else rn_layer_t<RN_NBW, 3, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+        if (!L.spatial || n_nb == 1) RN_L(1, 3);
+        else if constexpr (NBWMAX > 1) { if (n_nb == 2) RN_L(2, 3); else RN_L(RN_NBW, 3); }
     } else if (L.kk > 1) {
-        if (n_nb == 1) rn_layer_t<1, 2, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
-        else if (n_nb == 2) rn_layer_t<2, 2, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
-        else rn_layer_t<3, 2, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+        if (n_nb == 1) RN_L(1, 2);
+        else if constexpr (NBWMAX > 1) { if (n_nb == 2) RN_L(2, 2); else RN_L(3, 2); }
     } else if (L.spatial) {
-        if (n_nb == 1) rn_layer_t<1, 1, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
-        else if (n_nb == 2) rn_layer_t<2, 1, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
-        else rn_layer_t<RN_NBW, 1, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+        if (n_nb == 1) RN_L(1, 1);
+        else if constexpr (NBWMAX > 1) { if (n_nb == 2) RN_L(2, 1); else RN_L(RN_NBW, 1); }
     } else {
-        rn_layer_t<1, 0, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg);
+        RN_L(1, 0);
     }
+#undef RN_L
 }
 
 // This wave's first-unit operands of layer L (no-op for a wave without one)
@@ -478,7 +477,7 @@ __device__ void rn_fill_ktabs(const RPlan& R, float* lds, int NG, int Wb, int P)
 // PF: the next layer's plan entry, first A chunk and epilogue parameters are
 // loaded before each layer barrier (kernels with the register room: 512
 // threads).  Layers [i0, i1) (i1 < 0: to the end).
-template <bool NARROW = false, bool PF = false>
+template <bool NARROW = false, bool PF = false, int NBWMAX = 3>
 __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const float* flat, float* lds, int NG,
                                        int Wb, int P, float bn_s, unsigned long long* st = nullptr, int i0 = 0,
                                        int i1 = -1) {
@@ -500,7 +499,7 @@ __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const 
 #ifdef MZ_STAMPS
             if (st && i - i0 < 31) dbg = st + 1024 + 8 * (i - i0);
 #endif
-            rn_layer<NARROW, true>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, &pf, dbg);
+            rn_layer<NARROW, true, NBWMAX>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, &pf, dbg);
             if (i + 1 < i1) rn_prefetch<NARROW>(Ln, Wimg, flat, NG, P, pf);
 #ifdef MZ_STAMPS
             if (st && (threadIdx.x & 63) == 0 && i - i0 < 31) st[wv * 64 + 2 * (i - i0)] = __builtin_amdgcn_s_memtime();
@@ -513,7 +512,7 @@ __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const 
         }
     } else {
         for (int i = i0; i < i1; ++i) {
-            rn_layer<NARROW>(rn_layer_at(R, i), Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+            rn_layer<NARROW, false, NBWMAX>(rn_layer_at(R, i), Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
 #ifdef MZ_STAMPS
             if (st && (threadIdx.x & 63) == 0 && i - i0 < 31) st[wv * 64 + 2 * (i - i0)] = __builtin_amdgcn_s_memtime();
 #endif
@@ -1043,7 +1042,8 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_kernel(RUnro
 // trunk output of step s to ts[b][s-1]; mz_runroll_pred then runs the B·K
 // predictions (blockIdx.y = 0) and the B·K reward heads (y = 1) as one wide
 // launch on tiles of ng items.
-extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrollParams U) {
+template <int NBWMAX>
+__device__ __forceinline__ void runroll_chain_body(const RUnrollParams& U) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const RPlan& Rr = U.plans_l[MZ_NET_REPR];
     const RPlan& Rd = U.plans_l[MZ_NET_DYN];
@@ -1074,7 +1074,7 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrol
         rn_stage_l(lds + Rr.in_off, Rr.in_kb, NG, U.P, Rr.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
     }
     __syncthreads();
-    rn_run<true, true>(Rr, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, st_r);         // :347
+    rn_run<true, true, NBWMAX>(Rr, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, st_r);         // :347
     if (ok) rn_unstage_l(lds + Rr.out0_off, Rr.out0_kb, NG, U.P, H, t, [&](int f, float v) { hs[f] = v; });
     if (ok && t.f0 == 0) U.pr[bs * K1] = 0.0f;                                 // :352 zeros
     for (int s = 1; s <= K; ++s) {
@@ -1086,7 +1086,7 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrol
             rn_stage_l(lds + Rd.in_off, Rd.in_kb, NG, U.P, Rd.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? hp[f] * 2.0f : av; });
         }
         __syncthreads();
-        rn_run<true, true>(Rd, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, s == 1 ? st_d : nullptr, 0, split);  // :362
+        rn_run<true, true, NBWMAX>(Rd, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, s == 1 ? st_d : nullptr, 0, split);  // :362
         if (ok) {
             if (s < K) rn_unstage_l(lds + Rd.out0_off, Rd.out0_kb, NG, U.P, H, t,
                                     [&](int f, float v) { hs[(size_t)s * H + f] = v; });
@@ -1095,11 +1095,14 @@ extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrol
     }
 }
 
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrollParams U) { runroll_chain_body<3>(U); }
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain1(RUnrollParams U) { runroll_chain_body<1>(U); }
+
 // blockIdx.y = 0: prediction(h_s) for items i = b·KH + s (KH = max(K, 1)):
 // step s + 1's value and policy, and step 0's too for s = 0 (Q10: :351 and
 // :356 at i = 1 both predict from h_0).  y = 1: the dynamics reward head on
 // the trunk output of step s + 1 (items b·K + s): r_{s+1}.
-template <bool NARROW>
+template <bool NARROW, int NBWMAX = 3>
 __device__ __forceinline__ void runroll_pred_body(const RUnrollParams& U) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const bool rew = blockIdx.y == 1;
@@ -1118,7 +1121,7 @@ __device__ __forceinline__ void runroll_pred_body(const RUnrollParams& U) {
                    [&](int f) { return ok ? x[f] : 0.0f; });
     }
     __syncthreads();
-    rn_run<NARROW, true>(R, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, nullptr, i0);   // :351 / :356, :362
+    rn_run<NARROW, true, NBWMAX>(R, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, nullptr, i0);   // :351 / :356, :362
     if (!ok) return;
     const size_t b = ic / KH;
     const int s = (int)(ic - b * KH);
@@ -1136,3 +1139,6 @@ __device__ __forceinline__ void runroll_pred_body(const RUnrollParams& U) {
 // (chain) plans — B·K workgroups, a short per-layer critical path
 extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred(RUnrollParams U) { runroll_pred_body<false>(U); }
 extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred_n(RUnrollParams U) { runroll_pred_body<true>(U); }
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred_n1(RUnrollParams U) {
+    runroll_pred_body<true, 1>(U);
+}
