@@ -296,7 +296,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         if (tid < 64) {
             // ---- select (:256-268)
             if (active) {
-                const SelectOut so = select_path<true>(tree, path, sg_rootN[g], sg_root_tp[g], legal, sg_mmin[g],
+                const SelectOut so = select_path<true, 16, T>(tree, path, sg_rootN[g], sg_root_tp[g], legal, sg_mmin[g],
                                                        sg_mmax[g], a, lane, A, P.players, P.discount, l_pbterm, l_pbc,
                                                        l_sqrt, P.seed, gid, P.rng_step, s);
                 if (a == 0) { sg_leaf_e[g] = so.leaf_e; sg_leaf_a[g] = so.leaf_a; sg_vtp[g] = so.vtp; sg_depth[g] = so.depth; }

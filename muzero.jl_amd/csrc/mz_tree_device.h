@@ -233,7 +233,10 @@ __device__ __forceinline__ float g16_vmax(float v) {
 // to -inf), a DPP max, a ballot, and the chosen edge's record by DPP.  The
 // path stays in registers while depth < GW (lane d keeps level d) and is
 // written to `path` once at the end; deeper levels are stored directly.
-template <bool TAB, int GW = 16>
+// NGRP: GW-lane groups in use in this wave (GW = 16: the argmax lane and the
+// chosen record are then found per group with scalar ops on the ballot and a
+// readlane, instead of per-lane shifts and a DPP OR chain).
+template <bool TAB, int GW = 16, int NGRP = 4>
 __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, int root_N, int root_tp,
                                                  uint32_t legal, float mmin, float mmax, int a, int lane,
                                                  int A, int players, float discount, const double* pbterm,
@@ -250,6 +253,9 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
         // the parent's pUCT table entries depend only on Np: read them with the record
         double pbn = 0.0, sqn = 0.0;
         if constexpr (!TAB) { pbn = pbc_tab[Np]; sqn = sqrt_tab[Np]; }
+        // the pb_term row of the parent depends on Np alone: formed while the
+        // record is in flight
+        const double* prow = TAB ? pbterm + (__umul24((unsigned)Np, (unsigned)(Np + 1)) >> 1) : nullptr;
         float4 ed = t.e[(int)__umul24((unsigned)e, (unsigned)A) + ac];
         // keep the whole record one load and the score branch-free: without
         // these the compiler sinks the ev load and the division into an
@@ -258,19 +264,25 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
         const uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
         const int Nc = (int)(nc & 0xffffu);
         double pb_c;
+        float num = ed.w - mmin;
         if constexpr (TAB) {
-            pb_c = pbterm[pbterm_index(Np, Nc < Np ? Nc : Np)];
+            pb_c = prow[Nc < Np ? Nc : Np];               // pbterm[pbterm_index(Np, min(Nc, Np))]
+            // the read is issued here (memory clobber) and the division below
+            // depends on this asm: it runs while the entry is in flight
+            asm volatile("" : "+v"(num) :: "memory");
         } else {
             pb_c = pbn * (sqn / (double)(Nc + 1));
         }
-        const double prior_score = pb_c * (double)ed.z;
         // normalize (:33-39), the IEEE division: a reciprocal per walk plus a
         // Markstein correction is exact on [2^-60, 2^60] but needs a per-level
         // range test and branch, which measured slower
-        float vn = (ed.w - mmin) / den;                  // discarded unless norm and Nc > 0
-        asm volatile("" : "+v"(vn));
+        float vn = num / den;                            // discarded unless norm and Nc > 0
+        asm volatile("" : "+v"(vn));                     // (unconditional: not sunk into an Nc > 0 branch)
         const float vs = Nc > 0 ? (norm ? vn : ed.w) : 0.0f;
-        const float us = (float)(prior_score + (double)vs);
+        double pz = (double)ed.z, vsd = (double)vs;      // ready before the pb_term entry lands
+        asm volatile("" : "+v"(pz), "+v"(vsd), "+v"(pb_c));
+        const double prior_score = pb_c * pz;
+        const float us = (float)(prior_score + vsd);
         const float u = lg ? us : -INFINITY;
         float m = g16_vmax(u);
         if constexpr (GW == 32) {
@@ -280,19 +292,57 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
             m = fx > fy ? fx : fy;
         }
         const uint64_t bal = __builtin_amdgcn_ballot_w64(lg && u == m);
-        const uint32_t mask = GW == 16 ? (uint32_t)(bal >> (lane & 48)) & 0xffffu : (uint32_t)(bal >> (lane & 32));
         depth += 1;
-        int ach = __builtin_ctz(mask);
-        // ties (rare): one wave-uniform test, then the Philox draw per group
-        if (__builtin_amdgcn_ballot_w64((mask & (mask - 1)) != 0) != 0) {
-            const int nt = __builtin_popcount(mask);
-            if (nt > 1) {
-                const uint32_t r = mz_rng_u32(seed, MZ_RNG_TIE, gid, step, ((uint32_t)sim << 12) | (uint32_t)depth);
-                ach = nth_set_bit(mask, (int)mz_rng_below(r, (uint32_t)nt));
+        int ach;
+        uint32_t ncc;
+        if constexpr (GW == 16) {
+            // per group g: its candidate mask, first candidate and whether it ties
+            // (wave-uniform, scalar); each lane takes its group's by select
+            const int grp = lane >> 4;
+            uint32_t gm[NGRP];
+            int gf[NGRP];
+            bool tie = false;
+#pragma unroll
+            for (int g = 0; g < NGRP; ++g) {
+                gm[g] = (uint32_t)(bal >> (16 * g)) & 0xffffu;
+                gf[g] = __builtin_ctz(gm[g] | 0x10000u);
+                tie |= (gm[g] & (gm[g] - 1)) != 0;
             }
+            ach = gf[0];
+#pragma unroll
+            for (int g = 1; g < NGRP; ++g) ach = grp == g ? gf[g] : ach;
+            if (tie) {                                    // ties (rare): the Philox draw per group
+                uint32_t mask = gm[0];
+#pragma unroll
+                for (int g = 1; g < NGRP; ++g) mask = grp == g ? gm[g] : mask;
+                const int nt = __builtin_popcount(mask);
+                if (nt > 1) {
+                    const uint32_t r = mz_rng_u32(seed, MZ_RNG_TIE, gid, step, ((uint32_t)sim << 12) | (uint32_t)depth);
+                    ach = nth_set_bit(mask, (int)mz_rng_below(r, (uint32_t)nt));
+                }
+                ncc = g16_or(a == ach ? nc : 0u);
+            } else {                                      // the chosen lane's nc by readlane
+                ncc = (uint32_t)__builtin_amdgcn_readlane((int)nc, gf[0]);
+#pragma unroll
+                for (int g = 1; g < NGRP; ++g) {
+                    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)nc, 16 * g + (gf[g] & 15));
+                    ncc = grp == g ? v : ncc;
+                }
+            }
+        } else {
+            const uint32_t mask = (uint32_t)(bal >> (lane & 32));
+            ach = __builtin_ctz(mask);
+            // ties (rare): one wave-uniform test, then the Philox draw per group
+            if (__builtin_amdgcn_ballot_w64((mask & (mask - 1)) != 0) != 0) {
+                const int nt = __builtin_popcount(mask);
+                if (nt > 1) {
+                    const uint32_t r = mz_rng_u32(seed, MZ_RNG_TIE, gid, step, ((uint32_t)sim << 12) | (uint32_t)depth);
+                    ach = nth_set_bit(mask, (int)mz_rng_below(r, (uint32_t)nt));
+                }
+            }
+            ncc = gor<GW>(a == ach ? nc : 0u);           // the chosen lane's nc, via DPP
         }
         const int ei = (int)__umul24((unsigned)e, (unsigned)A) + ach;
-        const uint32_t ncc = gor<GW>(a == ach ? nc : 0u);  // the chosen lane's nc, via DPP
         const int Cch = (int)(ncc >> 16);
         const bool keep = a == depth;                     // depth < GW: lane `depth` keeps the level
         pe = keep ? ei : pe;
