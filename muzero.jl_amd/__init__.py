@@ -8,4 +8,5 @@ kernels are hand-written HIP for gfx950.  Load via `_mzpkg.load()`.
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libmz.so")
+# MZ_LIB: an A/B variant of the library (tools/build_variants.py); default the in-tree build
+LIB_PATH = os.environ.get("MZ_LIB") or os.path.join(PKG_DIR, "lib", "libmz.so")

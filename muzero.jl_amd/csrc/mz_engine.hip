@@ -47,6 +47,7 @@ extern "C" __global__ void mz_runroll_pred(RUnrollParams U);
 extern "C" __global__ void mz_runroll_pred_n(RUnrollParams U);
 extern "C" __global__ void mz_runroll_pred_n1(RUnrollParams U);
 extern "C" __global__ void mz_runroll_chain1(RUnrollParams U);
+extern "C" __global__ void mz_runroll_chain_r(RUnrollParams U);
 extern "C" __global__ void mz_sp_prepare(SpParams S);
 extern "C" __global__ void mz_sp_commit(SpParams S);
 extern "C" __global__ void mz_sp_order(SpParams S);
@@ -154,6 +155,7 @@ struct mz_handle {
     float* d_rhs = nullptr;                 // [bcap][K][H] learner unroll scratch (h between the nets)
     float* d_rts = nullptr;                 // [bcap][K][H] dynamics trunk outputs (the reward heads' input)
     int rn_dyn_split = 0;                   // first reward-head layer of the dynamics plan
+    bool rd_chain = false;                  // the chain runs as mz_runroll_chain_r (rd_chain_ok)
     std::vector<int> rtab;                  // offset tables of the narrow (chain) plans
     int* d_rtab = nullptr;
     int device = 0, max_games = 0;
@@ -812,6 +814,22 @@ static void rn_otab_fill(std::vector<int>& t, const RLayer& L, int NG, int W, in
                     }
 }
 
+// mz_runroll_chain_r applies when the learner chain's tiles are one column
+// block and the dynamics chain ([0, dyn_split)) is RD_NL 1x1 conv layers of 64
+// channels with BatchNorm + relu: layer 0 on the plain input with 4 < nq <= 8
+// (nf + 1 channels: two A chunks), the others K = 64 on k-blocked inputs
+static size_t rd_chain_lds(const mz_handle* h) { return h->rn_lds_l + (size_t)RD_NL * 64 * 16; }
+static bool rd_chain_ok(const mz_handle* h) {
+    const RPlan& R = h->rplan_l[MZ_NET_DYN];
+    if (h->rn_dyn_split != RD_NL || (h->plane * h->rn_ng_l + 15) / 16 != 1) return false;
+    for (int i = 0; i < RD_NL; ++i) {
+        const RLayer& L = R.L[i];
+        if (L.kk != 1 || L.cout != 64 || L.n_ob != 4 || !L.spatial || !L.bn || L.act != MZ_ACT_RELU) return false;
+        if (i == 0 ? (L.in_kb || L.nq <= 4 || L.nq > 8) : (!L.in_kb || L.K != 64 || L.nq != 4)) return false;
+    }
+    return rd_chain_lds(h) <= kLdsMax;
+}
+
 static RPlan rn_plan(const mz_handle* h, const std::vector<RSpec>& sp, int net, int NG, size_t flat_off,
                      int& w_img, std::vector<int>* srcw, bool sep_b2 = false, std::vector<int>* otab = nullptr) {
     const mz_config& c = h->rconf;
@@ -1175,6 +1193,7 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
             CK(h->rplan_l[n].n < 0 ? fail(h, "ResNet plan: a k-blocked output buffer") : 0);
             h->rn_lds_l = std::max(h->rn_lds_l, (size_t)h->rplan_l[n].lds_floats * 4);
         }
+        h->rd_chain = rd_chain_ok(h) && !std::getenv("MZ_RN_NO_RD");
     }
     h->inv_tile.assign(h->nflat, -1);
     for (size_t i = 0; i < sw.size(); ++i) if (sw[i] >= 0) h->inv_tile[(size_t)sw[i]] = (int)i;
@@ -1229,6 +1248,9 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
                ? 0 : fail(h, "hipFuncSetAttribute(runroll narrow)"));
     CK(hipFuncSetAttribute((const void*)mz_runroll_chain, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)h->rn_lds_l) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_chain)"));
+    if (h->rd_chain)
+        CK(hipFuncSetAttribute((const void*)mz_runroll_chain_r, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)rd_chain_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_chain_r)"));
     CK(hipFuncSetAttribute((const void*)mz_rsearch_nets, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)rsearch_nets_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(nets)"));
     // search buffers (trees and hidden states in HBM)
@@ -1807,9 +1829,14 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
         const int KH = std::max(U.K, 1);
         // tiles of one column block: the 1-block instances (a fifth of the code)
         const bool nb1 = (U.P * U.ng_l + 15) / 16 == 1;
-        MZ_TRY(h, hipLaunchKernel(nb1 ? (const void*)mz_runroll_chain1 : (const void*)mz_runroll_chain,
-                                  dim3((B + U.ng_l - 1) / U.ng_l), dim3(RN_THREADS),
-                                  args, h->rn_lds_l, st));
+        U.rd_ep_off = (int)(h->rn_lds_l / 4);
+        if (h->rd_chain)
+            MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_chain_r, dim3((B + U.ng_l - 1) / U.ng_l),
+                                      dim3(RD_THREADS), args, rd_chain_lds(h), st));
+        else
+            MZ_TRY(h, hipLaunchKernel(nb1 ? (const void*)mz_runroll_chain1 : (const void*)mz_runroll_chain,
+                                      dim3((B + U.ng_l - 1) / U.ng_l), dim3(RN_THREADS),
+                                      args, h->rn_lds_l, st));
         // the B·K predictions and reward heads: narrow tiles unless MZ_RN_PRED_WIDE
         static const bool wide = std::getenv("MZ_RN_PRED_WIDE") != nullptr;
         if (wide)

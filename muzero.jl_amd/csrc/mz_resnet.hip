@@ -25,7 +25,12 @@ __device__ __forceinline__ float rn_act(int act, float v) {
 __device__ __forceinline__ void rn_load_a(float (&a)[4][4], const float* __restrict__ Wimg, const RLayer& L,
                                           int ob, int c, int lane) {
     const int nch = (L.nq + 3) >> 2;
-    const float* base = Wimg + L.w_img + (size_t)ob * (16 * nch * 64) + (size_t)lane * 4;
+    #ifdef RN_HOTA
+    const float* base = Wimg + (size_t)ob
+#else
+    const float* base = Wimg + L.w_img + (size_t)ob
+#endif
+                       * (16 * nch * 64) + (size_t)lane * 4;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const float4 v = *reinterpret_cast<const float4*>(base + (size_t)((q * nch + c) * 64) * 4);
@@ -48,7 +53,11 @@ __device__ __forceinline__ void rn_load_a(float (&a)[4][4], const float* __restr
 // BatchNorm entries of layers without one read 0)
 __device__ __forceinline__ void rn_load_ep(float (&ep)[3][4], const RLayer& L, const float* __restrict__ Wimg,
                                            int ob, int kl) {
+    #ifdef RN_HOTA
+    const float4* e = reinterpret_cast<const float4*>(Wimg) + ob * 16 + kl * 4;
+#else
     const float4* e = reinterpret_cast<const float4*>(Wimg + L.ep_img) + ob * 16 + kl * 4;
+#endif
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const float4 v = e[r];
@@ -1097,6 +1106,195 @@ __device__ __forceinline__ void runroll_chain_body(const RUnrollParams& U) {
 
 extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrollParams U) { runroll_chain_body<3>(U); }
 extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain1(RUnrollParams U) { runroll_chain_body<1>(U); }
+
+// ---- the chain with a register-resident dynamics path (mz_runroll_chain_r)
+// The K dynamics steps run the same RD_NL trunk + state-head layers K times:
+// 1x1 convs of 64 output channels (one 16-row block per wave, waves 0..3) on
+// one 16-column block.  Their A fragments are loaded into registers once per
+// launch (layer 0, K = nf + 1 on the plain input: two chunks; layers 1.. (K =
+// 64, k-blocked input): one chunk each) and their epilogue parameters staged in
+// LDS, so a layer is LDS reads, 16 MFMAs and a branch-free epilogue between two
+// barriers: no plan decode through the generic layer code, no global loads.
+// The arithmetic is rn_layer_t's (MODE 1 / MODE 3, NBW = 1) and
+// rn_epilogue's, operation for operation.  256 threads: one wave per SIMD, so
+// the resident fragments (16 floats per chunk) have the register file's room.
+template <bool RES_ADD>
+__device__ __forceinline__ void rd_epilogue(const RLayer& L, const mz_f32x4 (&acc)[4], const float4 (&ep)[4],
+                                            const float (&res)[4], float* lds, int ob, int kl, int n, int ncols,
+                                            float bn_s, float bn_r) {
+    float d[4];
+    bool tiny = false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float t = (acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r]);
+        t = t + ep[r].x;
+        d[r] = t;
+        tiny |= !(fabsf(t) >= 0x1p-100f) || fabsf(t) == INFINITY;
+    }
+    float q[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float t = d[r] - 0.0f;
+        const float q0 = t * bn_r;
+        const float e = fmaf(-q0, bn_s, t);
+        q[r] = fmaf(e, bn_r, q0);
+    }
+    if (__builtin_expect(__ballot(tiny) != 0, 0)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (!(fabsf(d[r]) >= 0x1p-100f) || fabsf(d[r]) == INFINITY) q[r] = (d[r] - 0.0f) / bn_s;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) d[r] = ep[r].y * q[r] + ep[r].z;
+    if (n < ncols) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v = d[r];
+            if constexpr (RES_ADD) v = v + res[r];
+            lds[L.out_off + rn_out_idx(L.out_kb, ob, kl, r, n, ncols)] = mz_relu(v);
+        }
+    }
+}
+
+// layer I of the resident chain (wave ob < 4); a[] = this layer's chunks
+template <int NCH>
+__device__ __forceinline__ void rd_layer(const RLayer& L, const float (&a)[NCH][4][4], const float4* ep_lds,
+                                         float* lds, int ncols, float bn_s, float bn_r) {
+    const int lane = threadIdx.x & 63, ob = threadIdx.x >> 6, kl = lane >> 4, n = lane & 15;
+    float4 ep[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ep[r] = ep_lds[ob * 16 + kl * 4 + r];
+    float res[4];
+    const int nc = n < ncols ? n : ncols - 1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) res[r] = L.res_add ? lds[L.res_off + rn_out_idx(L.res_kb, ob, kl, r, nc, ncols)] : 0.0f;
+    mz_f32x4 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = mz_f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (NCH == 1) {                   // MODE 3: K = 64, NQ = 4, k-blocked input
+        const uint32_t b0 = (uint32_t)(L.in_off + n * 16 + 4 * (((n >> 2) & 3) ^ rn_kb_sigma(kl))) * 4u;
+        float4 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            v[q] = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(lds) + b0 +
+                                                    (uint32_t)(q * ncols) * 64u);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float bv = jj == 0 ? v[q].x : jj == 1 ? v[q].y : jj == 2 ? v[q].z : v[q].w;
+                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][q][jj], bv, acc[q], 0, 0, 0);
+            }
+    } else {                                    // MODE 1: plain input, NQ = L.nq in (4, 4 NCH]
+        const int NQ = L.nq, K = L.K;
+        const int cb = L.in_off + nc;
+        float b[NCH][4][4];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int k = (q * NQ + 4 * c + jj) * 4 + kl;
+                    const bool kin = k < K && 4 * c + jj < NQ;
+                    const float v = lds[cb + (kin ? k : K - 1) * ncols];
+                    b[c][jj][q] = kin ? v : 0.0f;
+                }
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                if (4 * c + jj >= NQ) break;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][q][jj], b[c][jj][q], acc[q], 0, 0, 0);
+            }
+    }
+    if (L.res_add) rd_epilogue<true>(L, acc, ep, res, lds, ob, kl, n, ncols, bn_s, bn_r);
+    else rd_epilogue<false>(L, acc, ep, res, lds, ob, kl, n, ncols, bn_s, bn_r);
+}
+
+template <int I>
+__device__ __forceinline__ void rd_run(const RPlan& Rd, const float (&a0)[2][4][4], const float (&ar)[RD_NL][4][4],
+                                       const float4* ep_lds, float* lds, int ncols, float bn_s, float bn_r) {
+    if constexpr (I < RD_NL) {
+        const RLayer L = rn_layer_at(Rd, I);
+        if (threadIdx.x < 256) {
+            if constexpr (I == 0) {
+                rd_layer<2>(L, a0, ep_lds, lds, ncols, bn_s, bn_r);
+            } else {
+                const float (&a1)[1][4][4] = *reinterpret_cast<const float (*)[1][4][4]>(&ar[I]);
+                rd_layer<1>(L, a1, ep_lds + I * 64, lds, ncols, bn_s, bn_r);
+            }
+        }
+        __syncthreads();
+        rd_run<I + 1>(Rd, a0, ar, ep_lds, lds, ncols, bn_s, bn_r);
+    }
+}
+
+extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r(RUnrollParams U) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const RPlan& Rr = U.plans_l[MZ_NET_REPR];
+    const RPlan& Rd = U.plans_l[MZ_NET_DYN];
+    const int NG = U.ng_l, t0 = blockIdx.x * NG, H = U.H, A = U.A, K = U.K, K1 = K + 1;
+    const RnLane t = rn_lane(NG);
+    const int b = t0 + t.g;
+    const bool ok = b < U.B;
+    const size_t bs = (size_t)(ok ? b : 0);
+    const int KH = K > 0 ? K : 1;
+    const int split = U.dyn_split;
+    const int trunk = Rd.L[split].in_off;
+    const int ncols = U.P * NG;
+    float* hs = U.hs + bs * KH * H;
+    float* ts = U.ts + bs * KH * H;
+    float4* ep_lds = reinterpret_cast<float4*>(lds + U.rd_ep_off);   // [RD_NL][64] {bias, γ, β, 0}
+    // resident A fragments of the dynamics chain: issued first, they land
+    // while the representation runs (wave w = row block w)
+    const int lane = threadIdx.x & 63, ob = threadIdx.x >> 6;
+    float a0[2][4][4], ar[RD_NL][4][4];
+    {
+        const RLayer L0 = rn_layer_at(Rd, 0);
+        rn_load_a(a0[0], U.Wimg, L0, ob, 0, lane);
+        rn_load_a(a0[1], U.Wimg, L0, ob, 1, lane);
+#pragma unroll
+        for (int i = 1; i < RD_NL; ++i) rn_load_a(ar[i], U.Wimg, rn_layer_at(Rd, i), ob, 0, lane);
+    }
+    for (int i = threadIdx.x; i < RD_NL * 64; i += blockDim.x) {
+        const RLayer L = rn_layer_at(Rd, i >> 6);
+        ep_lds[i] = reinterpret_cast<const float4*>(U.Wimg + L.ep_img)[i & 63];
+    }
+    rn_fill_ktabs(Rr, lds, NG, U.W, U.P);
+    if (Rr.tab_n) {
+        const int4* src = reinterpret_cast<const int4*>(U.otab + Rr.tab_src);
+        int4* dst = reinterpret_cast<int4*>(reinterpret_cast<int*>(lds) + Rr.tab_lds);
+        for (int i = threadIdx.x; i < Rr.tab_n / 4; i += blockDim.x) dst[i] = src[i];
+        if (threadIdx.x == 0) lds[Rr.zero_off] = 0.0f;
+    }
+    {
+        const float* x = U.obs + bs * U.obs_feat;
+        rn_stage_l(lds + Rr.in_off, Rr.in_kb, NG, U.P, Rr.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
+    }
+    __syncthreads();
+    rn_run<true, true, 1>(Rr, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                  // :347
+    if (ok) rn_unstage_l(lds + Rr.out0_off, Rr.out0_kb, NG, U.P, H, t, [&](int f, float v) { hs[f] = v; });
+    if (ok && t.f0 == 0) U.pr[bs * K1] = 0.0f;                                 // :352 zeros
+    const float bn_r = 1.0f / U.bn_s;
+    for (int s = 1; s <= K; ++s) {
+        __syncthreads();
+        {                                                                      // make_dynamics_input (:293-304)
+            const float av = ok ? U.actions[bs * K1 + (s - 1)] / (float)A : 0.0f;
+            const float* hp = hs + (size_t)(s - 1) * H;
+            rn_stage_l(lds + Rd.in_off, Rd.in_kb, NG, U.P, Rd.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? hp[f] * 2.0f : av; });
+        }
+        __syncthreads();
+        rd_run<0>(Rd, a0, ar, ep_lds, lds, ncols, U.bn_s, bn_r);              // :362, layers [0, split)
+        if (ok) {
+            if (s < K) rn_unstage_l(lds + Rd.out0_off, Rd.out0_kb, NG, U.P, H, t,
+                                    [&](int f, float v) { hs[(size_t)s * H + f] = v; });
+            rn_unstage_l(lds + trunk, Rd.L[split].in_kb, NG, U.P, H, t, [&](int f, float v) { ts[(size_t)(s - 1) * H + f] = v; });
+        }
+    }
+}
 
 // blockIdx.y = 0: prediction(h_s) for items i = b·KH + s (KH = max(K, 1)):
 // step s + 1's value and policy, and step 0's too for s = 0 (Q10: :351 and

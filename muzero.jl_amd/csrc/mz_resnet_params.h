@@ -180,7 +180,12 @@ struct RUnrollParams {
     int dyn_split;                     // first reward-head layer of the dynamics plans
     float* ts;                         // [B][K][H] dynamics trunk outputs (split form: the reward heads' input)
     unsigned long long* stamps;        // -DMZ_STAMPS builds: per-layer ticks of chain block 0 (repr, dyn s = 1)
+    int rd_ep_off;                     // mz_runroll_chain_r: LDS float offset of the staged epilogue parameters
 };
+// mz_runroll_chain_r: the dynamics chain's layers ([0, dyn_split) = RD_NL:
+// trunk + state head of 2-block towers) with register-resident A fragments
+#define RD_NL 10
+#define RD_THREADS 256
 
 // Downsampler of the ResNet representation (ResNetHP.downsample,
 // Learning.jl:175-187; BASELINE configs[4]): stride-2 convs without
