@@ -173,7 +173,7 @@ struct RnPf {
     float ep[3][4];
 };
 
-template <int NBW, int MODE, bool PF = false>
+template <int NBW, int MODE, bool PF = false, bool PIPE = false>
 __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restrict__ Wimg,
                                            const float* __restrict__ flat, float* lds, int NG, int Wb, int P,
                                            float bn_s, float bn_r, const RnPf* pf = nullptr,
@@ -271,6 +271,56 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
             const int* tb = reinterpret_cast<const int*>(lds) + L.ktab + n0 * 16 +
                             4 * (((n0 >> 2) & 3) ^ rn_kb_sigma(kl));
             constexpr int QG = NBW == 1 ? 4 : 2;
+            if constexpr (PIPE && NBW == 1) {
+                // software-pipelined (the 256-thread chain kernel's register room):
+                // chunk c's MFMAs run under the B reads of chunk c + 1 and the
+                // offset reads of chunk c + 2 (past the end: re-reads, unused)
+                const char* lb = reinterpret_cast<const char*>(lds);
+                auto rd_o = [&](int c, int4 (&o)[4]) {
+#pragma unroll
+                    for (int h = 0; h < 4; ++h) o[h] = *reinterpret_cast<const int4*>(tb + (h * nch4 + c) * ncols_t * 16);
+                };
+                auto rd_b = [&](const int4 (&o)[4], float (&bv)[4][4]) {
+#pragma unroll
+                    for (int h = 0; h < 4; ++h) {
+                        bv[h][0] = *reinterpret_cast<const float*>(lb + o[h].x);
+                        bv[h][1] = *reinterpret_cast<const float*>(lb + o[h].y);
+                        bv[h][2] = *reinterpret_cast<const float*>(lb + o[h].z);
+                        bv[h][3] = *reinterpret_cast<const float*>(lb + o[h].w);
+                    }
+                };
+                int4 o1[4];
+                float bv[4][4];
+                rd_o(0, o1);
+                rd_b(o1, bv);
+                rd_o(nch4 > 1 ? 1 : 0, o1);
+                for (int c = 0; c < nch4; ++c) {
+                    float ac[4][4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj) ac[q][jj] = an[q][jj];
+                    {
+                        const int un = c + 1 < nch4 ? u : u + nwaves, cn = c + 1 < nch4 ? c + 1 : 0;
+                        if (un < units) rn_load_a(an, Wimg, L, un / n_grp, cn, lane);
+                    }
+                    float bn[4][4];
+                    int4 o2[4];
+                    rd_b(o1, bn);
+                    rd_o(c + 2 < nch4 ? c + 2 : nch4 - 1, o2);
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            acc[0][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[q][jj], bv[q][jj], acc[0][q], 0, 0, 0);
+#pragma unroll
+                    for (int h = 0; h < 4; ++h) {
+                        o1[h] = o2[h];
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj) bv[h][jj] = bn[h][jj];
+                    }
+                }
+            } else
             for (int c = 0; c < nch4; ++c) {
                 float ac[4][4];                         // this chunk's A; the next one's loads fly under it
 #pragma unroll
@@ -425,13 +475,13 @@ __device__ __forceinline__ int rn_nbw(const RLayer& L, int NG, int P) {
 
 // NBWMAX = 1: a narrow kernel instance for tiles of one column block (the host
 // launches it only then): the 1-block units alone, a fifth of the code
-template <bool NARROW, bool PF = false, int NBWMAX = 3>
+template <bool NARROW, bool PF = false, int NBWMAX = 3, bool PIPE = false>
 __device__ __forceinline__ void rn_layer(const RLayer& L, const float* __restrict__ Wimg,
                                          const float* __restrict__ flat, float* lds, int NG, int Wb, int P,
                                          float bn_s, float bn_r, const RnPf* pf = nullptr,
                                          unsigned long long* dbg = nullptr) {
     const int n_nb = NBWMAX == 1 ? 1 : NARROW && L.spatial ? (P * NG + 15) >> 4 : 3;     // as rn_nbw
-#define RN_L(NB, M) rn_layer_t<NB, M, PF>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg)
+#define RN_L(NB, M) rn_layer_t<NB, M, PF, PIPE>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg)
     if (NARROW && L.otab) {                                           // kernel > 1x1 through the offset table
         if (n_nb == 1) RN_L(1, 4);
         else if constexpr (NBWMAX > 1) { if (n_nb == 2) RN_L(2, 4); else RN_L(3, 4); }
@@ -486,7 +536,7 @@ __device__ void rn_fill_ktabs(const RPlan& R, float* lds, int NG, int Wb, int P)
 // PF: the next layer's plan entry, first A chunk and epilogue parameters are
 // loaded before each layer barrier (kernels with the register room: 512
 // threads).  Layers [i0, i1) (i1 < 0: to the end).
-template <bool NARROW = false, bool PF = false, int NBWMAX = 3>
+template <bool NARROW = false, bool PF = false, int NBWMAX = 3, bool PIPE = false>
 __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const float* flat, float* lds, int NG,
                                        int Wb, int P, float bn_s, unsigned long long* st = nullptr, int i0 = 0,
                                        int i1 = -1) {
@@ -508,7 +558,7 @@ __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const 
 #ifdef MZ_STAMPS
             if (st && i - i0 < 31) dbg = st + 1024 + 8 * (i - i0);
 #endif
-            rn_layer<NARROW, true, NBWMAX>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, &pf, dbg);
+            rn_layer<NARROW, true, NBWMAX, PIPE>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, &pf, dbg);
             if (i + 1 < i1) rn_prefetch<NARROW>(Ln, Wimg, flat, NG, P, pf);
 #ifdef MZ_STAMPS
             if (st && (threadIdx.x & 63) == 0 && i - i0 < 31) st[wv * 64 + 2 * (i - i0)] = __builtin_amdgcn_s_memtime();
@@ -1216,20 +1266,29 @@ __device__ __forceinline__ void rd_layer(const RLayer& L, const float (&a)[NCH][
 
 template <int I>
 __device__ __forceinline__ void rd_run(const RPlan& Rd, const float (&a0)[2][4][4], const float (&ar)[RD_NL][4][4],
-                                       const float4* ep_lds, float* lds, int ncols, float bn_s, float bn_r) {
+                                       const float4* ep_lds, float* lds, int ncols, float bn_s, float bn_r,
+                                       unsigned long long* st) {
     if constexpr (I < RD_NL) {
         const RLayer L = rn_layer_at(Rd, I);
-        if (threadIdx.x < 256) {
-            if constexpr (I == 0) {
-                rd_layer<2>(L, a0, ep_lds, lds, ncols, bn_s, bn_r);
-            } else {
-                const float (&a1)[1][4][4] = *reinterpret_cast<const float (*)[1][4][4]>(&ar[I]);
-                rd_layer<1>(L, a1, ep_lds + I * 64, lds, ncols, bn_s, bn_r);
-            }
+        if constexpr (I == 0) {
+#ifdef MZ_STAMPS
+            if (st && (threadIdx.x & 63) == 0) st[(threadIdx.x >> 6) * 64 + 63] = __builtin_amdgcn_s_memtime();
+#endif
+            rd_layer<2>(L, a0, ep_lds, lds, ncols, bn_s, bn_r);
+        } else {
+            const float (&a1)[1][4][4] = *reinterpret_cast<const float (*)[1][4][4]>(&ar[I]);
+            rd_layer<1>(L, a1, ep_lds + I * 64, lds, ncols, bn_s, bn_r);
         }
+#ifdef MZ_STAMPS
+        if (st && (threadIdx.x & 63) == 0) st[(threadIdx.x >> 6) * 64 + 2 * I] = __builtin_amdgcn_s_memtime();
+#endif
         __syncthreads();
-        rd_run<I + 1>(Rd, a0, ar, ep_lds, lds, ncols, bn_s, bn_r);
+#ifdef MZ_STAMPS
+        if (st && (threadIdx.x & 63) == 0) st[(threadIdx.x >> 6) * 64 + 2 * I + 1] = __builtin_amdgcn_s_memtime();
+#endif
+        rd_run<I + 1>(Rd, a0, ar, ep_lds, lds, ncols, bn_s, bn_r, st);
     }
+    (void)st;
 }
 
 extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r(RUnrollParams U) {
@@ -1247,18 +1306,12 @@ extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r(RUnr
     const int ncols = U.P * NG;
     float* hs = U.hs + bs * KH * H;
     float* ts = U.ts + bs * KH * H;
+    unsigned long long* st_r = nullptr;
+    unsigned long long* st_d = nullptr;
+#ifdef MZ_STAMPS
+    if (U.stamps && blockIdx.x == 0) { st_r = U.stamps; st_d = U.stamps + 512; }
+#endif
     float4* ep_lds = reinterpret_cast<float4*>(lds + U.rd_ep_off);   // [RD_NL][64] {bias, γ, β, 0}
-    // resident A fragments of the dynamics chain: issued first, they land
-    // while the representation runs (wave w = row block w)
-    const int lane = threadIdx.x & 63, ob = threadIdx.x >> 6;
-    float a0[2][4][4], ar[RD_NL][4][4];
-    {
-        const RLayer L0 = rn_layer_at(Rd, 0);
-        rn_load_a(a0[0], U.Wimg, L0, ob, 0, lane);
-        rn_load_a(a0[1], U.Wimg, L0, ob, 1, lane);
-#pragma unroll
-        for (int i = 1; i < RD_NL; ++i) rn_load_a(ar[i], U.Wimg, rn_layer_at(Rd, i), ob, 0, lane);
-    }
     for (int i = threadIdx.x; i < RD_NL * 64; i += blockDim.x) {
         const RLayer L = rn_layer_at(Rd, i >> 6);
         ep_lds[i] = reinterpret_cast<const float4*>(U.Wimg + L.ep_img)[i & 63];
@@ -1275,7 +1328,18 @@ extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r(RUnr
         rn_stage_l(lds + Rr.in_off, Rr.in_kb, NG, U.P, Rr.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
     }
     __syncthreads();
-    rn_run<true, true, 1>(Rr, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s);                  // :347
+    rn_run<true, true, 1, true>(Rr, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, st_r);      // :347
+    // resident A fragments of the dynamics chain (wave w = row block w), issued
+    // after the representation (live across it, they cost its code registers)
+    const int lane = threadIdx.x & 63, ob = threadIdx.x >> 6;
+    float a0[2][4][4], ar[RD_NL][4][4];
+    {
+        const RLayer L0 = rn_layer_at(Rd, 0);
+        rn_load_a(a0[0], U.Wimg, L0, ob, 0, lane);
+        rn_load_a(a0[1], U.Wimg, L0, ob, 1, lane);
+#pragma unroll
+        for (int i = 1; i < RD_NL; ++i) rn_load_a(ar[i], U.Wimg, rn_layer_at(Rd, i), ob, 0, lane);
+    }
     if (ok) rn_unstage_l(lds + Rr.out0_off, Rr.out0_kb, NG, U.P, H, t, [&](int f, float v) { hs[f] = v; });
     if (ok && t.f0 == 0) U.pr[bs * K1] = 0.0f;                                 // :352 zeros
     const float bn_r = 1.0f / U.bn_s;
@@ -1287,7 +1351,7 @@ extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r(RUnr
             rn_stage_l(lds + Rd.in_off, Rd.in_kb, NG, U.P, Rd.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? hp[f] * 2.0f : av; });
         }
         __syncthreads();
-        rd_run<0>(Rd, a0, ar, ep_lds, lds, ncols, U.bn_s, bn_r);              // :362, layers [0, split)
+        rd_run<0>(Rd, a0, ar, ep_lds, lds, ncols, U.bn_s, bn_r, s == 1 ? st_d : nullptr);   // :362, [0, split)
         if (ok) {
             if (s < K) rn_unstage_l(lds + Rd.out0_off, Rd.out0_kb, NG, U.P, H, t,
                                     [&](int f, float v) { hs[(size_t)s * H + f] = v; });

@@ -22,8 +22,9 @@ from muzero_jl_amd.networks import init_nets  # noqa: E402
 
 def show(st, name, dbg=None):
     st = st.reshape(8, 64).astype(np.int64)
+    st = st[st[:, 63] != 0]                # waves that ran (mz_runroll_chain_r has 4)
     t0 = st[:, 63].min()
-    print(f"== {name}: per layer [compute end - previous barrier exit | barrier wait] ticks, waves 0..7")
+    print(f"== {name}: per layer [compute end - previous barrier exit | barrier wait] ticks, waves 0..{len(st) - 1}")
     prev = st[:, 63].copy()
     tot_c = tot_w = 0
     for i in range(31):
