@@ -964,6 +964,8 @@ static RPlan rn_plan(const mz_handle* h, const std::vector<RSpec>& sp, int net, 
             if (R.L[i].kk > 1 && !R.L[i].otab && R.L[i].ktab < 0) R.L[i].ktab = region(R.L[i].K);
     }
     region(16 * 16 * 4);           // slack: past-the-tile lanes of k-blocked reads (MODE 3) read up to 15 columns on
+    R.n_ktab = 0;
+    for (int j = 0; j < R.n; ++j) R.n_ktab += R.L[j].kk > 1 && !R.L[j].otab;
     R.lds_floats = off;
     R.out0_kb = kb(R.out0_off);
     for (int j = 0; j < R.n; ++j) R.k[j] = rn_rk_pack(R.L[j]);

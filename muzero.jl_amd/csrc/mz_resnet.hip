@@ -517,6 +517,7 @@ __device__ __forceinline__ void rn_prefetch(const RLayer& L, const float* __rest
 
 // the k tables of the layers with a kernel > 1x1 (filled once per launch)
 __device__ void rn_fill_ktabs(const RPlan& R, float* lds, int NG, int Wb, int P) {
+    if (R.n_ktab == 0) return;                      // (walking the layer list costs a scalar load per layer)
     for (int i = 0; i < R.n; ++i) {
         const RLayer& L = R.L[i];
         if (L.kk == 1 || L.otab) continue;
@@ -624,6 +625,40 @@ __device__ __forceinline__ void rn_unstage_l(const float* src, int kb, int NG, i
     if (!kb) { rn_unstage(src, NG, n, t, put); return; }
 #pragma unroll 4
     for (int f = t.f0; f < n; f += t.fs) put(f, src[rn_conv_idx(1, f, t.g, NG, P)]);
+}
+
+// LDS tile [f][g] (plain or k-blocked) <- scale · row_g[f] for f < H (H % 4 == 0,
+// rows 16-byte aligned; row_g = nullptr: zeros): lane l reads the 16-byte piece
+// l / NG of row l mod NG (a wave instruction: 64 bytes of each of 16 rows, where
+// rn_stage's layout reads 4 bytes of each), four pieces in flight per thread;
+// the LDS writes of consecutive lanes stay on consecutive games' banks
+template <class RowFn>
+__device__ __forceinline__ void rn_stage_rows(float* dst, int kb, int NG, int P, int H, float scale, RowFn row) {
+    const int H4 = H >> 2, n4 = NG * H4, nt = blockDim.x, lg = __ffs(NG) - 1;   // NG a power of two
+    for (int i0 = threadIdx.x; i0 < n4; i0 += 4 * nt) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * nt;
+            v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (i < n4) {
+                const int g = i & (NG - 1);
+                const float* r = row(g);
+                if (r) v[u] = reinterpret_cast<const float4*>(r)[i >> lg];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * nt;
+            if (i < n4) {
+                const int g = i & (NG - 1), f = (i >> lg) * 4;
+                dst[rn_conv_idx(kb, f, g, NG, P)] = v[u].x * scale;
+                dst[rn_conv_idx(kb, f + 1, g, NG, P)] = v[u].y * scale;
+                dst[rn_conv_idx(kb, f + 2, g, NG, P)] = v[u].z * scale;
+                dst[rn_conv_idx(kb, f + 3, g, NG, P)] = v[u].w * scale;
+            }
+        }
+    }
 }
 
 // Batched forward of one net (mz_net_forward): x (in_feat, n) -> out0, out1.
@@ -1000,21 +1035,38 @@ extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RS
     const int NG = P.ng, t0 = blockIdx.x * NG, H = P.H, S = P.S;
     unsigned long long* st = nullptr;
 #ifdef MZ_STAMPS
-    if (P.stamps && blockIdx.x == 0 && P.s == 0) st = P.stamps + blockIdx.y * 512;
+    if (P.stamps && blockIdx.x == 0 && P.s == 0) st = P.stamps + blockIdx.y * 1024;   // 12 waves x 64
     if (st && (threadIdx.x & 63) == 0) st[(threadIdx.x >> 6) * 64 + 60] = __builtin_amdgcn_s_memtime();
 #endif
     rn_fill_ktabs(R, lds, NG, P.W, P.P);
     const RnLane t = rn_lane(NG);
     const int gg = t0 + t.g;
     const bool ok = gg < P.G;
-    if (net == MZ_NET_PRED) {
-        const float* x = P.x_pred + (size_t)(ok ? gg : 0) * H;
-        rn_stage_l(lds + R.in_off, R.in_kb, NG, P.P, H, t, [&](int f) { return ok ? x[f] : 0.0f; });
+    // prediction(parent h) and dynamics(2h ⊕ a/|A|) both read x_pred, the
+    // parent's h before the tree step doubled it in place (Q1): 2·x_pred is that
+    // doubled value bit for bit.  The dynamics' a/|A| plane (features H ..
+    // in_feat - 1): the leaf actions are loaded first, so their latency overlaps
+    // the row loads; a/|A| as the host's table, (float)((a + 1) / |A|) in f64
+    const int np = R.in_feat - H, npl = net == MZ_NET_DYN ? NG * np : 0;
+    int la = 0;
+    if ((int)threadIdx.x < npl) {
+        const int gq = t0 + (int)threadIdx.x / np;
+        if (gq < P.G) la = P.gst[(size_t)gq * RG_INTS + RG_LEAF_A];
+    }
+    if ((H & 3) == 0) {
+        rn_stage_rows(lds + R.in_off, R.in_kb, NG, P.P, H, net == MZ_NET_PRED ? 1.0f : 2.0f, [&](int g) {
+            return t0 + g < P.G ? P.x_pred + (size_t)(t0 + g) * H : nullptr;
+        });
     } else {
-        const int* st = P.gst + (size_t)(ok ? gg : 0) * RG_INTS;
-        const float* x = P.hid + ((size_t)(ok ? gg : 0) * (S + 1) + st[RG_LEAF_E]) * H;
-        const float av = P.aval_tab[st[RG_LEAF_A]];
-        rn_stage_l(lds + R.in_off, R.in_kb, NG, P.P, R.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? x[f] : av; });
+        const float* x = P.x_pred + (size_t)(ok ? gg : 0) * H;
+        const float sc = net == MZ_NET_PRED ? 1.0f : 2.0f;
+        rn_stage_l(lds + R.in_off, R.in_kb, NG, P.P, H, t, [&](int f) { return ok ? x[f] * sc : 0.0f; });
+    }
+    for (int i = threadIdx.x; i < npl; i += blockDim.x) {
+        const int g = i / np, f = H + (i - g * np);
+        if (i >= (int)blockDim.x && t0 + g < P.G) la = P.gst[(size_t)(t0 + g) * RG_INTS + RG_LEAF_A];
+        const float av = t0 + g < P.G ? (float)((double)(la + 1) / (double)P.A) : 0.0f;
+        lds[R.in_off + rn_conv_idx(R.in_kb, f, g, NG, P.P)] = av;
     }
     __syncthreads();
     rn_run(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st);

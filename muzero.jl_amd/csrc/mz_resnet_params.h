@@ -98,6 +98,7 @@ struct RPlan {
     // from the engine's table buffer at tab_src to LDS at tab_lds (tab_n ints) by
     // the kernel; zero_off = an LDS float kept 0 (out-of-board taps, padding)
     int tab_src, tab_lds, tab_n, zero_off;
+    int n_ktab;                        // layers with a k table (kernel > 1x1 read through rn_fill_ktabs' tables)
 };
 
 struct RNetParams {

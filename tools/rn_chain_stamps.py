@@ -51,6 +51,8 @@ def main():
     if "--no-build" not in sys.argv:
         subprocess.run(["/opt/rocm/bin/hipcc"] + mzbuild.FLAGS + ["-DMZ_STAMPS", "-shared", "-o", lib] + srcs,
                        check=True)
+    if "--build-only" in sys.argv:
+        return
     abi._lib = None
     L = abi.load_library(lib)
     L.mz_debug_stamps.restype = ctypes.c_int

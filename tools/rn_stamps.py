@@ -24,7 +24,9 @@ def main():
     lib = os.path.join(pkg.PKG_DIR, "lib", "libmz_stamps.so")
     srcs = [os.path.join(pkg.PKG_DIR, "csrc", s) for s in mzbuild.SOURCES]
     if "--no-build" not in sys.argv:
-        subprocess.run(["/opt/rocm/bin/hipcc"] + mzbuild.FLAGS + ["-DMZ_STAMPS", "-o", lib] + srcs, check=True)
+        subprocess.run(["/opt/rocm/bin/hipcc"] + mzbuild.FLAGS + ["-DMZ_STAMPS", "-shared", "-o", lib] + srcs, check=True)
+    if "--build-only" in sys.argv:
+        return
     abi._lib = None
     L = abi.load_library(lib)
     L.mz_debug_stamps.restype = ctypes.c_int
@@ -37,12 +39,12 @@ def main():
     obs, legal, tp = random_positions(ttt.BatchedTicTacToe, G, seed=100)
     for k in range(2):
         eng.mcts_search(obs, legal, tp, rng_step=k)
-    out = np.zeros(128 * 8, np.uint64)
-    assert L.mz_debug_stamps(eng.h, out.ctypes.data_as(ctypes.c_void_p), 128) == 0
+    out = np.zeros(256 * 8, np.uint64)
+    assert L.mz_debug_stamps(eng.h, out.ctypes.data_as(ctypes.c_void_p), 256) == 0
     for y, name in ((0, "pred"), (1, "dyn")):
-        st = out[y * 512:(y + 1) * 512].reshape(8, 64).astype(np.int64)
+        st = out[y * 1024:y * 1024 + 768].reshape(12, 64).astype(np.int64)
         t0 = st[:, 63].min()
-        print(f"== {name}: per layer [compute end - previous barrier exit | barrier wait] ticks, waves 0..7")
+        print(f"== {name}: per layer [compute end - previous barrier exit | barrier wait] ticks, waves 0..11")
         prev = st[:, 63].copy()
         for i in range(31):
             if not st[:, 2 * i].any():
