@@ -97,6 +97,30 @@ __device__ __forceinline__ void rn_load_res(const RLayer& L, const float* lds, f
         }
 }
 
+// The common case of rn_epilogue, the same operations without per-element
+// branches: a full 16-row block (o < cout for all rows) and a relu / identity
+// activation; the layout, BatchNorm and residual choices are wave-uniform and
+// taken once, outside the element loops (OUT_KB, RES, RELU instances).
+template <int NB, bool OUT_KB, bool RES, bool RELU>
+__device__ __forceinline__ void rn_epilogue_full(const RLayer& L, const float (&d)[NB][4], float* lds, int ob, int kl,
+                                                 const int (&n)[NB], int ncols, const float (&res)[NB][4]) {
+    float* out = lds + L.out_off;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            v[r] = d[i][r];
+            if constexpr (RES) v[r] = v[r] + res[i][r];
+            if constexpr (RELU) v[r] = mz_relu(v[r]);
+        }
+        if (n[i] < ncols) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) out[rn_out_idx(OUT_KB, ob, kl, r, n[i], ncols)] = v[r];
+        }
+    }
+}
+
 template <int NB>
 __device__ __forceinline__ void rn_epilogue(const RLayer& L, const mz_f32x4 (&acc)[NB][4], const float (&ep)[3][4],
                                             float* lds, int ob, int kl, const int (&n)[NB], int ncols, float bn_s,
@@ -137,6 +161,19 @@ __device__ __forceinline__ void rn_epilogue(const RLayer& L, const mz_f32x4 (&ac
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int i = 0; i < NB; ++i) d[i][r] = ep[1][r] * q[i][r] + ep[2][r];
+    }
+    if ((ob + 1) * 16 <= L.cout && L.act != MZ_ACT_TANH) {
+        const bool relu = L.act == MZ_ACT_RELU;
+#define RN_EF(KB, RS, RL) rn_epilogue_full<NB, KB, RS, RL>(L, d, lds, ob, kl, n, ncols, res)
+        if (L.out_kb) {
+            if (L.res_add) { if (relu) RN_EF(true, true, true); else RN_EF(true, true, false); }
+            else { if (relu) RN_EF(true, false, true); else RN_EF(true, false, false); }
+        } else {
+            if (L.res_add) { if (relu) RN_EF(false, true, true); else RN_EF(false, true, false); }
+            else { if (relu) RN_EF(false, false, true); else RN_EF(false, false, false); }
+        }
+#undef RN_EF
+        return;
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
