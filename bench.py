@@ -314,7 +314,7 @@ def main():
     lstep_ms = float(np.mean([a.elapsed_time(b) for a, b in lev]))
     # the learner's dominant kernel: FC world 1 = the whole step is one launch
     # (mz_learn_small*), timed by the events around it; ResNet = the unroll
-    # (mz_runroll_chain + mz_runroll_pred), timed by the engine's events on its launch stream
+    # (chain + predictions, the pair mz_learner_variant names), timed by the engine's events on its launch stream
     if resnet:
         eng.debug_enable(4)
         eng.debug_kernel_time()
@@ -323,7 +323,7 @@ def main():
         torch.cuda.synchronize()
         t_ms, n_l = eng.debug_kernel_time()
         eng.debug_enable(0)
-        lkern, lkern_ms = "mz_runroll_chain+mz_runroll_pred", t_ms / n_l
+        lkern, lkern_ms = eng.learner_variant(), t_ms / n_l
     else:
         lkern = "mz_learn_small1" if world == 1 else None
         lkern_ms = lstep_ms

@@ -408,6 +408,10 @@ int mz_checkpoint_load(mz_handle* h, const char* path, int64_t* training_step);
  * MZ_SEARCH_KERNEL=tile16|small (read at create) forces a family.          */
 const char* mz_search_variant(const mz_handle* h);
 
+/* The learner unroll's kernels of the last ResNet learner step, "+"-joined
+ * (e.g. mz_runroll_chain_r+mz_runroll_pred_n1), for profiles; "none" before. */
+const char* mz_learner_variant(const mz_handle* h);
+
 /* Synchronize the handle's stream. */
 int mz_sync(mz_handle* h);
 

@@ -85,6 +85,7 @@ SIGNATURES = {
     "mz_checkpoint_save": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int64]),
     "mz_checkpoint_load": (ctypes.c_int, [_VP, ctypes.c_char_p, _VP]),
     "mz_search_variant": (ctypes.c_char_p, [_VP]),
+    "mz_learner_variant": (ctypes.c_char_p, [_VP]),
     "mz_sync": (ctypes.c_int, [_VP]),
 }
 
@@ -462,6 +463,9 @@ class Engine:
 
     def search_variant(self):
         return self.lib.mz_search_variant(self.h).decode()
+
+    def learner_variant(self):
+        return self.lib.mz_learner_variant(self.h).decode()
 
     def sync(self):
         self._check(self.lib.mz_sync(self.h), "mz_sync")

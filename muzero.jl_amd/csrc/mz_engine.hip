@@ -210,6 +210,7 @@ struct mz_handle {
     std::vector<int> inv_tile, inv_small;
     int* d_inv_tile = nullptr; int* d_inv_small = nullptr;
     std::string last_variant = "none";
+    std::string last_lvariant = "none";     // the learner unroll's kernels (mz_learner_variant)
     int force_T = 0;                        // MZ_SMALL_T=1|2|4 (tests)
     float* d_hid = nullptr;
     float* d_obs = nullptr; uint8_t* d_legal = nullptr; int32_t* d_tp = nullptr;
@@ -1825,6 +1826,7 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
         MZ_TRY(h, hipEventRecord(e0, st));
     }
     if (std::getenv("MZ_RUNROLL_FUSED")) {          // the one-kernel unroll (pred inside the chain)
+        h->last_lvariant = "mz_runroll_kernel";
         MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_kernel, dim3((B + U.ng - 1) / U.ng), dim3(RN_THREADS),
                                   args, runroll_lds(h), st));
     } else {                                        // chain on narrow tiles, then the B·K predictions
@@ -1832,6 +1834,9 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
         // tiles of one column block: the 1-block instances (a fifth of the code)
         const bool nb1 = (U.P * U.ng_l + 15) / 16 == 1;
         U.rd_ep_off = (int)(h->rn_lds_l / 4);
+        static const bool wide_p = std::getenv("MZ_RN_PRED_WIDE") != nullptr;
+        h->last_lvariant = std::string(h->rd_chain ? "mz_runroll_chain_r" : nb1 ? "mz_runroll_chain1" : "mz_runroll_chain") +
+                           (wide_p ? "+mz_runroll_pred" : nb1 ? "+mz_runroll_pred_n1" : "+mz_runroll_pred_n");
         if (h->rd_chain)
             MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_chain_r, dim3((B + U.ng_l - 1) / U.ng_l),
                                       dim3(RD_THREADS), args, rd_chain_lds(h), st));
@@ -2177,6 +2182,11 @@ int mz_debug_stamps(mz_handle* h, unsigned long long* out, int n_blocks) {
 const char* mz_search_variant(const mz_handle* h) {
     if (!h) return "";
     return h->last_variant.c_str();
+}
+
+const char* mz_learner_variant(const mz_handle* h) {
+    if (!h) return "";
+    return h->last_lvariant.c_str();
 }
 
 // ------------------------------------------------ device self-play + replay

@@ -21,16 +21,23 @@ pmc() {  # tag, bench args, kernels...
   python tools/pmc_kernels.py $O/pmc2_${T}_${t}.json "python bench.py $args" $O/${t}_fetch $O/${t}_write $O/${t}_sq -- "$@" > /dev/null || exit 1
 }
 B1="--steps 10 --warmup 2 --no-cpu --pipeline-moves 0 --train-moves 0 --learner-steps 50"
+if [ -z "$SKIP_DEFAULT" ]; then
 run kt_default 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_default -o run -- python bench.py
 pmc default "$B1" mz_search_small2 mz_learn_small1 mz_bp_tile mz_bp_dw mz_bp_fold
+fi
+if [ -z "$SKIP_RESNET" ]; then
 BR="--net resnet --steps 4 --warmup 1 --no-cpu --pipeline-moves 0 --train-moves 0 --learner-steps 10"
-run kt_resnet 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_resnet -o run -- python bench.py --net resnet --no-cpu
-pmc resnet "$BR" mz_rsearch_nets mz_runroll_chain mz_runroll_pred mz_rsearch_tree_lds mz_rsearch_root mz_learner_grad_kernel
+run kt_resnet 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_resnet -o run -- python bench.py --net resnet
+pmc resnet "$BR" mz_rsearch_nets mz_runroll_chain_r mz_runroll_pred_n1 mz_rsearch_tree_lds mz_rsearch_root mz_learner_grad_kernel
+fi
+if [ -z "$SKIP_ATARI" ]; then
 BA="--game atari --steps 2 --warmup 1 --no-cpu --learner-steps 10"
-run kt_atari 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_atari -o run -- python bench.py --game atari --no-cpu
+run kt_atari 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_atari -o run -- python bench.py --game atari
 pmc atari "$BA" mz_rsearch_nets mz_runroll_chain mz_runroll_pred mz_rsearch_tree_lds32 mz_downsample_kernel
+fi
 for f in default resnet atari; do
+  [ -f $O/kt_$f.log ] || continue
   grep '^{' $O/kt_$f.log | tail -1 > $O/${T}_${f}_bench_under_rocprof.json
   cp $O/kt_$f/run_kernel_stats.csv $O/${T}_${f}_kernel_stats.csv
 done
-head -5 $O/${T}_default_kernel_stats.csv
+ls $O

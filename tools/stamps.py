@@ -25,7 +25,7 @@ def main():
     srcs = [os.path.join(pkg.PKG_DIR, "csrc", s) for s in mzbuild.SOURCES]
     if "--no-build" not in sys.argv:
         extra = os.environ.get("STAMPS_DEFS", "").split()
-        subprocess.run(["/opt/rocm/bin/hipcc"] + mzbuild.FLAGS + ["-DMZ_STAMPS"] + extra + ["-o", lib] + srcs,
+        subprocess.run(["/opt/rocm/bin/hipcc"] + mzbuild.FLAGS + ["-DMZ_STAMPS"] + extra + ["-shared", "-o", lib] + srcs,
                        check=True)
     abi._lib = None
     L = abi.load_library(lib)
