@@ -129,6 +129,8 @@ def main():
                     help="timed moves of the device self-play loop (0 = skip that leg)")
     ap.add_argument("--sims", type=int, default=None, help="sims per move (default 50; atari 200)")
     ap.add_argument("--learner-steps", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="learner batch size (default conf.batch_size = 32; SURVEY §8d config 3 also names 2048)")
     ap.add_argument("--train-moves", type=int, default=20,
                     help="timed moves of the actor-learner loop mz_train_run (0 = skip that leg)")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -265,7 +267,7 @@ def main():
     # ---- learner leg: ref_semantics learner step at B = batch_size (32) on
     # batches sampled on the device from this rank's replay shard (§8f-2),
     # gradient bucket all-reduced over RCCL when world > 1
-    B, K = conf.batch_size, conf.num_unroll_steps
+    B, K = args.batch or conf.batch_size, conf.num_unroll_steps
     grad = torch.empty(eng.grad_count(), dtype=torch.float32, device=dev)
     losses = torch.empty(8, dtype=torch.float32, device=dev)
 
@@ -366,7 +368,7 @@ def main():
     train = None
     if args.train_moves > 0 and world == 1 and game is not atari:
         eng.selfplay_init(env_kind, G, max(G, conf.replay_buffer_size))
-        eng.train_init(B)
+        eng.train_init(conf.batch_size)
         eng.train_run(3, move0=mv, game_offset=rank * G, stream=sp)
         mv += 3
         torch.cuda.synchronize()

@@ -1834,7 +1834,11 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
         // tiles of one column block: the 1-block instances (a fifth of the code)
         const bool nb1 = (U.P * U.ng_l + 15) / 16 == 1;
         U.rd_ep_off = (int)(h->rn_lds_l / 4);
-        static const bool wide_p = std::getenv("MZ_RN_PRED_WIDE") != nullptr;
+        // the B·K predictions on wide tiles (ng items) once they fill the chip
+        // (B = 2048: 640 workgroups; one-item tiles there measured 2.4x slower),
+        // else one-item tiles (B = 32: 160 workgroups instead of 10)
+        static const bool wide_env = std::getenv("MZ_RN_PRED_WIDE") != nullptr;
+        const bool wide_p = wide_env || (B * KH + U.ng - 1) / U.ng >= h->n_cu;
         h->last_lvariant = std::string(h->rd_chain ? "mz_runroll_chain_r" : nb1 ? "mz_runroll_chain1" : "mz_runroll_chain") +
                            (wide_p ? "+mz_runroll_pred" : nb1 ? "+mz_runroll_pred_n1" : "+mz_runroll_pred_n");
         if (h->rd_chain)
@@ -1844,9 +1848,8 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
             MZ_TRY(h, hipLaunchKernel(nb1 ? (const void*)mz_runroll_chain1 : (const void*)mz_runroll_chain,
                                       dim3((B + U.ng_l - 1) / U.ng_l), dim3(RN_THREADS),
                                       args, h->rn_lds_l, st));
-        // the B·K predictions and reward heads: narrow tiles unless MZ_RN_PRED_WIDE
-        static const bool wide = std::getenv("MZ_RN_PRED_WIDE") != nullptr;
-        if (wide)
+        // the B·K predictions and reward heads (wide_p above)
+        if (wide_p)
             MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred, dim3((B * KH + U.ng - 1) / U.ng, U.K > 0 ? 2 : 1),
                                       dim3(RN_THREADS), args, runroll_lds(h), st));
         else
