@@ -80,15 +80,26 @@ def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0, resnet=False,
                        f"oracle/mz_oracle.c on {threads} host thread{'s' if threads > 1 else ''}, {dt:.1f} s")
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, line=None):
     """HBM bytes per launch of `kernel` ("a+b": the sum over a launch pair)
     from the committed PMC summaries
     (profiles/pmc_*.json of tools/pmc_summary.py, profiles/pmc2_*.json of
     tools/pmc_kernels.py: FETCH_SIZE x2 for the 16 B/lane image reads, per
-    MI355X_MICROARCH.md, + WRITE_SIZE); the latest round wins; None if none."""
+    MI355X_MICROARCH.md, + WRITE_SIZE); the latest round wins, and among
+    pmc2 summaries the bench line's own (`line` in the file name: default /
+    resnet / atari — the same kernel runs different nets there); None if none."""
     if "+" in kernel:
-        parts = [pmc_traffic(k) for k in kernel.split("+")]
+        parts = [pmc_traffic(k, line) for k in kernel.split("+")]
         return None if any(p is None for p in parts) else sum(parts)
+    if line:
+        own = None
+        for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc2_*_{line}.json"))):
+            with open(pmc) as f:
+                rec = json.load(f).get("kernels", {}).get(kernel)
+            if rec and "hbm_bytes_per_launch_fetch_x2" in rec:
+                own = rec["hbm_bytes_per_launch_fetch_x2"]
+        if own is not None:
+            return own
     traffic = None
     for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
         with open(pmc) as f:
@@ -397,7 +408,8 @@ def main():
         # HBM bytes per launch from the committed PMC summary of THIS kernel
         # variant (tools/pmc_summary.py; latest round wins), else null
         variant = "mz_rsearch_nets" if resnet else eng.search_variant()
-        traffic = pmc_traffic(variant)
+        pmc_line = "atari" if game is atari else "resnet" if resnet else "default" if game is ttt else None
+        traffic = pmc_traffic(variant, pmc_line)
         # learner roofline (north_star: HBM GB/s and MFMA utilisation of the
         # learner): algorithmic FLOP of the unroll (2·B·(repr +
         # (K+1)·pred + K·dyn) MACs) + ADAM (~10 FLOP/param, FC one-launch step);
@@ -411,7 +423,7 @@ def main():
             lflop = f_unroll + (0 if resnet else 10 * nparam)
             lbytes = 0 if resnet else 28 * nparam
             lach = lflop / (lkern_ms * 1e-3) / 1e12
-            ltraffic = pmc_traffic(lkern)
+            ltraffic = pmc_traffic(lkern, pmc_line)
             hbm_gbs = (ltraffic if ltraffic else lbytes) / (lkern_ms * 1e-3) / 1e9
             lroof = {"bound": "mfma", "achieved": round(lach, 4), "peak": PEAK_F32, "unit": "TFLOP/s",
                      "frac": round(lach / PEAK_F32, 5), "traffic": ltraffic, "kernel": lkern,
