@@ -491,12 +491,13 @@ static bool sm_schedule(const mz_handle* h, const std::vector<int>& set, const s
         std::stable_sort(ready.begin(), ready.end(), [&](int a, int b) { return prio[a] > prio[b]; });
         // 4 groups of 16 rows per slot: the 16 lanes of a DPP row serve the
         // 16 rows of one group and broadcast one shared input vector
-        int fr[2] = {4, 4};
+        int fr[SM_SLOTS];
+        for (int x = 0; x < SM_SLOTS; ++x) fr[x] = 4;
         std::array<int, 2> kq = {0, 0};
         for (int i : ready) {
             const LayerSpec& L = h->layers[set[i]];
             const int nb = (L.out + 15) / 16;
-            for (int x = 0; x < 2; ++x)
+            for (int x = 0; x < SM_SLOTS; ++x)
                 if (fr[x] >= nb) {
                     st[i] = s; sl[i] = x; b0[i] = 4 * (4 - fr[x]); fr[x] -= nb; ++done;   // b0 in 4-row units
                     break;
@@ -537,7 +538,7 @@ static int build_small(mz_handle* h) {
     h->sm_n_root = (int)kq_r.size();
     const int nrec = h->sm_n_sim + h->sm_n_root;
     // weight / bias gather images: [rec][slot][q*64 + lane][16] and [rec][slot][row]
-    std::vector<int> sw((size_t)nrec * 2 * 256 * 16, -1), sb((size_t)nrec * 2 * 64, -1);
+    std::vector<int> sw((size_t)nrec * SM_SLOTS * 256 * 16, -1), sb((size_t)nrec * SM_SLOTS * 64, -1);
     auto fill = [&](const std::vector<int>& set, const std::vector<int>& st, const std::vector<int>& sl,
                     const std::vector<int>& b0, int rec0) {
         for (size_t i = 0; i < set.size(); ++i) {
@@ -545,12 +546,12 @@ static int build_small(mz_handle* h) {
             const int kq = 4 * ((L.in + 15) / 16), r = rec0 + st[i];
             for (int row = 0; row < L.out; ++row) {
                 const int srow = 4 * b0[i] + row;                       // slot row
-                sb[((size_t)r * 2 + sl[i]) * 64 + srow] = (int)(L.flux_b + row);
+                sb[((size_t)r * SM_SLOTS + sl[i]) * 64 + srow] = (int)(L.flux_b + row);
                 for (int q = 0; q < 4; ++q)
                     for (int j = 0; j < kq; ++j) {
                         const int k = q * kq + j;
                         if (k >= L.in) continue;
-                        sw[(((size_t)r * 2 + sl[i]) * 256 + q * 64 + srow) * 16 + j] =
+                        sw[(((size_t)r * SM_SLOTS + sl[i]) * 256 + q * 64 + srow) * 16 + j] =
                             (int)(L.flux_w + row + (size_t)L.out * k);
                     }
             }

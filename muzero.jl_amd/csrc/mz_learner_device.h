@@ -117,25 +117,71 @@ __device__ __forceinline__ void lg_step_terms(int t, int a, int A, int v_act, in
 // j·(MZ_L2_BLOCKS·256) as one thread's ascending f64 sum; four per pass with
 // every load issued before any store (the fused ADAM's f64 chains overlap).
 // ad.on: ADAM with ∇ = 2θ in place (= mz_adam_kernel, gscale 1), else G = 2θ.
+// ADAM operands of one 4-group (adam_update4's loads, issued ahead)
+struct LgAdamOps { float x[4], mo[4], vo[4]; int it[4], is[4]; };
+__device__ __forceinline__ void lg_adam_load(const LgAdam& ad, const float* P, size_t i0, size_t stride, size_t rem,
+                                             bool on, LgAdamOps& o) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const size_t i = i0 + u * stride;
+        const bool in = u * stride < rem;
+        o.x[u] = in ? P[i] : 0.0f;
+        o.mo[u] = in && on ? ad.M[i] : 0.0f; o.vo[u] = in && on ? ad.V[i] : 0.0f;
+        o.it[u] = in && on ? ad.inv_tile[i] : -1; o.is[u] = in && on ? ad.inv_small[i] : -1;
+    }
+}
+// adam_update4's arithmetic and stores on preloaded operands
+__device__ __forceinline__ void lg_adam_store(const LgAdam& ad, float* P, size_t i0, size_t stride, size_t rem,
+                                              const LgAdamOps& o) {
+    const double b1 = 0.9, b2 = 0.999, eps = 1e-8;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        if (u * stride >= rem) continue;
+        const size_t i = i0 + u * stride;
+        const float g = o.x[u] * 2.0f;
+        const float m = (float)(b1 * (double)o.mo[u] + (1.0 - b1) * (double)g);
+        const float g2 = g * g;
+        const float v = (float)(b2 * (double)o.vo[u] + (1.0 - b2) * (double)g2);
+        ad.M[i] = m; ad.V[i] = v;
+        const float d = (float)((double)m / (1.0 - ad.bp1) / (sqrt((double)v / (1.0 - ad.bp2)) + eps) * ad.eta);
+        const float xn = o.x[u] - d;
+        P[i] = xn;
+        mz_scatter(xn, o.it[u], ad.Wp, ad.Bp);
+        mz_scatter(xn, o.is[u], ad.smw, ad.smb);
+    }
+}
+
+// Σθ² of slice blk of net (f64, this thread's elements in ascending order) and
+// the ADAM step (∇ = 2θ) or ∇ into G.  Software-pipelined: the next 4-group's
+// loads are issued before this group's stores (the stores could alias them
+// as far as the compiler knows, so a plain loop waits one memory latency per
+// group).
 __device__ __forceinline__ double lg_l2_slice(int net, int blk, int tid, const size_t* netoff, float* flat,
                                               float* G, const LgAdam& ad) {
     const size_t off = netoff[net], cnt = netoff[3 + net];
     double s = 0.0;
     const size_t stride = (size_t)MZ_L2_BLOCKS * MZ_THREADS;
-    for (size_t i = (size_t)blk * MZ_THREADS + tid; i < cnt; i += 4 * stride) {
-        float x[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) x[u] = i + u * stride < cnt ? flat[off + i + u * stride] : 0.0f;
+    size_t i = (size_t)blk * MZ_THREADS + tid;
+    if (i >= cnt) return s;
+    LgAdam a = ad;                                  // the net's slice of the per-parameter arrays
+    if (ad.on) { a.M += off; a.V += off; a.inv_tile += off; a.inv_small += off; }
+    LgAdamOps cur;
+    lg_adam_load(a, flat + off, i, stride, cnt - i, ad.on, cur);
+    for (; i < cnt; i += 4 * stride) {
+        LgAdamOps nxt;
+        const size_t in = i + 4 * stride;
+        if (in < cnt) lg_adam_load(a, flat + off, in, stride, cnt - in, ad.on, nxt);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (i + u * stride < cnt) s += (double)x[u] * (double)x[u];
+            if (i + u * stride < cnt) s += (double)cur.x[u] * (double)cur.x[u];
         if (ad.on) {
-            adam_update4(ad, flat, off + i, stride, cnt - i, x);
+            lg_adam_store(a, flat + off, i, stride, cnt - i, cur);
         } else {
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                if (i + u * stride < cnt) G[off + i + u * stride] = x[u] * 2.0f;
+                if (i + u * stride < cnt) G[off + i + u * stride] = cur.x[u] * 2.0f;
         }
+        cur = nxt;
     }
     return s;
 }

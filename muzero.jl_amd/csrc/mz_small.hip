@@ -235,7 +235,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     for (int i = tid; i < (int)pbterm_count(S); i += SM_THREADS) l_pbterm[i] = P.pbterm[i];
     for (int i = tid; i < nrec * SM_REC_INTS; i += SM_THREADS) rec[i] = P.rec[i];
     __syncthreads();
-    for (int i = tid; i < nrec * 128; i += SM_THREADS)
+    for (int i = tid; i < nrec * SM_SLOTS * 64; i += SM_THREADS)
         rec[4 * i + 3] = __float_as_int(P.bias[i]);
     // ---- root inputs
     for (int i = tid; i < T * P.obs_feat; i += SM_THREADS) {
@@ -443,7 +443,7 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
     for (int i = tid; i < P.act_total; i += SM_THREADS) act[i] = 0.0f;
     for (int i = tid; i < nrec * SM_REC_INTS; i += SM_THREADS) rec[i] = P.rec[i];
     __syncthreads();
-    for (int i = tid; i < nrec * 128; i += SM_THREADS) rec[4 * i + 3] = __float_as_int(P.bias[i]);
+    for (int i = tid; i < nrec * SM_SLOTS * 64; i += SM_THREADS) rec[4 * i + 3] = __float_as_int(P.bias[i]);
     for (int i = tid; i < T * P.obs_feat; i += SM_THREADS) {
         const int gl = i / P.obs_feat, k = i - gl * P.obs_feat;
         act[P.x_rep + k * T + gl] = tile0 + gl < P.B ? P.obs[(size_t)(tile0 + gl) * P.obs_feat + k] : 0.0f;
@@ -546,15 +546,16 @@ __device__ __forceinline__ void learn_body(const SmallUnrollParams& P, const Lea
 #endif
     } else {
         const int half = tid >> 8, t256 = tid & (MZ_THREADS - 1);
-        const int vb = ((int)blockIdx.x - L.nU) * 2 + half;
+        const int vb = ((int)blockIdx.x - L.nU) * SM_SLOTS + half;
+        const bool vin = vb < 3 * MZ_L2_BLOCKS;       // (SM_SLOTS not dividing the slice count: idle groups)
         const int net = vb / MZ_L2_BLOCKS, blk = vb % MZ_L2_BLOCKS;
-        red[tid] = lg_l2_slice(net, blk, t256, L.netoff, L.flat, nullptr, L.ad);
+        red[tid] = vin ? lg_l2_slice(net, blk, t256, L.netoff, L.flat, nullptr, L.ad) : 0.0;
         __syncthreads();
         for (int o = MZ_THREADS / 2; o > 0; o >>= 1) {            // lg_tree256 on each half
             if (t256 < o) red[tid] += red[tid + o];
             __syncthreads();
         }
-        if (t256 == 0) L.part[net * MZ_L2_BLOCKS + blk] = red[tid];
+        if (t256 == 0 && vin) L.part[net * MZ_L2_BLOCKS + blk] = red[tid];
     }
     lg_fold(P.B, P.K, vsq, cet, L.gscale, nullptr, L.part, L.counter, L.out);
 }

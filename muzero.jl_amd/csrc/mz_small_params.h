@@ -4,9 +4,15 @@
 #include "mz_internal.h"
 #include "mz_selfplay_params.h"
 
-#define SM_THREADS 512
+// SM_SLOTS 64-row slots per stage, 256 threads each (build-time choice: more
+// slots = fewer, wider stages and fewer resident weight registers per thread)
+#ifndef SM_SLOTS
 #define SM_SLOTS 2
+#endif
+#define SM_THREADS (256 * SM_SLOTS)
+#ifndef SM_MAX_SIM
 #define SM_MAX_SIM 8       // stages of the prediction ‖ dynamics schedule
+#endif
 #define SM_MAX_ROOT 6      // stages of the representation schedule
 
 typedef float sm_f32x4 __attribute__((ext_vector_type(4)));
@@ -76,5 +82,5 @@ struct LearnParams {
     float* terms; float* flat; const size_t* netoff; double* part; unsigned* counter; float* out;
     LgAdam ad;
 };
-#define LEARN_L2_GROUPS (3 * MZ_L2_BLOCKS / 2)
+#define LEARN_L2_GROUPS ((3 * MZ_L2_BLOCKS + SM_SLOTS - 1) / SM_SLOTS)
 
