@@ -48,40 +48,218 @@ __device__ __forceinline__ bp_f32x4 bp_gemm_block(int nk, int kq, FA fa, FB fb) 
     return acc;
 }
 
-// y = act(W x + b) for the tile (all 256 threads; rows in blocks of 16 per wave)
-__device__ __forceinline__ void bp_dense_fwd(const BpApp& P, const float* __restrict__ flat, float* T) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
+// y = act(W x + b), output rows ob·16 .. ob·16 + 15 of the tile (one wave)
+__device__ __forceinline__ void bp_dense_fwd_blk(const BpApp& P, const float* __restrict__ flat, float* T, int ob) {
+    const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
     const float* W = flat + P.w_off;
     const float* X = T + P.x;
     float* Y = T + P.y;
-    const int nob = (P.out + 15) >> 4, nk = (P.in + 3) >> 2;
-    for (int ob = wave; ob < nob; ob += 4) {
-        const int o = ob * 16 + m;
+    const int nk = (P.in + 3) >> 2;
+    const int o = ob * 16 + m;
+    const bool oin = o < P.out;
+    const bp_f32x4 acc = bp_gemm_block(nk, kq,
+        [&](int i) { return oin && i < P.in ? W[o + (size_t)P.out * i] : 0.0f; },
+        [&](int i) { return i < P.in ? X[i * 16 + m] : 0.0f; });
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int oo = ob * 16 + kq * 4 + r;
+        if (oo < P.out) Y[oo * 16 + m] = bp_act(P.act, acc[r] + flat[P.b_off + oo]);
+    }
+}
+// y = act(W x + b) for the tile (all 256 threads; rows in blocks of 16 per wave)
+__device__ __forceinline__ void bp_dense_fwd(const BpApp& P, const float* __restrict__ flat, float* T) {
+    const int wave = threadIdx.x >> 6, nob = (P.out + 15) >> 4;
+    for (int ob = wave; ob < nob; ob += 4) bp_dense_fwd_blk(P, flat, T, ob);
+}
+
+// G[x] += Wᵀ dZ with dZ = G[y] ⊙ act'(y) formed as the operand is loaded;
+// input rows ib·16 .. ib·16 + 15 (one wave)
+__device__ __forceinline__ void bp_dense_dx_blk(const BpApp& P, const float* __restrict__ flat, const float* T,
+                                                float* G, int ib) {
+    const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
+    const float* W = flat + P.w_off;
+    const float* DY = G + P.y;
+    const float* Y = T + P.y;
+    float* DX = G + P.x;
+    const int nk = (P.out + 3) >> 2;
+    const int i = ib * 16 + m;
+    const bool iin = i < P.in;
+    const bp_f32x4 acc = bp_gemm_block(nk, kq,
+        [&](int o) { return iin && o < P.out ? W[o + (size_t)P.out * i] : 0.0f; },
+        [&](int o) { return o < P.out ? bp_dz(P.act, DY[o * 16 + m], Y[o * 16 + m]) : 0.0f; });
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int ii = ib * 16 + kq * 4 + r;
+        if (ii < P.in) DX[ii * 16 + m] += acc[r];
+    }
+}
+__device__ __forceinline__ void bp_dense_dx(const BpApp& P, const float* __restrict__ flat, const float* T,
+                                            float* G) {
+    const int wave = threadIdx.x >> 6, nib = (P.in + 15) >> 4;
+    for (int ib = wave; ib < nib; ib += 4) bp_dense_dx_blk(P, flat, T, G, ib);
+}
+
+// Tile arenas, loss terms and reward read-outs zeroed, the observation staged
+__device__ __forceinline__ void bp_prologue(const BpParams& Q, float* T, float* G) {
+    const int tid = threadIdx.x, nt = blockDim.x, t0 = blockIdx.x * 16, K1 = Q.K + 1;
+    for (int e = tid; e < Q.tile_floats; e += nt) G[e] = 0.0f;
+    for (int e = tid; e < 16 * K1 * 3; e += nt) {
+        const int b = t0 + e / (K1 * 3);
+        if (b < Q.B) Q.terms[(size_t)t0 * K1 * 3 + e] = 0.0f;
+    }
+    for (int e = tid; e < 16 * K1; e += nt) {                 // rewards: 0 at step 0 (and without heads)
+        const int b = t0 + e / K1;
+        if (b < Q.B) Q.pr[(size_t)t0 * K1 + e] = 0.0f;
+    }
+    for (int e = tid; e < Q.obs_feat * 16; e += nt) {        // observation_batch (:347)
+        const int f = e >> 4, s = e & 15, b = t0 + s;
+        T[Q.obs_t + e] = b < Q.B ? Q.obs[(size_t)b * Q.obs_feat + f] : 0.0f;
+    }
+}
+
+// make_dynamics_input (:293-304) over the threads [t, t + nt) of the block
+__device__ __forceinline__ void bp_concat_fwd(const BpParams& Q, const BpApp& P, float* T, int t, int nt) {
+    const int t0 = blockIdx.x * 16, K1 = Q.K + 1;
+    for (int e = t; e < P.out * 16; e += nt) {
+        const int i = e >> 4, s = e & 15, b = t0 + s;
+        float v;
+        if (i < P.in) v = T[P.x + e] * 2.0f;
+        else v = b < Q.B ? Q.actions[(size_t)b * K1 + P.step] / (float)Q.A : 0.0f;
+        T[P.y + e] = v;
+    }
+}
+
+__device__ void bp_heads(const BpParams& Q, float* T, float* G);
+
+extern "C" __global__ __launch_bounds__(256) void mz_bp_tile(BpParams Q) {
+    const int tid = threadIdx.x;
+    float* T = Q.act + (size_t)blockIdx.x * Q.tile_floats;
+    float* G = Q.grad + (size_t)blockIdx.x * Q.tile_floats;
+    bp_prologue(Q, T, G);
+    __syncthreads();
+    // ---- forward: representation, K dynamics steps, K+1 predictions (Q10)
+    for (int a = 0; a < Q.n_app; ++a) {
+        const BpApp P = Q.apps[a];
+        if (P.op == BP_DENSE) bp_dense_fwd(P, Q.flat, T);
+        else bp_concat_fwd(Q, P, T, tid, 256);
+        __syncthreads();
+    }
+    bp_heads(Q, T, G);
+    __syncthreads();
+    // ---- backward, reverse order
+    for (int a = Q.n_app - 1; a >= 0; --a) {
+        const BpApp P = Q.apps[a];
+        if (P.op == BP_DENSE) {
+            bp_dense_dx(P, Q.flat, T, G);
+        } else {                                              // ∂(2h)/∂h
+            for (int e = tid; e < P.in * 16; e += 256) G[P.x + e] += 2.0f * G[P.y + e];
+        }
+        __syncthreads();
+    }
+}
+
+// The same computation on the host-built level schedule (BpParams.funits /
+// bunits): every unit of a level runs on its own wave, one barrier per level
+// instead of one per application.  A dense application's output (forward) or
+// input (backward) row blocks are independent; applications of one level read
+// only earlier levels and write distinct tensors; backward applications that
+// accumulate into the same input gradient G[x] sit in distinct levels in the
+// sequential kernel's (reverse) order — so every value, accumulation order
+// included, equals mz_bp_tile's bit for bit.  The schedule and the
+// application descriptors are staged in LDS, and a wave's operands of the next
+// level that do not depend on this level — its unit, the weight fragment of
+// the first k-chunk, the bias — are loaded before the barrier: after it, one
+// memory round trip (the input rows) precedes the MFMAs.
+struct BpPre {
+    int app, blk;         // app < 0: no unit
+    float a[BP_KC];       // A operands of the first k-chunk (dense)
+    float bias[4];        // forward: the bias of the lane's four output rows
+};
+
+// dense forward / backward block with the first chunk's A operands preloaded
+template <class FA, class FB>
+__device__ __forceinline__ bp_f32x4 bp_gemm_block_pre(int nk, int kq, const float (&a0)[BP_KC], FA fa, FB fb) {
+    bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < nk; k0 += BP_KC) {
+        float a[BP_KC], b[BP_KC];
+#pragma unroll
+        for (int j = 0; j < BP_KC; ++j) {
+            const int k = (k0 + j) * 4 + kq;
+            a[j] = k0 == 0 ? a0[j] : k0 + j < nk ? fa(k) : 0.0f;
+            b[j] = k0 + j < nk ? fb(k) : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < BP_KC; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+    }
+    return acc;
+}
+
+template <bool FWD>
+__device__ __forceinline__ void bp_lv_fetch(const BpApp* apps, const int2* units, int u, int u_end,
+                                            const float* __restrict__ flat, BpPre& pr) {
+    const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
+    pr.app = -1; pr.blk = 0;
+    if (u >= u_end) return;
+    const int2 un = units[u];
+    pr.app = un.x; pr.blk = un.y;
+    const BpApp P = apps[un.x];
+    if (P.op != BP_DENSE) return;
+    const float* W = flat + P.w_off;
+    if (FWD) {
+        const int o = un.y * 16 + m;
         const bool oin = o < P.out;
-        const bp_f32x4 acc = bp_gemm_block(nk, kq,
+        const int nk = (P.in + 3) >> 2;
+#pragma unroll
+        for (int j = 0; j < BP_KC; ++j) {
+            const int i = j * 4 + kq;
+            pr.a[j] = oin && j < nk && i < P.in ? W[o + (size_t)P.out * i] : 0.0f;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int oo = un.y * 16 + kq * 4 + r;
+            pr.bias[r] = oo < P.out ? flat[P.b_off + oo] : 0.0f;
+        }
+    } else {
+        const int i = un.y * 16 + m;
+        const bool iin = i < P.in;
+        const int nk = (P.out + 3) >> 2;
+#pragma unroll
+        for (int j = 0; j < BP_KC; ++j) {
+            const int o = j * 4 + kq;
+            pr.a[j] = iin && j < nk && o < P.out ? W[o + (size_t)P.out * i] : 0.0f;
+        }
+    }
+}
+
+template <bool FWD>
+__device__ __forceinline__ void bp_lv_run(const BpParams& Q, const BpApp& P, const BpPre& pr, float* T, float* G) {
+    const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
+    const float* W = Q.flat + P.w_off;
+    if (P.op != BP_DENSE) {
+        if (FWD) bp_concat_fwd(Q, P, T, lane, 64);
+        else for (int e = lane; e < P.in * 16; e += 64) G[P.x + e] += 2.0f * G[P.y + e];   // ∂(2h)/∂h
+        return;
+    }
+    if (FWD) {                                               // as bp_dense_fwd_blk
+        const int ob = pr.blk, o = ob * 16 + m;
+        const bool oin = o < P.out;
+        const float* X = T + P.x;
+        float* Y = T + P.y;
+        const bp_f32x4 acc = bp_gemm_block_pre((P.in + 3) >> 2, kq, pr.a,
             [&](int i) { return oin && i < P.in ? W[o + (size_t)P.out * i] : 0.0f; },
             [&](int i) { return i < P.in ? X[i * 16 + m] : 0.0f; });
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int oo = ob * 16 + kq * 4 + r;
-            if (oo < P.out) Y[oo * 16 + m] = bp_act(P.act, acc[r] + flat[P.b_off + oo]);
+            if (oo < P.out) Y[oo * 16 + m] = bp_act(P.act, acc[r] + pr.bias[r]);
         }
-    }
-}
-
-// G[x] += Wᵀ dZ with dZ = G[y] ⊙ act'(y) formed as the operand is loaded
-__device__ __forceinline__ void bp_dense_dx(const BpApp& P, const float* __restrict__ flat, const float* T,
-                                            float* G) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
-    const float* W = flat + P.w_off;
-    const float* DY = G + P.y;
-    const float* Y = T + P.y;
-    float* DX = G + P.x;
-    const int nib = (P.in + 15) >> 4, nk = (P.out + 3) >> 2;
-    for (int ib = wave; ib < nib; ib += 4) {
-        const int i = ib * 16 + m;
+    } else {                                                 // as bp_dense_dx_blk
+        const int ib = pr.blk, i = ib * 16 + m;
         const bool iin = i < P.in;
-        const bp_f32x4 acc = bp_gemm_block(nk, kq,
+        const float* DY = G + P.y;
+        const float* Y = T + P.y;
+        float* DX = G + P.x;
+        const bp_f32x4 acc = bp_gemm_block_pre((P.out + 3) >> 2, kq, pr.a,
             [&](int o) { return iin && o < P.out ? W[o + (size_t)P.out * i] : 0.0f; },
             [&](int o) { return o < P.out ? bp_dz(P.act, DY[o * 16 + m], Y[o * 16 + m]) : 0.0f; });
 #pragma unroll
@@ -92,42 +270,91 @@ __device__ __forceinline__ void bp_dense_dx(const BpApp& P, const float* __restr
     }
 }
 
-extern "C" __global__ __launch_bounds__(256) void mz_bp_tile(BpParams Q) {
-    const int tid = threadIdx.x, t0 = blockIdx.x * 16, K1 = Q.K + 1;
-    float* T = Q.act + (size_t)blockIdx.x * Q.tile_floats;
-    float* G = Q.grad + (size_t)blockIdx.x * Q.tile_floats;
-    for (int e = tid; e < Q.tile_floats; e += 256) G[e] = 0.0f;
-    for (int e = tid; e < 16 * K1 * 3; e += 256) {
-        const int b = t0 + e / (K1 * 3);
-        if (b < Q.B) Q.terms[(size_t)t0 * K1 * 3 + e] = 0.0f;
-    }
-    for (int e = tid; e < 16 * K1; e += 256) {                // rewards: 0 at step 0 (and without heads)
-        const int b = t0 + e / K1;
-        if (b < Q.B) Q.pr[(size_t)t0 * K1 + e] = 0.0f;
-    }
-    for (int e = tid; e < Q.obs_feat * 16; e += 256) {       // observation_batch (:347)
-        const int f = e >> 4, s = e & 15, b = t0 + s;
-        T[Q.obs_t + e] = b < Q.B ? Q.obs[(size_t)b * Q.obs_feat + f] : 0.0f;
-    }
-    __syncthreads();
-    // ---- forward: representation, K dynamics steps, K+1 predictions (Q10)
-    for (int a = 0; a < Q.n_app; ++a) {
-        const BpApp P = Q.apps[a];
-        if (P.op == BP_DENSE) {
-            bp_dense_fwd(P, Q.flat, T);
-        } else {                                              // make_dynamics_input (:293-304)
-            for (int e = tid; e < P.out * 16; e += 256) {
-                const int i = e >> 4, s = e & 15, b = t0 + s;
-                float v;
-                if (i < P.in) v = T[P.x + e] * 2.0f;
-                else v = b < Q.B ? Q.actions[(size_t)b * K1 + P.step] / (float)Q.A : 0.0f;
-                T[P.y + e] = v;
+template <bool FWD>
+__device__ __forceinline__ void bp_lv_levels(const BpParams& Q, const BpApp* apps, const int2* units, const int* lev,
+                                             int nlev, float* T, float* G) {
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#if BP_LV_SIMPLE
+    const int lane = threadIdx.x & 63;
+    for (int l = 0; l < nlev; ++l) {
+        for (int u = lev[l] + wave; u < lev[l + 1]; u += nw) {
+            const int2 un = units[u];
+            const BpApp P = apps[un.x];
+            if (P.op == BP_DENSE) {
+                if (FWD) bp_dense_fwd_blk(P, Q.flat, T, un.y);
+                else bp_dense_dx_blk(P, Q.flat, T, G, un.y);
+            } else if (FWD) {
+                bp_concat_fwd(Q, P, T, lane, 64);
+            } else {
+                for (int e = lane; e < P.in * 16; e += 64) G[P.x + e] += 2.0f * G[P.y + e];
             }
         }
         __syncthreads();
     }
-    // ---- heads: dL/dy of the value / policy / reward outputs, loss terms
-    for (int e = tid; e < Q.n_head * 16; e += 256) {
+#elif BP_LV_PREFETCH
+    BpPre cur;
+    bp_lv_fetch<FWD>(apps, units, lev[0] + wave, lev[1], Q.flat, cur);
+    for (int l = 0; l < nlev; ++l) {
+        if (cur.app >= 0) bp_lv_run<FWD>(Q, apps[cur.app], cur, T, G);
+        for (int u = lev[l] + wave + nw; u < lev[l + 1]; u += nw) {       // more units than waves (rare)
+            BpPre x;
+            bp_lv_fetch<FWD>(apps, units, u, lev[l + 1], Q.flat, x);
+            bp_lv_run<FWD>(Q, apps[x.app], x, T, G);
+        }
+        BpPre nxt;
+        nxt.app = -1;
+        if (l + 1 < nlev) bp_lv_fetch<FWD>(apps, units, lev[l + 1] + wave, lev[l + 2], Q.flat, nxt);
+        __syncthreads();
+        cur = nxt;
+    }
+#else
+    for (int l = 0; l < nlev; ++l) {
+        for (int u = lev[l] + wave; u < lev[l + 1]; u += nw) {
+            BpPre x;
+            bp_lv_fetch<FWD>(apps, units, u, lev[l + 1], Q.flat, x);
+            bp_lv_run<FWD>(Q, apps[x.app], x, T, G);
+        }
+        __syncthreads();
+    }
+#endif
+}
+
+extern "C" __global__ __launch_bounds__(BP_LV_THREADS) void mz_bp_tile_lv(BpParams Q) {
+    extern __shared__ __attribute__((aligned(16))) int bp_lds[];
+    float* T = Q.act + (size_t)blockIdx.x * Q.tile_floats;
+    float* G = Q.grad + (size_t)blockIdx.x * Q.tile_floats;
+    // the schedule and the descriptors in LDS: [apps][funits][bunits][flev][blev]
+    const int nfu = 0, nbu = 0;
+    (void)nfu; (void)nbu;
+    BpApp* apps = reinterpret_cast<BpApp*>(bp_lds);
+    int2* fun = reinterpret_cast<int2*>(apps + Q.n_app);
+    int2* bun = fun + Q.n_funit;
+    int* flev = reinterpret_cast<int*>(bun + Q.n_bunit);
+    int* blev = flev + Q.n_flev + 2;
+    for (int i = threadIdx.x; i < Q.n_app; i += blockDim.x) apps[i] = Q.apps[i];
+    for (int i = threadIdx.x; i < Q.n_funit; i += blockDim.x) fun[i] = Q.funits[i];
+    for (int i = threadIdx.x; i < Q.n_bunit; i += blockDim.x) bun[i] = Q.bunits[i];
+    for (int i = threadIdx.x; i < Q.n_flev + 2; i += blockDim.x) flev[i] = i <= Q.n_flev ? Q.flev[i] : Q.n_funit;
+    for (int i = threadIdx.x; i < Q.n_blev + 2; i += blockDim.x) blev[i] = i <= Q.n_blev ? Q.blev[i] : Q.n_bunit;
+    bp_prologue(Q, T, G);
+    __syncthreads();
+#if BP_LV_LDS
+    bp_lv_levels<true>(Q, apps, fun, flev, Q.n_flev, T, G);
+    bp_heads(Q, T, G);
+    __syncthreads();
+    bp_lv_levels<false>(Q, apps, bun, blev, Q.n_blev, T, G);
+#else   // descriptors by scalar loads (wave-uniform values straight into SGPRs)
+    bp_lv_levels<true>(Q, Q.apps, Q.funits, Q.flev, Q.n_flev, T, G);
+    bp_heads(Q, T, G);
+    __syncthreads();
+    bp_lv_levels<false>(Q, Q.apps, Q.bunits, Q.blev, Q.n_blev, T, G);
+#endif
+}
+
+// ---- heads: dL/dy of the value / policy / reward outputs, loss terms
+__device__ void bp_heads(const BpParams& Q, float* T, float* G) {
+    const int tid = threadIdx.x, nt = blockDim.x, t0 = blockIdx.x * 16, K1 = Q.K + 1;
+    for (int e = tid; e < Q.n_head * 16; e += nt) {
         const BpHead hd = Q.heads[e >> 4];
         const int s = e & 15, b = t0 + s, k = hd.step;
         if (b >= Q.B) continue;
@@ -161,17 +388,6 @@ extern "C" __global__ __launch_bounds__(256) void mz_bp_tile(BpParams Q) {
             Q.terms[bk * 3 + 1] = ce;
         }
     }
-    __syncthreads();
-    // ---- backward, reverse order
-    for (int a = Q.n_app - 1; a >= 0; --a) {
-        const BpApp P = Q.apps[a];
-        if (P.op == BP_DENSE) {
-            bp_dense_dx(P, Q.flat, T, G);
-        } else {                                              // ∂(2h)/∂h
-            for (int e = tid; e < P.in * 16; e += 256) G[P.x + e] += 2.0f * G[P.y + e];
-        }
-        __syncthreads();
-    }
 }
 
 extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
@@ -180,14 +396,21 @@ extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
     const int lane = threadIdx.x, m = lane & 15, kq = lane >> 4;
     if (J.ib < 0) {                                           // db = Σ dZ, + 2b
         const int o = J.ob * 16 + lane;
-        if (lane >= 16 || o >= L.out) return;
-        float s = 0.0f;
-        for (int t = 0; t < Q.tiles; ++t)
-            for (int u = 0; u < L.n_use; ++u) {
-                const size_t e = (size_t)t * Q.tile_floats + Q.uses[L.use0 + u].y + o * 16;
-                for (int j = 0; j < 16; ++j) s += bp_dz(L.act, Q.grad[e + j], Q.act[e + j]);
-            }
-        Q.out[L.b_off + o] = s + 2.0f * Q.flat[L.b_off + o];
+        const bool in = lane < 16 && o < L.out;
+        double q = 0.0;
+        if (in) {
+            float s = 0.0f;
+            for (int t = 0; t < Q.tiles; ++t)
+                for (int u = 0; u < L.n_use; ++u) {
+                    const size_t e = (size_t)t * Q.tile_floats + Q.uses[L.use0 + u].y + o * 16;
+                    for (int j = 0; j < 16; ++j) s += bp_dz(L.act, Q.grad[e + j], Q.act[e + j]);
+                }
+            const float th = Q.flat[L.b_off + o];
+            Q.out[L.b_off + o] = s + 2.0f * th;
+            q = (double)th * (double)th;
+        }
+        for (int d = 32; d > 0; d >>= 1) q += __shfl_xor(q, d);    // fixed tree: Σθ² of the block
+        if (lane == 0) Q.sq[blockIdx.x] = q;
         return;
     }
     const int o = J.ob * 16 + m, i = J.ib * 16 + m;
@@ -207,14 +430,19 @@ extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
             }
         }
     }
+    double q = 0.0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int oo = J.ob * 16 + kq * 4 + r;
         if (oo < L.out && iin) {
             const size_t p = (size_t)L.w_off + oo + (size_t)L.out * i;
-            Q.out[p] = acc[r] + 2.0f * Q.flat[p];
+            const float th = Q.flat[p];
+            Q.out[p] = acc[r] + 2.0f * th;
+            q += (double)th * (double)th;
         }
     }
+    for (int d = 32; d > 0; d >>= 1) q += __shfl_xor(q, d);        // fixed tree: Σθ² of the block
+    if (lane == 0) Q.sq[blockIdx.x] = q;
 }
 
 // blocks 0..2: Σθ² of each net; block 3: the losses (per sample in ascending
@@ -223,15 +451,8 @@ extern "C" __global__ __launch_bounds__(256) void mz_bp_fold(BpFoldParams Q) {
     __shared__ double red[3][256];
     const int tid = threadIdx.x;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    if (blockIdx.x < 3) {                       // 8 loads in flight per thread, then their squares in order
-        const size_t off = Q.netoff[blockIdx.x], n = Q.netoff[3 + blockIdx.x];
-        for (size_t i0 = tid; i0 < n; i0 += 8 * 256) {
-            float x[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) x[u] = i0 + u * 256 < n ? Q.flat[off + i0 + u * 256] : 0.0f;
-#pragma unroll
-            for (int u = 0; u < 8; ++u) s0 += (double)x[u] * (double)x[u];
-        }
+    if (blockIdx.x < 3) {                       // the net's per-block Σθ² of mz_bp_dw, ascending job order
+        for (int j = Q.job0[blockIdx.x] + tid; j < Q.job0[blockIdx.x + 1]; j += 256) s0 += Q.sq[j];
     } else {
         const int K1 = Q.K + 1;
         for (int b = tid; b < Q.B; b += 256) {

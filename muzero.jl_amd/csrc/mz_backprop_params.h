@@ -57,13 +57,34 @@ struct BpParams {
     const float* gscale; const float* weights;
     float* terms;                         // [B][K+1][3]: (v−z)², CE, (r−u)²
     float* pv; float* pp; float* pr;      // the read-outs (K+1,B) / (A,K+1,B) / (K+1,B), as the unroll's
+    // level schedule (mz_bp_tile_lv): the forward / backward applications
+    // grouped into dependency levels, each a list of units {app, block} — a
+    // dense layer's 16-row output block (forward) or 16-row input block
+    // (backward dX), or a whole concatenation (block 0); lev[l] .. lev[l+1]
+    int n_flev, n_blev, n_funit, n_bunit;
+    const int2* funits; const int* flev;
+    const int2* bunits; const int* blev;
 };
+#ifndef BP_LV_THREADS
+#define BP_LV_THREADS 1024                // mz_bp_tile_lv: 16 waves, a unit per wave per level
+#endif
+#ifndef BP_LV_LDS
+#define BP_LV_LDS 1                       // the schedule and descriptors staged in LDS
+#endif
+#ifndef BP_LV_SIMPLE
+#define BP_LV_SIMPLE 1                    // units run as bp_dense_*_blk (operands loaded in the unit)
+#endif
+#ifndef BP_LV_PREFETCH
+#define BP_LV_PREFETCH 0                  // the next level's unit, weights and bias loaded before each barrier
+                                          // (measured slower: 1.91k vs 2.29k steps/s, tools/ab_corrected.sh)
+#endif
 
 struct BpDwParams {
     int tiles, tile_floats, n_job;
     const BpJob* jobs; const BpLayer* layers; const BpUse* uses;
     const float* act; const float* grad; const float* flat;
     float* out;                           // Flux-order gradient (data term + 2θ)
+    double* sq;                           // [n_job]: Σθ² of each job's parameter block (f64, fixed order)
 };
 
 struct BpFoldParams {
@@ -71,4 +92,5 @@ struct BpFoldParams {
     const float* terms; const float* gscale; const float* weights;
     const float* flat; const size_t* netoff;
     float* losses;                        // {value, reward, policy, Σθ² repr, pred, dyn}
+    const double* sq; int job0[4];        // mz_bp_dw's per-job Σθ²; jobs [job0[n], job0[n+1]) are net n's
 };

@@ -41,6 +41,7 @@ extern "C" __global__ void mz_rsearch_nets(RSearchParams P);
 extern "C" __global__ void mz_runroll_kernel(RUnrollParams U);
 extern "C" __global__ void mz_runroll_chain(RUnrollParams U);
 extern "C" __global__ void mz_bp_tile(BpParams Q);
+extern "C" __global__ void mz_bp_tile_lv(BpParams Q);
 extern "C" __global__ void mz_bp_dw(BpDwParams Q);
 extern "C" __global__ void mz_bp_fold(BpFoldParams Q);
 extern "C" __global__ void mz_runroll_pred(RUnrollParams U);
@@ -256,6 +257,9 @@ struct mz_handle {
     int bp_n_app = 0, bp_n_head = 0, bp_n_job = 0, bp_tile_floats = 0, bp_obs_t = 0, bp_tiles_cap = 0;
     BpApp* d_bp_apps = nullptr; BpHead* d_bp_heads = nullptr; BpLayer* d_bp_layers = nullptr;
     BpUse* d_bp_uses = nullptr; BpJob* d_bp_jobs = nullptr;
+    int2* d_bp_funits = nullptr; int* d_bp_flev = nullptr; int2* d_bp_bunits = nullptr; int* d_bp_blev = nullptr;
+    int bp_n_flev = 0, bp_n_blev = 0, bp_n_funit = 0, bp_n_bunit = 0;
+    double* d_bp_sq = nullptr; int bp_job0[4] = {0, 0, 0, 0};
     float* d_bp_act = nullptr; float* d_bp_grad = nullptr; float* d_bp_terms = nullptr;
     std::vector<void*> sp_allocs;
     std::vector<void*> allocs;
@@ -2017,12 +2021,57 @@ static int build_bp(mz_handle* h) {
         heads.push_back(BpHead{BP_HEAD_V, chain(MZ_NET_PRED, CH_HEAD1, t), k});
         heads.push_back(BpHead{BP_HEAD_P, chain(MZ_NET_PRED, CH_HEAD2, t), k});
     }
+    // level schedule of the tile kernel (mz_bp_tile_lv).  Forward: an
+    // application's level is one past its input's producer (the observation:
+    // level 0).  Backward, in reverse application order: one past the latest
+    // consumer of its output (the applications reading it, which accumulate
+    // G[y]), and past every later application accumulating into the same G[x]
+    // (so no two units of a level add into one tensor, and the sequential
+    // kernel's accumulation order holds)
+    const int na = (int)apps.size();
+    std::vector<int> flv(na, 0), blv(na, 0);
+    int nfl = 0, nbl = 0;
+    for (int a = 0; a < na; ++a) {
+        int l = 0;
+        for (int p = 0; p < a; ++p) if (apps[p].y == apps[a].x) l = std::max(l, flv[p] + 1);
+        flv[a] = l; nfl = std::max(nfl, l + 1);
+    }
+    for (int a = na - 1; a >= 0; --a) {
+        int l = 0;
+        for (int c = a + 1; c < na; ++c) {
+            if (apps[c].x == apps[a].y) l = std::max(l, blv[c] + 1);           // consumers of y
+            if (apps[c].x == apps[a].x) l = std::max(l, blv[c] + 1);           // same G[x], earlier in backward
+        }
+        blv[a] = l; nbl = std::max(nbl, l + 1);
+    }
+    std::vector<int2> fun, bun;
+    std::vector<int> flev, blev;
+    for (int l = 0; l < nfl; ++l) {
+        flev.push_back((int)fun.size());
+        for (int a = 0; a < na; ++a)
+            if (flv[a] == l) {
+                const int nb = apps[a].op == BP_DENSE ? (apps[a].out + 15) / 16 : 1;
+                for (int b = 0; b < nb; ++b) fun.push_back(make_int2(a, b));
+            }
+    }
+    flev.push_back((int)fun.size());
+    for (int l = 0; l < nbl; ++l) {
+        blev.push_back((int)bun.size());
+        for (int a = na - 1; a >= 0; --a)
+            if (blv[a] == l) {
+                const int nb = apps[a].op == BP_DENSE ? (apps[a].in + 15) / 16 : 1;
+                for (int b = 0; b < nb; ++b) bun.push_back(make_int2(a, b));
+            }
+    }
+    blev.push_back((int)bun.size());
     // dW: every layer's applications, one wave per 16x16 block (+ one per bias block)
     std::vector<BpLayer> layers(h->layers.size());
     std::vector<BpUse> uses;
     std::vector<BpJob> jobs;
+    for (int n = 0; n < 4; ++n) h->bp_job0[n] = -1;
     for (size_t li = 0; li < h->layers.size(); ++li) {
         const LayerSpec& L = h->layers[li];
+        if (h->bp_job0[L.net] < 0) h->bp_job0[L.net] = (int)jobs.size();   // layers are in net order
         BpLayer& bl = layers[li];
         bl.w_off = (int)L.flux_w; bl.b_off = (int)L.flux_b; bl.in = L.in; bl.out = L.out; bl.act = L.act;
         bl.use0 = (int)uses.size();
@@ -2039,9 +2088,14 @@ static int build_bp(mz_handle* h) {
         return 0;
     };
     if (up(&h->d_bp_apps, apps) || up(&h->d_bp_heads, heads) || up(&h->d_bp_layers, layers) ||
-        up(&h->d_bp_uses, uses) || up(&h->d_bp_jobs, jobs))
+        up(&h->d_bp_uses, uses) || up(&h->d_bp_jobs, jobs) || up(&h->d_bp_funits, fun) ||
+        up(&h->d_bp_flev, flev) || up(&h->d_bp_bunits, bun) || up(&h->d_bp_blev, blev))
         return -1;
+    h->bp_n_flev = nfl; h->bp_n_blev = nbl; h->bp_n_funit = (int)fun.size(); h->bp_n_bunit = (int)bun.size();
     h->bp_n_app = (int)apps.size(); h->bp_n_head = (int)heads.size(); h->bp_n_job = (int)jobs.size();
+    h->bp_job0[3] = (int)jobs.size();
+    for (int n = 2; n >= 0; --n) if (h->bp_job0[n] < 0) h->bp_job0[n] = h->bp_job0[n + 1];
+    MZ_TRY(h, dalloc(h, &h->d_bp_sq, jobs.size()));
     h->bp_tile_floats = off; h->bp_obs_t = obs_t;
     h->bp_built = true;
     return 0;
@@ -2067,15 +2121,26 @@ static int bp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* loss
     Q.obs = b->observation; Q.actions = b->actions; Q.tv = b->target_values; Q.tr = b->target_rewards;
     Q.tp = b->target_policies; Q.gscale = b->gradient_scale; Q.weights = b->weights; Q.terms = h->d_bp_terms;
     Q.pv = h->d_pv; Q.pp = h->d_pp; Q.pr = h->d_pr;
-    hipLaunchKernelGGL(mz_bp_tile, dim3(tiles), dim3(256), 0, st, Q);
+    Q.n_flev = h->bp_n_flev; Q.n_blev = h->bp_n_blev; Q.n_funit = h->bp_n_funit; Q.n_bunit = h->bp_n_bunit;
+    const size_t lv_lds = (size_t)Q.n_app * sizeof(BpApp) + (size_t)(Q.n_funit + Q.n_bunit) * sizeof(int2) +
+                          (size_t)(Q.n_flev + Q.n_blev + 4) * sizeof(int);
+    Q.funits = h->d_bp_funits; Q.flev = h->d_bp_flev; Q.bunits = h->d_bp_bunits; Q.blev = h->d_bp_blev;
+    // the level schedule (default) or the one-application-per-barrier kernel
+    // (MZ_BP_SEQ=1, the same bits: tests/test_corrected_learner_gpu.py)
+    if (std::getenv("MZ_BP_SEQ")) hipLaunchKernelGGL(mz_bp_tile, dim3(tiles), dim3(256), 0, st, Q);
+    else if (lv_lds <= kLdsMax) hipLaunchKernelGGL(mz_bp_tile_lv, dim3(tiles), dim3(BP_LV_THREADS), lv_lds, st, Q);
+    else return fail(h, "corrected learner: the level schedule exceeds the LDS");
     BpDwParams D;
     D.tiles = tiles; D.tile_floats = h->bp_tile_floats; D.n_job = h->bp_n_job; D.jobs = h->d_bp_jobs;
     D.layers = h->d_bp_layers; D.uses = h->d_bp_uses; D.act = h->d_bp_act; D.grad = h->d_bp_grad; D.flat = h->d_flat;
     D.out = grad_dev ? grad_dev : h->d_grad;
+    D.sq = h->d_bp_sq;
     hipLaunchKernelGGL(mz_bp_dw, dim3(h->bp_n_job), dim3(64), 0, st, D);
     BpFoldParams F;
     F.B = B; F.K = K; F.terms = h->d_bp_terms; F.gscale = b->gradient_scale; F.weights = b->weights;
     F.flat = h->d_flat; F.netoff = h->d_netoff; F.losses = losses_dev ? losses_dev : h->d_loss;
+    F.sq = h->d_bp_sq;
+    for (int n = 0; n < 4; ++n) F.job0[n] = h->bp_job0[n];
     hipLaunchKernelGGL(mz_bp_fold, dim3(4), dim3(256), 0, st, F);
     MZ_TRY(h, hipGetLastError());
     return 0;
