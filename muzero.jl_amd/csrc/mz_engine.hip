@@ -49,6 +49,7 @@ extern "C" __global__ void mz_runroll_pred_n(RUnrollParams U);
 extern "C" __global__ void mz_runroll_pred_n1(RUnrollParams U);
 extern "C" __global__ void mz_runroll_chain1(RUnrollParams U);
 extern "C" __global__ void mz_runroll_chain_r(RUnrollParams U);
+extern "C" __global__ void mz_runroll_pred_r(RUnrollParams U);
 extern "C" __global__ void mz_sp_prepare(SpParams S);
 extern "C" __global__ void mz_sp_commit(SpParams S);
 extern "C" __global__ void mz_sp_order(SpParams S);
@@ -157,6 +158,7 @@ struct mz_handle {
     float* d_rts = nullptr;                 // [bcap][K][H] dynamics trunk outputs (the reward heads' input)
     int rn_dyn_split = 0;                   // first reward-head layer of the dynamics plan
     bool rd_chain = false;                  // the chain runs as mz_runroll_chain_r (rd_chain_ok)
+    bool rp_pred = false;                   // one-item predictions run as mz_runroll_pred_r (rp_pred_ok)
     std::vector<int> rtab;                  // offset tables of the narrow (chain) plans
     int* d_rtab = nullptr;
     int device = 0, max_games = 0;
@@ -835,6 +837,21 @@ static bool rd_chain_ok(const mz_handle* h) {
     }
     return rd_chain_lds(h) <= kLdsMax;
 }
+// mz_runroll_pred_r applies when the prediction trunk ([0, RP_NL), the
+// first head layer next) is RP_NL such layers, all on k-blocked inputs
+static size_t rp_pred_lds(const mz_handle* h) { return h->rn_lds_l + (size_t)RP_NL * 64 * 16; }
+static bool rp_pred_ok(const mz_handle* h) {
+    const RPlan& R = h->rplan_l[MZ_NET_PRED];
+    if ((h->plane * h->rn_ng_l + 15) / 16 != 1 || R.n <= RP_NL || R.L[RP_NL].cout == 64) return false;
+    if (2 * h->rhp.num_blocks + 1 != RP_NL) return false;
+    for (int i = 0; i < RP_NL; ++i) {
+        const RLayer& L = R.L[i];
+        if (L.kk != 1 || L.cout != 64 || L.n_ob != 4 || !L.spatial || !L.bn || L.act != MZ_ACT_RELU ||
+            !L.in_kb || L.K != 64 || L.nq != 4)
+            return false;
+    }
+    return rp_pred_lds(h) <= kLdsMax;
+}
 
 static RPlan rn_plan(const mz_handle* h, const std::vector<RSpec>& sp, int net, int NG, size_t flat_off,
                      int& w_img, std::vector<int>* srcw, bool sep_b2 = false, std::vector<int>* otab = nullptr) {
@@ -1202,6 +1219,7 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
             h->rn_lds_l = std::max(h->rn_lds_l, (size_t)h->rplan_l[n].lds_floats * 4);
         }
         h->rd_chain = rd_chain_ok(h) && !std::getenv("MZ_RN_NO_RD");
+        h->rp_pred = rp_pred_ok(h) && !std::getenv("MZ_RN_NO_RD");
     }
     h->inv_tile.assign(h->nflat, -1);
     for (size_t i = 0; i < sw.size(); ++i) if (sw[i] >= 0) h->inv_tile[(size_t)sw[i]] = (int)i;
@@ -1259,6 +1277,9 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
     if (h->rd_chain)
         CK(hipFuncSetAttribute((const void*)mz_runroll_chain_r, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)rd_chain_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_chain_r)"));
+    if (h->rp_pred)
+        CK(hipFuncSetAttribute((const void*)mz_runroll_pred_r, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)rp_pred_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_pred_r)"));
     CK(hipFuncSetAttribute((const void*)mz_rsearch_nets, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)rsearch_nets_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(nets)"));
     // search buffers (trees and hidden states in HBM)
@@ -1845,7 +1866,8 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
         static const bool wide_env = std::getenv("MZ_RN_PRED_WIDE") != nullptr;
         const bool wide_p = wide_env || (B * KH + U.ng - 1) / U.ng >= h->n_cu;
         h->last_lvariant = std::string(h->rd_chain ? "mz_runroll_chain_r" : nb1 ? "mz_runroll_chain1" : "mz_runroll_chain") +
-                           (wide_p ? "+mz_runroll_pred" : nb1 ? "+mz_runroll_pred_n1" : "+mz_runroll_pred_n");
+                           (wide_p ? "+mz_runroll_pred" : h->rp_pred ? "+mz_runroll_pred_r" : nb1 ? "+mz_runroll_pred_n1"
+                                                                                       : "+mz_runroll_pred_n");
         if (h->rd_chain)
             MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_chain_r, dim3((B + U.ng_l - 1) / U.ng_l),
                                       dim3(RD_THREADS), args, rd_chain_lds(h), st));
@@ -1857,6 +1879,9 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
         if (wide_p)
             MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred, dim3((B * KH + U.ng - 1) / U.ng, U.K > 0 ? 2 : 1),
                                       dim3(RN_THREADS), args, runroll_lds(h), st));
+        else if (h->rp_pred)
+            MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred_r, dim3((B * KH + U.ng_l - 1) / U.ng_l,
+                                      U.K > 0 ? 2 : 1), dim3(RD_THREADS), args, rp_pred_lds(h), st));
         else
             MZ_TRY(h, hipLaunchKernel(nb1 ? (const void*)mz_runroll_pred_n1 : (const void*)mz_runroll_pred_n,
                                       dim3((B * KH + U.ng_l - 1) / U.ng_l, U.K > 0 ? 2 : 1), dim3(RN_THREADS), args,

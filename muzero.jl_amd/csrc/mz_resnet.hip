@@ -1486,6 +1486,72 @@ __device__ __forceinline__ void runroll_pred_body(const RUnrollParams& U) {
         rn_unstage(lds + R.out1_off, NG, A, t, [&](int f, float v) { o[f] = v; });
     }
 }
+// mz_runroll_pred_r: runroll_pred_body<true, 1> with the prediction trunk's
+// RP_NL layers (1x1 convs of 64 channels on the k-blocked one-item tile) run
+// by rd_layer on A fragments loaded at kernel start (all five layers' loads in
+// flight together, under the input staging) and epilogue parameters staged in
+// LDS; the heads (and the reward-head workgroups, y = 1) on the generic path.
+template <int I>
+__device__ __forceinline__ void rp_run(const RPlan& R, const float (&ar)[RP_NL][4][4], const float4* ep_lds,
+                                       float* lds, int ncols, float bn_s, float bn_r) {
+    if constexpr (I < RP_NL) {
+        const RLayer L = rn_layer_at(R, I);
+        const float (&a1)[1][4][4] = *reinterpret_cast<const float (*)[1][4][4]>(&ar[I]);
+        rd_layer<1>(L, a1, ep_lds + I * 64, lds, ncols, bn_s, bn_r);
+        __syncthreads();
+        rp_run<I + 1>(R, ar, ep_lds, lds, ncols, bn_s, bn_r);
+    }
+}
+
+extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_pred_r(RUnrollParams U) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const bool rew = blockIdx.y == 1;
+    const RPlan& R = U.plans_l[rew ? MZ_NET_DYN : MZ_NET_PRED];
+    const int NG = U.ng_l, H = U.H, A = U.A, K = U.K, K1 = K + 1, KH = K > 0 ? K : 1;
+    const int n_items = U.B * KH, t0 = blockIdx.x * NG;
+    const int i0 = rew ? U.dyn_split : 0;
+    const RnLane t = rn_lane(NG);
+    const int it = t0 + t.g;
+    const bool ok = it < n_items;
+    const size_t ic = (size_t)(ok ? it : 0);
+    const int lane = threadIdx.x & 63, ob = threadIdx.x >> 6;
+    float4* ep_lds = reinterpret_cast<float4*>(lds + U.rd_ep_off);
+    float ar[RP_NL][4][4];
+    if (!rew) {
+#pragma unroll
+        for (int i = 0; i < RP_NL; ++i) rn_load_a(ar[i], U.Wimg, rn_layer_at(R, i), ob, 0, lane);
+        for (int i = threadIdx.x; i < RP_NL * 64; i += blockDim.x) {
+            const RLayer L = rn_layer_at(R, i >> 6);
+            ep_lds[i] = reinterpret_cast<const float4*>(U.Wimg + L.ep_img)[i & 63];
+        }
+    }
+    rn_fill_ktabs(R, lds, NG, U.W, U.P);
+    {
+        const float* x = (rew ? U.ts : U.hs) + ic * H;
+        rn_stage_l(lds + (rew ? R.L[i0].in_off : R.in_off), rew ? R.L[i0].in_kb : R.in_kb, NG, U.P, H, t,
+                   [&](int f) { return ok ? x[f] : 0.0f; });
+    }
+    __syncthreads();
+    if (!rew) {
+        rp_run<0>(R, ar, ep_lds, lds, U.P * NG, U.bn_s, 1.0f / U.bn_s);                    // trunk (:351 / :356)
+        rn_run<true, true, 1>(R, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, nullptr, RP_NL);   // heads
+    } else {
+        rn_run<true, true, 1>(R, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, nullptr, i0);      // :362 reward head
+    }
+    if (!ok) return;
+    const size_t b = ic / KH;
+    const int s = (int)(ic - b * KH);
+    if (rew) {
+        if (t.f0 == 0) U.pr[b * K1 + s + 1] = lds[R.out1_off + t.g];
+        return;
+    }
+    for (int j = s == 0 ? 0 : s + 1; j <= (s + 1 <= K ? s + 1 : 0); ++j) {
+        if (t.f0 == 0) U.pv[b * K1 + j] = lds[R.out0_off + t.g];
+        float* o = U.pp + (b * K1 + j) * A;
+        rn_unstage(lds + R.out1_off, NG, A, t, [&](int f, float v) { o[f] = v; });
+    }
+}
+
 // wide tiles of ng items (plans), or one item per workgroup on the narrow
 // (chain) plans — B·K workgroups, a short per-layer critical path
 extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred(RUnrollParams U) { runroll_pred_body<false>(U); }

@@ -187,6 +187,8 @@ struct RUnrollParams {
 // trunk + state head of 2-block towers) with register-resident A fragments
 #define RD_NL 10
 #define RD_THREADS 256
+// mz_runroll_pred_r: the prediction trunk's RP_NL layers (1 + 2 blocks) the same way
+#define RP_NL 5
 
 // Downsampler of the ResNet representation (ResNetHP.downsample,
 // Learning.jl:175-187; BASELINE configs[4]): stride-2 convs without
