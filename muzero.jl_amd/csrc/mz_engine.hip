@@ -49,6 +49,7 @@ extern "C" __global__ void mz_runroll_pred_n(RUnrollParams U);
 extern "C" __global__ void mz_runroll_pred_n1(RUnrollParams U);
 extern "C" __global__ void mz_runroll_chain1(RUnrollParams U);
 extern "C" __global__ void mz_runroll_chain_r(RUnrollParams U);
+extern "C" __global__ void mz_runroll_chain_r3(RUnrollParams U);
 extern "C" __global__ void mz_runroll_pred_r(RUnrollParams U);
 extern "C" __global__ void mz_sp_prepare(SpParams S);
 extern "C" __global__ void mz_sp_commit(SpParams S);
@@ -157,7 +158,8 @@ struct mz_handle {
     float* d_rhs = nullptr;                 // [bcap][K][H] learner unroll scratch (h between the nets)
     float* d_rts = nullptr;                 // [bcap][K][H] dynamics trunk outputs (the reward heads' input)
     int rn_dyn_split = 0;                   // first reward-head layer of the dynamics plan
-    bool rd_chain = false;                  // the chain runs as mz_runroll_chain_r (rd_chain_ok)
+    bool rd_chain = false;                  // the chain runs as mz_runroll_chain_r[3] (rd_chain_ok)
+    int rd_nb = 1;                          // its column blocks (1: mz_runroll_chain_r, 3: _r3)
     bool rp_pred = false;                   // one-item predictions run as mz_runroll_pred_r (rp_pred_ok)
     std::vector<int> rtab;                  // offset tables of the narrow (chain) plans
     int* d_rtab = nullptr;
@@ -822,20 +824,24 @@ static void rn_otab_fill(std::vector<int>& t, const RLayer& L, int NG, int W, in
                     }
 }
 
-// mz_runroll_chain_r applies when the learner chain's tiles are one column
-// block and the dynamics chain ([0, dyn_split)) is RD_NL 1x1 conv layers of 64
-// channels with BatchNorm + relu: layer 0 on the plain input with 4 < nq <= 8
-// (nf + 1 channels: two A chunks), the others K = 64 on k-blocked inputs
-static size_t rd_chain_lds(const mz_handle* h) { return h->rn_lds_l + (size_t)RD_NL * 64 * 16; }
-static bool rd_chain_ok(const mz_handle* h) {
+// mz_runroll_chain_r[3] applies when the dynamics chain ([0, dyn_split)) is
+// RD_NL (one column block) or RD_NL3 (three column blocks) 1x1 conv layers of
+// 64 channels with BatchNorm + relu: layer 0 on the plain input with 4 < nq <=
+// 8 (nf + 1 channels: two A chunks), the others K = 64 on k-blocked inputs
+static size_t rd_chain_lds(const mz_handle* h) { return h->rn_lds_l + (size_t)h->rn_dyn_split * 64 * 16; }
+static int rd_chain_ok(const mz_handle* h) {          // the column blocks, or 0
     const RPlan& R = h->rplan_l[MZ_NET_DYN];
-    if (h->rn_dyn_split != RD_NL || (h->plane * h->rn_ng_l + 15) / 16 != 1) return false;
-    for (int i = 0; i < RD_NL; ++i) {
+    const int nb = (h->plane * h->rn_ng_l + 15) / 16;
+    // (three blocks / 18 layers: 304 resident VGPRs, the kernel spills — measured 1.27k vs 1.53k learner
+    // steps/s on Connect4 ResNet-8 — so only on request, MZ_RN_RD3=1)
+    static const bool rd3 = std::getenv("MZ_RN_RD3") != nullptr;
+    if (!((nb == 1 && h->rn_dyn_split == RD_NL) || (rd3 && nb == 3 && h->rn_dyn_split == RD_NL3))) return 0;
+    for (int i = 0; i < h->rn_dyn_split; ++i) {
         const RLayer& L = R.L[i];
-        if (L.kk != 1 || L.cout != 64 || L.n_ob != 4 || !L.spatial || !L.bn || L.act != MZ_ACT_RELU) return false;
-        if (i == 0 ? (L.in_kb || L.nq <= 4 || L.nq > 8) : (!L.in_kb || L.K != 64 || L.nq != 4)) return false;
+        if (L.kk != 1 || L.cout != 64 || L.n_ob != 4 || !L.spatial || !L.bn || L.act != MZ_ACT_RELU) return 0;
+        if (i == 0 ? (L.in_kb || L.nq <= 4 || L.nq > 8) : (!L.in_kb || L.K != 64 || L.nq != 4)) return 0;
     }
-    return rd_chain_lds(h) <= kLdsMax;
+    return rd_chain_lds(h) <= kLdsMax ? nb : 0;
 }
 // mz_runroll_pred_r applies when the prediction trunk ([0, RP_NL), the
 // first head layer next) is RP_NL such layers, all on k-blocked inputs
@@ -1218,7 +1224,8 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
             CK(h->rplan_l[n].n < 0 ? fail(h, "ResNet plan: a k-blocked output buffer") : 0);
             h->rn_lds_l = std::max(h->rn_lds_l, (size_t)h->rplan_l[n].lds_floats * 4);
         }
-        h->rd_chain = rd_chain_ok(h) && !std::getenv("MZ_RN_NO_RD");
+        h->rd_nb = rd_chain_ok(h);
+        h->rd_chain = h->rd_nb > 0 && !std::getenv("MZ_RN_NO_RD");
         h->rp_pred = rp_pred_ok(h) && !std::getenv("MZ_RN_NO_RD");
     }
     h->inv_tile.assign(h->nflat, -1);
@@ -1275,7 +1282,8 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
     CK(hipFuncSetAttribute((const void*)mz_runroll_chain, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)h->rn_lds_l) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_chain)"));
     if (h->rd_chain)
-        CK(hipFuncSetAttribute((const void*)mz_runroll_chain_r, hipFuncAttributeMaxDynamicSharedMemorySize,
+        CK(hipFuncSetAttribute(h->rd_nb == 3 ? (const void*)mz_runroll_chain_r3 : (const void*)mz_runroll_chain_r,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)rd_chain_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_chain_r)"));
     if (h->rp_pred)
         CK(hipFuncSetAttribute((const void*)mz_runroll_pred_r, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1865,11 +1873,13 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
         // else one-item tiles (B = 32: 160 workgroups instead of 10)
         static const bool wide_env = std::getenv("MZ_RN_PRED_WIDE") != nullptr;
         const bool wide_p = wide_env || (B * KH + U.ng - 1) / U.ng >= h->n_cu;
-        h->last_lvariant = std::string(h->rd_chain ? "mz_runroll_chain_r" : nb1 ? "mz_runroll_chain1" : "mz_runroll_chain") +
+        h->last_lvariant = std::string(h->rd_chain ? (h->rd_nb == 3 ? "mz_runroll_chain_r3" : "mz_runroll_chain_r")
+                                                   : nb1 ? "mz_runroll_chain1" : "mz_runroll_chain") +
                            (wide_p ? "+mz_runroll_pred" : h->rp_pred ? "+mz_runroll_pred_r" : nb1 ? "+mz_runroll_pred_n1"
                                                                                        : "+mz_runroll_pred_n");
         if (h->rd_chain)
-            MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_chain_r, dim3((B + U.ng_l - 1) / U.ng_l),
+            MZ_TRY(h, hipLaunchKernel(h->rd_nb == 3 ? (const void*)mz_runroll_chain_r3 : (const void*)mz_runroll_chain_r,
+                                      dim3((B + U.ng_l - 1) / U.ng_l),
                                       dim3(RD_THREADS), args, rd_chain_lds(h), st));
         else
             MZ_TRY(h, hipLaunchKernel(nb1 ? (const void*)mz_runroll_chain1 : (const void*)mz_runroll_chain,

@@ -1295,92 +1295,101 @@ __device__ __forceinline__ void rd_epilogue(const RLayer& L, const mz_f32x4 (&ac
     }
 }
 
-// layer I of the resident chain (wave ob < 4); a[] = this layer's chunks
-template <int NCH>
+// layer I of the resident chain (wave ob < 4); a[] = this layer's chunks;
+// NB column blocks of 16, one after the other (reads, 16 MFMAs, epilogue)
+template <int NCH, int NB = 1>
 __device__ __forceinline__ void rd_layer(const RLayer& L, const float (&a)[NCH][4][4], const float4* ep_lds,
                                          float* lds, int ncols, float bn_s, float bn_r) {
     const int lane = threadIdx.x & 63, ob = threadIdx.x >> 6, kl = lane >> 4, n = lane & 15;
     float4 ep[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) ep[r] = ep_lds[ob * 16 + kl * 4 + r];
-    float res[4];
-    const int nc = n < ncols ? n : ncols - 1;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) res[r] = L.res_add ? lds[L.res_off + rn_out_idx(L.res_kb, ob, kl, r, nc, ncols)] : 0.0f;
-    mz_f32x4 acc[4];
+    for (int i = 0; i < NB; ++i) {
+        const int ni = i * 16 + n;
+        const int nc = ni < ncols ? ni : ncols - 1;
+        float res[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = mz_f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (NCH == 1) {                   // MODE 3: K = 64, NQ = 4, k-blocked input
-        const uint32_t b0 = (uint32_t)(L.in_off + n * 16 + 4 * (((n >> 2) & 3) ^ rn_kb_sigma(kl))) * 4u;
-        float4 v[4];
+        for (int r = 0; r < 4; ++r)
+            res[r] = L.res_add ? lds[L.res_off + rn_out_idx(L.res_kb, ob, kl, r, nc, ncols)] : 0.0f;
+        mz_f32x4 acc[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            v[q] = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(lds) + b0 +
-                                                    (uint32_t)(q * ncols) * 64u);
+        for (int q = 0; q < 4; ++q) acc[q] = mz_f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (NCH == 1) {               // MODE 3: K = 64, NQ = 4, k-blocked input
+            const uint32_t b0 = (uint32_t)(L.in_off + n * 16 + 4 * (((n >> 2) & 3) ^ rn_kb_sigma(kl))) * 4u +
+                                1024u * i;
+            float4 v[4];
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float bv = jj == 0 ? v[q].x : jj == 1 ? v[q].y : jj == 2 ? v[q].z : v[q].w;
-                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][q][jj], bv, acc[q], 0, 0, 0);
-            }
-    } else {                                    // MODE 1: plain input, NQ = L.nq in (4, 4 NCH]
-        const int NQ = L.nq, K = L.K;
-        const int cb = L.in_off + nc;
-        float b[NCH][4][4];
-#pragma unroll
-        for (int c = 0; c < NCH; ++c)
+            for (int q = 0; q < 4; ++q)
+                v[q] = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(lds) + b0 +
+                                                        (uint32_t)(q * ncols) * 64u);
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const int k = (q * NQ + 4 * c + jj) * 4 + kl;
-                    const bool kin = k < K && 4 * c + jj < NQ;
-                    const float v = lds[cb + (kin ? k : K - 1) * ncols];
-                    b[c][jj][q] = kin ? v : 0.0f;
+                    const float bv = jj == 0 ? v[q].x : jj == 1 ? v[q].y : jj == 2 ? v[q].z : v[q].w;
+                    acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][q][jj], bv, acc[q], 0, 0, 0);
                 }
+        } else {                                // MODE 1: plain input, NQ = L.nq in (4, 4 NCH]
+            const int NQ = L.nq, K = L.K;
+            const int cb = L.in_off + nc;
+            float b[NCH][4][4];
 #pragma unroll
-        for (int c = 0; c < NCH; ++c)
+            for (int c = 0; c < NCH; ++c)
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                if (4 * c + jj >= NQ) break;
+                for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][q][jj], b[c][jj][q], acc[q], 0, 0, 0);
-            }
+                    for (int q = 0; q < 4; ++q) {
+                        const int k = (q * NQ + 4 * c + jj) * 4 + kl;
+                        const bool kin = k < K && 4 * c + jj < NQ;
+                        const float v = lds[cb + (kin ? k : K - 1) * ncols];
+                        b[c][jj][q] = kin ? v : 0.0f;
+                    }
+#pragma unroll
+            for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    if (4 * c + jj >= NQ) break;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][q][jj], b[c][jj][q], acc[q], 0, 0, 0);
+                }
+        }
+        if (L.res_add) rd_epilogue<true>(L, acc, ep, res, lds, ob, kl, ni, ncols, bn_s, bn_r);
+        else rd_epilogue<false>(L, acc, ep, res, lds, ob, kl, ni, ncols, bn_s, bn_r);
     }
-    if (L.res_add) rd_epilogue<true>(L, acc, ep, res, lds, ob, kl, n, ncols, bn_s, bn_r);
-    else rd_epilogue<false>(L, acc, ep, res, lds, ob, kl, n, ncols, bn_s, bn_r);
 }
 
-template <int I>
-__device__ __forceinline__ void rd_run(const RPlan& Rd, const float (&a0)[2][4][4], const float (&ar)[RD_NL][4][4],
+template <int I, int NL, int NB>
+__device__ __forceinline__ void rd_run(const RPlan& Rd, const float (&a0)[2][4][4], const float (&ar)[NL][4][4],
                                        const float4* ep_lds, float* lds, int ncols, float bn_s, float bn_r,
                                        unsigned long long* st) {
-    if constexpr (I < RD_NL) {
+    if constexpr (I < NL) {
         const RLayer L = rn_layer_at(Rd, I);
         if constexpr (I == 0) {
 #ifdef MZ_STAMPS
             if (st && (threadIdx.x & 63) == 0) st[(threadIdx.x >> 6) * 64 + 63] = __builtin_amdgcn_s_memtime();
 #endif
-            rd_layer<2>(L, a0, ep_lds, lds, ncols, bn_s, bn_r);
+            rd_layer<2, NB>(L, a0, ep_lds, lds, ncols, bn_s, bn_r);
         } else {
             const float (&a1)[1][4][4] = *reinterpret_cast<const float (*)[1][4][4]>(&ar[I]);
-            rd_layer<1>(L, a1, ep_lds + I * 64, lds, ncols, bn_s, bn_r);
+            rd_layer<1, NB>(L, a1, ep_lds + I * 64, lds, ncols, bn_s, bn_r);
         }
 #ifdef MZ_STAMPS
-        if (st && (threadIdx.x & 63) == 0) st[(threadIdx.x >> 6) * 64 + 2 * I] = __builtin_amdgcn_s_memtime();
+        if (st && (threadIdx.x & 63) == 0 && I < 31) st[(threadIdx.x >> 6) * 64 + 2 * I] = __builtin_amdgcn_s_memtime();
 #endif
         __syncthreads();
 #ifdef MZ_STAMPS
-        if (st && (threadIdx.x & 63) == 0) st[(threadIdx.x >> 6) * 64 + 2 * I + 1] = __builtin_amdgcn_s_memtime();
+        if (st && (threadIdx.x & 63) == 0 && I < 31) st[(threadIdx.x >> 6) * 64 + 2 * I + 1] = __builtin_amdgcn_s_memtime();
 #endif
-        rd_run<I + 1>(Rd, a0, ar, ep_lds, lds, ncols, bn_s, bn_r, st);
+        rd_run<I + 1, NL, NB>(Rd, a0, ar, ep_lds, lds, ncols, bn_s, bn_r, st);
     }
     (void)st;
 }
 
-extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r(RUnrollParams U) {
+// NL: the dynamics chain's layers ([0, dyn_split)); NB: column blocks of the tile
+template <int NL, int NB>
+__device__ __forceinline__ void runroll_chain_r_body(const RUnrollParams& U) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const RPlan& Rr = U.plans_l[MZ_NET_REPR];
     const RPlan& Rd = U.plans_l[MZ_NET_DYN];
@@ -1400,8 +1409,8 @@ extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r(RUnr
 #ifdef MZ_STAMPS
     if (U.stamps && blockIdx.x == 0) { st_r = U.stamps; st_d = U.stamps + 512; }
 #endif
-    float4* ep_lds = reinterpret_cast<float4*>(lds + U.rd_ep_off);   // [RD_NL][64] {bias, γ, β, 0}
-    for (int i = threadIdx.x; i < RD_NL * 64; i += blockDim.x) {
+    float4* ep_lds = reinterpret_cast<float4*>(lds + U.rd_ep_off);   // [NL][64] {bias, γ, β, 0}
+    for (int i = threadIdx.x; i < NL * 64; i += blockDim.x) {
         const RLayer L = rn_layer_at(Rd, i >> 6);
         ep_lds[i] = reinterpret_cast<const float4*>(U.Wimg + L.ep_img)[i & 63];
     }
@@ -1417,17 +1426,17 @@ extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r(RUnr
         rn_stage_l(lds + Rr.in_off, Rr.in_kb, NG, U.P, Rr.in_feat, t, [&](int f) { return ok ? x[f] : 0.0f; });
     }
     __syncthreads();
-    rn_run<true, true, 1, true>(Rr, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, st_r);      // :347
+    rn_run<true, true, NB == 1 ? 1 : 3, true>(Rr, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, st_r);   // :347
     // resident A fragments of the dynamics chain (wave w = row block w), issued
     // after the representation (live across it, they cost its code registers)
     const int lane = threadIdx.x & 63, ob = threadIdx.x >> 6;
-    float a0[2][4][4], ar[RD_NL][4][4];
+    float a0[2][4][4], ar[NL][4][4];
     {
         const RLayer L0 = rn_layer_at(Rd, 0);
         rn_load_a(a0[0], U.Wimg, L0, ob, 0, lane);
         rn_load_a(a0[1], U.Wimg, L0, ob, 1, lane);
 #pragma unroll
-        for (int i = 1; i < RD_NL; ++i) rn_load_a(ar[i], U.Wimg, rn_layer_at(Rd, i), ob, 0, lane);
+        for (int i = 1; i < NL; ++i) rn_load_a(ar[i], U.Wimg, rn_layer_at(Rd, i), ob, 0, lane);
     }
     if (ok) rn_unstage_l(lds + Rr.out0_off, Rr.out0_kb, NG, U.P, H, t, [&](int f, float v) { hs[f] = v; });
     if (ok && t.f0 == 0) U.pr[bs * K1] = 0.0f;                                 // :352 zeros
@@ -1440,13 +1449,21 @@ extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r(RUnr
             rn_stage_l(lds + Rd.in_off, Rd.in_kb, NG, U.P, Rd.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? hp[f] * 2.0f : av; });
         }
         __syncthreads();
-        rd_run<0>(Rd, a0, ar, ep_lds, lds, ncols, U.bn_s, bn_r, s == 1 ? st_d : nullptr);   // :362, [0, split)
+        rd_run<0, NL, NB>(Rd, a0, ar, ep_lds, lds, ncols, U.bn_s, bn_r, s == 1 ? st_d : nullptr);   // :362, [0, split)
         if (ok) {
             if (s < K) rn_unstage_l(lds + Rd.out0_off, Rd.out0_kb, NG, U.P, H, t,
                                     [&](int f, float v) { hs[(size_t)s * H + f] = v; });
             rn_unstage_l(lds + trunk, Rd.L[split].in_kb, NG, U.P, H, t, [&](int f, float v) { ts[(size_t)(s - 1) * H + f] = v; });
         }
     }
+}
+// TicTacToe resnet_hyper (2 blocks: 10 chain layers, 3x3 board: one column
+// block) and Connect4 ResNet-8 (4 blocks: 18 layers, 6x7 board: three)
+extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r(RUnrollParams U) {
+    runroll_chain_r_body<RD_NL, 1>(U);
+}
+extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r3(RUnrollParams U) {
+    runroll_chain_r_body<RD_NL3, 3>(U);
 }
 
 // blockIdx.y = 0: prediction(h_s) for items i = b·KH + s (KH = max(K, 1)):

@@ -186,6 +186,7 @@ struct RUnrollParams {
 // mz_runroll_chain_r: the dynamics chain's layers ([0, dyn_split) = RD_NL:
 // trunk + state head of 2-block towers) with register-resident A fragments
 #define RD_NL 10
+#define RD_NL3 18        // mz_runroll_chain_r3: 4-block towers on three column blocks (Connect4 ResNet-8)
 #define RD_THREADS 256
 // mz_runroll_pred_r: the prediction trunk's RP_NL layers (1 + 2 blocks) the same way
 #define RP_NL 5
