@@ -1205,6 +1205,9 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
         CK(h->rplan[n].n < 0 ? fail(h, "ResNet plan: a k-blocked output buffer") : 0);
         h->rn_lds[n] = (size_t)h->rplan[n].lds_floats * 4;
     }
+    for (int n = 1; n < 3; ++n)                          // mz_rsearch_nets has no k-table path (NOKK)
+        for (int i = 0; i < h->rplan[n].n; ++i)
+            CK(h->rplan[n].L[i].kk > 1 ? fail(h, "ResNet plan: a prediction / dynamics kernel > 1x1") : 0);
     h->packed_w_n = sw.size(); h->packed_b_n = 0;
     h->rn_dyn_split = (int)sp[MZ_NET_DYN].size();     // the reward head: the dynamics layers of chain 2
     for (size_t i = 0; i < sp[MZ_NET_DYN].size(); ++i)

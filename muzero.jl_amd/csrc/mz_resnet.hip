@@ -512,7 +512,7 @@ __device__ __forceinline__ int rn_nbw(const RLayer& L, int NG, int P) {
 
 // NBWMAX = 1: a narrow kernel instance for tiles of one column block (the host
 // launches it only then): the 1-block units alone, a fifth of the code
-template <bool NARROW, bool PF = false, int NBWMAX = 3, bool PIPE = false>
+template <bool NARROW, bool PF = false, int NBWMAX = 3, bool PIPE = false, bool NOKK = false>
 __device__ __forceinline__ void rn_layer(const RLayer& L, const float* __restrict__ Wimg,
                                          const float* __restrict__ flat, float* lds, int NG, int Wb, int P,
                                          float bn_s, float bn_r, const RnPf* pf = nullptr,
@@ -525,9 +525,11 @@ __device__ __forceinline__ void rn_layer(const RLayer& L, const float* __restric
     } else if (L.in_kb) {                                             // 1x1 conv / Dense, K % 64 == 0
         if (!L.spatial || n_nb == 1) RN_L(1, 3);
         else if constexpr (NBWMAX > 1) { if (n_nb == 2) RN_L(2, 3); else RN_L(RN_NBW, 3); }
-    } else if (L.kk > 1) {
-        if (n_nb == 1) RN_L(1, 2);
-        else if constexpr (NBWMAX > 1) { if (n_nb == 2) RN_L(2, 2); else RN_L(3, 2); }
+    } else if (!NOKK && L.kk > 1) {              // (NOKK: plans of 1x1 convs and Dense layers only)
+        if constexpr (!NOKK) {
+            if (n_nb == 1) RN_L(1, 2);
+            else if constexpr (NBWMAX > 1) { if (n_nb == 2) RN_L(2, 2); else RN_L(3, 2); }
+        }
     } else if (L.spatial) {
         if (n_nb == 1) RN_L(1, 1);
         else if constexpr (NBWMAX > 1) { if (n_nb == 2) RN_L(2, 1); else RN_L(RN_NBW, 1); }
@@ -574,7 +576,7 @@ __device__ void rn_fill_ktabs(const RPlan& R, float* lds, int NG, int Wb, int P)
 // PF: the next layer's plan entry, first A chunk and epilogue parameters are
 // loaded before each layer barrier (kernels with the register room: 512
 // threads).  Layers [i0, i1) (i1 < 0: to the end).
-template <bool NARROW = false, bool PF = false, int NBWMAX = 3, bool PIPE = false>
+template <bool NARROW = false, bool PF = false, int NBWMAX = 3, bool PIPE = false, bool NOKK = false>
 __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const float* flat, float* lds, int NG,
                                        int Wb, int P, float bn_s, unsigned long long* st = nullptr, int i0 = 0,
                                        int i1 = -1) {
@@ -596,7 +598,7 @@ __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const 
 #ifdef MZ_STAMPS
             if (st && i - i0 < 31) dbg = st + 1024 + 8 * (i - i0);
 #endif
-            rn_layer<NARROW, true, NBWMAX, PIPE>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, &pf, dbg);
+            rn_layer<NARROW, true, NBWMAX, PIPE, NOKK>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, &pf, dbg);
             if (i + 1 < i1) rn_prefetch<NARROW>(Ln, Wimg, flat, NG, P, pf);
 #ifdef MZ_STAMPS
             if (st && (threadIdx.x & 63) == 0 && i - i0 < 31) st[wv * 64 + 2 * (i - i0)] = __builtin_amdgcn_s_memtime();
@@ -609,7 +611,7 @@ __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const 
         }
     } else {
         for (int i = i0; i < i1; ++i) {
-            rn_layer<NARROW, false, NBWMAX>(rn_layer_at(R, i), Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+            rn_layer<NARROW, false, NBWMAX, false, NOKK>(rn_layer_at(R, i), Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
 #ifdef MZ_STAMPS
             if (st && (threadIdx.x & 63) == 0 && i - i0 < 31) st[wv * 64 + 2 * (i - i0)] = __builtin_amdgcn_s_memtime();
 #endif
@@ -1106,7 +1108,9 @@ extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RS
         lds[R.in_off + rn_conv_idx(R.in_kb, f, g, NG, P.P)] = av;
     }
     __syncthreads();
-    rn_run(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st);
+    // prediction / dynamics: 1x1 convs and Dense layers only (rn_specs), so
+    // the k-table path is left out of this kernel (registers: the 12-wave cap)
+    rn_run<false, false, 3, false, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st);
 #ifdef MZ_STAMPS
     if (st && (threadIdx.x & 63) == 0) st[(threadIdx.x >> 6) * 64 + 61] = __builtin_amdgcn_s_memtime();
 #endif
