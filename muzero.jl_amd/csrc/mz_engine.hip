@@ -874,7 +874,12 @@ static RPlan rn_plan(const mz_handle* h, const std::vector<RSpec>& sp, int net, 
     // LDS allows) has its own region, so that its layout can be k-blocked
     const int X = region(std::max(in_feat * NG, net == MZ_NET_DYN && !sep_b2 ? big : 0));
     const int B0 = region(big), B1 = region(big);
-    const int B2 = net == MZ_NET_DYN && sep_b2 ? region(big) : X;
+    // (aliased, B2 sits at the END of X's region, at a different offset from X:
+    // a region's layout follows the readers of its offset, so B2 can be
+    // k-blocked for the state head's 1x1 convs while X stays plain for the
+    // K = nf + 1 first layer; X is dead once that layer has run)
+    const int xsz = (std::max(in_feat * NG, net == MZ_NET_DYN && !sep_b2 ? big : 0) + 3) / 4 * 4;
+    const int B2 = net == MZ_NET_DYN && sep_b2 ? region(big) : X + (xsz - big) / 4 * 4;
     int headc = 0;
     for (const RSpec& r : sp) if (r.chain && r.conv && r.cout != nf) headc = std::max(headc, r.cout * P * NG);
     const int S0 = region(std::max(headc, hs * NG)), S1 = region(hs * NG), S2 = region(hs * NG);
