@@ -223,6 +223,19 @@ __device__ __forceinline__ float g16_vmax(float v) {
     return v;
 }
 
+// g16_vmax into a fresh register (the first step reads u through DPP, so no
+// copy of u is made); no pad after the last step, whose consumer (the tie
+// compare) is not a DPP instruction.
+__device__ __forceinline__ float g16_vmax_to(float u) {
+    float m;
+    asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf"
+                 : "=&v"(m) : "v"(u));
+    return m;
+}
+
 // select_child loop (SelfPlay.jl:256-268) for the game of this GW-lane group.
 // pUCT (ucb_score :171-184) in f64 with one rounding to f32 (Q5); ties by
 // exact equality, broken by the Philox TIE stream keyed (sim, depth) — the
@@ -248,6 +261,7 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
     const int ac = a < A ? a : A - 1;
     int e = 0, Np = root_N, depth = 0, vtp = root_tp;
     int pe = 0, pc = 0;
+    const uint64_t lgmask = __builtin_amdgcn_ballot_w64(lg);
     SelectOut out;
     for (;;) {
         // the parent's pUCT table entries depend only on Np: read them with the record
@@ -260,7 +274,8 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
         // keep the whole record one load and the score branch-free: without
         // these the compiler sinks the ev load and the division into an
         // Nc > 0 branch (a second LDS round trip and two exec branches)
-        asm volatile("" : "+v"(ed.x), "+v"(ed.y), "+v"(ed.z), "+v"(ed.w), "+v"(pbn), "+v"(sqn));
+        asm volatile("" : "+v"(ed.x), "+v"(ed.y), "+v"(ed.z), "+v"(ed.w));
+        if constexpr (!TAB) asm volatile("" : "+v"(pbn), "+v"(sqn));
         const uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
         const int Nc = (int)(nc & 0xffffu);
         double pb_c;
@@ -284,14 +299,20 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
         const double prior_score = pb_c * pz;
         const float us = (float)(prior_score + vsd);
         const float u = lg ? us : -INFINITY;
-        float m = g16_vmax(u);
+        // GW = 32: the padded form (its consumer is the row-pair permlane)
+        float m = GW == 16 ? g16_vmax_to(u) : g16_vmax(u);
         if constexpr (GW == 32) {
             uint32_t x, y;
             row_pair(__builtin_bit_cast(uint32_t, m), x, y);
             const float fx = __builtin_bit_cast(float, x), fy = __builtin_bit_cast(float, y);
             m = fx > fy ? fx : fy;
         }
-        const uint64_t bal = __builtin_amdgcn_ballot_w64(lg && u == m);
+        // ballot(lg && u == m): one compare into an SGPR pair and a scalar AND
+        // with the walk-invariant legal mask (the builtin form compiled to a
+        // compare, a select and a second compare on the per-level chain)
+        uint64_t eqm;
+        asm volatile("v_cmp_eq_f32_e64 %0, %1, %2" : "=s"(eqm) : "v"(u), "v"(m));
+        const uint64_t bal = eqm & lgmask;
         depth += 1;
         int ach;
         uint32_t ncc;
