@@ -246,6 +246,18 @@ struct mz_handle {
     int32_t* d_rs_index = nullptr;
     int rs_cap = 0;
     bool sp_has_games = false;              // the FIFO never empties once a game is in
+    // get_batch one step ahead (the one-launch FC learner, PER off): the launch
+    // for step t also samples step t+1's batch into the other batch set and
+    // stamps that set's header {epoch, games played, step, B}; the next launch
+    // uses a set only if its header still matches (the same shard state — a
+    // stored game bumps `played` — step and B), else it samples in place.
+    // Anything else that fills set 0 or re-creates the shard bumps the epoch.
+    float *d_rs2_obs = nullptr, *d_rs2_act = nullptr, *d_rs2_tv = nullptr, *d_rs2_tr = nullptr,
+          *d_rs2_tp = nullptr, *d_rs2_gs = nullptr;
+    int32_t* d_rs2_index = nullptr;
+    int pf_cap = 0, pf_cur = 0;
+    long long* d_pf_hdr = nullptr;          // [2][4]
+    long long pf_epoch = 1;
     // actor–learner loop (mz_train_*): the actors' weight set (flat + the
     // search images), the queued nets (remote_NNs, flat), the learner step t
     struct WSet { float* flat = nullptr; float* Wp = nullptr; float* Bp = nullptr; float* smw = nullptr;
@@ -1990,6 +2002,7 @@ static int small_unroll_params(mz_handle* h, const mz_batch* b, int ti, const Rp
         U.stamps = h->d_stamps;
 #endif
         U.sample = rp != nullptr;
+        U.pf_hdr = nullptr; U.pf_epoch = 0;
         if (rp) U.rp = *rp; else std::memset(&U.rp, 0, sizeof(U.rp));
         *Uo = U;
     }
@@ -2471,6 +2484,7 @@ int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games) {
     for (void* p : h->sp_allocs) (void)hipFree(p);
     h->sp_allocs.clear();
     h->rs_cap = 0;
+    h->pf_cap = 0; h->pf_cur = 0; h->d_pf_hdr = nullptr; ++h->pf_epoch;
     h->sp_has_games = false;
     h->tr_B = 0;                                // a new shard: mz_train_init again
     h->sp_env = env_kind; h->sp_G = G; h->sp_cap = replay_games;
@@ -2602,7 +2616,9 @@ int mz_replay_save_game(mz_handle* h, int32_t T, const uint8_t* obs, const int32
 
 // get_batch parameters for B samples at learner step `step` into the
 // engine's batch arrays (allocated on first use); batch = those arrays
-static int rs_params(mz_handle* h, int32_t B, uint32_t step, hipStream_t st, RpSampleParams* Qo, mz_batch* batch) {
+static int rs_params(mz_handle* h, int32_t B, uint32_t step, hipStream_t st, RpSampleParams* Qo, mz_batch* batch,
+                     bool prefetching = false) {
+    if (!prefetching) ++h->pf_epoch;              // set 0 is about to be refilled: its header is stale
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
     if (B < 1) return fail(h, "batch_size must be >= 1");
     if (!h->sp_has_games) {                       // sample_n_games needs a non-empty buffer
@@ -2623,6 +2639,7 @@ static int rs_params(mz_handle* h, int32_t B, uint32_t step, hipStream_t st, RpS
         MZ_TRY(h, spalloc(h, &h->d_rs_index, (size_t)B * 2, false));
         MZ_TRY(h, spalloc(h, &h->d_rs_w, (size_t)B, false));
         h->rs_cap = B;
+        ++h->pf_epoch;
     }
     RpSampleParams Q;
     std::memset(&Q, 0, sizeof(Q));
@@ -2681,6 +2698,35 @@ int mz_replay_sample(mz_handle* h, int32_t B, uint32_t step, mz_batch* batch, in
     return 0;
 }
 
+// the second batch set and the two headers of the get_batch prefetch
+static int ensure_pf(mz_handle* h, int B) {
+    if (B <= h->pf_cap && h->d_pf_hdr) return 0;
+    const int K1 = h->conf.num_unroll_steps + 1, A = h->A;
+    MZ_TRY(h, spalloc(h, &h->d_rs2_obs, (size_t)B * h->obs_feat, false));
+    MZ_TRY(h, spalloc(h, &h->d_rs2_act, (size_t)B * K1, false));
+    MZ_TRY(h, spalloc(h, &h->d_rs2_tv, (size_t)B * K1, false));
+    MZ_TRY(h, spalloc(h, &h->d_rs2_tr, (size_t)B * K1, false));
+    MZ_TRY(h, spalloc(h, &h->d_rs2_tp, (size_t)B * K1 * A, false));
+    MZ_TRY(h, spalloc(h, &h->d_rs2_gs, (size_t)B, false));
+    MZ_TRY(h, spalloc(h, &h->d_rs2_index, (size_t)B * 2, false));
+    if (!h->d_pf_hdr) MZ_TRY(h, spalloc(h, &h->d_pf_hdr, 8));   // zeroed: matches no epoch
+    h->pf_cap = B;
+    ++h->pf_epoch;
+    return 0;
+}
+
+// point the sampler's outputs and the batch at batch set s (0: d_rs_*, 1: d_rs2_*)
+static void pf_set(mz_handle* h, int s, RpSampleParams* Q, mz_batch* b) {
+    Q->obs = s ? h->d_rs2_obs : h->d_rs_obs; Q->actions = s ? h->d_rs2_act : h->d_rs_act;
+    Q->tv = s ? h->d_rs2_tv : h->d_rs_tv; Q->tr = s ? h->d_rs2_tr : h->d_rs_tr;
+    Q->tpol = s ? h->d_rs2_tp : h->d_rs_tp; Q->gscale = s ? h->d_rs2_gs : h->d_rs_gs;
+    Q->index = s ? h->d_rs2_index : h->d_rs_index;
+    if (b) {
+        b->observation = Q->obs; b->actions = Q->actions; b->target_values = Q->tv;
+        b->target_rewards = Q->tr; b->target_policies = Q->tpol; b->gradient_scale = Q->gscale;
+    }
+}
+
 // Learner iteration on a batch drawn from this GPU's replay shard
 // (get_batch + learning!, ReplayBuffer.jl:188-217, Learning.jl:327-404) with
 // the sampling fused into the FC unroll kernel: results are those of
@@ -2692,8 +2738,13 @@ static int learner_sampled(mz_handle* h, int32_t B, uint32_t step, float* grad_d
     MZ_TRY(h, hipSetDevice(h->device));
     RpSampleParams Q;
     mz_batch b;
-    if (rs_params(h, B, step, st, &Q, &b)) return -1;
+    const int ti = small_unroll_ti(h, B);
+    const bool fused = train && ti >= 0 && !h->conf.PER && h->A <= 16 && h->d_sm_w2 && h->kind != 1 &&
+                       h->learn_mode != MZ_LEARN_CORRECTED && !std::getenv("MZ_LEARN_2LAUNCH");
+    const bool pf = fused && !std::getenv("MZ_NO_BATCH_PREFETCH");
+    if (rs_params(h, B, step, st, &Q, &b, pf)) return -1;
     if (ensure_batch(h, B)) return -1;
+    if (pf && ensure_pf(h, B)) return -1;
     h->rs_last_B = B;
     if (h->kind == 1) {                             // ResNet: sample, then the network unroll
         hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, Q);
@@ -2711,12 +2762,25 @@ static int learner_sampled(mz_handle* h, int32_t B, uint32_t step, float* grad_d
         if (per_update(h, B, st)) return -1;                       // Learning.jl:400-404
         return train ? mz_learner_apply_dev(h, nullptr, 1.0f, eta, st) : 0;
     }
-    const int ti = small_unroll_ti(h, B);
-    if (train && ti >= 0 && !h->conf.PER && h->A <= 16 && h->d_sm_w2 && !std::getenv("MZ_LEARN_2LAUNCH")) {
-        // one launch: unroll + losses ‖ Σθ² + ADAM into the second image set, then swap the sets
+    if (fused) {
+        // one launch: unroll + losses ‖ Σθ² + ADAM into the second image set, then swap the sets;
+        // with the prefetch, plus step + 1's get_batch into the other batch set
+        const int cur = pf ? h->pf_cur : 0;
+        RpSampleParams Qn = Q;
+        if (pf) {
+            pf_set(h, cur, &Q, &b);
+            pf_set(h, 1 - cur, &Qn, nullptr);
+            Qn.step = step + 1;
+        }
         SmallUnrollParams U;
         if (small_unroll_params(h, &b, ti, &Q, &U)) return -1;
+        U.pf_hdr = pf ? h->d_pf_hdr + 4 * cur : nullptr;
+        U.pf_epoch = h->pf_epoch;
         LearnParams L;
+        L.pf_nb = pf ? (B + SM_THREADS / 64 - 1) / (SM_THREADS / 64) : 0;
+        L.pfq = Qn;
+        L.pf_hdr_next = pf ? h->d_pf_hdr + 4 * (1 - cur) : nullptr;
+        L.pf_epoch = h->pf_epoch;
         L.nU = (B + ti) / (ti + 1);
         L.tv = b.target_values; L.tp = b.target_policies; L.gscale = b.gradient_scale;
         L.terms = h->d_lterm; L.flat = h->d_flat; L.netoff = h->d_netoff; L.part = h->d_sq; L.counter = h->d_counter;
@@ -2725,7 +2789,9 @@ static int learner_sampled(mz_handle* h, int32_t B, uint32_t step, float* grad_d
                       h->d_sm_bias2, h->d_inv_small};
         void* args[] = {&U, &L};
         MZ_TRY(h, hipLaunchKernel(ti == 0 ? (const void*)mz_learn_small1 : (const void*)mz_learn_small2,
-                                  dim3(L.nU + LEARN_L2_GROUPS), dim3(SM_THREADS), args, unroll_small_lds(h, ti), st));
+                                  dim3(L.nU + LEARN_L2_GROUPS + L.pf_nb), dim3(SM_THREADS), args,
+                                  unroll_small_lds(h, ti), st));
+        if (pf) h->pf_cur = 1 - cur;
         std::swap(h->d_Wp, h->d_Wp2); std::swap(h->d_Bp, h->d_Bp2);
         std::swap(h->d_sm_w, h->d_sm_w2); std::swap(h->d_sm_bias, h->d_sm_bias2);
         adam_advance(h);

@@ -435,11 +435,20 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
     // get_batch of this tile's samples on waves 0..T-1, BEFORE their weight
     // loads: a wave's loads complete in order (vmcnt), so behind 56 image
     // loads the sampler's dependent chain would start only once they land
-    if (P.sample && (tid >> 6) < T && tile0 + (tid >> 6) < P.B)
-        rp_sample_one(P.rp, tile0 + (tid >> 6), tid & 63);
+    bool have = false;                            // prefetched by the previous launch (same shard state)
+    if (P.pf_hdr)
+        have = P.pf_hdr[0] == P.pf_epoch && P.pf_hdr[1] == P.rp.counters[0] && P.pf_hdr[2] == (long long)P.rp.step &&
+               P.pf_hdr[3] == (long long)P.B;
     float wr[SM_MAX_SIM][16];
+    if (!P.pf_hdr && P.sample && (tid >> 6) < T && tile0 + (tid >> 6) < P.B)
+        rp_sample_one(P.rp, tile0 + (tid >> 6), tid & 63);
     sm_load<SM_MAX_SIM>(0, P.n_root, P.w_root, wr);
     sm_load<SM_MAX_SIM>(P.n_root, P.n_sim, P.w_sim, wr);   // sim stages the representation leaves free
+    // with a prefetch the header's answer is waited for only here, under the
+    // weight loads; the in-place sampling it may call for (the first step
+    // after the shard changed) then queues behind them
+    if (P.pf_hdr && P.sample && !have && (tid >> 6) < T && tile0 + (tid >> 6) < P.B)
+        rp_sample_one(P.rp, tile0 + (tid >> 6), tid & 63);
     for (int i = tid; i < P.act_total; i += SM_THREADS) act[i] = 0.0f;
     for (int i = tid; i < nrec * SM_REC_INTS; i += SM_THREADS) rec[i] = P.rec[i];
     __syncthreads();
@@ -544,6 +553,16 @@ __device__ __forceinline__ void learn_body(const SmallUnrollParams& P, const Lea
             P.stamps[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memtime() - t_unroll;
         }
 #endif
+    } else if ((int)blockIdx.x >= L.nU + LEARN_L2_GROUPS) {
+        // the next step's get_batch into the other batch set (read by the next launch)
+        const int b = ((int)blockIdx.x - L.nU - LEARN_L2_GROUPS) * (SM_THREADS / 64) + (tid >> 6);
+        if (b < L.pfq.B) rp_sample_one(L.pfq, b, tid & 63);
+        if ((int)blockIdx.x == L.nU + LEARN_L2_GROUPS && tid == 0) {
+            L.pf_hdr_next[0] = L.pf_epoch;
+            L.pf_hdr_next[1] = L.pfq.counters[0];
+            L.pf_hdr_next[2] = (long long)L.pfq.step;
+            L.pf_hdr_next[3] = (long long)L.pfq.B;
+        }
     } else {
         const int half = tid >> 8, t256 = tid & (MZ_THREADS - 1);
         const int vb = ((int)blockIdx.x - L.nU) * SM_SLOTS + half;

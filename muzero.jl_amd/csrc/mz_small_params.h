@@ -68,6 +68,12 @@ struct SmallUnrollParams {
     // and actions are the arrays above), under the weight-image loads
     int sample;
     RpSampleParams rp;
+    // get_batch prefetched by the previous launch (mz_engine.hip, learner_sampled):
+    // this batch set's header {epoch, games played, step, B}; when it matches
+    // (pf_epoch, rp.counters[0], rp.step, B) the set already holds this step's
+    // batch and the sampling above is skipped.  nullptr: no prefetch.
+    const long long* pf_hdr;
+    long long pf_epoch;
 };
 
 // One-launch learner step (mz_learn_small*, mz_learner_train_dev on one GPU,
@@ -81,6 +87,13 @@ struct LearnParams {
     const float* tv; const float* tp; const float* gscale;
     float* terms; float* flat; const size_t* netoff; double* part; unsigned* counter; float* out;
     LgAdam ad;
+    // blocks [nU + LEARN_L2_GROUPS, + pf_nb): get_batch of the next step (pfq:
+    // the other batch set, step + 1), one wave per sample; the first of them
+    // stamps pf_hdr_next
+    int pf_nb;
+    RpSampleParams pfq;
+    long long* pf_hdr_next;
+    long long pf_epoch;
 };
 #define LEARN_L2_GROUPS ((3 * MZ_L2_BLOCKS + SM_SLOTS - 1) / SM_SLOTS)
 

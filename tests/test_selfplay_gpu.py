@@ -212,6 +212,50 @@ def test_fused_learner_matches_separate_calls(kind, resnet, B):
     e1.close(); e2.close()
 
 
+@pytest.mark.parametrize("kind,B", [("ttt", 32), ("ttt", 40), ("c4", 24)])
+def test_batch_prefetch_matches_in_place_sampling(kind, B, monkeypatch):
+    """The one-launch learner samples step t+1's batch during step t (the
+    other batch set); a prefetched set is used only while the shard, the step
+    and B still match.  Runs with the prefetch and with MZ_NO_BATCH_PREFETCH=1
+    stay bit-identical across every way the match can break: consecutive steps
+    (prefetch used), a step gap, a self-play move storing games, a separate
+    mz_replay_sample (refills set 0), a split learner step, a batch size change."""
+    import torch
+    from muzero_jl_amd.config import cos_schedule
+    mod, _, env_kind = _env(kind)
+    moves = 14 if kind == "ttt" else 30
+    e1, e2 = _device_pair(kind, 16, moves, cap=64)
+    l1 = torch.empty(8, dtype=torch.float32, device="cuda")
+    l2 = torch.empty(8, dtype=torch.float32, device="cuda")
+    grad = torch.empty(e1.grad_count(), dtype=torch.float32, device="cuda")
+    plan = [("t", 1), ("t", 2), ("t", 3), ("t", 5), ("t", 6), ("move", 0), ("t", 7), ("t", 8), ("sample", 9),
+            ("t", 9), ("t", 10), ("split", 11), ("t", 12), ("t", 13), ("B", 14), ("t", 15), ("t", 16)]
+    for eng, lo, pf in ((e1, l1, False), (e2, l2, True)):
+        if pf:
+            monkeypatch.delenv("MZ_NO_BATCH_PREFETCH", raising=False)
+        else:
+            monkeypatch.setenv("MZ_NO_BATCH_PREFETCH", "1")
+        b_cur = B
+        for op, step in plan:
+            if op == "t":
+                eng.learner_train_dev(b_cur, step, cos_schedule(step), lo.data_ptr())
+            elif op == "move":
+                eng.selfplay_move(100 + moves, game_offset=7)
+            elif op == "sample":
+                eng.replay_sample(b_cur, step)
+            elif op == "split":
+                eng.learner_grad_sampled_dev(b_cur, step, grad.data_ptr(), lo.data_ptr())
+                eng.learner_apply_dev(grad.data_ptr(), 1.0, cos_schedule(step))
+            else:
+                b_cur = B + 8
+        eng.sync()
+    monkeypatch.delenv("MZ_NO_BATCH_PREFETCH", raising=False)
+    assert np.array_equal(l1.cpu().numpy()[:6], l2.cpu().numpy()[:6])
+    for n in range(3):
+        assert np.array_equal(e1.get_weights(n), e2.get_weights(n)), n
+    e1.close(); e2.close()
+
+
 @pytest.mark.parametrize("kind,opp,mzp", [("ttt", "random", 1), ("ttt", "random", 2), ("c4", "random", 2),
                                           ("ttt", "self", 1)])
 def test_evaluation_play_matches_host(kind, opp, mzp):
