@@ -333,7 +333,12 @@ int mz_replay_sample(mz_handle* h, int32_t B, uint32_t step, mz_batch* batch, in
  * a gradient exchange before mz_learner_apply_dev).  _train_dev (one GPU,
  * world = 1): also the ADAM step with learning rate eta, fused into the loss
  * kernel — results of the three calls with grad_scale 1.  The batch arrays
- * are left in the handle's mz_replay_sample buffers.  Replaces, per step,
+ * of _grad_sampled_dev are left in the handle's mz_replay_sample buffers.
+ * _train_dev on the one-launch FC path (PER off) also draws step + 1's batch
+ * into a second batch set, which the next call uses only while the shard
+ * (games stored), the step, B and every other sampling call since still
+ * match — identical results, the sampler off the next step's critical path
+ * (env MZ_NO_BATCH_PREFETCH=1 turns it off).  Replaces, per step,
  * the learner's fetch of the buffer + get_batch + learning! iteration
  * (Learning.jl:329-404).                                                    */
 int mz_learner_grad_sampled_dev(mz_handle* h, int32_t B, uint32_t step, float* grad_dev,
