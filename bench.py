@@ -455,8 +455,11 @@ def main():
             "train_loop": train,
             "learner_config": {"batch_size": B, "num_unroll_steps": K, "mode": "ref_semantics",
                                "batch_source": "synthetic device batch" if game is atari else
-                               ("mz_learner_train_dev: one launch — device get_batch + make_target + unroll + "
-                                "losses, ADAM into the second image set" if world == 1 else
+                               (("mz_learner_train_dev: one launch — unroll + losses, ADAM into the second "
+                                 "image set, and step t+1's device get_batch + make_target into the other batch "
+                                 "set (step t's was drawn by the previous launch)" if not resnet else
+                                 "mz_learner_train_dev: device get_batch + make_target, ResNet unroll chain + "
+                                 "predictions, losses with ADAM") if world == 1 else
                                 "mz_learner_grad_sampled_dev (device get_batch fused into the unroll) + RCCL "
                                 "all-reduce + mz_learner_apply_dev")},
             "selfplay_pipeline": pipe,
