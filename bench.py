@@ -26,6 +26,52 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+
+def _self_launch():
+    """`--gpus N` (N > 1) without a torch.distributed launcher (WORLD_SIZE
+    unset): start N fresh child processes of this script, one rank per GPU,
+    with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT
+    set, and exit with their status.  This runs before torch or libmz is
+    imported, so the parent never touches the GPU; the children inherit
+    stdout, and rank 0 prints the one JSON line.  If a rank fails, the others
+    are terminated (by their own Popen handles) and its exit code is
+    returned.  Returns None when there is nothing to launch."""
+    import socket
+    import subprocess
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    a, _ = ap.parse_known_args()
+    if a.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+if __name__ == "__main__":
+    _rc = _self_launch()
+    if _rc is not None:
+        sys.exit(_rc)
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402  (import before libmz: one shared HIP runtime)
 import torch.distributed as dist  # noqa: E402
@@ -80,38 +126,51 @@ def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0, resnet=False,
                        f"oracle/mz_oracle.c on {threads} host thread{'s' if threads > 1 else ''}, {dt:.1f} s")
 
 
-def pmc_traffic(kernel, line=None):
-    """HBM bytes per launch of `kernel` ("a+b": the sum over a launch pair)
-    from the committed PMC summaries
-    (profiles/pmc_*.json of tools/pmc_summary.py, profiles/pmc2_*.json of
-    tools/pmc_kernels.py: FETCH_SIZE x2 for the 16 B/lane image reads, per
-    MI355X_MICROARCH.md, + WRITE_SIZE); the latest round wins, and among
-    pmc2 summaries the bench line's own (`line` in the file name: default /
-    resnet / atari — the same kernel runs different nets there); None if none."""
+def pmc_record(kernel, line=None):
+    """(HBM bytes per launch, source file, counters) of `kernel` ("a+b": the
+    sum over a launch pair) from the committed PMC summaries — profiles/pmc_*.json
+    of tools/pmc_summary.py and profiles/pmc2_*.json of tools/pmc_kernels.py
+    (FETCH_SIZE x2 for the 16 B/lane image reads, per MI355X_MICROARCH.md, +
+    WRITE_SIZE).  The latest round wins, and among pmc2 summaries the bench
+    line's own (`line` in the file name: default / resnet / atari — the same
+    kernel runs different nets there).  These are the committed figures of a
+    separate --pmc run of this command, not a measurement of this run: the
+    line names the file (`traffic_source`).  (None, None, {}) if none."""
     if "+" in kernel:
-        parts = [pmc_traffic(k, line) for k in kernel.split("+")]
-        return None if any(p is None for p in parts) else sum(parts)
+        parts = [pmc_record(k, line) for k in kernel.split("+")]
+        if any(p[0] is None for p in parts):
+            return None, None, {}
+        return sum(p[0] for p in parts), " + ".join(p[1] for p in parts), {}
+    found = (None, None, {})
     if line:
-        own = None
         for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc2_*_{line}.json"))):
             with open(pmc) as f:
                 rec = json.load(f).get("kernels", {}).get(kernel)
             if rec and "hbm_bytes_per_launch_fetch_x2" in rec:
-                own = rec["hbm_bytes_per_launch_fetch_x2"]
-        if own is not None:
-            return own
-    traffic = None
+                found = (rec["hbm_bytes_per_launch_fetch_x2"], os.path.relpath(pmc, ROOT), rec)
+        if found[0] is not None:
+            return found
     for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
         with open(pmc) as f:
             rec = json.load(f)
         if rec.get("kernel") == kernel:
-            traffic = rec.get("hbm_bytes_per_launch")
+            found = (rec.get("hbm_bytes_per_launch"), os.path.relpath(pmc, ROOT), rec)
     for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc2_*.json"))):
         with open(pmc) as f:
             rec = json.load(f).get("kernels", {}).get(kernel)
         if rec and "hbm_bytes_per_launch_fetch_x2" in rec:
-            traffic = rec["hbm_bytes_per_launch_fetch_x2"]
-    return traffic
+            found = (rec["hbm_bytes_per_launch_fetch_x2"], os.path.relpath(pmc, ROOT), rec)
+    return found
+
+
+def bound_of(kernel, rec):
+    """"mfma" for the kernels built on f32 MFMA; "valu" for the VALU-only FC
+    small kernels (their PMC shows SQ_INSTS_MFMA = 0): the peak is the same
+    157.3 TFLOP/s f32 vector rate, and what actually limits them is latency
+    (the share of wave cycles parked is `wait_any_frac`)."""
+    if rec.get("SQ_INSTS_MFMA") == 0.0 or kernel.startswith(("mz_search_small", "mz_learn_small")):
+        return "valu"
+    return "mfma"
 
 
 def workload(game, resnet, G, S):
@@ -148,11 +207,30 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host threads of the oracle baseline (the box's CPU share for one GPU is 16)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--search-only", action="store_true",
+                    help="the search leg only (no self-play pipeline, learner or actor-learner legs): the command "
+                         "whose rocprof kernel stats cover the timed searches alone")
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="(tests) ranks join a gloo group, all-reduce their rank ids on the CPU and rank 0 prints "
+                         "one JSON line; no GPU call")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE = {world}"
+    if args.launcher_selftest:
+        if world > 1:
+            dist.init_process_group("gloo")
+        t = torch.tensor([float(rank + 1)])
+        if world > 1:
+            dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "rank_sum": float(t.item()), "pid": os.getpid()}), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     # one rank per GPU over RCCL ("nccl").  MZ_DIST_BACKEND=gloo with more ranks
     # than GPUs rehearses the N > 1 path on a one-GPU box (ranks share device
     # local % #GPUs; gloo all-reduces the CUDA gradient through the host)
@@ -247,7 +325,7 @@ def main():
     if game is not atari:                                 # (no Atari env: the search leg is configs[4]'s step)
         eng.selfplay_init(env_kind, G, max(G, conf.replay_buffer_size))
     mv = 1 << 20                                          # move counter (RNG step keys)
-    if args.pipeline_moves > 0 and game is not atari:
+    if args.pipeline_moves > 0 and game is not atari and not args.search_only:
         for _ in range(3):
             eng.selfplay_move(mv, game_offset=rank * G, stream=sp)
             mv += 1
@@ -267,7 +345,7 @@ def main():
                 "node_expansions_per_s": round(world * G * S * args.pipeline_moves / tpl, 1),
                 "ms_per_move": round(tpl / args.pipeline_moves * 1e3, 4), "moves": args.pipeline_moves}
     torch.cuda.synchronize()                              # (replay_counts syncs only libmz's own stream)
-    while game is not atari and eng.replay_counts()[1] == 0:   # the learner needs finished games
+    while game is not atari and not args.search_only and eng.replay_counts()[1] == 0:   # the learner needs finished games
         eng.selfplay_move(mv, game_offset=rank * G, stream=sp)
         mv += 1
         torch.cuda.synchronize()
@@ -279,73 +357,77 @@ def main():
     # batches sampled on the device from this rank's replay shard (§8f-2),
     # gradient bucket all-reduced over RCCL when world > 1
     B, K = args.batch or conf.batch_size, conf.num_unroll_steps
-    grad = torch.empty(eng.grad_count(), dtype=torch.float32, device=dev)
-    losses = torch.empty(8, dtype=torch.float32, device=dev)
+    learner_sps = lstep_ms = lkern = None
+    if not args.search_only:
+        grad = torch.empty(eng.grad_count(), dtype=torch.float32, device=dev)
+        losses = torch.empty(8, dtype=torch.float32, device=dev)
 
-    if game is atari:                                     # a synthetic batch resident in HBM
-        rng = np.random.default_rng(7 + rank)
-        tpol = rng.random((B, K + 1, A)).astype(np.float32)
-        sb = [atari.observations(B, seed=1000 + rank), rng.integers(1, A + 1, (B, K + 1)).astype(np.float32),
-              rng.uniform(-1, 1, (B, K + 1)).astype(np.float32), np.zeros((B, K + 1), np.float32),
-              tpol / tpol.sum(-1, keepdims=True), rng.integers(1, K + 1, B).astype(np.float32)]
-        sb = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in sb]
+        if game is atari:                                     # a synthetic batch resident in HBM
+            rng = np.random.default_rng(7 + rank)
+            tpol = rng.random((B, K + 1, A)).astype(np.float32)
+            sb = [atari.observations(B, seed=1000 + rank), rng.integers(1, A + 1, (B, K + 1)).astype(np.float32),
+                  rng.uniform(-1, 1, (B, K + 1)).astype(np.float32), np.zeros((B, K + 1), np.float32),
+                  tpol / tpol.sum(-1, keepdims=True), rng.integers(1, K + 1, B).astype(np.float32)]
+            sb = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in sb]
 
-    def lstep(k):
-        if game is atari:
-            eng.learner_grad_dev([x.data_ptr() for x in sb], B, grad.data_ptr(), losses.data_ptr(), stream=sp)
-        elif world == 1:                                  # get_batch + unroll, losses + ADAM: two launches
-            eng.learner_train_dev(B, k + 1, cos_schedule(k + 1), losses.data_ptr(), stream=sp)
-            return
-        else:                                             # get_batch fused into the unroll; ∇ exchanged
-            eng.learner_grad_sampled_dev(B, k + 1, grad.data_ptr(), losses.data_ptr(), stream=sp)
-        if world > 1:
-            dist.all_reduce(grad)
-        eng.learner_apply_dev(grad.data_ptr(), 1.0 / world, cos_schedule(k + 1), stream=sp)
+        def lstep(k):
+            if game is atari:
+                eng.learner_grad_dev([x.data_ptr() for x in sb], B, grad.data_ptr(), losses.data_ptr(), stream=sp)
+            elif world == 1:                                  # get_batch + unroll, losses + ADAM: two launches
+                eng.learner_train_dev(B, k + 1, cos_schedule(k + 1), losses.data_ptr(), stream=sp)
+                return
+            else:                                             # get_batch fused into the unroll; ∇ exchanged
+                eng.learner_grad_sampled_dev(B, k + 1, grad.data_ptr(), losses.data_ptr(), stream=sp)
+            if world > 1:
+                dist.all_reduce(grad)
+            eng.learner_apply_dev(grad.data_ptr(), 1.0 / world, cos_schedule(k + 1), stream=sp)
 
-    for k in range(5):
-        lstep(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    tl0 = time.perf_counter()
-    for k in range(args.learner_steps):
-        lstep(5 + k)
-    torch.cuda.synchronize()
-    tl = torch.tensor([time.perf_counter() - tl0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tl, op=dist.ReduceOp.MAX)
-    learner_sps = args.learner_steps / float(tl.item())
-    # per-step device time: events around each step on the launch stream, in
-    # a separate loop (recording events between steps adds host work)
-    nev = 20
-    lev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nev)]
-    for k in range(nev):
-        lev[k][0].record(stream)
-        lstep(5 + args.learner_steps + k)
-        lev[k][1].record(stream)
-    torch.cuda.synchronize()
-    lstep_ms = float(np.mean([a.elapsed_time(b) for a, b in lev]))
-    # the learner's dominant kernel: FC world 1 = the whole step is one launch
-    # (mz_learn_small*), timed by the events around it; ResNet = the unroll
-    # (chain + predictions, the pair mz_learner_variant names), timed by the engine's events on its launch stream
-    if resnet:
-        eng.debug_enable(4)
-        eng.debug_kernel_time()
         for k in range(5):
-            lstep(5 + args.learner_steps + nev + k)
+            lstep(k)
         torch.cuda.synchronize()
-        t_ms, n_l = eng.debug_kernel_time()
-        eng.debug_enable(0)
-        lkern, lkern_ms = eng.learner_variant(), t_ms / n_l
-    else:
-        lkern = "mz_learn_small1" if world == 1 else None
-        lkern_ms = lstep_ms
+        if world > 1:
+            dist.barrier()
+        tl0 = time.perf_counter()
+        for k in range(args.learner_steps):
+            lstep(5 + k)
+        torch.cuda.synchronize()
+        tl = torch.tensor([time.perf_counter() - tl0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tl, op=dist.ReduceOp.MAX)
+        learner_sps = args.learner_steps / float(tl.item())
+        # per-step device time: events around each step on the launch stream, in
+        # a separate loop (recording events between steps adds host work)
+        nev = 20
+        lev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nev)]
+        for k in range(nev):
+            lev[k][0].record(stream)
+            lstep(5 + args.learner_steps + k)
+            lev[k][1].record(stream)
+        torch.cuda.synchronize()
+        lstep_ms = float(np.mean([a.elapsed_time(b) for a, b in lev]))
+        # the learner's dominant kernel: FC world 1 = the whole step is one launch
+        # (mz_learn_small*), timed by the events around it; ResNet = the unroll
+        # (chain + predictions, the pair mz_learner_variant names), timed by the engine's events on its launch stream
+        if resnet:
+            eng.debug_enable(4)
+            eng.debug_kernel_time()
+            for k in range(5):
+                lstep(5 + args.learner_steps + nev + k)
+            torch.cuda.synchronize()
+            t_ms, n_l = eng.debug_kernel_time()
+            eng.debug_enable(0)
+            lkern, lkern_ms = eng.learner_variant(), t_ms / n_l
+        else:
+            # world 1: the whole step is one launch (mz_learn_small1 / _small2 by batch size, as the engine
+            # records it); world > 1: unroll, all-reduce and ADAM are separate launches (no single kernel)
+            lkern = eng.learner_variant() if world == 1 else None
+            lkern_ms = lstep_ms
 
     # ---- corrected-gradient learner (MZ_LEARN_CORRECTED, FC nets): real
     # backprop through the unroll on MFMA; with world > 1 the exchanged
     # gradient is data-dependent
     corrected = None
-    if not resnet and args.learner_steps > 0:
+    if not resnet and args.learner_steps > 0 and not args.search_only:
         from muzero_jl_amd.abi import LEARN_CORRECTED, LEARN_REF_SEMANTICS
         eng.learner_set_mode(LEARN_CORRECTED)
         for k in range(3):
@@ -377,7 +459,7 @@ def main():
     # moves with the actors' nets and one learner step per finished game, the
     # actors refreshed one checkpoint behind (mz_train_run, one GPU)
     train = None
-    if args.train_moves > 0 and world == 1 and game is not atari:
+    if args.train_moves > 0 and world == 1 and game is not atari and not args.search_only:
         eng.selfplay_init(env_kind, G, max(G, conf.replay_buffer_size))
         eng.train_init(conf.batch_size)
         eng.train_run(3, move0=mv, game_offset=rank * G, stream=sp)
@@ -409,27 +491,36 @@ def main():
         # variant (tools/pmc_summary.py; latest round wins), else null
         variant = "mz_rsearch_nets" if resnet else eng.search_variant()
         pmc_line = "atari" if game is atari else "resnet" if resnet else "default" if game is ttt else None
-        traffic = pmc_traffic(variant, pmc_line)
+        traffic, traffic_src, search_pmc = pmc_record(variant, pmc_line)
         # learner roofline (north_star: HBM GB/s and MFMA utilisation of the
         # learner): algorithmic FLOP of the unroll (2·B·(repr +
         # (K+1)·pred + K·dyn) MACs) + ADAM (~10 FLOP/param, FC one-launch step);
         # algorithmic bytes of the ADAM step = 28 B/param (θ, m, v read and
-        # written, the image scatter), measured traffic from the PMC summary
+        # written, the image scatter; FC and ResNet alike), traffic from the
+        # committed PMC summary of the same kernel
         lroof = None
         if lkern is not None:
             nparam = sum(int(x.size) for x in nets)
             f_unroll = 2 * B * (net_macs(conf, hyper, 0) + (K + 1) * net_macs(conf, hyper, 1) +
                                 K * net_macs(conf, hyper, 2))
+            # ResNet: the timed launch pair is the unroll alone (ADAM runs in the loss kernel after it)
             lflop = f_unroll + (0 if resnet else 10 * nparam)
-            lbytes = 0 if resnet else 28 * nparam
+            # FC: the one-launch step's ADAM (28 B/param); ResNet: the unroll pair alone reads the weights
+            # once (4 B/param), the batch's observations and actions, and writes value / reward / A logits
+            # per (sample, step)
+            lbytes = 28 * nparam if not resnet else \
+                4 * nparam + 4 * B * (obs.shape[1] + (K + 1)) + 4 * B * (K + 1) * (A + 2)
+            lbytes_step = 28 * nparam
             lach = lflop / (lkern_ms * 1e-3) / 1e12
-            ltraffic = pmc_traffic(lkern, pmc_line)
+            ltraffic, ltraffic_src, lpmc = pmc_record(lkern, pmc_line)
             hbm_gbs = (ltraffic if ltraffic else lbytes) / (lkern_ms * 1e-3) / 1e9
-            lroof = {"bound": "mfma", "achieved": round(lach, 4), "peak": PEAK_F32, "unit": "TFLOP/s",
-                     "frac": round(lach / PEAK_F32, 5), "traffic": ltraffic, "kernel": lkern,
+            lroof = {"bound": bound_of(lkern, lpmc), "achieved": round(lach, 4), "peak": PEAK_F32,
+                     "unit": "TFLOP/s", "frac": round(lach / PEAK_F32, 5), "traffic": ltraffic,
+                     "traffic_source": ltraffic_src, "kernel": lkern,
                      "kernel_ms": round(lkern_ms, 5), "flop_per_launch": lflop,
-                     "hbm_bytes_algorithmic": lbytes, "hbm_GBps": round(hbm_gbs, 2),
-                     "hbm_frac": round(hbm_gbs / 8000.0, 5)}
+                     "hbm_bytes_algorithmic": lbytes, "hbm_bytes_algorithmic_per_step": lbytes_step,
+                     "hbm_GBps": round(hbm_gbs, 2), "hbm_frac": round(hbm_gbs / 8000.0, 5),
+                     "mfma_util_chip": lpmc.get("mfma_util_chip")}
         cpu = cpu1 = None
         if world == 1 and not args.no_cpu:
             nt = max(1, min(args.cpu_threads, os.cpu_count() or 1))
@@ -448,8 +539,8 @@ def main():
             "config": {"workload": workload(game, resnet, G, S),
                        "games_per_gpu": G, "sims_per_move": S, "global_games": G * world,
                        "parallelism": f"games sharded x{world}, learner dp{world} (RCCL all-reduce)"},
-            "learner_steps_per_s": round(learner_sps, 1),
-            "learner_step_ms": round(lstep_ms, 5),
+            "learner_steps_per_s": round(learner_sps, 1) if learner_sps else None,
+            "learner_step_ms": round(lstep_ms, 5) if lstep_ms else None,
             "learner_roofline": lroof,
             "learner_corrected": corrected,
             "train_loop": train,
@@ -463,10 +554,11 @@ def main():
                                 "mz_learner_grad_sampled_dev (device get_batch fused into the unroll) + RCCL "
                                 "all-reduce + mz_learner_apply_dev")},
             "selfplay_pipeline": pipe,
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 4), "peak": PEAK_F32, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_F32, 5), "traffic": traffic,
-                         "kernel": variant, "kernel_ms": round(kern_ms, 4),
-                         "flop_per_launch": flop_launch},
+            "roofline": {"bound": bound_of(variant, search_pmc), "achieved": round(achieved, 4), "peak": PEAK_F32,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32, 5), "traffic": traffic,
+                         "traffic_source": traffic_src, "kernel": variant, "kernel_ms": round(kern_ms, 4),
+                         "flop_per_launch": flop_launch, "wait_any_frac": search_pmc.get("wait_any_frac"),
+                         "mfma_util_chip": search_pmc.get("mfma_util_chip")},
             "cpu_baseline": cpu,
             "cpu_baseline_1thread": cpu1,    # the reference's single self-play worker (main.jl:2)
         }

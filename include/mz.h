@@ -380,19 +380,38 @@ int mz_selfplay_slots(mz_handle* h, int32_t* history_len, uint8_t* board, int32_
  * device, for the G lockstep slots of mz_selfplay_init:
  *   mz_train_init: the actors' weight set and the queue start as copies of
  *     the engine's current (initial) nets; learner step t = 0; B = batch.
+ *   mz_train_init_at: the same from learner step t0 (a resume: pass the
+ *     training_step mz_checkpoint_load returned; the Cos η phase, the
+ *     training_steps bound, the temperature and the checkpoint cadence then
+ *     continue from t0).  Checkpoints hold the learner's nets and ADAM state,
+ *     not the actors' or queued sets, so a resume restarts the one-checkpoint
+ *     lag: actors and queue start as copies of the loaded learner nets.
  *   mz_train_run: `moves` times: one self-play move of every slot with the
- *     ACTORS' nets (mz_selfplay_move, move key move0 + m, temperature
- *     visit_softmax_temperature_fn(t)); then one learner step per game saved
- *     by that move (mz_learner_train_dev with step t+1, eta = Cos(t+1)) while
- *     t <= training_steps; after step t with t % checkpoint_interval == 0 and
- *     t > 1 the actors take the queued nets and the learner's nets are queued.
- *     Reads the shard's game counter back once per move (one sync).
- *     state_out[4] = {t, num_played_games, actor refreshes, learner steps of
- *     this call}; losses_dev (device, 6 floats, or NULL) = the last step's.
+ *     ACTORS' nets (mz_selfplay_move, move key move0 + m); each game plays
+ *     at the temperature visit_softmax_temperature_fn(t) of the step t at
+ *     which it started (play_game takes T once per game, SelfPlay.jl:396-407;
+ *     games in progress at mz_train_init_at take that of t0); then one
+ *     learner step per game saved by that move (mz_learner_train_dev with
+ *     step t+1, eta = Cos(t+1)) while t <= training_steps; after step t with
+ *     t % checkpoint_interval == 0 and t > 1 the actors take the queued nets
+ *     and the learner's nets are queued, and — when a networks path is set and
+ *     t > round(0.9 training_steps) — the learner's state is written to
+ *     <networks_path>/<t>.safetensors (mz_checkpoint_save; Learning.jl:416-432).
+ *     Deliberate deviation: the G games run in lockstep on one weight set, so
+ *     a refresh reaches every slot at once, games in progress included; the
+ *     reference's single actor takes new nets only between games
+ *     (SelfPlay.jl:399-401).  Reads the shard's game counter back once per
+ *     move (one sync).  state_out[4] = {t, num_played_games, actor refreshes,
+ *     learner steps of this call}; losses_dev (device, 6 floats, or NULL) =
+ *     the last step's.
+ *   mz_train_set_networks_path: conf.networks_path (Constructors.jl:47) for
+ *     the periodic checkpoints; NULL or "" (the default) writes none.
  *   mz_train_weights_get: the learner's, actors' or queued nets (Flux order).
  * One GPU (world = 1).  oracle/mz_oracle.c ora_train_loop restates it.      */
 enum { MZ_TRAIN_LEARNER = 0, MZ_TRAIN_ACTOR = 1, MZ_TRAIN_QUEUED = 2 };
 int mz_train_init(mz_handle* h, int32_t batch_size);
+int mz_train_init_at(mz_handle* h, int32_t batch_size, int64_t t0);
+int mz_train_set_networks_path(mz_handle* h, const char* networks_path);
 int mz_train_run(mz_handle* h, int32_t moves, uint32_t move0, uint32_t game_offset, int64_t* state_out,
                  float* losses_dev, void* stream);
 int mz_train_weights_get(mz_handle* h, int which, int net, float* flat, size_t n);

@@ -80,6 +80,8 @@ SIGNATURES = {
     "mz_selfplay_slots": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
     "mz_learner_set_mode": (ctypes.c_int, [_VP, ctypes.c_int]),
     "mz_train_init": (ctypes.c_int, [_VP, ctypes.c_int32]),
+    "mz_train_init_at": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_int64]),
+    "mz_train_set_networks_path": (ctypes.c_int, [_VP, ctypes.c_char_p]),
     "mz_train_run": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, _VP, _VP, _VP]),
     "mz_train_weights_get": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP, ctypes.c_size_t]),
     "mz_checkpoint_save": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int64]),
@@ -309,10 +311,17 @@ class Engine:
         """LEARN_REF_SEMANTICS (∇ = 2θ, quirk Q11) or LEARN_CORRECTED (backprop)."""
         self._check(self.lib.mz_learner_set_mode(self.h, mode), "mz_learner_set_mode")
 
-    def train_init(self, batch_size):
+    def train_init(self, batch_size, t0=0):
         """Actor–learner loop (self_play! ‖ learning!, Q16): actors and the
-        queued nets start from the current weights (mz_train_init)."""
-        self._check(self.lib.mz_train_init(self.h, batch_size), "mz_train_init")
+        queued nets start from the current weights (mz_train_init_at; t0 = the
+        learner step to continue from, e.g. a loaded checkpoint's)."""
+        self._check(self.lib.mz_train_init_at(self.h, batch_size, int(t0)), "mz_train_init_at")
+
+    def train_set_networks_path(self, path):
+        """conf.networks_path: periodic checkpoints <path>/<t>.safetensors past
+        0.9 training_steps (Learning.jl:416-432); None = none."""
+        self._check(self.lib.mz_train_set_networks_path(self.h, path.encode() if path else None),
+                    "mz_train_set_networks_path")
 
     def train_run(self, moves, move0=0, game_offset=0, losses_ptr=None, stream=None):
         """`moves` self-play moves with the actors' nets, one learner step per

@@ -30,9 +30,11 @@ def build(force=False, verbose=False, jobs=None, out=None, objdir=None, extra=()
     inc = os.path.join(os.path.dirname(PKG_DIR), "include")
     lib_path = out or LIB_PATH
     objdir = objdir or os.path.join(os.path.dirname(LIB_PATH), "obj")
-    srcs = [os.path.join(csrc, s) for s in SOURCES if os.path.exists(os.path.join(csrc, s))]
-    hdrs = [os.path.join(csrc, h) for h in HEADERS if os.path.exists(os.path.join(csrc, h))] + \
-        [os.path.join(inc, f) for f in ("mz.h", "mz_detmath.h")]
+    srcs = [os.path.join(csrc, s) for s in SOURCES]
+    hdrs = [os.path.join(csrc, h) for h in HEADERS] + [os.path.join(inc, f) for f in ("mz.h", "mz_detmath.h")]
+    missing = [f for f in srcs + hdrs if not os.path.exists(f)]
+    if missing:                      # a dropped source would link into a library with undefined symbols
+        raise FileNotFoundError(f"libmz sources missing: {missing}")
     hdr_t = max(os.path.getmtime(d) for d in hdrs)
     os.makedirs(objdir, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -55,7 +57,8 @@ def build(force=False, verbose=False, jobs=None, out=None, objdir=None, extra=()
         with ThreadPoolExecutor(jobs or min(len(todo), os.cpu_count() or 4, 16)) as ex:
             list(ex.map(compile_one, todo))
     if todo or not os.path.exists(lib_path) or os.path.getmtime(lib_path) < max(os.path.getmtime(o) for o in objs):
-        cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib_path + ".tmp"] + objs
+        cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-Wl,--no-undefined", "-o", lib_path + ".tmp"] + \
+            objs + ["-ldl"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

@@ -238,6 +238,9 @@ struct mz_handle {
     long long* d_sp_counters = nullptr;
     int32_t* d_sp_done = nullptr; int32_t* d_sp_rpos = nullptr;
     float* d_sp_temp = nullptr;             // [G] per-slot temperatures (temperature_threshold)
+    float* d_sp_tgame = nullptr;            // [G] each game's own temperature (mz_train_run)
+    bool sp_latch = false;                  // mz_selfplay_move latches temperatures per game
+    std::string tr_ckpt_path;               // mz_train_set_networks_path: periodic checkpoints
     int sp_eval = 0, sp_opp = MZ_OPP_SELF, sp_mzp = 1;    // mz_selfplay_mode
     long long* d_eval = nullptr;                          // [4] evaluation tally
     float* d_sp_dpow = nullptr;
@@ -1955,6 +1958,7 @@ static int fc_unroll(mz_handle* h, const mz_batch* b, hipStream_t st, const RpSa
         void* args[] = {&U};
         MZ_TRY(h, hipLaunchKernel(ti == 0 ? (const void*)mz_unroll_small1 : (const void*)mz_unroll_small2,
                                   dim3((B + T - 1) / T), dim3(SM_THREADS), args, unroll_small_lds(h, ti), st));
+        h->last_lvariant = ti == 0 ? "mz_unroll_small1" : "mz_unroll_small2";
     } else {
         if (rp) {
             hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, *rp);
@@ -1966,6 +1970,7 @@ static int fc_unroll(mz_handle* h, const mz_batch* b, hipStream_t st, const RpSa
         U.Wp = h->d_Wp; U.Bp = h->d_Bp; U.plan_repr = h->d_plan[0]; U.plan_sim = h->d_plan[4]; U.lay = h->lay;
         hipLaunchKernelGGL(mz_unroll_kernel, dim3((B + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
                            (size_t)h->lay.total * 4, st, U);
+        h->last_lvariant = "mz_unroll_kernel";
     }
     MZ_TRY(h, hipGetLastError());
     return 0;
@@ -2498,6 +2503,7 @@ int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games) {
     MZ_TRY(h, spalloc(h, &h->d_sp_done, (size_t)G));
     MZ_TRY(h, spalloc(h, &h->d_sp_rpos, (size_t)G));
     MZ_TRY(h, spalloc(h, &h->d_sp_temp, (size_t)G));
+    MZ_TRY(h, spalloc(h, &h->d_sp_tgame, (size_t)G));
     MZ_TRY(h, spalloc(h, &h->d_eval, 4));
     MZ_TRY(h, spalloc(h, &h->d_per_cum, (size_t)h->sp_cap));
     MZ_TRY(h, spalloc(h, &h->d_per_p, (size_t)h->sp_cap));
@@ -2529,7 +2535,8 @@ int mz_selfplay_move(mz_handle* h, uint32_t rng_step, uint32_t game_offset, floa
     // temperature_threshold (SelfPlay.jl:344-346): per-slot temperatures
     const bool thr = h->conf.temperature_threshold >= 0;
     S.temperature = temperature; S.temp_threshold = h->conf.temperature_threshold;
-    S.temp_g = thr ? h->d_sp_temp : nullptr;
+    S.temp_g = thr || h->sp_latch ? h->d_sp_temp : nullptr;
+    S.tgame = h->sp_latch ? h->d_sp_tgame : nullptr;
     const int G = h->sp_G;
     const dim3 waves((G + 3) / 4);
     hipLaunchKernelGGL(mz_sp_prepare, waves, dim3(256), 0, st, S);
@@ -2792,6 +2799,7 @@ static int learner_sampled(mz_handle* h, int32_t B, uint32_t step, float* grad_d
                                   dim3(L.nU + LEARN_L2_GROUPS + L.pf_nb), dim3(SM_THREADS), args,
                                   unroll_small_lds(h, ti), st));
         if (pf) h->pf_cur = 1 - cur;
+        h->last_lvariant = ti == 0 ? "mz_learn_small1" : "mz_learn_small2";
         std::swap(h->d_Wp, h->d_Wp2); std::swap(h->d_Bp, h->d_Bp2);
         std::swap(h->d_sm_w, h->d_sm_w2); std::swap(h->d_sm_bias, h->d_sm_bias2);
         adam_advance(h);
@@ -2955,8 +2963,19 @@ static double cos_schedule(int64_t t) {
     return range * (1.0 + std::cos(a)) / 2.0 + off;
 }
 
-int mz_train_init(mz_handle* h, int32_t B) {
+static float temp_fn(int64_t t) { return t < 500000 ? 1.0f : t < 750000 ? 0.5f : 0.25f; }   // SelfPlay.jl:48-56
+
+int mz_train_init(mz_handle* h, int32_t B) { return mz_train_init_at(h, B, 0); }
+
+int mz_train_set_networks_path(mz_handle* h, const char* networks_path) {
     if (!h) return -2;
+    h->tr_ckpt_path = networks_path ? networks_path : "";
+    return 0;
+}
+
+int mz_train_init_at(mz_handle* h, int32_t B, int64_t t0) {
+    if (!h) return -2;
+    if (t0 < 0) return fail(h, "the starting training step must be >= 0");
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
     if (B < 1) return fail(h, "batch_size must be >= 1");
     if (h->dp_world > 1) return fail(h, "mz_train_run is the single-GPU loop (world = 1)");
@@ -2978,7 +2997,10 @@ int mz_train_init(mz_handle* h, int32_t B) {
     if (wset_repack(h, w, h->stream)) return -1;
     MZ_TRY(h, hipMemcpyAsync(h->h_tr_cnt, h->d_sp_counters, sizeof(long long), hipMemcpyDeviceToHost, h->stream));
     MZ_TRY(h, hipStreamSynchronize(h->stream));
-    h->tr_B = B; h->tr_t = 0; h->tr_refresh = 0;
+    // games already in progress keep visit_softmax_temperature_fn(t0) to their end
+    std::vector<float> tg((size_t)h->sp_G, temp_fn(t0));
+    MZ_TRY(h, hipMemcpy(h->d_sp_tgame, tg.data(), tg.size() * 4, hipMemcpyHostToDevice));
+    h->tr_B = B; h->tr_t = t0; h->tr_refresh = 0;
     h->tr_games = h->h_tr_cnt[0];
     return 0;
 }
@@ -2994,9 +3016,12 @@ int mz_train_run(mz_handle* h, int32_t moves, uint32_t move0, uint32_t game_offs
     for (int32_t mv = 0; mv < moves; ++mv) {
         // 1. self-play move with the actors' nets (SelfPlay.jl:343-380); temperature
         //    visit_softmax_temperature_fn(t) (:48-56, 396-397)
-        const float temp = h->tr_t < 500000 ? 1.0f : h->tr_t < 750000 ? 0.5f : 0.25f;
+        //    for the games that start on this move; a game in progress keeps its own
+        const float temp = temp_fn(h->tr_t);
         wset_swap(h, h->tr_actor);
+        h->sp_latch = true;
         const int rc = mz_selfplay_move(h, move0 + (uint32_t)mv, game_offset, temp, st);
+        h->sp_latch = false;
         wset_swap(h, h->tr_actor);
         if (rc) return rc;
         // 2. games saved this move (save_game in slot order, inside the move)
@@ -3018,6 +3043,14 @@ int mz_train_run(mz_handle* h, int32_t moves, uint32_t move0, uint32_t game_offs
                 if (wset_repack(h, h->tr_actor, st)) return -1;
                 MZ_TRY(h, hipMemcpyAsync(h->d_tr_queued, h->d_flat, h->nflat * 4, hipMemcpyDeviceToDevice, st));
                 ++h->tr_refresh;
+                // Learning.jl:427-432: past round(Int, 0.9 training_steps) the nets go to disk
+                // (round half to even, as Julia's round)
+                if (!h->tr_ckpt_path.empty() &&
+                    (double)t > std::nearbyint(0.9 * (double)h->conf.training_steps)) {
+                    MZ_TRY(h, hipStreamSynchronize(st));
+                    const std::string path = h->tr_ckpt_path + "/" + std::to_string(t) + ".safetensors";
+                    if (mz_checkpoint_save(h, path.c_str(), t)) return -1;
+                }
             }
         }
     }

@@ -123,8 +123,13 @@ extern "C" __global__ __launch_bounds__(256) void mz_sp_prepare(SpParams S) {
         const uint32_t m = env_legal(S, g);
         for (int a = 0; a < S.A; ++a) S.legal[(size_t)g * S.A + a] = (m >> a) & 1u;
         S.tp[g] = S.player[g];                                     // :351
+        float tg = S.temperature;
+        if (S.tgame) {                                             // one temperature per game (:396-407)
+            if (t == 0) S.tgame[g] = S.temperature;
+            tg = S.tgame[g];
+        }
         if (S.temp_g)                                              // :344-346
-            S.temp_g[g] = S.temp_threshold >= 0 && t >= S.temp_threshold ? 0.0f : S.temperature;
+            S.temp_g[g] = S.temp_threshold >= 0 && t >= S.temp_threshold ? 0.0f : tg;
     }
 }
 

@@ -51,6 +51,10 @@ struct SpParams {
     // temperature_threshold (SelfPlay.jl:344-346): a game with >= temp_threshold
     // moves recorded plays at temperature 0 (-1 = nothing: every slot at `temperature`)
     float temperature; int temp_threshold; float* temp_g;   // temp_g [G]
+    // actor-learner loop (mz_train_run): each game keeps the temperature of its first move,
+    // as play_game(env, temperature, ...) takes it once per game (SelfPlay.jl:396-407);
+    // tgame [G] holds it (nullptr: every move uses `temperature`)
+    float* tgame;
 };
 
 // get_batch + make_target (ReplayBuffer.jl:5-50, 73-107, 188-217) on the shard

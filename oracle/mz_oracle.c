@@ -1154,6 +1154,7 @@ EXPORT int ora_eval_play(const mz_config* c, const ora_nethp* hp, const float* P
     OCtx X; ctx_init(&X, c, hp, Prep, Ppred, Pdyn, seed);
     float* s_obs = calloc((size_t)G * Tm * OS, 4); int32_t* s_act = calloc((size_t)G * Tm, 4);
     int* s_len = calloc(G, sizeof(int));
+    float* s_temp = calloc(G, sizeof(float));
     OTTT* env = malloc(sizeof(OTTT) * G);
     for (int g = 0; g < G; ++g) ttt_reset(&env[g]);
     float stacked[1024];
@@ -1206,7 +1207,9 @@ EXPORT int ora_eval_play(const mz_config* c, const ora_nethp* hp, const float* P
  *   1. one move of every slot (play_game's loop body, SelfPlay.jl:343-380)
  *      with the ACTOR's nets: move key move0 + m, game id game_offset + g,
  *      temperature visit_softmax_temperature_fn(t) (:48-56, t = learner steps
- *      so far), 0 once a game has temperature_threshold moves (:344-346);
+ *      so far) taken at the game's first move and kept to its end (play_game
+ *      takes T once per game, :396-407), 0 once a game has
+ *      temperature_threshold moves (:344-346);
  *   2. the games that ended are saved in slot order (save_game,
  *      ReplayBuffer.jl:133-161, FIFO of `cap` games) and their slots restart;
  *   3. one learner step per saved game (self_play! take!s training_step once
@@ -1245,6 +1248,7 @@ EXPORT int ora_train_loop(const mz_config* cin, const ora_nethp* hp, float* Pl0,
     float* s_rew = calloc((size_t)G * Tm, 4); int32_t* s_tp = calloc((size_t)G * Tm, 4);
     float* s_cv = calloc((size_t)G * Tm * A, 4); float* s_rv = calloc((size_t)G * Tm, 4);
     int* s_len = calloc(G, sizeof(int));
+    float* s_temp = calloc(G, sizeof(float));
     OTTT* env = malloc(sizeof(OTTT) * G);
     for (int g = 0; g < G; ++g) ttt_reset(&env[g]);
     float* r_obs = calloc((size_t)cap * Tm * OS, 4); int32_t* r_act = calloc((size_t)cap * Tm, 4);
@@ -1271,7 +1275,8 @@ EXPORT int ora_train_loop(const mz_config* cin, const ora_nethp* hp, float* Pl0,
             ora_stacked_obs(&c, oh, s_act + (size_t)g * Tm, T + 1, stacked);           /* :355 */
             uint8_t legal[MAXA]; ttt_legal(&env[g], legal);
             const int p = env[g].player;                                /* :351 */
-            float temp = (float)ora_temp_fn(t);
+            if (T == 0) s_temp[g] = (float)ora_temp_fn(t);   /* one temperature per game, :396-407 */
+            float temp = s_temp[g];
             if (c.temperature_threshold >= 0 && T >= c.temperature_threshold) temp = 0.0f;   /* :344-346 */
             const uint32_t gid = game_offset + (uint32_t)g;
             int root = run_mcts(&X, stacked, legal, p, 1, gid, step, NULL);               /* :359 */
@@ -1337,7 +1342,7 @@ EXPORT int ora_train_loop(const mz_config* cin, const ora_nethp* hp, float* Pl0,
         memcpy(slot_board + (size_t)g * OS, env[g].b, OS);
     }
     ctx_free(&X);
-    free(s_obs); free(s_act); free(s_rew); free(s_tp); free(s_cv); free(s_rv); free(s_len); free(env);
+    free(s_obs); free(s_act); free(s_rew); free(s_tp); free(s_cv); free(s_rv); free(s_len); free(s_temp); free(env);
     free(r_obs); free(r_act); free(r_rew); free(r_tp); free(r_cv); free(r_rv); free(r_len);
     free(b_obs); free(b_act); free(b_tv); free(b_tr); free(b_tp); free(b_gs); free(b_idx); free(hist); free(fin);
     return nh;

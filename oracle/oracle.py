@@ -255,7 +255,7 @@ class Oracle:
         return losses
 
 
-def train_loop(ora, G, cap, moves, move0=0, game_offset=0, state=None):
+def train_loop(ora, G, cap, moves, move0=0, game_offset=0, state=None, t0=0):
     """ora_train_loop (oracle/mz_oracle.c): the actor–learner schedule of
     mz_train_run from fresh slots — ora.params are the learner's nets (updated
     in place); returns dict(t, counters, held games, slots, actor / queued
@@ -266,7 +266,7 @@ def train_loop(ora, G, cap, moves, move0=0, game_offset=0, state=None):
     st = state or ora.learner_state()
     actor = [p.copy() for p in ora.params]
     queued = [p.copy() for p in ora.params]
-    t = np.zeros(1, np.int64)
+    t = np.full(1, t0, np.int64)
     counters = np.zeros(3, np.int64)
     hT = np.zeros(cap, np.int32)
     hobs = np.zeros((cap, Tm, 27), np.float32)

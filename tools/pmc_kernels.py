@@ -7,7 +7,8 @@ derived figures when the counters are present: HBM bytes per launch
 (FETCH_SIZE, WRITE_SIZE are KB; the raw sum and the sum with FETCH_SIZE x2 —
 gfx950 reports half of 16 B/lane streaming reads, MI355X_MICROARCH.md HBM
 section), VALU instructions per MFMA, the share of wave cycles parked
-(SQ_WAIT_ANY / SQ_WAVE_CYCLES) and MFMA busy per busy cycle."""
+(SQ_WAIT_ANY / SQ_WAVE_CYCLES) and the MFMA utilisation against the
+chip (busy cycles / (1,024 SIMDs x kernel cycles))."""
 import csv
 import glob
 import json
@@ -41,8 +42,18 @@ def main():
             r["valu_per_mfma"] = r.get("SQ_INSTS_VALU", 0.0) / r["SQ_INSTS_MFMA"]
         if r.get("SQ_WAVE_CYCLES"):
             r["wait_any_frac"] = r.get("SQ_WAIT_ANY", 0.0) / r["SQ_WAVE_CYCLES"]
-        if r.get("SQ_BUSY_CYCLES") and "SQ_VALU_MFMA_BUSY_CYCLES" in r:
-            r["mfma_busy_per_busy_cycle"] = r["SQ_VALU_MFMA_BUSY_CYCLES"] / r["SQ_BUSY_CYCLES"]
+        # MFMA utilisation against the chip: SQ_VALU_MFMA_BUSY_CYCLES is summed over every SIMD
+        # (= 32 cycles per v_mfma_f32_16x16x4_f32 issued), so divide by 1,024 SIMDs x the kernel's
+        # cycles.  Kernel cycles: GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs, MI355X_MICROARCH.md
+        # "DVFS give-back") when that pass was collected, else SQ_BUSY_CYCLES / 32 (one count per
+        # shader engine, 32 of them).
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in r:
+            cyc = r["GRBM_GUI_ACTIVE"] / 8.0 if r.get("GRBM_GUI_ACTIVE") else \
+                r["SQ_BUSY_CYCLES"] / 32.0 if r.get("SQ_BUSY_CYCLES") else None
+            if cyc:
+                r["kernel_cycles"] = cyc
+                r["kernel_cycles_source"] = "GRBM_GUI_ACTIVE/8" if r.get("GRBM_GUI_ACTIVE") else "SQ_BUSY_CYCLES/32"
+                r["mfma_util_chip"] = r["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cyc)
         res["kernels"][k] = r
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
