@@ -16,7 +16,8 @@
  *     host-synchronous call (weights, state, checkpoints, replay / debug
  *     read-outs, the host-buffer search and learner step) first waits for all
  *     of the process's work on the device, so `_dev` work queued on a caller
- *     stream is complete before it reads or overwrites engine memory;
+ *     stream is complete before it reads or overwrites engine memory
+ *     (mz_set_sync_stream narrows that wait to one caller stream);
  *   - action ids are 1-based (Julia convention), arrays are column-major with
  *     the reference's shapes (W,H,C,N): feature index = w + W*h + W*H*c.
  */
@@ -168,6 +169,14 @@ int mz_mcts_search_dev(mz_handle* h, int G, const float* obs, const uint8_t* leg
                        uint32_t game_offset, float temperature,
                        float* child_visits, float* root_value, int32_t* action_out,
                        void* stream);
+
+/* Host-synchronous calls wait for ALL of the process's device work by
+ * default (hipDeviceSynchronize), which is always safe.  A caller that
+ * orders its own `_dev` work can narrow that wait with narrow = 1: the calls
+ * then wait only for `stream` (a hipStream_t as void*; NULL = the legacy
+ * default stream) and the handle's own stream.  narrow = 0 restores the
+ * device-wide wait.                                                        */
+int mz_set_sync_stream(mz_handle* h, void* stream, int narrow);
 
 /* Debug/parity: flags & 1 = keep a copy of every search's final tree in HBM
  * (the LDS-resident tree is otherwise discarded at kernel exit); flags & 2 =

@@ -189,6 +189,10 @@ function train_weights(e::Engine, which::Cint, net::Cint)
     flat
 end
 
+# host-synchronous calls wait only for `stream` (a HIP stream handle) and the engine's own; narrow=false: all work
+set_sync_stream!(e::Engine, stream::Ptr{Cvoid}; narrow=true) =
+    check(e, ccall((:mz_set_sync_stream, libmz), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Cint), e.h, stream, Cint(narrow)))
+
 # ---- data-parallel learner over RCCL without torch (one engine per GPU / Distributed.jl worker)
 function dp_unique_id()                        # on rank 0; send the 128 bytes to the other workers
     id = zeros(UInt8, 128)

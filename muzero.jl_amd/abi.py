@@ -54,6 +54,7 @@ SIGNATURES = {
     "mz_mcts_search_dev": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, ctypes.c_int, ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_float, _VP, _VP, _VP, _VP]),
     "mz_debug_enable": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "mz_set_sync_stream": (ctypes.c_int, [_VP, _VP, ctypes.c_int]),
     "mz_debug_tree": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP]),
     "mz_debug_unroll": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP]),
     "mz_debug_kernel_time": (ctypes.c_int, [_VP, _VP, _VP]),
@@ -235,6 +236,10 @@ class Engine:
         self._check(self.lib.mz_mcts_search_dev(self.h, G, obs_ptr, legal_ptr, tp_ptr, int(exploration),
                                                 rng_step & 0xffffffff, game_offset, temperature, cv_ptr,
                                                 rv_ptr, act_ptr, stream), "mz_mcts_search_dev")
+
+    def set_sync_stream(self, stream, narrow=True):
+        """Narrow the host-synchronous calls' wait to `stream` + the handle's own (mz_set_sync_stream)."""
+        self._check(self.lib.mz_set_sync_stream(self.h, stream, int(narrow)), "mz_set_sync_stream")
 
     def debug_enable(self, flags=1):
         self._check(self.lib.mz_debug_enable(self.h, flags), "mz_debug_enable")

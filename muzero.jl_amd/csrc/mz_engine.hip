@@ -167,6 +167,7 @@ struct mz_handle {
     uint64_t seed = 0;
     std::string err;
     hipStream_t stream = nullptr;
+    hipStream_t sync_stream = nullptr; bool sync_narrow = false;   // mz_set_sync_stream
 
     std::vector<LayerSpec> layers;
     std::vector<int> chains[3][3];          // [net][chain] -> layer indices
@@ -300,8 +301,14 @@ static int timing_events(mz_handle* h, hipEvent_t* e0, hipEvent_t* e1);
 // copies) wait for ALL of this process's work on the device, not only the
 // handle's stream: `_dev` calls may have queued work on a caller stream
 // (torch's, created non-blocking like the handle's), which a blocking
-// hipMemcpy would not wait for.
-static hipError_t sync_device(mz_handle* h) { (void)h; return hipDeviceSynchronize(); }
+// hipMemcpy would not wait for.  A caller that orders its own
+// work narrows the wait to one named stream plus the handle's own with
+// mz_set_sync_stream, so unrelated device work is not waited for.
+static hipError_t sync_device(mz_handle* h) {
+    if (!h->sync_narrow) return hipDeviceSynchronize();
+    hipError_t e = hipStreamSynchronize(h->sync_stream);
+    return e != hipSuccess ? e : hipStreamSynchronize(h->stream);
+}
 
 template <typename T>
 static hipError_t dalloc(mz_handle* h, T** p, size_t n) {
@@ -560,7 +567,7 @@ static int build_small(mz_handle* h) {
     h->sm_n_sim = (int)kq_s.size();
     h->sm_n_root = (int)kq_r.size();
     const int nrec = h->sm_n_sim + h->sm_n_root;
-    // weight / bias gather images: [rec][slot][q*64 + lane][16] and [rec][slot][row]
+    // weight / bias gather images: [rec] stage images (sm_widx) and [rec][slot][row]
     std::vector<int> sw((size_t)nrec * SM_SLOTS * 256 * 16, -1), sb((size_t)nrec * SM_SLOTS * 64, -1);
     auto fill = [&](const std::vector<int>& set, const std::vector<int>& st, const std::vector<int>& sl,
                     const std::vector<int>& b0, int rec0) {
@@ -574,7 +581,7 @@ static int build_small(mz_handle* h) {
                     for (int j = 0; j < kq; ++j) {
                         const int k = q * kq + j;
                         if (k >= L.in) continue;
-                        sw[(((size_t)r * SM_SLOTS + sl[i]) * 256 + q * 64 + srow) * 16 + j] =
+                        sw[sm_widx(r, sl[i], q, srow, j)] =
                             (int)(L.flux_w + row + (size_t)L.out * k);
                     }
             }
@@ -662,7 +669,9 @@ static int build_small(mz_handle* h) {
                       (size_t)4 * (S + 2) + MZ_MAX_ACTIONS;
         // + the pb_term triangle (the small kernel requires it in LDS; when
         // the total exceeds the LDS budget the tile-16 kernel is used)
-        h->sm_lds[ti] = ints * 4 + (size_t)T * h->tree_game_bytes + pbterm_count(S) * 8;
+        h->sm_lds[ti] = ints * 4 + (size_t)T * h->tree_game_bytes + pbterm_count(S) * 8 +
+                        // the cached select: entries, path levels, N per slot, tags
+                        (size_t)T * (8 * NN + 8 * (S + 2) + 4 * NN) + 16 + 4 * 16 + 4 * 8;
     }
     return 1;
 }
@@ -1775,6 +1784,13 @@ int mz_mcts_search(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     MZ_TRY(h, hipMemcpyAsync(root_value, h->d_rv, (size_t)G * 4, hipMemcpyDeviceToHost, h->stream));
     MZ_TRY(h, hipMemcpyAsync(action_out, h->d_act, (size_t)G * 4, hipMemcpyDeviceToHost, h->stream));
     MZ_TRY(h, sync_device(h));
+    return 0;
+}
+
+int mz_set_sync_stream(mz_handle* h, void* stream, int narrow) {
+    if (!h) return -1;
+    h->sync_stream = (hipStream_t)stream;
+    h->sync_narrow = narrow != 0;
     return 0;
 }
 

@@ -150,22 +150,20 @@ __device__ __forceinline__ void sm_run(int n, const float (&wr)[NMAX][16], const
 }
 
 // Weights of this thread's (slot, row, quarter) for stages 0..n-1 from the
-// host image [stage][slot][q*64 + row][16].
+// host image (sm_widx: chunk i of the slot's 256 threads is 4 KiB contiguous).
 // Stages [k0, k1) only (others untouched: sm_run never reads stages >= n,
 // so the representation's free registers can be filled with sim stages
 // while it runs).
 template <int NMAX>
 __device__ __forceinline__ void sm_load(int k0, int k1, const float* W, float (&wr)[NMAX][16]) {
-    const int tid = threadIdx.x;
-    const int sr = sm_slot_row(tid), sl = sr >> 6, r = sr & 63, q = (tid >> 4) & 3;
+    const int tid = threadIdx.x, sl = tid >> 8, t = tid & 255;
 #pragma unroll
     for (int k = 0; k < NMAX; ++k) {
         if (k >= k0 && k < k1) {
-            const float4* src = reinterpret_cast<const float4*>(
-                W + (((size_t)k * SM_SLOTS + sl) * 256 + q * 64 + r) * 16);
+            const float4* src = reinterpret_cast<const float4*>(W + (((size_t)k * SM_SLOTS + sl) * 4) * 1024) + t;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float4 v = src[i];
+                const float4 v = src[i * 256];
                 wr[k][4 * i] = v.x; wr[k][4 * i + 1] = v.y; wr[k][4 * i + 2] = v.z; wr[k][4 * i + 3] = v.w;
             }
         }
@@ -208,6 +206,16 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     float* l_aval = reinterpret_cast<float*>(l_sqrt + (S + 2));                 // [32]
     double* l_pbterm = reinterpret_cast<double*>(l_aval + MZ_MAX_ACTIONS);     // [pbterm_count(S)]
     char* lds_tree = reinterpret_cast<char*>(l_pbterm + pbterm_count(S));
+    // the cached select (mz_tree_device.h select_path_cached): per game the
+    // entries [NN], the last path's (slot, N) per level [S+2], N per slot [NN]
+    uint2* c_cache = reinterpret_cast<uint2*>(lds_tree + (size_t)T * P.tree_game_bytes);
+    uint2* c_lvl = c_cache + T * NN;
+    int* c_nN = reinterpret_cast<int*>(c_lvl + T * (S + 2));
+    // per game, written by backup for the recompute: {min / max moved (recompute
+    // every node), select depth, tag, root legal mask} and {min, max}
+    int4* c_hdr = reinterpret_cast<int4*>(reinterpret_cast<char*>(smem) +                 // [4], 16-byte aligned
+                                          ((reinterpret_cast<char*>(c_nN + T * NN) - reinterpret_cast<char*>(smem) + 15) & ~15));
+    float2* c_mmx = reinterpret_cast<float2*>(c_hdr + 4);         // [4]
 
     const int tid = threadIdx.x;
     const int g = tid >> 4, a = tid & 15, lane = tid & 63;
@@ -243,6 +251,9 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         const int ggl = tile0 + gl;
         act[P.x_rep + k * T + gl] = ggl < P.G ? P.obs[(size_t)ggl * P.obs_feat + k] : 0.0f;
     }
+    for (int i = tid; i < T * NN; i += SM_THREADS) c_cache[i] = make_uint2(0u, 0u);
+    if (tid < 4) { c_hdr[tid] = make_int4(0, -1, 1, 0); c_mmx[tid] = make_float2(0.0f, 0.0f); }   // no rows
+    int ver = 1;                                                  // wave 0: the tag of this lane's game
     if (tree_thread && a == 0) {
         uint32_t m = 0;
         if (active)
@@ -296,9 +307,9 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         if (tid < 64) {
             // ---- select (:256-268)
             if (active) {
-                const SelectOut so = select_path<true, 16, T>(tree, path, sg_rootN[g], sg_root_tp[g], legal, sg_mmin[g],
-                                                       sg_mmax[g], a, lane, A, P.players, P.discount, l_pbterm, l_pbc,
-                                                       l_sqrt, P.seed, gid, P.rng_step, s);
+                const SelectOut so = select_path_cached(tree, c_cache + g * NN, (uint32_t)ver, path, sg_rootN[g],
+                                                        sg_root_tp[g], legal, sg_mmin[g], sg_mmax[g], a, lane, A,
+                                                        P.players, l_pbterm, P.seed, gid, P.rng_step, s);
                 if (a == 0) { sg_leaf_e[g] = so.leaf_e; sg_leaf_a[g] = so.leaf_a; sg_vtp[g] = so.vtp; sg_depth[g] = so.depth; }
             }
             __builtin_amdgcn_wave_barrier();
@@ -349,9 +360,16 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
                 __builtin_amdgcn_wave_barrier();
                 int rN = sg_rootN[g];
                 float rW = sg_rootW[g], mmin = sg_mmin[g], mmax = sg_mmax[g];
+                const uint32_t omin = __float_as_uint(mmin), omax = __float_as_uint(mmax);
                 backup_path(tree, path, depth, val, tl, A, P.players, P.discount, rN, rW, sg_root_tp[g], mmin,
-                            mmax, a);
-                if (a == 0) { sg_rootN[g] = rN; sg_rootW[g] = rW; sg_mmin[g] = mmin; sg_mmax[g] = mmax; }
+                            mmax, a, c_lvl + g * (S + 2), c_nN + g * NN);
+                const bool moved = __float_as_uint(mmin) != omin || __float_as_uint(mmax) != omax;
+                ver += moved ? 1 : 0;                     // min / max moved: every entry is stale
+                if (a == 0) {
+                    sg_rootN[g] = rN; sg_rootW[g] = rW; sg_mmin[g] = mmin; sg_mmax[g] = mmax;
+                    c_hdr[g] = make_int4(moved ? 1 : 0, depth, ver, (int)legal);
+                    c_mmx[g] = make_float2(mmin, mmax);
+                }
             }
         } else if (tid >= 128 && tid < 128 + 16 * T) {
             // ---- expand slot s+1 (:280): wave 2 lanes 16 g2 + a2 (g2, a2 as wave 0's g, a)
@@ -373,6 +391,34 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         }
         __syncthreads();
         SM_STAMP(4);
+        // ---- the cached select's entries for the next simulation (all waves,
+        // one 16-lane row per node): the nodes of this path, or every
+        // expanded node when min / max moved
+        if (s + 1 < S) {
+            const int r = tid >> 4, gq = r % T, j0 = r / T;
+            // every read of the first row is independent of the others: the header,
+            // min / max, and both candidate (slot, N) sources
+            const int4 hd = c_hdr[gq];
+            const float2 mm = c_mmx[gq];
+            const uint2 l0 = c_lvl[gq * (S + 2) + j0];
+            const int n0 = c_nN[gq * NN + j0];
+            const bool full = hd.x != 0;
+            const int n = full ? s + 2 : hd.y + 1;
+            const bool lgl = a < A && (((uint32_t)hd.w >> a) & 1u);
+            const TreeView tq = tree_view(lds_tree + (size_t)gq * P.tree_game_bytes, E, NN);
+            uint2* cq = c_cache + gq * NN;
+            if (j0 < n)
+                cache_row(tq, cq, (uint32_t)hd.z, full ? j0 : (int)l0.x, full ? n0 : (int)l0.y, lgl, a, A, mm.x, mm.y,
+                          l_pbterm, lane);
+            for (int j = j0 + SM_THREADS / 16 / T; j < n; j += SM_THREADS / 16 / T) {   // deep paths, large trees
+                int slot, Np;
+                if (full) { slot = j; Np = c_nN[gq * NN + j]; }
+                else { const uint2 l = c_lvl[gq * (S + 2) + j]; slot = (int)l.x; Np = (int)l.y; }
+                cache_row(tq, cq, (uint32_t)hd.z, slot, Np, lgl, a, A, mm.x, mm.y, l_pbterm, lane);
+            }
+            __syncthreads();
+            SM_STAMP(6);                           // stamp build: slot 6 = the cache recompute (+ finish)
+        }
     }
     __syncthreads();
 

@@ -17,6 +17,16 @@
 
 typedef float sm_f32x4 __attribute__((ext_vector_type(4)));
 
+// Register image of one stage: [slot][chunk c = j/4][thread t of the slot][4],
+// t = (slot row / 16)*64 + q*16 + slot row % 16 — thread (tid & 255) of the
+// slot holds weight j of its (row, quarter) at chunk j/4, so every one of a
+// wave's four float4 loads per stage reads 1 KiB contiguous (whole cache
+// lines) instead of 16 B at a 64-B stride.
+__host__ __device__ __forceinline__ size_t sm_widx(int stage, int slot, int q, int srow, int j) {
+    const int t = (srow >> 4) * 64 + q * 16 + (srow & 15);
+    return ((((size_t)stage * SM_SLOTS + slot) * 4 + (j >> 2)) * 256 + t) * 4 + (j & 3);
+}
+
 // Per stage, the host-built record: one int4 per [slot][row] (copied to LDS)
 //   .x  input base of the row's layer in the activation buffer (0 if unused:
 //       the row's weights are zero and its output is dropped)
@@ -34,8 +44,8 @@ struct SmallParams {
     const float* obs; const uint8_t* legal; const int32_t* to_play;
     float* child_visits; float* root_value; int32_t* action_out;
     int n_sim, n_root;
-    const float* w_sim;    // [n_sim][slot][q*64 + lane][16]
-    const float* w_root;   // [n_root][slot][q*64 + lane][16]
+    const float* w_sim;    // [n_sim] stage images (sm_widx)
+    const float* w_root;   // [n_root] stage images (sm_widx)
     const int* rec;        // [n_sim + n_root][SM_REC_INTS] (bias slots filled from `bias`)
     const float* bias;     // [n_sim + n_root][slot][64] (re-gathered from the parameters)
     int act_total;
@@ -55,8 +65,8 @@ struct SmallUnrollParams {
     const float* actions;  // (K+1, B) float action ids
     float* pv; float* pp; float* pr;   // (K+1,B), (A,K+1,B), (K+1,B)
     int n_sim, n_root;
-    const float* w_sim;    // [n_sim][slot][q*64 + row][16] register image (as the search)
-    const float* w_root;   // [n_root][slot][q*64 + row][16]
+    const float* w_sim;    // [n_sim] stage images (sm_widx), as the search
+    const float* w_root;   // [n_root] stage images (sm_widx)
     const float* bias;     // [n_sim + n_root][slot][64]
     const int* rec;        // [n_sim + n_root][SM_REC_INTS]
     int act_total;

@@ -377,6 +377,120 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
     return out;
 }
 
+// ---------------------------------------------------------------------------
+// Cached select (the small kernel, GW = 16).  select_child's argmax at a node
+// depends on the node's N, its children's (N, W, P, ev) and MinMaxStats.  The
+// first two change only when the node lies on a backup path; MinMaxStats
+// changes with any backup.  So after every backup the argmax of each node on
+// the path is recomputed (cache_row, all waves, one 16-lane row per node),
+// and of EVERY expanded node when the backup moved min or max (the game's
+// tag `ver` is then bumped).  An entry {ver << 5 | child, nc of that edge}
+// stamped with the current tag is therefore exactly select_child's answer,
+// and select walks the tree by one LDS read per level.  A node whose maximum
+// ties is stored as 0 (never current): select computes it in full, with the
+// Philox TIE draw keyed by (simulation, depth) as the oracle does.  The score
+// is the same f32/f64 expression as select_path's, so the entries are
+// bit-identical to a full evaluation.
+__device__ __forceinline__ float pucb_score(const float4& ed, const double* prow, int Np, bool lg, bool norm,
+                                            float mmin, float den) {
+    const uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
+    const int Nc = (int)(nc & 0xffffu);
+    const double pb_c = prow[Nc < Np ? Nc : Np];
+    const float vn = (ed.w - mmin) / den;
+    const float vs = Nc > 0 ? (norm ? vn : ed.w) : 0.0f;
+    const double prior_score = pb_c * (double)ed.z;
+    const float us = (float)(prior_score + (double)vs);
+    return lg ? us : -INFINITY;
+}
+
+// One 16-lane row (a DPP row, row-uniform call) recomputes node `slot`'s entry.
+__device__ __forceinline__ void cache_row(const TreeView& t, uint2* cache, uint32_t tag, int slot, int Np, bool lg,
+                                          int a, int A, float mmin, float mmax, const double* pbterm, int lane) {
+    const int ac = a < A ? a : A - 1;
+    const double* prow = pbterm + (__umul24((unsigned)Np, (unsigned)(Np + 1)) >> 1);
+    const float4 ed = t.e[(int)__umul24((unsigned)slot, (unsigned)A) + ac];
+    const float u = pucb_score(ed, prow, Np, lg, mmax > mmin, mmin, mmax - mmin);
+    const float m = g16_vmax_to(u);
+    const uint64_t eq = __builtin_amdgcn_ballot_w64(lg && u == m);
+    const uint32_t msk = (uint32_t)(eq >> (lane & 48)) & 0xffffu;
+    const int ach = __builtin_ctz(msk | 0x10000u);
+    if (a == ach) {
+        const bool tie = (msk & (msk - 1)) != 0;
+        cache[slot] = tie ? make_uint2(0u, 0u) : make_uint2((tag << 5) | (uint32_t)ach, __builtin_bit_cast(uint32_t, ed.x));
+    }
+}
+
+// select_path (TAB, GW = 16) with the per-node cache: a level whose entry
+// carries the game's current tag costs one ds_read_b64 (the next slot and N
+// come with it); otherwise (a tie, or the root before the first backup) the
+// level is evaluated in full, behind one wave-uniform test.  The games of the
+// wave walk in lockstep, so `depth` is wave-uniform; to_play at the leaf is
+// mod1(root_tp + depth, |players|) (SelfPlay.jl:267), formed once.
+__device__ __forceinline__ SelectOut select_path_cached(const TreeView& t, const uint2* cache, uint32_t ver,
+                                                        int* path, int root_N, int root_tp, uint32_t legal,
+                                                        float mmin, float mmax, int a, int lane, int A, int players,
+                                                        const double* pbterm, uint64_t seed, uint32_t gid,
+                                                        uint32_t step, int sim) {
+    constexpr int GW = 16;
+    const bool lg = a < A && ((legal >> a) & 1u);
+    const bool norm = mmax > mmin;
+    const float den = mmax - mmin;
+    const int ac = a < A ? a : A - 1;
+    int e = 0, Np = root_N, depth = 0;
+    int pe = 0, pc = 0, leaf_e = 0, leaf_a = 0, leaf_d = 0;
+    bool done = false;
+    const uint64_t lgmask = __builtin_amdgcn_ballot_w64(lg);
+    // uniform control flow: a group that reached its leaf idles (its values
+    // frozen by selects) until every group of the wave has
+    for (;;) {
+        uint2 ce = cache[e];
+        asm volatile("" : "+v"(ce.x), "+v"(ce.y));       // one ds_read_b64 (not split into the branches)
+        depth += 1;
+        int ach = (int)(ce.x & 31u);
+        uint32_t ncc = ce.y;
+        const bool stale = !done && (ce.x >> 5) != ver;
+        if (__builtin_amdgcn_ballot_w64(stale) != 0) {   // rare: the level in full, for every group
+            const double* prow = pbterm + (__umul24((unsigned)Np, (unsigned)(Np + 1)) >> 1);
+            const float4 ed = t.e[(int)__umul24((unsigned)e, (unsigned)A) + ac];
+            const uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
+            const float u = pucb_score(ed, prow, Np, lg, norm, mmin, den);
+            const float m = g16_vmax_to(u);
+            uint64_t eqm;
+            asm volatile("v_cmp_eq_f32_e64 %0, %1, %2" : "=s"(eqm) : "v"(u), "v"(m));
+            const uint32_t mask = (uint32_t)((eqm & lgmask) >> (lane & 48)) & 0xffffu;
+            int ch = __builtin_ctz(mask | 0x10000u);
+            const int nt = __builtin_popcount(mask);
+            if (stale && nt > 1) {                        // ties: the Philox draw (oracle select_child)
+                const uint32_t r = mz_rng_u32(seed, MZ_RNG_TIE, gid, step, ((uint32_t)sim << 12) | (uint32_t)depth);
+                ch = nth_set_bit(mask, (int)mz_rng_below(r, (uint32_t)nt));
+            }
+            const uint32_t nch = g16_or(a == ch ? nc : 0u);
+            ach = stale ? ch : ach;
+            ncc = stale ? nch : ncc;
+        }
+        const int ei = (int)__umul24((unsigned)e, (unsigned)A) + ach;
+        const int Cch = (int)(ncc >> 16);
+        const bool keep = !done && a == depth;            // depth < GW: lane `depth` keeps the level
+        pe = keep ? ei : pe;
+        pc = keep ? Cch - 1 : pc;
+        if (depth >= GW) {                                // wave-uniform (rare: deep paths)
+            if (!done && a == 0) { path[2 * depth] = ei; path[2 * depth + 1] = Cch - 1; }
+        }
+        const bool leaf = !done && Cch == 0;
+        leaf_e = leaf ? e : leaf_e;
+        leaf_a = leaf ? ach : leaf_a;
+        leaf_d = leaf ? depth : leaf_d;
+        done = done || Cch == 0;
+        e = done ? e : Cch - 1;
+        Np = done ? Np : (int)(ncc & 0xffffu);
+        if (__builtin_amdgcn_ballot_w64(!done) == 0) break;
+    }
+    depth = leaf_d;
+    if (a >= 1 && a <= depth) { path[2 * a] = pe; path[2 * a + 1] = pc; }
+    const int vtp = players == 2 ? ((root_tp - 1 + depth) & 1) + 1 : (root_tp - 1 + depth) % players + 1;
+    return SelectOut{leaf_e, leaf_a, vtp, depth};
+}
+
 // backpropagate! (SelfPlay.jl:190-217), quirk Q7, for the GW-lane group.
 // Node d of the path (0 = root ... depth = the just-expanded leaf with
 // to_play tl) receives v_in(d): v_in(depth) = the leaf value; otherwise
@@ -390,7 +504,8 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
 template <int GW = 16>
 __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, int depth, float value, int tl,
                                             int A, int players, float discount, int& root_N, float& root_W,
-                                            int root_tp, float& mmin, float& mmax, int a) {
+                                            int root_tp, float& mmin, float& mmax, int a, uint2* lvl = nullptr,
+                                            int* nN = nullptr) {
     if (players != 2) {
         if (a == 0) {
             float v = value;
@@ -413,6 +528,10 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
                     t.ev(i) = R + (players == 1 ? discount * q : discount * (-q));
                 }
                 else { root_N = N; root_W = W; }
+                if (lvl) {                               // the cached select's (slot, N) per level
+                    const int c = d > 0 ? path[2 * d + 1] : 0;
+                    lvl[d] = make_uint2((uint32_t)c, (uint32_t)N); nN[c] = N;
+                }
             }
         }
         root_N = __shfl(root_N, 0, GW); root_W = __shfl(root_W, 0, GW);
@@ -457,6 +576,7 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
                 nc = (nc & 0xffff0000u) | (uint32_t)N;
                 t.nc(i) = nc; t.w(i) = W; t.ev(i) = R + discount * (-q);
             } else { rN = N; rW = W; }
+            if (lvl) { lvl[d] = make_uint2((uint32_t)c, (uint32_t)N); nN[c] = N; }   // the cached select's (slot, N)
         }
     }
     lmin = gmin<GW>(lmin);

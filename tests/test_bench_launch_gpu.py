@@ -112,3 +112,46 @@ def test_configs1_fc_512x50_dev_path():
     from muzero_jl_amd.games import tictactoe as ttt
     variant, _ = _bench_launch(ttt, False, 512, 50, rng_step=3)
     assert variant == "mz_search_small2"
+
+
+def test_narrow_sync_stream():
+    """mz_set_sync_stream: with the wait narrowed to the caller's
+    stream, a host-synchronous call after `_dev` work queued on that stream
+    still sees it complete — the device-buffer search and the host-buffer
+    search give the same bits, and weights written before both read back."""
+    import torch
+    from muzero_jl_amd.abi import Engine
+    from muzero_jl_amd.games import tictactoe as ttt
+    from muzero_jl_amd.networks import init_nets
+    from muzero_jl_amd.selfplay import random_positions
+
+    G = 40
+    conf = dataclasses.replace(ttt.conf, num_iters=16)
+    eng = Engine(conf, ttt.hyper, device=0, max_games=G, rng_seed=1)
+    nets = init_nets(conf, ttt.hyper, seed=5)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(device=dev)
+    eng.set_sync_stream(stream.cuda_stream)
+    for n, w in enumerate(nets):
+        eng.set_weights(n, w)
+    obs, legal, tp = random_positions(ttt.BatchedTicTacToe, G, seed=100)
+    d_obs = torch.from_numpy(np.ascontiguousarray(obs, np.float32)).to(dev)
+    d_legal = torch.from_numpy(np.ascontiguousarray(legal, np.uint8)).to(dev)
+    d_tp = torch.from_numpy(np.ascontiguousarray(tp, np.int32)).to(dev)
+    d_cv = torch.empty((G, 9), dtype=torch.float32, device=dev)
+    d_rv = torch.empty(G, dtype=torch.float32, device=dev)
+    d_act = torch.empty(G, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    eng.mcts_search_dev(G, d_obs.data_ptr(), d_legal.data_ptr(), d_tp.data_ptr(), d_cv.data_ptr(),
+                        d_rv.data_ptr(), d_act.data_ptr(), rng_step=2, stream=stream.cuda_stream)
+    cv, rv, act = eng.mcts_search(obs, legal, tp, rng_step=2)      # narrow wait: `stream` + the handle's
+    stream.synchronize()
+    assert np.array_equal(d_cv.cpu().numpy(), cv)
+    assert np.array_equal(d_rv.cpu().numpy(), rv)
+    assert np.array_equal(d_act.cpu().numpy(), act)
+    for n, w in enumerate(nets):
+        assert np.array_equal(eng.get_weights(n), w)
+    eng.set_sync_stream(None, narrow=False)
+    cv2, _, _ = eng.mcts_search(obs, legal, tp, rng_step=2)
+    assert np.array_equal(cv2, cv)
+    eng.close()

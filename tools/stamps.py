@@ -17,7 +17,7 @@ from muzero_jl_amd.games import tictactoe as ttt  # noqa: E402
 from muzero_jl_amd.networks import init_nets  # noqa: E402
 from muzero_jl_amd.selfplay import random_positions  # noqa: E402
 
-PHASES = ["root", "select", "gather", "nets", "expand", "backup", "finish", "-"]
+PHASES = ["root", "select", "gather", "nets", "expand", "backup", "recomp", "-"]
 
 
 def main():
