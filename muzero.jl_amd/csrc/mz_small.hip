@@ -51,9 +51,29 @@ __device__ __forceinline__ void fmac_bcast(float& acc, float x, float w) {
                  : "+v"(acc) : "v"(x), "v"(w), "i"(J));
 }
 
+#define SM_F2(j, wj)                                                                              \
+    "v_fmac_f32_dpp %0, %2, " wj " row_newbcast:" #j " row_mask:0xf bank_mask:0xf\n\t"            \
+    "v_fmac_f32_dpp %1, %3, " wj " row_newbcast:" #j " row_mask:0xf bank_mask:0xf\n\t"
+
 template <int T, int J = 0>
 __device__ __forceinline__ void sm_chain(const float (&w)[16], const float (&x)[T], float (&acc)[T]) {
-    if constexpr (J < 16) {
+    if constexpr (T == 2 && J == 0) {
+        // the two games' chains interleaved in one block.  The DPP hazard (a
+        // VALU write followed by a DPP read, 2 wait states) concerns the
+        // lane-swizzled source x, which nothing writes inside the chain; the
+        // compiler also pads for the accumulator (an s_nop per pair), which
+        // the interleave already separates by one instruction.  One s_nop 1
+        // up front covers x written by VALU just before (the fused first stage).
+        asm volatile("s_nop 1\n\t"
+                     SM_F2(0, "%4") SM_F2(1, "%5") SM_F2(2, "%6") SM_F2(3, "%7")
+                     SM_F2(4, "%8") SM_F2(5, "%9") SM_F2(6, "%10") SM_F2(7, "%11")
+                     SM_F2(8, "%12") SM_F2(9, "%13") SM_F2(10, "%14") SM_F2(11, "%15")
+                     SM_F2(12, "%16") SM_F2(13, "%17") SM_F2(14, "%18") SM_F2(15, "%19")
+                     : "+v"(acc[0]), "+v"(acc[1])
+                     : "v"(x[0]), "v"(x[1]), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]),
+                       "v"(w[6]), "v"(w[7]), "v"(w[8]), "v"(w[9]), "v"(w[10]), "v"(w[11]), "v"(w[12]), "v"(w[13]),
+                       "v"(w[14]), "v"(w[15]));
+    } else if constexpr (J < 16) {
 #pragma unroll
         for (int g = 0; g < T; ++g) fmac_bcast<J>(acc[g], x[g], w[J]);
         sm_chain<T, J + 1>(w, x, acc);
@@ -398,10 +418,12 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
             const int r = tid >> 4, gq = r % T, j0 = r / T;
             // every read of the first row is independent of the others: the header,
             // min / max, and both candidate (slot, N) sources
-            const int4 hd = c_hdr[gq];
-            const float2 mm = c_mmx[gq];
-            const uint2 l0 = c_lvl[gq * (S + 2) + j0];
-            const int n0 = c_nN[gq * NN + j0];
+            int4 hd = c_hdr[gq];
+            float2 mm = c_mmx[gq];
+            uint2 l0 = c_lvl[gq * (S + 2) + j0];
+            int n0 = c_nN[gq * NN + j0];
+            asm volatile("" : "+v"(hd.x), "+v"(hd.y), "+v"(hd.z), "+v"(hd.w), "+v"(mm.x), "+v"(mm.y), "+v"(l0.x),
+                              "+v"(l0.y), "+v"(n0));   // all issued together, one wait
             const bool full = hd.x != 0;
             const int n = full ? s + 2 : hd.y + 1;
             const bool lgl = a < A && (((uint32_t)hd.w >> a) & 1u);

@@ -391,6 +391,24 @@ __device__ __forceinline__ SelectOut select_path(const TreeView& t, int* path, i
 // Philox TIE draw keyed by (simulation, depth) as the oracle does.  The score
 // is the same f32/f64 expression as select_path's, so the entries are
 // bit-identical to a full evaluation.
+// Lane-mask helpers (SGPR masks, no i1 round trips): v_cmp into an SGPR
+// pair, and v_cndmask on one.
+__device__ __forceinline__ uint64_t mz_vcmp_ne(uint32_t x, uint32_t y) {
+    uint64_t m;
+    asm("v_cmp_ne_u32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(y));
+    return m;
+}
+__device__ __forceinline__ uint64_t mz_vcmp_eq(uint32_t x, uint32_t y) {
+    uint64_t m;
+    asm("v_cmp_eq_u32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(y));
+    return m;
+}
+__device__ __forceinline__ int mz_vsel(uint64_t m, int if_set, int if_clear) {
+    int r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(m));
+    return r;
+}
+
 __device__ __forceinline__ float pucb_score(const float4& ed, const double* prow, int Np, bool lg, bool norm,
                                             float mmin, float den) {
     const uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
@@ -436,20 +454,24 @@ __device__ __forceinline__ SelectOut select_path_cached(const TreeView& t, const
     const bool norm = mmax > mmin;
     const float den = mmax - mmin;
     const int ac = a < A ? a : A - 1;
-    int e = 0, Np = root_N, depth = 0;
-    int pe = 0, pc = 0, leaf_e = 0, leaf_a = 0, leaf_d = 0;
-    bool done = false;
     const uint64_t lgmask = __builtin_amdgcn_ballot_w64(lg);
-    // uniform control flow: a group that reached its leaf idles (its values
-    // frozen by selects) until every group of the wave has
-    for (;;) {
+    // Lane state, frozen per group once its leaf is reached: e = the node being
+    // selected from (at the end: the leaf's parent), npc = the nc word of the
+    // edge into e (its N), lach / dg = action and depth of the last level
+    // walked.  `am` = lanes whose group is still walking (an SGPR mask, so the
+    // freezes are single v_cndmask ops and the loop exit a scalar test).
+    int e = 0, dg = 0, lach = 0, pe = 0, pc = 0;
+    uint32_t npc = (uint32_t)root_N;
+    uint64_t am = __builtin_amdgcn_ballot_w64(true);
+    for (int depth = 1;; ++depth) {
         uint2 ce = cache[e];
         asm volatile("" : "+v"(ce.x), "+v"(ce.y));       // one ds_read_b64 (not split into the branches)
-        depth += 1;
         int ach = (int)(ce.x & 31u);
         uint32_t ncc = ce.y;
-        const bool stale = !done && (ce.x >> 5) != ver;
-        if (__builtin_amdgcn_ballot_w64(stale) != 0) {   // rare: the level in full, for every group
+        const uint64_t stm = mz_vcmp_ne(ce.x >> 5, ver) & am;
+        if (stm != 0) {                                   // rare: the level in full, for every group
+            const bool stale = (stm >> lane) & 1u;
+            const int Np = (int)(npc & 0xffffu);
             const double* prow = pbterm + (__umul24((unsigned)Np, (unsigned)(Np + 1)) >> 1);
             const float4 ed = t.e[(int)__umul24((unsigned)e, (unsigned)A) + ac];
             const uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
@@ -469,26 +491,26 @@ __device__ __forceinline__ SelectOut select_path_cached(const TreeView& t, const
             ncc = stale ? nch : ncc;
         }
         const int ei = (int)__umul24((unsigned)e, (unsigned)A) + ach;
-        const int Cch = (int)(ncc >> 16);
-        const bool keep = !done && a == depth;            // depth < GW: lane `depth` keeps the level
-        pe = keep ? ei : pe;
-        pc = keep ? Cch - 1 : pc;
+        const int Cch = (int)(ncc >> 16);                 // child slot + 1, 0 = the leaf
+        const uint64_t km = mz_vcmp_eq((uint32_t)a, (uint32_t)depth) & am;   // lane `depth` keeps the level
+        pe = mz_vsel(km, ei, pe);
+        pc = mz_vsel(km, Cch, pc);
+        lach = mz_vsel(am, ach, lach);
+        dg = mz_vsel(am, depth, dg);
         if (depth >= GW) {                                // wave-uniform (rare: deep paths)
-            if (!done && a == 0) { path[2 * depth] = ei; path[2 * depth + 1] = Cch - 1; }
+            uint64_t wm = am;
+            asm volatile("" : "+s"(wm));                  // the lane test stays inside this branch
+            if (a == 0 && ((wm >> lane) & 1u)) { path[2 * depth] = ei; path[2 * depth + 1] = Cch - 1; }
         }
-        const bool leaf = !done && Cch == 0;
-        leaf_e = leaf ? e : leaf_e;
-        leaf_a = leaf ? ach : leaf_a;
-        leaf_d = leaf ? depth : leaf_d;
-        done = done || Cch == 0;
-        e = done ? e : Cch - 1;
-        Np = done ? Np : (int)(ncc & 0xffffu);
-        if (__builtin_amdgcn_ballot_w64(!done) == 0) break;
+        const uint64_t nm = mz_vcmp_ne((uint32_t)Cch, 0u) & am;   // groups still walking after this level
+        e = mz_vsel(nm, Cch - 1, e);
+        npc = (uint32_t)mz_vsel(nm, (int)ncc, (int)npc);
+        am = nm;
+        if (am == 0) break;
     }
-    depth = leaf_d;
-    if (a >= 1 && a <= depth) { path[2 * a] = pe; path[2 * a + 1] = pc; }
-    const int vtp = players == 2 ? ((root_tp - 1 + depth) & 1) + 1 : (root_tp - 1 + depth) % players + 1;
-    return SelectOut{leaf_e, leaf_a, vtp, depth};
+    if (a >= 1 && a <= dg) { path[2 * a] = pe; path[2 * a + 1] = pc - 1; }
+    const int vtp = players == 2 ? ((root_tp - 1 + dg) & 1) + 1 : (root_tp - 1 + dg) % players + 1;
+    return SelectOut{e, lach, vtp, dg};
 }
 
 // backpropagate! (SelfPlay.jl:190-217), quirk Q7, for the GW-lane group.
