@@ -209,6 +209,8 @@ struct mz_handle {
     int* d_sm_rec[3] = {nullptr, nullptr, nullptr};   // per T in {1,2,4}
     int sm_lay[3][8];                       // per T: act_total, x_rep, x_pred, x_dyn, h_out, v_out, p_out, r_out
     size_t sm_lds[3] = {0, 0, 0};
+    std::vector<uint32_t> sm_nzm;           // nonzero-chunk masks of the register images (SM_NZM_N)
+    float* d_zero16 = nullptr;              // 64 zero bytes (sm_load's skipped chunks)
     int force_kernel = 0;                   // 0 auto, 1 tile16, 2 small
     // inverse image maps, one code per flat parameter: >= 0 position in the
     // weight image, <= -2 position -code-2 in the bias image, -1 none.  ADAM
@@ -590,9 +592,22 @@ static int build_small(mz_handle* h) {
     fill(sim, st_s, sl_s, b0_s, 0);
     fill(root, st_r, sl_r, b0_r, h->sm_n_sim);
     h->sm_w_n = sw.size(); h->sm_b_n = sb.size();
+    // nonzero-chunk masks (mz_small_params.h SM_NZM_N): per stage and wave,
+    // bit q*4 + c set when any row of the wave's group gathers a weight into
+    // chunk c of DPP row q
+    h->sm_nzm.assign(SM_NZM_N, 0);
+    for (int r = 0; r < nrec; ++r)
+        for (int sl2 = 0; sl2 < SM_SLOTS; ++sl2)
+            for (int srow = 0; srow < 64; ++srow)
+                for (int q = 0; q < 4; ++q)
+                    for (int j = 0; j < 16; ++j)
+                        if (sw[sm_widx(r, sl2, q, srow, j)] >= 0)
+                            h->sm_nzm[(size_t)(sl2 * 4 + (srow >> 4)) * SM_NZM_ST + r] |= 1u << (q * 4 + j / 4);
     h->inv_small.assign(h->nflat, -1);
     for (size_t i = 0; i < sw.size(); ++i) if (sw[i] >= 0) h->inv_small[(size_t)sw[i]] = (int)i;
     for (size_t i = 0; i < sb.size(); ++i) if (sb[i] >= 0) h->inv_small[(size_t)sb[i]] = -(int)i - 2;
+    MZ_TRY(h, dalloc(h, &h->d_zero16, 16));
+    MZ_TRY(h, hipMemset(h->d_zero16, 0, 64));
     MZ_TRY(h, dalloc(h, &h->d_sm_srcw, sw.size()));
     MZ_TRY(h, dalloc(h, &h->d_sm_srcb, sb.size()));
     MZ_TRY(h, dalloc(h, &h->d_sm_w, sw.size()));
@@ -1725,6 +1740,8 @@ static int search_dev(mz_handle* h, int G, const float* obs, const uint8_t* lega
         Q.child_visits = child_visits; Q.root_value = root_value; Q.action_out = action_out;
         Q.n_sim = h->sm_n_sim; Q.n_root = h->sm_n_root;
         Q.w_sim = h->d_sm_w;
+        std::memcpy(Q.nzm, h->sm_nzm.data(), sizeof(Q.nzm));
+        Q.zero16 = reinterpret_cast<const float4*>(h->d_zero16);
         Q.w_root = h->d_sm_w + (size_t)h->sm_n_sim * SM_SLOTS * 256 * 16;
         Q.rec = h->d_sm_rec[ti]; Q.bias = h->d_sm_bias;
         const int* lay = h->sm_lay[ti];
@@ -1998,7 +2015,8 @@ static int small_unroll_ti(const mz_handle* h, int B) {
     const int ti_u = B <= 4 * h->n_cu ? 0 : 1;
     // one item per thread in the unroll's per-step loops; a/|A| staging of 64 floats
     const bool ok = h->small_ok && (ti_u + 1) * h->H <= 256 && (ti_u + 1) * h->plane <= 256 &&
-                    (ti_u + 1) * (A + 2) <= SM_THREADS && (ti_u + 1) * (K + 1) <= 64;
+                    (ti_u + 1) * (A + 2) <= SM_THREADS && (ti_u + 1) * (K + 1) <= 64 &&
+                    (ti_u + 1) * h->obs_feat <= SM_THREADS;      // one observation item per thread (setup)
     return ok ? ti_u : -1;
 }
 
@@ -2014,6 +2032,8 @@ static int small_unroll_params(mz_handle* h, const mz_batch* b, int ti, const Rp
         U.obs = b->observation; U.actions = b->actions; U.pv = h->d_pv; U.pp = h->d_pp; U.pr = h->d_pr;
         U.n_sim = h->sm_n_sim; U.n_root = h->sm_n_root; U.w_sim = h->d_sm_w;
         U.w_root = h->d_sm_w + (size_t)h->sm_n_sim * SM_SLOTS * 256 * 16;
+        std::memcpy(U.nzm, h->sm_nzm.data(), sizeof(U.nzm));
+        U.zero16 = reinterpret_cast<const float4*>(h->d_zero16);
         U.bias = h->d_sm_bias; U.rec = h->d_sm_rec[ti]; U.act_total = lay[0];
         U.x_rep = lay[1]; U.x_pred = lay[2]; U.x_dyn = lay[3]; U.h_out = lay[4]; U.v_out = lay[5];
         U.p_out = lay[6]; U.r_out = lay[7]; U.v_act = h->lay.v_act; U.r_act = h->lay.r_act;

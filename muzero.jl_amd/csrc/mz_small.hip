@@ -84,6 +84,10 @@ __device__ __forceinline__ void sm_chain(const float (&w)[16], const float (&x)[
 // store (no gather copy, no barrier): prediction's input x_pred = the parent's
 // h, dynamics' x_dyn = 2h ⊕ a/|A| (make_state_action, SelfPlay.jl:7-14; Q1's
 // in-place doubling of the parent is written back after the networks).
+// The learner's steps use the same fusion (FI = 2): x_pred = h_{i-1} read
+// from the activation buffer (h_out, [k][T]) and x_dyn = 2h ⊕ a_{i-1}/|A|
+// (make_dynamics_input, Learning.jl:293-304): `hid` = act + h_out, `aval` =
+// the step's a/|A| of game 0 (game g's at aval[g * NN]).
 struct SmFusedIn {
     const float* hid; const int* leaf_e; const int* leaf_a; const float* aval;
     int NN, H, plane, x_pred, x_dyn;
@@ -91,7 +95,7 @@ struct SmFusedIn {
 
 // One stage.  R = this thread's record of stage K; the record of stage K+1
 // (constant for the whole kernel) is fetched while stage K computes.
-template <int T, bool FI = false>
+template <int T, int FI = 0>
 __device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int4* rec_next, float* lds,
                                          const SmFusedIn* fi = nullptr) {
     const int q = (threadIdx.x >> 4) & 3, i = threadIdx.x & 15;
@@ -99,16 +103,21 @@ __device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int
     // input buffers are zero beyond K, so every step is exact)
     const float* xp = lds + R.x + (q * R.y + i) * T;
     float x[T];
-    if constexpr (FI) {
+    if constexpr (FI != 0) {
         const int k = q * R.y + i;
         const bool pred = R.x == fi->x_pred, dyn = R.x == fi->x_dyn;
 #pragma unroll
         for (int g = 0; g < T; ++g) {
-            const float* hp = fi->hid + ((size_t)g * fi->NN + fi->leaf_e[g]) * fi->H;
-            const float hv = k < fi->H ? hp[k] : 0.0f;
-            x[g] = pred ? hv
-                 : dyn ? (k < fi->H ? hv * 2.0f : k < fi->H + fi->plane ? fi->aval[fi->leaf_a[g]] : 0.0f)
-                 : xp[g];
+            float hv, av;
+            if constexpr (FI == 1) {
+                const float* hp = fi->hid + ((size_t)g * fi->NN + fi->leaf_e[g]) * fi->H;
+                hv = k < fi->H ? hp[k] : 0.0f;
+                av = fi->aval[fi->leaf_a[g]];
+            } else {
+                hv = k < fi->H ? fi->hid[k * T + g] : 0.0f;
+                av = fi->aval[g * fi->NN];
+            }
+            x[g] = pred ? hv : dyn ? (k < fi->H ? hv * 2.0f : k < fi->H + fi->plane ? av : 0.0f) : xp[g];
         }
     } else if constexpr (T == 1) {
         x[0] = xp[0];
@@ -151,22 +160,25 @@ __device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int
 }
 
 // rec: this thread's record of stage 0 ([stage][slot][row] int4, stride 128)
-template <int T, int NMAX, int K = 0>
+template <int T, int NMAX, int FI, int OFF, int K = 0>
 __device__ __forceinline__ void sm_run_k(int n, const float (&wr)[NMAX][16], int4 R, const int4* rec, float* lds,
                                          const SmFusedIn* fi) {
-    if constexpr (K < NMAX) {
+    if constexpr (K + OFF < NMAX) {
         if (K < n) {
-            const int4 Rn = K == 0 && fi ? sm_stage<T, true>(wr[K], R, rec + (K + 1) * (SM_SLOTS * 64), lds, fi)
-                                         : sm_stage<T>(wr[K], R, rec + (K + 1) * (SM_SLOTS * 64), lds);
-            sm_run_k<T, NMAX, K + 1>(n, wr, Rn, rec, lds, fi);
+            const int4 Rn = K == 0 && FI != 0
+                ? sm_stage<T, FI>(wr[K + OFF], R, rec + (K + 1) * (SM_SLOTS * 64), lds, fi)
+                : sm_stage<T>(wr[K + OFF], R, rec + (K + 1) * (SM_SLOTS * 64), lds);
+            sm_run_k<T, NMAX, FI, OFF, K + 1>(n, wr, Rn, rec, lds, fi);
         }
     }
 }
 
-template <int T, int NMAX>
+// FI: 0 = inputs from the activation buffer, 1 = the search's fused first
+// stage, 2 = the learner's (SmFusedIn).  Stage K runs on register set K + OFF.
+template <int T, int NMAX, int FI = 0, int OFF = 0>
 __device__ __forceinline__ void sm_run(int n, const float (&wr)[NMAX][16], const int4* rec, float* lds,
                                        const SmFusedIn* fi = nullptr) {
-    sm_run_k<T, NMAX>(n, wr, rec[0], rec, lds, fi);
+    sm_run_k<T, NMAX, FI, OFF>(n, wr, rec[0], rec, lds, fi);
 }
 
 // Weights of this thread's (slot, row, quarter) for stages 0..n-1 from the
@@ -174,22 +186,34 @@ __device__ __forceinline__ void sm_run(int n, const float (&wr)[NMAX][16], const
 // Stages [k0, k1) only (others untouched: sm_run never reads stages >= n,
 // so the representation's free registers can be filled with sim stages
 // while it runs).
-template <int NMAX>
-__device__ __forceinline__ void sm_load(int k0, int k1, const float* W, float (&wr)[NMAX][16]) {
-    const int tid = threadIdx.x, sl = tid >> 8, t = tid & 255;
+template <int NMAX, int DST = 0>   // image stage k -> register set k + DST
+__device__ __forceinline__ void sm_load(int k0, int k1, const float* W, float (&wr)[NMAX][16], const uint32_t* nzm,
+                                        const float4* zero16) {
+    const int tid = threadIdx.x, sl = tid >> 8, t = tid & 255, q = (tid >> 4) & 3;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint32_t mk[NMAX - DST];                           // the wave's masks: one batch of scalar loads
 #pragma unroll
-    for (int k = 0; k < NMAX; ++k) {
+    for (int k = 0; k < NMAX - DST; ++k) mk[k] = nzm[w * SM_NZM_ST + k];
+#pragma unroll
+    for (int k = 0; k < NMAX - DST; ++k) {
         if (k >= k0 && k < k1) {
             const float4* src = reinterpret_cast<const float4*>(W + (((size_t)k * SM_SLOTS + sl) * 4) * 1024) + t;
+            const uint32_t m = mk[k] >> (4 * q);       // this DPP row's chunks
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float4 v = src[i * 256];
-                wr[k][4 * i] = v.x; wr[k][4 * i + 1] = v.y; wr[k][4 * i + 2] = v.z; wr[k][4 * i + 3] = v.w;
+                // a skipped chunk reads the shared zero line (branch-free; one
+                // cache line for every skipping lane)
+#ifdef MZ_NO_WLOAD   // diagnostic only (wrong results): the setup without the weight stream
+                const float4 v = make_float4((float)(m >> i & 1u), 0.0f, 0.0f, 0.0f);
+#else
+                const float4 v = *((m >> i) & 1u ? src + i * 256 : zero16);
+#endif
+                wr[k + DST][4 * i] = v.x; wr[k + DST][4 * i + 1] = v.y; wr[k + DST][4 * i + 2] = v.z;
+                wr[k + DST][4 * i + 3] = v.w;
             }
         }
     }
 }
-
 
 template <int T>
 __device__ __forceinline__ void small_body(const SmallParams& P) {
@@ -255,8 +279,8 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     // representation (SelfPlay.jl:234) runs on its own schedule; the sim
     // stages it leaves free are preloaded, the rest reloaded after it.
     float wr[SM_MAX_SIM][16];
-    sm_load<SM_MAX_SIM>(0, P.n_root, P.w_root, wr);
-    sm_load<SM_MAX_SIM>(P.n_root, P.n_sim, P.w_sim, wr);
+    sm_load<SM_MAX_SIM>(0, P.n_root, P.w_root, wr, P.nzm + P.n_sim, P.zero16);
+    sm_load<SM_MAX_SIM>(P.n_root, P.n_sim, P.w_sim, wr, P.nzm, P.zero16);
     for (int i = tid; i < P.act_total; i += SM_THREADS) act[i] = 0.0f;
     for (int i = tid; i < S + 2; i += SM_THREADS) { l_pbc[i] = P.pbc_tab[i]; l_sqrt[i] = P.sqrt_tab[i]; }
     if (tid < A) l_aval[tid] = P.aval_tab[tid];
@@ -299,7 +323,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         act[P.x_pred + k * T + gl] = h;
     }
     // prediction ‖ dynamics weights: resident for the whole search
-    sm_load<SM_MAX_SIM>(0, P.n_root < P.n_sim ? P.n_root : P.n_sim, P.w_sim, wr);
+    sm_load<SM_MAX_SIM>(0, P.n_root < P.n_sim ? P.n_root : P.n_sim, P.w_sim, wr, P.nzm, P.zero16);
     __syncthreads();
     // prediction(h) for the root (:239); the dynamics half runs on zeros, unused
     sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act);
@@ -346,7 +370,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         SM_STAMP(2);
         // ---- prediction(parent.h) ‖ dynamics(2h ⊕ a/|A|): the first stage
         // reads the parent's h from the hidden-state store (gather fused)
-        sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act, &fin);
+        sm_run<T, SM_MAX_SIM, 1>(P.n_sim, wr, rec_sim, act, &fin);
         SM_STAMP(3);
         const int e_new = s + 1;
         // expand (wave 2) runs beside the read-outs + backup (wave 0): they
@@ -496,59 +520,80 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
     const int tid = threadIdx.x;
     const int tile0 = blockIdx.x * T;
     // per-thread item of the per-step loops (each has < SM_THREADS items)
-    const int h_gl = tid / H, h_k = tid - h_gl * H;                   // h copy: tid < T*H
-    const int pl_t = tid - 256;                                       // a/|A| plane: threads 256..
-    const int pl_gl = pl_t >= 0 ? pl_t / P.plane : 0, pl_k = pl_t - pl_gl * P.plane;
     const int o_gl = tid / (A + 2), o_c = tid - o_gl * (A + 2);      // raw outputs: tid < T*(A+2)
-    // get_batch of this tile's samples on waves 0..T-1, BEFORE their weight
-    // loads: a wave's loads complete in order (vmcnt), so behind 56 image
-    // loads the sampler's dependent chain would start only once they land
-    bool have = false;                            // prefetched by the previous launch (same shard state)
-    if (P.pf_hdr)
-        have = P.pf_hdr[0] == P.pf_epoch && P.pf_hdr[1] == P.rp.counters[0] && P.pf_hdr[2] == (long long)P.rp.step &&
-               P.pf_hdr[3] == (long long)P.B;
+    // Every global load of the setup is issued before the weight image (a
+    // wave's loads complete in order, vmcnt): the prefetch header, the stage
+    // records with their biases merged, the batch's observation and actions.
+    // Without a prefetch the sampler (waves 0..T-1) runs first and the batch is
+    // read after it.  The chain is then one global round trip, not three.
+    const int nri = nrec * SM_SLOTS * 64;                             // int4 records (one per slot row)
+    constexpr int RPT = ((SM_MAX_SIM + SM_MAX_ROOT) * SM_SLOTS * 64 + SM_THREADS - 1) / SM_THREADS;
+    const bool sample_first = !P.pf_hdr && P.sample;
+    if (sample_first && (tid >> 6) < T && tile0 + (tid >> 6) < P.B) rp_sample_one(P.rp, tile0 + (tid >> 6), tid & 63);
+    if (sample_first) { __threadfence_block(); __syncthreads(); }
+    long long hd[4] = {0, 0, 0, 0}, cnt0 = 0;
+    if (P.pf_hdr) { hd[0] = P.pf_hdr[0]; hd[1] = P.pf_hdr[1]; hd[2] = P.pf_hdr[2]; hd[3] = P.pf_hdr[3]; cnt0 = P.rp.counters[0]; }
+    int rx[RPT], ry[RPT], rz[RPT];                                    // (plain ints: the HIP vector type
+    float bv[RPT];                                                    //  kept the array in scratch)
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int i = tid + u * SM_THREADS;
+        const int ic = i < nri ? i : 0;
+        const int4 r = reinterpret_cast<const int4*>(P.rec)[ic];
+        rx[u] = r.x; ry[u] = r.y; rz[u] = r.z;
+        bv[u] = P.bias[ic];
+    }
+    const int o_i = tid / P.obs_feat, o_k = tid - o_i * P.obs_feat;   // observation item: tid < T*obs_feat
+    const int a_i = tid / (K + 1), a_k = tid - a_i * (K + 1);        // action item: tid < T*(K+1)
+    const bool o_in = tid < T * P.obs_feat && tile0 + o_i < P.B, a_in = tid < T * (K + 1) && tile0 + a_i < P.B;
+    float ov = o_in ? P.obs[(size_t)(tile0 + o_i) * P.obs_feat + o_k] : 0.0f;
+    float av = a_in ? P.actions[(size_t)(tile0 + a_i) * (K + 1) + a_k] : 0.0f;
     float wr[SM_MAX_SIM][16];
-    if (!P.pf_hdr && P.sample && (tid >> 6) < T && tile0 + (tid >> 6) < P.B)
-        rp_sample_one(P.rp, tile0 + (tid >> 6), tid & 63);
-    sm_load<SM_MAX_SIM>(0, P.n_root, P.w_root, wr);
-    sm_load<SM_MAX_SIM>(P.n_root, P.n_sim, P.w_sim, wr);   // sim stages the representation leaves free
-    // with a prefetch the header's answer is waited for only here, under the
-    // weight loads; the in-place sampling it may call for (the first step
-    // after the shard changed) then queues behind them
-    if (P.pf_hdr && P.sample && !have && (tid >> 6) < T && tile0 + (tid >> 6) < P.B)
-        rp_sample_one(P.rp, tile0 + (tid >> 6), tid & 63);
+    // the representation runs on register sets RO.. (RO + n_root), so the first
+    // RO sim stages are loaded now and step 1 starts on them while the sets
+    // the representation used are reloaded (no exposed reload)
+    constexpr int RO = SM_MAX_SIM - SM_MAX_ROOT;
+    sm_load<SM_MAX_SIM, RO>(0, P.n_root, P.w_root, wr, P.nzm + P.n_sim, P.zero16);
+    sm_load<SM_MAX_SIM>(0, RO < P.n_sim ? RO : P.n_sim, P.w_sim, wr, P.nzm, P.zero16);
+    sm_load<SM_MAX_SIM>(RO + P.n_root, P.n_sim, P.w_sim, wr, P.nzm, P.zero16);
+    // a prefetched batch (the previous launch sampled this step's) is used
+    // while its header still matches the shard; otherwise (the first step after
+    // the shard changed) waves 0..T-1 sample in place and the batch is re-read
+    const bool have = P.pf_hdr && hd[0] == P.pf_epoch && hd[1] == cnt0 && hd[2] == (long long)P.rp.step &&
+                      hd[3] == (long long)P.B;
+    if (P.pf_hdr && P.sample && !have) {
+        if ((tid >> 6) < T && tile0 + (tid >> 6) < P.B) rp_sample_one(P.rp, tile0 + (tid >> 6), tid & 63);
+        __threadfence_block();
+        __syncthreads();
+        ov = o_in ? P.obs[(size_t)(tile0 + o_i) * P.obs_feat + o_k] : 0.0f;
+        av = a_in ? P.actions[(size_t)(tile0 + a_i) * (K + 1) + a_k] : 0.0f;
+    }
     for (int i = tid; i < P.act_total; i += SM_THREADS) act[i] = 0.0f;
-    for (int i = tid; i < nrec * SM_REC_INTS; i += SM_THREADS) rec[i] = P.rec[i];
-    __syncthreads();
-    for (int i = tid; i < nrec * SM_SLOTS * 64; i += SM_THREADS) rec[4 * i + 3] = __float_as_int(P.bias[i]);
-    for (int i = tid; i < T * P.obs_feat; i += SM_THREADS) {
-        const int gl = i / P.obs_feat, k = i - gl * P.obs_feat;
-        act[P.x_rep + k * T + gl] = tile0 + gl < P.B ? P.obs[(size_t)(tile0 + gl) * P.obs_feat + k] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int i = tid + u * SM_THREADS;
+        if (i < nri) reinterpret_cast<int4*>(rec)[i] = make_int4(rx[u], ry[u], rz[u], __float_as_int(bv[u]));
     }
-    for (int i = tid; i < T * (K + 1); i += SM_THREADS) {          // make_dynamics_input's a/|A| (:294)
-        const int gl = i / (K + 1), k = i - gl * (K + 1);
-        aval[i] = tile0 + gl < P.B ? P.actions[(size_t)(tile0 + gl) * (K + 1) + k] / (float)A : 0.0f;
-    }
+    if (tid < SM_REC_INTS / 4) reinterpret_cast<int4*>(rec)[nri + tid] = make_int4(0, 0, -1, 0);   // slack stage
+    __syncthreads();                               // act zeroed before the inputs land in it
+    if (o_in) act[P.x_rep + o_k * T + o_i] = ov;
+    if (a_in) aval[a_i * (K + 1) + a_k] = av / (float)A;           // make_dynamics_input's a/|A| (:294)
     __syncthreads();
     SM_STAMP(0);                                   // setup: records, bias gather, inputs
     const int4* rec_sim = reinterpret_cast<const int4*>(rec) + sm_slot_row(tid);
     const int4* rec_root = rec_sim + P.n_sim * (SM_SLOTS * 64);
-    sm_run<T, SM_MAX_SIM>(P.n_root, wr, rec_root, act);
+    sm_run<T, SM_MAX_SIM, 0, RO>(P.n_root, wr, rec_root, act);
     SM_STAMP(1);                                   // repr stages
-    sm_load<SM_MAX_SIM>(0, P.n_root < P.n_sim ? P.n_root : P.n_sim, P.w_sim, wr);
-    __syncthreads();
-    SM_STAMP(2);                                   // sim gather
+    // reload the representation's sets; in flight under step 1's first RO stages
+    sm_load<SM_MAX_SIM>(RO, RO + P.n_root < P.n_sim ? RO + P.n_root : P.n_sim, P.w_sim, wr, P.nzm, P.zero16);
+    SM_STAMP(2);                                   // sim reload (issue only)
     for (int i = 1; i <= K; ++i) {
-        if (tid < T * H) {                                         // make_dynamics_input (:293-304)
-            const float h = act[P.h_out + h_k * T + h_gl];
-            act[P.x_pred + h_k * T + h_gl] = h;
-            act[P.x_dyn + h_k * T + h_gl] = h * 2.0f;
-        } else if (pl_t >= 0 && pl_t < T * P.plane) {
-            act[P.x_dyn + (H + pl_k) * T + pl_gl] = aval[pl_gl * (K + 1) + (i - 1)];
-        }
-        __syncthreads();
-        SM_STAMP(3);                               // step inputs
-        sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act);
+        // make_dynamics_input (:293-304) fused into the first stage: it reads
+        // h_{i-1} (h_out, written by the previous step's last stage, a barrier
+        // ago) and the step's a/|A|
+        const SmFusedIn fin{act + P.h_out, nullptr, nullptr, aval + (i - 1), K + 1, H, P.plane, P.x_pred, P.x_dyn};
+        SM_STAMP(3);                               // step inputs (none left: fused)
+        sm_run<T, SM_MAX_SIM, 2>(P.n_sim, wr, rec_sim, act, &fin);
         SM_STAMP(4);                               // the 8 stages
         // raw outputs (logits, value, reward before their read-out
         // activations); mz_learner_grad_kernel applies softmax / tanh for all

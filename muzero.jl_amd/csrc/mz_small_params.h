@@ -27,6 +27,15 @@ __host__ __device__ __forceinline__ size_t sm_widx(int stage, int slot, int q, i
     return ((((size_t)stage * SM_SLOTS + slot) * 4 + (j >> 2)) * 256 + t) * 4 + (j & 3);
 }
 
+// Per wave of the workgroup (slot * 4 + 16-row group) and image stage (sim
+// stages, then root stages), bit q*4 + c: chunk c (weights 4c..4c+3) of DPP
+// row q holds a nonzero gather for some row of the group.  Chunks whose bit
+// is clear are all zero in the image (an empty slot, a quarter past K, steps
+// past kq): sm_load skips them.  [wave][stage], so a wave's masks are one
+// scalar load.
+#define SM_NZM_ST (SM_MAX_SIM + SM_MAX_ROOT)
+#define SM_NZM_N (SM_NZM_ST * SM_SLOTS * 4)
+
 // Per stage, the host-built record: one int4 per [slot][row] (copied to LDS)
 //   .x  input base of the row's layer in the activation buffer (0 if unused:
 //       the row's weights are zero and its output is dropped)
@@ -55,6 +64,8 @@ struct SmallParams {
     const double* pbterm;  // pb_term triangle (mz_tree_device.h), copied to LDS
     char* tree; size_t tree_game_bytes; int dump_tree;
     unsigned long long* stamps;
+    const float4* zero16;    // 16 zero bytes: the address of a skipped chunk's load
+    uint32_t nzm[SM_NZM_N];  // nonzero-chunk masks [wave][stage]: sim stages, then root stages
 };
 
 // Learner unroll on the small-kernel schedule (mz_unroll_small*): T samples
@@ -84,6 +95,8 @@ struct SmallUnrollParams {
     // batch and the sampling above is skipped.  nullptr: no prefetch.
     const long long* pf_hdr;
     long long pf_epoch;
+    const float4* zero16;    // as SmallParams
+    uint32_t nzm[SM_NZM_N];  // nonzero-chunk masks (as SmallParams)
 };
 
 // One-launch learner step (mz_learn_small*, mz_learner_train_dev on one GPU,

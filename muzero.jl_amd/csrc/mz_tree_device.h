@@ -421,20 +421,92 @@ __device__ __forceinline__ float pucb_score(const float4& ed, const double* prow
     return lg ? us : -INFINITY;
 }
 
-// One 16-lane row (a DPP row, row-uniform call) recomputes node `slot`'s entry.
+// The same score without the pb_term table (select_path<false>: the pbc and
+// sqrt entries of the parent and one f64 division; S too large for the triangle).
+__device__ __forceinline__ float pucb_score_nt(const float4& ed, double pbn, double sqn, bool lg, bool norm,
+                                               float mmin, float den) {
+    const uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
+    const int Nc = (int)(nc & 0xffffu);
+    const double pb_c = pbn * (sqn / (double)(Nc + 1));
+    const float vn = (ed.w - mmin) / den;
+    const float vs = Nc > 0 ? (norm ? vn : ed.w) : 0.0f;
+    const double prior_score = pb_c * (double)ed.z;
+    const float us = (float)(prior_score + (double)vs);
+    return lg ? us : -INFINITY;
+}
+
+// the score of this lane's child of node e (parent visits Np): with the
+// pb_term triangle (TAB) or the pbc / sqrt tables
+template <bool TAB>
+__device__ __forceinline__ float pucb_lane(const float4& ed, int Np, bool lg, bool norm, float mmin, float den,
+                                           const double* pbterm, const double* pbc_tab, const double* sqrt_tab) {
+    if constexpr (TAB)
+        return pucb_score(ed, pbterm + (__umul24((unsigned)Np, (unsigned)(Np + 1)) >> 1), Np, lg, norm, mmin, den);
+    else
+        return pucb_score_nt(ed, pbc_tab[Np], sqrt_tab[Np], lg, norm, mmin, den);
+}
+
+template <int GW> __device__ __forceinline__ float gmax_sel(float u) {
+    if constexpr (GW == 16) return g16_vmax_to(u);
+    else return gmax<GW>(u);
+}
+template <int GW> __device__ __forceinline__ uint32_t grp_mask(uint64_t m, int lane) {
+    return (uint32_t)(m >> (lane & (64 - GW))) & (GW == 32 ? 0xffffffffu : 0xffffu);
+}
+
+// One GW-lane group (row-uniform call) recomputes node `slot`'s entry; with
+// `cache_g` the entry is also stored there (the tree's HBM home).
+template <int GW = 16, bool TAB = true>
 __device__ __forceinline__ void cache_row(const TreeView& t, uint2* cache, uint32_t tag, int slot, int Np, bool lg,
-                                          int a, int A, float mmin, float mmax, const double* pbterm, int lane) {
+                                          int a, int A, float mmin, float mmax, const double* pbterm, int lane,
+                                          const double* pbc_tab = nullptr, const double* sqrt_tab = nullptr,
+                                          uint2* cache_g = nullptr) {
     const int ac = a < A ? a : A - 1;
-    const double* prow = pbterm + (__umul24((unsigned)Np, (unsigned)(Np + 1)) >> 1);
     const float4 ed = t.e[(int)__umul24((unsigned)slot, (unsigned)A) + ac];
-    const float u = pucb_score(ed, prow, Np, lg, mmax > mmin, mmin, mmax - mmin);
-    const float m = g16_vmax_to(u);
-    const uint64_t eq = __builtin_amdgcn_ballot_w64(lg && u == m);
-    const uint32_t msk = (uint32_t)(eq >> (lane & 48)) & 0xffffu;
-    const int ach = __builtin_ctz(msk | 0x10000u);
+    const float u = pucb_lane<TAB>(ed, Np, lg, mmax > mmin, mmin, mmax - mmin, pbterm, pbc_tab, sqrt_tab);
+    const float m = gmax_sel<GW>(u);
+    const uint32_t msk = grp_mask<GW>(__builtin_amdgcn_ballot_w64(lg && u == m), lane);
+    const int ach = (int)__builtin_ctzll((uint64_t)msk | (1ull << GW));
     if (a == ach) {
         const bool tie = (msk & (msk - 1)) != 0;
-        cache[slot] = tie ? make_uint2(0u, 0u) : make_uint2((tag << 5) | (uint32_t)ach, __builtin_bit_cast(uint32_t, ed.x));
+        const uint2 v = tie ? make_uint2(0u, 0u) : make_uint2((tag << 5) | (uint32_t)ach, __builtin_bit_cast(uint32_t, ed.x));
+        cache[slot] = v;
+        if (cache_g) cache_g[slot] = v;
+    }
+}
+
+// U nodes at once (independent rows, one GW-lane group per game): every load
+// of the U nodes is issued before any score is formed, so one pass costs about
+// one node's latency.  Inactive entries (act = false, group-uniform) compute on
+// slot 0 and store nothing.
+template <int GW, bool TAB, int U>
+__device__ __forceinline__ void cache_rows(const TreeView& t, uint2* cache, uint32_t tag, const int (&slot)[U],
+                                           const int (&Np)[U], const bool (&act)[U], bool lg, int a, int A,
+                                           float mmin, float mmax, const double* pbterm, int lane,
+                                           const double* pbc_tab, const double* sqrt_tab, uint2* cache_g) {
+    const int ac = a < A ? a : A - 1;
+    float4 ed[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ed[u] = t.e[(int)__umul24((unsigned)(act[u] ? slot[u] : 0), (unsigned)A) + ac];
+    float sc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        sc[u] = pucb_lane<TAB>(ed[u], act[u] ? Np[u] : 0, lg, mmax > mmin, mmin, mmax - mmin, pbterm, pbc_tab,
+                               sqrt_tab);
+    float m[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) m[u] = gmax_sel<GW>(sc[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t msk = grp_mask<GW>(__builtin_amdgcn_ballot_w64(lg && sc[u] == m[u]), lane);
+        const int ach = (int)__builtin_ctzll((uint64_t)msk | (1ull << GW));
+        if (act[u] && a == ach) {
+            const bool tie = (msk & (msk - 1)) != 0;
+            const uint2 v = tie ? make_uint2(0u, 0u)
+                                : make_uint2((tag << 5) | (uint32_t)ach, __builtin_bit_cast(uint32_t, ed[u].x));
+            cache[slot[u]] = v;
+            if (cache_g) cache_g[slot[u]] = v;
+        }
     }
 }
 
@@ -444,12 +516,13 @@ __device__ __forceinline__ void cache_row(const TreeView& t, uint2* cache, uint3
 // level is evaluated in full, behind one wave-uniform test.  The games of the
 // wave walk in lockstep, so `depth` is wave-uniform; to_play at the leaf is
 // mod1(root_tp + depth, |players|) (SelfPlay.jl:267), formed once.
+template <int GW = 16, bool TAB = true>
 __device__ __forceinline__ SelectOut select_path_cached(const TreeView& t, const uint2* cache, uint32_t ver,
                                                         int* path, int root_N, int root_tp, uint32_t legal,
                                                         float mmin, float mmax, int a, int lane, int A, int players,
                                                         const double* pbterm, uint64_t seed, uint32_t gid,
-                                                        uint32_t step, int sim) {
-    constexpr int GW = 16;
+                                                        uint32_t step, int sim, const double* pbc_tab = nullptr,
+                                                        const double* sqrt_tab = nullptr) {
     const bool lg = a < A && ((legal >> a) & 1u);
     const bool norm = mmax > mmin;
     const float den = mmax - mmin;
@@ -472,21 +545,20 @@ __device__ __forceinline__ SelectOut select_path_cached(const TreeView& t, const
         if (stm != 0) {                                   // rare: the level in full, for every group
             const bool stale = (stm >> lane) & 1u;
             const int Np = (int)(npc & 0xffffu);
-            const double* prow = pbterm + (__umul24((unsigned)Np, (unsigned)(Np + 1)) >> 1);
             const float4 ed = t.e[(int)__umul24((unsigned)e, (unsigned)A) + ac];
             const uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
-            const float u = pucb_score(ed, prow, Np, lg, norm, mmin, den);
-            const float m = g16_vmax_to(u);
+            const float u = pucb_lane<TAB>(ed, Np, lg, norm, mmin, den, pbterm, pbc_tab, sqrt_tab);
+            const float m = gmax_sel<GW>(u);
             uint64_t eqm;
             asm volatile("v_cmp_eq_f32_e64 %0, %1, %2" : "=s"(eqm) : "v"(u), "v"(m));
-            const uint32_t mask = (uint32_t)((eqm & lgmask) >> (lane & 48)) & 0xffffu;
-            int ch = __builtin_ctz(mask | 0x10000u);
+            const uint32_t mask = grp_mask<GW>(eqm & lgmask, lane);
+            int ch = (int)__builtin_ctzll((uint64_t)mask | (1ull << GW));
             const int nt = __builtin_popcount(mask);
             if (stale && nt > 1) {                        // ties: the Philox draw (oracle select_child)
                 const uint32_t r = mz_rng_u32(seed, MZ_RNG_TIE, gid, step, ((uint32_t)sim << 12) | (uint32_t)depth);
                 ch = nth_set_bit(mask, (int)mz_rng_below(r, (uint32_t)nt));
             }
-            const uint32_t nch = g16_or(a == ch ? nc : 0u);
+            const uint32_t nch = gor<GW>(a == ch ? nc : 0u);
             ach = stale ? ch : ach;
             ncc = stale ? nch : ncc;
         }
@@ -626,7 +698,8 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
 template <int GW>
 __device__ __forceinline__ void backup_path_1p(const TreeView& t, const int* path, int depth, float value,
                                                float discount, int& root_N, float& root_W, float& mmin,
-                                               float& mmax, int a, float* rr, float* vin) {
+                                               float& mmax, int a, float* rr, float* vin, uint2* lvl = nullptr,
+                                               int* nN = nullptr) {
     for (int d = 1 + a; d <= depth; d += GW) rr[d] = t.nr[path[2 * d + 1]];
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
@@ -666,6 +739,10 @@ __device__ __forceinline__ void backup_path_1p(const TreeView& t, const int* pat
             nc = (nc & 0xffff0000u) | (uint32_t)N;
             t.nc(i) = nc; t.w(i) = W; t.ev(i) = R + discount * q;
         } else { rN = N; rW = W; }
+        if (lvl) {                                       // the cached select's (slot, N) per level
+            const int c = d0 > 0 ? path[2 * d0 + 1] : 0;
+            lvl[d0] = make_uint2((uint32_t)c, (uint32_t)N); nN[c] = N;
+        }
     }
     lmin = gmin<GW>(lmin);
     lmax = gmax<GW>(lmax);

@@ -23,11 +23,11 @@ PHASES = ["setup", "repr", "sim gather", "step inputs", "8 stages", "raw writes"
 
 def main():
     abi._lib = None
-    L = abi.load_library(os.path.join(pkg.PKG_DIR, "lib", "libmz_stamps.so"))
+    L = abi.load_library(os.path.join(pkg.PKG_DIR, "lib", os.environ.get("STAMPS_LIB", "libmz_stamps.so")))
     L.mz_debug_stamps.restype = ctypes.c_int
     L.mz_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     conf = dataclasses.replace(ttt.conf, num_iters=8)
-    B = conf.batch_size
+    B = int(os.environ.get("B", conf.batch_size))
     eng = abi.Engine(conf, ttt.hyper, device=0, max_games=512, rng_seed=1)
     for n, w in enumerate(init_nets(conf, ttt.hyper, seed=1234)):
         eng.set_weights(n, w)
