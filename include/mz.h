@@ -78,7 +78,7 @@ typedef struct mz_ffhp {
     int32_t depth_value;             /* 1 */
     int32_t depth_reward;            /* 1 */
     int32_t depth_state_head;        /* 3 */
-    int32_t use_batch_norm;          /* false (BatchNorm FC path not supported: error) */
+    int32_t use_batch_norm;          /* false; true: make_dense = Dense then BatchNorm(out, relu) in test mode (Learning.jl:70-78) */
     float batch_norm_momentum;       /* 0.6 */
     int32_t hidden_state_size;       /* 27 = prod(observation_shape) */
     int32_t reward_activation;       /* MZ_ACT_TANH */

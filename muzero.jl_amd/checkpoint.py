@@ -48,9 +48,12 @@ def param_table(conf, hyper, net):
                 add((op["cout"], op["cin"]))
                 add((op["cout"],))
     else:
-        for _, fin, fout, _ in layer_specs(conf, hyper, net):
+        for _, fin, fout, _, bn in layer_specs(conf, hyper, net, True):
             add((fout, fin))
             add((fout,))
+            if bn:                                        # make_dense's BatchNorm: β, γ
+                add((fout,))
+                add((fout,))
     assert off == param_count(conf, hyper, net)
     return out
 

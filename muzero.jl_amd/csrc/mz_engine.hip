@@ -97,6 +97,8 @@ enum { CH_TRUNK = 0, CH_HEAD1 = 1, CH_HEAD2 = 2 };
 struct LayerSpec {
     int net, chain, in, out, act;
     size_t flux_w, flux_b;     // offsets in the global flat parameter vector
+    int bn = 0;                // make_dense with use_batch_norm: BatchNorm β at flux_be, γ at flux_be + out
+    size_t flux_be = 0;
     int nq, n_ob;
     int packed_w, packed_b;    // offsets in the packed images
 };
@@ -210,6 +212,7 @@ struct mz_handle {
     int sm_lay[3][8];                       // per T: act_total, x_rep, x_pred, x_dyn, h_out, v_out, p_out, r_out
     size_t sm_lds[3] = {0, 0, 0};
     std::vector<uint32_t> sm_nzm;           // nonzero-chunk masks of the register images (SM_NZM_N)
+    bool sm_bn = false;                     // BatchNorm FC layers: the bias image carries γ, β sections
     float* d_zero16 = nullptr;              // 64 zero bytes (sm_load's skipped chunks)
     int force_kernel = 0;                   // 0 auto, 1 tile16, 2 small
     // inverse image maps, one code per flat parameter: >= 0 position in the
@@ -320,15 +323,17 @@ static hipError_t dalloc(mz_handle* h, T** p, size_t n) {
 }
 
 // ------------------------------------------------------------ specs & plans
-static void add_layer(mz_handle* h, int net, int chain, int in, int out, int act) {
+static void add_layer(mz_handle* h, int net, int chain, int in, int out, int act, bool bn = false) {
     LayerSpec L;
     L.net = net; L.chain = chain; L.in = in; L.out = out; L.act = act;
     L.flux_w = h->flat_off[net] + h->nparams[net]; h->nparams[net] += (size_t)in * out;
     L.flux_b = h->flat_off[net] + h->nparams[net]; h->nparams[net] += (size_t)out;
+    if (bn) { L.bn = 1; L.flux_be = h->flat_off[net] + h->nparams[net]; h->nparams[net] += (size_t)2 * out; }
     L.nq = (in + 15) / 16;
     L.n_ob = (out + 15) / 16;
     L.packed_w = (int)h->packed_w_n; h->packed_w_n += (size_t)L.n_ob * 4 * L.nq * 64;
-    L.packed_b = (int)h->packed_b_n; h->packed_b_n += (size_t)L.n_ob * 16;
+    // packed bias image: b, then (BatchNorm) γ and β, each n_ob*16 entries
+    L.packed_b = (int)h->packed_b_n; h->packed_b_n += (size_t)L.n_ob * 16 * (bn ? 3 : 1);
     h->chains[net][chain].push_back((int)h->layers.size());
     h->layers.push_back(L);
 }
@@ -342,26 +347,27 @@ static void build_specs(mz_handle* h) {
     h->obs_feat = W * Hh * (C * (c.stacked_observations + 1) + c.stacked_observations);   // :88
     h->plane = W * Hh;
     h->H = hid; h->A = A; h->S = c.num_iters;
+    const bool bn = p.use_batch_norm != 0;                 // make_dense (Learning.jl:70-78)
     // repr
     h->flat_off[MZ_NET_REPR] = 0;
-    add_layer(h, MZ_NET_REPR, CH_TRUNK, h->obs_feat, hs, MZ_ACT_RELU);
-    for (int i = 0; i < p.depth_representation; ++i) add_layer(h, MZ_NET_REPR, CH_TRUNK, hs, hs, MZ_ACT_RELU);
+    add_layer(h, MZ_NET_REPR, CH_TRUNK, h->obs_feat, hs, MZ_ACT_RELU, bn);
+    for (int i = 0; i < p.depth_representation; ++i) add_layer(h, MZ_NET_REPR, CH_TRUNK, hs, hs, MZ_ACT_RELU, bn);
     add_layer(h, MZ_NET_REPR, CH_TRUNK, hs, hid, MZ_ACT_IDENTITY);
     // pred
     h->flat_off[MZ_NET_PRED] = h->nparams[MZ_NET_REPR];
-    add_layer(h, MZ_NET_PRED, CH_TRUNK, hid, hs, MZ_ACT_RELU);
-    for (int i = 0; i < p.depth_prediction; ++i) add_layer(h, MZ_NET_PRED, CH_TRUNK, hs, hs, MZ_ACT_RELU);
-    for (int i = 0; i < p.depth_value; ++i) add_layer(h, MZ_NET_PRED, CH_HEAD1, hs, hs, MZ_ACT_RELU);
+    add_layer(h, MZ_NET_PRED, CH_TRUNK, hid, hs, MZ_ACT_RELU, bn);
+    for (int i = 0; i < p.depth_prediction; ++i) add_layer(h, MZ_NET_PRED, CH_TRUNK, hs, hs, MZ_ACT_RELU, bn);
+    for (int i = 0; i < p.depth_value; ++i) add_layer(h, MZ_NET_PRED, CH_HEAD1, hs, hs, MZ_ACT_RELU, bn);
     add_layer(h, MZ_NET_PRED, CH_HEAD1, hs, 1, MZ_ACT_TANH);
-    for (int i = 0; i < p.depth_policy; ++i) add_layer(h, MZ_NET_PRED, CH_HEAD2, hs, hs, MZ_ACT_RELU);
+    for (int i = 0; i < p.depth_policy; ++i) add_layer(h, MZ_NET_PRED, CH_HEAD2, hs, hs, MZ_ACT_RELU, bn);
     add_layer(h, MZ_NET_PRED, CH_HEAD2, hs, A, MZ_ACT_IDENTITY);
     // dyn
     h->flat_off[MZ_NET_DYN] = h->flat_off[MZ_NET_PRED] + h->nparams[MZ_NET_PRED];
-    add_layer(h, MZ_NET_DYN, CH_TRUNK, W * Hh * (C + 1), hs, MZ_ACT_RELU);                 // :120
-    for (int i = 0; i < p.depth_dynamics; ++i) add_layer(h, MZ_NET_DYN, CH_TRUNK, hs, hs, MZ_ACT_RELU);
-    for (int i = 0; i < p.depth_state_head; ++i) add_layer(h, MZ_NET_DYN, CH_HEAD1, hs, hs, MZ_ACT_RELU);
+    add_layer(h, MZ_NET_DYN, CH_TRUNK, W * Hh * (C + 1), hs, MZ_ACT_RELU, bn);                 // :120
+    for (int i = 0; i < p.depth_dynamics; ++i) add_layer(h, MZ_NET_DYN, CH_TRUNK, hs, hs, MZ_ACT_RELU, bn);
+    for (int i = 0; i < p.depth_state_head; ++i) add_layer(h, MZ_NET_DYN, CH_HEAD1, hs, hs, MZ_ACT_RELU, bn);
     add_layer(h, MZ_NET_DYN, CH_HEAD1, hs, hid, MZ_ACT_IDENTITY);
-    for (int i = 0; i < p.depth_reward; ++i) add_layer(h, MZ_NET_DYN, CH_HEAD2, hs, hs, MZ_ACT_RELU);
+    for (int i = 0; i < p.depth_reward; ++i) add_layer(h, MZ_NET_DYN, CH_HEAD2, hs, hs, MZ_ACT_RELU, bn);
     add_layer(h, MZ_NET_DYN, CH_HEAD2, hs, 1, p.reward_activation);
     h->nflat = h->flat_off[MZ_NET_DYN] + h->nparams[MZ_NET_DYN];
 
@@ -408,7 +414,7 @@ static int place_chain(mz_handle* h, PlanBuild& pb, int net, int ch, int st0, in
     for (int i = 0; i < n; ++i) {
         const LayerSpec& S = h->layers[ls[i]];
         LayerDesc d;
-        d.w_off = S.packed_w; d.b_off = S.packed_b; d.nq = S.nq; d.n_ob = S.n_ob; d.act = S.act;
+        d.w_off = S.packed_w; d.b_off = S.packed_b; d.nq = S.nq; d.n_ob = S.n_ob; d.act = S.act; d.bn = S.bn;
         d.in_off = i == 0 ? in_first : h->chain_buf[net][ch][(i - 1) & 1];
         d.out_off = i == n - 1 ? out_last : h->chain_buf[net][ch][i & 1];
         d.out_rows = S.out;
@@ -471,7 +477,8 @@ static int build_plans(mz_handle* h) {
             const LayerDesc& L = sim.layers[sim.stages[st][t].first];
             const int w = t % NW;
             if (L.nq > 4) ok = false;
-            const int rt[RT] = {st, L.w_off, L.b_off, L.nq, sim.stages[st][t].second, L.act, L.in_off, L.out_off, 0};
+            const int rt[RT] = {st, L.w_off, L.b_off, L.nq, sim.stages[st][t].second, L.act, L.in_off, L.out_off,
+                                L.bn ? L.n_ob : 0};
             per[w].insert(per[w].end(), rt, rt + RT);
         }
     for (auto& v : per) if ((int)v.size() / RT > NT) ok = false;
@@ -569,8 +576,13 @@ static int build_small(mz_handle* h) {
     h->sm_n_sim = (int)kq_s.size();
     h->sm_n_root = (int)kq_r.size();
     const int nrec = h->sm_n_sim + h->sm_n_root;
-    // weight / bias gather images: [rec] stage images (sm_widx) and [rec][slot][row]
-    std::vector<int> sw((size_t)nrec * SM_SLOTS * 256 * 16, -1), sb((size_t)nrec * SM_SLOTS * 64, -1);
+    // weight / bias gather images: [rec] stage images (sm_widx) and [rec][slot][row]; with
+    // BatchNorm FC layers the bias image has two more sections of the same shape: γ, β
+    bool any_bn = false;
+    for (const LayerSpec& L : h->layers) any_bn |= L.bn != 0;
+    h->sm_bn = any_bn;
+    const size_t nri = (size_t)nrec * SM_SLOTS * 64;
+    std::vector<int> sw((size_t)nrec * SM_SLOTS * 256 * 16, -1), sb(nri * (any_bn ? 3 : 1), -1);
     auto fill = [&](const std::vector<int>& set, const std::vector<int>& st, const std::vector<int>& sl,
                     const std::vector<int>& b0, int rec0) {
         for (size_t i = 0; i < set.size(); ++i) {
@@ -579,6 +591,10 @@ static int build_small(mz_handle* h) {
             for (int row = 0; row < L.out; ++row) {
                 const int srow = 4 * b0[i] + row;                       // slot row
                 sb[((size_t)r * SM_SLOTS + sl[i]) * 64 + srow] = (int)(L.flux_b + row);
+                if (L.bn) {
+                    sb[nri + ((size_t)r * SM_SLOTS + sl[i]) * 64 + srow] = (int)(L.flux_be + L.out + row);   // γ
+                    sb[2 * nri + ((size_t)r * SM_SLOTS + sl[i]) * 64 + srow] = (int)(L.flux_be + row);      // β
+                }
                 for (int q = 0; q < 4; ++q)
                     for (int j = 0; j < kq; ++j) {
                         const int k = q * kq + j;
@@ -670,7 +686,8 @@ static int build_small(mz_handle* h) {
                     int* e = R + 4 * (sl[i] * 64 + 4 * b0[i] + row);
                     e[0] = in_off;
                     e[1] = kq;
-                    e[2] = row < L.out ? (out_off + row * T) | (L.act == MZ_ACT_RELU ? 1 << 30 : 0) : -1;
+                    e[2] = row < L.out ? (out_off + row * T) | (L.act == MZ_ACT_RELU ? 1 << 30 : 0) |
+                                             (L.bn ? 1 << 29 : 0) : -1;
                 }
             }
         };
@@ -686,7 +703,8 @@ static int build_small(mz_handle* h) {
         // the total exceeds the LDS budget the tile-16 kernel is used)
         h->sm_lds[ti] = ints * 4 + (size_t)T * h->tree_game_bytes + pbterm_count(S) * 8 +
                         // the cached select: entries, path levels, N per slot, tags
-                        (size_t)T * (8 * NN + 8 * (S + 2) + 4 * NN) + 16 + 4 * 16 + 4 * 8;
+                        (size_t)T * (8 * NN + 8 * (S + 2) + 4 * NN) + 16 + 4 * 16 + 4 * 8 +
+                        (any_bn ? nri * 8 : 0);                          // BatchNorm (γ, β) per record row
     }
     return 1;
 }
@@ -705,6 +723,11 @@ static int build_pack_index(mz_handle* h) {
                     if (o < L.out && k < L.in) sw[dst] = (int)(L.flux_w + o + (size_t)L.out * k);
                 }
         for (int o = 0; o < L.out; ++o) sb[(size_t)L.packed_b + o] = (int)(L.flux_b + o);
+        if (L.bn)                                   // γ, β after the bias (LayerDesc.bn)
+            for (int o = 0; o < L.out; ++o) {
+                sb[(size_t)L.packed_b + L.n_ob * 16 + o] = (int)(L.flux_be + L.out + o);
+                sb[(size_t)L.packed_b + 2 * L.n_ob * 16 + o] = (int)(L.flux_be + o);
+            }
     }
     h->inv_tile.assign(h->nflat, -1);
     for (size_t i = 0; i < sw.size(); ++i) if (sw[i] >= 0) h->inv_tile[(size_t)sw[i]] = (int)i;
@@ -747,7 +770,9 @@ static int repack(mz_handle* h, hipStream_t st = nullptr) {
 
 // LDS of mz_unroll_small{1,2}: activations, records (+1 slack stage), staging
 static size_t unroll_small_lds(const mz_handle* h, int ti) {
-    return ((size_t)h->sm_lay[ti][0] + (size_t)(h->sm_n_sim + h->sm_n_root + 1) * SM_REC_INTS + 64) * 4;
+    const size_t nri = (size_t)(h->sm_n_sim + h->sm_n_root) * SM_SLOTS * 64;
+    return ((size_t)h->sm_lay[ti][0] + (size_t)(h->sm_n_sim + h->sm_n_root + 1) * SM_REC_INTS + 64) * 4 +
+           (h->sm_bn ? nri * 8 : 0);                                   // BatchNorm (γ, β) per record row
 }
 
 static size_t tree_game_bytes(int S, int A) {
@@ -1426,7 +1451,6 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
         return bad("action_space_size must be in 1..16 (16-lane select groups)");
     if (c.players < 1 || c.players > 2) return bad("players must be 1 or 2");
     if (c.num_iters < 1 || c.num_iters >= (1 << 20)) return bad("num_iters out of range");
-    if (hyper->use_batch_norm) return bad("FeedForwardHP.use_batch_norm is not supported");
     if (hyper->hidden_state_size != c.observation_shape[0] * c.observation_shape[1] * c.observation_shape[2])
         return bad("hidden_state_size must equal prod(observation_shape) (the FC path reshapes h to it)");
     if (max_games < 1) return bad("max_games must be >= 1");
@@ -1741,6 +1765,7 @@ static int search_dev(mz_handle* h, int G, const float* obs, const uint8_t* lega
         Q.n_sim = h->sm_n_sim; Q.n_root = h->sm_n_root;
         Q.w_sim = h->d_sm_w;
         std::memcpy(Q.nzm, h->sm_nzm.data(), sizeof(Q.nzm));
+        Q.bn = h->sm_bn;
         Q.zero16 = reinterpret_cast<const float4*>(h->d_zero16);
         Q.w_root = h->d_sm_w + (size_t)h->sm_n_sim * SM_SLOTS * 256 * 16;
         Q.rec = h->d_sm_rec[ti]; Q.bias = h->d_sm_bias;
@@ -2033,6 +2058,7 @@ static int small_unroll_params(mz_handle* h, const mz_batch* b, int ti, const Rp
         U.n_sim = h->sm_n_sim; U.n_root = h->sm_n_root; U.w_sim = h->d_sm_w;
         U.w_root = h->d_sm_w + (size_t)h->sm_n_sim * SM_SLOTS * 256 * 16;
         std::memcpy(U.nzm, h->sm_nzm.data(), sizeof(U.nzm));
+        U.bn = h->sm_bn;
         U.zero16 = reinterpret_cast<const float4*>(h->d_zero16);
         U.bias = h->d_sm_bias; U.rec = h->d_sm_rec[ti]; U.act_total = lay[0];
         U.x_rep = lay[1]; U.x_pred = lay[2]; U.x_dyn = lay[3]; U.h_out = lay[4]; U.v_out = lay[5];
@@ -2247,6 +2273,8 @@ int mz_learner_set_mode(mz_handle* h, int mode) {
     if (!h) return -2;
     if (mode != MZ_LEARN_REF_SEMANTICS && mode != MZ_LEARN_CORRECTED) return fail(h, "unknown learner mode");
     if (mode == MZ_LEARN_CORRECTED && h->kind != 0) return fail(h, "the corrected learner supports the FC nets");
+    if (mode == MZ_LEARN_CORRECTED && h->hp.use_batch_norm)
+        return fail(h, "the corrected learner does not backpropagate through BatchNorm FC layers");
     h->learn_mode = mode;
     return 0;
 }
@@ -2375,6 +2403,7 @@ std::vector<MzParamDesc> mz_param_table(const mz_handle* h) {
                 if (L.net != net) continue;
                 add({L.out, L.in}, L.flux_w);
                 add({L.out}, L.flux_b);
+                if (L.bn) { add({L.out}, L.flux_be); add({L.out}, L.flux_be + L.out); }   // BatchNorm β, γ
             }
         } else {                                              // Conv: W (kw,kh,cin,cout), b, BatchNorm β, γ
             size_t np = 0;

@@ -31,7 +31,18 @@ struct LayerDesc {
     int in_off;    // LDS activation input  [16*nq*4 rows][16]
     int out_off;   // LDS activation output [n_ob*16 rows][16]
     int out_rows;  // real outputs
+    int bn;        // make_dense with use_batch_norm: BatchNorm(out, relu) after the affine;
+                   // γ at b_off + n_ob*16, β at b_off + 2*n_ob*16 of the packed bias image
 };
+
+// Flux BatchNorm in test mode (μ = 0, σ² = 1, ϵ = 1f-5, the reference's
+// never-updated running statistics): γ·((t − 0)/√(1 + ϵ)) + β, IEEE division
+// by the f32 √(1 + 1f-5) (0x3f80002a), as the oracle's bn_apply.
+#define MZ_BN_S 0x1.000054p+0f
+__host__ __device__ __forceinline__ float mz_bn_apply(float t, float g, float b) {
+    const float xh = (t - 0.0f) / MZ_BN_S;
+    return g * xh + b;
+}
 
 // Device plan image (int array):
 //   [0] n_stages, [1] n_layers, [2] n_tasks,

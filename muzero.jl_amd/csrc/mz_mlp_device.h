@@ -55,6 +55,7 @@ __device__ __forceinline__ void mlp_block_t(const LayerDesc& L, int ob, const fl
     for (int r = 0; r < 4; ++r) {
         float d = (acc0[r] + acc1[r]) + (acc2[r] + acc3[r]);
         d = d + bb[r];
+        if (L.bn) d = mz_bn_apply(d, bb[L.n_ob * 16 + r], bb[2 * L.n_ob * 16 + r]);
         out[r * 16] = mz_act(L.act, d);
     }
 }
@@ -77,6 +78,7 @@ __device__ __forceinline__ void mlp_block_any(const LayerDesc& L, int ob, const 
     for (int r = 0; r < 4; ++r) {
         float d = (acc0[r] + acc1[r]) + (acc2[r] + acc3[r]);
         d = d + bb[r];
+        if (L.bn) d = mz_bn_apply(d, bb[L.n_ob * 16 + r], bb[2 * L.n_ob * 16 + r]);
         out[r * 16] = mz_act(L.act, d);
     }
 }
@@ -116,7 +118,7 @@ __device__ __forceinline__ void run_plan(const int* plan, const float* __restric
 //   [0] n_stages, [1] NT (task slots per wave), then per wave w:
 //   [ntasks, NT x ResTask].
 #define MZ_RES_TASKS 16
-struct ResTask { int stage, w_off, b_off, nq, ob, act, in_off, out_off, pad; };
+struct ResTask { int stage, w_off, b_off, nq, ob, act, in_off, out_off, bn_ob; };   // bn_ob: n_ob if BatchNorm, else 0
 
 __device__ __forceinline__ const ResTask* res_tasks(const int* img, int wave, int& nt) {
     const int NT = img[1];
@@ -165,11 +167,17 @@ __device__ __forceinline__ void res_block(const ResTask& t, const float (&wr)[16
         acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[OFF + 3 * NQ + j], x[3 * NQ + j], acc3, 0, 0, 0);
     }
     float* out = lds + t.out_off + (t.ob * 16 + (lane >> 4) * 4) * 16 + (lane & 15);
-    float d;
-    d = (acc0[0] + acc1[0]) + (acc2[0] + acc3[0]); d = d + b0; out[0] = mz_act(t.act, d);
-    d = (acc0[1] + acc1[1]) + (acc2[1] + acc3[1]); d = d + b1; out[16] = mz_act(t.act, d);
-    d = (acc0[2] + acc1[2]) + (acc2[2] + acc3[2]); d = d + b2; out[32] = mz_act(t.act, d);
-    d = (acc0[3] + acc1[3]) + (acc2[3] + acc3[3]); d = d + b3; out[48] = mz_act(t.act, d);
+    float d[4];
+    d[0] = (acc0[0] + acc1[0]) + (acc2[0] + acc3[0]); d[0] = d[0] + b0;
+    d[1] = (acc0[1] + acc1[1]) + (acc2[1] + acc3[1]); d[1] = d[1] + b1;
+    d[2] = (acc0[2] + acc1[2]) + (acc2[2] + acc3[2]); d[2] = d[2] + b2;
+    d[3] = (acc0[3] + acc1[3]) + (acc2[3] + acc3[3]); d[3] = d[3] + b3;
+    if (t.bn_ob) {                                           // BatchNorm (test mode) after the affine
+#pragma unroll
+        for (int r = 0; r < 4; ++r) d[r] = mz_bn_apply(d[r], bb[t.bn_ob * 16 + r], bb[2 * t.bn_ob * 16 + r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[16 * r] = mz_act(t.act, d[r]);
 }
 
 template <int K>

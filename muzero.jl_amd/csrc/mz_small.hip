@@ -97,7 +97,7 @@ struct SmFusedIn {
 // (constant for the whole kernel) is fetched while stage K computes.
 template <int T, int FI = 0>
 __device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int4* rec_next, float* lds,
-                                         const SmFusedIn* fi = nullptr) {
+                                         const SmFusedIn* fi = nullptr, const float2* bnp = nullptr) {
     const int q = (threadIdx.x >> 4) & 3, i = threadIdx.x & 15;
     // x[q*kq + i] of the T games (rows beyond kq meet zero weights; the 64-row
     // input buffers are zero beyond K, so every step is exact)
@@ -146,12 +146,15 @@ __device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int
         acc[g] = __builtin_bit_cast(float, (unsigned)s2[0]) + __builtin_bit_cast(float, (unsigned)s2[1]);
     }
     if (q == 0 && R.z >= 0) {
-        const int o = R.z & 0x3fffffff;
+        const int o = R.z & 0x1fffffff;
         const bool relu = (R.z >> 30) != 0;
         const float bias = __int_as_float(R.w);
+        const bool bn = (R.z >> 29) & 1;                  // make_dense with BatchNorm (test mode)
+        const float2 gb = bn ? *bnp : make_float2(1.0f, 0.0f);
 #pragma unroll
         for (int g = 0; g < T; ++g) {
-            const float d = acc[g] + bias;
+            float d = acc[g] + bias;
+            if (bn) d = mz_bn_apply(d, gb.x, gb.y);
             lds[o + g] = relu ? mz_relu(d) : d;
         }
     }
@@ -162,23 +165,25 @@ __device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int
 // rec: this thread's record of stage 0 ([stage][slot][row] int4, stride 128)
 template <int T, int NMAX, int FI, int OFF, int K = 0>
 __device__ __forceinline__ void sm_run_k(int n, const float (&wr)[NMAX][16], int4 R, const int4* rec, float* lds,
-                                         const SmFusedIn* fi) {
+                                         const SmFusedIn* fi, const float2* bnp) {
     if constexpr (K + OFF < NMAX) {
         if (K < n) {
+            const float2* bk = bnp + K * (SM_SLOTS * 64);
             const int4 Rn = K == 0 && FI != 0
-                ? sm_stage<T, FI>(wr[K + OFF], R, rec + (K + 1) * (SM_SLOTS * 64), lds, fi)
-                : sm_stage<T>(wr[K + OFF], R, rec + (K + 1) * (SM_SLOTS * 64), lds);
-            sm_run_k<T, NMAX, FI, OFF, K + 1>(n, wr, Rn, rec, lds, fi);
+                ? sm_stage<T, FI>(wr[K + OFF], R, rec + (K + 1) * (SM_SLOTS * 64), lds, fi, bk)
+                : sm_stage<T>(wr[K + OFF], R, rec + (K + 1) * (SM_SLOTS * 64), lds, nullptr, bk);
+            sm_run_k<T, NMAX, FI, OFF, K + 1>(n, wr, Rn, rec, lds, fi, bnp);
         }
     }
 }
 
 // FI: 0 = inputs from the activation buffer, 1 = the search's fused first
 // stage, 2 = the learner's (SmFusedIn).  Stage K runs on register set K + OFF.
+// bnp: this thread's (γ, β) column, laid out as `rec` (read only by BatchNorm rows).
 template <int T, int NMAX, int FI = 0, int OFF = 0>
 __device__ __forceinline__ void sm_run(int n, const float (&wr)[NMAX][16], const int4* rec, float* lds,
-                                       const SmFusedIn* fi = nullptr) {
-    sm_run_k<T, NMAX, FI, OFF>(n, wr, rec[0], rec, lds, fi);
+                                       const SmFusedIn* fi, const float2* bnp) {
+    sm_run_k<T, NMAX, FI, OFF>(n, wr, rec[0], rec, lds, fi, bnp);
 }
 
 // Weights of this thread's (slot, row, quarter) for stages 0..n-1 from the
@@ -260,6 +265,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     int4* c_hdr = reinterpret_cast<int4*>(reinterpret_cast<char*>(smem) +                 // [4], 16-byte aligned
                                           ((reinterpret_cast<char*>(c_nN + T * NN) - reinterpret_cast<char*>(smem) + 15) & ~15));
     float2* c_mmx = reinterpret_cast<float2*>(c_hdr + 4);         // [4]
+    float2* bnl = c_mmx + 4;                                      // [nrec][slot][64] BatchNorm (γ, β) (P.bn)
 
     const int tid = threadIdx.x;
     const int g = tid >> 4, a = tid & 15, lane = tid & 63;
@@ -274,6 +280,8 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     // read (never used) past each schedule's last stage
     const int4* rec_sim = reinterpret_cast<const int4*>(rec) + sm_slot_row(tid);
     const int4* rec_root = rec_sim + P.n_sim * (SM_SLOTS * 64);
+    const float2* bn_sim = bnl + sm_slot_row(tid);
+    const float2* bn_root = bn_sim + P.n_sim * (SM_SLOTS * 64);
 
     // ---- weight-image loads first: in flight under the setup copies.  The
     // representation (SelfPlay.jl:234) runs on its own schedule; the sim
@@ -289,6 +297,9 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     __syncthreads();
     for (int i = tid; i < nrec * SM_SLOTS * 64; i += SM_THREADS)
         rec[4 * i + 3] = __float_as_int(P.bias[i]);
+    if (P.bn)
+        for (int i = tid; i < nrec * SM_SLOTS * 64; i += SM_THREADS)
+            bnl[i] = make_float2(P.bias[nrec * SM_SLOTS * 64 + i], P.bias[2 * nrec * SM_SLOTS * 64 + i]);
     // ---- root inputs
     for (int i = tid; i < T * P.obs_feat; i += SM_THREADS) {
         const int gl = i / P.obs_feat, k = i - gl * P.obs_feat;
@@ -315,7 +326,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     if (P.exploration && active)
         sg_noise[16 * g + a] = root_noise_lane(sg_legal[g], a, A, P.seed, gid, P.rng_step, P.dirichlet_alpha,
                                                sg_stage + 16 * g);
-    sm_run<T, SM_MAX_SIM>(P.n_root, wr, rec_root, act);
+    sm_run<T, SM_MAX_SIM>(P.n_root, wr, rec_root, act, nullptr, bn_root);
     for (int i = tid; i < T * H; i += SM_THREADS) {     // h -> hidden slot 0 and the prediction input
         const int gl = i / H, k = i - gl * H;
         const float h = act[P.h_out + k * T + gl];
@@ -326,7 +337,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     sm_load<SM_MAX_SIM>(0, P.n_root < P.n_sim ? P.n_root : P.n_sim, P.w_sim, wr, P.nzm, P.zero16);
     __syncthreads();
     // prediction(h) for the root (:239); the dynamics half runs on zeros, unused
-    sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act);
+    sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act, nullptr, bn_sim);
 
     const uint32_t legal = tree_thread ? sg_legal[g] : 0u;
     if (tree_thread) {   // expand_node!(root, legal, to_play, 0, policy, h) (:245)
@@ -370,7 +381,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         SM_STAMP(2);
         // ---- prediction(parent.h) ‖ dynamics(2h ⊕ a/|A|): the first stage
         // reads the parent's h from the hidden-state store (gather fused)
-        sm_run<T, SM_MAX_SIM, 1>(P.n_sim, wr, rec_sim, act, &fin);
+        sm_run<T, SM_MAX_SIM, 1>(P.n_sim, wr, rec_sim, act, &fin, bn_sim);
         SM_STAMP(3);
         const int e_new = s + 1;
         // expand (wave 2) runs beside the read-outs + backup (wave 0): they
@@ -517,6 +528,7 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
     float* act = smem;
     int* rec = reinterpret_cast<int*>(act + P.act_total);
     float* aval = reinterpret_cast<float*>(rec + (nrec + 1) * SM_REC_INTS);    // [T][K+1] a/|A| per step
+    float2* bnl = reinterpret_cast<float2*>(aval + 64);                     // [nrec][slot][64] (γ, β) (P.bn)
     const int tid = threadIdx.x;
     const int tile0 = blockIdx.x * T;
     // per-thread item of the per-step loops (each has < SM_THREADS items)
@@ -575,6 +587,8 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
         if (i < nri) reinterpret_cast<int4*>(rec)[i] = make_int4(rx[u], ry[u], rz[u], __float_as_int(bv[u]));
     }
     if (tid < SM_REC_INTS / 4) reinterpret_cast<int4*>(rec)[nri + tid] = make_int4(0, 0, -1, 0);   // slack stage
+    if (P.bn)
+        for (int i = tid; i < nri; i += SM_THREADS) bnl[i] = make_float2(P.bias[nri + i], P.bias[2 * nri + i]);
     __syncthreads();                               // act zeroed before the inputs land in it
     if (o_in) act[P.x_rep + o_k * T + o_i] = ov;
     if (a_in) aval[a_i * (K + 1) + a_k] = av / (float)A;           // make_dynamics_input's a/|A| (:294)
@@ -582,7 +596,9 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
     SM_STAMP(0);                                   // setup: records, bias gather, inputs
     const int4* rec_sim = reinterpret_cast<const int4*>(rec) + sm_slot_row(tid);
     const int4* rec_root = rec_sim + P.n_sim * (SM_SLOTS * 64);
-    sm_run<T, SM_MAX_SIM, 0, RO>(P.n_root, wr, rec_root, act);
+    const float2* bn_sim = bnl + sm_slot_row(tid);
+    const float2* bn_root = bn_sim + P.n_sim * (SM_SLOTS * 64);
+    sm_run<T, SM_MAX_SIM, 0, RO>(P.n_root, wr, rec_root, act, nullptr, bn_root);
     SM_STAMP(1);                                   // repr stages
     // reload the representation's sets; in flight under step 1's first RO stages
     sm_load<SM_MAX_SIM>(RO, RO + P.n_root < P.n_sim ? RO + P.n_root : P.n_sim, P.w_sim, wr, P.nzm, P.zero16);
@@ -593,7 +609,7 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
         // ago) and the step's a/|A|
         const SmFusedIn fin{act + P.h_out, nullptr, nullptr, aval + (i - 1), K + 1, H, P.plane, P.x_pred, P.x_dyn};
         SM_STAMP(3);                               // step inputs (none left: fused)
-        sm_run<T, SM_MAX_SIM, 2>(P.n_sim, wr, rec_sim, act, &fin);
+        sm_run<T, SM_MAX_SIM, 2>(P.n_sim, wr, rec_sim, act, &fin, bn_sim);
         SM_STAMP(4);                               // the 8 stages
         // raw outputs (logits, value, reward before their read-out
         // activations); mz_learner_grad_kernel applies softmax / tanh for all

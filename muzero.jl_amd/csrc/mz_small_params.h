@@ -40,7 +40,7 @@ __host__ __device__ __forceinline__ size_t sm_widx(int stage, int slot, int q, i
 //   .x  input base of the row's layer in the activation buffer (0 if unused:
 //       the row's weights are zero and its output is dropped)
 //   .y  kq of the layer (k steps per quarter)
-//   .z  output offset of the row | relu << 30, or -1 = unused row
+//   .z  output offset of the row | relu << 30 | BatchNorm << 29, or -1 = unused row
 //   .w  bias bits (filled at kernel start from the re-gathered bias image)
 #define SM_REC_INTS (SM_SLOTS * 64 * 4)
 
@@ -66,6 +66,7 @@ struct SmallParams {
     unsigned long long* stamps;
     const float4* zero16;    // 16 zero bytes: the address of a skipped chunk's load
     uint32_t nzm[SM_NZM_N];  // nonzero-chunk masks [wave][stage]: sim stages, then root stages
+    int bn;                  // BatchNorm FC layers: `bias` has γ and β sections after the biases
 };
 
 // Learner unroll on the small-kernel schedule (mz_unroll_small*): T samples
@@ -97,6 +98,7 @@ struct SmallUnrollParams {
     long long pf_epoch;
     const float4* zero16;    // as SmallParams
     uint32_t nzm[SM_NZM_N];  // nonzero-chunk masks (as SmallParams)
+    int bn;                  // as SmallParams
 };
 
 // One-launch learner step (mz_learn_small*, mz_learner_train_dev on one GPU,

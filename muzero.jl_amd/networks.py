@@ -16,31 +16,37 @@ from .config import ACT_IDENTITY, ACT_RELU, ACT_TANH, ResNetHP, stacked_features
 NET_REPR, NET_PRED, NET_DYN = 0, 1, 2
 
 
-def layer_specs(conf, hyper, net):
+def layer_specs(conf, hyper, net, with_bn=False):
+    """(chain, in, out, act) per Dense; with_bn: (chain, in, out, act, bn), bn
+    set on make_dense's layers (Learning.jl:70-78) when use_batch_norm — the
+    Dense then has no activation and BatchNorm(out, relu) follows it, whose β,
+    γ come after the Dense's W, b in Flux.params."""
     w, h, c = conf.observation_shape
     hs, hid, A = hyper.width_hidden, hyper.hidden_state_size, len(conf.action_space)
     act_r = {"tanh": ACT_TANH, "relu": ACT_RELU, "identity": ACT_IDENTITY}[
         hyper.reward_activation if isinstance(hyper.reward_activation, str) else hyper.reward_activation.__name__]
+    bn = bool(getattr(hyper, "use_batch_norm", False))
+    md = lambda ch, i, o: (ch, i, o, ACT_RELU, bn)       # make_dense
     L = []
     if net == NET_REPR:                                   # init_representation (:87-98)
-        L.append((0, stacked_features(conf), hs, ACT_RELU))
-        L += [(0, hs, hs, ACT_RELU)] * hyper.depth_representation
-        L.append((0, hs, hid, ACT_IDENTITY))
+        L.append(md(0, stacked_features(conf), hs))
+        L += [md(0, hs, hs)] * hyper.depth_representation
+        L.append((0, hs, hid, ACT_IDENTITY, False))
     elif net == NET_PRED:                                 # init_prediction (:100-116)
-        L.append((0, hid, hs, ACT_RELU))
-        L += [(0, hs, hs, ACT_RELU)] * hyper.depth_prediction
-        L += [(1, hs, hs, ACT_RELU)] * hyper.depth_value
-        L.append((1, hs, 1, ACT_TANH))
-        L += [(2, hs, hs, ACT_RELU)] * hyper.depth_policy
-        L.append((2, hs, A, ACT_IDENTITY))               # then softmax
+        L.append(md(0, hid, hs))
+        L += [md(0, hs, hs)] * hyper.depth_prediction
+        L += [md(1, hs, hs)] * hyper.depth_value
+        L.append((1, hs, 1, ACT_TANH, False))
+        L += [md(2, hs, hs)] * hyper.depth_policy
+        L.append((2, hs, A, ACT_IDENTITY, False))        # then softmax
     else:                                                 # init_dynamics (:118-142)
-        L.append((0, w * h * (c + 1), hs, ACT_RELU))
-        L += [(0, hs, hs, ACT_RELU)] * hyper.depth_dynamics
-        L += [(1, hs, hs, ACT_RELU)] * hyper.depth_state_head
-        L.append((1, hs, hid, ACT_IDENTITY))
-        L += [(2, hs, hs, ACT_RELU)] * hyper.depth_reward
-        L.append((2, hs, 1, act_r))
-    return L
+        L.append(md(0, w * h * (c + 1), hs))
+        L += [md(0, hs, hs)] * hyper.depth_dynamics
+        L += [md(1, hs, hs)] * hyper.depth_state_head
+        L.append((1, hs, hid, ACT_IDENTITY, False))
+        L += [md(2, hs, hs)] * hyper.depth_reward
+        L.append((2, hs, 1, act_r, False))
+    return L if with_bn else [x[:4] for x in L]
 
 
 def _act(a):
@@ -156,7 +162,7 @@ def _op_params(op):
 def param_count(conf, hyper, net):
     if isinstance(hyper, ResNetHP):
         return sum(_op_params(op) for op in resnet_specs(conf, hyper, net))
-    return sum(i * o + o for _, i, o, _ in layer_specs(conf, hyper, net))
+    return sum(i * o + o + (2 * o if bn else 0) for _, i, o, _, bn in layer_specs(conf, hyper, net, True))
 
 
 def net_macs(conf, hyper, net):
@@ -206,9 +212,12 @@ def init_net(conf, hyper, net, seed=0):
                     parts.append(np.zeros(op["cout"], np.float32))   # β
                     parts.append(np.ones(op["cout"], np.float32))    # γ
         return np.concatenate(parts)
-    for _, i, o, _ in layer_specs(conf, hyper, net):
+    for _, i, o, _, bn in layer_specs(conf, hyper, net, True):
         parts.append(glorot_uniform(rng, o, i).reshape(-1))
         parts.append(np.zeros(o, np.float32))
+        if bn:
+            parts.append(np.zeros(o, np.float32))         # BatchNorm β
+            parts.append(np.ones(o, np.float32))          # BatchNorm γ
     return np.concatenate(parts)
 
 
@@ -244,13 +253,18 @@ def unflatten_resnet(conf, hyper, net, flat):
     return out
 
 
-def unflatten(conf, hyper, net, flat):
-    """-> list of (chain, W (out,in) as numpy, b, act)."""
+def unflatten(conf, hyper, net, flat, with_bn=False):
+    """-> list of (chain, W (out,in) as numpy, b, act); with_bn: (chain, W, b,
+    act, (β, γ) or None)."""
     out, off = [], 0
-    for ch, i, o, act in layer_specs(conf, hyper, net):
+    for ch, i, o, act, bn in layer_specs(conf, hyper, net, True):
         W = flat[off: off + i * o].reshape(i, o).T
         off += i * o
         b = flat[off: off + o]
         off += o
-        out.append((ch, W, b, act))
+        bg = None
+        if bn:
+            bg = (flat[off: off + o], flat[off + o: off + 2 * o])
+            off += 2 * o
+        out.append((ch, W, b, act, bg) if with_bn else (ch, W, b, act))
     return out

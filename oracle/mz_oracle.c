@@ -73,6 +73,15 @@ static OLayer* onet_add(ONet* net, int part, int in, int out, int act) {
     return l;
 }
 
+/* make_dense (Learning.jl:70-78): Dense(in, out, relu), or with
+ * use_batch_norm Chain(Dense(in, out), BatchNorm(out, relu)) — β, γ follow
+ * the Dense's W, b in Flux.params */
+static OLayer* onet_dense(ONet* net, int part, int in, int out, int bn) {
+    OLayer* l = onet_add(net, part, in, out, MZ_ACT_RELU);
+    if (bn) { l->bn = 1; l->bnoff = net->nparams; net->nparams += (size_t)2 * out; }
+    return l;
+}
+
 /* Conv(k, in => out, pad = k .÷ 2) [+ BatchNorm(out, act)] on a W x H board */
 static OLayer* onet_conv(ONet* net, int part, int in, int out, int kw, int kh, int W, int H, int bn, int act) {
     OLayer* l = &net->L[part][net->n[part]++];
@@ -211,26 +220,27 @@ static void onet_build(ONet* net, int which, const mz_config* c, const ora_nethp
     const mz_ffhp* hp = &nh->ff;
     int W = c->observation_shape[0], H = c->observation_shape[1], C = c->observation_shape[2];
     int hs = hp->width_hidden, hid = hp->hidden_state_size, A = c->action_space_size;
+    const int bn = hp->use_batch_norm != 0;
     if (which == MZ_NET_REPR) {
         int indim = W * H * (C * (c->stacked_observations + 1) + c->stacked_observations); /* :88 */
-        onet_add(net, 0, indim, hs, MZ_ACT_RELU);
-        for (int i = 0; i < hp->depth_representation; ++i) onet_add(net, 0, hs, hs, MZ_ACT_RELU);
+        onet_dense(net, 0, indim, hs, bn);
+        for (int i = 0; i < hp->depth_representation; ++i) onet_dense(net, 0, hs, hs, bn);
         onet_add(net, 0, hs, hid, MZ_ACT_IDENTITY);
     } else if (which == MZ_NET_PRED) {
-        onet_add(net, 0, hid, hs, MZ_ACT_RELU);
-        for (int i = 0; i < hp->depth_prediction; ++i) onet_add(net, 0, hs, hs, MZ_ACT_RELU);
-        for (int i = 0; i < hp->depth_value; ++i) onet_add(net, 1, hs, hs, MZ_ACT_RELU);
+        onet_dense(net, 0, hid, hs, bn);
+        for (int i = 0; i < hp->depth_prediction; ++i) onet_dense(net, 0, hs, hs, bn);
+        for (int i = 0; i < hp->depth_value; ++i) onet_dense(net, 1, hs, hs, bn);
         onet_add(net, 1, hs, 1, MZ_ACT_TANH);                                  /* :110 */
-        for (int i = 0; i < hp->depth_policy; ++i) onet_add(net, 2, hs, hs, MZ_ACT_RELU);
+        for (int i = 0; i < hp->depth_policy; ++i) onet_dense(net, 2, hs, hs, bn);
         onet_add(net, 2, hs, A, MZ_ACT_IDENTITY);                              /* :113 */
         net->softmax_head2 = 1;                                                 /* :114 */
     } else {
         int indim = W * H * (C + 1);                                            /* :120 */
-        onet_add(net, 0, indim, hs, MZ_ACT_RELU);
-        for (int i = 0; i < hp->depth_dynamics; ++i) onet_add(net, 0, hs, hs, MZ_ACT_RELU);
-        for (int i = 0; i < hp->depth_state_head; ++i) onet_add(net, 1, hs, hs, MZ_ACT_RELU);
+        onet_dense(net, 0, indim, hs, bn);
+        for (int i = 0; i < hp->depth_dynamics; ++i) onet_dense(net, 0, hs, hs, bn);
+        for (int i = 0; i < hp->depth_state_head; ++i) onet_dense(net, 1, hs, hs, bn);
         onet_add(net, 1, hs, hid, MZ_ACT_IDENTITY);                            /* :136 */
-        for (int i = 0; i < hp->depth_reward; ++i) onet_add(net, 2, hs, hs, MZ_ACT_RELU);
+        for (int i = 0; i < hp->depth_reward; ++i) onet_dense(net, 2, hs, hs, bn);
         onet_add(net, 2, hs, 1, hp->reward_activation);                        /* :140 */
     }
     onet_finish(net);
@@ -269,10 +279,14 @@ static float bn_apply(const OLayer* l, const float* P, int o, float t) {
     return P[l->bnoff + l->out + o] * xh + P[l->bnoff + o];
 }
 
-/* Flux Dense: σ.(W*x .+ b) */
+/* Flux Dense: σ.(W*x .+ b); make_dense with use_batch_norm (Learning.jl:70-78):
+ * Dense(in, out) then BatchNorm(out, relu) in test mode (bn_apply) */
 static void dense_fwd(const OLayer* l, const float* P, const float* x, float* y) {
-    for (int o = 0; o < l->out; ++o)
-        y[o] = act_apply(l->act, mz_dot(P + l->woff, l->out, l->in, o, x) + P[l->boff + o]);
+    for (int o = 0; o < l->out; ++o) {
+        float t = mz_dot(P + l->woff, l->out, l->in, o, x) + P[l->boff + o];
+        if (l->bn) t = bn_apply(l, P, o, t);
+        y[o] = act_apply(l->act, t);
+    }
 }
 
 /* Flux Conv (zero padding, kernel flipped) on a (Wi, Hi, cin) column-major
