@@ -79,7 +79,7 @@ import torch.distributed as dist  # noqa: E402
 import _mzpkg  # noqa: E402
 
 _mzpkg.load()
-from muzero_jl_amd.abi import ENV_CONNECT4, ENV_TICTACTOE, Engine  # noqa: E402
+from muzero_jl_amd.abi import ENV_ATARI, ENV_CONNECT4, ENV_TICTACTOE, Engine  # noqa: E402
 from muzero_jl_amd.config import cos_schedule, to_c_config, to_c_ffhp, to_c_resnet_hp  # noqa: E402
 from muzero_jl_amd.games import atari_synth as atari  # noqa: E402
 from muzero_jl_amd.games import connect4 as c4  # noqa: E402
@@ -321,11 +321,12 @@ def main():
     # device — observation/stacked planes, search, env step, GameHistory and
     # replay-shard append — G games per rank, timed like the search leg
     pipe = None
-    env_kind = ENV_CONNECT4 if game is c4 else ENV_TICTACTOE
-    if game is not atari:                                 # (no Atari env: the search leg is configs[4]'s step)
-        eng.selfplay_init(env_kind, G, max(G, conf.replay_buffer_size))
+    env_kind = ENV_ATARI if game is atari else ENV_CONNECT4 if game is c4 else ENV_TICTACTOE
+    # replay shard: the config's capacity (Atari: 2G games of <= max_moves + 1 frames, 7 KB each)
+    cap = max(G, min(conf.replay_buffer_size, 2 * G) if game is atari else conf.replay_buffer_size)
+    eng.selfplay_init(env_kind, G, cap)
     mv = 1 << 20                                          # move counter (RNG step keys)
-    if args.pipeline_moves > 0 and game is not atari and not args.search_only:
+    if args.pipeline_moves > 0 and not args.search_only:
         for _ in range(3):
             eng.selfplay_move(mv, game_offset=rank * G, stream=sp)
             mv += 1
@@ -345,7 +346,7 @@ def main():
                 "node_expansions_per_s": round(world * G * S * args.pipeline_moves / tpl, 1),
                 "ms_per_move": round(tpl / args.pipeline_moves * 1e3, 4), "moves": args.pipeline_moves}
     torch.cuda.synchronize()                              # (replay_counts syncs only libmz's own stream)
-    while game is not atari and not args.search_only and eng.replay_counts()[1] == 0:   # the learner needs finished games
+    while not args.search_only and eng.replay_counts()[1] == 0:   # the learner needs finished games
         eng.selfplay_move(mv, game_offset=rank * G, stream=sp)
         mv += 1
         torch.cuda.synchronize()
@@ -362,18 +363,8 @@ def main():
         grad = torch.empty(eng.grad_count(), dtype=torch.float32, device=dev)
         losses = torch.empty(8, dtype=torch.float32, device=dev)
 
-        if game is atari:                                     # a synthetic batch resident in HBM
-            rng = np.random.default_rng(7 + rank)
-            tpol = rng.random((B, K + 1, A)).astype(np.float32)
-            sb = [atari.observations(B, seed=1000 + rank), rng.integers(1, A + 1, (B, K + 1)).astype(np.float32),
-                  rng.uniform(-1, 1, (B, K + 1)).astype(np.float32), np.zeros((B, K + 1), np.float32),
-                  tpol / tpol.sum(-1, keepdims=True), rng.integers(1, K + 1, B).astype(np.float32)]
-            sb = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in sb]
-
         def lstep(k):
-            if game is atari:
-                eng.learner_grad_dev([x.data_ptr() for x in sb], B, grad.data_ptr(), losses.data_ptr(), stream=sp)
-            elif world == 1:                                  # get_batch + unroll, losses + ADAM: two launches
+            if world == 1:                                  # get_batch + unroll, losses + ADAM: two launches
                 eng.learner_train_dev(B, k + 1, cos_schedule(k + 1), losses.data_ptr(), stream=sp)
                 return
             else:                                             # get_batch fused into the unroll; ∇ exchanged
@@ -459,8 +450,8 @@ def main():
     # moves with the actors' nets and one learner step per finished game, the
     # actors refreshed one checkpoint behind (mz_train_run, one GPU)
     train = None
-    if args.train_moves > 0 and world == 1 and game is not atari and not args.search_only:
-        eng.selfplay_init(env_kind, G, max(G, conf.replay_buffer_size))
+    if args.train_moves > 0 and world == 1 and not args.search_only:
+        eng.selfplay_init(env_kind, G, cap)
         eng.train_init(conf.batch_size)
         eng.train_run(3, move0=mv, game_offset=rank * G, stream=sp)
         mv += 3
@@ -532,8 +523,9 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "node-expansions/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": ("synthetic: 84x84x4 U[0,1) Philox observations, random glorot weights; synthetic learner "
-                     "batch resident in HBM" if game is atari else
+            "data": ("synthetic: 84x84x4 U[0,1) Philox observations for the timed searches, random glorot weights; "
+                     "learner batches sampled on the device from the self-play shard of the synthetic Atari-like "
+                     "env (games/atari_synth.py)" if game is atari else
                      f"synthetic: random-play {game.__name__.split('.')[-1]} positions, random glorot weights; "
                      "learner batches sampled on the device from the self-play replay shard"),
             "config": {"workload": workload(game, resnet, G, S),
@@ -545,8 +537,7 @@ def main():
             "learner_corrected": corrected,
             "train_loop": train,
             "learner_config": {"batch_size": B, "num_unroll_steps": K, "mode": "ref_semantics",
-                               "batch_source": "synthetic device batch" if game is atari else
-                               (("mz_learner_train_dev: one launch — unroll + losses, ADAM into the second "
+                               "batch_source": (("mz_learner_train_dev: one launch — unroll + losses, ADAM into the second "
                                  "image set, and step t+1's device get_batch + make_target into the other batch "
                                  "set (step t's was drawn by the previous launch)" if not resnet else
                                  "mz_learner_train_dev: device get_batch + make_target, ResNet unroll chain + "

@@ -273,7 +273,7 @@ int mz_learner_train_dp(mz_handle* h, int32_t B, uint32_t step, double eta, floa
 /* ---- Device self-play and replay shard ------------
  * The loop body of play_game (SelfPlay.jl:330-382) and the replay buffer
  * (ReplayBuffer.jl) kept in HBM: no host round trip per move or per batch. */
-enum { MZ_ENV_TICTACTOE = 0, MZ_ENV_CONNECT4 = 1 };
+enum { MZ_ENV_TICTACTOE = 0, MZ_ENV_CONNECT4 = 1, MZ_ENV_ATARI = 2 };
 
 /* Device self-play state for G <= max_games game slots: env boards
  * (games/tictactoe/game.jl with quirk Q14, or the Connect4 env of BASELINE
@@ -282,7 +282,11 @@ enum { MZ_ENV_TICTACTOE = 0, MZ_ENV_CONNECT4 = 1 };
  * replay_games >= G finished games (ReplayBuffer.jl:133-161, PER = false;
  * the RemoteBufferChannel Dict keyed by game number).  Every slot starts a
  * new game.  The conf must match the env (TicTacToe (3,3,3)/9 actions,
- * Connect4 (6,7,3)/7 actions).  Calling it again discards the state.       */
+ * Connect4 (6,7,3)/7 actions, the synthetic Atari-like env of configs[4]
+ * (84,84,4)/18 actions with stacked_observations = 0: Philox-keyed frames,
+ * rules in muzero.jl_amd/games/atari_synth.py; the records and the shard
+ * hold one 84x84 byte frame per move and the observation is the env's
+ * four-frame stack).  Calling it again discards the state.                 */
 int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games);
 
 /* One move of every slot, on the device, stream-ordered: observation append

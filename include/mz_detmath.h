@@ -192,7 +192,9 @@ enum {
     MZ_RNG_GAME = 4,       /* sample_n_games, ReplayBuffer.jl:102             */
     MZ_RNG_POS = 5,        /* sample_position, ReplayBuffer.jl:80             */
     MZ_RNG_ABSORB = 6,     /* absorbing-state action, ReplayBuffer.jl:46      */
-    MZ_RNG_OPPONENT = 7    /* random opponent, select_opponent_action :321    */
+    MZ_RNG_OPPONENT = 7,   /* random opponent, select_opponent_action :321    */
+    MZ_RNG_ENV = 8,        /* synthetic Atari-like env: reset key, step      */
+    MZ_RNG_FRAME = 9       /* synthetic Atari-like env: frame bytes of a key */
 };
 
 MZ_HD uint32_t mz_rng_u32(uint64_t seed, uint32_t purpose, uint32_t id, uint32_t step, uint32_t idx) {

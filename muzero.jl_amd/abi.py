@@ -16,7 +16,7 @@ from .config import (MzConfig, MzFFHP, MzResNetHP, ResNetHP, hidden_size, stacke
                      to_c_ffhp, to_c_resnet_hp)
 
 NET_REPR, NET_PRED, NET_DYN = 0, 1, 2
-ENV_TICTACTOE, ENV_CONNECT4 = 0, 1
+ENV_TICTACTOE, ENV_CONNECT4, ENV_ATARI = 0, 1, 2
 SP_TRAIN, SP_EVAL = 0, 1
 TRAIN_LEARNER, TRAIN_ACTOR, TRAIN_QUEUED = 0, 1, 2
 LEARN_REF_SEMANTICS, LEARN_CORRECTED = 0, 1
@@ -307,6 +307,8 @@ class Engine:
         self._check(self.lib.mz_selfplay_init(self.h, env_kind, G, replay_games), "mz_selfplay_init")
         self.sp_G = G
         self.osz = int(np.prod(self.conf.observation_shape))
+        if env_kind == ENV_ATARI:                      # one 84x84 frame per move in the records
+            self.osz = int(self.conf.observation_shape[0] * self.conf.observation_shape[1])
 
     def selfplay_move(self, rng_step, game_offset=0, temperature=1.0, stream=None):
         self._check(self.lib.mz_selfplay_move(self.h, rng_step, game_offset, temperature, stream),
@@ -363,7 +365,7 @@ class Engine:
     def replay_save_game(self, hist):
         """save_game of a host GameHistory (selfplay.GameHistory)."""
         a = hist.as_arrays()
-        obs = np.ascontiguousarray(a["observation"] != 0, np.uint8)
+        obs = np.ascontiguousarray(a["observation"], np.uint8)      # 0/1 planes, or frame bytes
         self._check(self.lib.mz_replay_save_game(
             self.h, len(a["action"]), _p(obs), _p(np.ascontiguousarray(a["action"], np.int32)),
             _p(np.ascontiguousarray(a["reward"], np.float32)), _p(np.ascontiguousarray(a["to_play"], np.int32)),

@@ -55,6 +55,7 @@ extern "C" __global__ void mz_sp_prepare(SpParams S);
 extern "C" __global__ void mz_sp_commit(SpParams S);
 extern "C" __global__ void mz_sp_order(SpParams S);
 extern "C" __global__ void mz_sp_store(SpParams S);
+extern "C" __global__ void mz_sp_reset(SpParams S);
 extern "C" __global__ void mz_rp_sample(RpSampleParams Q);
 extern "C" __global__ void mz_rp_per_init(SpHist ring, int slot, int len, int Tmax, int td, const float* disc_pow,
                                           int alpha);
@@ -240,6 +241,7 @@ struct mz_handle {
     // device self-play + replay shard (mz_selfplay.hip); own allocation list (re-init frees it)
     int sp_env = -1, sp_G = 0, sp_T = 0, sp_osz = 0, sp_cap = 0;
     uint8_t* d_sp_board = nullptr; int32_t* d_sp_player = nullptr; uint8_t* d_sp_over = nullptr;
+    uint32_t* d_sp_ekey = nullptr; int sp_frames = 0;
     SpHist sp_hist{}, sp_ring{};
     long long* d_sp_counters = nullptr;
     int32_t* d_sp_done = nullptr; int32_t* d_sp_rpos = nullptr;
@@ -2524,6 +2526,7 @@ static SpParams sp_params(mz_handle* h) {
     S.osz = h->sp_osz; S.P = h->plane; S.A = h->A; S.F = h->obs_feat; S.stacked = c.stacked_observations;
     S.T = h->sp_T; S.max_moves = c.max_moves;
     S.board = h->d_sp_board; S.player = h->d_sp_player; S.over = h->d_sp_over;
+    S.frames = h->sp_frames; S.ekey = h->d_sp_ekey;
     S.hist = h->sp_hist; S.ring = h->sp_ring; S.cap = h->sp_cap; S.counters = h->d_sp_counters;
     S.obs = h->d_obs; S.legal = h->d_legal; S.tp = h->d_tp; S.cv = h->d_cv; S.rv = h->d_rv; S.act = h->d_act;
     S.done = h->d_sp_done; S.ring_pos = h->d_sp_rpos;
@@ -2543,6 +2546,9 @@ int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games) {
         if (W != 3 || H != 3 || C != 3 || h->A != 9) return fail(h, "TicTacToe needs observation_shape (3,3,3), 9 actions");
     } else if (env_kind == MZ_ENV_CONNECT4) {
         if (W != 6 || H != 7 || C != 3 || h->A != 7) return fail(h, "Connect4 needs observation_shape (6,7,3), 7 actions");
+    } else if (env_kind == MZ_ENV_ATARI) {
+        if (W != 84 || H != 84 || C != 4 || h->A != 18 || c.stacked_observations != 0)
+            return fail(h, "the Atari-like env needs observation_shape (84,84,4), 18 actions, stacked_observations 0");
     } else {
         return fail(h, "unknown env_kind");
     }
@@ -2559,9 +2565,12 @@ int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games) {
     h->tr_B = 0;                                // a new shard: mz_train_init again
     h->sp_env = env_kind; h->sp_G = G; h->sp_cap = replay_games;
     h->sp_T = c.max_moves + 1; h->sp_osz = W * H * C;
+    h->sp_frames = 0;
+    if (env_kind == MZ_ENV_ATARI) { h->sp_osz = W * H; h->sp_frames = C; }   // one frame per move
     MZ_TRY(h, spalloc(h, &h->d_sp_board, (size_t)G * h->sp_osz));
     MZ_TRY(h, spalloc(h, &h->d_sp_player, (size_t)G));
     MZ_TRY(h, spalloc(h, &h->d_sp_over, (size_t)G));
+    MZ_TRY(h, spalloc(h, &h->d_sp_ekey, (size_t)G));
     if (sp_alloc_hist(h, h->sp_hist, (size_t)G)) return -1;
     if (sp_alloc_hist(h, h->sp_ring, (size_t)replay_games)) return -1;
     MZ_TRY(h, spalloc(h, &h->d_sp_counters, 4));
@@ -2579,6 +2588,14 @@ int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games) {
     for (int n = 0; n < (int)dp.size(); ++n) dp[n] = (float)std::pow((double)c.discount, (double)n);
     MZ_TRY(h, spalloc(h, &h->d_sp_dpow, dp.size()));
     MZ_TRY(h, hipMemcpy(h->d_sp_dpow, dp.data(), dp.size() * 4, hipMemcpyHostToDevice));
+    if (env_kind == MZ_ENV_ATARI) {                 // every slot: new game (key and first frame on the device)
+        SpParams S = sp_params(h);
+        S.reset_step = 0xFFFFFFFFu;
+        hipLaunchKernelGGL(mz_sp_reset, dim3((G + 3) / 4), dim3(256), 0, h->stream, S);
+        MZ_TRY(h, hipGetLastError());
+        MZ_TRY(h, hipStreamSynchronize(h->stream));
+        return 0;
+    }
     // every slot: new game (boards: empty plane set, player 1)
     std::vector<uint8_t> b((size_t)G * h->sp_osz, 0);
     const int cells = W * H;
@@ -2717,6 +2734,7 @@ static int rs_params(mz_handle* h, int32_t B, uint32_t step, hipStream_t st, RpS
     std::memset(&Q, 0, sizeof(Q));
     Q.B = B; Q.K = K1 - 1; Q.A = A; Q.osz = h->sp_osz; Q.P = h->plane; Q.F = h->obs_feat;
     Q.stacked = h->conf.stacked_observations; Q.T = h->sp_T; Q.td = h->conf.td_steps; Q.cap = h->sp_cap;
+    Q.frames = h->sp_frames;
     Q.seed = h->seed; Q.step = step; Q.ring = h->sp_ring; Q.counters = h->d_sp_counters; Q.disc_pow = h->d_sp_dpow;
     Q.obs = h->d_rs_obs; Q.actions = h->d_rs_act; Q.tv = h->d_rs_tv; Q.tr = h->d_rs_tr; Q.tpol = h->d_rs_tp;
     Q.gscale = h->d_rs_gs; Q.index = h->d_rs_index;

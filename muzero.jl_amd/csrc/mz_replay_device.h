@@ -26,6 +26,30 @@ __device__ __forceinline__ void stacked_obs(float* out, const uint8_t* cur, cons
     }
 }
 
+// The synthetic Atari-like env's observation at 1-based move `index`
+// (games/atari_synth.py): channel c = frame index-n+1+c (newest last), zeros
+// before move 1, byte x as f32(x) * f32(1/255).  frames = the record's
+// per-move frames (osz bytes each, osz % 4 == 0, 4-byte aligned).
+__device__ __forceinline__ void frame_stack_obs(float* out, const uint8_t* frames, int index, int osz, int n,
+                                                int lane) {
+    const float scale = 1.0f / 255.0f;
+    const int nw = osz >> 2;
+    for (int c = 0; c < n; ++c) {
+        const int s = index - n + 1 + c;
+        float4* o = reinterpret_cast<float4*>(out + (size_t)c * osz);
+        if (s < 1) {
+            for (int q = lane; q < nw; q += 64) o[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            continue;
+        }
+        const uint32_t* f = reinterpret_cast<const uint32_t*>(frames + (size_t)(s - 1) * osz);
+        for (int q = lane; q < nw; q += 64) {
+            const uint32_t w = f[q];
+            o[q] = make_float4((float)(w & 255u) * scale, (float)((w >> 8) & 255u) * scale,
+                               (float)((w >> 16) & 255u) * scale, (float)(w >> 24) * scale);
+        }
+    }
+}
+
 // compute_target_value (ReplayBuffer.jl:5-20, Q9), f32, 1-based index
 __device__ __forceinline__ float rp_target_value(int td, const float* disc_pow, const float* rv, const int32_t* tp,
                                                  const float* rew, int T, int index) {
@@ -155,8 +179,11 @@ __device__ __forceinline__ void rp_sample_one(const RpSampleParams& Q, int b, in
         const int k = e / A, a = e - k * A, ci = pos + k;
         Q.tpol[(size_t)b * K1 * A + e] = ci < T ? cv[(size_t)(ci - 1) * A + a] : uni;
     }
-    stacked_obs(Q.obs + (size_t)b * Q.F, Q.ring.obs + (base + pos - 1) * Q.osz, Q.ring.obs + base * Q.osz, act, pos,
-                Q.osz, Q.P, Q.stacked, lane);
+    if (Q.frames)
+        frame_stack_obs(Q.obs + (size_t)b * Q.F, Q.ring.obs + base * Q.osz, pos, Q.osz, Q.frames, lane);
+    else
+        stacked_obs(Q.obs + (size_t)b * Q.F, Q.ring.obs + (base + pos - 1) * Q.osz, Q.ring.obs + base * Q.osz, act,
+                    pos, Q.osz, Q.P, Q.stacked, lane);
     if (lane == 0) {
         const int gs = T + 1 - pos;                                // :212 min(K, len(action_history)+1-pos)
         Q.gscale[b] = (float)(Q.K < gs ? Q.K : gs);

@@ -9,8 +9,11 @@
 //
 // Env rules: TicTacToe exactly as games/tictactoe/game.jl with quirk Q14 (the
 // win test looks at the plane of the player TO MOVE; reward ±1 by the mover's
-// id), Connect4 as games/connect4.py.  Host mirrors:
-// muzero.jl_amd/games/{tictactoe,connect4}.py, selfplay.py, replay_buffer.py.
+// id), Connect4 as games/connect4.py, the synthetic Atari-like env of
+// configs[4] as games/atari_synth.py (Philox-keyed frames, one frame per move
+// in the records, a four-frame stack as the observation).  Host mirrors:
+// muzero.jl_amd/games/{tictactoe,connect4,atari_synth}.py, selfplay.py,
+// replay_buffer.py.
 #include "mz_internal.h"
 #include "mz_selfplay_params.h"
 #include "mz_replay_device.h"
@@ -45,10 +48,28 @@ __device__ __forceinline__ bool c4_wins(const uint8_t* stones, int w, int h, int
     return false;
 }
 
+// ---- synthetic Atari-like env (games/atari_synth.py): the frame of key
+// `key` (osz = 84·84 bytes = 441 Philox blocks of 16 bytes), written by the
+// 64 lanes of one wave
+__device__ void atari_frame(const SpParams& S, int g, uint32_t key, int lane) {
+    uint4* f = reinterpret_cast<uint4*>(S.board + (size_t)g * S.osz);
+    for (int j = lane; j < (S.osz >> 4); j += 64) {
+        const mz_u32x4 r = mz_philox((uint32_t)j, key, 0u, MZ_RNG_FRAME, (uint32_t)S.seed, (uint32_t)(S.seed >> 32));
+        f[j] = make_uint4(r.v[0], r.v[1], r.v[2], r.v[3]);
+    }
+}
+// reset: key = u32(seed, ENV, slot, step, ~0)
+__device__ void atari_reset(const SpParams& S, int g, uint32_t step, int lane) {
+    const uint32_t key = mz_rng_u32(S.seed, MZ_RNG_ENV, (uint32_t)g, step, 0xFFFFFFFFu);
+    atari_frame(S, g, key, lane);
+    if (lane == 0) { S.ekey[g] = key; S.player[g] = 1; S.over[g] = 0; }
+}
+
 // legal actions (1..A) as a bit mask
 __device__ uint32_t env_legal(const SpParams& S, int g) {
     const uint8_t* b = S.board + (size_t)g * S.osz;
     uint32_t m = 0;
+    if (S.env == MZ_ENV_ATARI) return S.A >= 32 ? 0xFFFFFFFFu : (1u << S.A) - 1u;
     if (S.env == MZ_ENV_TICTACTOE) {                    // game.jl:37-43
         if (ttt_line(b, S.player[g])) return 0;
         for (int c = 0; c < 9; ++c) m |= (uint32_t)b[18 + c] << c;
@@ -102,6 +123,7 @@ __device__ __forceinline__ int game_winner(const SpParams& S, float last_reward,
 }
 
 __device__ void env_reset(const SpParams& S, int g, int lane) {
+    if (S.env == MZ_ENV_ATARI) { atari_reset(S, g, S.step, lane); return; }
     uint8_t* b = S.board + (size_t)g * S.osz;
     const int cells = S.osz / 3;
     for (int k = lane; k < S.osz; k += 64) b[k] = k >= 2 * cells;
@@ -117,8 +139,11 @@ extern "C" __global__ __launch_bounds__(256) void mz_sp_prepare(SpParams S) {
     uint8_t* ho = S.hist.obs + ((size_t)g * S.T + t) * S.osz;     // observation_history append (:352)
     const uint8_t* b = S.board + (size_t)g * S.osz;
     for (int k = lane; k < S.osz; k += 64) ho[k] = b[k];
-    stacked_obs(S.obs + (size_t)g * S.F, b, S.hist.obs + (size_t)g * S.T * S.osz, S.hist.act + (size_t)g * S.T,
-                t + 1, S.osz, S.P, S.stacked, lane);                // :355
+    if (S.frames)                                                  // the env's frame stack (same lanes wrote ho)
+        frame_stack_obs(S.obs + (size_t)g * S.F, S.hist.obs + (size_t)g * S.T * S.osz, t + 1, S.osz, S.frames, lane);
+    else
+        stacked_obs(S.obs + (size_t)g * S.F, b, S.hist.obs + (size_t)g * S.T * S.osz, S.hist.act + (size_t)g * S.T,
+                    t + 1, S.osz, S.P, S.stacked, lane);            // :355
     if (lane == 0) {
         const uint32_t m = env_legal(S, g);
         for (int a = 0; a < S.A; ++a) S.legal[(size_t)g * S.A + a] = (m >> a) & 1u;
@@ -139,6 +164,22 @@ extern "C" __global__ __launch_bounds__(256) void mz_sp_commit(SpParams S) {
     const int t = S.hist.len[g];
     const size_t r = (size_t)g * S.T + t;
     for (int a = lane; a < S.A; a += 64) S.hist.cv[r * S.A + a] = S.cv[(size_t)g * S.A + a];   // :375-379
+    if (S.env == MZ_ENV_ATARI) {                                   // every lane steps the env (the frame is wave work)
+        const int a = S.act[g];
+        const uint32_t key = S.ekey[g];
+        const mz_u32x4 v = mz_philox(0u, key, (uint32_t)a, MZ_RNG_ENV, (uint32_t)S.seed, (uint32_t)(S.seed >> 32));
+        atari_frame(S, g, v.v[2], lane);
+        if (lane == 0) {
+            S.ekey[g] = v.v[2];
+            S.hist.act[r] = a;
+            S.hist.rew[r] = (int)mz_rng_below(v.v[0], (uint32_t)S.A) == a - 1 ? 1.0f : 0.0f;
+            S.hist.tp[r] = S.player[g];
+            S.hist.rv[r] = S.rv[g];
+            S.hist.len[g] = t + 1;
+            S.done[g] = (v.v[1] & 127u) == 0 || t + 1 > S.max_moves;
+        }
+        return;
+    }
     if (lane == 0) {
         int a = S.act[g];
         const int mover = S.player[g];
@@ -162,6 +203,12 @@ extern "C" __global__ __launch_bounds__(256) void mz_sp_commit(SpParams S) {
         S.hist.len[g] = t + 1;
         S.done[g] = done || t + 1 > S.max_moves;                  // :343 (> max_moves)
     }
+}
+
+// initial games of the synthetic Atari-like env (mz_selfplay_init), one wave per slot
+extern "C" __global__ __launch_bounds__(256) void mz_sp_reset(SpParams S) {
+    const int g = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (g < S.G) atari_reset(S, g, S.reset_step, lane);
 }
 
 // Ring slots of this move's finished games in slot order (the host driver

@@ -4,9 +4,11 @@
 //
 // Per game slot g (G slots played in lockstep, SelfPlay.jl:330-382):
 //   env      board[g][osz] (0/1 bytes: planes [p1, p2, empty], col-major cells),
-//            player[g] (1 or 2), over[g];
+//            player[g] (1 or 2), over[g]; the synthetic Atari-like env
+//            (frames = 4): board[g] = the current 84x84 frame, ekey[g] its key;
 //   history  GameHistory (Constructors.jl:6-16) of the game in progress, up to
-//            T = max_moves + 1 moves: obs[g][T][osz] bytes, act / rew / tp /
+//            T = max_moves + 1 moves: obs[g][T][osz] bytes (one frame per move
+//            when frames > 0: the observation stacks the last `frames`), act / rew / tp /
 //            rv [g][T], cv [g][T][A], len[g] = moves recorded.
 // Replay shard (ReplayBuffer.jl:133-161, PER = false): a FIFO ring of `cap`
 // finished games with the same per-game layout; game number n (1-based, the
@@ -28,7 +30,10 @@ struct SpHist {                 // a set of game records: [n][T] ...
 
 struct SpParams {
     int G, env, W, H, osz, P, A, F, stacked, T, max_moves;
+    int frames;                 // > 0: the env stacks its last `frames` frames (atari_synth), 0: board games
     uint8_t* board; int32_t* player; uint8_t* over;
+    uint32_t* ekey;             // [G] synthetic Atari-like env state
+    uint32_t reset_step;        // mz_sp_reset: the step key of the initial games
     SpHist hist;                // [G] games in progress
     SpHist ring;                // [cap] replay shard
     int cap;
@@ -60,6 +65,7 @@ struct SpParams {
 // get_batch + make_target (ReplayBuffer.jl:5-50, 73-107, 188-217) on the shard
 struct RpSampleParams {
     int B, K, A, osz, P, F, stacked, T, td, cap;
+    int frames;                 // the env's frame stack (0: stacked observations, Q15)
     uint64_t seed; uint32_t step;
     SpHist ring;
     const long long* counters;

@@ -12,7 +12,7 @@ from collections import OrderedDict
 
 import numpy as np
 
-from .selfplay import GameHistory, get_stacked_observations
+from .selfplay import GameHistory, frame_stack_obs, get_stacked_observations
 
 MZ_RNG_GAME, MZ_RNG_POS, MZ_RNG_ABSORB = 4, 5, 6
 from .rng import _M, _philox, rng_below, rng_u32  # noqa: F401  (re-exported)
@@ -106,9 +106,12 @@ def per_categorical(w, u):
 class ReplayBuffer:
     """Per-GPU buffer: Dict{game_id => GameHistory} with FIFO eviction."""
 
-    def __init__(self, conf, seed=0):
+    def __init__(self, conf, seed=0, frame_stack=0):
+        """frame_stack: the env's own frame stacking (games/atari_synth.py,
+        observation_history holds one frame per move), 0 for board games."""
         self.conf = conf
         self.seed = seed
+        self.frame_stack = frame_stack
         self.buffer = OrderedDict()
         self.num_played_games = 0
         self.num_played_steps = 0
@@ -172,8 +175,11 @@ class ReplayBuffer:
             else:
                 pos = rng_below(rp, T) + 1                                         # sample_position :80
             tv[b], tr[b], tp[b], acts[b] = make_target(c, h, pos, self.seed, b, step)
-            obs[b] = get_stacked_observations(h.observation_history, h.action_history, pos,
-                                              c.stacked_observations, plane)
+            if self.frame_stack:
+                obs[b] = frame_stack_obs(h.observation_history, pos, self.frame_stack)
+            else:
+                obs[b] = get_stacked_observations(h.observation_history, h.action_history, pos,
+                                                  c.stacked_observations, plane)
             gs[b] = min(K, len(h.action_history) + 1 - pos)                        # :212
             index_batch.append((ids[gi], pos))
         out = dict(observation=obs, actions=acts, target_values=tv, target_rewards=tr,

@@ -24,3 +24,19 @@ def rng_u32(seed, purpose, ident, step, idx):
 
 def rng_below(r, n):
     return (r * n) >> 32
+
+
+def philox_np(c0, c1, c2, c3, k0, k1):
+    """Philox4x32-10 over numpy arrays (broadcast), the same rounds as _philox;
+    returns four uint32 arrays."""
+    import numpy as np
+    m = np.uint64(_M)
+    c0, c1, c2, c3 = (np.asarray(c, np.uint64) & m for c in (c0, c1, c2, c3))
+    k0, k1 = np.asarray(k0, np.uint64) & m, np.asarray(k1, np.uint64) & m
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * c0
+        p1 = np.uint64(0xCD9E8D57) * c2
+        c0, c1, c2, c3 = (p1 >> np.uint64(32)) ^ c1 ^ k0, p1 & m, (p0 >> np.uint64(32)) ^ c3 ^ k1, p0 & m
+        k0 = (k0 + np.uint64(0x9E3779B9)) & m
+        k1 = (k1 + np.uint64(0xBB67AE85)) & m
+    return tuple(x.astype(np.uint32) for x in (c0, c1, c2, c3))

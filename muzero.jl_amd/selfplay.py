@@ -57,6 +57,19 @@ class GameHistory:                                               # Constructors.
                     root_values=np.array(self.root_values, np.float32))
 
 
+def frame_stack_obs(frames, index, n):
+    """The frame-stacked observation at 1-based move `index` (games/atari_synth.py):
+    frames index-n+1 .. index as the channels, zeros before move 1, bytes x f32(1/255)."""
+    plane = np.asarray(frames[0]).size
+    out = np.zeros(n * plane, np.float32)
+    scale = np.float32(1.0) / np.float32(255.0)
+    for c in range(n):
+        s = index - n + 1 + c
+        if s >= 1:
+            out[c * plane:(c + 1) * plane] = np.asarray(frames[s - 1], np.uint8).astype(np.float32) * scale
+    return out
+
+
 def get_stacked_observations(obs_hist, action_hist, index, num_stacked, plane):
     """SelfPlay.jl:128-149 (Q15): [obs_t, (action plane, obs_{t-1}) ...], zeros before
     the first move; the action plane holds the raw action id.  `index` is 1-based."""
@@ -84,7 +97,9 @@ class BatchedSelfPlay:
         self.eng = engine
         self.conf = engine.conf
         self.G = G
-        self.env = env_cls(G)
+        # keyed envs (games/atari_synth.py) draw from the engine's Philox streams
+        self.env = env_cls(G, seed=engine.rng_seed) if getattr(env_cls, "KEYED", False) else env_cls(G)
+        self.frame_stack = getattr(env_cls, "FRAME_STACK", 0)
         self.game_offset = game_offset
         self.step = step0
         self.plane = self.conf.observation_shape[0] * self.conf.observation_shape[1]
@@ -95,6 +110,9 @@ class BatchedSelfPlay:
         c = self.conf
         out = np.empty((self.G, stacked_features(c)), np.float32)
         for g, h in enumerate(self.histories):
+            if self.frame_stack:                         # the env's own frame stack (atari_synth)
+                out[g] = frame_stack_obs(h.observation_history, len(h.observation_history), self.frame_stack)
+                continue
             out[g] = get_stacked_observations(h.observation_history, h.action_history,
                                               len(h.observation_history), c.stacked_observations, self.plane)
         return out
@@ -104,7 +122,8 @@ class BatchedSelfPlay:
         c = self.conf
         tp = self.env.player.copy()                                           # :351
         for g, h in enumerate(self.histories):
-            h.observation_history.append(self.env.board[g].astype(np.float32))  # :352
+            h.observation_history.append(self.env.board[g].copy() if self.frame_stack else
+                                         self.env.board[g].astype(np.float32))   # :352
         obs = self._stacked()                                                 # :355
         legal = self.env.legal_mask()
         cv, rv, act = self.eng.mcts_search(obs, legal, tp, exploration=True, rng_step=self.step,
@@ -138,7 +157,10 @@ class BatchedSelfPlay:
             self.finished.append(self.histories[g])
             self.histories[g] = GameHistory()
         if len(ended):
-            self.env.reset(ended)
+            if getattr(self.env, "KEYED", False):
+                self.env.reset(ended, step=self.step)
+            else:
+                self.env.reset(ended)
         self.step += 1
         return ended
 
