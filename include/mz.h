@@ -234,9 +234,10 @@ int mz_learner_step(mz_handle* h, const mz_batch* batch, double eta, float* loss
 
 /* Learner mode.  MZ_LEARN_REF_SEMANTICS (default): the reference as written
  * — its pullbacks see only sum(sqnorm, params), so ∇ = 2θ (quirk Q11), and
- * the reported policy loss is Q11's broadcast.  MZ_LEARN_CORRECTED (FC nets):
- * the loss Learning.jl:261-288 means, differentiated through the unroll
- * (real backpropagation on MFMA, mz_backprop.hip), as a per-sample mean so a
+ * the reported policy loss is Q11's broadcast.  MZ_LEARN_CORRECTED (FC nets
+ * without BatchNorm, and the ResNet nets without the downsampler): the loss
+ * Learning.jl:261-288 means, differentiated through the unroll (real
+ * backpropagation on MFMA, mz_backprop.hip), as a per-sample mean so a
  * data-parallel all-reduce-mean equals the global batch:
  *   L = (1/B) Σ_b (w_b/g_b) [Σ_k (v−z)² + Σ_k CE(logits, π) + ir·Σ_k (r−u)²] + Σθ²
  * (CE = logitcrossentropy on the policy head's logits).  Every learner entry

@@ -481,3 +481,244 @@ extern "C" __global__ __launch_bounds__(256) void mz_bp_fold(BpFoldParams Q) {
         }
     }
 }
+
+// ============================================================================
+// The corrected learner for the ResNet nets (mz_backprop_params.h RbpApp):
+// one 256-thread workgroup per sample, its arena T (activations), G (their
+// gradients) and DT (the current application's ∂L/∂t) in HBM.
+#define RBP_THREADS 256
+
+// im2col operand of a conv, input element (k, p) for k = i + kw·j + kw·kh·c:
+// x[c] at (px, py) = (p mod W + (kw−1−i) − kw/2, p div W + (kh−1−j) − kh/2),
+// zero off the board (Flux's flipped kernel, "same" padding)
+__device__ __forceinline__ float rbp_xhat(const float* X, const RbpApp& L, int P, int Wb, int k, int p) {
+    const int kk = L.kw * L.kh;
+    if (k >= kk * L.cin || p >= P) return 0.0f;
+    const int c = k / kk, r = k - c * kk, j = r / L.kw, i = r - j * L.kw;
+    const int px = p % Wb + (L.kw - 1 - i) - L.kw / 2, py = p / Wb + (L.kh - 1 - j) - L.kh / 2;
+    return px >= 0 && px < Wb && py >= 0 && py < P / Wb ? X[c * P + px + Wb * py] : 0.0f;
+}
+
+// forward: output block (16 channels x 16 positions) u of a conv
+__device__ void rbp_conv_fwd(const RbpParams& Q, const RbpApp& L, float* T, int u) {
+    const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4, P = Q.P;
+    const int npb = (P + 15) >> 4, ob = u / npb, pb = u - ob * npb;
+    const int K = L.kw * L.kh * L.cin, co = ob * 16 + m, p = pb * 16 + m;
+    const float* W = Q.flat + L.w_off;
+    const float* X = T + L.x;
+    const bp_f32x4 acc = bp_gemm_block((K + 3) >> 2, kq,
+        [&](int k) { return co < L.cout && k < K ? W[k + (size_t)K * co] : 0.0f; },
+        [&](int k) { return rbp_xhat(X, L, P, Q.Wb, k, p); });
+    const int pc = pb * 16 + m;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int o = ob * 16 + kq * 4 + r;
+        if (o >= L.cout || pc >= P) continue;
+        const int e = o * P + pc;
+        const float t = acc[r] + Q.flat[L.b_off + o];
+        float v = t;
+        if (L.bn_off >= 0) {
+            T[L.z + e] = t;
+            v = mz_bn_apply(t, Q.flat[L.bn_off + L.cout + o], Q.flat[L.bn_off + o]);
+        }
+        if (L.res >= 0) v = v + T[L.res + e];
+        T[L.y + e] = bp_act(L.act, v);
+    }
+}
+
+__device__ void rbp_dense_fwd(const RbpParams& Q, const RbpApp& L, float* T) {
+    const float* W = Q.flat + L.w_off;
+    for (int o = threadIdx.x; o < L.cout; o += blockDim.x) {
+        float s = 0.0f;
+        for (int i = 0; i < L.cin; ++i) s = fmaf(W[o + (size_t)L.cout * i], T[L.x + i], s);
+        T[L.y + o] = bp_act(L.act, s + Q.flat[L.b_off + o]);
+    }
+}
+
+// ∂L/∂t of a conv (t = Wx + b) into DT, the residual input's share of ∂L/∂y,
+// and the per-channel sums: db = Σ dt, dβ = Σ du, dγ = Σ du·t/√(1+ε)
+__device__ void rbp_conv_dt(const RbpParams& Q, const RbpApp& L, const float* T, float* G, float* DT, float* gs) {
+    const int P = Q.P;
+    for (int o = threadIdx.x; o < L.cout; o += blockDim.x) {
+        const bool bn = L.bn_off >= 0;
+        const float gr = bn ? Q.flat[L.bn_off + L.cout + o] / MZ_BN_S : 1.0f;
+        float sb = 0.0f, sbe = 0.0f, sga = 0.0f;
+        for (int p = 0; p < P; ++p) {
+            const int e = o * P + p;
+            const float du = bp_dz(L.act, G[L.y + e], T[L.y + e]);
+            if (L.res >= 0) G[L.res + e] += du;
+            const float dt = bn ? du * gr : du;
+            if (bn) { sbe += du; sga += du * (T[L.z + e] / MZ_BN_S); }
+            DT[e] = dt;
+            sb += dt;
+        }
+        gs[L.b_off + o] += sb;
+        if (bn) { gs[L.bn_off + o] += sbe; gs[L.bn_off + L.cout + o] += sga; }
+    }
+}
+
+// G[x] += the transposed conv of DT: input block (16 channels x 16 positions) u
+__device__ void rbp_conv_dx(const RbpParams& Q, const RbpApp& L, const float* DT, float* G, int u) {
+    const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4, P = Q.P, Wb = Q.Wb;
+    const int npb = (P + 15) >> 4, ib = u / npb, pb = u - ib * npb;
+    const int kk = L.kw * L.kh, K = kk * L.cin, Kt = kk * L.cout, ci = ib * 16 + m, p = pb * 16 + m;
+    const float* W = Q.flat + L.w_off;
+    const bp_f32x4 acc = bp_gemm_block((Kt + 3) >> 2, kq,
+        [&](int k) {
+            if (ci >= L.cin || k >= Kt) return 0.0f;
+            const int co = k / kk, tap = k - co * kk;
+            return W[tap + kk * ci + (size_t)K * co];
+        },
+        [&](int k) {
+            if (k >= Kt || p >= P) return 0.0f;
+            const int co = k / kk, tap = k - co * kk, j = tap / L.kw, i = tap - j * L.kw;
+            const int qx = p % Wb - ((L.kw - 1 - i) - L.kw / 2), qy = p / Wb - ((L.kh - 1 - j) - L.kh / 2);
+            return qx >= 0 && qx < Wb && qy >= 0 && qy < P / Wb ? DT[co * P + qx + Wb * qy] : 0.0f;
+        });
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int c = ib * 16 + kq * 4 + r;
+        if (c < L.cin && p < P) G[L.x + c * P + p] += acc[r];
+    }
+}
+
+// this sample's dW of a conv, block (16 output channels x 16 k) u: Σ_p dt ⊗ x̂
+__device__ void rbp_conv_dw(const RbpParams& Q, const RbpApp& L, const float* T, const float* DT, float* gs, int u) {
+    const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4, P = Q.P;
+    const int K = L.kw * L.kh * L.cin, nkb = (K + 15) >> 4, ob = u / nkb, kb = u - ob * nkb;
+    const int co = ob * 16 + m, kc = kb * 16 + m;
+    const float* X = T + L.x;
+    const bp_f32x4 acc = bp_gemm_block((P + 3) >> 2, kq,
+        [&](int p) { return co < L.cout && p < P ? DT[co * P + p] : 0.0f; },
+        [&](int p) { return rbp_xhat(X, L, P, Q.Wb, kc, p); });
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int o = ob * 16 + kq * 4 + r;
+        if (o < L.cout && kc < K) gs[L.w_off + kc + (size_t)K * o] += acc[r];
+    }
+}
+
+// dL/dy of the heads for sample b (bp_heads for one sample)
+__device__ void rbp_heads(const RbpParams& Q, const float* T, float* G, int b) {
+    const int K1 = Q.K + 1;
+    for (int e = threadIdx.x; e < Q.n_head; e += blockDim.x) {
+        const BpHead hd = Q.heads[e];
+        const int k = hd.step;
+        const float w = Q.weights ? Q.weights[b] : 1.0f;
+        const float c = w / (Q.gscale[b] * (float)Q.B);
+        const size_t bk = (size_t)b * K1 + k;
+        if (hd.kind == BP_HEAD_V || hd.kind == BP_HEAD_R) {
+            const bool v = hd.kind == BP_HEAD_V;
+            const float y = T[hd.y];
+            const float d = y - (v ? Q.tv[bk] : Q.tr[bk]);
+            const bool on = v || Q.intermediate_rewards;
+            (v ? Q.pv : Q.pr)[bk] = y;
+            G[hd.y] = on ? c * 2.0f * d : 0.0f;
+            Q.terms[bk * 3 + (v ? 0 : 2)] = on ? d * d : 0.0f;
+        } else {                                              // logitcrossentropy on the logits
+            const float* l = T + hd.y;
+            const float* pi = Q.tp + bk * Q.A;
+            float mx = l[0];
+            for (int a = 1; a < Q.A; ++a) mx = fmaxf(mx, l[a]);
+            float S = 0.0f, sp = 0.0f;
+            for (int a = 0; a < Q.A; ++a) { S += det_expf(l[a] - mx); sp += pi[a]; }
+            const float lS = det_logf(S);
+            float ce = 0.0f;
+            for (int a = 0; a < Q.A; ++a) {
+                const float z = l[a] - mx;
+                ce -= pi[a] * (z - lS);
+                const float pa = det_expf(z) / S;
+                G[hd.y + a] = c * (pa * sp - pi[a]);
+                Q.pp[bk * Q.A + a] = pa;
+            }
+            Q.terms[bk * 3 + 1] = ce;
+        }
+    }
+}
+
+extern "C" __global__ __launch_bounds__(RBP_THREADS) void mz_rbp_sample(RbpParams Q) {
+    const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x, wave = tid >> 6, nw = nt >> 6, K1 = Q.K + 1;
+    float* T = Q.act + (size_t)b * Q.arena;
+    float* G = Q.grad + (size_t)b * Q.arena;
+    float* DT = Q.dt + (size_t)b * Q.dt_floats;
+    float* gs = Q.gsam + (size_t)b * Q.nflat;
+    for (int e = tid; e < Q.arena; e += nt) G[e] = 0.0f;
+    for (int e = tid; e < Q.nflat; e += nt) gs[e] = 0.0f;
+    for (int e = tid; e < K1 * 3; e += nt) Q.terms[(size_t)b * K1 * 3 + e] = 0.0f;
+    for (int e = tid; e < K1; e += nt) Q.pr[(size_t)b * K1 + e] = 0.0f;        // rewards: 0 at step 0
+    for (int e = tid; e < Q.obs_feat; e += nt) T[Q.obs_t + e] = Q.obs[(size_t)b * Q.obs_feat + e];
+    __syncthreads();
+    const int npb = (Q.P + 15) >> 4;
+    // ---- forward: representation, K dynamics steps, K+1 predictions (Q10)
+    for (int a = 0; a < Q.n_app; ++a) {
+        const RbpApp L = Q.apps[a];
+        if (L.op == RBP_CONV) {
+            const int units = ((L.cout + 15) >> 4) * npb;
+            for (int u = wave; u < units; u += nw) rbp_conv_fwd(Q, L, T, u);
+        } else if (L.op == RBP_DENSE) {
+            rbp_dense_fwd(Q, L, T);
+        } else {                                              // make_dynamics_input (:293-304)
+            const float av = Q.actions[(size_t)b * K1 + L.step] / (float)Q.A;
+            for (int f = tid; f < L.cout; f += nt) T[L.y + f] = f < L.cin ? T[L.x + f] * 2.0f : av;
+        }
+        __syncthreads();
+    }
+    rbp_heads(Q, T, G, b);
+    __syncthreads();
+    // ---- backward, reverse order
+    for (int a = Q.n_app - 1; a >= 0; --a) {
+        const RbpApp L = Q.apps[a];
+        if (L.op == RBP_CONV) {
+            rbp_conv_dt(Q, L, T, G, DT, gs);
+            __syncthreads();
+            const int K = L.kw * L.kh * L.cin;
+            const int ndx = L.step ? 0 : ((L.cin + 15) >> 4) * npb, ndw = ((L.cout + 15) >> 4) * ((K + 15) >> 4);
+            for (int u = wave; u < ndx + ndw; u += nw) {
+                if (u < ndx) rbp_conv_dx(Q, L, DT, G, u);
+                else rbp_conv_dw(Q, L, T, DT, gs, u - ndx);
+            }
+        } else if (L.op == RBP_DENSE) {
+            for (int o = tid; o < L.cout; o += nt) {
+                const float dz = bp_dz(L.act, G[L.y + o], T[L.y + o]);
+                DT[o] = dz;
+                gs[L.b_off + o] += dz;
+            }
+            __syncthreads();
+            const float* W = Q.flat + L.w_off;
+            for (int e = tid; e < L.cout * L.cin; e += nt) {
+                const int i = e / L.cout, o = e - i * L.cout;
+                gs[L.w_off + e] += DT[o] * T[L.x + i];
+            }
+            if (!L.step)
+                for (int i = tid; i < L.cin; i += nt) {
+                    float s = 0.0f;
+                    for (int o = 0; o < L.cout; ++o) s = fmaf(W[o + (size_t)L.cout * i], DT[o], s);
+                    G[L.x + i] += s;
+                }
+        } else {                                              // ∂(2h)/∂h
+            for (int f = tid; f < L.cin; f += nt) G[L.x + f] += 2.0f * G[L.y + f];
+        }
+        __syncthreads();
+    }
+}
+
+// Σ over samples (ascending) + 2θ, and Σθ² of each chunk (f64, fixed tree)
+extern "C" __global__ __launch_bounds__(256) void mz_rbp_reduce(RbpReduceParams R) {
+    __shared__ double red[256];
+    const int tid = threadIdx.x, s0 = R.chunk_start[blockIdx.x], s1 = R.chunk_start[blockIdx.x + 1];
+    double q = 0.0;
+    for (int i = s0 + tid; i < s1; i += 256) {
+        float s = 0.0f;
+        for (int b = 0; b < R.B; ++b) s += R.gsam[(size_t)b * R.nflat + i];
+        const float th = R.flat[i];
+        R.out[i] = s + 2.0f * th;
+        q += (double)th * (double)th;
+    }
+    red[tid] = q;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) red[tid] += red[tid + o];
+        __syncthreads();
+    }
+    if (tid == 0) R.sq[blockIdx.x] = red[0];
+}

@@ -94,3 +94,44 @@ struct BpFoldParams {
     float* losses;                        // {value, reward, policy, Σθ² repr, pred, dyn}
     const double* sq; int job0[4];        // mz_bp_dw's per-job Σθ²; jobs [job0[n], job0[n+1]) are net n's
 };
+
+// ---- the corrected learner for the ResNet nets (mz_rbp_sample / mz_rbp_reduce)
+// One workgroup per sample: the unroll's list of applications on that sample's
+// arena in HBM (conv tensors [channel][position], f = p + P·c, the Flux.flatten
+// order; dense vectors [feature]), the heads, then the list in reverse.  Convs
+// run as 16x16 f32 MFMA blocks (rows = output channels, columns = board
+// positions; the operand of a k×k conv is gathered through the kernel taps,
+// Flux's flipped cross-correlation, zero off the board); BatchNorm is the
+// test-mode affine γ·(t/√(1+ε)) + β; a block's second conv adds the saved
+// input before its relu.  Each sample accumulates its own parameter gradient
+// (the backward's dW, db, dβ, dγ) in gsam[b]; mz_rbp_reduce sums the samples
+// in ascending order and adds 2θ.
+enum { RBP_CONV = 0, RBP_DENSE = 1, RBP_CONCAT = 2 };
+
+struct RbpApp {
+    int op;
+    int w_off, b_off, bn_off;   // flat offsets; bn_off: β at bn_off, γ at bn_off + cout (-1: no BatchNorm)
+    int cin, cout, kw, kh, act; // conv: channels and kernel; dense: in, out
+    int x, y, z, res;           // arena offsets: input, output (after the activation), the conv's t = Wx + b
+                                // (BatchNorm layers), the residual input (-1: none)
+    int step;                   // concat: action column; conv / dense: 1 = no input gradient (the observation)
+};
+
+struct RbpParams {
+    int B, K, A, H, P, Wb, obs_feat, arena, n_app, n_head, obs_t, intermediate_rewards, nflat, dt_floats;
+    const RbpApp* apps; const BpHead* heads;
+    float* act; float* grad; float* dt;   // [B][arena] activations / their gradients, [B][dt_floats] scratch
+    float* gsam;                          // [B][nflat] per-sample parameter gradients
+    const float* flat;
+    const float* obs; const float* actions; const float* tv; const float* tr; const float* tp;
+    const float* gscale; const float* weights;
+    float* terms; float* pv; float* pp; float* pr;
+};
+
+struct RbpReduceParams {
+    int B, nflat, chunk;
+    const float* gsam; const float* flat;
+    float* out;                           // Flux-order gradient (data term + 2θ)
+    double* sq;                           // [blocks]: Σθ² of each chunk (no chunk straddles two nets)
+    const int* chunk_start;               // [blocks + 1]
+};

@@ -43,6 +43,8 @@ extern "C" __global__ void mz_runroll_chain(RUnrollParams U);
 extern "C" __global__ void mz_bp_tile(BpParams Q);
 extern "C" __global__ void mz_bp_tile_lv(BpParams Q);
 extern "C" __global__ void mz_bp_dw(BpDwParams Q);
+extern "C" __global__ void mz_rbp_sample(RbpParams Q);
+extern "C" __global__ void mz_rbp_reduce(RbpReduceParams R);
 extern "C" __global__ void mz_bp_fold(BpFoldParams Q);
 extern "C" __global__ void mz_runroll_pred(RUnrollParams U);
 extern "C" __global__ void mz_runroll_pred_n(RUnrollParams U);
@@ -281,6 +283,13 @@ struct mz_handle {
     // corrected-gradient learner (mz_backprop.hip): the unrolled graph and its arenas
     int learn_mode = MZ_LEARN_REF_SEMANTICS;
     bool bp_built = false;
+    // the corrected learner for the ResNet nets (mz_rbp_sample / mz_rbp_reduce)
+    bool rbp_built = false;
+    int rbp_n_app = 0, rbp_n_head = 0, rbp_arena = 0, rbp_obs_t = 0, rbp_dt = 0, rbp_n_chunk = 0, rbp_cap = 0;
+    int rbp_job0[4] = {0, 0, 0, 0};
+    RbpApp* d_rbp_apps = nullptr; BpHead* d_rbp_heads = nullptr; int* d_rbp_chunks = nullptr;
+    float* d_rbp_act = nullptr; float* d_rbp_grad = nullptr; float* d_rbp_dt = nullptr; float* d_rbp_gsam = nullptr;
+    float* d_rbp_terms = nullptr; double* d_rbp_sq = nullptr;
     int bp_n_app = 0, bp_n_head = 0, bp_n_job = 0, bp_tile_floats = 0, bp_obs_t = 0, bp_tiles_cap = 0;
     BpApp* d_bp_apps = nullptr; BpHead* d_bp_heads = nullptr; BpLayer* d_bp_layers = nullptr;
     BpUse* d_bp_uses = nullptr; BpJob* d_bp_jobs = nullptr;
@@ -1993,10 +2002,10 @@ static int small_unroll_params(mz_handle* h, const mz_batch* b, int ti, const Rp
 // forward unroll + losses + ∇ = 2θ into grad_dev (device batch pointers)
 int mz_learner_grad_dev(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, void* stream) {
     if (!h || !b) return -2;
-    if (h->kind == 1) return rlearner_grad(h, b, grad_dev, losses_dev, stream);
     if (b->batch_size < 1) return fail(h, "batch_size must be >= 1");
     if (h->learn_mode == MZ_LEARN_CORRECTED)
         return bp_grad(h, b, grad_dev, losses_dev, stream ? (hipStream_t)stream : h->stream);
+    if (h->kind == 1) return rlearner_grad(h, b, grad_dev, losses_dev, stream);
     if (ensure_batch(h, b->batch_size)) return -1;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     if (fc_unroll(h, b, st, nullptr)) return -1;
@@ -2226,8 +2235,119 @@ static int build_bp(mz_handle* h) {
     return 0;
 }
 
+// ---- the corrected learner for the ResNet nets (mz_backprop.hip mz_rbp_*):
+// the same unrolled graph as build_bp, on the layers of rn_specs (convs with
+// BatchNorm and residual blocks, the heads' 1x1 convs, Dense layers), one
+// arena per sample: conv tensors [channel][position], dense vectors.
+static int build_rbp(mz_handle* h) {
+    const int K = h->conf.num_unroll_steps, P = h->plane, H = h->H;
+    std::vector<RbpApp> apps;
+    std::vector<BpHead> heads;
+    int off = 0, dtf = 0;
+    auto tensor = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
+    const int obs_t = tensor(h->rin_feat);
+    std::vector<RSpec> sp[3];
+    size_t np[3];
+    for (int n = 0; n < 3; ++n) sp[n] = rn_specs(h->rconf, h->rhp, n, &np[n]);
+    auto chain = [&](int net, int ch, int x, bool first_obs) {
+        int saved = -1;
+        for (const RSpec& r : sp[net]) {
+            if (r.chain != ch) continue;
+            RbpApp a{};
+            a.op = r.conv ? RBP_CONV : RBP_DENSE;
+            a.w_off = (int)(h->flat_off[net] + r.woff); a.b_off = (int)(h->flat_off[net] + r.boff);
+            a.bn_off = r.conv && r.bn ? (int)(h->flat_off[net] + r.bnoff) : -1;
+            a.cin = r.cin; a.cout = r.cout; a.kw = r.kw; a.kh = r.kh; a.act = r.act;
+            a.x = x; a.y = tensor(r.conv ? r.cout * P : r.cout);
+            a.z = a.bn_off >= 0 ? tensor(r.cout * P) : -1;
+            a.res = r.res_add ? saved : -1;
+            if (r.res_save) saved = x;
+            a.step = first_obs ? 1 : 0;
+            first_obs = false;
+            dtf = std::max(dtf, r.conv ? r.cout * P : r.cout);
+            apps.push_back(a);
+            x = a.y;
+        }
+        return x;
+    };
+    std::vector<int> hs(K + 1, -1);
+    hs[0] = chain(MZ_NET_REPR, 0, obs_t, true);                                 // :347
+    for (int k = 1; k <= K; ++k) {                                              // :355-362
+        RbpApp c{};
+        c.op = RBP_CONCAT; c.cin = H; c.cout = H + P; c.x = hs[k - 1]; c.y = tensor(c.cout); c.step = k - 1;
+        c.bn_off = -1; c.z = -1; c.res = -1;
+        apps.push_back(c);
+        const int t = chain(MZ_NET_DYN, 0, c.y, false);
+        if (k < K) hs[k] = chain(MZ_NET_DYN, 1, t, false);
+        if (h->conf.intermediate_rewards) heads.push_back(BpHead{BP_HEAD_R, chain(MZ_NET_DYN, 2, t, false), k});
+    }
+    for (int k = 0; k <= K; ++k) {                                              // :351, :356 (Q10)
+        const int t = chain(MZ_NET_PRED, 0, hs[k <= 1 ? 0 : k - 1], false);
+        heads.push_back(BpHead{BP_HEAD_V, chain(MZ_NET_PRED, 1, t, false), k});
+        heads.push_back(BpHead{BP_HEAD_P, chain(MZ_NET_PRED, 2, t, false), k});
+    }
+    // the reduction's chunks: 4096 parameters, none straddling two nets (Σθ² per net, mz_bp_fold)
+    std::vector<int> chunks;
+    for (int n = 0; n < 3; ++n) {
+        h->rbp_job0[n] = (int)chunks.size();
+        for (size_t i = 0; i < np[n]; i += 4096) chunks.push_back((int)(h->flat_off[n] + i));
+    }
+    h->rbp_job0[3] = (int)chunks.size();
+    chunks.push_back((int)h->nflat);
+    auto up = [&](auto** d, const auto& v) -> int {
+        MZ_TRY(h, dalloc(h, d, v.size()));
+        MZ_TRY(h, hipMemcpy(*d, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice));
+        return 0;
+    };
+    if (up(&h->d_rbp_apps, apps) || up(&h->d_rbp_heads, heads) || up(&h->d_rbp_chunks, chunks)) return -1;
+    MZ_TRY(h, dalloc(h, &h->d_rbp_sq, chunks.size()));
+    h->rbp_n_app = (int)apps.size(); h->rbp_n_head = (int)heads.size(); h->rbp_n_chunk = (int)chunks.size() - 1;
+    h->rbp_arena = off; h->rbp_obs_t = obs_t; h->rbp_dt = (dtf + 3) & ~3;
+    h->rbp_built = true;
+    return 0;
+}
+
+static int rbp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, hipStream_t st) {
+    const int B = b->batch_size, K = h->conf.num_unroll_steps;
+    if (!h->rbp_built && build_rbp(h)) return -1;
+    if (ensure_batch(h, B)) return -1;
+    if (B > h->rbp_cap) {
+        MZ_TRY(h, dalloc(h, &h->d_rbp_act, (size_t)B * h->rbp_arena));
+        MZ_TRY(h, dalloc(h, &h->d_rbp_grad, (size_t)B * h->rbp_arena));
+        MZ_TRY(h, dalloc(h, &h->d_rbp_dt, (size_t)B * h->rbp_dt));
+        MZ_TRY(h, dalloc(h, &h->d_rbp_gsam, (size_t)B * h->nflat));
+        MZ_TRY(h, dalloc(h, &h->d_rbp_terms, (size_t)B * (K + 1) * 3));
+        h->rbp_cap = B;
+    }
+    RbpParams Q;
+    Q.B = B; Q.K = K; Q.A = h->A; Q.H = h->H; Q.P = h->plane; Q.Wb = h->rconf.observation_shape[0];
+    Q.obs_feat = h->rin_feat; Q.arena = h->rbp_arena; Q.n_app = h->rbp_n_app; Q.n_head = h->rbp_n_head;
+    Q.obs_t = h->rbp_obs_t; Q.intermediate_rewards = h->conf.intermediate_rewards; Q.nflat = (int)h->nflat;
+    Q.dt_floats = h->rbp_dt;
+    Q.apps = h->d_rbp_apps; Q.heads = h->d_rbp_heads;
+    Q.act = h->d_rbp_act; Q.grad = h->d_rbp_grad; Q.dt = h->d_rbp_dt; Q.gsam = h->d_rbp_gsam; Q.flat = h->d_flat;
+    Q.obs = b->observation; Q.actions = b->actions; Q.tv = b->target_values; Q.tr = b->target_rewards;
+    Q.tp = b->target_policies; Q.gscale = b->gradient_scale; Q.weights = b->weights; Q.terms = h->d_rbp_terms;
+    Q.pv = h->d_pv; Q.pp = h->d_pp; Q.pr = h->d_pr;
+    hipLaunchKernelGGL(mz_rbp_sample, dim3(B), dim3(256), 0, st, Q);
+    RbpReduceParams R;
+    R.B = B; R.nflat = (int)h->nflat; R.chunk = 4096; R.gsam = h->d_rbp_gsam; R.flat = h->d_flat;
+    R.out = grad_dev ? grad_dev : h->d_grad; R.sq = h->d_rbp_sq; R.chunk_start = h->d_rbp_chunks;
+    hipLaunchKernelGGL(mz_rbp_reduce, dim3(h->rbp_n_chunk), dim3(256), 0, st, R);
+    BpFoldParams F;
+    F.B = B; F.K = K; F.terms = h->d_rbp_terms; F.gscale = b->gradient_scale; F.weights = b->weights;
+    F.flat = h->d_flat; F.netoff = h->d_netoff; F.losses = losses_dev ? losses_dev : h->d_loss;
+    F.sq = h->d_rbp_sq;
+    for (int n = 0; n < 4; ++n) F.job0[n] = h->rbp_job0[n];
+    hipLaunchKernelGGL(mz_bp_fold, dim3(4), dim3(256), 0, st, F);
+    MZ_TRY(h, hipGetLastError());
+    h->last_lvariant = "mz_rbp_sample+mz_rbp_reduce";
+    return 0;
+}
+
 // corrected step: gradient (data term + 2θ) into grad_dev, losses, read-outs
 static int bp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, hipStream_t st) {
+    if (h->kind == 1) return rbp_grad(h, b, grad_dev, losses_dev, st);
     const int B = b->batch_size, K = h->conf.num_unroll_steps;
     if (!h->bp_built && build_bp(h)) return -1;
     if (ensure_batch(h, B)) return -1;
@@ -2274,7 +2394,8 @@ static int bp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* loss
 int mz_learner_set_mode(mz_handle* h, int mode) {
     if (!h) return -2;
     if (mode != MZ_LEARN_REF_SEMANTICS && mode != MZ_LEARN_CORRECTED) return fail(h, "unknown learner mode");
-    if (mode == MZ_LEARN_CORRECTED && h->kind != 0) return fail(h, "the corrected learner supports the FC nets");
+    if (mode == MZ_LEARN_CORRECTED && h->kind == 1 && h->ds)
+        return fail(h, "the corrected learner does not backpropagate through the downsampler (ResNetHP.downsample)");
     if (mode == MZ_LEARN_CORRECTED && h->hp.use_batch_norm)
         return fail(h, "the corrected learner does not backpropagate through BatchNorm FC layers");
     h->learn_mode = mode;
@@ -2836,14 +2957,6 @@ static int learner_sampled(mz_handle* h, int32_t B, uint32_t step, float* grad_d
     if (ensure_batch(h, B)) return -1;
     if (pf && ensure_pf(h, B)) return -1;
     h->rs_last_B = B;
-    if (h->kind == 1) {                             // ResNet: sample, then the network unroll
-        hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, Q);
-        MZ_TRY(h, hipGetLastError());
-        if (per_norm(h, B, st)) return -1;
-        // one GPU: ADAM fused into the loss / Σθ² kernel (as the FC path)
-        if (rlearner_grad(h, &b, train ? nullptr : grad_dev, losses_dev, st, train, eta)) return -1;
-        return per_update(h, B, st);                               // Learning.jl:400-404
-    }
     if (h->learn_mode == MZ_LEARN_CORRECTED) {     // sample, backprop, (ADAM)
         hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, Q);
         MZ_TRY(h, hipGetLastError());
@@ -2851,6 +2964,14 @@ static int learner_sampled(mz_handle* h, int32_t B, uint32_t step, float* grad_d
         if (bp_grad(h, &b, train ? nullptr : grad_dev, losses_dev, st)) return -1;
         if (per_update(h, B, st)) return -1;                       // Learning.jl:400-404
         return train ? mz_learner_apply_dev(h, nullptr, 1.0f, eta, st) : 0;
+    }
+    if (h->kind == 1) {                             // ResNet: sample, then the network unroll
+        hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, Q);
+        MZ_TRY(h, hipGetLastError());
+        if (per_norm(h, B, st)) return -1;
+        // one GPU: ADAM fused into the loss / Σθ² kernel (as the FC path)
+        if (rlearner_grad(h, &b, train ? nullptr : grad_dev, losses_dev, st, train, eta)) return -1;
+        return per_update(h, B, st);                               // Learning.jl:400-404
     }
     if (fused) {
         // one launch: unroll + losses ‖ Σθ² + ADAM into the second image set, then swap the sets;

@@ -1,10 +1,13 @@
-"""The corrected-gradient learner (MZ_LEARN_CORRECTED: backpropagation
-through the unroll on MFMA, mz_backprop.hip) against an independent torch
-autograd reference (tests/torch_learner_ref.py, float64), at the 1e-5
-tolerance of north_star: the data gradient of every net relative to its
-largest entry, the read-outs and the losses.  Reference loss:
-src/Learning.jl:261-288 (differentiated, unlike the reference's pullbacks,
-quirk Q11), unroll :347-370."""
+"""The corrected-gradient learner on the ResNet nets (MZ_LEARN_CORRECTED;
+mz_backprop.hip mz_rbp_sample / mz_rbp_reduce: backpropagation through
+convolutions, test-mode BatchNorm, residual blocks and the Dense heads of the
+K-step unroll on f32 MFMA) against the independent torch autograd reference
+(tests/torch_learner_ref.py, float64) at the 1e-5 tolerance of north_star:
+every net's data gradient relative to its largest entry, the losses and the
+read-outs.  TicTacToe ResNet (configs[2]'s nets, 3x3 kernels in the
+representation) and Connect4 ResNet-8 (configs[3]).  Reference:
+src/Learning.jl:148-255 (the nets, Q12), :261-288 (the loss, differentiated
+unlike the reference's pullbacks, Q11), :347-370 (the unroll)."""
 import dataclasses
 
 import numpy as np
@@ -13,6 +16,13 @@ import pytest
 from torch_learner_ref import corrected_loss_and_grads
 
 pytestmark = pytest.mark.gpu
+
+
+def _lively(conf, hyper, seed):
+    """init_nets with β ~ N(0, 0.1), γ ~ U(0.5, 1.5), biases ~ N(0, 0.1)."""
+    from test_resnet_oracle import _perturb_bn
+    from muzero_jl_amd.networks import init_nets
+    return _perturb_bn(conf, hyper, init_nets(conf, hyper, seed=seed), seed=seed + 1)
 
 
 def _batch(B, K, A, feat, rng):
@@ -25,20 +35,25 @@ def _batch(B, K, A, feat, rng):
                 gradient_scale=rng.integers(1, max(K, 1) + 1, B).astype(np.float32))
 
 
-@pytest.mark.parametrize("B,K,ir,per", [(32, 5, False, False), (20, 3, True, True), (40, 5, True, False),
-                                        (7, 0, False, False)])
-def test_corrected_gradient_matches_torch(ttt, B, K, ir, per):
+@pytest.mark.parametrize("game,B,K,ir,per", [("ttt", 12, 3, True, False), ("ttt", 7, 0, False, True),
+                                             ("c4", 4, 2, True, True)])
+def test_corrected_resnet_gradient_matches_torch(ttt, game, B, K, ir, per):
     import torch
     from muzero_jl_amd import abi
-    from muzero_jl_amd.networks import init_nets
-    conf = dataclasses.replace(ttt.conf, batch_size=B, num_unroll_steps=K, intermediate_rewards=ir)
-    nets = [n * np.float32(3.0) for n in init_nets(conf, ttt.hyper, seed=B + K)]   # livelier activations
-    eng = abi.Engine(conf, ttt.hyper, device=0, max_games=8, rng_seed=1)
+    from muzero_jl_amd.games import connect4 as c4
+    mod = ttt if game == "ttt" else c4
+    conf = dataclasses.replace(mod.conf, batch_size=B, num_unroll_steps=K, intermediate_rewards=ir)
+    hyper = mod.resnet_hyper
+    nets = _lively(conf, hyper, B + K)
+    eng = abi.Engine(conf, hyper, device=0, max_games=8, rng_seed=1)
     for n, w in enumerate(nets):
         eng.set_weights(n, w)
     eng.learner_set_mode(abi.LEARN_CORRECTED)
+    A = len(conf.action_space)
+    feat = int(np.prod(conf.observation_shape)) * (conf.stacked_observations + 1) + \
+        conf.observation_shape[0] * conf.observation_shape[1] * conf.stacked_observations
     rng = np.random.default_rng(B)
-    batch = _batch(B, K, 9, 63, rng)
+    batch = _batch(B, K, A, feat, rng)
     wts = (rng.random(B).astype(np.float32) * 0.9 + 0.1) if per else None
     dev = [torch.from_numpy(np.ascontiguousarray(batch[k])).cuda() for k in
            ("observation", "actions", "target_values", "target_rewards", "target_policies", "gradient_scale")]
@@ -48,7 +63,7 @@ def test_corrected_gradient_matches_torch(ttt, B, K, ir, per):
     eng.learner_grad_dev([t.data_ptr() if t is not None else None for t in dev], B, grad.data_ptr(),
                          losses.data_ptr())
     eng.sync()
-    ref = corrected_loss_and_grads(conf, ttt.hyper, nets, batch, wts)
+    ref = corrected_loss_and_grads(conf, hyper, nets, batch, wts)
     g = grad.cpu().numpy()
     off = 0
     for n in range(3):
@@ -74,18 +89,19 @@ def test_corrected_gradient_matches_torch(ttt, B, K, ir, per):
     eng.close()
 
 
-def test_corrected_learner_trains_and_matches_apply(ttt):
-    """mz_learner_step in corrected mode = grad_dev + apply (ADAM); the
-    device-sampled fused call runs too; a few steps move the losses."""
+def test_corrected_resnet_learner_steps(ttt):
+    """mz_learner_step in corrected mode = grad_dev + apply (ADAM into the
+    ResNet images), bit for bit; the device-sampled learner runs on a
+    self-play shard; the downsampler (configs[4]) is refused."""
     import torch
     from muzero_jl_amd import abi
     from muzero_jl_amd.config import cos_schedule
+    from muzero_jl_amd.games import atari_synth
     from muzero_jl_amd.networks import init_nets
-    B = 32
+    B = 16
     conf = dataclasses.replace(ttt.conf, batch_size=B, num_iters=4)
-    nets = init_nets(conf, ttt.hyper, seed=3)
-    e1 = abi.Engine(conf, ttt.hyper, device=0, max_games=16, rng_seed=2)
-    e2 = abi.Engine(conf, ttt.hyper, device=0, max_games=16, rng_seed=2)
+    nets = init_nets(conf, ttt.resnet_hyper, seed=3)
+    e1, e2 = (abi.Engine(conf, ttt.resnet_hyper, device=0, max_games=16, rng_seed=2) for _ in range(2))
     for e in (e1, e2):
         for n, w in enumerate(nets):
             e.set_weights(n, w)
@@ -104,49 +120,26 @@ def test_corrected_learner_trains_and_matches_apply(ttt):
         assert np.array_equal(l1, losses.cpu().numpy()[:6])
         for n in range(3):
             assert np.array_equal(e1.get_weights(n), e2.get_weights(n))
-    # the device-sampled learner in corrected mode
+    assert not np.array_equal(e1.get_weights(0), nets[0])
+    # the searches read the updated images: both engines still agree
+    obs = (rng.random((8, 63)) < 0.3).astype(np.float32)
+    legal = np.ones((8, 9), bool)
+    tp = np.ones(8, np.int32)
+    assert all(np.array_equal(a, b) for a, b in zip(e1.mcts_search(obs, legal, tp, rng_step=5),
+                                                    e2.mcts_search(obs, legal, tp, rng_step=5)))
     e1.selfplay_init(abi.ENV_TICTACTOE, 16, 64)
     for m in range(12):
         e1.selfplay_move(m)
     out = torch.zeros(8, dtype=torch.float32, device="cuda")
-    for t in range(4, 8):
+    for t in range(4, 7):
         e1.learner_train_dev(B, t, cos_schedule(t), out.data_ptr())
     e1.sync()
     assert np.all(np.isfinite(out.cpu().numpy()[:6]))
     e1.close(); e2.close()
-
-
-@pytest.mark.parametrize("B,K,ir", [(32, 5, True), (40, 3, False)])
-def test_level_schedule_equals_sequential_tile_kernel(ttt, B, K, ir, monkeypatch):
-    """mz_bp_tile_lv (the unroll's applications grouped into dependency
-    levels, one barrier per level) against mz_bp_tile (one application per
-    barrier, MZ_BP_SEQ=1): gradient, losses and read-outs identical bit for bit
-    — the level schedule keeps every accumulation into a shared input gradient
-    in the sequential kernel's order."""
-    import torch
-    from muzero_jl_amd import abi
-    from muzero_jl_amd.networks import init_nets
-    conf = dataclasses.replace(ttt.conf, batch_size=B, num_unroll_steps=K, intermediate_rewards=ir)
-    nets = [n * np.float32(3.0) for n in init_nets(conf, ttt.hyper, seed=5)]
-    eng = abi.Engine(conf, ttt.hyper, device=0, max_games=8, rng_seed=1)
-    for n, w in enumerate(nets):
-        eng.set_weights(n, w)
-    eng.learner_set_mode(abi.LEARN_CORRECTED)
-    batch = _batch(B, K, 9, 63, np.random.default_rng(B + 1))
-    dev = [torch.from_numpy(np.ascontiguousarray(batch[k])).cuda() for k in
-           ("observation", "actions", "target_values", "target_rewards", "target_policies", "gradient_scale")]
-    out = []
-    for seq in (False, True):
-        if seq:
-            monkeypatch.setenv("MZ_BP_SEQ", "1")
-        grad = torch.zeros(eng.grad_count(), dtype=torch.float32, device="cuda")
-        losses = torch.zeros(8, dtype=torch.float32, device="cuda")
-        eng.learner_grad_dev([d.data_ptr() for d in dev] + [None], B, grad.data_ptr(), losses.data_ptr())
-        eng.sync()
-        out.append((grad.cpu().numpy(), losses.cpu().numpy()[:6], [x.copy() for x in eng.debug_unroll(B)]))
-    (g0, l0, u0), (g1, l1, u1) = out
-    assert np.array_equal(g0, g1), "gradients differ between the level and sequential schedules"
-    assert np.array_equal(l0, l1)
-    for a, b in zip(u0, u1):
-        assert np.array_equal(a, b)
-    eng.close()
+    ac = dataclasses.replace(atari_synth.conf, num_iters=4)
+    with pytest.raises(abi.MzError, match="downsampler"):
+        r = abi.Engine(ac, atari_synth.resnet_hyper, device=0, max_games=2, rng_seed=1)
+        try:
+            r.learner_set_mode(abi.LEARN_CORRECTED)
+        finally:
+            r.close()

@@ -1,5 +1,6 @@
 """Independent torch autograd reference of the corrected-gradient learner
 (MZ_LEARN_CORRECTED; include/mz.h): the FC nets of Learning.jl:87-142 built
+(or the ResNet nets of Learning.jl:148-255, Q12's intended architecture)
 from the Flux-order flat vectors, the unroll of Learning.jl:347-370 (Q10
 alignment: predictions on h0, h0, h1 .. h_{K-1}; make_dynamics_input's 2h and
 a/|A| plane, :293-304) and the per-sample-mean loss
@@ -11,10 +12,8 @@ import numpy as np
 import torch
 
 
-def corrected_loss_and_grads(conf, hyper, nets, batch, weights=None, dtype=torch.float64):
+def _fc_chain(conf, hyper, nets, params):
     from muzero_jl_amd.networks import unflatten
-    K, A = conf.num_unroll_steps, len(conf.action_space)
-    params = [torch.tensor(np.asarray(f), dtype=dtype, requires_grad=True) for f in nets]
 
     def layers(net):
         # the same slicing as networks.unflatten, on the autograd leaves
@@ -37,6 +36,75 @@ def corrected_loss_and_grads(conf, hyper, nets, batch, weights=None, dtype=torch
             x = x @ W.T + b
             x = torch.relu(x) if act == 1 else torch.tanh(x) if act == 2 else x
         return x
+    return chain
+
+
+def _resnet_chain(conf, hyper, params):
+    """The ResNet nets (networks.resnet_specs, Flux-order slices of the leaves):
+    convolution = cross-correlation with the kernel flipped, "same" padding,
+    BatchNorm in test mode (μ = 0, σ² = 1, ε = 1e-5), residual blocks, the
+    column-major (W,H,C) flatten.  Without the downsampler."""
+    import torch.nn.functional as F
+    from muzero_jl_amd.networks import resnet_board, resnet_specs
+    Wb, Hb = resnet_board(conf, hyper)
+
+    def ops(net):
+        out, off = [], 0
+        p = params[net]
+        for op in resnet_specs(conf, hyper, net):
+            op = dict(op)
+            assert op["kind"] != "pool", "no downsampler"
+            if op["kind"] == "dense":
+                i, o = op["cin"], op["cout"]
+                op["w"] = p[off: off + i * o].reshape(i, o).T
+                off += i * o
+            else:
+                kw, kh, ci, co = op["kw"], op["kh"], op["cin"], op["cout"]
+                op["w"] = torch.flip(p[off: off + kw * kh * ci * co].reshape(co, ci, kh, kw), dims=[2, 3])
+                off += kw * kh * ci * co
+            op["b"] = p[off: off + op["cout"]]
+            off += op["cout"]
+            if op["kind"] == "conv" and op["bn"]:
+                op["beta"] = p[off: off + op["cout"]]
+                op["gamma"] = p[off + op["cout"]: off + 2 * op["cout"]]
+                off += 2 * op["cout"]
+            out.append(op)
+        return out
+
+    O = [ops(n) for n in range(3)]
+
+    def act(t, a):
+        return torch.relu(t) if a == 1 else torch.tanh(t) if a == 2 else t
+
+    def chain(net, ch, t):
+        res = None
+        for op in O[net]:
+            if op["chain"] != ch:
+                continue
+            if op["kind"] == "conv":
+                if t.dim() == 2:                       # (n, W*H*C) column-major -> (n, C, H, W)
+                    t = t.reshape(t.shape[0], op["cin"], Hb, Wb)
+                if op["res_save"]:
+                    res = t
+                y = F.conv2d(t, op["w"], op["b"], padding=(op["kh"] // 2, op["kw"] // 2))
+                if op["bn"]:
+                    y = F.batch_norm(y, torch.zeros(op["cout"], dtype=y.dtype), torch.ones(op["cout"], dtype=y.dtype),
+                                     op["gamma"], op["beta"], training=False, eps=1e-5)
+                if op["res_add"]:
+                    y = y + res
+                t = act(y, op["act"])
+            else:
+                t = act(t.reshape(t.shape[0], -1) @ op["w"].T + op["b"], op["act"])
+        return t.reshape(t.shape[0], -1) if t.dim() == 4 else t
+    return chain
+
+
+def corrected_loss_and_grads(conf, hyper, nets, batch, weights=None, dtype=torch.float64):
+    from muzero_jl_amd.config import ResNetHP
+    K, A = conf.num_unroll_steps, len(conf.action_space)
+    params = [torch.tensor(np.asarray(f), dtype=dtype, requires_grad=True) for f in nets]
+    chain = (_resnet_chain(conf, hyper, params) if isinstance(hyper, ResNetHP)
+             else _fc_chain(conf, hyper, nets, params))
 
     obs = torch.tensor(batch["observation"], dtype=dtype)
     acts = torch.tensor(batch["actions"], dtype=dtype)
