@@ -484,29 +484,83 @@ extern "C" __global__ __launch_bounds__(256) void mz_bp_fold(BpFoldParams Q) {
 
 // ============================================================================
 // The corrected learner for the ResNet nets (mz_backprop_params.h RbpApp):
-// one 256-thread workgroup per sample, its arena T (activations), G (their
-// gradients) and DT (the current application's ∂L/∂t) in HBM.
+// one 256-thread workgroup per sample, its arena T (activations) and G (their
+// gradients) in HBM; the current application's input and ∂L/∂t staged in LDS.
 #define RBP_THREADS 256
 
 // im2col operand of a conv, input element (k, p) for k = i + kw·j + kw·kh·c:
 // x[c] at (px, py) = (p mod W + (kw−1−i) − kw/2, p div W + (kh−1−j) − kh/2),
 // zero off the board (Flux's flipped kernel, "same" padding)
+// n / d for 0 <= n < 2^20 and a small wave-uniform d, by an f32 reciprocal
+// (the quotient's fraction is at least 1/d away from the next integer)
+__device__ __forceinline__ int rbp_div(int n, int d, float rd) { return (int)(((float)n + 0.5f) * rd); }
+
 __device__ __forceinline__ float rbp_xhat(const float* X, const RbpApp& L, int P, int Wb, int k, int p) {
     const int kk = L.kw * L.kh;
     if (k >= kk * L.cin || p >= P) return 0.0f;
-    const int c = k / kk, r = k - c * kk, j = r / L.kw, i = r - j * L.kw;
-    const int px = p % Wb + (L.kw - 1 - i) - L.kw / 2, py = p / Wb + (L.kh - 1 - j) - L.kh / 2;
+    if (kk == 1) return X[k * P + p];                        // 1x1 conv
+    const int c = rbp_div(k, kk, 1.0f / (float)kk), r = k - c * kk;
+    const int j = rbp_div(r, L.kw, 1.0f / (float)L.kw), i = r - j * L.kw;
+    const int pyy = rbp_div(p, Wb, 1.0f / (float)Wb);
+    const int px = p - pyy * Wb + (L.kw - 1 - i) - L.kw / 2, py = pyy + (L.kh - 1 - j) - L.kh / 2;
     return px >= 0 && px < Wb && py >= 0 && py < P / Wb ? X[c * P + px + Wb * py] : 0.0f;
 }
 
+// bp_gemm_block with RBP_KC k-steps of operands in flight per chunk (one
+// workgroup per sample leaves the registers for it); the tail chunk's MFMAs
+// stop at K, so short reductions (1x1 convs over 64 channels, dW over the
+// board) run no padded MFMAs
+#define RBP_KC 32
+template <class FA, class FB>
+__device__ __forceinline__ bp_f32x4 rbp_gemm_block(int nk, int kq, FA fa, FB fb) {
+    bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    int k0 = 0;
+    for (; k0 + RBP_KC <= nk; k0 += RBP_KC) {                // full chunks
+        float a[RBP_KC], b[RBP_KC];
+#pragma unroll
+        for (int j = 0; j < RBP_KC; ++j) {
+            const int k = (k0 + j) * 4 + kq;
+            a[j] = fa(k);
+            b[j] = fb(k);
+        }
+#pragma unroll
+        for (int j = 0; j < RBP_KC; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+    }
+#ifdef RBP_TAIL4
+    for (; k0 < nk; k0 += 4) {
+        float a[4], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = (k0 + j) * 4 + kq;
+            a[j] = k0 + j < nk ? fa(k) : 0.0f;
+            b[j] = k0 + j < nk ? fb(k) : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+    }
+#endif
+    if (k0 < nk) {                                            // the tail: one chunk, its loads in flight together
+        float a[RBP_KC], b[RBP_KC];
+#pragma unroll
+        for (int j = 0; j < RBP_KC; ++j) {
+            const int k = (k0 + j) * 4 + kq;
+            a[j] = k0 + j < nk ? fa(k) : 0.0f;
+            b[j] = k0 + j < nk ? fb(k) : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < RBP_KC; ++j)
+            if (k0 + j < nk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+    }
+    return acc;
+}
+
 // forward: output block (16 channels x 16 positions) u of a conv
-__device__ void rbp_conv_fwd(const RbpParams& Q, const RbpApp& L, float* T, int u) {
+__device__ __forceinline__ void rbp_conv_fwd(const RbpParams& Q, const RbpApp& L, const float* X, float* T, int u) {
     const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4, P = Q.P;
     const int npb = (P + 15) >> 4, ob = u / npb, pb = u - ob * npb;
     const int K = L.kw * L.kh * L.cin, co = ob * 16 + m, p = pb * 16 + m;
     const float* W = Q.flat + L.w_off;
-    const float* X = T + L.x;
-    const bp_f32x4 acc = bp_gemm_block((K + 3) >> 2, kq,
+    const bp_f32x4 acc = rbp_gemm_block((K + 3) >> 2, kq,
         [&](int k) { return co < L.cout && k < K ? W[k + (size_t)K * co] : 0.0f; },
         [&](int k) { return rbp_xhat(X, L, P, Q.Wb, k, p); });
     const int pc = pb * 16 + m;
@@ -526,7 +580,7 @@ __device__ void rbp_conv_fwd(const RbpParams& Q, const RbpApp& L, float* T, int 
     }
 }
 
-__device__ void rbp_dense_fwd(const RbpParams& Q, const RbpApp& L, float* T) {
+__device__ __forceinline__ void rbp_dense_fwd(const RbpParams& Q, const RbpApp& L, float* T) {
     const float* W = Q.flat + L.w_off;
     for (int o = threadIdx.x; o < L.cout; o += blockDim.x) {
         float s = 0.0f;
@@ -537,7 +591,7 @@ __device__ void rbp_dense_fwd(const RbpParams& Q, const RbpApp& L, float* T) {
 
 // ∂L/∂t of a conv (t = Wx + b) into DT, the residual input's share of ∂L/∂y,
 // and the per-channel sums: db = Σ dt, dβ = Σ du, dγ = Σ du·t/√(1+ε)
-__device__ void rbp_conv_dt(const RbpParams& Q, const RbpApp& L, const float* T, float* G, float* DT, float* gs) {
+__device__ __forceinline__ void rbp_conv_dt(const RbpParams& Q, const RbpApp& L, const float* T, float* G, float* DT, float* gs) {
     const int P = Q.P;
     for (int o = threadIdx.x; o < L.cout; o += blockDim.x) {
         const bool bn = L.bn_off >= 0;
@@ -558,21 +612,25 @@ __device__ void rbp_conv_dt(const RbpParams& Q, const RbpApp& L, const float* T,
 }
 
 // G[x] += the transposed conv of DT: input block (16 channels x 16 positions) u
-__device__ void rbp_conv_dx(const RbpParams& Q, const RbpApp& L, const float* DT, float* G, int u) {
+__device__ __forceinline__ void rbp_conv_dx(const RbpParams& Q, const RbpApp& L, const float* DT, float* G, int u) {
     const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4, P = Q.P, Wb = Q.Wb;
     const int npb = (P + 15) >> 4, ib = u / npb, pb = u - ib * npb;
     const int kk = L.kw * L.kh, K = kk * L.cin, Kt = kk * L.cout, ci = ib * 16 + m, p = pb * 16 + m;
+    const float rkk = 1.0f / (float)kk, rkw = 1.0f / (float)L.kw;
+    const int py0 = rbp_div(p, Wb, 1.0f / (float)Wb), px0 = p - py0 * Wb;
     const float* W = Q.flat + L.w_off;
-    const bp_f32x4 acc = bp_gemm_block((Kt + 3) >> 2, kq,
+    const bp_f32x4 acc = rbp_gemm_block((Kt + 3) >> 2, kq,
         [&](int k) {
             if (ci >= L.cin || k >= Kt) return 0.0f;
-            const int co = k / kk, tap = k - co * kk;
+            if (kk == 1) return W[ci + (size_t)L.cin * k];
+            const int co = rbp_div(k, kk, rkk), tap = k - co * kk;
             return W[tap + kk * ci + (size_t)K * co];
         },
         [&](int k) {
             if (k >= Kt || p >= P) return 0.0f;
-            const int co = k / kk, tap = k - co * kk, j = tap / L.kw, i = tap - j * L.kw;
-            const int qx = p % Wb - ((L.kw - 1 - i) - L.kw / 2), qy = p / Wb - ((L.kh - 1 - j) - L.kh / 2);
+            if (kk == 1) return DT[k * P + p];
+            const int co = rbp_div(k, kk, rkk), tap = k - co * kk, j = rbp_div(tap, L.kw, rkw), i = tap - j * L.kw;
+            const int qx = px0 - ((L.kw - 1 - i) - L.kw / 2), qy = py0 - ((L.kh - 1 - j) - L.kh / 2);
             return qx >= 0 && qx < Wb && qy >= 0 && qy < P / Wb ? DT[co * P + qx + Wb * qy] : 0.0f;
         });
 #pragma unroll
@@ -583,12 +641,11 @@ __device__ void rbp_conv_dx(const RbpParams& Q, const RbpApp& L, const float* DT
 }
 
 // this sample's dW of a conv, block (16 output channels x 16 k) u: Σ_p dt ⊗ x̂
-__device__ void rbp_conv_dw(const RbpParams& Q, const RbpApp& L, const float* T, const float* DT, float* gs, int u) {
+__device__ __forceinline__ void rbp_conv_dw(const RbpParams& Q, const RbpApp& L, const float* X, const float* DT, float* gs, int u) {
     const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4, P = Q.P;
     const int K = L.kw * L.kh * L.cin, nkb = (K + 15) >> 4, ob = u / nkb, kb = u - ob * nkb;
     const int co = ob * 16 + m, kc = kb * 16 + m;
-    const float* X = T + L.x;
-    const bp_f32x4 acc = bp_gemm_block((P + 3) >> 2, kq,
+    const bp_f32x4 acc = rbp_gemm_block((P + 3) >> 2, kq,
         [&](int p) { return co < L.cout && p < P ? DT[co * P + p] : 0.0f; },
         [&](int p) { return rbp_xhat(X, L, P, Q.Wb, kc, p); });
 #pragma unroll
@@ -599,7 +656,7 @@ __device__ void rbp_conv_dw(const RbpParams& Q, const RbpApp& L, const float* T,
 }
 
 // dL/dy of the heads for sample b (bp_heads for one sample)
-__device__ void rbp_heads(const RbpParams& Q, const float* T, float* G, int b) {
+__device__ __forceinline__ void rbp_heads(const RbpParams& Q, const float* T, float* G, int b) {
     const int K1 = Q.K + 1;
     for (int e = threadIdx.x; e < Q.n_head; e += blockDim.x) {
         const BpHead hd = Q.heads[e];
@@ -637,10 +694,12 @@ __device__ void rbp_heads(const RbpParams& Q, const float* T, float* G, int b) {
 }
 
 extern "C" __global__ __launch_bounds__(RBP_THREADS) void mz_rbp_sample(RbpParams Q) {
+    extern __shared__ __attribute__((aligned(16))) float rbp_lds[];
     const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x, wave = tid >> 6, nw = nt >> 6, K1 = Q.K + 1;
     float* T = Q.act + (size_t)b * Q.arena;
     float* G = Q.grad + (size_t)b * Q.arena;
-    float* DT = Q.dt + (size_t)b * Q.dt_floats;
+    float* DT = rbp_lds;                                      // [dt_floats] ∂L/∂t of the current application
+    float* XS = rbp_lds + Q.dt_floats;                        // [xs_floats] its input, staged
     float* gs = Q.gsam + (size_t)b * Q.nflat;
     for (int e = tid; e < Q.arena; e += nt) G[e] = 0.0f;
     for (int e = tid; e < Q.nflat; e += nt) gs[e] = 0.0f;
@@ -653,8 +712,10 @@ extern "C" __global__ __launch_bounds__(RBP_THREADS) void mz_rbp_sample(RbpParam
     for (int a = 0; a < Q.n_app; ++a) {
         const RbpApp L = Q.apps[a];
         if (L.op == RBP_CONV) {
+            for (int e = tid; e < L.cin * Q.P; e += nt) XS[e] = T[L.x + e];
+            __syncthreads();
             const int units = ((L.cout + 15) >> 4) * npb;
-            for (int u = wave; u < units; u += nw) rbp_conv_fwd(Q, L, T, u);
+            for (int u = wave; u < units; u += nw) rbp_conv_fwd(Q, L, XS, T, u);
         } else if (L.op == RBP_DENSE) {
             rbp_dense_fwd(Q, L, T);
         } else {                                              // make_dynamics_input (:293-304)
@@ -670,12 +731,13 @@ extern "C" __global__ __launch_bounds__(RBP_THREADS) void mz_rbp_sample(RbpParam
         const RbpApp L = Q.apps[a];
         if (L.op == RBP_CONV) {
             rbp_conv_dt(Q, L, T, G, DT, gs);
+            for (int e = tid; e < L.cin * Q.P; e += nt) XS[e] = T[L.x + e];
             __syncthreads();
             const int K = L.kw * L.kh * L.cin;
             const int ndx = L.step ? 0 : ((L.cin + 15) >> 4) * npb, ndw = ((L.cout + 15) >> 4) * ((K + 15) >> 4);
             for (int u = wave; u < ndx + ndw; u += nw) {
                 if (u < ndx) rbp_conv_dx(Q, L, DT, G, u);
-                else rbp_conv_dw(Q, L, T, DT, gs, u - ndx);
+                else rbp_conv_dw(Q, L, XS, DT, gs, u - ndx);
             }
         } else if (L.op == RBP_DENSE) {
             for (int o = tid; o < L.cout; o += nt) {

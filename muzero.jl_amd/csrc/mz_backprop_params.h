@@ -120,7 +120,8 @@ struct RbpApp {
 struct RbpParams {
     int B, K, A, H, P, Wb, obs_feat, arena, n_app, n_head, obs_t, intermediate_rewards, nflat, dt_floats;
     const RbpApp* apps; const BpHead* heads;
-    float* act; float* grad; float* dt;   // [B][arena] activations / their gradients, [B][dt_floats] scratch
+    float* act; float* grad;              // [B][arena] activations / their gradients
+    // LDS: [dt_floats] the application's ∂L/∂t, then its input (the largest conv input)
     float* gsam;                          // [B][nflat] per-sample parameter gradients
     const float* flat;
     const float* obs; const float* actions; const float* tv; const float* tr; const float* tp;

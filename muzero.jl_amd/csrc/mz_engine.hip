@@ -285,10 +285,10 @@ struct mz_handle {
     bool bp_built = false;
     // the corrected learner for the ResNet nets (mz_rbp_sample / mz_rbp_reduce)
     bool rbp_built = false;
-    int rbp_n_app = 0, rbp_n_head = 0, rbp_arena = 0, rbp_obs_t = 0, rbp_dt = 0, rbp_n_chunk = 0, rbp_cap = 0;
+    int rbp_n_app = 0, rbp_n_head = 0, rbp_arena = 0, rbp_obs_t = 0, rbp_dt = 0, rbp_xs = 0, rbp_n_chunk = 0, rbp_cap = 0;
     int rbp_job0[4] = {0, 0, 0, 0};
     RbpApp* d_rbp_apps = nullptr; BpHead* d_rbp_heads = nullptr; int* d_rbp_chunks = nullptr;
-    float* d_rbp_act = nullptr; float* d_rbp_grad = nullptr; float* d_rbp_dt = nullptr; float* d_rbp_gsam = nullptr;
+    float* d_rbp_act = nullptr; float* d_rbp_grad = nullptr; float* d_rbp_gsam = nullptr;
     float* d_rbp_terms = nullptr; double* d_rbp_sq = nullptr;
     int bp_n_app = 0, bp_n_head = 0, bp_n_job = 0, bp_tile_floats = 0, bp_obs_t = 0, bp_tiles_cap = 0;
     BpApp* d_bp_apps = nullptr; BpHead* d_bp_heads = nullptr; BpLayer* d_bp_layers = nullptr;
@@ -2243,7 +2243,7 @@ static int build_rbp(mz_handle* h) {
     const int K = h->conf.num_unroll_steps, P = h->plane, H = h->H;
     std::vector<RbpApp> apps;
     std::vector<BpHead> heads;
-    int off = 0, dtf = 0;
+    int off = 0, dtf = 0, xsf = 0;
     auto tensor = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
     const int obs_t = tensor(h->rin_feat);
     std::vector<RSpec> sp[3];
@@ -2265,6 +2265,7 @@ static int build_rbp(mz_handle* h) {
             a.step = first_obs ? 1 : 0;
             first_obs = false;
             dtf = std::max(dtf, r.conv ? r.cout * P : r.cout);
+            if (r.conv) xsf = std::max(xsf, r.cin * P);
             apps.push_back(a);
             x = a.y;
         }
@@ -2302,7 +2303,8 @@ static int build_rbp(mz_handle* h) {
     if (up(&h->d_rbp_apps, apps) || up(&h->d_rbp_heads, heads) || up(&h->d_rbp_chunks, chunks)) return -1;
     MZ_TRY(h, dalloc(h, &h->d_rbp_sq, chunks.size()));
     h->rbp_n_app = (int)apps.size(); h->rbp_n_head = (int)heads.size(); h->rbp_n_chunk = (int)chunks.size() - 1;
-    h->rbp_arena = off; h->rbp_obs_t = obs_t; h->rbp_dt = (dtf + 3) & ~3;
+    h->rbp_arena = off; h->rbp_obs_t = obs_t; h->rbp_dt = (dtf + 3) & ~3; h->rbp_xs = (xsf + 3) & ~3;
+    if ((size_t)(h->rbp_dt + h->rbp_xs) * 4 > kLdsMax) return fail(h, "corrected learner: a conv's tensors exceed the LDS");
     h->rbp_built = true;
     return 0;
 }
@@ -2314,7 +2316,6 @@ static int rbp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* los
     if (B > h->rbp_cap) {
         MZ_TRY(h, dalloc(h, &h->d_rbp_act, (size_t)B * h->rbp_arena));
         MZ_TRY(h, dalloc(h, &h->d_rbp_grad, (size_t)B * h->rbp_arena));
-        MZ_TRY(h, dalloc(h, &h->d_rbp_dt, (size_t)B * h->rbp_dt));
         MZ_TRY(h, dalloc(h, &h->d_rbp_gsam, (size_t)B * h->nflat));
         MZ_TRY(h, dalloc(h, &h->d_rbp_terms, (size_t)B * (K + 1) * 3));
         h->rbp_cap = B;
@@ -2325,11 +2326,11 @@ static int rbp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* los
     Q.obs_t = h->rbp_obs_t; Q.intermediate_rewards = h->conf.intermediate_rewards; Q.nflat = (int)h->nflat;
     Q.dt_floats = h->rbp_dt;
     Q.apps = h->d_rbp_apps; Q.heads = h->d_rbp_heads;
-    Q.act = h->d_rbp_act; Q.grad = h->d_rbp_grad; Q.dt = h->d_rbp_dt; Q.gsam = h->d_rbp_gsam; Q.flat = h->d_flat;
+    Q.act = h->d_rbp_act; Q.grad = h->d_rbp_grad; Q.gsam = h->d_rbp_gsam; Q.flat = h->d_flat;
     Q.obs = b->observation; Q.actions = b->actions; Q.tv = b->target_values; Q.tr = b->target_rewards;
     Q.tp = b->target_policies; Q.gscale = b->gradient_scale; Q.weights = b->weights; Q.terms = h->d_rbp_terms;
     Q.pv = h->d_pv; Q.pp = h->d_pp; Q.pr = h->d_pr;
-    hipLaunchKernelGGL(mz_rbp_sample, dim3(B), dim3(256), 0, st, Q);
+    hipLaunchKernelGGL(mz_rbp_sample, dim3(B), dim3(256), (size_t)(h->rbp_dt + h->rbp_xs) * 4, st, Q);
     RbpReduceParams R;
     R.B = B; R.nflat = (int)h->nflat; R.chunk = 4096; R.gsam = h->d_rbp_gsam; R.flat = h->d_flat;
     R.out = grad_dev ? grad_dev : h->d_grad; R.sq = h->d_rbp_sq; R.chunk_start = h->d_rbp_chunks;
