@@ -506,10 +506,10 @@ __device__ __forceinline__ float rbp_xhat(const float* X, const RbpApp& L, int P
     return px >= 0 && px < Wb && py >= 0 && py < P / Wb ? X[c * P + px + Wb * py] : 0.0f;
 }
 
-// bp_gemm_block with RBP_KC k-steps of operands in flight per chunk (one
-// workgroup per sample leaves the registers for it); the tail chunk's MFMAs
-// stop at K, so short reductions (1x1 convs over 64 channels, dW over the
-// board) run no padded MFMAs
+// bp_gemm_block with RBP_KC k-steps of operands in flight per full chunk (one
+// workgroup per sample leaves the registers for it) and a tail of four k-steps
+// at a time (measured faster than one predicated chunk: 377 vs 312 steps/s on
+// TicTacToe ResNet, tools/ab_rbp.sh), so short reductions run few padded MFMAs
 #define RBP_KC 32
 template <class FA, class FB>
 __device__ __forceinline__ bp_f32x4 rbp_gemm_block(int nk, int kq, FA fa, FB fb) {
@@ -526,8 +526,7 @@ __device__ __forceinline__ bp_f32x4 rbp_gemm_block(int nk, int kq, FA fa, FB fb)
 #pragma unroll
         for (int j = 0; j < RBP_KC; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
     }
-#ifdef RBP_TAIL4
-    for (; k0 < nk; k0 += 4) {
+    for (; k0 < nk; k0 += 4) {                                // the tail, four k-steps at a time
         float a[4], b[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -537,19 +536,6 @@ __device__ __forceinline__ bp_f32x4 rbp_gemm_block(int nk, int kq, FA fa, FB fb)
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
-    }
-#endif
-    if (k0 < nk) {                                            // the tail: one chunk, its loads in flight together
-        float a[RBP_KC], b[RBP_KC];
-#pragma unroll
-        for (int j = 0; j < RBP_KC; ++j) {
-            const int k = (k0 + j) * 4 + kq;
-            a[j] = k0 + j < nk ? fa(k) : 0.0f;
-            b[j] = k0 + j < nk ? fb(k) : 0.0f;
-        }
-#pragma unroll
-        for (int j = 0; j < RBP_KC; ++j)
-            if (k0 + j < nk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
     }
     return acc;
 }

@@ -517,7 +517,7 @@ extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_search_small4(Sma
 // order; value / reward with their read-out activations — applied by the
 // loss kernel, which visits every (sample, step) pair in parallel.
 template <int T>
-__device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
+__device__ __forceinline__ void unroll_body(const SmallUnrollParams& P, int lb) {
 #ifdef MZ_STAMPS
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long st_last = __builtin_amdgcn_s_memtime();
@@ -530,7 +530,7 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
     float* aval = reinterpret_cast<float*>(rec + (nrec + 1) * SM_REC_INTS);    // [T][K+1] a/|A| per step
     float2* bnl = reinterpret_cast<float2*>(aval + 64);                     // [nrec][slot][64] (γ, β) (P.bn)
     const int tid = threadIdx.x;
-    const int tile0 = blockIdx.x * T;
+    const int tile0 = lb * T;
     // per-thread item of the per-step loops (each has < SM_THREADS items)
     const int o_gl = tid / (A + 2), o_c = tid - o_gl * (A + 2);      // raw outputs: tid < T*(A+2)
     // Every global load of the setup is issued before the weight image (a
@@ -642,12 +642,12 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P) {
     }
 #ifdef MZ_STAMPS
     if (threadIdx.x == 0 && P.stamps)
-        for (int i = 0; i < 8; ++i) P.stamps[blockIdx.x * 8 + i] = st_acc[i];
+        for (int i = 0; i < 8; ++i) P.stamps[lb * 8 + i] = st_acc[i];
 #endif
 }
 
-extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small1(SmallUnrollParams P) { unroll_body<1>(P); }
-extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small2(SmallUnrollParams P) { unroll_body<2>(P); }
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small1(SmallUnrollParams P) { unroll_body<1>(P, blockIdx.x); }
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small2(SmallUnrollParams P) { unroll_body<2>(P, blockIdx.x); }
 
 // One learner iteration in one launch (LearnParams): unroll (+ get_batch) and
 // each tile's loss terms ‖ Σθ² + ADAM into the second image set; last block
@@ -665,28 +665,34 @@ __device__ __forceinline__ void learn_body(const SmallUnrollParams& P, const Lea
 #ifdef MZ_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
 #endif
-    if ((int)blockIdx.x < L.nU) {
-        unroll_body<T>(P);
+    // logical block: with L.xcd the unroll workgroups are the physical blocks
+    // 0, 8, 16, .. (one XCD under round-robin dispatch: their weight image is
+    // fetched into one L2), the other roles take the remaining blocks in order
+    const int pb = (int)blockIdx.x;
+    const int lb = L.xcd ? ((pb & 7) == 0 ? pb >> 3 : L.nU + pb - (pb >> 3) - 1) : pb;
+    if (lb < L.nU) {
+        unroll_body<T>(P, lb);
 #ifdef MZ_STAMPS
         const unsigned long long t_unroll = __builtin_amdgcn_s_memtime();
 #endif
         __syncthreads();                               // the tile's raw outputs -> its loss groups
         const int g16 = tid >> 4, a = tid & 15, gl = g16 / K1, k = g16 - gl * K1;
-        const int b = blockIdx.x * T + gl;
+        const int b = lb * T + gl;
         if (gl < T && b < P.B)
             lg_step_terms<16>(b * K1 + k, a, P.A, P.v_act, P.r_act, P.pv, P.pp, P.pr, L.tv, L.tp, vsq, cet,
                               stg + (tid & ~15));
 #ifdef MZ_STAMPS   // slot 6: unroll start -> end, slot 7: loss terms (wave 0)
         if (tid == 0 && P.stamps) {
-            P.stamps[blockIdx.x * 8 + 6] = t_unroll - t_start;
-            P.stamps[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memtime() - t_unroll;
+            P.stamps[lb * 8 + 6] = t_unroll - t_start;
+            P.stamps[lb * 8 + 7] = __builtin_amdgcn_s_memtime() - t_unroll;
         }
 #endif
-    } else if ((int)blockIdx.x >= L.nU + LEARN_L2_GROUPS) {
-        // the next step's get_batch into the other batch set (read by the next launch)
-        const int b = ((int)blockIdx.x - L.nU - LEARN_L2_GROUPS) * (SM_THREADS / 64) + (tid >> 6);
-        if (b < L.pfq.B) rp_sample_one(L.pfq, b, tid & 63);
-        if ((int)blockIdx.x == L.nU + LEARN_L2_GROUPS && tid == 0) {
+    } else if (lb >= L.nU + LEARN_L2_GROUPS) {
+        // the next step's get_batch into the other batch set (read by the next launch;
+        // blocks past the last sample are idle)
+        const int b = (lb - L.nU - LEARN_L2_GROUPS) * (SM_THREADS / 64) + (tid >> 6);
+        if (b < L.pfq.B && L.pf_nb > 0) rp_sample_one(L.pfq, b, tid & 63);
+        if (lb == L.nU + LEARN_L2_GROUPS && L.pf_nb > 0 && tid == 0) {
             L.pf_hdr_next[0] = L.pf_epoch;
             L.pf_hdr_next[1] = L.pfq.counters[0];
             L.pf_hdr_next[2] = (long long)L.pfq.step;
@@ -694,7 +700,7 @@ __device__ __forceinline__ void learn_body(const SmallUnrollParams& P, const Lea
         }
     } else {
         const int half = tid >> 8, t256 = tid & (MZ_THREADS - 1);
-        const int vb = ((int)blockIdx.x - L.nU) * SM_SLOTS + half;
+        const int vb = (lb - L.nU) * SM_SLOTS + half;
         const bool vin = vb < 3 * MZ_L2_BLOCKS;       // (SM_SLOTS not dividing the slice count: idle groups)
         const int net = vb / MZ_L2_BLOCKS, blk = vb % MZ_L2_BLOCKS;
         red[tid] = vin ? lg_l2_slice(net, blk, t256, L.netoff, L.flat, nullptr, L.ad) : 0.0;

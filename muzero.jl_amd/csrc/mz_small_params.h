@@ -109,6 +109,7 @@ struct SmallUnrollParams {
 // race them; the last block folds the losses.
 struct LearnParams {
     int nU;
+    int xcd;              // the unroll workgroups on physical blocks 0, 8, .. (grid 8·nU; learn_body)
     const float* tv; const float* tp; const float* gscale;
     float* terms; float* flat; const size_t* netoff; double* part; unsigned* counter; float* out;
     LgAdam ad;
