@@ -40,7 +40,7 @@ end
 
 const NET_REPR, NET_PRED, NET_DYN = Cint(0), Cint(1), Cint(2)
 const ACT_IDENTITY, ACT_RELU, ACT_TANH = Int32(0), Int32(1), Int32(2)
-const ENV_TICTACTOE, ENV_CONNECT4 = Cint(0), Cint(1)
+const ENV_TICTACTOE, ENV_CONNECT4, ENV_ATARI = Cint(0), Cint(1), Cint(2)   # ENV_ATARI: the synthetic frame-stacked env of configs[4]
 const SP_TRAIN, SP_EVAL, OPP_SELF, OPP_RANDOM = Cint(0), Cint(1), Cint(0), Cint(1)
 const LEARN_REF_SEMANTICS, LEARN_CORRECTED = Cint(0), Cint(1)
 const TRAIN_LEARNER, TRAIN_ACTOR, TRAIN_QUEUED = Cint(0), Cint(1), Cint(2)
@@ -145,7 +145,8 @@ function learner_step!(e::Engine, batch, eta::Real)
 end
 
 """learner_mode!(e, LEARN_CORRECTED) — real backpropagation through the unroll
-(FC nets) instead of the reference's ∇ = 2θ (quirk Q11)."""
+(FC nets, and ResNet nets without the downsampler) instead of the reference's
+∇ = 2θ (quirk Q11)."""
 learner_mode!(e::Engine, mode::Cint) =
     check(e, ccall((:mz_learner_set_mode, libmz), Cint, (Ptr{Cvoid}, Cint), e.h, mode))
 
