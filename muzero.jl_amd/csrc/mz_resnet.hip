@@ -22,7 +22,7 @@ __device__ __forceinline__ float rn_act(int act, float v) {
 
 // A fragments of 16 output rows (block ob) for chunk c = k-steps 4c..4c+3 of
 // the four quarter chains: a[q][jj] (image [ob][q][nq4/4][lane][4]).
-__device__ __forceinline__ void rn_load_a(float (&a)[4][4], const float* __restrict__ Wimg, const RLayer& L,
+__device__ __forceinline__ void rn_load_a(float (*a)[4], const float* __restrict__ Wimg, const RLayer& L,
                                           int ob, int c, int lane) {
     const int nch = (L.nq + 3) >> 2;
     #ifdef RN_HOTA
@@ -88,12 +88,24 @@ __device__ __forceinline__ int rn_out_idx(int kb, int ob, int kl, int r, int n, 
 template <int NB>
 __device__ __forceinline__ void rn_load_res(const RLayer& L, const float* lds, float (&res)[NB][4], int ob, int kl,
                                             const int (&n)[NB], int ncols) {
+    if (!L.res_add) {                                   // wave-uniform
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) res[i][r] = 0.0f;
+        return;
+    }
+    // branch-free: out-of-tile lanes read a clamped in-range element, then take 0
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
             const bool in = ob * 16 + kl * 4 + r < L.cout && n[i] < ncols;
-            res[i][r] = L.res_add && in ? lds[L.res_off + rn_out_idx(L.res_kb, ob, kl, r, n[i], ncols)] : 0.0f;
+            const int nc = n[i] < ncols ? n[i] : ncols - 1;
+            const int oc = ob * 16 + kl * 4 + r < L.cout ? ob : 0;
+            const float x = lds[L.res_off + rn_out_idx(L.res_kb, oc, kl, ob * 16 + kl * 4 + r < L.cout ? r : 0, nc,
+                                                       ncols)];
+            res[i][r] = in ? x : 0.0f;
         }
 }
 
@@ -611,7 +623,12 @@ __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const 
         }
     } else {
         for (int i = i0; i < i1; ++i) {
-            rn_layer<NARROW, false, NBWMAX, false, NOKK>(rn_layer_at(R, i), Wimg, flat, lds, NG, Wb, P, bn_s, bn_r);
+            unsigned long long* dbg = nullptr;
+#ifdef MZ_STAMPS   // wave 0's first unit: [start, operands, chunks, epilogue] at st + 768 + 8·layer
+            if (st && i - i0 < 32) dbg = st + 768 + 8 * (i - i0);
+#endif
+            rn_layer<NARROW, false, NBWMAX, false, NOKK>(rn_layer_at(R, i), Wimg, flat, lds, NG, Wb, P, bn_s, bn_r,
+                                                         nullptr, dbg);
 #ifdef MZ_STAMPS
             if (st && (threadIdx.x & 63) == 0 && i - i0 < 31) st[wv * 64 + 2 * (i - i0)] = __builtin_amdgcn_s_memtime();
 #endif
@@ -1070,6 +1087,9 @@ extern "C" __global__ __launch_bounds__(64) void mz_rsearch_tree_lds32(RSearchPa
 extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RSearchParams P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int net = blockIdx.y == 0 ? MZ_NET_PRED : MZ_NET_DYN;
+#ifdef RN_DIAG_ONLY          // diagnostic builds (wrong results): time one net alone
+    if ((int)blockIdx.y != RN_DIAG_ONLY) return;
+#endif
     const RPlan& R = P.plans[net];
     const int NG = P.ng, t0 = blockIdx.x * NG, H = P.H, S = P.S;
     unsigned long long* st = nullptr;
@@ -1110,6 +1130,8 @@ extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RS
     __syncthreads();
     // prediction / dynamics: 1x1 convs and Dense layers only (rn_specs), so
     // the k-table path is left out of this kernel (registers: the 12-wave cap)
+    // (the PF prefetch set does not fit the 12-wave register budget: 200 spilled VGPRs, and an A-only
+    // prefetch into the layer's own registers measured 76 vs 70 µs)
     rn_run<false, false, 3, false, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st);
 #ifdef MZ_STAMPS
     if (st && (threadIdx.x & 63) == 0) st[(threadIdx.x >> 6) * 64 + 61] = __builtin_amdgcn_s_memtime();

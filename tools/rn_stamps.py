@@ -53,6 +53,9 @@ def main():
             wait = st[:, 2 * i + 1] - st[:, 2 * i]
             prev = st[:, 2 * i + 1].copy()
             print(f"  layer {i:2d}: " + " ".join(f"{c:6d}|{w:<6d}" for c, w in zip(comp, wait)))
+            d = out[y * 1024 + 768 + 8 * i: y * 1024 + 768 + 8 * i + 4].astype(np.int64)
+            if d.all():
+                print(f"      wave 0 unit 0: operands {d[1] - d[0]}  chunks {d[2] - d[1]}  epilogue {d[3] - d[2]}")
         last = max(2 * i + 1 for i in range(31) if st[:, 2 * i].any())
         k0 = st[:, 60].min()
         print(f"  staging {t0 - k0}  layers {st[:, last].max() - t0}  outputs {st[:, 61].max() - st[:, last].max()}"
