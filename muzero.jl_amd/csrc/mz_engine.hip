@@ -714,7 +714,7 @@ static int build_small(mz_handle* h) {
         // the total exceeds the LDS budget the tile-16 kernel is used)
         h->sm_lds[ti] = ints * 4 + (size_t)T * h->tree_game_bytes + pbterm_count(S) * 8 +
                         // the cached select: entries, path levels, N per slot, tags
-                        (size_t)T * (8 * NN + 8 * (S + 2) + 4 * NN) + 16 + 4 * 16 + 4 * 8 +
+                        (size_t)T * (8 * NN + 8 * (S + 2) + 4 * NN) + 16 + 4 * 16 + 4 * 8 + 4 * 4 +
                         (any_bn ? nri * 8 : 0);                          // BatchNorm (γ, β) per record row
     }
     return 1;

@@ -265,7 +265,10 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     int4* c_hdr = reinterpret_cast<int4*>(reinterpret_cast<char*>(smem) +                 // [4], 16-byte aligned
                                           ((reinterpret_cast<char*>(c_nN + T * NN) - reinterpret_cast<char*>(smem) + 15) & ~15));
     float2* c_mmx = reinterpret_cast<float2*>(c_hdr + 4);         // [4]
-    float2* bnl = c_mmx + 4;                                      // [nrec][slot][64] BatchNorm (γ, β) (P.bn)
+    // [4] per game: the select's start level (the last path's prefix the
+    // recompute found unchanged; 0 = from the root)
+    int* c_skip = reinterpret_cast<int*>(c_mmx + 4);
+    float2* bnl = reinterpret_cast<float2*>(c_skip + 4);          // [nrec][slot][64] BatchNorm (γ, β) (P.bn)
 
     const int tid = threadIdx.x;
     const int g = tid >> 4, a = tid & 15, lane = tid & 63;
@@ -307,7 +310,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         act[P.x_rep + k * T + gl] = ggl < P.G ? P.obs[(size_t)ggl * P.obs_feat + k] : 0.0f;
     }
     for (int i = tid; i < T * NN; i += SM_THREADS) c_cache[i] = make_uint2(0u, 0u);
-    if (tid < 4) { c_hdr[tid] = make_int4(0, -1, 1, 0); c_mmx[tid] = make_float2(0.0f, 0.0f); }   // no rows
+    if (tid < 4) { c_hdr[tid] = make_int4(0, -1, 1, 0); c_mmx[tid] = make_float2(0.0f, 0.0f); c_skip[tid] = 0; }
     int ver = 1;                                                  // wave 0: the tag of this lane's game
     if (tree_thread && a == 0) {
         uint32_t m = 0;
@@ -362,9 +365,18 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         if (tid < 64) {
             // ---- select (:256-268)
             if (active) {
+                // the start level and its node / incoming edge from the last path
+#ifdef MZ_NO_SKIP   // A/B: every walk from the root
+                const int D = 0;
+#else
+                const int D = c_skip[g];
+#endif
+                const int e0 = D > 0 ? path[2 * D + 1] : 0;
+                const uint32_t npc0 = D > 0 ? tree.nc(path[2 * D]) : 0u;
                 const SelectOut so = select_path_cached(tree, c_cache + g * NN, (uint32_t)ver, path, sg_rootN[g],
                                                         sg_root_tp[g], legal, sg_mmin[g], sg_mmax[g], a, lane, A,
-                                                        P.players, l_pbterm, P.seed, gid, P.rng_step, s);
+                                                        P.players, l_pbterm, P.seed, gid, P.rng_step, s, nullptr,
+                                                        nullptr, D, e0, npc0);
                 if (a == 0) { sg_leaf_e[g] = so.leaf_e; sg_leaf_a[g] = so.leaf_a; sg_vtp[g] = so.vtp; sg_depth[g] = so.depth; }
             }
             __builtin_amdgcn_wave_barrier();
@@ -424,6 +436,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
                     sg_rootN[g] = rN; sg_rootW[g] = rW; sg_mmin[g] = mmin; sg_mmax[g] = mmax;
                     c_hdr[g] = make_int4(moved ? 1 : 0, depth, ver, (int)legal);
                     c_mmx[g] = make_float2(mmin, mmax);
+                    c_skip[g] = moved ? 0 : depth;            // lowered by the recompute's path rows
                 }
             }
         } else if (tid >= 128 && tid < 128 + 16 * T) {
@@ -464,14 +477,21 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
             const bool lgl = a < A && (((uint32_t)hd.w >> a) & 1u);
             const TreeView tq = tree_view(lds_tree + (size_t)gq * P.tree_game_bytes, E, NN);
             uint2* cq = c_cache + gq * NN;
-            if (j0 < n)
-                cache_row(tq, cq, (uint32_t)hd.z, full ? j0 : (int)l0.x, full ? n0 : (int)l0.y, lgl, a, A, mm.x, mm.y,
-                          l_pbterm, lane);
+            // a path row whose new choice leaves the last path (or ties) bounds the
+            // next select's skip-ahead: levels below it are retraced as they were
+            const int* pq = sg_path + gq * PS;
+            const int pe0 = !full && j0 < hd.y ? pq[2 * (j0 + 1)] : 0;
+            if (j0 < n) {
+                const int ch = cache_row(tq, cq, (uint32_t)hd.z, full ? j0 : (int)l0.x, full ? n0 : (int)l0.y, lgl,
+                                         a, A, mm.x, mm.y, l_pbterm, lane);
+                if (!full && a == 0 && (j0 >= hd.y || ch != pe0 - (int)l0.x * A)) atomicMin(c_skip + gq, j0);
+            }
             for (int j = j0 + SM_THREADS / 16 / T; j < n; j += SM_THREADS / 16 / T) {   // deep paths, large trees
                 int slot, Np;
                 if (full) { slot = j; Np = c_nN[gq * NN + j]; }
                 else { const uint2 l = c_lvl[gq * (S + 2) + j]; slot = (int)l.x; Np = (int)l.y; }
-                cache_row(tq, cq, (uint32_t)hd.z, slot, Np, lgl, a, A, mm.x, mm.y, l_pbterm, lane);
+                const int ch = cache_row(tq, cq, (uint32_t)hd.z, slot, Np, lgl, a, A, mm.x, mm.y, l_pbterm, lane);
+                if (!full && a == 0 && (j >= hd.y || ch != pq[2 * (j + 1)] - slot * A)) atomicMin(c_skip + gq, j);
             }
             __syncthreads();
             SM_STAMP(6);                           // stamp build: slot 6 = the cache recompute (+ finish)

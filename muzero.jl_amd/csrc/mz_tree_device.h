@@ -457,22 +457,23 @@ template <int GW> __device__ __forceinline__ uint32_t grp_mask(uint64_t m, int l
 // One GW-lane group (row-uniform call) recomputes node `slot`'s entry; with
 // `cache_g` the entry is also stored there (the tree's HBM home).
 template <int GW = 16, bool TAB = true>
-__device__ __forceinline__ void cache_row(const TreeView& t, uint2* cache, uint32_t tag, int slot, int Np, bool lg,
-                                          int a, int A, float mmin, float mmax, const double* pbterm, int lane,
-                                          const double* pbc_tab = nullptr, const double* sqrt_tab = nullptr,
-                                          uint2* cache_g = nullptr) {
+__device__ __forceinline__ int cache_row(const TreeView& t, uint2* cache, uint32_t tag, int slot, int Np, bool lg,
+                                         int a, int A, float mmin, float mmax, const double* pbterm, int lane,
+                                         const double* pbc_tab = nullptr, const double* sqrt_tab = nullptr,
+                                         uint2* cache_g = nullptr) {
     const int ac = a < A ? a : A - 1;
     const float4 ed = t.e[(int)__umul24((unsigned)slot, (unsigned)A) + ac];
     const float u = pucb_lane<TAB>(ed, Np, lg, mmax > mmin, mmin, mmax - mmin, pbterm, pbc_tab, sqrt_tab);
     const float m = gmax_sel<GW>(u);
     const uint32_t msk = grp_mask<GW>(__builtin_amdgcn_ballot_w64(lg && u == m), lane);
     const int ach = (int)__builtin_ctzll((uint64_t)msk | (1ull << GW));
+    const bool tie = (msk & (msk - 1)) != 0;
     if (a == ach) {
-        const bool tie = (msk & (msk - 1)) != 0;
         const uint2 v = tie ? make_uint2(0u, 0u) : make_uint2((tag << 5) | (uint32_t)ach, __builtin_bit_cast(uint32_t, ed.x));
         cache[slot] = v;
         if (cache_g) cache_g[slot] = v;
     }
+    return tie ? -1 : ach;                               // the entry's child (-1: evaluated in full at select)
 }
 
 // U nodes at once (independent rows, one GW-lane group per game): every load
@@ -522,7 +523,8 @@ __device__ __forceinline__ SelectOut select_path_cached(const TreeView& t, const
                                                         float mmin, float mmax, int a, int lane, int A, int players,
                                                         const double* pbterm, uint64_t seed, uint32_t gid,
                                                         uint32_t step, int sim, const double* pbc_tab = nullptr,
-                                                        const double* sqrt_tab = nullptr) {
+                                                        const double* sqrt_tab = nullptr, int D = 0, int e0 = 0,
+                                                        uint32_t npc0 = 0) {
     const bool lg = a < A && ((legal >> a) & 1u);
     const bool norm = mmax > mmin;
     const float den = mmax - mmin;
@@ -533,10 +535,15 @@ __device__ __forceinline__ SelectOut select_path_cached(const TreeView& t, const
     // edge into e (its N), lach / dg = action and depth of the last level
     // walked.  `am` = lanes whose group is still walking (an SGPR mask, so the
     // freezes are single v_cndmask ops and the loop exit a scalar test).
-    int e = 0, dg = 0, lach = 0, pe = 0, pc = 0;
-    uint32_t npc = (uint32_t)root_N;
+    // Skip-ahead: a group starts at level D (its node e0, npc0 the nc word of
+    // the edge into it): the recompute found levels 0..D-1 of the last path
+    // still selected (their entries current and pointing along it), so the walk
+    // from the root would retrace them; lv = the level being chosen, per group.
+    int e = D > 0 ? e0 : 0, dg = D, lach = 0, pe = 0, pc = 0;
+    uint32_t npc = D > 0 ? npc0 : (uint32_t)root_N;
     uint64_t am = __builtin_amdgcn_ballot_w64(true);
-    for (int depth = 1;; ++depth) {
+    for (int it = 1;; ++it) {
+        const int lv = D + it;
         uint2 ce = cache[e];
         asm volatile("" : "+v"(ce.x), "+v"(ce.y));       // one ds_read_b64 (not split into the branches)
         int ach = (int)(ce.x & 31u);
@@ -555,7 +562,7 @@ __device__ __forceinline__ SelectOut select_path_cached(const TreeView& t, const
             int ch = (int)__builtin_ctzll((uint64_t)mask | (1ull << GW));
             const int nt = __builtin_popcount(mask);
             if (stale && nt > 1) {                        // ties: the Philox draw (oracle select_child)
-                const uint32_t r = mz_rng_u32(seed, MZ_RNG_TIE, gid, step, ((uint32_t)sim << 12) | (uint32_t)depth);
+                const uint32_t r = mz_rng_u32(seed, MZ_RNG_TIE, gid, step, ((uint32_t)sim << 12) | (uint32_t)lv);
                 ch = nth_set_bit(mask, (int)mz_rng_below(r, (uint32_t)nt));
             }
             const uint32_t nch = gor<GW>(a == ch ? nc : 0u);
@@ -564,15 +571,16 @@ __device__ __forceinline__ SelectOut select_path_cached(const TreeView& t, const
         }
         const int ei = (int)__umul24((unsigned)e, (unsigned)A) + ach;
         const int Cch = (int)(ncc >> 16);                 // child slot + 1, 0 = the leaf
-        const uint64_t km = mz_vcmp_eq((uint32_t)a, (uint32_t)depth) & am;   // lane `depth` keeps the level
+        const uint64_t km = mz_vcmp_eq((uint32_t)a, (uint32_t)lv) & am;   // lane `lv` keeps the level
         pe = mz_vsel(km, ei, pe);
         pc = mz_vsel(km, Cch, pc);
         lach = mz_vsel(am, ach, lach);
-        dg = mz_vsel(am, depth, dg);
-        if (depth >= GW) {                                // wave-uniform (rare: deep paths)
-            uint64_t wm = am;
+        dg = mz_vsel(am, lv, dg);
+        const uint64_t deep = __builtin_amdgcn_ballot_w64(lv >= GW) & am;
+        if (deep != 0) {                                  // rare: deep paths past the register-held levels
+            uint64_t wm = deep;
             asm volatile("" : "+s"(wm));                  // the lane test stays inside this branch
-            if (a == 0 && ((wm >> lane) & 1u)) { path[2 * depth] = ei; path[2 * depth + 1] = Cch - 1; }
+            if (a == 0 && ((wm >> lane) & 1u)) { path[2 * lv] = ei; path[2 * lv + 1] = Cch - 1; }
         }
         const uint64_t nm = mz_vcmp_ne((uint32_t)Cch, 0u) & am;   // groups still walking after this level
         e = mz_vsel(nm, Cch - 1, e);
@@ -580,7 +588,7 @@ __device__ __forceinline__ SelectOut select_path_cached(const TreeView& t, const
         am = nm;
         if (am == 0) break;
     }
-    if (a >= 1 && a <= dg) { path[2 * a] = pe; path[2 * a + 1] = pc - 1; }
+    if (a > D && a <= dg && a < GW) { path[2 * a] = pe; path[2 * a + 1] = pc - 1; }
     const int vtp = players == 2 ? ((root_tp - 1 + dg) & 1) + 1 : (root_tp - 1 + dg) % players + 1;
     return SelectOut{e, lach, vtp, dg};
 }
