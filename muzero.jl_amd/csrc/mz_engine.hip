@@ -53,6 +53,8 @@ extern "C" __global__ void mz_runroll_chain1(RUnrollParams U);
 extern "C" __global__ void mz_runroll_chain_r(RUnrollParams U);
 extern "C" __global__ void mz_runroll_chain_r3(RUnrollParams U);
 extern "C" __global__ void mz_runroll_pred_r(RUnrollParams U);
+extern "C" __global__ void mz_runroll_fused_r(RUnrollParams U);
+extern "C" __global__ void mz_runroll_fused_r3(RUnrollParams U);
 extern "C" __global__ void mz_sp_prepare(SpParams S);
 extern "C" __global__ void mz_sp_commit(SpParams S);
 extern "C" __global__ void mz_sp_order(SpParams S);
@@ -166,6 +168,8 @@ struct mz_handle {
     bool rd_chain = false;                  // the chain runs as mz_runroll_chain_r[3] (rd_chain_ok)
     int rd_nb = 1;                          // its column blocks (1: mz_runroll_chain_r, 3: _r3)
     bool rp_pred = false;                   // one-item predictions run as mz_runroll_pred_r (rp_pred_ok)
+    unsigned long long* d_prog = nullptr;   // [bcap] mz_runroll_fused_r progress words
+    unsigned long long prog_epoch = 0;      // launches of mz_runroll_fused_r (prog_base = epoch · 64)
     std::vector<int> rtab;                  // offset tables of the narrow (chain) plans
     int* d_rtab = nullptr;
     int device = 0, max_games = 0;
@@ -1371,6 +1375,11 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
     if (h->rp_pred)
         CK(hipFuncSetAttribute((const void*)mz_runroll_pred_r, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)rp_pred_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(runroll_pred_r)"));
+    if (h->rd_chain && h->rp_pred)
+        CK(hipFuncSetAttribute(h->rd_nb == 3 ? (const void*)mz_runroll_fused_r3 : (const void*)mz_runroll_fused_r,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)std::max(rd_chain_lds(h), rp_pred_lds(h))) == hipSuccess
+               ? 0 : fail(h, "hipFuncSetAttribute(runroll_fused_r)"));
     CK(hipFuncSetAttribute((const void*)mz_rsearch_nets, hipFuncAttributeMaxDynamicSharedMemorySize,
                            (int)rsearch_nets_lds(h)) == hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(nets)"));
     // search buffers (trees and hidden states in HBM)
@@ -1909,6 +1918,9 @@ static int ensure_batch(mz_handle* h, int B) {
     if (h->kind == 1) {
         MZ_TRY(h, dalloc(h, &h->d_rhs, (size_t)B * std::max(K, 1) * h->H));
         MZ_TRY(h, dalloc(h, &h->d_rts, (size_t)B * std::max(K, 1) * h->H));
+        MZ_TRY(h, dalloc(h, &h->d_prog, (size_t)B));
+        MZ_TRY(h, hipMemset(h->d_prog, 0, (size_t)B * sizeof(unsigned long long)));
+        h->prog_epoch = 0;
     }
     h->bcap = B;
     return 0;
@@ -1924,7 +1936,7 @@ static int learner_losses(mz_handle* h, const mz_batch* b, float* grad_dev, floa
 // ResNet learner: the unroll on the network kernels, then the shared loss /
 // ∇ = 2θ kernel (the plans' outputs are already activated)
 static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, void* stream,
-                         bool fuse_adam = false, double eta = 0.0) {
+                         bool fuse_adam = false, double eta = 0.0, const RpSampleParams* rq = nullptr) {
     const int B = b->batch_size;
     if (B < 1) return fail(h, "batch_size must be >= 1");
     if (ensure_batch(h, B)) return -1;
@@ -1946,30 +1958,53 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
     U.stamps = h->d_stamps;
 #endif
     void* args[] = {&U};
+    const int KH = std::max(U.K, 1);
+    // the B·K predictions on wide tiles (ng items) once they fill the chip
+    // (B = 2048: 640 workgroups; one-item tiles there measured 2.4x slower),
+    // else one-item tiles (B = 32: 160 workgroups instead of 10)
+    static const bool wide_env = std::getenv("MZ_RN_PRED_WIDE") != nullptr;
+    static const bool one_kernel = std::getenv("MZ_RUNROLL_FUSED") != nullptr;
+    const bool wide_p = wide_env || (B * KH + U.ng - 1) / U.ng >= h->n_cu;
+    // one launch (mz_runroll_fused_r): the chain blocks, then the items, each
+    // item waiting for its sample's chain instead of the whole launch; with
+    // rq, each chain block also draws its sample (the get_batch launch folded in)
+    static const bool no_fuse = std::getenv("MZ_RN_NO_FUSE") != nullptr;
+    const bool fused = !one_kernel && h->rd_chain && h->rp_pred && !wide_p && !no_fuse && U.ng_l == 1 &&
+                       U.K + 1 < 64 && !h->ds && h->d_prog;
+    static const bool no_fuse_sample = std::getenv("MZ_RN_NO_FUSE_SAMPLE") != nullptr;   // A/B only
+    if (rq && (!fused || no_fuse_sample)) {
+        hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, *rq);
+        MZ_TRY(h, hipGetLastError());
+    }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->time_unroll) {
         if (timing_events(h, &e0, &e1)) return -1;
         MZ_TRY(h, hipEventRecord(e0, st));
     }
-    if (std::getenv("MZ_RUNROLL_FUSED")) {          // the one-kernel unroll (pred inside the chain)
+    if (one_kernel) {          // the one-kernel unroll (pred inside the chain)
         h->last_lvariant = "mz_runroll_kernel";
         MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_kernel, dim3((B + U.ng - 1) / U.ng), dim3(RN_THREADS),
                                   args, runroll_lds(h), st));
     } else {                                        // chain on narrow tiles, then the B·K predictions
-        const int KH = std::max(U.K, 1);
         // tiles of one column block: the 1-block instances (a fifth of the code)
         const bool nb1 = (U.P * U.ng_l + 15) / 16 == 1;
         U.rd_ep_off = (int)(h->rn_lds_l / 4);
-        // the B·K predictions on wide tiles (ng items) once they fill the chip
-        // (B = 2048: 640 workgroups; one-item tiles there measured 2.4x slower),
-        // else one-item tiles (B = 32: 160 workgroups instead of 10)
-        static const bool wide_env = std::getenv("MZ_RN_PRED_WIDE") != nullptr;
-        const bool wide_p = wide_env || (B * KH + U.ng - 1) / U.ng >= h->n_cu;
         h->last_lvariant = std::string(h->rd_chain ? (h->rd_nb == 3 ? "mz_runroll_chain_r3" : "mz_runroll_chain_r")
                                                    : nb1 ? "mz_runroll_chain1" : "mz_runroll_chain") +
                            (wide_p ? "+mz_runroll_pred" : h->rp_pred ? "+mz_runroll_pred_r" : nb1 ? "+mz_runroll_pred_n1"
                                                                                        : "+mz_runroll_pred_n");
-        if (h->rd_chain)
+        if (fused) {
+            U.prog = h->d_prog;
+            U.prog_base = (++h->prog_epoch) * 64ull;
+            U.n_chain = B;
+            U.fuse_sample = rq != nullptr && !no_fuse_sample;
+            if (rq) U.rq = *rq;
+            h->last_lvariant = h->rd_nb == 3 ? "mz_runroll_fused_r3" : "mz_runroll_fused_r";
+            const int nitems = B * KH * (U.K > 0 ? 2 : 1);
+            MZ_TRY(h, hipLaunchKernel(h->rd_nb == 3 ? (const void*)mz_runroll_fused_r3 : (const void*)mz_runroll_fused_r,
+                                      dim3(B + nitems), dim3(RD_THREADS), args,
+                                      std::max(rd_chain_lds(h), rp_pred_lds(h)), st));
+        } else if (h->rd_chain)
             MZ_TRY(h, hipLaunchKernel(h->rd_nb == 3 ? (const void*)mz_runroll_chain_r3 : (const void*)mz_runroll_chain_r,
                                       dim3((B + U.ng_l - 1) / U.ng_l),
                                       dim3(RD_THREADS), args, rd_chain_lds(h), st));
@@ -1978,7 +2013,8 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
                                       dim3((B + U.ng_l - 1) / U.ng_l), dim3(RN_THREADS),
                                       args, h->rn_lds_l, st));
         // the B·K predictions and reward heads (wide_p above)
-        if (wide_p)
+        if (fused) {
+        } else if (wide_p)
             MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred, dim3((B * KH + U.ng - 1) / U.ng, U.K > 0 ? 2 : 1),
                                       dim3(RN_THREADS), args, runroll_lds(h), st));
         else if (h->rp_pred)
@@ -2967,11 +3003,14 @@ static int learner_sampled(mz_handle* h, int32_t B, uint32_t step, float* grad_d
         return train ? mz_learner_apply_dev(h, nullptr, 1.0f, eta, st) : 0;
     }
     if (h->kind == 1) {                             // ResNet: sample, then the network unroll
-        hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, Q);
-        MZ_TRY(h, hipGetLastError());
-        if (per_norm(h, B, st)) return -1;
+        if (h->conf.PER || h->ds) {                 // (else the sample is drawn inside the unroll launch)
+            hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, Q);
+            MZ_TRY(h, hipGetLastError());
+            if (per_norm(h, B, st)) return -1;
+        }
         // one GPU: ADAM fused into the loss / Σθ² kernel (as the FC path)
-        if (rlearner_grad(h, &b, train ? nullptr : grad_dev, losses_dev, st, train, eta)) return -1;
+        if (rlearner_grad(h, &b, train ? nullptr : grad_dev, losses_dev, st, train, eta,
+                          h->conf.PER || h->ds ? nullptr : &Q)) return -1;
         return per_update(h, B, st);                               // Learning.jl:400-404
     }
     if (fused) {

@@ -18,7 +18,7 @@
 
 #define MZ_TILE 16          // games (or samples) per workgroup tile = MFMA N
 #define MZ_THREADS 256      // 4 wavefronts
-#define MZ_L2_BLOCKS 32     // Σθ² / ∇ (/ fused ADAM) blocks per net in mz_learner_grad_kernel*
+#define MZ_L2_BLOCKS 128    // Σθ² / ∇ (/ fused ADAM) blocks per net in mz_learner_grad_kernel* (oracle ora_sqnorm: NB)
 #define MZ_MAX_STAGES 64
 
 // One Dense layer inside a plan.  All offsets are in floats.

@@ -13,6 +13,7 @@
 // B[l>>4][l&15].
 #include "mz_mlp_device.h"
 #include "mz_resnet_params.h"
+#include "mz_replay_device.h"
 
 __device__ __forceinline__ float rn_act(int act, float v) {
     if (act == MZ_ACT_RELU) return mz_relu(v);
@@ -1234,7 +1235,7 @@ __device__ __forceinline__ void runroll_chain_body(const RUnrollParams& U) {
     unsigned long long* st_r = nullptr;
     unsigned long long* st_d = nullptr;
 #ifdef MZ_STAMPS
-    if (U.stamps && blockIdx.x == 0) { st_r = U.stamps; st_d = U.stamps + 512; }
+    if (U.stamps && tile == 0) { st_r = U.stamps; st_d = U.stamps + 512; }
 #endif
     rn_fill_ktabs(Rr, lds, NG, U.W, U.P);
     if (Rr.tab_n) {                                 // the representation's offset tables (+ the zero float)
@@ -1413,13 +1414,53 @@ __device__ __forceinline__ void rd_run(const RPlan& Rd, const float (&a0)[2][4][
     (void)st;
 }
 
-// NL: the dynamics chain's layers ([0, dyn_split)); NB: column blocks of the tile
-template <int NL, int NB>
-__device__ __forceinline__ void runroll_chain_r_body(const RUnrollParams& U) {
+// mz_runroll_fused_r's hand-off between workgroups, on the scoped caches of
+// gfx950 without whole-L2 write-back / invalidate: the chain stores h and the
+// trunk outputs as agent-scope atomics (written through to the agent's
+// coherence point), every wave waits for its stores (vmcnt 0), then after the
+// barrier one agent-scope store of the progress word.  An item polls the word
+// with agent-scope loads (bounded: a chain that never publishes lets the item
+// run on stale data rather than hang) and reads its input with agent-scope
+// loads (they miss any stale L1 / L2 copy).
+__device__ __forceinline__ void rd_st(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float rd_ld(const float* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void rd_publish(const RUnrollParams& U, int b, int p) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(U.prog + b, U.prog_base + (unsigned long long)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void rd_wait(const RUnrollParams& U, int b, int p) {
+    if (threadIdx.x == 0) {
+        const unsigned long long want = U.prog_base + (unsigned long long)p;
+        for (int n = 0; n < (1 << 21); ++n) {
+            if (__hip_atomic_load(U.prog + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+}
+
+// NL: the dynamics chain's layers ([0, dyn_split)); NB: column blocks of the tile;
+// FUSE: mz_runroll_fused_r's chain blocks (ng_l = 1: tile = sample), which
+// draw their sample first when U.fuse_sample and publish their progress
+template <int NL, int NB, bool FUSE = false>
+__device__ __forceinline__ void runroll_chain_r_body(const RUnrollParams& U, int tile) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const RPlan& Rr = U.plans_l[MZ_NET_REPR];
     const RPlan& Rd = U.plans_l[MZ_NET_DYN];
-    const int NG = U.ng_l, t0 = blockIdx.x * NG, H = U.H, A = U.A, K = U.K, K1 = K + 1;
+    const int NG = U.ng_l, t0 = tile * NG, H = U.H, A = U.A, K = U.K, K1 = K + 1;
+    if constexpr (FUSE) {
+        if (U.fuse_sample) {                                   // get_batch (ReplayBuffer.jl:188-217)
+            if (threadIdx.x < 64 && t0 < U.B) rp_sample_one(U.rq, t0, threadIdx.x);
+            __threadfence_block();
+            __syncthreads();
+        }
+    }
     const RnLane t = rn_lane(NG);
     const int b = t0 + t.g;
     const bool ok = b < U.B;
@@ -1433,7 +1474,7 @@ __device__ __forceinline__ void runroll_chain_r_body(const RUnrollParams& U) {
     unsigned long long* st_r = nullptr;
     unsigned long long* st_d = nullptr;
 #ifdef MZ_STAMPS
-    if (U.stamps && blockIdx.x == 0) { st_r = U.stamps; st_d = U.stamps + 512; }
+    if (U.stamps && tile == 0) { st_r = U.stamps; st_d = U.stamps + 512; }
 #endif
     float4* ep_lds = reinterpret_cast<float4*>(lds + U.rd_ep_off);   // [NL][64] {bias, γ, β, 0}
     for (int i = threadIdx.x; i < NL * 64; i += blockDim.x) {
@@ -1464,8 +1505,11 @@ __device__ __forceinline__ void runroll_chain_r_body(const RUnrollParams& U) {
 #pragma unroll
         for (int i = 1; i < NL; ++i) rn_load_a(ar[i], U.Wimg, rn_layer_at(Rd, i), ob, 0, lane);
     }
-    if (ok) rn_unstage_l(lds + Rr.out0_off, Rr.out0_kb, NG, U.P, H, t, [&](int f, float v) { hs[f] = v; });
+    if (ok) rn_unstage_l(lds + Rr.out0_off, Rr.out0_kb, NG, U.P, H, t, [&](int f, float v) {
+        if constexpr (FUSE) rd_st(hs + f, v); else hs[f] = v;
+    });
     if (ok && t.f0 == 0) U.pr[bs * K1] = 0.0f;                                 // :352 zeros
+    if constexpr (FUSE) rd_publish(U, t0, 1);                                 // h_0
     const float bn_r = 1.0f / U.bn_s;
     for (int s = 1; s <= K; ++s) {
         __syncthreads();
@@ -1477,19 +1521,23 @@ __device__ __forceinline__ void runroll_chain_r_body(const RUnrollParams& U) {
         __syncthreads();
         rd_run<0, NL, NB>(Rd, a0, ar, ep_lds, lds, ncols, U.bn_s, bn_r, s == 1 ? st_d : nullptr);   // :362, [0, split)
         if (ok) {
-            if (s < K) rn_unstage_l(lds + Rd.out0_off, Rd.out0_kb, NG, U.P, H, t,
-                                    [&](int f, float v) { hs[(size_t)s * H + f] = v; });
-            rn_unstage_l(lds + trunk, Rd.L[split].in_kb, NG, U.P, H, t, [&](int f, float v) { ts[(size_t)(s - 1) * H + f] = v; });
+            if (s < K) rn_unstage_l(lds + Rd.out0_off, Rd.out0_kb, NG, U.P, H, t, [&](int f, float v) {
+                if constexpr (FUSE) rd_st(hs + (size_t)s * H + f, v); else hs[(size_t)s * H + f] = v;
+            });
+            rn_unstage_l(lds + trunk, Rd.L[split].in_kb, NG, U.P, H, t, [&](int f, float v) {
+                if constexpr (FUSE) rd_st(ts + (size_t)(s - 1) * H + f, v); else ts[(size_t)(s - 1) * H + f] = v;
+            });
         }
+        if constexpr (FUSE) rd_publish(U, t0, s + 1);                         // h_s (s < K), trunk of step s
     }
 }
 // TicTacToe resnet_hyper (2 blocks: 10 chain layers, 3x3 board: one column
 // block) and Connect4 ResNet-8 (4 blocks: 18 layers, 6x7 board: three)
 extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r(RUnrollParams U) {
-    runroll_chain_r_body<RD_NL, 1>(U);
+    runroll_chain_r_body<RD_NL, 1>(U, blockIdx.x);
 }
 extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r3(RUnrollParams U) {
-    runroll_chain_r_body<RD_NL3, 3>(U);
+    runroll_chain_r_body<RD_NL3, 3>(U, blockIdx.x);
 }
 
 // blockIdx.y = 0: prediction(h_s) for items i = b·KH + s (KH = max(K, 1)):
@@ -1546,12 +1594,14 @@ __device__ __forceinline__ void rp_run(const RPlan& R, const float (&ar)[RP_NL][
     }
 }
 
-extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_pred_r(RUnrollParams U) {
+// FUSE: an item of mz_runroll_fused_r (ng_l = 1: tile = item b·KH + s), which
+// waits until the chain of sample b has published its input
+template <bool FUSE>
+__device__ __forceinline__ void runroll_pred_r_body(const RUnrollParams& U, bool rew, int tile) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const bool rew = blockIdx.y == 1;
     const RPlan& R = U.plans_l[rew ? MZ_NET_DYN : MZ_NET_PRED];
     const int NG = U.ng_l, H = U.H, A = U.A, K = U.K, K1 = K + 1, KH = K > 0 ? K : 1;
-    const int n_items = U.B * KH, t0 = blockIdx.x * NG;
+    const int n_items = U.B * KH, t0 = tile * NG;
     const int i0 = rew ? U.dyn_split : 0;
     const RnLane t = rn_lane(NG);
     const int it = t0 + t.g;
@@ -1569,10 +1619,14 @@ extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_pred_r(RUnro
         }
     }
     rn_fill_ktabs(R, lds, NG, U.W, U.P);
+    if constexpr (FUSE) {                       // h_s: progress s + 1; trunk of step s + 1: s + 2
+        const int bw = (int)(ic / KH), sw = (int)(ic - (size_t)bw * KH);
+        rd_wait(U, bw, sw + (rew ? 2 : 1));
+    }
     {
         const float* x = (rew ? U.ts : U.hs) + ic * H;
         rn_stage_l(lds + (rew ? R.L[i0].in_off : R.in_off), rew ? R.L[i0].in_kb : R.in_kb, NG, U.P, H, t,
-                   [&](int f) { return ok ? x[f] : 0.0f; });
+                   [&](int f) { return ok ? (FUSE ? rd_ld(x + f) : x[f]) : 0.0f; });
     }
     __syncthreads();
     if (!rew) {
@@ -1593,6 +1647,34 @@ extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_pred_r(RUnro
         float* o = U.pp + (b * K1 + j) * A;
         rn_unstage(lds + R.out1_off, NG, A, t, [&](int f, float v) { o[f] = v; });
     }
+}
+extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_pred_r(RUnrollParams U) {
+    runroll_pred_r_body<false>(U, blockIdx.y == 1, blockIdx.x);
+}
+
+// The whole B = small unroll in one launch: blocks [0, n_chain) are the chain
+// (representation + K dynamics steps of one sample, mz_runroll_chain_r, and
+// with fuse_sample its get_batch draw); the rest are the prediction and
+// reward-head items of mz_runroll_pred_r in step-major order, each starting
+// as soon as its sample's chain has published the input (rd_wait).  Blocks
+// dispatch in index order, so every chain block is resident before any item
+// waits on it; the waits are bounded.  Same arithmetic as the two launches.
+template <int NL, int NB>
+__device__ __forceinline__ void runroll_fused_r_body(const RUnrollParams& U) {
+    const int bi = blockIdx.x;
+    if (bi < U.n_chain) { runroll_chain_r_body<NL, NB, true>(U, bi); return; }
+    const int ny = U.K > 0 ? 2 : 1, KH = U.K > 0 ? U.K : 1;
+    const int idx = bi - U.n_chain, per_s = ny * U.B;
+    const int s = idx / per_s, r = idx - s * per_s;
+    const bool rew = r >= U.B;
+    const int b = rew ? r - U.B : r;
+    runroll_pred_r_body<true>(U, rew, b * KH + s);
+}
+extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_fused_r(RUnrollParams U) {
+    runroll_fused_r_body<RD_NL, 1>(U);
+}
+extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_fused_r3(RUnrollParams U) {
+    runroll_fused_r_body<RD_NL3, 3>(U);
 }
 
 // wide tiles of ng items (plans), or one item per workgroup on the narrow

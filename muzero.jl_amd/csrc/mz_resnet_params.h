@@ -10,6 +10,7 @@
 // reads x[w + (kw-1-i) - pw, h + (kh-1-j) - ph, c] (Flux convolution, kernel
 // flipped) or 0 outside the board.
 #pragma once
+#include "mz_selfplay_params.h"
 
 #define RN_MAX_LAYERS 96
 #ifndef RN_THREADS
@@ -182,6 +183,14 @@ struct RUnrollParams {
     float* ts;                         // [B][K][H] dynamics trunk outputs (split form: the reward heads' input)
     unsigned long long* stamps;        // -DMZ_STAMPS builds: per-layer ticks of chain block 0 (repr, dyn s = 1)
     int rd_ep_off;                     // mz_runroll_chain_r: LDS float offset of the staged epilogue parameters
+    // mz_runroll_fused_r (one launch: chain blocks [0, n_chain), then the B·K
+    // prediction / reward-head items, each waiting for its sample's chain):
+    // prog[b] = prog_base + p once the chain of sample b has stored h_0..h_{p-1}
+    // and the trunk outputs of steps 1..p-1 (prog_base = launch epoch · 64)
+    unsigned long long* prog; unsigned long long prog_base;
+    int n_chain;
+    int fuse_sample;                   // 1: chain block b draws sample b (get_batch, rq) first
+    RpSampleParams rq;
 };
 // mz_runroll_chain_r: the dynamics chain's layers ([0, dyn_split) = RD_NL:
 // trunk + state head of 2-block towers) with register-resident A fragments

@@ -976,14 +976,14 @@ EXPORT void ora_losses(const mz_config* c, int B, const float* pv, const float* 
 }
 
 /* sum(sqnorm, params) (:287) in f64, in the engine's fixed order
- * (lg_l2_slice + lg_tree256 + lg_fold): 32 slices of 256 threads, thread t
- * of slice b summing elements b·256 + t + j·8192 in ascending j, a pairwise
- * tree over the 256 threads (offsets 128..1), then the 32 slice sums on
- * lanes 0..31 of the 64-lane butterfly.                                      */
+ * (lg_l2_slice + lg_tree256 + lg_fold): 128 slices of 256 threads (MZ_L2_BLOCKS),
+ * thread t of slice b summing elements b·256 + t + j·32768 in ascending j, a
+ * pairwise tree over the 256 threads (offsets 128..1), then lane l of the
+ * 64-lane butterfly holding slices l and l + 64 (summed in that order).      */
 EXPORT double ora_sqnorm(const float* P, size_t n) {
-    enum { NB = 32, NT = 256 };
+    enum { NB = 128, NT = 256 };
     const size_t stride = (size_t)NB * NT;
-    double part[64] = {0};
+    double part[NB], lanes[64];
     for (int b = 0; b < NB; ++b) {
         double red[NT];
         for (int t = 0; t < NT; ++t) {
@@ -995,7 +995,12 @@ EXPORT double ora_sqnorm(const float* P, size_t n) {
             for (int t = 0; t < o; ++t) red[t] += red[t + o];
         part[b] = red[0];
     }
-    return fold64(part);
+    for (int l = 0; l < 64; ++l) {
+        double s = 0.0;
+        for (int b = l; b < NB; b += 64) s += part[b];
+        lanes[l] = s;
+    }
+    return fold64(lanes);
 }
 
 /* Flux 0.12 ADAMW() = Optimiser(ADAM(η, (0.9, 0.999)), WeightDecay(0));
