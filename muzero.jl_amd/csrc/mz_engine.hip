@@ -1336,6 +1336,10 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
            ? 0 : fail(h, "copy"));
     CK(al(&h->d_flat, h->nflat));
     CK(al(&h->d_Wp, h->packed_w_n));
+    if (h->rd_chain && h->rp_pred) {                // second image set of mz_runroll_fused_r's ADAM blocks
+        CK(al(&h->d_Wp2, h->packed_w_n));
+        CK(hipMemset(h->d_Wp2, 0, h->packed_w_n * 4) == hipSuccess ? 0 : fail(h, "memset"));
+    }
     CK(hipMemset(h->d_flat, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
     CK(repack(h));
     CK(al(&h->d_m, h->nflat)); CK(al(&h->d_v, h->nflat)); CK(al(&h->d_grad, h->nflat));
@@ -1931,7 +1935,8 @@ static size_t runroll_lds(const mz_handle* h) {
 }
 
 static int learner_losses(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, hipStream_t st,
-                          int v_act, int r_act, bool fuse_adam = false, double eta = 0.0);
+                          int v_act, int r_act, bool fuse_adam = false, double eta = 0.0, bool l2_done = false);
+static void adam_advance(mz_handle* h);
 
 // ResNet learner: the unroll on the network kernels, then the shared loss /
 // ∇ = 2θ kernel (the plans' outputs are already activated)
@@ -1972,6 +1977,8 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
     const bool fused = !one_kernel && h->rd_chain && h->rp_pred && !wide_p && !no_fuse && U.ng_l == 1 &&
                        U.K + 1 < 64 && !h->ds && h->d_prog;
     static const bool no_fuse_sample = std::getenv("MZ_RN_NO_FUSE_SAMPLE") != nullptr;   // A/B only
+    static const bool no_fuse_adam = std::getenv("MZ_RN_NO_FUSE_ADAM") != nullptr;       // A/B only
+    bool l2_fused = false;
     if (rq && (!fused || no_fuse_sample)) {
         hipLaunchKernelGGL(mz_rp_sample, dim3((B + 3) / 4), dim3(256), 0, st, *rq);
         MZ_TRY(h, hipGetLastError());
@@ -1989,6 +1996,7 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
         // tiles of one column block: the 1-block instances (a fifth of the code)
         const bool nb1 = (U.P * U.ng_l + 15) / 16 == 1;
         U.rd_ep_off = (int)(h->rn_lds_l / 4);
+        U.rd_trunk_nl = 1 + 2 * h->rhp.num_blocks;
         h->last_lvariant = std::string(h->rd_chain ? (h->rd_nb == 3 ? "mz_runroll_chain_r3" : "mz_runroll_chain_r")
                                                    : nb1 ? "mz_runroll_chain1" : "mz_runroll_chain") +
                            (wide_p ? "+mz_runroll_pred" : h->rp_pred ? "+mz_runroll_pred_r" : nb1 ? "+mz_runroll_pred_n1"
@@ -1999,10 +2007,17 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
             U.n_chain = B;
             U.fuse_sample = rq != nullptr && !no_fuse_sample;
             if (rq) U.rq = *rq;
+            // ADAM beside the unroll: the launch reads the current image (d_Wp) and
+            // writes the updated one into d_Wp2, swapped after the launch
+            U.n_l2 = fuse_adam && h->d_Wp2 && !no_fuse_adam ? 96 : 0;
+            U.ad = LgAdam{1, h->d_m, h->d_v, h->bp1, h->bp2, eta, h->d_Wp2, h->d_Bp, h->d_inv_tile, nullptr,
+                          nullptr, h->d_inv_small};
+            U.flat_w = h->d_flat; U.netoff = h->d_netoff; U.part = h->d_sq;
+            l2_fused = U.n_l2 > 0;
             h->last_lvariant = h->rd_nb == 3 ? "mz_runroll_fused_r3" : "mz_runroll_fused_r";
             const int nitems = B * KH * (U.K > 0 ? 2 : 1);
             MZ_TRY(h, hipLaunchKernel(h->rd_nb == 3 ? (const void*)mz_runroll_fused_r3 : (const void*)mz_runroll_fused_r,
-                                      dim3(B + nitems), dim3(RD_THREADS), args,
+                                      dim3(B + U.n_l2 + nitems), dim3(RD_THREADS), args,
                                       std::max(rd_chain_lds(h), rp_pred_lds(h)), st));
         } else if (h->rd_chain)
             MZ_TRY(h, hipLaunchKernel(h->rd_nb == 3 ? (const void*)mz_runroll_chain_r3 : (const void*)mz_runroll_chain_r,
@@ -2026,7 +2041,13 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
                                       h->rn_lds_l, st));
     }
     if (e1) MZ_TRY(h, hipEventRecord(e1, st));
-    return learner_losses(h, b, grad_dev, losses_dev, st, MZ_ACT_IDENTITY, MZ_ACT_IDENTITY, fuse_adam, eta);
+    if (learner_losses(h, b, grad_dev, losses_dev, st, MZ_ACT_IDENTITY, MZ_ACT_IDENTITY, fuse_adam, eta, l2_fused))
+        return -1;
+    if (l2_fused) {
+        std::swap(h->d_Wp, h->d_Wp2);
+        adam_advance(h);
+    }
+    return 0;
 }
 
 static int fc_unroll(mz_handle* h, const mz_batch* b, hipStream_t st, const RpSampleParams* rp);
@@ -2137,18 +2158,20 @@ static void adam_advance(mz_handle* h) {
 // fuse_adam (world = 1) the ∇ is not stored: each parameter slice's block
 // applies the ADAM update (learning rate eta) right after reading θ for Σθ²
 static int learner_losses(mz_handle* h, const mz_batch* b, float* grad_dev, float* losses_dev, hipStream_t st,
-                          int v_act, int r_act, bool fuse_adam, double eta) {
+                          int v_act, int r_act, bool fuse_adam, double eta, bool l2_done) {
     const int B = b->batch_size, K = h->conf.num_unroll_steps, A = h->A;
     float* lo = losses_dev ? losses_dev : h->d_loss;
     float* g = grad_dev ? grad_dev : h->d_grad;
     const int gw = A > 16 ? 32 : 16;            // lanes per (sample, step) group
     const int nlb = (B * (K + 1) + MZ_THREADS / gw - 1) / (MZ_THREADS / gw);
     const LgAdam ad = adam_args(h, fuse_adam ? 1 : 0, eta);
-    hipLaunchKernelGGL(gw == 32 ? mz_learner_grad_kernel32 : mz_learner_grad_kernel, dim3(nlb + 3 * MZ_L2_BLOCKS), dim3(MZ_THREADS), 0, st, B, K, A,
+    // l2_done: the Σθ² slices (and the ADAM step) ran in the unroll launch; only the loss blocks and the fold
+    hipLaunchKernelGGL(gw == 32 ? mz_learner_grad_kernel32 : mz_learner_grad_kernel,
+                       dim3(nlb + (l2_done ? 0 : 3 * MZ_L2_BLOCKS)), dim3(MZ_THREADS), 0, st, B, K, A,
                        v_act, r_act, h->d_pv, h->d_pp, h->d_pr, b->target_values, b->target_policies,
                        b->gradient_scale, h->d_lterm, h->d_flat, h->d_netoff, g, h->d_sq, h->d_counter, lo, b->weights, ad);
     MZ_TRY(h, hipGetLastError());
-    if (fuse_adam) adam_advance(h);
+    if (fuse_adam && !l2_done) adam_advance(h);
     return 0;
 }
 

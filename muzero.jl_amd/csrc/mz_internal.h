@@ -18,7 +18,9 @@
 
 #define MZ_TILE 16          // games (or samples) per workgroup tile = MFMA N
 #define MZ_THREADS 256      // 4 wavefronts
+#ifndef MZ_L2_BLOCKS         // (-D override: timing A/B builds only; the oracle's order is NB below)
 #define MZ_L2_BLOCKS 128    // Σθ² / ∇ (/ fused ADAM) blocks per net in mz_learner_grad_kernel* (oracle ora_sqnorm: NB)
+#endif
 #define MZ_MAX_STAGES 64
 
 // One Dense layer inside a plan.  All offsets are in floats.

@@ -105,8 +105,9 @@ __device__ __forceinline__ void lg_step_terms(int t, int a, int A, int v_act, in
         if (a == 0) {
             pv[t] = y;
             const float d = y - tv[t];
-            vsq[t] = d * d;
-            cet[t] = ce;
+            // read by the last block's fold: agent-scope stores (lg_fold)
+            __hip_atomic_store(vsq + t, d * d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(cet + t, ce, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             pr[t] = y;
         }
@@ -209,11 +210,14 @@ __device__ __forceinline__ void lg_fold(int B, int K, const float* vsq, const fl
                                         const float* wts, const double* part, unsigned* counter, float* out) {
     __shared__ bool last;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // the block's fold inputs (loss terms, Σθ² partial) are agent-scope stores,
+    // complete once every wave has drained its stores; no per-block L2
+    // write-back / invalidate (a __threadfence in each of the 3·MZ_L2_BLOCKS +
+    // loss blocks cost 4 µs at 128 slices and 40 µs at 512)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
-        __threadfence();
-        last = atomicAdd(counter, 1u) == gridDim.x - 1;
-    }
+    if (tid == 0)
+        last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     __syncthreads();
     if (!last) return;
     __threadfence();

@@ -124,7 +124,7 @@ __device__ __forceinline__ void learner_grad_body(
         const int net = nb / MZ_L2_BLOCKS, blk = nb % MZ_L2_BLOCKS;
         red[tid] = lg_l2_slice(net, blk, tid, netoff, flat, G, ad);
         lg_tree256(red, tid);
-        if (tid == 0) part[net * MZ_L2_BLOCKS + blk] = red[0];
+        if (tid == 0) __hip_atomic_store(part + net * MZ_L2_BLOCKS + blk, red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     lg_fold(B, K, vsq, cet, gscale, wts, part, counter, out);
 }

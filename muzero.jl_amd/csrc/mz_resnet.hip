@@ -1390,8 +1390,9 @@ __device__ __forceinline__ void rd_layer(const RLayer& L, const float (&a)[NCH][
 template <int I, int NL, int NB>
 __device__ __forceinline__ void rd_run(const RPlan& Rd, const float (&a0)[2][4][4], const float (&ar)[NL][4][4],
                                        const float4* ep_lds, float* lds, int ncols, float bn_s, float bn_r,
-                                       unsigned long long* st) {
+                                       unsigned long long* st, int nrun = NL) {
     if constexpr (I < NL) {
+        if (I >= nrun) return;                          // (wave-uniform: the last step's trunk only)
         const RLayer L = rn_layer_at(Rd, I);
         if constexpr (I == 0) {
 #ifdef MZ_STAMPS
@@ -1409,7 +1410,7 @@ __device__ __forceinline__ void rd_run(const RPlan& Rd, const float (&a0)[2][4][
 #ifdef MZ_STAMPS
         if (st && (threadIdx.x & 63) == 0 && I < 31) st[(threadIdx.x >> 6) * 64 + 2 * I + 1] = __builtin_amdgcn_s_memtime();
 #endif
-        rd_run<I + 1, NL, NB>(Rd, a0, ar, ep_lds, lds, ncols, bn_s, bn_r, st);
+        rd_run<I + 1, NL, NB>(Rd, a0, ar, ep_lds, lds, ncols, bn_s, bn_r, st, nrun);
     }
     (void)st;
 }
@@ -1519,7 +1520,10 @@ __device__ __forceinline__ void runroll_chain_r_body(const RUnrollParams& U, int
             rn_stage_l(lds + Rd.in_off, Rd.in_kb, NG, U.P, Rd.in_feat, t, [&](int f) { return !ok ? 0.0f : f < H ? hp[f] * 2.0f : av; });
         }
         __syncthreads();
-        rd_run<0, NL, NB>(Rd, a0, ar, ep_lds, lds, ncols, U.bn_s, bn_r, s == 1 ? st_d : nullptr);   // :362, [0, split)
+        // :362, [0, split); the last step's state head is skipped: h_K is never read
+        // (predictions take h_0..h_{K-1}, the reward heads the trunk outputs)
+        rd_run<0, NL, NB>(Rd, a0, ar, ep_lds, lds, ncols, U.bn_s, bn_r, s == 1 ? st_d : nullptr,
+                          s < K ? NL : U.rd_trunk_nl);
         if (ok) {
             if (s < K) rn_unstage_l(lds + Rd.out0_off, Rd.out0_kb, NG, U.P, H, t, [&](int f, float v) {
                 if constexpr (FUSE) rd_st(hs + (size_t)s * H + f, v); else hs[(size_t)s * H + f] = v;
@@ -1652,6 +1656,8 @@ extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_pred_r(RUnro
     runroll_pred_r_body<false>(U, blockIdx.y == 1, blockIdx.x);
 }
 
+#include "mz_learner_device.h"
+
 // The whole B = small unroll in one launch: blocks [0, n_chain) are the chain
 // (representation + K dynamics steps of one sample, mz_runroll_chain_r, and
 // with fuse_sample its get_batch draw); the rest are the prediction and
@@ -1659,12 +1665,31 @@ extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_pred_r(RUnro
 // as soon as its sample's chain has published the input (rd_wait).  Blocks
 // dispatch in index order, so every chain block is resident before any item
 // waits on it; the waits are bounded.  Same arithmetic as the two launches.
+// Σθ² / ADAM block j of n_l2: slices j, j + n_l2, .. of the 3·MZ_L2_BLOCKS
+// (the slice decomposition of mz_learner_grad_kernel, so the same sums)
+__device__ __forceinline__ void runroll_l2_block(const RUnrollParams& U, int j) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    double* red = reinterpret_cast<double*>(lds);
+    const int tid = threadIdx.x;
+    for (int vb0 = 0; vb0 < 3 * MZ_L2_BLOCKS; vb0 += U.n_l2) {        // (block-uniform trip count)
+        const int vb = vb0 + j;
+        const bool vin = vb < 3 * MZ_L2_BLOCKS;
+        const int net = vb / MZ_L2_BLOCKS, blk = vb % MZ_L2_BLOCKS;
+        red[tid] = vin ? lg_l2_slice(net, blk, tid, U.netoff, U.flat_w, nullptr, U.ad) : 0.0;
+        lg_tree256(red, tid);
+        if (tid == 0 && vin)
+            __hip_atomic_store(U.part + net * MZ_L2_BLOCKS + blk, red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+    }
+}
+
 template <int NL, int NB>
 __device__ __forceinline__ void runroll_fused_r_body(const RUnrollParams& U) {
     const int bi = blockIdx.x;
     if (bi < U.n_chain) { runroll_chain_r_body<NL, NB, true>(U, bi); return; }
+    if (bi < U.n_chain + U.n_l2) { runroll_l2_block(U, bi - U.n_chain); return; }
     const int ny = U.K > 0 ? 2 : 1, KH = U.K > 0 ? U.K : 1;
-    const int idx = bi - U.n_chain, per_s = ny * U.B;
+    const int idx = bi - U.n_chain - U.n_l2, per_s = ny * U.B;
     const int s = idx / per_s, r = idx - s * per_s;
     const bool rew = r >= U.B;
     const int b = rew ? r - U.B : r;

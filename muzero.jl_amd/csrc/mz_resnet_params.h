@@ -183,6 +183,8 @@ struct RUnrollParams {
     float* ts;                         // [B][K][H] dynamics trunk outputs (split form: the reward heads' input)
     unsigned long long* stamps;        // -DMZ_STAMPS builds: per-layer ticks of chain block 0 (repr, dyn s = 1)
     int rd_ep_off;                     // mz_runroll_chain_r: LDS float offset of the staged epilogue parameters
+    int rd_trunk_nl;                   // mz_runroll_chain_r: the dynamics trunk's layers (1 + 2·num_blocks); the
+                                       // last step runs only these (its h_K feeds nothing in the unroll)
     // mz_runroll_fused_r (one launch: chain blocks [0, n_chain), then the B·K
     // prediction / reward-head items, each waiting for its sample's chain):
     // prog[b] = prog_base + p once the chain of sample b has stored h_0..h_{p-1}
@@ -191,6 +193,13 @@ struct RUnrollParams {
     int n_chain;
     int fuse_sample;                   // 1: chain block b draws sample b (get_batch, rq) first
     RpSampleParams rq;
+    // n_l2 > 0 (one GPU, ADAM fused): blocks [n_chain, n_chain + n_l2) take the
+    // Σθ² slices of mz_learner_grad_kernel (lg_l2_slice: Σθ² into part, ADAM on
+    // flat_w in place, the new MFMA image into ad.Wp = the second image set,
+    // which the kernels of this launch do not read); the loss kernel then runs
+    // without its slice blocks
+    int n_l2;
+    LgAdam ad; float* flat_w; const size_t* netoff; double* part;
 };
 // mz_runroll_chain_r: the dynamics chain's layers ([0, dyn_split) = RD_NL:
 // trunk + state head of 2-block towers) with register-resident A fragments

@@ -720,16 +720,21 @@ __device__ __forceinline__ void learn_body(const SmallUnrollParams& P, const Lea
         }
     } else {
         const int half = tid >> 8, t256 = tid & (MZ_THREADS - 1);
-        const int vb = (lb - L.nU) * SM_SLOTS + half;
-        const bool vin = vb < 3 * MZ_L2_BLOCKS;       // (SM_SLOTS not dividing the slice count: idle groups)
-        const int net = vb / MZ_L2_BLOCKS, blk = vb % MZ_L2_BLOCKS;
-        red[tid] = vin ? lg_l2_slice(net, blk, t256, L.netoff, L.flat, nullptr, L.ad) : 0.0;
-        __syncthreads();
-        for (int o = MZ_THREADS / 2; o > 0; o >>= 1) {            // lg_tree256 on each half
-            if (t256 < o) red[tid] += red[tid + o];
+        for (int pass = 0; pass < LEARN_L2_PASSES; ++pass) {       // (block-uniform trip count: barriers inside)
+            const int vb = (pass * LEARN_L2_GROUPS + lb - L.nU) * SM_SLOTS + half;
+            const bool vin = vb < 3 * MZ_L2_BLOCKS;
+            const int net = vb / MZ_L2_BLOCKS, blk = vb % MZ_L2_BLOCKS;
+            red[tid] = vin ? lg_l2_slice(net, blk, t256, L.netoff, L.flat, nullptr, L.ad) : 0.0;
             __syncthreads();
+            for (int o = MZ_THREADS / 2; o > 0; o >>= 1) {        // lg_tree256 on each half
+                if (t256 < o) red[tid] += red[tid + o];
+                __syncthreads();
+            }
+            if (t256 == 0 && vin)                  // agent scope: read by the fold (lg_fold)
+                __hip_atomic_store(L.part + net * MZ_L2_BLOCKS + blk, red[tid], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();                       // red[] reused by the next pass
         }
-        if (t256 == 0 && vin) L.part[net * MZ_L2_BLOCKS + blk] = red[tid];
     }
     lg_fold(P.B, P.K, vsq, cet, L.gscale, nullptr, L.part, L.counter, L.out);
 }
