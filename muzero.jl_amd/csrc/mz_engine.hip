@@ -935,6 +935,12 @@ static bool rp_pred_ok(const mz_handle* h) {
             !L.in_kb || L.K != 64 || L.nq != 4)
             return false;
     }
+    // the heads in rn_specs order: value [RP_NL, RP_NL + nv), policy after (the fused
+    // launch runs them in separate blocks)
+    const int nv = 3 + h->rhp.depth_value;
+    if (R.n != RP_NL + 2 * nv || R.L[RP_NL].cout != h->rhp.num_first_head_filters ||
+        R.L[RP_NL + nv].cout != h->rhp.num_second_head_filters || R.L[RP_NL + nv - 1].cout != 1)
+        return false;
     return rp_pred_lds(h) <= kLdsMax;
 }
 
@@ -2015,7 +2021,8 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
             U.flat_w = h->d_flat; U.netoff = h->d_netoff; U.part = h->d_sq;
             l2_fused = U.n_l2 > 0;
             h->last_lvariant = h->rd_nb == 3 ? "mz_runroll_fused_r3" : "mz_runroll_fused_r";
-            const int nitems = B * KH * (U.K > 0 ? 2 : 1);
+            U.rp_nv = 3 + h->rhp.depth_value;       // value head: conv, Dense, depth_value × Dense, Dense
+            const int nitems = B * KH * (U.K > 0 ? 3 : 2);
             MZ_TRY(h, hipLaunchKernel(h->rd_nb == 3 ? (const void*)mz_runroll_fused_r3 : (const void*)mz_runroll_fused_r,
                                       dim3(B + U.n_l2 + nitems), dim3(RD_THREADS), args,
                                       std::max(rd_chain_lds(h), rp_pred_lds(h)), st));

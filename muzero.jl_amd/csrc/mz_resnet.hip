@@ -339,6 +339,15 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
                         bv[h][3] = *reinterpret_cast<const float*>(lb + o[h].w);
                     }
                 };
+                // A fragments two chunks ahead (an: chunk c + 1, an2: chunk c + 2, in
+                // the wave's (unit, chunk) order): an L2 round trip is longer than
+                // one chunk's 16 MFMAs (3x3 convs: 11.7 k ticks for 9 chunks with
+                // one chunk of look-ahead)
+                float an2[4][4];
+                {
+                    const int un = u + (1 / nch4) * nwaves, cn = 1 % nch4;
+                    if (un < units) rn_load_a(an2, Wimg, L, un / n_grp, cn, lane);
+                }
                 int4 o1[4];
                 float bv[4][4];
                 rd_o(0, o1);
@@ -349,10 +358,10 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
 #pragma unroll
-                        for (int jj = 0; jj < 4; ++jj) ac[q][jj] = an[q][jj];
+                        for (int jj = 0; jj < 4; ++jj) { ac[q][jj] = an[q][jj]; an[q][jj] = an2[q][jj]; }
                     {
-                        const int un = c + 1 < nch4 ? u : u + nwaves, cn = c + 1 < nch4 ? c + 1 : 0;
-                        if (un < units) rn_load_a(an, Wimg, L, un / n_grp, cn, lane);
+                        const int un = u + ((c + 2) / nch4) * nwaves, cn = (c + 2) % nch4;
+                        if (un < units) rn_load_a(an2, Wimg, L, un / n_grp, cn, lane);
                     }
                     float bn[4][4];
                     int4 o2[4];
@@ -1235,7 +1244,7 @@ __device__ __forceinline__ void runroll_chain_body(const RUnrollParams& U) {
     unsigned long long* st_r = nullptr;
     unsigned long long* st_d = nullptr;
 #ifdef MZ_STAMPS
-    if (U.stamps && tile == 0) { st_r = U.stamps; st_d = U.stamps + 512; }
+    if (U.stamps && blockIdx.x == 0) { st_r = U.stamps; st_d = U.stamps + 512; }
 #endif
     rn_fill_ktabs(Rr, lds, NG, U.W, U.P);
     if (Rr.tab_n) {                                 // the representation's offset tables (+ the zero float)
@@ -1434,6 +1443,9 @@ __device__ __forceinline__ void rd_publish(const RUnrollParams& U, int b, int p)
     __syncthreads();
     if (threadIdx.x == 0)
         __hip_atomic_store(U.prog + b, U.prog_base + (unsigned long long)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef MZ_STAMPS
+    if (U.stamps && threadIdx.x == 0) U.stamps[2048 + 4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 __device__ __forceinline__ void rd_wait(const RUnrollParams& U, int b, int p) {
     if (threadIdx.x == 0) {
@@ -1442,6 +1454,9 @@ __device__ __forceinline__ void rd_wait(const RUnrollParams& U, int b, int p) {
             if (__hip_atomic_load(U.prog + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
             __builtin_amdgcn_s_sleep(2);
         }
+#ifdef MZ_STAMPS
+        if (U.stamps) U.stamps[2048 + 4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
     }
     __syncthreads();
 }
@@ -1599,9 +1614,11 @@ __device__ __forceinline__ void rp_run(const RPlan& R, const float (&ar)[RP_NL][
 }
 
 // FUSE: an item of mz_runroll_fused_r (ng_l = 1: tile = item b·KH + s), which
-// waits until the chain of sample b has published its input
+// waits until the chain of sample b has published its input; head (prediction
+// items): 0 both heads, 1 the value head only, 2 the policy head only (each
+// block runs the trunk, then its head: the two heads side by side)
 template <bool FUSE>
-__device__ __forceinline__ void runroll_pred_r_body(const RUnrollParams& U, bool rew, int tile) {
+__device__ __forceinline__ void runroll_pred_r_body(const RUnrollParams& U, bool rew, int tile, int head = 0) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const RPlan& R = U.plans_l[rew ? MZ_NET_DYN : MZ_NET_PRED];
     const int NG = U.ng_l, H = U.H, A = U.A, K = U.K, K1 = K + 1, KH = K > 0 ? K : 1;
@@ -1635,7 +1652,8 @@ __device__ __forceinline__ void runroll_pred_r_body(const RUnrollParams& U, bool
     __syncthreads();
     if (!rew) {
         rp_run<0>(R, ar, ep_lds, lds, U.P * NG, U.bn_s, 1.0f / U.bn_s);                    // trunk (:351 / :356)
-        rn_run<true, true, 1>(R, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, nullptr, RP_NL);   // heads
+        const int h0 = head == 2 ? RP_NL + U.rp_nv : RP_NL, h1 = head == 1 ? RP_NL + U.rp_nv : -1;
+        rn_run<true, true, 1>(R, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, nullptr, h0, h1);   // heads
     } else {
         rn_run<true, true, 1>(R, U.Wimg, U.flat, lds, NG, U.W, U.P, U.bn_s, nullptr, i0);      // :362 reward head
     }
@@ -1647,9 +1665,9 @@ __device__ __forceinline__ void runroll_pred_r_body(const RUnrollParams& U, bool
         return;
     }
     for (int j = s == 0 ? 0 : s + 1; j <= (s + 1 <= K ? s + 1 : 0); ++j) {
-        if (t.f0 == 0) U.pv[b * K1 + j] = lds[R.out0_off + t.g];
+        if (head != 2 && t.f0 == 0) U.pv[b * K1 + j] = lds[R.out0_off + t.g];
         float* o = U.pp + (b * K1 + j) * A;
-        rn_unstage(lds + R.out1_off, NG, A, t, [&](int f, float v) { o[f] = v; });
+        if (head != 1) rn_unstage(lds + R.out1_off, NG, A, t, [&](int f, float v) { o[f] = v; });
     }
 }
 extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_pred_r(RUnrollParams U) {
@@ -1686,14 +1704,23 @@ __device__ __forceinline__ void runroll_l2_block(const RUnrollParams& U, int j) 
 template <int NL, int NB>
 __device__ __forceinline__ void runroll_fused_r_body(const RUnrollParams& U) {
     const int bi = blockIdx.x;
-    if (bi < U.n_chain) { runroll_chain_r_body<NL, NB, true>(U, bi); return; }
-    if (bi < U.n_chain + U.n_l2) { runroll_l2_block(U, bi - U.n_chain); return; }
-    const int ny = U.K > 0 ? 2 : 1, KH = U.K > 0 ? U.K : 1;
+#ifdef MZ_STAMPS   // diagnostic build: per block {start, input published / chain's last publish, end} (s_memrealtime)
+    unsigned long long* fs = U.stamps ? U.stamps + 2048 + 4 * bi : nullptr;
+    if (fs && threadIdx.x == 0) fs[0] = __builtin_amdgcn_s_memrealtime();
+#define RD_FS_END() do { if (fs && threadIdx.x == 0) fs[2] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define RD_FS_END() do {} while (0)
+#endif
+    if (bi < U.n_chain) { runroll_chain_r_body<NL, NB, true>(U, bi); RD_FS_END(); return; }
+    if (bi < U.n_chain + U.n_l2) { runroll_l2_block(U, bi - U.n_chain); RD_FS_END(); return; }
+    // per step: B value-head items, B policy-head items, B reward heads (K > 0)
+    const int ny = U.K > 0 ? 3 : 2, KH = U.K > 0 ? U.K : 1;
     const int idx = bi - U.n_chain - U.n_l2, per_s = ny * U.B;
-    const int s = idx / per_s, r = idx - s * per_s;
-    const bool rew = r >= U.B;
-    const int b = rew ? r - U.B : r;
-    runroll_pred_r_body<true>(U, rew, b * KH + s);
+    const int s = idx / per_s, r = idx - s * per_s, role = r / U.B;
+    const int b = r - role * U.B;
+    runroll_pred_r_body<true>(U, role == 2, b * KH + s, role == 2 ? 0 : role + 1);
+    RD_FS_END();
+#undef RD_FS_END
 }
 extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_fused_r(RUnrollParams U) {
     runroll_fused_r_body<RD_NL, 1>(U);

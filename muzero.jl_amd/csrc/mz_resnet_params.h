@@ -200,6 +200,8 @@ struct RUnrollParams {
     // without its slice blocks
     int n_l2;
     LgAdam ad; float* flat_w; const size_t* netoff; double* part;
+    int rp_nv;                         // the prediction plan's value-head layers ([RP_NL, RP_NL + rp_nv)); the
+                                       // fused launch runs the value and the policy head of an item in two blocks
 };
 // mz_runroll_chain_r: the dynamics chain's layers ([0, dyn_split) = RD_NL:
 // trunk + state head of 2-block towers) with register-resident A fragments
