@@ -339,15 +339,6 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
                         bv[h][3] = *reinterpret_cast<const float*>(lb + o[h].w);
                     }
                 };
-                // A fragments two chunks ahead (an: chunk c + 1, an2: chunk c + 2, in
-                // the wave's (unit, chunk) order): an L2 round trip is longer than
-                // one chunk's 16 MFMAs (3x3 convs: 11.7 k ticks for 9 chunks with
-                // one chunk of look-ahead)
-                float an2[4][4];
-                {
-                    const int un = u + (1 / nch4) * nwaves, cn = 1 % nch4;
-                    if (un < units) rn_load_a(an2, Wimg, L, un / n_grp, cn, lane);
-                }
                 int4 o1[4];
                 float bv[4][4];
                 rd_o(0, o1);
@@ -358,10 +349,10 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
 #pragma unroll
-                        for (int jj = 0; jj < 4; ++jj) { ac[q][jj] = an[q][jj]; an[q][jj] = an2[q][jj]; }
+                        for (int jj = 0; jj < 4; ++jj) ac[q][jj] = an[q][jj];
                     {
-                        const int un = u + ((c + 2) / nch4) * nwaves, cn = (c + 2) % nch4;
-                        if (un < units) rn_load_a(an2, Wimg, L, un / n_grp, cn, lane);
+                        const int un = c + 1 < nch4 ? u : u + nwaves, cn = c + 1 < nch4 ? c + 1 : 0;
+                        if (un < units) rn_load_a(an, Wimg, L, un / n_grp, cn, lane);
                     }
                     float bn[4][4];
                     int4 o2[4];

@@ -28,7 +28,7 @@ fi
 if [ -z "$SKIP_RESNET" ]; then
 BR="--net resnet --steps 4 --warmup 1 --no-cpu --pipeline-moves 0 --train-moves 0 --learner-steps 10"
 run kt_resnet 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_resnet -o run -- python bench.py --net resnet
-pmc resnet "$BR" mz_rsearch_nets mz_runroll_chain_r mz_runroll_pred_r mz_runroll_pred_n1 mz_rsearch_tree_lds mz_rsearch_root mz_learner_grad_kernel
+pmc resnet "$BR" mz_rsearch_nets mz_runroll_fused_r mz_runroll_chain_r mz_runroll_pred_r mz_runroll_pred_n1 mz_rsearch_tree_lds mz_rsearch_root mz_learner_grad_kernel
 fi
 if [ -z "$SKIP_ATARI" ]; then
 BA="--game atari --steps 2 --warmup 1 --no-cpu --learner-steps 10"
