@@ -169,6 +169,9 @@ struct mz_handle {
     int rd_nb = 1;                          // its column blocks (1: mz_runroll_chain_r, 3: _r3)
     bool rp_pred = false;                   // one-item predictions run as mz_runroll_pred_r (rp_pred_ok)
     unsigned long long* d_prog = nullptr;   // [bcap] mz_runroll_fused_r progress words
+    float* d_rtrunk = nullptr;              // [max_games][H] dynamics trunk outputs (mz_rsearch_nets rew_split)
+    unsigned long long* d_tprog = nullptr;  // [tiles] their publish words
+    unsigned long long tprog_epoch = 0;     // mz_rsearch_nets launches
     unsigned long long prog_epoch = 0;      // launches of mz_runroll_fused_r (prog_base = epoch · 64)
     std::vector<int> rtab;                  // offset tables of the narrow (chain) plans
     int* d_rtab = nullptr;
@@ -1718,6 +1721,17 @@ static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     void* args[] = {&P};
     const int gw = h->A > 16 ? 32 : 16;             // lanes per game in the tree kernels
     const unsigned tiles = (unsigned)((G + P.ng - 1) / P.ng), groups = (unsigned)((G + 256 / gw - 1) / (256 / gw));
+    // the dynamics reward head on the prediction workgroup (RSearchParams.rew_split)
+    static const bool no_rsplit = std::getenv("MZ_RN_NO_RSPLIT") != nullptr;
+    if (!no_rsplit && !h->d_rtrunk) {
+        const size_t mt = (size_t)(h->max_games + P.ng - 1) / P.ng;
+        MZ_TRY(h, dalloc(h, &h->d_rtrunk, (size_t)h->max_games * h->H));
+        MZ_TRY(h, dalloc(h, &h->d_tprog, mt));
+        MZ_TRY(h, hipMemset(h->d_tprog, 0, mt * sizeof(unsigned long long)));
+    }
+    P.rew_split = no_rsplit ? 0 : 1;
+    P.trunk_nl = 1 + 2 * h->rhp.num_blocks; P.dyn_split = h->rn_dyn_split;
+    P.trunk = h->d_rtrunk; P.tprog = h->d_tprog;
     const void* kroot = gw == 32 ? (const void*)mz_rsearch_root32 : (const void*)mz_rsearch_root;
     // tree step: LDS-cached (one wave per 64/gw games) unless the tree exceeds the LDS
     const bool tl = h->rtree_lds != 0;
@@ -1740,6 +1754,7 @@ static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
             e0 = h->tev[h->tev_used++]; e1 = h->tev[h->tev_used++];
             MZ_TRY(h, hipEventRecord(e0, st));
         }
+        P.tepoch = ++h->tprog_epoch;
         MZ_TRY(h, hipLaunchKernel((const void*)mz_rsearch_nets, dim3(tiles, 2), dim3(RN_THREADS_NETS), args,
                                   rsearch_nets_lds(h), st));
         if (e1) MZ_TRY(h, hipEventRecord(e1, st));

@@ -1084,10 +1084,14 @@ extern "C" __global__ __launch_bounds__(64) void mz_rsearch_tree_lds32(RSearchPa
 }
 
 // Networks of simulation s: blockIdx.y = 0 prediction(parent h), 1 dynamics
-// (2h ⊕ a/|A|, Q1) writing h' into hidden slot s+1.
+// (2h ⊕ a/|A|, Q1) writing h' into hidden slot s+1.  With P.rew_split the
+// dynamics is y = 0 (the producer, dispatched first: no consumer can occupy
+// the CU its producer needs) and the prediction workgroup of the tile runs the
+// dynamics reward head after its own heads, on the published trunk output.
 extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RSearchParams P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int net = blockIdx.y == 0 ? MZ_NET_PRED : MZ_NET_DYN;
+    const bool split = P.rew_split != 0;
+    const int net = (blockIdx.y == 0) != split ? MZ_NET_PRED : MZ_NET_DYN;
 #ifdef RN_DIAG_ONLY          // diagnostic builds (wrong results): time one net alone
     if ((int)blockIdx.y != RN_DIAG_ONLY) return;
 #endif
@@ -1133,6 +1137,51 @@ extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RS
     // the k-table path is left out of this kernel (registers: the 12-wave cap)
     // (the PF prefetch set does not fit the 12-wave register budget: 200 spilled VGPRs, and an A-only
     // prefetch into the layer's own registers measured 76 vs 70 µs)
+    if (split) {
+        if (net == MZ_NET_DYN) {
+            rn_run<false, false, 3, false, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st, 0, P.trunk_nl);
+            const RLayer Ls = rn_layer_at(R, P.dyn_split);             // the reward head's input: the trunk output
+            if (ok)
+                rn_unstage_l(lds + Ls.in_off, Ls.in_kb, NG, P.P, H, t, [&](int f, float v) {
+                    __hip_atomic_store(P.trunk + (size_t)gg * H + f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                });
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");            // every wave's stores performed
+            __syncthreads();
+            if (threadIdx.x == 0)
+                __hip_atomic_store(P.tprog + blockIdx.x, P.tepoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            rn_run<false, false, 3, false, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, nullptr, P.trunk_nl,
+                                                 P.dyn_split);                        // the state head
+            if (ok) {
+                float* o = P.hid + ((size_t)gg * (S + 1) + P.s + 1) * H;
+                rn_unstage_l(lds + R.out0_off, R.out0_kb, NG, P.P, H, t, [&](int f, float v) { o[f] = v; });
+            }
+            return;
+        }
+        rn_run<false, false, 3, false, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st);
+        if (ok) {
+            if (t.f0 == 0) P.o_v[gg] = lds[R.out0_off + t.g];
+            float* o = P.o_logit + (size_t)gg * P.A;
+            rn_unstage(lds + R.out1_off, NG, P.A, t, [&](int f, float v) { o[f] = v; });
+        }
+        __syncthreads();                                              // the outputs read before the LDS is reused
+        if (threadIdx.x == 0)                                         // (bounded: no hang if never published)
+            for (int n = 0; n < (1 << 21); ++n) {
+                if (__hip_atomic_load(P.tprog + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= P.tepoch)
+                    break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+        __syncthreads();
+        const RPlan& Rd = P.plans[MZ_NET_DYN];
+        const RLayer Ls = rn_layer_at(Rd, P.dyn_split);
+        rn_stage_l(lds + Ls.in_off, Ls.in_kb, NG, P.P, H, t, [&](int f) {
+            return ok ? __hip_atomic_load(P.trunk + (size_t)gg * H + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : 0.0f;
+        });
+        __syncthreads();
+        rn_run<false, false, 3, false, true>(Rd, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, nullptr, P.dyn_split);
+        if (ok && t.f0 == 0) P.o_r[gg] = lds[Rd.out1_off + t.g];
+        return;
+    }
     rn_run<false, false, 3, false, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st);
 #ifdef MZ_STAMPS
     if (st && (threadIdx.x & 63) == 0) st[(threadIdx.x >> 6) * 64 + 61] = __builtin_amdgcn_s_memtime();

@@ -140,6 +140,13 @@ struct RSearchParams {
     const RPlan* plans;    // repr, pred, dyn
     unsigned long long* stamps;   // -DMZ_STAMPS builds: per-layer ticks of nets blocks (0,0), (0,1)
     const float* Wimg; const float* flat;
+    // rew_split (mz_rsearch_nets): y = 0 runs the dynamics trunk, publishes its
+    // output (trunk[G][H], agent-scope stores, then tprog[tile] = tepoch) and runs
+    // the state head; y = 1 runs the prediction, then the dynamics reward head
+    // ([dyn_split, n)) on the published trunk output — the two workgroups of a
+    // tile carry about equal work instead of 101 k / 142 k ticks
+    int rew_split, trunk_nl, dyn_split;
+    float* trunk; unsigned long long* tprog; unsigned long long tepoch;
 };
 
 // LDS layout of the LDS-cached tree step (mz_rsearch_tree_lds*): one wave per
