@@ -1173,7 +1173,6 @@ EXPORT int ora_eval_play(const mz_config* c, const ora_nethp* hp, const float* P
     OCtx X; ctx_init(&X, c, hp, Prep, Ppred, Pdyn, seed);
     float* s_obs = calloc((size_t)G * Tm * OS, 4); int32_t* s_act = calloc((size_t)G * Tm, 4);
     int* s_len = calloc(G, sizeof(int));
-    float* s_temp = calloc(G, sizeof(float));
     OTTT* env = malloc(sizeof(OTTT) * G);
     for (int g = 0; g < G; ++g) ttt_reset(&env[g]);
     float stacked[1024];
