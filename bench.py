@@ -123,7 +123,28 @@ def cpu_baseline(conf, hyper, nets, obs, legal, tp, budget_s=10.0, resnet=False,
     n_games = sum(counts)
     return dict(value=n_games * conf.num_iters / dt, unit="node-expansions/s", cores=threads, kind="port",
                 sample=f"{n_games} games x {conf.num_iters} sims ({batch}-game batches of the bench positions), "
-                       f"oracle/mz_oracle.c on {threads} host thread{'s' if threads > 1 else ''}, {dt:.1f} s")
+                       f"oracle/mz_oracle.c on {threads} host thread{'s' if threads > 1 else ''}, {dt:.1f} s",
+                **host_cpu())
+
+
+def host_cpu():
+    """The host the CPU baseline ran on: logical CPUs of the machine
+    (os.cpu_count: the whole box, not this job's share), the CPUs this
+    process may run on, and the CPU model (/proc/cpuinfo)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return dict(host_cpus=os.cpu_count(), host_cpus_allowed=affinity, cpu_model=model)
 
 
 def pmc_record(kernel, line=None):
@@ -374,7 +395,7 @@ def main():
             if world == 1:                                  # get_batch + unroll, losses + ADAM: two launches
                 eng.learner_train_dev(B, k + 1, cos_schedule(k + 1), losses.data_ptr(), stream=sp)
                 return
-            else:                                             # get_batch fused into the unroll; ∇ exchanged
+            else:                  # get_batch fused into the unroll; the data term of ∇ exchanged, 2θ added by apply
                 eng.learner_grad_sampled_dev(B, k + 1, grad.data_ptr(), losses.data_ptr(), stream=sp)
             if world > 1:
                 dist.all_reduce(grad)

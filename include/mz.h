@@ -246,9 +246,15 @@ enum { MZ_LEARN_REF_SEMANTICS = 0, MZ_LEARN_CORRECTED = 1 };
 int mz_learner_set_mode(mz_handle* h, int mode);
 
 /* Split learner step for data-parallel training: (1) forward + losses +
- * gradient into grad_dev (device, mz_grad_count floats), (2) the caller
- * all-reduces (sum) grad_dev across ranks, (3) apply ADAM with scale
- * 1/world.  Stream-ordered on `stream`.                                   */
+ * the DATA TERM of the gradient into grad_dev (device, mz_grad_count
+ * floats): ∂/∂θ of the loss without Σθ² — zero in ref_semantics (Q11),
+ * the backpropagated term in the corrected mode; (2) the caller all-reduces
+ * (sum) grad_dev across ranks; (3) mz_learner_apply_dev runs ADAM on
+ * ∇ = grad_dev · grad_scale + 2θ (grad_scale = 1/world).  The rank-invariant
+ * 2θ = ∂Σθ²/∂θ is added after the exchange, so the update equals the
+ * single-GPU update bit for bit at every world size in ref_semantics (an
+ * exchanged 2θ would be summed in f32 and round differently at world 8).
+ * Stream-ordered on `stream`.                                              */
 int mz_grad_count(const mz_handle* h, size_t* n);
 int mz_learner_grad_dev(mz_handle* h, const mz_batch* dev_batch, float* grad_dev,
                         float* losses_dev, void* stream);
@@ -262,8 +268,8 @@ int mz_learner_apply_dev(mz_handle* h, const float* grad_dev, float grad_scale,
  * RemoteChannel / Distributed.jl of the reference host); each rank calls
  * mz_dp_init.  mz_dp_allreduce sums the gradient bucket (mz_grad_count
  * floats, grad_dev or the handle's gradient if NULL) in place over RCCL on
- * `stream`; mz_learner_train_dp = mz_learner_grad_sampled_dev + that
- * all-reduce + mz_learner_apply_dev(1/world).  librccl.so.1 is loaded on
+ * `stream`; mz_learner_train_dp = mz_learner_grad_sampled_dev (data term)
+ * + that all-reduce + mz_learner_apply_dev(1/world, + 2θ).  librccl.so.1 is loaded on
  * first use (the copy already in the process if any).                      */
 #define MZ_DP_ID_BYTES 128
 int mz_dp_unique_id(uint8_t* id);
@@ -287,7 +293,9 @@ enum { MZ_ENV_TICTACTOE = 0, MZ_ENV_CONNECT4 = 1, MZ_ENV_ATARI = 2 };
  * (84,84,4)/18 actions with stacked_observations = 0: Philox-keyed frames,
  * rules in muzero.jl_amd/games/atari_synth.py; the records and the shard
  * hold one 84x84 byte frame per move and the observation is the env's
- * four-frame stack).  Calling it again discards the state.                 */
+ * four-frame stack; its slots' initial games are drawn at the first
+ * mz_selfplay_move, keyed by that move's global game ids game_offset + slot).
+ * Calling it again discards the state.                                      */
 int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games);
 
 /* One move of every slot, on the device, stream-ordered: observation append

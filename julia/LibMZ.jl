@@ -202,7 +202,7 @@ function dp_unique_id()                        # on rank 0; send the 128 bytes t
 end
 dp_init!(e::Engine, rank, world, id) =
     check(e, ccall((:mz_dp_init, libmz), Cint, (Ptr{Cvoid}, Cint, Cint, Ptr{UInt8}), e.h, rank, world, id))
-learner_train_dp!(e::Engine, B, step, eta; losses=C_NULL) =   # grad + RCCL all-reduce + ADAM(1/world)
+learner_train_dp!(e::Engine, B, step, eta; losses=C_NULL) =   # data term, RCCL all-reduce, ADAM(1/world, + 2θ)
     check(e, ccall((:mz_learner_train_dp, libmz), Cint, (Ptr{Cvoid}, Int32, UInt32, Float64, Ptr{Float32}, Ptr{Cvoid}),
                    e.h, B, step, eta, losses, C_NULL))
 

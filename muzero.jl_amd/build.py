@@ -13,7 +13,7 @@ SOURCES = ["mz_engine.hip", "mz_search.hip", "mz_small.hip", "mz_nets.hip", "mz_
            "mz_downsample.hip", "mz_checkpoint.cpp", "mz_backprop.hip"]
 HEADERS = ["mz_internal.h", "mz_mlp_device.h", "mz_tree_device.h", "mz_small_params.h", "mz_resnet_params.h",
            "mz_selfplay_params.h", "mz_ckpt_iface.h", "mz_replay_device.h", "mz_learner_device.h",
-           "mz_backprop_params.h"]
+           "mz_backprop_params.h", "mz_st_header.h"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
          # the numerics contract (include/mz_detmath.h): no FP contraction, IEEE
          # division/sqrt, f32 denormals kept (hipcc defaults for the last two)

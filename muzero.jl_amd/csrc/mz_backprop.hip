@@ -10,9 +10,11 @@
 //               operand is loaded (the dW kernel forms it the same way).
 //   mz_bp_dw    one wave per 16x16 block of a layer's dW: Σ over tiles, the
 //               layer's applications and the 16 samples of dZ ⊗ x (MFMA with
-//               K = samples), + 2θ (∂Σθ²/∂θ); one wave per bias block.
+//               K = samples): the data term of the gradient; one wave per
+//               bias block.
 //   mz_bp_fold  Σθ² per net and the reported losses (deterministic f64 trees).
-// The ADAM step that follows is mz_adam_kernel (gradient scale 1/world).
+// The ADAM step that follows is mz_adam_kernel: ∇ = (Σ_ranks data term) ·
+// 1/world + 2θ, the rank-invariant ∂Σθ²/∂θ added after the exchange.
 #include "mz_internal.h"
 #include "mz_backprop_params.h"
 
@@ -394,7 +396,7 @@ extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
     const BpJob J = Q.jobs[blockIdx.x];
     const BpLayer L = Q.layers[J.layer];
     const int lane = threadIdx.x, m = lane & 15, kq = lane >> 4;
-    if (J.ib < 0) {                                           // db = Σ dZ, + 2b
+    if (J.ib < 0) {                                           // db = Σ dZ (data term)
         const int o = J.ob * 16 + lane;
         const bool in = lane < 16 && o < L.out;
         double q = 0.0;
@@ -406,7 +408,7 @@ extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
                     for (int j = 0; j < 16; ++j) s += bp_dz(L.act, Q.grad[e + j], Q.act[e + j]);
                 }
             const float th = Q.flat[L.b_off + o];
-            Q.out[L.b_off + o] = s + 2.0f * th;
+            Q.out[L.b_off + o] = s;                               // data term (2θ: mz_adam_kernel)
             q = (double)th * (double)th;
         }
         for (int d = 32; d > 0; d >>= 1) q += __shfl_xor(q, d);    // fixed tree: Σθ² of the block
@@ -437,7 +439,7 @@ extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
         if (oo < L.out && iin) {
             const size_t p = (size_t)L.w_off + oo + (size_t)L.out * i;
             const float th = Q.flat[p];
-            Q.out[p] = acc[r] + 2.0f * th;
+            Q.out[p] = acc[r];
             q += (double)th * (double)th;
         }
     }
@@ -750,7 +752,8 @@ extern "C" __global__ __launch_bounds__(RBP_THREADS) void mz_rbp_sample(RbpParam
     }
 }
 
-// Σ over samples (ascending) + 2θ, and Σθ² of each chunk (f64, fixed tree)
+// Σ over samples (ascending) = the data term, and Σθ² of each chunk (f64,
+// fixed tree); mz_adam_kernel adds 2θ after the data-parallel exchange
 extern "C" __global__ __launch_bounds__(256) void mz_rbp_reduce(RbpReduceParams R) {
     __shared__ double red[256];
     const int tid = threadIdx.x, s0 = R.chunk_start[blockIdx.x], s1 = R.chunk_start[blockIdx.x + 1];
@@ -759,7 +762,7 @@ extern "C" __global__ __launch_bounds__(256) void mz_rbp_reduce(RbpReduceParams 
         float s = 0.0f;
         for (int b = 0; b < R.B; ++b) s += R.gsam[(size_t)b * R.nflat + i];
         const float th = R.flat[i];
-        R.out[i] = s + 2.0f * th;
+        R.out[i] = s;
         q += (double)th * (double)th;
     }
     red[tid] = q;

@@ -83,7 +83,7 @@ struct BpDwParams {
     int tiles, tile_floats, n_job;
     const BpJob* jobs; const BpLayer* layers; const BpUse* uses;
     const float* act; const float* grad; const float* flat;
-    float* out;                           // Flux-order gradient (data term + 2θ)
+    float* out;                           // Flux-order data term of the gradient (2θ: mz_adam_kernel)
     double* sq;                           // [n_job]: Σθ² of each job's parameter block (f64, fixed order)
 };
 
@@ -105,7 +105,7 @@ struct BpFoldParams {
 // test-mode affine γ·(t/√(1+ε)) + β; a block's second conv adds the saved
 // input before its relu.  Each sample accumulates its own parameter gradient
 // (the backward's dW, db, dβ, dγ) in gsam[b]; mz_rbp_reduce sums the samples
-// in ascending order and adds 2θ.
+// in ascending order (the data term; mz_adam_kernel adds 2θ).
 enum { RBP_CONV = 0, RBP_DENSE = 1, RBP_CONCAT = 2 };
 
 struct RbpApp {
@@ -132,7 +132,7 @@ struct RbpParams {
 struct RbpReduceParams {
     int B, nflat, chunk;
     const float* gsam; const float* flat;
-    float* out;                           // Flux-order gradient (data term + 2θ)
+    float* out;                           // Flux-order data term of the gradient (2θ: mz_adam_kernel)
     double* sq;                           // [blocks]: Σθ² of each chunk (no chunk straddles two nets)
     const int* chunk_start;               // [blocks + 1]
 };

@@ -26,76 +26,9 @@
 #include <vector>
 
 #include "mz_ckpt_iface.h"
+#include "mz_st_header.h"
 
 namespace {
-
-// ---- a minimal JSON reader for the safetensors header
-struct JV {
-    enum T { NUL, NUM, STR, ARR, OBJ } t = NUL;
-    double num = 0;
-    std::string str;
-    std::vector<JV> arr;
-    std::map<std::string, JV> obj;
-};
-
-struct JP {
-    const char* p;
-    const char* e;
-    bool ok = true;
-    void ws() { while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p; }
-    bool eat(char c) { ws(); if (p < e && *p == c) { ++p; return true; } return false; }
-    std::string string() {
-        std::string s;
-        if (!eat('"')) { ok = false; return s; }
-        while (p < e && *p != '"') {
-            if (*p == '\\' && p + 1 < e) {
-                ++p;
-                const char c = *p++;
-                if (c == 'n') s += '\n'; else if (c == 't') s += '\t'; else if (c == 'u') { s += '?'; p += 4; }
-                else s += c;
-            } else {
-                s += *p++;
-            }
-        }
-        if (p >= e) { ok = false; return s; }
-        ++p;
-        return s;
-    }
-    JV value() {
-        JV v;
-        ws();
-        if (p >= e) { ok = false; return v; }
-        if (*p == '{') {
-            ++p;
-            v.t = JV::OBJ;
-            if (eat('}')) return v;
-            do {
-                std::string k = string();
-                if (!eat(':')) { ok = false; return v; }
-                v.obj[k] = value();
-            } while (ok && eat(','));
-            if (!eat('}')) ok = false;
-        } else if (*p == '[') {
-            ++p;
-            v.t = JV::ARR;
-            if (eat(']')) return v;
-            do v.arr.push_back(value()); while (ok && eat(','));
-            if (!eat(']')) ok = false;
-        } else if (*p == '"') {
-            v.t = JV::STR;
-            v.str = string();
-        } else if (!strncmp(p, "null", 4) && p + 4 <= e) {
-            p += 4;
-        } else {
-            char* q = nullptr;
-            v.t = JV::NUM;
-            v.num = strtod(p, &q);
-            if (q == p) ok = false;
-            p = q;
-        }
-        return v;
-    }
-};
 
 std::string esc(const std::string& s) {
     std::string o;
@@ -168,31 +101,19 @@ int mz_checkpoint_load(mz_handle* h, const char* path, int64_t* training_step) {
     if (std::fread(&hl, 8, 1, f) != 1 || hl > (1u << 28)) return mz_set_error(h, "not a safetensors file");
     std::string hdr(hl, '\0');
     if (std::fread(&hdr[0], 1, hl, f) != hl) return mz_set_error(h, "truncated header");
-    JP jp{hdr.data(), hdr.data() + hdr.size()};
-    JV root = jp.value();
-    if (!jp.ok || root.t != JV::OBJ) return mz_set_error(h, "bad safetensors header");
+    mzst::JV root;
+    const std::string perr = mzst::parse_header(hdr.data(), hdr.size(), &root);
+    if (!perr.empty()) return mz_set_error(h, perr);
     std::fseek(f, 0, SEEK_END);
     const long long fsize = std::ftell(f);
-    const long long base = 8 + (long long)hl;
     auto read = [&](const std::string& name, const char* dtype, size_t esz, std::vector<int64_t> shape,
                     void* dst) -> int {
-        auto it = root.obj.find(name);
-        if (it == root.obj.end() || it->second.t != JV::OBJ) return mz_set_error(h, "checkpoint lacks " + name);
-        const JV& e = it->second;
-        auto dt = e.obj.find("dtype");
-        auto sh = e.obj.find("shape");
-        auto of = e.obj.find("data_offsets");
-        if (dt == e.obj.end() || sh == e.obj.end() || of == e.obj.end() || of->second.arr.size() != 2)
-            return mz_set_error(h, "bad header entry " + name);
-        if (dt->second.str != dtype) return mz_set_error(h, name + ": dtype " + dt->second.str + ", expected " + dtype);
-        std::vector<int64_t> got;
-        for (const JV& x : sh->second.arr) got.push_back((int64_t)x.num);
-        if (got != shape) return mz_set_error(h, name + ": shape differs from this engine's network");
+        long long off = 0;
+        const std::string err = mzst::entry_span(root, name, dtype, esz, shape, hl, fsize, &off);
+        if (!err.empty()) return mz_set_error(h, err);
         size_t cnt = 1;
         for (int64_t d : shape) cnt *= (size_t)d;
-        const long long a = (long long)of->second.arr[0].num, b = (long long)of->second.arr[1].num;
-        if (b - a != (long long)(cnt * esz) || base + b > fsize) return mz_set_error(h, name + ": bad data offsets");
-        std::fseek(f, (long)(base + a), SEEK_SET);
+        std::fseek(f, (long)off, SEEK_SET);
         if (std::fread(dst, 1, cnt * esz, f) != cnt * esz) return mz_set_error(h, name + ": short read");
         return 0;
     };
@@ -209,9 +130,9 @@ int mz_checkpoint_load(mz_handle* h, const char* path, int64_t* training_step) {
     if (training_step) {
         *training_step = 0;
         auto md = root.obj.find("__metadata__");
-        if (md != root.obj.end()) {
+        if (md != root.obj.end() && md->second.t == mzst::JV::OBJ) {
             auto ts = md->second.obj.find("training_step");
-            if (ts != md->second.obj.end()) *training_step = std::strtoll(ts->second.str.c_str(), nullptr, 10);
+            if (ts != md->second.obj.end() && ts->second.t == mzst::JV::STR) *training_step = std::strtoll(ts->second.str.c_str(), nullptr, 10);
         }
     }
     return mz_state_set(h, flat.data(), m.data(), v.data(), bp);

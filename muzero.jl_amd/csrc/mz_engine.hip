@@ -224,6 +224,9 @@ struct mz_handle {
     std::vector<uint32_t> sm_nzm;           // nonzero-chunk masks of the register images (SM_NZM_N)
     bool sm_bn = false;                     // BatchNorm FC layers: the bias image carries γ, β sections
     float* d_zero16 = nullptr;              // 64 zero bytes (sm_load's skipped chunks)
+    unsigned* d_fault = nullptr;            // device fault word (MZ_FAULT_*), checked at host synchronisation
+    int dbg_skip = -1;                      // debug: the hand-off producer that skips its publish
+    unsigned long long poll_ticks = MZ_POLL_TICKS;
     int force_kernel = 0;                   // 0 auto, 1 tile16, 2 small
     // inverse image maps, one code per flat parameter: >= 0 position in the
     // weight image, <= -2 position -code-2 in the bias image, -1 none.  ADAM
@@ -266,6 +269,7 @@ struct mz_handle {
     int32_t* d_rs_index = nullptr;
     int rs_cap = 0;
     bool sp_has_games = false;              // the FIFO never empties once a game is in
+    bool sp_reset_pending = false;          // Atari-like env: the initial games start at the first move
     // get_batch one step ahead (the one-launch FC learner, PER off): the launch
     // for step t also samples step t+1's batch into the other batch set and
     // stamps that set's header {epoch, games played, step, B}; the next launch
@@ -332,6 +336,30 @@ static hipError_t sync_device(mz_handle* h) {
     hipError_t e = hipStreamSynchronize(h->sync_stream);
     return e != hipSuccess ? e : hipStreamSynchronize(h->stream);
 }
+
+// After a synchronisation: a kernel that gave up on a cross-workgroup publish
+// (mz_poll_ge) left bits in d_fault; report them once (the word is cleared)
+// as this call's error.  The outputs of the launches since the last check
+// are then not to be trusted.
+static int check_fault(mz_handle* h) {
+    if (!h->d_fault) return 0;
+    unsigned v = 0;
+    MZ_TRY(h, hipMemcpy(&v, h->d_fault, 4, hipMemcpyDeviceToHost));
+    if (!v) return 0;
+    MZ_TRY(h, hipMemset(h->d_fault, 0, 4));
+    std::string m = "device fault: a workgroup waited 2 s for a publish that never came (";
+    if (v & MZ_FAULT_RS_TRUNK) m += "mz_rsearch_nets trunk hand-off ";
+    if (v & MZ_FAULT_RD_PROGRESS) m += "mz_runroll_fused_r chain progress ";
+    h->err = m + "); the results of the launches since the last synchronisation are invalid";
+    return -1;
+}
+
+// every host-synchronous call: wait (sync_device), then report a device fault
+#define MZ_SYNC(h)                                    \
+    do {                                              \
+        MZ_TRY(h, sync_device(h));                    \
+        if (check_fault(h)) return -1;                \
+    } while (0)
 
 template <typename T>
 static hipError_t dalloc(mz_handle* h, T** p, size_t n) {
@@ -629,7 +657,7 @@ static int build_small(mz_handle* h) {
     // nonzero-chunk masks (mz_small_params.h SM_NZM_N): per stage and wave,
     // bit q*4 + c set when any row of the wave's group gathers a weight into
     // chunk c of DPP row q
-    h->sm_nzm.assign(SM_NZM_N, 0);
+    h->sm_nzm.assign(SM_NZM_ALLOC, 0);        // zero padding past SM_NZM_N
     for (int r = 0; r < nrec; ++r)
         for (int sl2 = 0; sl2 < SM_SLOTS; ++sl2)
             for (int srow = 0; srow < 64; ++srow)
@@ -1130,6 +1158,12 @@ static int alloc_learner(mz_handle* h) {
     MZ_TRY(h, dalloc(h, &h->d_netoff, 6));
     MZ_TRY(h, dalloc(h, &h->d_counter, 1));
     MZ_TRY(h, hipMemset(h->d_counter, 0, 4));
+    MZ_TRY(h, dalloc(h, &h->d_fault, 1));
+    MZ_TRY(h, hipMemset(h->d_fault, 0, 4));
+    // debug (tests/test_fault_gpu.py): MZ_DEBUG_SKIP_PUBLISH=1 at create makes
+    // tile / sample 0 of the cross-workgroup hand-offs skip its publish, with a
+    // 10 ms poll bound, so the reported fault can be tested
+    if (std::getenv("MZ_DEBUG_SKIP_PUBLISH")) { h->dbg_skip = 0; h->poll_ticks = 1000000ull; }
     MZ_TRY(h, hipMemcpy(h->d_netoff, oc, sizeof(oc), hipMemcpyHostToDevice));
     return 0;
 }
@@ -1606,10 +1640,10 @@ int mz_weights_set(mz_handle* h, int net, const float* flat, size_t n) {
     if (net < 0 || net > 2) return fail(h, "bad net id");
     if (n != h->nparams[net]) return fail(h, "weights_set: wrong parameter count");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));                  // no search / learner launch still reads the old weights
+    MZ_SYNC(h);                  // no search / learner launch still reads the old weights
     MZ_TRY(h, hipMemcpyAsync(h->d_flat + h->flat_off[net], flat, n * 4, hipMemcpyHostToDevice, h->stream));
     if (repack(h)) return -1;
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     return 0;
 }
 
@@ -1618,9 +1652,9 @@ int mz_weights_get(mz_handle* h, int net, float* flat, size_t n) {
     if (net < 0 || net > 2) return fail(h, "bad net id");
     if (n != h->nparams[net]) return fail(h, "weights_get: wrong parameter count");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));                  // learner steps queued on any stream have landed
+    MZ_SYNC(h);                  // learner steps queued on any stream have landed
     MZ_TRY(h, hipMemcpyAsync(flat, h->d_flat + h->flat_off[net], n * 4, hipMemcpyDeviceToHost, h->stream));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     return 0;
 }
 
@@ -1653,7 +1687,7 @@ static int rnet_forward(mz_handle* h, int net, const float* x, int n, float* out
     (void)hipFree(dx); (void)hipFree(d0); (void)hipFree(d1);
     MZ_TRY(h, le);
     MZ_TRY(h, se);
-    return 0;
+    return check_fault(h);
 }
 
 int mz_net_forward(mz_handle* h, int net, const float* x, int n, float* out0, float* out1) {
@@ -1662,7 +1696,7 @@ int mz_net_forward(mz_handle* h, int net, const float* x, int n, float* out0, fl
     if (n < 0) return fail(h, "negative batch");
     if (n == 0) return 0;
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));                  // weights written by `_dev` calls on other streams
+    MZ_SYNC(h);                  // weights written by `_dev` calls on other streams
     if (h->kind == 1) return rnet_forward(h, net, x, n, out0, out1);
     const int H = h->H, A = h->A;
     const int in_feat = net == MZ_NET_REPR ? h->obs_feat : net == MZ_NET_PRED ? H : H + h->plane;
@@ -1688,7 +1722,7 @@ int mz_net_forward(mz_handle* h, int net, const float* x, int n, float* out0, fl
     (void)hipFree(dx); (void)hipFree(d0); (void)hipFree(d1);
     MZ_TRY(h, le);
     MZ_TRY(h, se);
-    return 0;
+    return check_fault(h);
 }
 
 // ResNet search: root launch, S x (tree step, networks), final tree step
@@ -1732,6 +1766,7 @@ static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     P.rew_split = no_rsplit ? 0 : 1;
     P.trunk_nl = 1 + 2 * h->rhp.num_blocks; P.dyn_split = h->rn_dyn_split;
     P.trunk = h->d_rtrunk; P.tprog = h->d_tprog;
+    P.fault = h->d_fault; P.poll_ticks = h->poll_ticks; P.dbg_skip = h->dbg_skip;
     const void* kroot = gw == 32 ? (const void*)mz_rsearch_root32 : (const void*)mz_rsearch_root;
     // tree step: LDS-cached (one wave per 64/gw games) unless the tree exceeds the LDS
     const bool tl = h->rtree_lds != 0;
@@ -1860,7 +1895,7 @@ int mz_mcts_search(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
         if (to_play[g] < 1 || to_play[g] > h->conf.players) return fail(h, "to_play out of range");
     }
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));                  // `_dev` work on other streams first
+    MZ_SYNC(h);                  // `_dev` work on other streams first
     MZ_TRY(h, hipMemcpyAsync(h->d_obs, obs, (size_t)G * h->obs_feat * 4, hipMemcpyHostToDevice, h->stream));
     MZ_TRY(h, hipMemcpyAsync(h->d_legal, legal_mask, (size_t)G * A, hipMemcpyHostToDevice, h->stream));
     MZ_TRY(h, hipMemcpyAsync(h->d_tp, to_play, (size_t)G * 4, hipMemcpyHostToDevice, h->stream));
@@ -1870,7 +1905,7 @@ int mz_mcts_search(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     MZ_TRY(h, hipMemcpyAsync(child_visits, h->d_cv, (size_t)G * A * 4, hipMemcpyDeviceToHost, h->stream));
     MZ_TRY(h, hipMemcpyAsync(root_value, h->d_rv, (size_t)G * 4, hipMemcpyDeviceToHost, h->stream));
     MZ_TRY(h, hipMemcpyAsync(action_out, h->d_act, (size_t)G * 4, hipMemcpyDeviceToHost, h->stream));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     return 0;
 }
 
@@ -1894,7 +1929,7 @@ int mz_debug_tree(mz_handle* h, int G, int32_t* eN, float* eW, float* eP, float*
     if (G < 0 || G > h->max_games) return fail(h, "G exceeds max_games");
     if (h->lds_tree && !h->dump_tree) return fail(h, "mz_debug_tree needs mz_debug_enable(h, 1) before the search");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     const int S = h->S, A = h->A, NN = S + 1, E = NN * A;
     const size_t gb = h->tree_game_bytes;
     std::vector<char> buf((size_t)G * gb);
@@ -2025,6 +2060,7 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
         if (fused) {
             U.prog = h->d_prog;
             U.prog_base = (++h->prog_epoch) * 64ull;
+            U.fault = h->d_fault; U.poll_ticks = h->poll_ticks; U.dbg_skip = h->dbg_skip;
             U.n_chain = B;
             U.fuse_sample = rq != nullptr && !no_fuse_sample;
             if (rq) U.rq = *rq;
@@ -2385,7 +2421,10 @@ static int build_rbp(mz_handle* h) {
     MZ_TRY(h, dalloc(h, &h->d_rbp_sq, chunks.size()));
     h->rbp_n_app = (int)apps.size(); h->rbp_n_head = (int)heads.size(); h->rbp_n_chunk = (int)chunks.size() - 1;
     h->rbp_arena = off; h->rbp_obs_t = obs_t; h->rbp_dt = (dtf + 3) & ~3; h->rbp_xs = (xsf + 3) & ~3;
-    if ((size_t)(h->rbp_dt + h->rbp_xs) * 4 > kLdsMax) return fail(h, "corrected learner: a conv's tensors exceed the LDS");
+    const size_t lds = (size_t)(h->rbp_dt + h->rbp_xs) * 4;
+    if (lds > kLdsMax) return fail(h, "corrected learner: a conv's tensors exceed the LDS");
+    // above the 64 KB default (e.g. 256 filters on the 6x7 board: ~86 KB)
+    MZ_TRY(h, hipFuncSetAttribute((const void*)mz_rbp_sample, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     h->rbp_built = true;
     return 0;
 }
@@ -2502,7 +2541,7 @@ int mz_learner_step(mz_handle* h, const mz_batch* b, double eta, float* losses_o
     MZ_TRY(h, hipSetDevice(h->device));
     if (B < 1) return fail(h, "batch_size must be >= 1");
     if (ensure_batch(h, B)) return -1;
-    MZ_TRY(h, sync_device(h));                  // `_dev` work on other streams first
+    MZ_SYNC(h);                  // `_dev` work on other streams first
     hipStream_t st = h->stream;
     MZ_TRY(h, hipMemcpyAsync(h->d_bobs, b->observation, (size_t)B * h->obs_feat * 4, hipMemcpyHostToDevice, st));
     MZ_TRY(h, hipMemcpyAsync(h->d_bact, b->actions, (size_t)B * (K + 1) * 4, hipMemcpyHostToDevice, st));
@@ -2521,7 +2560,7 @@ int mz_learner_step(mz_handle* h, const mz_batch* b, double eta, float* losses_o
     if (rc) return rc;
     if (losses_out) MZ_TRY(h, hipMemcpyAsync(losses_out, h->d_loss, 6 * 4, hipMemcpyDeviceToHost, st));
     MZ_TRY(h, hipStreamSynchronize(st));
-    return 0;
+    return check_fault(h);
 }
 
 // the next (start, stop) event pair of the measurement list (mz_debug_kernel_time)
@@ -2556,7 +2595,7 @@ int mz_debug_unroll(mz_handle* h, int B, float* values, float* policies, float* 
     if (!h) return -2;
     if (B < 0 || B > h->bcap) return fail(h, "B exceeds the last learner batch");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     const size_t n = (size_t)B * (h->conf.num_unroll_steps + 1);
     if (values) MZ_TRY(h, hipMemcpy(values, h->d_pv, n * 4, hipMemcpyDeviceToHost));
     if (policies) MZ_TRY(h, hipMemcpy(policies, h->d_pp, n * h->A * 4, hipMemcpyDeviceToHost));
@@ -2569,7 +2608,7 @@ int mz_debug_stamps(mz_handle* h, unsigned long long* out, int n_blocks) {
     if (!h) return -2;
 #ifdef MZ_STAMPS
     if (!h->d_stamps) return fail(h, "no stamps recorded");
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     MZ_TRY(h, hipMemcpy(out, h->d_stamps, (size_t)n_blocks * 8 * 8, hipMemcpyDeviceToHost));
     return 0;
 #else
@@ -2641,7 +2680,7 @@ size_t mz_flat_count(const mz_handle* h) { return h->nflat; }
 
 int mz_state_get(mz_handle* h, float* flat, float* m, float* v, double* beta_pow) {
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     if (flat) MZ_TRY(h, hipMemcpy(flat, h->d_flat, h->nflat * 4, hipMemcpyDeviceToHost));
     if (m) MZ_TRY(h, hipMemcpy(m, h->d_m, h->nflat * 4, hipMemcpyDeviceToHost));
     if (v) MZ_TRY(h, hipMemcpy(v, h->d_v, h->nflat * 4, hipMemcpyDeviceToHost));
@@ -2651,13 +2690,13 @@ int mz_state_get(mz_handle* h, float* flat, float* m, float* v, double* beta_pow
 
 int mz_state_set(mz_handle* h, const float* flat, const float* m, const float* v, const double* beta_pow) {
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     MZ_TRY(h, hipMemcpy(h->d_flat, flat, h->nflat * 4, hipMemcpyHostToDevice));
     MZ_TRY(h, hipMemcpy(h->d_m, m, h->nflat * 4, hipMemcpyHostToDevice));
     MZ_TRY(h, hipMemcpy(h->d_v, v, h->nflat * 4, hipMemcpyHostToDevice));
     h->bp1 = beta_pow[0]; h->bp2 = beta_pow[1];
     if (repack(h)) return -1;
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     return 0;
 }
 
@@ -2759,12 +2798,13 @@ int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games) {
     if (replay_games < G) return fail(h, "replay_games must be >= G (one move can finish every slot)");
     if (c.max_moves < 1) return fail(h, "max_moves must be >= 1");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     for (void* p : h->sp_allocs) (void)hipFree(p);
     h->sp_allocs.clear();
     h->rs_cap = 0;
     h->pf_cap = 0; h->pf_cur = 0; h->d_pf_hdr = nullptr; ++h->pf_epoch;
     h->sp_has_games = false;
+    h->sp_reset_pending = false;
     h->tr_B = 0;                                // a new shard: mz_train_init again
     h->sp_env = env_kind; h->sp_G = G; h->sp_cap = replay_games;
     h->sp_T = c.max_moves + 1; h->sp_osz = W * H * C;
@@ -2791,12 +2831,12 @@ int mz_selfplay_init(mz_handle* h, int env_kind, int G, int replay_games) {
     for (int n = 0; n < (int)dp.size(); ++n) dp[n] = (float)std::pow((double)c.discount, (double)n);
     MZ_TRY(h, spalloc(h, &h->d_sp_dpow, dp.size()));
     MZ_TRY(h, hipMemcpy(h->d_sp_dpow, dp.data(), dp.size() * 4, hipMemcpyHostToDevice));
-    if (env_kind == MZ_ENV_ATARI) {                 // every slot: new game (key and first frame on the device)
-        SpParams S = sp_params(h);
-        S.reset_step = 0xFFFFFFFFu;
-        hipLaunchKernelGGL(mz_sp_reset, dim3((G + 3) / 4), dim3(256), 0, h->stream, S);
-        MZ_TRY(h, hipGetLastError());
-        MZ_TRY(h, hipStreamSynchronize(h->stream));
+    if (env_kind == MZ_ENV_ATARI) {
+        // every slot: new game, its key and first frame drawn on the device at
+        // the first mz_selfplay_move, keyed by the global game id game_offset +
+        // slot that the move carries (ranks of a data-parallel job hold
+        // different games, not copies of slot 0..G-1's)
+        h->sp_reset_pending = true;
         return 0;
     }
     // every slot: new game (boards: empty plane set, player 1)
@@ -2824,6 +2864,13 @@ int mz_selfplay_move(mz_handle* h, uint32_t rng_step, uint32_t game_offset, floa
     S.tgame = h->sp_latch ? h->d_sp_tgame : nullptr;
     const int G = h->sp_G;
     const dim3 waves((G + 3) / 4);
+    if (h->sp_reset_pending) {                      // the initial Atari-like games (mz_selfplay_init)
+        SpParams R = S;
+        R.reset_step = 0xFFFFFFFFu;
+        hipLaunchKernelGGL(mz_sp_reset, waves, dim3(256), 0, st, R);
+        MZ_TRY(h, hipGetLastError());
+        h->sp_reset_pending = false;
+    }
     hipLaunchKernelGGL(mz_sp_prepare, waves, dim3(256), 0, st, S);
     MZ_TRY(h, hipGetLastError());
     int rc = search_dev(h, G, h->d_obs, h->d_legal, h->d_tp, 1, rng_step, game_offset, temperature, h->d_cv,
@@ -2850,7 +2897,7 @@ int mz_eval_results(mz_handle* h, int64_t* out4) {
     if (!h || !out4) return -2;
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     long long c[4];
     MZ_TRY(h, hipMemcpy(c, h->d_eval, sizeof(c), hipMemcpyDeviceToHost));
     for (int i = 0; i < 4; ++i) out4[i] = c[i];
@@ -2861,7 +2908,7 @@ int mz_replay_counts(mz_handle* h, int64_t* counts, int32_t* games_in_buffer) {
     if (!h) return -2;
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     long long c[3];
     MZ_TRY(h, hipMemcpy(c, h->d_sp_counters, sizeof(c), hipMemcpyDeviceToHost));
     if (counts) for (int i = 0; i < 3; ++i) counts[i] = c[i];
@@ -2876,7 +2923,7 @@ int mz_replay_save_game(mz_handle* h, int32_t T, const uint8_t* obs, const int32
     if (T < 1 || T > h->sp_T) return fail(h, "game length must be in 1..max_moves+1");
     if (!obs || !actions || !rewards || !to_play || !child_visits || !root_values) return fail(h, "null array");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     long long c[3];
     MZ_TRY(h, hipMemcpy(c, h->d_sp_counters, sizeof(c), hipMemcpyDeviceToHost));
     const long long num = c[0] + 1;
@@ -2901,7 +2948,7 @@ int mz_replay_save_game(mz_handle* h, int32_t T, const uint8_t* obs, const int32
         hipLaunchKernelGGL(mz_rp_per_init, dim3(1), dim3(64), 0, h->stream, h->sp_ring, slot, (int)T, h->sp_T,
                            h->conf.td_steps, (const float*)h->d_sp_dpow, h->conf.PER_alpha);
         MZ_TRY(h, hipGetLastError());
-        MZ_TRY(h, sync_device(h));
+        MZ_SYNC(h);
     }
     return 0;
 }
@@ -3119,7 +3166,7 @@ int mz_replay_get_priorities(mz_handle* h, int32_t i, float* priorities, float* 
     if (!h) return -2;
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     long long played = 0;
     MZ_TRY(h, hipMemcpy(&played, h->d_sp_counters, sizeof(played), hipMemcpyDeviceToHost));
     const long long n = std::min<long long>(played, h->sp_cap);
@@ -3192,7 +3239,7 @@ int mz_replay_get_game(mz_handle* h, int32_t i, int32_t* T, uint8_t* obs, int32_
     if (!h) return -2;
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     long long c[3];
     MZ_TRY(h, hipMemcpy(c, h->d_sp_counters, sizeof(c), hipMemcpyDeviceToHost));
     const long long held = std::min<long long>(c[0], h->sp_cap);
@@ -3217,7 +3264,7 @@ int mz_selfplay_slots(mz_handle* h, int32_t* history_len, uint8_t* board, int32_
     if (!h) return -2;
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     const size_t G = (size_t)h->sp_G;
     if (history_len) MZ_TRY(h, hipMemcpy(history_len, h->sp_hist.len, G * 4, hipMemcpyDeviceToHost));
     if (board) MZ_TRY(h, hipMemcpy(board, h->d_sp_board, G * h->sp_osz, hipMemcpyDeviceToHost));
@@ -3276,7 +3323,7 @@ int mz_train_init_at(mz_handle* h, int32_t B, int64_t t0) {
     if (h->dp_world > 1) return fail(h, "mz_train_run is the single-GPU loop (world = 1)");
     if (h->conf.checkpoint_interval < 1) return fail(h, "checkpoint_interval must be >= 1");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     mz_handle::WSet& w = h->tr_actor;
     if (!w.flat) {
         MZ_TRY(h, dalloc(h, &w.flat, h->nflat));
@@ -3322,6 +3369,7 @@ int mz_train_run(mz_handle* h, int32_t moves, uint32_t move0, uint32_t game_offs
         // 2. games saved this move (save_game in slot order, inside the move)
         MZ_TRY(h, hipMemcpyAsync(h->h_tr_cnt, h->d_sp_counters, sizeof(long long), hipMemcpyDeviceToHost, st));
         MZ_TRY(h, hipStreamSynchronize(st));
+        if (check_fault(h)) return -1;
         const int64_t nfin = h->h_tr_cnt[0] - h->tr_games;
         h->tr_games = h->h_tr_cnt[0];
         // 3. one learner step per saved game while t <= training_steps (Learning.jl:327),
@@ -3363,7 +3411,7 @@ int mz_train_weights_get(mz_handle* h, int which, int net, float* flat, size_t n
     if (net < 0 || net > 2) return fail(h, "bad net id");
     if (n != h->nparams[net]) return fail(h, "wrong parameter count");
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, sync_device(h));
+    MZ_SYNC(h);
     const float* src = which == MZ_TRAIN_ACTOR ? h->tr_actor.flat : h->d_tr_queued;
     MZ_TRY(h, hipMemcpy(flat, src + h->flat_off[net], n * 4, hipMemcpyDeviceToHost));
     return 0;
@@ -3373,7 +3421,7 @@ int mz_sync(mz_handle* h) {
     if (!h) return -2;
     MZ_TRY(h, hipSetDevice(h->device));
     MZ_TRY(h, hipStreamSynchronize(h->stream));
-    return 0;
+    return check_fault(h);
 }
 
 }  // extern "C"

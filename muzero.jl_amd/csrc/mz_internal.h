@@ -23,6 +23,40 @@
 #endif
 #define MZ_MAX_STAGES 64
 
+// Device fault word (mz_handle d_fault): bits set by a kernel that gave up
+// waiting for another workgroup's publish; the host reads it at its next
+// synchronisation (every host-synchronous call and mz_sync), clears it and
+// fails that call with a message (mz_last_error) — a producer that never
+// publishes is reported, never silently consumed as stale data.
+enum { MZ_FAULT_RS_TRUNK = 1,      // mz_rsearch_nets: the dynamics workgroup's trunk publish
+       MZ_FAULT_RD_PROGRESS = 2 }; // mz_runroll_fused_r: a chain block's h_s / trunk publish
+#define MZ_POLL_TICKS 200000000ull // 2 s of the 100 MHz s_memrealtime clock
+
+// One lane polls a 64-bit progress word (relaxed, agent scope) until it
+// reaches `want`, sleeping between loads; after `ticks` of the constant clock
+// it ORs `code` into *fault and returns false (the caller still drains, so the
+// grid exits).  The payload is stored write-through (agent-scope atomic
+// stores), drained by every storing wave (vmcnt 0) before the barrier that
+// precedes the flag store, and read with agent-scope loads: the R1 hand-off
+// of cdna_hip_programming.md Guideline 16, which needs no release fence; the
+// wavefront-scope acquire after the poll only keeps the compiler from moving
+// the payload loads above it.
+__device__ __forceinline__ bool mz_poll_ge(const unsigned long long* w, unsigned long long want, unsigned* fault,
+                                           unsigned code, unsigned long long ticks) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok = true;
+    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+            if (fault) __hip_atomic_fetch_or(fault, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = false;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return ok;
+}
+
 // One Dense layer inside a plan.  All offsets are in floats.
 struct LayerDesc {
     int w_off;     // packed weights: [n_ob][4*nq k-steps][64 lanes]

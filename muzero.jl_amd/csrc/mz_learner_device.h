@@ -16,7 +16,9 @@
 //    logitcrossentropy of the probabilities (Q11's double softmax), every
 //    sum in ascending action order (g16_seqsum);
 //  * blocks [nlb, nlb + 3·MZ_L2_BLOCKS): θ² of a fixed slice summed in f64,
-//    and ∇ = 2θ written for it (Q11: only sum(sqnorm, params) depends on θ);
+//    and the data term of ∇ written for it: zero (Q11: only sum(sqnorm,
+//    params) depends on θ; mz_adam_kernel adds the rank-invariant 2θ after a
+//    data-parallel exchange, so the update is exact at every world size);
 //  * the last block to finish folds each sample's steps in ascending k, the
 //    cross-sample sums in f64 (tolerance-checked, not bitwise), and the Σθ²
 //    partials in a fixed order (one wave per net), then resets the counter.
@@ -117,7 +119,8 @@ __device__ __forceinline__ void lg_step_terms(int t, int a, int A, int v_act, in
 // Σθ² of slice blk of net (thread tid of 256): elements off + blk·256 + tid +
 // j·(MZ_L2_BLOCKS·256) as one thread's ascending f64 sum; four per pass with
 // every load issued before any store (the fused ADAM's f64 chains overlap).
-// ad.on: ADAM with ∇ = 2θ in place (= mz_adam_kernel, gscale 1), else G = 2θ.
+// ad.on: ADAM with ∇ = 2θ in place (= mz_adam_kernel, gscale 1), else G = 0
+// (the data term).
 // ADAM operands of one 4-group (adam_update4's loads, issued ahead)
 struct LgAdamOps { float x[4], mo[4], vo[4]; int it[4], is[4]; };
 __device__ __forceinline__ void lg_adam_load(const LgAdam& ad, const float* P, size_t i0, size_t stride, size_t rem,
@@ -153,7 +156,7 @@ __device__ __forceinline__ void lg_adam_store(const LgAdam& ad, float* P, size_t
 }
 
 // Σθ² of slice blk of net (f64, this thread's elements in ascending order) and
-// the ADAM step (∇ = 2θ) or ∇ into G.  Software-pipelined: the next 4-group's
+// the ADAM step (∇ = 2θ) or the data term of ∇ (0) into G.  Software-pipelined: the next 4-group's
 // loads are issued before this group's stores (the stores could alias them
 // as far as the compiler knows, so a plain loop waits one memory latency per
 // group).
@@ -179,8 +182,8 @@ __device__ __forceinline__ double lg_l2_slice(int net, int blk, int tid, const s
             lg_adam_store(a, flat + off, i, stride, cnt - i, cur);
         } else {
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (i + u * stride < cnt) G[off + i + u * stride] = cur.x[u] * 2.0f;
+            for (int u = 0; u < 4; ++u)          // the data term of ∇ (Q11: none); 2θ in mz_adam_kernel
+                if (i + u * stride < cnt) G[off + i + u * stride] = 0.0f;
         }
         cur = nxt;
     }

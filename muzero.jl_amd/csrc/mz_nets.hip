@@ -1,6 +1,7 @@
 // mz_nets.hip — batched network forward (the Flux Chain calls of
 // Learning.jl:87-142) and the learner step of Learning.jl:327-413 in
-// ref_semantics: K-step unroll (Q10), losses (:261-288), gradient 2θ (Q11),
+// ref_semantics: K-step unroll (Q10), losses (:261-288), gradient 2θ (Q11:
+// a zero data term, 2θ added by the ADAM kernel),
 // ADAM (Flux 0.12 ADAMW()[1]) and re-packing of the MFMA weight image.
 #include "mz_mlp_device.h"
 #include "mz_tree_device.h"
@@ -100,8 +101,8 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_unroll_kernel(Unroll
 // One launch after the unroll (Learning.jl:261-288, 380-393 in ref_semantics;
 // pieces in mz_learner_device.h):
 //  * blocks [0, nlb): one GW-lane group per (sample, step), lg_step_terms;
-//  * blocks [nlb, nlb + 3·MZ_L2_BLOCKS): lg_l2_slice (Σθ², ∇ = 2θ or the
-//    fused ADAM);
+//  * blocks [nlb, nlb + 3·MZ_L2_BLOCKS): lg_l2_slice (Σθ², the data term
+//    of ∇ (0) or the fused ADAM);
 //  * the last block out folds (lg_fold).
 template <int GW>
 __device__ __forceinline__ void learner_grad_body(
@@ -139,14 +140,22 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_grad_kernel3
     learner_grad_body<32>(MZ_LG_CALL);
 }
 
-// ADAM over all parameters (adam_update): grad = G[i] * gscale (gscale =
-// 1/world after an all-reduce sum; exact for power-of-two world sizes).
+// ADAM over all parameters (adam_update): ∇ = G[i]·gscale + 2θ_i, G the
+// data term of the gradient (summed over the ranks by the caller's
+// all-reduce; zero in ref_semantics), gscale = 1/world, and 2θ = ∂Σθ²/∂θ
+// added here, after the exchange: it is the same on every rank, so an
+// exchange that carried it (Σ_r 2θ · 1/world) would round differently from
+// 2θ for most worlds (a sequential f32 sum of eight equal terms is not 8x for
+// ~44 % of inputs).  At world 1, G·1 + 2θ is the single-GPU gradient bit for
+// bit (the corrected kernels' old s + 2θ).
 extern "C" __global__ void mz_adam_kernel(float* P, float* M, float* V, const float* G, float gscale,
                                           size_t n, double bp1, double bp2, double eta, float* Wp, float* Bp,
                                           const int* inv_tile, float* smw, float* smb, const int* inv_small) {
     const LgAdam ad{1, M, V, bp1, bp2, eta, Wp, Bp, inv_tile, smw, smb, inv_small};
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        adam_update(ad, P, i, G[i] * gscale);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const float d = G[i] * gscale;
+        adam_update(ad, P, i, d + P[i] * 2.0f);
+    }
 }
 
 // Rebuild the MFMA weight image from the Flux-order flat parameters:

@@ -1147,7 +1147,7 @@ extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RS
                 });
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");            // every wave's stores performed
             __syncthreads();
-            if (threadIdx.x == 0)
+            if (threadIdx.x == 0 && (int)blockIdx.x != P.dbg_skip)
                 __hip_atomic_store(P.tprog + blockIdx.x, P.tepoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             rn_run<false, false, 3, false, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, nullptr, P.trunk_nl,
                                                  P.dyn_split);                        // the state head
@@ -1164,12 +1164,8 @@ extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RS
             rn_unstage(lds + R.out1_off, NG, P.A, t, [&](int f, float v) { o[f] = v; });
         }
         __syncthreads();                                              // the outputs read before the LDS is reused
-        if (threadIdx.x == 0)                                         // (bounded: no hang if never published)
-            for (int n = 0; n < (1 << 21); ++n) {
-                if (__hip_atomic_load(P.tprog + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= P.tepoch)
-                    break;
-                __builtin_amdgcn_s_sleep(2);
-            }
+        if (threadIdx.x == 0)                   // bounded: a publish that never comes is reported (P.fault)
+            mz_poll_ge(P.tprog + blockIdx.x, P.tepoch, P.fault, MZ_FAULT_RS_TRUNK, P.poll_ticks);
         __syncthreads();
         const RPlan& Rd = P.plans[MZ_NET_DYN];
         const RLayer Ls = rn_layer_at(Rd, P.dyn_split);
@@ -1469,9 +1465,10 @@ __device__ __forceinline__ void rd_run(const RPlan& Rd, const float (&a0)[2][4][
 // trunk outputs as agent-scope atomics (written through to the agent's
 // coherence point), every wave waits for its stores (vmcnt 0), then after the
 // barrier one agent-scope store of the progress word.  An item polls the word
-// with agent-scope loads (bounded: a chain that never publishes lets the item
-// run on stale data rather than hang) and reads its input with agent-scope
-// loads (they miss any stale L1 / L2 copy).
+// with agent-scope loads (mz_poll_ge, bounded: a chain that never publishes
+// sets MZ_FAULT_RD_PROGRESS, which fails the host's next synchronisation,
+// instead of hanging the grid) and reads its input with agent-scope loads
+// (they miss any stale L1 / L2 copy).
 __device__ __forceinline__ void rd_st(float* p, float v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1481,7 +1478,7 @@ __device__ __forceinline__ float rd_ld(const float* p) {
 __device__ __forceinline__ void rd_publish(const RUnrollParams& U, int b, int p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0 && b != U.dbg_skip)
         __hip_atomic_store(U.prog + b, U.prog_base + (unsigned long long)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef MZ_STAMPS
     if (U.stamps && threadIdx.x == 0) U.stamps[2048 + 4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1489,11 +1486,7 @@ __device__ __forceinline__ void rd_publish(const RUnrollParams& U, int b, int p)
 }
 __device__ __forceinline__ void rd_wait(const RUnrollParams& U, int b, int p) {
     if (threadIdx.x == 0) {
-        const unsigned long long want = U.prog_base + (unsigned long long)p;
-        for (int n = 0; n < (1 << 21); ++n) {
-            if (__hip_atomic_load(U.prog + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
+        mz_poll_ge(U.prog + b, U.prog_base + (unsigned long long)p, U.fault, MZ_FAULT_RD_PROGRESS, U.poll_ticks);
 #ifdef MZ_STAMPS
         if (U.stamps) U.stamps[2048 + 4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 #endif

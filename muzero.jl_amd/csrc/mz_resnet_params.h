@@ -147,6 +147,9 @@ struct RSearchParams {
     // tile carry about equal work instead of 101 k / 142 k ticks
     int rew_split, trunk_nl, dyn_split;
     float* trunk; unsigned long long* tprog; unsigned long long tepoch;
+    unsigned* fault;                   // MZ_FAULT_RS_TRUNK on a publish that never came (mz_poll_ge)
+    unsigned long long poll_ticks;     // the poll's bound (MZ_POLL_TICKS)
+    int dbg_skip;                      // debug: the tile whose trunk publish is skipped (-1 = none)
 };
 
 // LDS layout of the LDS-cached tree step (mz_rsearch_tree_lds*): one wave per
@@ -209,6 +212,9 @@ struct RUnrollParams {
     LgAdam ad; float* flat_w; const size_t* netoff; double* part;
     int rp_nv;                         // the prediction plan's value-head layers ([RP_NL, RP_NL + rp_nv)); the
                                        // fused launch runs the value and the policy head of an item in two blocks
+    unsigned* fault;                   // MZ_FAULT_RD_PROGRESS on a publish that never came (mz_poll_ge)
+    unsigned long long poll_ticks;     // the poll's bound (MZ_POLL_TICKS)
+    int dbg_skip;                      // debug: the chain block (sample) whose publishes are skipped (-1 = none)
 };
 // mz_runroll_chain_r: the dynamics chain's layers ([0, dyn_split) = RD_NL:
 // trunk + state head of 2-block towers) with register-resident A fragments

@@ -58,9 +58,9 @@ __device__ void atari_frame(const SpParams& S, int g, uint32_t key, int lane) {
         f[j] = make_uint4(r.v[0], r.v[1], r.v[2], r.v[3]);
     }
 }
-// reset: key = u32(seed, ENV, slot, step, ~0)
+// reset: key = u32(seed, ENV, global game id = game_offset + slot, step, ~0)
 __device__ void atari_reset(const SpParams& S, int g, uint32_t step, int lane) {
-    const uint32_t key = mz_rng_u32(S.seed, MZ_RNG_ENV, (uint32_t)g, step, 0xFFFFFFFFu);
+    const uint32_t key = mz_rng_u32(S.seed, MZ_RNG_ENV, S.game_offset + (uint32_t)g, step, 0xFFFFFFFFu);
     atari_frame(S, g, key, lane);
     if (lane == 0) { S.ekey[g] = key; S.player[g] = 1; S.over[g] = 0; }
 }
@@ -205,7 +205,8 @@ extern "C" __global__ __launch_bounds__(256) void mz_sp_commit(SpParams S) {
     }
 }
 
-// initial games of the synthetic Atari-like env (mz_selfplay_init), one wave per slot
+// initial games of the synthetic Atari-like env (mz_selfplay_init's slots, at
+// the first mz_selfplay_move: S.game_offset is that move's), one wave per slot
 extern "C" __global__ __launch_bounds__(256) void mz_sp_reset(SpParams S) {
     const int g = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (g < S.G) atari_reset(S, g, S.reset_step, lane);

@@ -35,6 +35,11 @@ __host__ __device__ __forceinline__ size_t sm_widx(int stage, int slot, int q, i
 // scalar load.
 #define SM_NZM_ST (SM_MAX_SIM + SM_MAX_ROOT)
 #define SM_NZM_N (SM_NZM_ST * SM_SLOTS * 4)
+// the array as passed: sm_load preloads a wave's SM_MAX_SIM masks in one
+// batch of scalar loads from base + n_sim (root stages), whatever [k0, k1)
+// it then uses, so the last wave's batch may reach SM_MAX_SIM - 1 entries past
+// SM_NZM_N; the padding keeps that read inside the kernel-argument struct
+#define SM_NZM_ALLOC (SM_NZM_N + SM_MAX_SIM)
 
 // Per stage, the host-built record: one int4 per [slot][row] (copied to LDS)
 //   .x  input base of the row's layer in the activation buffer (0 if unused:
@@ -65,7 +70,7 @@ struct SmallParams {
     char* tree; size_t tree_game_bytes; int dump_tree;
     unsigned long long* stamps;
     const float4* zero16;    // 16 zero bytes: the address of a skipped chunk's load
-    uint32_t nzm[SM_NZM_N];  // nonzero-chunk masks [wave][stage]: sim stages, then root stages
+    uint32_t nzm[SM_NZM_ALLOC];  // nonzero-chunk masks [wave][stage]: sim stages, then root stages (+ pad)
     int bn;                  // BatchNorm FC layers: `bias` has γ and β sections after the biases
 };
 
@@ -97,7 +102,7 @@ struct SmallUnrollParams {
     const long long* pf_hdr;
     long long pf_epoch;
     const float4* zero16;    // as SmallParams
-    uint32_t nzm[SM_NZM_N];  // nonzero-chunk masks (as SmallParams)
+    uint32_t nzm[SM_NZM_ALLOC];  // nonzero-chunk masks (as SmallParams)
     int bn;                  // as SmallParams
 };
 

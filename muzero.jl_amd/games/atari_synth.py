@@ -15,8 +15,10 @@ The self-play data path (SelfPlay.jl:330-382 -> ReplayBuffer.jl:133-217) needs
 an environment.  `BatchedAtariSynth` is a Philox-keyed stand-in with the shape
 of a frame-stacked Atari game (same rules on the device, mz_selfplay.hip):
 
-* state: a 32-bit key per game.  reset: key = u32(seed, ENV, slot, step, ~0)
-  (step = the move at which the slot restarts; ~0 for the initial games);
+* state: a 32-bit key per game.  reset: key = u32(seed, ENV, game_offset +
+  slot, step, ~0) — the global game id, so the ranks of a data-parallel job
+  play different games (step = the move at which the slot restarts; ~0 for
+  the initial games);
 * frame(key): 84x84 bytes, column-major, the little-endian bytes of the words
   of Philox(c0 = j, c1 = key, c2 = 0, c3 = FRAME; seed), j = 0..440;
 * step(a): (v0, v1, v2, _) = Philox(0, key, a, ENV; seed); reward 1 if
@@ -84,9 +86,10 @@ class BatchedAtariSynth:
     FRAME_STACK = C
     KEYED = True
 
-    def __init__(self, G, seed=0):
+    def __init__(self, G, seed=0, game_offset=0):
         self.G = G
         self.seed = int(seed)
+        self.game_offset = int(game_offset)
         self.board = np.zeros((G, FRAME), np.uint8)       # the current frame
         self.player = np.ones(G, np.int32)
         self.key = np.zeros(G, np.uint32)
@@ -95,7 +98,7 @@ class BatchedAtariSynth:
     def reset(self, idx, step=None):
         s = 0xFFFFFFFF if step is None else int(step)
         for g in np.atleast_1d(idx):
-            self.key[g] = rng_u32(self.seed, MZ_RNG_ENV, int(g), s, 0xFFFFFFFF)
+            self.key[g] = rng_u32(self.seed, MZ_RNG_ENV, self.game_offset + int(g), s, 0xFFFFFFFF)
             self.board[g] = frame(self.seed, self.key[g])
 
     def legal_mask(self):

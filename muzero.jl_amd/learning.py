@@ -4,9 +4,10 @@ Each step: get_batch from the (per-GPU) replay buffer, then one
 ref_semantics learner step on the GPU (mz_learner_step: K-step unroll,
 losses, gradient 2θ per quirk Q11, Flux ADAM with the Cos(λ0=1e-4,
 λ1=1e-1, period=10) learning rate, Learning.jl:318-319,382).  Data-parallel
-training splits the step: gradient -> RCCL all-reduce (sum) of
-the flat bucket -> ADAM with scale 1/world, so every replica applies the same
-update.
+training splits the step: the gradient's data term -> RCCL
+all-reduce (sum) of the flat bucket -> ADAM on data·(1/world) + 2θ, so every
+replica applies the same update, equal to the single-GPU one in ref_semantics
+at any world size.
 """
 import numpy as np
 
@@ -40,19 +41,27 @@ class Learner:
 
 
 def allreduce_step(engine, dev_batch_ptrs, B, grad, losses, step, world, all_reduce, stream=None):
-    """Data-parallel learner step on device buffers: gradient into `grad`
-    (a device tensor of engine.grad_count() floats), `all_reduce(grad)` (sum
-    over ranks; RCCL via torch.distributed on GPU, gloo in CPU tests), then
-    ADAM with scale 1/world.  Power-of-two world sizes keep the replicas
-    bit-identical to the single-GPU update (2θ·world/world is exact)."""
+    """Data-parallel learner step on device buffers: the DATA TERM of the
+    gradient into `grad` (a device tensor of engine.grad_count() floats; zero
+    in ref_semantics, where only Σθ² depends on θ, Q11), `all_reduce(grad)`
+    (sum over ranks; RCCL via torch.distributed on GPU, gloo in CPU tests),
+    then ADAM on ∇ = Σ·(1/world) + 2θ.  The rank-invariant 2θ is added after
+    the exchange (mz_adam_kernel), so every replica's update equals the
+    single-GPU update bit for bit at EVERY world size in ref_semantics — an
+    exchange of the full 2θ would not: a sequential f32 sum of eight equal
+    terms differs from 8x for ~44 % of inputs (dp_gradient)."""
     engine.learner_grad_dev(dev_batch_ptrs, B, grad.data_ptr(), losses.data_ptr(), stream=stream)
     if world > 1:
         all_reduce(grad)
     engine.learner_apply_dev(grad.data_ptr(), 1.0 / world, cos_schedule(step + 1), stream=stream)
 
 
-def reduce_mean_grad(grad, world, all_reduce):
-    """Host-side reference of the DP gradient exchange: sum then scale."""
-    all_reduce(grad)
-    grad *= np.float32(1.0 / world) if isinstance(grad, np.ndarray) else (1.0 / world)
-    return grad
+def dp_gradient(data_grad, theta, world, all_reduce):
+    """Host reference of the data-parallel gradient mz_adam_kernel applies:
+    ∇ = (Σ_ranks data_grad) · f32(1/world) + 2θ, in f32 with the device's
+    operation order (the data term's product rounded, then the sum).
+    data_grad is summed in place by all_reduce (world > 1)."""
+    if world > 1:
+        all_reduce(data_grad)
+    d = np.asarray(data_grad, dtype=np.float32) * np.float32(1.0 / world)
+    return (d + np.asarray(theta, dtype=np.float32) * np.float32(2)).astype(np.float32)

@@ -98,7 +98,8 @@ class BatchedSelfPlay:
         self.conf = engine.conf
         self.G = G
         # keyed envs (games/atari_synth.py) draw from the engine's Philox streams
-        self.env = env_cls(G, seed=engine.rng_seed) if getattr(env_cls, "KEYED", False) else env_cls(G)
+        self.env = (env_cls(G, seed=engine.rng_seed, game_offset=game_offset) if getattr(env_cls, "KEYED", False)
+                    else env_cls(G))
         self.frame_stack = getattr(env_cls, "FRAME_STACK", 0)
         self.game_offset = game_offset
         self.step = step0

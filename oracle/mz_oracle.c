@@ -1019,6 +1019,20 @@ EXPORT void ora_adam_2theta(float* P, float* m, float* v, size_t n, const double
     }
 }
 
+/* The same update with an explicit gradient g (the data-parallel step:
+ * g = (Σ_ranks data term)·(1/world) + 2θ).                      */
+EXPORT void ora_adam_grad(float* P, float* m, float* v, const float* gr, size_t n, const double* bp, double eta) {
+    const double b1 = 0.9, b2 = 0.999, eps = 1e-8;
+    for (size_t i = 0; i < n; ++i) {
+        float g = gr[i];
+        m[i] = (float)(b1 * (double)m[i] + (1.0 - b1) * (double)g);
+        float g2 = g * g;
+        v[i] = (float)(b2 * (double)v[i] + (1.0 - b2) * (double)g2);
+        float d = (float)((double)m[i] / (1.0 - bp[0]) / (sqrt((double)v[i] / (1.0 - bp[1])) + eps) * eta);
+        P[i] = P[i] - d;
+    }
+}
+
 /* ParameterSchedulers 0.2.3 Cos(λ0, λ1, period) with Stateful (1-based t):
  * |λ0−λ1|·(1 + cos(2π(t−1)/period))/2 + min(λ0, λ1). */
 EXPORT double ora_cos_schedule(double l0, double l1, int period, int t) {

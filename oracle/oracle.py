@@ -55,6 +55,7 @@ def lib():
         L.ora_sqnorm.restype = ctypes.c_double
         L.ora_sqnorm.argtypes = [_VP, ctypes.c_size_t]
         L.ora_adam_2theta.argtypes = [_VP, _VP, _VP, ctypes.c_size_t, _VP, ctypes.c_double]
+        L.ora_adam_grad.argtypes = [_VP, _VP, _VP, _VP, ctypes.c_size_t, _VP, ctypes.c_double]
         L.ora_cos_schedule.restype = ctypes.c_double
         L.ora_cos_schedule.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int]
         L.ora_learner_step.argtypes = [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_int, _VP, _VP, _VP,

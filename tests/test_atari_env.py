@@ -45,6 +45,10 @@ def test_env_rules():
         assert env.key[g] == v[2] and np.array_equal(env.board[g], at.frame(5, v[2]))
     env.reset([1], step=42)
     assert env.key[1] == rng_u32(5, at.MZ_RNG_ENV, 1, 42, 0xFFFFFFFF)
+    # keyed by the global game id: slot g of a shard at game_offset o is game o + g
+    sh = at.BatchedAtariSynth(2, seed=5, game_offset=1)
+    assert sh.key[0] == rng_u32(5, at.MZ_RNG_ENV, 1, 0xFFFFFFFF, 0xFFFFFFFF)
+    assert np.array_equal(sh.board[1], at.BatchedAtariSynth(3, seed=5).board[2])
     # episode lengths: terminal with p = 1/128 per move
     env = at.BatchedAtariSynth(64, seed=1)
     ends = 0

@@ -67,7 +67,7 @@ def test_corrected_resnet_gradient_matches_torch(ttt, game, B, K, ir, per):
     g = grad.cpu().numpy()
     off = 0
     for n in range(3):
-        gn = g[off: off + nets[n].size].astype(np.float64) - 2.0 * nets[n]    # the data term (∂Σθ²/∂θ = 2θ)
+        gn = g[off: off + nets[n].size].astype(np.float64)   # grad_dev holds the data term (2θ: apply)
         rn = ref["grads"][n] - 2.0 * nets[n].astype(np.float64)
         off += nets[n].size
         scale = np.abs(rn).max()

@@ -1,6 +1,11 @@
-"""Multi-process (world_size 2, gloo, CPU) tests of the data-parallel paths:
-(1) the learner's gradient exchange (sum all-reduce, scale 1/world) keeps the
-replicas bit-identical to the single-process ref_semantics update;
+"""Multi-process (world_size 2, 4 and 8; gloo, CPU) tests of the
+data-parallel paths:
+(1) the learner's gradient exchange — the data term all-reduced (sum), scaled
+by 1/world, then the rank-invariant 2θ added (learning.dp_gradient, the rule
+of mz_adam_kernel) — keeps every replica bit-identical to the single-process
+ref_semantics update (ora_adam_2theta) at every world size, and the replicas
+identical to each other with a data-dependent term (the corrected mode's);
+the old rule (exchange 2θ itself, then scale) is shown to drift at world 8;
 (2) self-play sharding by game_offset = rank * G reproduces the unsharded
 search (games are independent; no data-path collective)."""
 import os
@@ -32,30 +37,51 @@ def _worker(rank, world, port, q):
     _mzpkg.load()
     from muzero_jl_amd.config import to_c_config, to_c_ffhp, cos_schedule
     from muzero_jl_amd.games import tictactoe as ttt
-    from muzero_jl_amd.learning import reduce_mean_grad
+    from muzero_jl_amd.learning import dp_gradient
     from muzero_jl_amd.networks import init_nets
     from oracle import Oracle, lib
     from conftest import random_positions
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     nets = init_nets(ttt.conf, ttt.hyper, seed=8)
-    theta = np.concatenate(nets)
-    # (1) gradient exchange: every rank's ref_semantics gradient is 2θ
+    theta0 = np.concatenate(nets)
     L = lib()
-    m = np.zeros_like(theta)
-    v = np.zeros_like(theta)
-    bp = np.array([0.9, 0.999])
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+
+    def run(data_fn):
+        th, m, v = theta0.copy(), np.zeros_like(theta0), np.zeros_like(theta0)
+        bp = np.array([0.9, 0.999])
+        for t in range(1, 4):
+            d = torch.from_numpy(data_fn(t))
+            g = dp_gradient(d, th, world, dist.all_reduce)
+            L.ora_adam_grad(vp(th), vp(m), vp(v), vp(g), th.size, vp(bp), cos_schedule(t))
+            bp = bp * np.array([0.9, 0.999])
+        return th
+
+    def identical(x):
+        gathered = [torch.zeros(x.size) for _ in range(world)]
+        dist.all_gather(gathered, torch.from_numpy(x).to(torch.float32))
+        return all(torch.equal(gathered[0], y) for y in gathered)
+
+    # (1a) ref_semantics: every rank's data term is 0 (Q11)
+    theta = run(lambda t: np.zeros_like(theta0))
+    same = identical(theta)
+    single = theta0.copy()
+    m, v, bp = np.zeros_like(single), np.zeros_like(single), np.array([0.9, 0.999])
     for t in range(1, 4):
-        g = torch.from_numpy(theta * np.float32(2))
-        reduce_mean_grad(g, world, dist.all_reduce)
-        assert np.array_equal(g.numpy(), theta * np.float32(2))   # exact for power-of-two world
-        L.ora_adam_2theta(theta.ctypes.data_as(ctypes.c_void_p), m.ctypes.data_as(ctypes.c_void_p),
-                          v.ctypes.data_as(ctypes.c_void_p), theta.size, bp.ctypes.data_as(ctypes.c_void_p),
-                          cos_schedule(t))
+        L.ora_adam_2theta(vp(single), vp(m), vp(v), single.size, vp(bp), cos_schedule(t))
         bp = bp * np.array([0.9, 0.999])
-    gathered = [torch.zeros(theta.size) for _ in range(world)]
-    dist.all_gather(gathered, torch.from_numpy(theta).to(torch.float32))
-    same = all(torch.equal(gathered[0], x) for x in gathered)
+    exact = np.array_equal(theta, single)
+    # (1b) a data-dependent term (rank-seeded): replicas still identical
+    theta_d = run(lambda t: np.random.default_rng(100 * rank + t).standard_normal(theta0.size).astype(np.float32))
+    same_d = identical(theta_d) and not np.array_equal(theta_d, theta)
+    # (1c) the old rule, emulated as RCCL's ring reduces a chunk (sequential f32 sum
+    # of the world's 2θ, then × 1/world): not 2θ for some elements at world 8
+    two = theta0 * np.float32(2)
+    acc = two.copy()
+    for _ in range(world - 1):
+        acc = acc + two
+    old_drift = int(np.count_nonzero(acc * np.float32(1.0 / world) != two))
     # (2) sharded search
     conf = dataclasses.replace(ttt.conf, num_iters=8)
     o = Oracle(to_c_config(conf), to_c_ffhp(ttt.hyper), seed=3)
@@ -69,22 +95,28 @@ def _worker(rank, world, port, q):
     dist.all_gather(acts, torch.from_numpy(act))
     if rank == 0:
         _, _, full = o.mcts_search(obs, legal, tp, rng_step=9, game_offset=0)
-        q.put((same, np.array_equal(torch.cat(acts).numpy(), full), theta.copy()))
+        q.put((same, exact, same_d, old_drift, np.array_equal(torch.cat(acts).numpy(), full)))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_gloo_dp_and_sharding():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gloo_dp_exact_and_sharding(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    same, shard_ok, theta = q.get(timeout=240)
+    same, exact, same_d, old_drift, shard_ok = q.get(timeout=240)
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert same, "replicas diverged"
+    assert exact, "the data-parallel update differs from the single-process ref_semantics update"
+    assert same_d, "replicas diverged with a data-dependent gradient term"
+    if world == 8:      # why 2θ is not exchanged: Σ of eight equal f32 terms is not always 8x
+        assert old_drift > 0
+    else:               # x+x, 2x+x, 3x+x are exact in f32
+        assert old_drift == 0
     assert shard_ok, "sharded search differs from the unsharded one"
