@@ -1084,6 +1084,11 @@ static RPlan rn_plan(const mz_handle* h, const std::vector<RSpec>& sp, int net, 
     if (net == MZ_NET_REPR) { R.out0_off = B0; R.out0_n = h->H; R.out1_n = 0; }
     else if (net == MZ_NET_PRED) { R.out0_off = O0; R.out0_n = 1; R.out1_off = O1; R.out1_n = h->A; }
     else { R.out0_off = B2; R.out0_n = h->H; R.out1_off = O1; R.out1_n = 1; }
+    R.out0_act = R.out1_act = MZ_ACT_IDENTITY;
+    for (int j = 0; j < R.n; ++j) {
+        if (R.L[j].out_off == R.out0_off) R.out0_act = R.L[j].act;
+        if (R.out1_n && R.L[j].out_off == R.out1_off) R.out1_act = R.L[j].act;
+    }
     if (otab) {   // narrow plans: offset tables for the kernels > 1x1 (shared by layers of the same input / shape)
         const int n_nb = (P * NG + 15) >> 4, nbw = n_nb == 1 ? 1 : n_nb == 2 ? 2 : 3;
         const int ncols_t = (n_nb + nbw - 1) / nbw * nbw * 16;
@@ -1333,8 +1338,14 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
         h->rn_lds[n] = (size_t)h->rplan[n].lds_floats * 4;
     }
     for (int n = 1; n < 3; ++n)                          // mz_rsearch_nets has no k-table path (NOKK)
-        for (int i = 0; i < h->rplan[n].n; ++i)
-            CK(h->rplan[n].L[i].kk > 1 ? fail(h, "ResNet plan: a prediction / dynamics kernel > 1x1") : 0);
+        for (int i = 0; i < h->rplan[n].n; ++i) {
+            const RLayer& L = h->rplan[n].L[i];
+            CK(L.kk > 1 ? fail(h, "ResNet plan: a prediction / dynamics kernel > 1x1") : 0);
+            // and applies a tanh only where the read-out does (RAWTANH): on the outputs
+            CK(L.act == MZ_ACT_TANH && L.out_off != h->rplan[n].out0_off &&
+                       !(h->rplan[n].out1_n && L.out_off == h->rplan[n].out1_off)
+                   ? fail(h, "ResNet plan: a tanh layer that is not an output") : 0);
+        }
     h->packed_w_n = sw.size(); h->packed_b_n = 0;
     h->rn_dyn_split = (int)sp[MZ_NET_DYN].size();     // the reward head: the dynamics layers of chain 2
     for (size_t i = 0; i < sp[MZ_NET_DYN].size(); ++i)

@@ -134,7 +134,7 @@ __device__ __forceinline__ void rn_epilogue_full(const RLayer& L, const float (&
     }
 }
 
-template <int NB>
+template <int NB, bool RAWTANH = false>
 __device__ __forceinline__ void rn_epilogue(const RLayer& L, const mz_f32x4 (&acc)[NB][4], const float (&ep)[3][4],
                                             float* lds, int ob, int kl, const int (&n)[NB], int ncols, float bn_s,
                                             float bn_r, const float (&res)[NB][4]) {
@@ -197,7 +197,9 @@ __device__ __forceinline__ void rn_epilogue(const RLayer& L, const mz_f32x4 (&ac
             if (n[i] >= ncols) continue;
             float v = d[i][r];
             if (L.res_add) v = v + res[i][r];
-            lds[L.out_off + rn_out_idx(L.out_kb, ob, kl, r, n[i], ncols)] = rn_act(L.act, v);
+            // RAWTANH: no det_tanhf (f64) code in the layer loop; the read-out applies it
+            lds[L.out_off + rn_out_idx(L.out_kb, ob, kl, r, n[i], ncols)] =
+                RAWTANH ? (L.act == MZ_ACT_RELU ? mz_relu(v) : v) : rn_act(L.act, v);
         }
     }
 }
@@ -223,7 +225,7 @@ struct RnPf {
     float ep[3][4];
 };
 
-template <int NBW, int MODE, bool PF = false, bool PIPE = false>
+template <int NBW, int MODE, bool PF = false, bool PIPE = false, bool RAWTANH = false>
 __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restrict__ Wimg,
                                            const float* __restrict__ flat, float* lds, int NG, int Wb, int P,
                                            float bn_s, float bn_r, const RnPf* pf = nullptr,
@@ -504,7 +506,7 @@ __device__ __forceinline__ void rn_layer_t(const RLayer& L, const float* __restr
 #endif
         RN_DBG_WAIT(2);                                 // chunks done (MFMA results consumed)
         if constexpr (NBW != 1) rn_load_res<NBW>(L, lds, res, ob, kl, nn, ncols);
-        rn_epilogue<NBW>(L, acc, ep, lds, ob, kl, nn, ncols, bn_s, bn_r, res);
+        rn_epilogue<NBW, RAWTANH>(L, acc, ep, lds, ob, kl, nn, ncols, bn_s, bn_r, res);
         RN_DBG_WAIT(3);                                 // epilogue stored
     }
 }
@@ -525,13 +527,13 @@ __device__ __forceinline__ int rn_nbw(const RLayer& L, int NG, int P) {
 
 // NBWMAX = 1: a narrow kernel instance for tiles of one column block (the host
 // launches it only then): the 1-block units alone, a fifth of the code
-template <bool NARROW, bool PF = false, int NBWMAX = 3, bool PIPE = false, bool NOKK = false>
+template <bool NARROW, bool PF = false, int NBWMAX = 3, bool PIPE = false, bool NOKK = false, bool RAWTANH = false>
 __device__ __forceinline__ void rn_layer(const RLayer& L, const float* __restrict__ Wimg,
                                          const float* __restrict__ flat, float* lds, int NG, int Wb, int P,
                                          float bn_s, float bn_r, const RnPf* pf = nullptr,
                                          unsigned long long* dbg = nullptr) {
     const int n_nb = NBWMAX == 1 ? 1 : NARROW && L.spatial ? (P * NG + 15) >> 4 : 3;     // as rn_nbw
-#define RN_L(NB, M) rn_layer_t<NB, M, PF, PIPE>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg)
+#define RN_L(NB, M) rn_layer_t<NB, M, PF, PIPE, RAWTANH>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, pf, dbg)
     if (NARROW && L.otab) {                                           // kernel > 1x1 through the offset table
         if (n_nb == 1) RN_L(1, 4);
         else if constexpr (NBWMAX > 1) { if (n_nb == 2) RN_L(2, 4); else RN_L(3, 4); }
@@ -589,7 +591,8 @@ __device__ void rn_fill_ktabs(const RPlan& R, float* lds, int NG, int Wb, int P)
 // PF: the next layer's plan entry, first A chunk and epilogue parameters are
 // loaded before each layer barrier (kernels with the register room: 512
 // threads).  Layers [i0, i1) (i1 < 0: to the end).
-template <bool NARROW = false, bool PF = false, int NBWMAX = 3, bool PIPE = false, bool NOKK = false>
+template <bool NARROW = false, bool PF = false, int NBWMAX = 3, bool PIPE = false, bool NOKK = false,
+          bool RAWTANH = false>
 __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const float* flat, float* lds, int NG,
                                        int Wb, int P, float bn_s, unsigned long long* st = nullptr, int i0 = 0,
                                        int i1 = -1) {
@@ -611,7 +614,7 @@ __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const 
 #ifdef MZ_STAMPS
             if (st && i - i0 < 31) dbg = st + 1024 + 8 * (i - i0);
 #endif
-            rn_layer<NARROW, true, NBWMAX, PIPE, NOKK>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, &pf, dbg);
+            rn_layer<NARROW, true, NBWMAX, PIPE, NOKK, RAWTANH>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, &pf, dbg);
             if (i + 1 < i1) rn_prefetch<NARROW>(Ln, Wimg, flat, NG, P, pf);
 #ifdef MZ_STAMPS
             if (st && (threadIdx.x & 63) == 0 && i - i0 < 31) st[wv * 64 + 2 * (i - i0)] = __builtin_amdgcn_s_memtime();
@@ -628,7 +631,7 @@ __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const 
 #ifdef MZ_STAMPS   // wave 0's first unit: [start, operands, chunks, epilogue] at st + 768 + 8·layer
             if (st && i - i0 < 32) dbg = st + 768 + 8 * (i - i0);
 #endif
-            rn_layer<NARROW, false, NBWMAX, false, NOKK>(rn_layer_at(R, i), Wimg, flat, lds, NG, Wb, P, bn_s, bn_r,
+            rn_layer<NARROW, false, NBWMAX, false, NOKK, RAWTANH>(rn_layer_at(R, i), Wimg, flat, lds, NG, Wb, P, bn_s, bn_r,
                                                          nullptr, dbg);
 #ifdef MZ_STAMPS
             if (st && (threadIdx.x & 63) == 0 && i - i0 < 31) st[wv * 64 + 2 * (i - i0)] = __builtin_amdgcn_s_memtime();
@@ -716,6 +719,78 @@ __device__ __forceinline__ void rn_stage_rows(float* dst, int kb, int NG, int P,
             }
         }
     }
+}
+
+// The reverse of rn_stage_rows: row_g[f..f+3] <- LDS tile [f][g] (plain or
+// k-blocked) for f < H (H % 4 == 0), each lane gathering the 16-byte piece
+// l / NG of game l mod NG (conflict-free LDS reads: consecutive lanes,
+// consecutive games) and handing it to put(g, piece, float4): one wave
+// instruction stores 64 contiguous bytes of each of 16 rows instead of 4
+// bytes (rn_unstage_l), four pieces in flight per thread
+template <class PutFn>
+__device__ __forceinline__ void rn_unstage_rows(const float* src, int kb, int NG, int P, int H, int t0, int G,
+                                                PutFn put) {
+    const int H4 = H >> 2, n4 = NG * H4, nt = blockDim.x, lg = __ffs(NG) - 1;
+    for (int i0 = threadIdx.x; i0 < n4; i0 += 4 * nt) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * nt;
+            if (i < n4) {
+                const int g = i & (NG - 1), f = (i >> lg) * 4;
+                v[u] = make_float4(src[rn_conv_idx(kb, f, g, NG, P)], src[rn_conv_idx(kb, f + 1, g, NG, P)],
+                                   src[rn_conv_idx(kb, f + 2, g, NG, P)], src[rn_conv_idx(kb, f + 3, g, NG, P)]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * nt;
+            const int g = i & (NG - 1);
+            if (i < n4 && t0 + g < G) put(g, i >> lg, v[u]);
+        }
+    }
+}
+
+// rn_stage_rows with the pieces from ld(g, piece) (a float4; games t0 + g >=
+// G stage zeros)
+template <class LdFn>
+__device__ __forceinline__ void rn_stage_rows_ld(float* dst, int kb, int NG, int P, int H, int t0, int G, LdFn ld) {
+    const int H4 = H >> 2, n4 = NG * H4, nt = blockDim.x, lg = __ffs(NG) - 1;
+    for (int i0 = threadIdx.x; i0 < n4; i0 += 4 * nt) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * nt;
+            const int g = i & (NG - 1);
+            v[u] = i < n4 && t0 + g < G ? ld(g, i >> lg) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * nt;
+            if (i < n4) {
+                const int g = i & (NG - 1), f = (i >> lg) * 4;
+                dst[rn_conv_idx(kb, f, g, NG, P)] = v[u].x;
+                dst[rn_conv_idx(kb, f + 1, g, NG, P)] = v[u].y;
+                dst[rn_conv_idx(kb, f + 2, g, NG, P)] = v[u].z;
+                dst[rn_conv_idx(kb, f + 3, g, NG, P)] = v[u].w;
+            }
+        }
+    }
+}
+
+// 16-byte write-through (sc1) store / load of a float4 at byte offset `off`
+// of buffer `rs`: the payload of a cross-workgroup hand-off (mz_poll_ge's R1
+// protocol) in whole 16-byte pieces, 64 contiguous bytes per row per wave
+// instruction (one 4-byte agent-scope store per element wrote each element's
+// line through separately: 25 MB of writes per configs[2] launch)
+typedef unsigned rn_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void rn_st_sc1(__amdgpu_buffer_rsrc_t rs, int off, float4 v) {
+    const rn_v4u u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 16);
+}
+__device__ __forceinline__ float4 rn_ld_sc1(__amdgpu_buffer_rsrc_t rs, int off) {
+    const rn_v4u u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+    return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
 }
 
 // Batched forward of one net (mz_net_forward): x (in_feat, n) -> out0, out1.
@@ -1139,27 +1214,37 @@ extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RS
     // prefetch into the layer's own registers measured 76 vs 70 µs)
     if (split) {
         if (net == MZ_NET_DYN) {
-            rn_run<false, false, 3, false, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st, 0, P.trunk_nl);
+            rn_run<false, false, 3, false, true, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st, 0, P.trunk_nl);
             const RLayer Ls = rn_layer_at(R, P.dyn_split);             // the reward head's input: the trunk output
-            if (ok)
+            if ((H & 3) == 0) {                                         // 16-byte sc1 pieces (rn_st_sc1)
+                const auto rs = __builtin_amdgcn_make_buffer_rsrc(P.trunk, (short)0, P.G * H * 4, 0x00020000);
+                rn_unstage_rows(lds + Ls.in_off, Ls.in_kb, NG, P.P, H, t0, P.G, [&](int g, int q, float4 v) {
+                    rn_st_sc1(rs, ((t0 + g) * H + 4 * q) * 4, v);
+                });
+            } else if (ok) {
                 rn_unstage_l(lds + Ls.in_off, Ls.in_kb, NG, P.P, H, t, [&](int f, float v) {
                     __hip_atomic_store(P.trunk + (size_t)gg * H + f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 });
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");            // every wave's stores performed
             __syncthreads();
             if (threadIdx.x == 0 && (int)blockIdx.x != P.dbg_skip)
                 __hip_atomic_store(P.tprog + blockIdx.x, P.tepoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            rn_run<false, false, 3, false, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, nullptr, P.trunk_nl,
+            rn_run<false, false, 3, false, true, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, nullptr, P.trunk_nl,
                                                  P.dyn_split);                        // the state head
-            if (ok) {
+            if ((H & 3) == 0) {
+                rn_unstage_rows(lds + R.out0_off, R.out0_kb, NG, P.P, H, t0, P.G, [&](int g, int q, float4 v) {
+                    reinterpret_cast<float4*>(P.hid + ((size_t)(t0 + g) * (S + 1) + P.s + 1) * H)[q] = v;
+                });
+            } else if (ok) {
                 float* o = P.hid + ((size_t)gg * (S + 1) + P.s + 1) * H;
                 rn_unstage_l(lds + R.out0_off, R.out0_kb, NG, P.P, H, t, [&](int f, float v) { o[f] = v; });
             }
             return;
         }
-        rn_run<false, false, 3, false, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st);
+        rn_run<false, false, 3, false, true, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st);
         if (ok) {
-            if (t.f0 == 0) P.o_v[gg] = lds[R.out0_off + t.g];
+            if (t.f0 == 0) P.o_v[gg] = rn_act(R.out0_act, lds[R.out0_off + t.g]);   // (RAWTANH)
             float* o = P.o_logit + (size_t)gg * P.A;
             rn_unstage(lds + R.out1_off, NG, P.A, t, [&](int f, float v) { o[f] = v; });
         }
@@ -1169,28 +1254,35 @@ extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RS
         __syncthreads();
         const RPlan& Rd = P.plans[MZ_NET_DYN];
         const RLayer Ls = rn_layer_at(Rd, P.dyn_split);
-        rn_stage_l(lds + Ls.in_off, Ls.in_kb, NG, P.P, H, t, [&](int f) {
-            return ok ? __hip_atomic_load(P.trunk + (size_t)gg * H + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : 0.0f;
-        });
+        if ((H & 3) == 0) {                                           // 16-byte sc1 pieces (rn_ld_sc1)
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(P.trunk, (short)0, P.G * H * 4, 0x00020000);
+            rn_stage_rows_ld(lds + Ls.in_off, Ls.in_kb, NG, P.P, H, t0, P.G, [&](int g, int q) {
+                return rn_ld_sc1(rs, ((t0 + g) * H + 4 * q) * 4);
+            });
+        } else {
+            rn_stage_l(lds + Ls.in_off, Ls.in_kb, NG, P.P, H, t, [&](int f) {
+                return ok ? __hip_atomic_load(P.trunk + (size_t)gg * H + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : 0.0f;
+            });
+        }
         __syncthreads();
-        rn_run<false, false, 3, false, true>(Rd, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, nullptr, P.dyn_split);
-        if (ok && t.f0 == 0) P.o_r[gg] = lds[Rd.out1_off + t.g];
+        rn_run<false, false, 3, false, true, true>(Rd, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, nullptr, P.dyn_split);
+        if (ok && t.f0 == 0) P.o_r[gg] = rn_act(Rd.out1_act, lds[Rd.out1_off + t.g]);
         return;
     }
-    rn_run<false, false, 3, false, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st);
+    rn_run<false, false, 3, false, true, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st);
 #ifdef MZ_STAMPS
     if (st && (threadIdx.x & 63) == 0) st[(threadIdx.x >> 6) * 64 + 61] = __builtin_amdgcn_s_memtime();
 #endif
     if (!ok) return;
     if (net == MZ_NET_PRED) {
-        if (t.f0 == 0) P.o_v[gg] = lds[R.out0_off + t.g];
+        if (t.f0 == 0) P.o_v[gg] = rn_act(R.out0_act, lds[R.out0_off + t.g]);
         float* o = P.o_logit + (size_t)gg * P.A;
         rn_unstage(lds + R.out1_off, NG, P.A, t, [&](int f, float v) { o[f] = v; });
     } else {
         float* o = P.hid + ((size_t)gg * (S + 1) + P.s + 1) * H;
         rn_unstage_l(lds + R.out0_off, R.out0_kb, NG, P.P, H, t, [&](int f, float v) { o[f] = v; });
-        if (t.f0 == 0) P.o_r[gg] = lds[R.out1_off + t.g];
+        if (t.f0 == 0) P.o_r[gg] = rn_act(R.out1_act, lds[R.out1_off + t.g]);
     }
 }
 

@@ -93,6 +93,8 @@ struct RPlan {
     int out0_off, out0_n;              // out0: h (REPR, DYN) or value (PRED)
     int out0_kb;                       // out0 k-blocked (h of the dynamics, when its state head reads it so)
     int out1_off, out1_n;              // out1: policy logits (PRED) or reward (DYN), n = 0 if none
+    int out0_act, out1_act;            // the activation of the layer writing out0 / out1 (rn_run<.., RAWTANH>
+                                       // leaves a tanh unapplied in LDS; the caller applies it on read-out)
     int lds_floats;                    // LDS per workgroup (floats), k tables included
     // narrow (learner chain) plans: the B-operand byte offsets of the layers with a
     // kernel > 1x1 ([q][chunk][column][slot][4 k-steps], rn_otab_fill), copied
