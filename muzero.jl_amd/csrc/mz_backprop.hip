@@ -486,9 +486,12 @@ extern "C" __global__ __launch_bounds__(256) void mz_bp_fold(BpFoldParams Q) {
 
 // ============================================================================
 // The corrected learner for the ResNet nets (mz_backprop_params.h RbpApp):
-// one 256-thread workgroup per sample, its arena T (activations) and G (their
-// gradients) in HBM; the current application's input and ∂L/∂t staged in LDS.
-#define RBP_THREADS 256
+// mz_rbp_sample, one workgroup per sample, its arena T (activations) and G
+// (their gradients) in HBM; the current application's input and ∂L/∂t staged
+// in LDS.  The parameter gradients: mz_rbp_dw.
+#ifndef RBP_THREADS
+#define RBP_THREADS 768                      // up to 12 waves: a Connect4 conv has 4 x 3 blocks per pass
+#endif
 
 // im2col operand of a conv, input element (k, p) for k = i + kw·j + kw·kh·c:
 // x[c] at (px, py) = (p mod W + (kw−1−i) − kw/2, p div W + (kh−1−j) − kh/2),
@@ -497,15 +500,18 @@ extern "C" __global__ __launch_bounds__(256) void mz_bp_fold(BpFoldParams Q) {
 // (the quotient's fraction is at least 1/d away from the next integer)
 __device__ __forceinline__ int rbp_div(int n, int d, float rd) { return (int)(((float)n + 0.5f) * rd); }
 
-__device__ __forceinline__ float rbp_xhat(const float* X, const RbpApp& L, int P, int Wb, int k, int p) {
-    const int kk = L.kw * L.kh;
-    if (k >= kk * L.cin || p >= P) return 0.0f;
+__device__ __forceinline__ float rbp_xhat_k(const float* X, int cin, int kw, int kh, int P, int Wb, int k, int p) {
+    const int kk = kw * kh;
+    if (k >= kk * cin || p >= P) return 0.0f;
     if (kk == 1) return X[k * P + p];                        // 1x1 conv
     const int c = rbp_div(k, kk, 1.0f / (float)kk), r = k - c * kk;
-    const int j = rbp_div(r, L.kw, 1.0f / (float)L.kw), i = r - j * L.kw;
+    const int j = rbp_div(r, kw, 1.0f / (float)kw), i = r - j * kw;
     const int pyy = rbp_div(p, Wb, 1.0f / (float)Wb);
-    const int px = p - pyy * Wb + (L.kw - 1 - i) - L.kw / 2, py = pyy + (L.kh - 1 - j) - L.kh / 2;
+    const int px = p - pyy * Wb + (kw - 1 - i) - kw / 2, py = pyy + (kh - 1 - j) - kh / 2;
     return px >= 0 && px < Wb && py >= 0 && py < P / Wb ? X[c * P + px + Wb * py] : 0.0f;
+}
+__device__ __forceinline__ float rbp_xhat(const float* X, const RbpApp& L, int P, int Wb, int k, int p) {
+    return rbp_xhat_k(X, L.cin, L.kw, L.kh, P, Wb, k, p);
 }
 
 // bp_gemm_block with RBP_KC k-steps of operands in flight per full chunk (one
@@ -577,25 +583,14 @@ __device__ __forceinline__ void rbp_dense_fwd(const RbpParams& Q, const RbpApp& 
     }
 }
 
-// ∂L/∂t of a conv (t = Wx + b) into DT, the residual input's share of ∂L/∂y,
-// and the per-channel sums: db = Σ dt, dβ = Σ du, dγ = Σ du·t/√(1+ε)
-__device__ __forceinline__ void rbp_conv_dt(const RbpParams& Q, const RbpApp& L, const float* T, float* G, float* DT, float* gs) {
+// ∂L/∂t of a conv (t = Wx + b) into DT and the residual input's share of ∂L/∂y
+__device__ __forceinline__ void rbp_conv_dt(const RbpParams& Q, const RbpApp& L, const float* T, float* G, float* DT) {
     const int P = Q.P;
-    for (int o = threadIdx.x; o < L.cout; o += blockDim.x) {
-        const bool bn = L.bn_off >= 0;
-        const float gr = bn ? Q.flat[L.bn_off + L.cout + o] / MZ_BN_S : 1.0f;
-        float sb = 0.0f, sbe = 0.0f, sga = 0.0f;
-        for (int p = 0; p < P; ++p) {
-            const int e = o * P + p;
-            const float du = bp_dz(L.act, G[L.y + e], T[L.y + e]);
-            if (L.res >= 0) G[L.res + e] += du;
-            const float dt = bn ? du * gr : du;
-            if (bn) { sbe += du; sga += du * (T[L.z + e] / MZ_BN_S); }
-            DT[e] = dt;
-            sb += dt;
-        }
-        gs[L.b_off + o] += sb;
-        if (bn) { gs[L.bn_off + o] += sbe; gs[L.bn_off + L.cout + o] += sga; }
+    for (int e = threadIdx.x; e < L.cout * P; e += blockDim.x) {
+        const int o = rbp_div(e, P, 1.0f / (float)P);
+        const float du = bp_dz(L.act, G[L.y + e], T[L.y + e]);
+        if (L.res >= 0) G[L.res + e] += du;
+        DT[e] = L.bn_off >= 0 ? du * (Q.flat[L.bn_off + L.cout + o] / MZ_BN_S) : du;
     }
 }
 
@@ -625,21 +620,6 @@ __device__ __forceinline__ void rbp_conv_dx(const RbpParams& Q, const RbpApp& L,
     for (int r = 0; r < 4; ++r) {
         const int c = ib * 16 + kq * 4 + r;
         if (c < L.cin && p < P) G[L.x + c * P + p] += acc[r];
-    }
-}
-
-// this sample's dW of a conv, block (16 output channels x 16 k) u: Σ_p dt ⊗ x̂
-__device__ __forceinline__ void rbp_conv_dw(const RbpParams& Q, const RbpApp& L, const float* X, const float* DT, float* gs, int u) {
-    const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4, P = Q.P;
-    const int K = L.kw * L.kh * L.cin, nkb = (K + 15) >> 4, ob = u / nkb, kb = u - ob * nkb;
-    const int co = ob * 16 + m, kc = kb * 16 + m;
-    const bp_f32x4 acc = rbp_gemm_block((P + 3) >> 2, kq,
-        [&](int p) { return co < L.cout && p < P ? DT[co * P + p] : 0.0f; },
-        [&](int p) { return rbp_xhat(X, L, P, Q.Wb, kc, p); });
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int o = ob * 16 + kq * 4 + r;
-        if (o < L.cout && kc < K) gs[L.w_off + kc + (size_t)K * o] += acc[r];
     }
 }
 
@@ -688,9 +668,7 @@ extern "C" __global__ __launch_bounds__(RBP_THREADS) void mz_rbp_sample(RbpParam
     float* G = Q.grad + (size_t)b * Q.arena;
     float* DT = rbp_lds;                                      // [dt_floats] ∂L/∂t of the current application
     float* XS = rbp_lds + Q.dt_floats;                        // [xs_floats] its input, staged
-    float* gs = Q.gsam + (size_t)b * Q.nflat;
     for (int e = tid; e < Q.arena; e += nt) G[e] = 0.0f;
-    for (int e = tid; e < Q.nflat; e += nt) gs[e] = 0.0f;
     for (int e = tid; e < K1 * 3; e += nt) Q.terms[(size_t)b * K1 * 3 + e] = 0.0f;
     for (int e = tid; e < K1; e += nt) Q.pr[(size_t)b * K1 + e] = 0.0f;        // rewards: 0 at step 0
     for (int e = tid; e < Q.obs_feat; e += nt) T[Q.obs_t + e] = Q.obs[(size_t)b * Q.obs_feat + e];
@@ -714,37 +692,28 @@ extern "C" __global__ __launch_bounds__(RBP_THREADS) void mz_rbp_sample(RbpParam
     }
     rbp_heads(Q, T, G, b);
     __syncthreads();
-    // ---- backward, reverse order
+    // ---- backward, reverse order: the input gradients (the parameter
+    // gradients are mz_rbp_dw's, from the arenas this leaves behind)
     for (int a = Q.n_app - 1; a >= 0; --a) {
         const RbpApp L = Q.apps[a];
         if (L.op == RBP_CONV) {
-            rbp_conv_dt(Q, L, T, G, DT, gs);
-            for (int e = tid; e < L.cin * Q.P; e += nt) XS[e] = T[L.x + e];
-            __syncthreads();
-            const int K = L.kw * L.kh * L.cin;
-            const int ndx = L.step ? 0 : ((L.cin + 15) >> 4) * npb, ndw = ((L.cout + 15) >> 4) * ((K + 15) >> 4);
-            for (int u = wave; u < ndx + ndw; u += nw) {
-                if (u < ndx) rbp_conv_dx(Q, L, DT, G, u);
-                else rbp_conv_dw(Q, L, XS, DT, gs, u - ndx);
+            rbp_conv_dt(Q, L, T, G, DT);
+            if (!L.step) {
+                __syncthreads();
+                const int ndx = ((L.cin + 15) >> 4) * npb;
+                for (int u = wave; u < ndx; u += nw) rbp_conv_dx(Q, L, DT, G, u);
             }
         } else if (L.op == RBP_DENSE) {
-            for (int o = tid; o < L.cout; o += nt) {
-                const float dz = bp_dz(L.act, G[L.y + o], T[L.y + o]);
-                DT[o] = dz;
-                gs[L.b_off + o] += dz;
-            }
-            __syncthreads();
-            const float* W = Q.flat + L.w_off;
-            for (int e = tid; e < L.cout * L.cin; e += nt) {
-                const int i = e / L.cout, o = e - i * L.cout;
-                gs[L.w_off + e] += DT[o] * T[L.x + i];
-            }
-            if (!L.step)
+            if (!L.step) {
+                for (int o = tid; o < L.cout; o += nt) DT[o] = bp_dz(L.act, G[L.y + o], T[L.y + o]);
+                __syncthreads();
+                const float* W = Q.flat + L.w_off;
                 for (int i = tid; i < L.cin; i += nt) {
                     float s = 0.0f;
                     for (int o = 0; o < L.cout; ++o) s = fmaf(W[o + (size_t)L.cout * i], DT[o], s);
                     G[L.x + i] += s;
                 }
+            }
         } else {                                              // ∂(2h)/∂h
             for (int f = tid; f < L.cin; f += nt) G[L.x + f] += 2.0f * G[L.y + f];
         }
@@ -752,24 +721,92 @@ extern "C" __global__ __launch_bounds__(RBP_THREADS) void mz_rbp_sample(RbpParam
     }
 }
 
-// Σ over samples (ascending) = the data term, and Σθ² of each chunk (f64,
-// fixed tree); mz_adam_kernel adds 2θ after the data-parallel exchange
-extern "C" __global__ __launch_bounds__(256) void mz_rbp_reduce(RbpReduceParams R) {
-    __shared__ double red[256];
-    const int tid = threadIdx.x, s0 = R.chunk_start[blockIdx.x], s1 = R.chunk_start[blockIdx.x + 1];
+// The parameter gradients of the ResNet nets, one wave per job (a 16x16 block
+// of a layer's W, or the db / dβ / dγ of 16 output channels): Σ over samples b,
+// the layer's applications u and positions p (f32 MFMA with K = that flattened
+// index, four per step) of ∂L/∂t ⊗ the im2col input — ∂L/∂t re-formed from the
+// arenas (dt = du·γ/√(1+ε) with BatchNorm, du = ∂L/∂y ⊙ act'(y)) as mz_rbp_sample
+// formed it.  Writes the data term and the block's Σθ² (f64, fixed tree).
+__device__ __forceinline__ void rbp_dw_index(int t, int nuP, float rnuP, int P, float rP, int& b, int& u, int& p) {
+    b = rbp_div(t, nuP, rnuP);
+    const int r = t - b * nuP;
+    u = rbp_div(r, P, rP);
+    p = r - u * P;
+}
+extern "C" __global__ __launch_bounds__(64) void mz_rbp_dw(RbpDwParams Q) {
+    const RbpJob J = Q.jobs[blockIdx.x];
+    const RbpLayer L = Q.layers[J.layer];
+    const int lane = threadIdx.x, m = lane & 15, kq = lane >> 4;
+    const int P = L.conv ? Q.P : 1, nuP = L.n_use * P, n = Q.B * nuP;
+    const float rnuP = 1.0f / (float)(nuP > 0 ? nuP : 1), rP = 1.0f / (float)P;
+    const bool bn = L.conv && L.bn_off >= 0;
     double q = 0.0;
-    for (int i = s0 + tid; i < s1; i += 256) {
-        float s = 0.0f;
-        for (int b = 0; b < R.B; ++b) s += R.gsam[(size_t)b * R.nflat + i];
-        const float th = R.flat[i];
-        R.out[i] = s;
-        q += (double)th * (double)th;
+    if (J.kb < 0) {                                           // db, dβ, dγ of channels ob·16 + m
+        const int o = J.ob * 16 + m;
+        const bool in = o < L.cout;
+        const float gr = bn && in ? Q.flat[L.bn_off + L.cout + o] / MZ_BN_S : 1.0f;
+        float sb = 0.0f, sbe = 0.0f, sga = 0.0f;
+        if (in)
+            for (int t = kq; t < n; t += 4) {                 // quarter kq of the reduction
+                int b, u, p;
+                rbp_dw_index(t, nuP, rnuP, P, rP, b, u, p);
+                const RbpUse U = Q.uses[L.use0 + u];
+                const float* T = Q.act + (size_t)b * Q.arena;
+                const float* G = Q.grad + (size_t)b * Q.arena;
+                const int e = o * P + p;
+                const float du = bp_dz(L.act, G[U.y + e], T[U.y + e]);
+                sb += bn ? du * gr : du;
+                if (bn) { sbe += du; sga += du * (T[U.z + e] / MZ_BN_S); }
+            }
+        // the four quarters in a fixed order: (q0 + q1) + (q2 + q3)
+        sb += __shfl_xor(sb, 16); sb += __shfl_xor(sb, 32);
+        sbe += __shfl_xor(sbe, 16); sbe += __shfl_xor(sbe, 32);
+        sga += __shfl_xor(sga, 16); sga += __shfl_xor(sga, 32);
+        if (kq == 0 && in) {
+            const float tb = Q.flat[L.b_off + o];
+            Q.out[L.b_off + o] = sb;
+            q = (double)tb * (double)tb;
+            if (bn) {
+                const float tbe = Q.flat[L.bn_off + o], tga = Q.flat[L.bn_off + L.cout + o];
+                Q.out[L.bn_off + o] = sbe;
+                Q.out[L.bn_off + L.cout + o] = sga;
+                q += (double)tbe * (double)tbe + (double)tga * (double)tga;
+            }
+        }
+    } else {                                                  // W block (rows ob·16.., columns kb·16..)
+        const int K = L.conv ? L.kw * L.kh * L.cin : L.cin;
+        const int co = J.ob * 16 + m, kc = J.kb * 16 + m;
+        const bool oin = co < L.cout, kin = kc < K;
+        const float gr = bn && oin ? Q.flat[L.bn_off + L.cout + co] / MZ_BN_S : 1.0f;
+        const bp_f32x4 acc = rbp_gemm_block((n + 3) >> 2, kq,
+            [&](int t) {
+                if (!oin || t >= n) return 0.0f;
+                int b, u, p;
+                rbp_dw_index(t, nuP, rnuP, P, rP, b, u, p);
+                const RbpUse U = Q.uses[L.use0 + u];
+                const size_t base = (size_t)b * Q.arena + U.y + co * P + p;
+                const float du = bp_dz(L.act, Q.grad[base], Q.act[base]);
+                return bn ? du * gr : du;
+            },
+            [&](int t) {
+                if (!kin || t >= n) return 0.0f;
+                int b, u, p;
+                rbp_dw_index(t, nuP, rnuP, P, rP, b, u, p);
+                const RbpUse U = Q.uses[L.use0 + u];
+                const float* X = Q.act + (size_t)b * Q.arena + U.x;
+                return L.conv ? rbp_xhat_k(X, L.cin, L.kw, L.kh, P, Q.Wb, kc, p) : X[kc];
+            });
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int o = J.ob * 16 + kq * 4 + r;
+            if (o < L.cout && kin) {
+                const size_t w = (size_t)L.w_off + (L.conv ? kc + (size_t)K * o : o + (size_t)L.cout * kc);
+                const float th = Q.flat[w];
+                Q.out[w] = acc[r];
+                q += (double)th * (double)th;
+            }
+        }
     }
-    red[tid] = q;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (tid < o) red[tid] += red[tid + o];
-        __syncthreads();
-    }
-    if (tid == 0) R.sq[blockIdx.x] = red[0];
+    for (int d = 32; d > 0; d >>= 1) q += __shfl_xor(q, d);        // fixed tree: Σθ² of the block
+    if (lane == 0) Q.sq[blockIdx.x] = q;
 }

@@ -95,17 +95,21 @@ struct BpFoldParams {
     const double* sq; int job0[4];        // mz_bp_dw's per-job Σθ²; jobs [job0[n], job0[n+1]) are net n's
 };
 
-// ---- the corrected learner for the ResNet nets (mz_rbp_sample / mz_rbp_reduce)
-// One workgroup per sample: the unroll's list of applications on that sample's
-// arena in HBM (conv tensors [channel][position], f = p + P·c, the Flux.flatten
-// order; dense vectors [feature]), the heads, then the list in reverse.  Convs
-// run as 16x16 f32 MFMA blocks (rows = output channels, columns = board
-// positions; the operand of a k×k conv is gathered through the kernel taps,
-// Flux's flipped cross-correlation, zero off the board); BatchNorm is the
-// test-mode affine γ·(t/√(1+ε)) + β; a block's second conv adds the saved
-// input before its relu.  Each sample accumulates its own parameter gradient
-// (the backward's dW, db, dβ, dγ) in gsam[b]; mz_rbp_reduce sums the samples
-// in ascending order (the data term; mz_adam_kernel adds 2θ).
+// ---- the corrected learner for the ResNet nets (mz_rbp_sample / mz_rbp_dw)
+// mz_rbp_sample, one workgroup per sample: the unroll's list of applications
+// on that sample's arena in HBM (conv tensors [channel][position], f = p + P·c,
+// the Flux.flatten order; dense vectors [feature]), the heads, then the list in
+// reverse for the input gradients.  Convs run as 16x16 f32 MFMA blocks (rows =
+// output channels, columns = board positions; the operand of a k×k conv is
+// gathered through the kernel taps, Flux's flipped cross-correlation, zero off
+// the board); BatchNorm is the test-mode affine γ·(t/√(1+ε)) + β; a block's
+// second conv adds the saved input before its relu.  The arenas keep every
+// application's output y, its pre-BatchNorm t and ∂L/∂y, so the parameter
+// gradients need no per-sample copy: mz_rbp_dw gives each 16x16 block of a
+// layer's dW (and each 16-channel block of db, dβ, dγ) one wave, which sums
+// over (sample, application of the layer, position) — the K dimension of its
+// MFMAs — with ∂L/∂t re-formed from the arenas as the operand is loaded.  The
+// result is the data term (mz_adam_kernel adds 2θ).
 enum { RBP_CONV = 0, RBP_DENSE = 1, RBP_CONCAT = 2 };
 
 struct RbpApp {
@@ -122,17 +126,25 @@ struct RbpParams {
     const RbpApp* apps; const BpHead* heads;
     float* act; float* grad;              // [B][arena] activations / their gradients
     // LDS: [dt_floats] the application's ∂L/∂t, then its input (the largest conv input)
-    float* gsam;                          // [B][nflat] per-sample parameter gradients
     const float* flat;
     const float* obs; const float* actions; const float* tv; const float* tr; const float* tp;
     const float* gscale; const float* weights;
     float* terms; float* pv; float* pp; float* pr;
 };
 
-struct RbpReduceParams {
-    int B, nflat, chunk;
-    const float* gsam; const float* flat;
+// One layer of the ResNet nets (conv or dense) and its applications in the unroll
+struct RbpLayer {
+    int conv;                   // 1 conv, 0 dense
+    int w_off, b_off, bn_off, cin, cout, kw, kh, act;
+    int use0, n_use;            // uses[use0 .. use0 + n_use)
+};
+struct RbpUse { int x, y, z; }; // arena offsets of one application: input, output, pre-BatchNorm t
+struct RbpJob { int layer, ob, kb; };   // a 16x16 block of dW; kb = -1: db (dβ, dγ) of channels ob·16 ..
+
+struct RbpDwParams {
+    int B, P, Wb, arena;
+    const RbpJob* jobs; const RbpLayer* layers; const RbpUse* uses;
+    const float* act; const float* grad; const float* flat;
     float* out;                           // Flux-order data term of the gradient (2θ: mz_adam_kernel)
-    double* sq;                           // [blocks]: Σθ² of each chunk (no chunk straddles two nets)
-    const int* chunk_start;               // [blocks + 1]
+    double* sq;                           // [jobs]: Σθ² of each job's parameter block (f64, fixed order)
 };

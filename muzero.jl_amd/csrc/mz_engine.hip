@@ -44,7 +44,7 @@ extern "C" __global__ void mz_bp_tile(BpParams Q);
 extern "C" __global__ void mz_bp_tile_lv(BpParams Q);
 extern "C" __global__ void mz_bp_dw(BpDwParams Q);
 extern "C" __global__ void mz_rbp_sample(RbpParams Q);
-extern "C" __global__ void mz_rbp_reduce(RbpReduceParams R);
+extern "C" __global__ void mz_rbp_dw(RbpDwParams Q);
 extern "C" __global__ void mz_bp_fold(BpFoldParams Q);
 extern "C" __global__ void mz_runroll_pred(RUnrollParams U);
 extern "C" __global__ void mz_runroll_pred_n(RUnrollParams U);
@@ -161,6 +161,7 @@ struct mz_handle {
     size_t rn_lds[3] = {0, 0, 0};
     float bn_s = 1.0f;
     int* d_rpath = nullptr; int* d_rgst = nullptr;          // ResNet search: [G][2(S+2)], [G][RG_INTS]
+    uint2* d_rcache = nullptr; int* d_rnN = nullptr;        // [G][S+1]: the LDS tree step's cached select
     float* d_rxpred = nullptr; float* d_rov = nullptr; float* d_rologit = nullptr; float* d_ror = nullptr;
     float* d_rhs = nullptr;                 // [bcap][K][H] learner unroll scratch (h between the nets)
     float* d_rts = nullptr;                 // [bcap][K][H] dynamics trunk outputs (the reward heads' input)
@@ -294,12 +295,14 @@ struct mz_handle {
     // corrected-gradient learner (mz_backprop.hip): the unrolled graph and its arenas
     int learn_mode = MZ_LEARN_REF_SEMANTICS;
     bool bp_built = false;
-    // the corrected learner for the ResNet nets (mz_rbp_sample / mz_rbp_reduce)
+    // the corrected learner for the ResNet nets (mz_rbp_sample / mz_rbp_dw)
     bool rbp_built = false;
-    int rbp_n_app = 0, rbp_n_head = 0, rbp_arena = 0, rbp_obs_t = 0, rbp_dt = 0, rbp_xs = 0, rbp_n_chunk = 0, rbp_cap = 0;
+    int rbp_n_app = 0, rbp_n_head = 0, rbp_arena = 0, rbp_obs_t = 0, rbp_dt = 0, rbp_xs = 0, rbp_n_job = 0, rbp_cap = 0;
+    int rbp_threads = 256;
     int rbp_job0[4] = {0, 0, 0, 0};
-    RbpApp* d_rbp_apps = nullptr; BpHead* d_rbp_heads = nullptr; int* d_rbp_chunks = nullptr;
-    float* d_rbp_act = nullptr; float* d_rbp_grad = nullptr; float* d_rbp_gsam = nullptr;
+    RbpApp* d_rbp_apps = nullptr; BpHead* d_rbp_heads = nullptr;
+    RbpLayer* d_rbp_layers = nullptr; RbpUse* d_rbp_uses = nullptr; RbpJob* d_rbp_jobs = nullptr;
+    float* d_rbp_act = nullptr; float* d_rbp_grad = nullptr;
     float* d_rbp_terms = nullptr; double* d_rbp_sq = nullptr;
     int bp_n_app = 0, bp_n_head = 0, bp_n_job = 0, bp_tile_floats = 0, bp_obs_t = 0, bp_tiles_cap = 0;
     BpApp* d_bp_apps = nullptr; BpHead* d_bp_heads = nullptr; BpLayer* d_bp_layers = nullptr;
@@ -1458,6 +1461,7 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
                        ? 0 : fail(h, "hipFuncSetAttribute(tree_lds)"));
         }
         CK(al(&h->d_rpath, G * 2 * (S + 2))); CK(al(&h->d_rgst, G * RG_INTS));
+        CK(al(&h->d_rcache, G * (S + 1))); CK(al(&h->d_rnN, G * (S + 1)));
         CK(al(&h->d_rxpred, G * H)); CK(al(&h->d_rov, G)); CK(al(&h->d_rologit, G * A)); CK(al(&h->d_ror, G));
         CK(al(&h->d_obs, G * h->obs_feat)); CK(al(&h->d_legal, G * A)); CK(al(&h->d_tp, G));
         CK(al(&h->d_cv, G * A)); CK(al(&h->d_rv, G)); CK(al(&h->d_act, G));
@@ -1750,8 +1754,9 @@ static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     P.exploration_eps = h->conf.exploration_eps;
     P.obs = obs; P.legal = legal_mask; P.to_play = to_play;
     P.child_visits = child_visits; P.root_value = root_value; P.action_out = action_out;
-    P.pbc_tab = h->d_pbc; P.sqrt_tab = h->d_sqrt; P.aval_tab = h->d_aval;
+    P.pbc_tab = h->d_pbc; P.sqrt_tab = h->d_sqrt; P.aval_tab = h->d_aval; P.pbterm = h->d_pbterm;
     P.tree = h->d_tree; P.tree_game_bytes = h->tree_game_bytes; P.hid = h->d_hid;
+    P.cache = h->d_rcache; P.nN = h->d_rnN;
     P.path = h->d_rpath; P.gst = h->d_rgst; P.x_pred = h->d_rxpred;
     P.o_v = h->d_rov; P.o_logit = h->d_rologit; P.o_r = h->d_ror;
     P.ng = h->rn_ng; P.bn_s = h->bn_s; P.plans = h->d_rplan; P.Wimg = h->d_Wp; P.flat = h->d_flat;
@@ -1787,7 +1792,7 @@ static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     MZ_TRY(h, hipLaunchKernel(kroot, dim3(tiles), dim3(RN_THREADS), args, rsearch_root_lds(h), st));
     for (int s = 0; s <= h->S; ++s) {
         P.s = s;
-        MZ_TRY(h, hipLaunchKernel(ktree, dim3(tgrid), dim3(tl ? 64 : 256), args, tl ? h->rtree_lds : 0, st));
+        MZ_TRY(h, hipLaunchKernel(ktree, dim3(tgrid), dim3(tl ? 64 * RT_WAVES : 256), args, tl ? h->rtree_lds : 0, st));
         if (s == h->S) break;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->time_nets) {
@@ -2371,15 +2376,21 @@ static int build_rbp(mz_handle* h) {
     const int K = h->conf.num_unroll_steps, P = h->plane, H = h->H;
     std::vector<RbpApp> apps;
     std::vector<BpHead> heads;
-    int off = 0, dtf = 0, xsf = 0;
+    int off = 0, dtf = 0, xsf = 0, max_units = 1;
     auto tensor = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
     const int obs_t = tensor(h->rin_feat);
     std::vector<RSpec> sp[3];
     size_t np[3];
     for (int n = 0; n < 3; ++n) sp[n] = rn_specs(h->rconf, h->rhp, n, &np[n]);
+    // one RbpLayer per spec (nets in order) and its applications
+    int lbase[3], nl = 0;
+    for (int n = 0; n < 3; ++n) { lbase[n] = nl; nl += (int)sp[n].size(); }
+    std::vector<std::vector<RbpUse>> luse(nl);
+    const int npb = (P + 15) / 16;
     auto chain = [&](int net, int ch, int x, bool first_obs) {
         int saved = -1;
-        for (const RSpec& r : sp[net]) {
+        for (size_t si = 0; si < sp[net].size(); ++si) {
+            const RSpec& r = sp[net][si];
             if (r.chain != ch) continue;
             RbpApp a{};
             a.op = r.conv ? RBP_CONV : RBP_DENSE;
@@ -2393,8 +2404,12 @@ static int build_rbp(mz_handle* h) {
             a.step = first_obs ? 1 : 0;
             first_obs = false;
             dtf = std::max(dtf, r.conv ? r.cout * P : r.cout);
-            if (r.conv) xsf = std::max(xsf, r.cin * P);
+            if (r.conv) {
+                xsf = std::max(xsf, r.cin * P);
+                max_units = std::max(max_units, std::max((r.cout + 15) / 16, (r.cin + 15) / 16) * npb);
+            }
             apps.push_back(a);
+            luse[lbase[net] + (int)si].push_back(RbpUse{a.x, a.y, a.z});
             x = a.y;
         }
         return x;
@@ -2415,23 +2430,50 @@ static int build_rbp(mz_handle* h) {
         heads.push_back(BpHead{BP_HEAD_V, chain(MZ_NET_PRED, 1, t, false), k});
         heads.push_back(BpHead{BP_HEAD_P, chain(MZ_NET_PRED, 2, t, false), k});
     }
-    // the reduction's chunks: 4096 parameters, none straddling two nets (Σθ² per net, mz_bp_fold)
-    std::vector<int> chunks;
+    // mz_rbp_dw's jobs, net by net (mz_bp_fold sums each net's Σθ² over its job range):
+    // per layer its W blocks, then its bias (BatchNorm) blocks; every parameter once
+    std::vector<RbpLayer> layers(nl);
+    std::vector<RbpUse> uses;
+    std::vector<RbpJob> jobs;
+    std::vector<char> covered(h->nflat, 0);
     for (int n = 0; n < 3; ++n) {
-        h->rbp_job0[n] = (int)chunks.size();
-        for (size_t i = 0; i < np[n]; i += 4096) chunks.push_back((int)(h->flat_off[n] + i));
+        h->rbp_job0[n] = (int)jobs.size();
+        for (size_t si = 0; si < sp[n].size(); ++si) {
+            const RSpec& r = sp[n][si];
+            const int li = lbase[n] + (int)si;
+            RbpLayer& L = layers[li];
+            L.conv = r.conv; L.w_off = (int)(h->flat_off[n] + r.woff); L.b_off = (int)(h->flat_off[n] + r.boff);
+            L.bn_off = r.conv && r.bn ? (int)(h->flat_off[n] + r.bnoff) : -1;
+            L.cin = r.cin; L.cout = r.cout; L.kw = r.kw; L.kh = r.kh; L.act = r.act;
+            L.use0 = (int)uses.size(); L.n_use = (int)luse[li].size();
+            for (const RbpUse& u : luse[li]) uses.push_back(u);
+            const int Kw = r.conv ? r.kw * r.kh * r.cin : r.cin;
+            for (int ob = 0; ob < (r.cout + 15) / 16; ++ob)
+                for (int kb = 0; kb < (Kw + 15) / 16; ++kb) jobs.push_back(RbpJob{li, ob, kb});
+            for (int ob = 0; ob < (r.cout + 15) / 16; ++ob) jobs.push_back(RbpJob{li, ob, -1});
+            const size_t nw = (size_t)Kw * r.cout, nb = (size_t)r.cout * (L.bn_off >= 0 ? 3 : 1);
+            for (size_t i = 0; i < nw; ++i) covered[(size_t)L.w_off + i] = 1;
+            for (int o = 0; o < r.cout; ++o) covered[(size_t)L.b_off + o] = 1;
+            if (L.bn_off >= 0) for (size_t i = 0; i < (size_t)2 * r.cout; ++i) covered[(size_t)L.bn_off + i] = 1;
+            (void)nb;
+        }
     }
-    h->rbp_job0[3] = (int)chunks.size();
-    chunks.push_back((int)h->nflat);
+    h->rbp_job0[3] = (int)jobs.size();
+    for (size_t i = 0; i < h->nflat; ++i)
+        if (!covered[i]) return fail(h, "corrected learner: a parameter no gradient job covers");
     auto up = [&](auto** d, const auto& v) -> int {
         MZ_TRY(h, dalloc(h, d, v.size()));
         MZ_TRY(h, hipMemcpy(*d, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice));
         return 0;
     };
-    if (up(&h->d_rbp_apps, apps) || up(&h->d_rbp_heads, heads) || up(&h->d_rbp_chunks, chunks)) return -1;
-    MZ_TRY(h, dalloc(h, &h->d_rbp_sq, chunks.size()));
-    h->rbp_n_app = (int)apps.size(); h->rbp_n_head = (int)heads.size(); h->rbp_n_chunk = (int)chunks.size() - 1;
+    if (up(&h->d_rbp_apps, apps) || up(&h->d_rbp_heads, heads) || up(&h->d_rbp_layers, layers) ||
+        up(&h->d_rbp_uses, uses) || up(&h->d_rbp_jobs, jobs))
+        return -1;
+    MZ_TRY(h, dalloc(h, &h->d_rbp_sq, jobs.size()));
+    h->rbp_n_app = (int)apps.size(); h->rbp_n_head = (int)heads.size(); h->rbp_n_job = (int)jobs.size();
     h->rbp_arena = off; h->rbp_obs_t = obs_t; h->rbp_dt = (dtf + 3) & ~3; h->rbp_xs = (xsf + 3) & ~3;
+    // a wave per 16x16 conv block of a pass (mz_rbp_sample), 4 to 12 waves
+    h->rbp_threads = 64 * std::min(12, std::max(4, max_units));
     const size_t lds = (size_t)(h->rbp_dt + h->rbp_xs) * 4;
     if (lds > kLdsMax) return fail(h, "corrected learner: a conv's tensors exceed the LDS");
     // above the 64 KB default (e.g. 256 filters on the 6x7 board: ~86 KB)
@@ -2447,25 +2489,28 @@ static int rbp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* los
     if (B > h->rbp_cap) {
         MZ_TRY(h, dalloc(h, &h->d_rbp_act, (size_t)B * h->rbp_arena));
         MZ_TRY(h, dalloc(h, &h->d_rbp_grad, (size_t)B * h->rbp_arena));
-        MZ_TRY(h, dalloc(h, &h->d_rbp_gsam, (size_t)B * h->nflat));
         MZ_TRY(h, dalloc(h, &h->d_rbp_terms, (size_t)B * (K + 1) * 3));
         h->rbp_cap = B;
     }
+    if ((size_t)B * (size_t)std::max(1, K + 1) * (size_t)h->plane >= (1u << 20))
+        return fail(h, "corrected learner: batch x unroll x board too large for the dW index");
     RbpParams Q;
     Q.B = B; Q.K = K; Q.A = h->A; Q.H = h->H; Q.P = h->plane; Q.Wb = h->rconf.observation_shape[0];
     Q.obs_feat = h->rin_feat; Q.arena = h->rbp_arena; Q.n_app = h->rbp_n_app; Q.n_head = h->rbp_n_head;
     Q.obs_t = h->rbp_obs_t; Q.intermediate_rewards = h->conf.intermediate_rewards; Q.nflat = (int)h->nflat;
     Q.dt_floats = h->rbp_dt;
     Q.apps = h->d_rbp_apps; Q.heads = h->d_rbp_heads;
-    Q.act = h->d_rbp_act; Q.grad = h->d_rbp_grad; Q.gsam = h->d_rbp_gsam; Q.flat = h->d_flat;
+    Q.act = h->d_rbp_act; Q.grad = h->d_rbp_grad; Q.flat = h->d_flat;
     Q.obs = b->observation; Q.actions = b->actions; Q.tv = b->target_values; Q.tr = b->target_rewards;
     Q.tp = b->target_policies; Q.gscale = b->gradient_scale; Q.weights = b->weights; Q.terms = h->d_rbp_terms;
     Q.pv = h->d_pv; Q.pp = h->d_pp; Q.pr = h->d_pr;
-    hipLaunchKernelGGL(mz_rbp_sample, dim3(B), dim3(256), (size_t)(h->rbp_dt + h->rbp_xs) * 4, st, Q);
-    RbpReduceParams R;
-    R.B = B; R.nflat = (int)h->nflat; R.chunk = 4096; R.gsam = h->d_rbp_gsam; R.flat = h->d_flat;
-    R.out = grad_dev ? grad_dev : h->d_grad; R.sq = h->d_rbp_sq; R.chunk_start = h->d_rbp_chunks;
-    hipLaunchKernelGGL(mz_rbp_reduce, dim3(h->rbp_n_chunk), dim3(256), 0, st, R);
+    hipLaunchKernelGGL(mz_rbp_sample, dim3(B), dim3(h->rbp_threads), (size_t)(h->rbp_dt + h->rbp_xs) * 4, st, Q);
+    RbpDwParams D;
+    D.B = B; D.P = h->plane; D.Wb = h->rconf.observation_shape[0]; D.arena = h->rbp_arena;
+    D.jobs = h->d_rbp_jobs; D.layers = h->d_rbp_layers; D.uses = h->d_rbp_uses;
+    D.act = h->d_rbp_act; D.grad = h->d_rbp_grad; D.flat = h->d_flat;
+    D.out = grad_dev ? grad_dev : h->d_grad; D.sq = h->d_rbp_sq;
+    hipLaunchKernelGGL(mz_rbp_dw, dim3(h->rbp_n_job), dim3(64), 0, st, D);
     BpFoldParams F;
     F.B = B; F.K = K; F.terms = h->d_rbp_terms; F.gscale = b->gradient_scale; F.weights = b->weights;
     F.flat = h->d_flat; F.netoff = h->d_netoff; F.losses = losses_dev ? losses_dev : h->d_loss;
@@ -2473,7 +2518,7 @@ static int rbp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* los
     for (int n = 0; n < 4; ++n) F.job0[n] = h->rbp_job0[n];
     hipLaunchKernelGGL(mz_bp_fold, dim3(4), dim3(256), 0, st, F);
     MZ_TRY(h, hipGetLastError());
-    h->last_lvariant = "mz_rbp_sample+mz_rbp_reduce";
+    h->last_lvariant = "mz_rbp_sample+mz_rbp_dw";
     return 0;
 }
 

@@ -1006,12 +1006,22 @@ __device__ __forceinline__ void glds_copy(const void* src, void* dst, int n, int
 #else
 #define RT_STAMP(k) do {} while (0)
 #endif
+// RT_WAVES (mz_resnet_params.h) waves per workgroup: wave 0 walks the trees
+// (expand, backup, select, the search statistics); every wave shares the
+// copies in, the cached select's recompute rows and the hidden-state gather.
+// The LDS trees already hold a CU alone, so the other waves cost no occupancy.
 template <int GW>
 __device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    // per game of the workgroup: rows to recompute, moved, depth, the select's
+    // start level (atomicMin over the rows), the tag, the selected leaf's parent
+    __shared__ int sh_rows[4], sh_moved[4], sh_depth[4], sh_skip[4], sh_leaf[4];
+    __shared__ uint32_t sh_ver[4];
+    __shared__ float sh_mm[4][2];                   // min / max after the backup
     RT_STAMP(0);
     constexpr int NGW = 64 / GW;
-    const int gl = threadIdx.x / GW, a = threadIdx.x % GW, lane = threadIdx.x & 63;
+    const int tid = threadIdx.x, wave = tid >> 6, nwv = blockDim.x >> 6;
+    const int lane = tid & 63, gl = lane / GW, a = lane % GW;
     const int gg = blockIdx.x * NGW + gl;
     const int A = P.A, H = P.H, S = P.S, PS = 2 * (S + 2), s = P.s;
     const int E = (S + 1) * A, NN = S + 1;
@@ -1025,120 +1035,222 @@ __device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
     int* st = P.gst + (size_t)gc * RG_INTS;
     const int4 st0 = reinterpret_cast<const int4*>(st)[0], st1 = reinterpret_cast<const int4*>(st)[1];
     const int4 st2 = reinterpret_cast<const int4*>(st)[2];
-    const float logit = s > 0 && a < A ? P.o_logit[(size_t)gc * A + a] : 0.0f;
-    const float o_r = s > 0 ? P.o_r[gc] : 0.0f, o_v = s > 0 ? P.o_v[gc] : 0.0f;
-    // LDS-DMA: tables, then per game the existing nodes 0..n_old-1 and the path
+    const float logit = wave == 0 && s > 0 && a < A ? P.o_logit[(size_t)gc * A + a] : 0.0f;
+    const float o_r = wave == 0 && s > 0 ? P.o_r[gc] : 0.0f, o_v = wave == 0 && s > 0 ? P.o_v[gc] : 0.0f;
+    // LDS-DMA, the arrays dealt round the waves: tables, then per game the
+    // existing nodes 0..n_old-1, the path, the cache entries and N per node
     const int n_old = s > 0 ? s : 1;
-    glds_copy<4>(P.pbc_tab, pbc, 2 * (S + 2), lane);
-    glds_copy<4>(P.sqrt_tab, sqt, 2 * (S + 2), lane);
-    for (int g = 0; g < NGW; ++g) {
-        const int gq = blockIdx.x * NGW + g;
-        if (gq >= P.G) break;
-        const char* src = P.tree + (size_t)gq * P.tree_game_bytes;
-        char* dst = lb + L.tables + g * L.game;
-        glds_copy<16>(src, dst, n_old * A, lane);                                    // edge records
-        glds_copy<4>(src + 16 * (size_t)E, dst + 16 * (size_t)E, n_old, lane);        // nr
-        glds_copy<4>(src + 16 * (size_t)E + 4 * (size_t)NN, dst + 16 * (size_t)E + 4 * (size_t)NN,
-                     (n_old + 3) / 4, lane);                                           // ntp (bytes, as dwords)
-        glds_copy<4>(P.path + (size_t)gq * PS, dst + L.path, PS, lane);
+    {
+        int k = 0;
+        auto job = [&](auto fn) { if (k++ % nwv == wave) fn(); };
+        job([&] { glds_copy<4>(P.pbc_tab, pbc, 2 * (S + 2), lane); });
+        job([&] { glds_copy<4>(P.sqrt_tab, sqt, 2 * (S + 2), lane); });
+        for (int g = 0; g < NGW; ++g) {
+            const int gq = blockIdx.x * NGW + g;
+            if (gq >= P.G) break;
+            const char* src = P.tree + (size_t)gq * P.tree_game_bytes;
+            char* dst = lb + L.tables + g * L.game;
+            // the edge records in up to nwv pieces of whole 64-record instructions
+            const int ne = n_old * A, per = ((ne + nwv * 64 - 1) / (nwv * 64)) * 64;
+            for (int c0 = 0; c0 < ne; c0 += per)
+                job([&] { glds_copy<16>(src + 16 * (size_t)c0, dst + 16 * (size_t)c0, ne - c0 < per ? ne - c0 : per, lane); });
+            job([&] { glds_copy<4>(src + 16 * (size_t)E, dst + 16 * (size_t)E, n_old, lane); });          // nr
+            job([&] { glds_copy<4>(src + 16 * (size_t)E + 4 * (size_t)NN, dst + 16 * (size_t)E + 4 * (size_t)NN,
+                                   (n_old + 3) / 4, lane); });                                        // ntp (as dwords)
+            job([&] { glds_copy<4>(P.path + (size_t)gq * PS, dst + L.path, PS, lane); });
+            if (s > 0) {
+                job([&] { glds_copy<4>(P.cache + (size_t)gq * NN, dst + L.cache, 2 * n_old, lane); });
+                job([&] { glds_copy<4>(P.nN + (size_t)gq * NN, dst + L.nn, n_old, lane); });
+            }
+        }
     }
     RT_STAMP(1);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     RT_STAMP(2);
-    if (!live) return;                              // whole GW-lane groups leave together
     char* gb = lb + L.tables + gl * L.game;
     TreeView tree = tree_view(gb, E, NN);
-    TreeView gt = rs_tree(P, gg);
     int* path = reinterpret_cast<int*>(gb + L.path);
-    float* stg = reinterpret_cast<float*>(gb + L.stg);
+    uint2* cache = reinterpret_cast<uint2*>(gb + L.cache);
+    uint2* lvl = reinterpret_cast<uint2*>(gb + L.lvl);
+    int* nn = reinterpret_cast<int*>(gb + L.nn);
+    uint2* cache_g = P.cache + (size_t)gc * NN;
     const uint32_t legal = (uint32_t)st0.x;
     const int root_tp = st0.y;
     const uint32_t gid = P.game_offset + (uint32_t)gg;
     int rN = st0.z;
     float rW = __int_as_float(st0.w), mmin = __int_as_float(st1.x), mmax = __int_as_float(st1.y);
-    if (s > 0) {
-        const int e_new = s;                        // the node simulation s-1 expanded (:280)
-        const float prior = double_softmax_prior<GW>(logit, a, A, legal, stg);
-        init_edges(tree, e_new, a, A, prior);
-        const int tl = st2.x, depth = st2.y;
+    // ---- wave 0: expand + backup of simulation s-1 (:280-281)
+    if (wave == 0 && live) {
+        TreeView gt = rs_tree(P, gg);
+        float* stg = reinterpret_cast<float*>(gb + L.stg);
+        uint32_t ver = s > 0 ? (uint32_t)st2.z : 1u;    // the cached select's tag (RG_VER)
+        int rows = 0, moved = 0, depth = 0;
+        if (s == 0) {                                   // a new search: no entry is current
+            if (a == 0) { cache[0] = make_uint2(0u, 0u); st[RG_VER] = 1; }
+        } else {
+            const int e_new = s;                        // the node simulation s-1 expanded (:280)
+            const float prior = double_softmax_prior<GW>(logit, a, A, legal, stg);
+            init_edges(tree, e_new, a, A, prior);
+            const int tl = st2.x;
+            depth = st2.y;
+            if (a == 0) {
+                const int li = st1.z * A + st1.w;
+                tree.nc(li) = (tree.nc(li) & 0xffffu) | ((uint32_t)(e_new + 1) << 16);
+                tree.nr[e_new] = o_r;
+                tree.ntp[e_new] = (int8_t)tl;
+                path[2 * depth + 1] = e_new;
+                P.path[(size_t)gg * PS + 2 * depth + 1] = e_new;   // (a skip-ahead may keep this level)
+                gt.nr[e_new] = o_r;
+                gt.ntp[e_new] = (int8_t)tl;
+            }
+            __threadfence_block();
+            __builtin_amdgcn_wave_barrier();
+            RT_STAMP(3);
+            const uint32_t omin = __float_as_uint(mmin), omax = __float_as_uint(mmax);
+            if (P.players == 1)
+                backup_path_1p<GW>(tree, path, depth, o_v, P.discount, rN, rW, mmin, mmax, a,
+                                   reinterpret_cast<float*>(gb + L.rr), reinterpret_cast<float*>(gb + L.vin), lvl, nn);
+            else
+                backup_path<GW>(tree, path, depth, o_v, tl, A, P.players, P.discount, rN, rW, root_tp, mmin, mmax,
+                                a, lvl, nn);                                    // :281
+            // the min / max moved: every entry is stale (the tag is bumped) and
+            // every expanded node is recomputed; else the path's nodes
+            moved = __float_as_uint(mmin) != omin || __float_as_uint(mmax) != omax;
+            ver += moved ? 1u : 0u;
+            rows = s < S ? (moved ? e_new + 1 : depth + 1) : 0;
+            // write-back: the new node's edges, the path edges, N per path node
+            if (a < A) gt.e[e_new * A + a] = tree.e[e_new * A + a];
+            for (int d = 1 + a; d <= depth; d += GW) {
+                const int i = path[2 * d];
+                gt.e[i] = tree.e[i];
+            }
+            for (int d = a; d <= depth; d += GW) {
+                const uint2 l = lvl[d];
+                P.nN[(size_t)gg * NN + l.x] = (int)l.y;
+            }
+            if (a == 0) {
+                st[RG_ROOTN] = rN; st[RG_ROOTW] = __float_as_int(rW);
+                st[RG_MMIN] = __float_as_int(mmin); st[RG_MMAX] = __float_as_int(mmax);
+                st[RG_VER] = (int)ver;
+            }
+            RT_STAMP(4);
+        }
         if (a == 0) {
-            const int li = st1.z * A + st1.w;
-            tree.nc(li) = (tree.nc(li) & 0xffffu) | ((uint32_t)(e_new + 1) << 16);
-            tree.nr[e_new] = o_r;
-            tree.ntp[e_new] = (int8_t)tl;
-            path[2 * depth + 1] = e_new;
-            gt.nr[e_new] = o_r;
-            gt.ntp[e_new] = (int8_t)tl;
+            sh_rows[gl] = rows; sh_moved[gl] = moved; sh_depth[gl] = depth; sh_ver[gl] = ver;
+            sh_mm[gl][0] = mmin; sh_mm[gl][1] = mmax;
+            sh_skip[gl] = moved ? 0 : depth;            // the leaf's level always counts
         }
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
-        RT_STAMP(3);
-        if (P.players == 1)
-            backup_path_1p<GW>(tree, path, depth, o_v, P.discount, rN, rW, mmin, mmax, a,
-                               reinterpret_cast<float*>(gb + L.rr), reinterpret_cast<float*>(gb + L.vin));
-        else
-            backup_path<GW>(tree, path, depth, o_v, tl, A, P.players, P.discount, rN, rW, root_tp, mmin, mmax,
-                            a);                                                 // :281
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
-        RT_STAMP(4);
-        // write-back: the new node's edges, then the path edges (the leaf edge last level)
-        if (a < A) gt.e[e_new * A + a] = tree.e[e_new * A + a];
-        for (int d = 1 + a; d <= depth; d += GW) {
-            const int i = path[2 * d];
-            gt.e[i] = tree.e[i];
-        }
-        if (a == 0) {
-            st[RG_ROOTN] = rN; st[RG_ROOTW] = __float_as_int(rW);
-            st[RG_MMIN] = __float_as_int(mmin); st[RG_MMAX] = __float_as_int(mmax);
-        }
-        RT_STAMP(5);
     }
-    if (s < S) {
-        const SelectOut so = select_path<false, GW>(tree, P.path + (size_t)gg * PS, rN, root_tp, legal, mmin, mmax,
-                                                    a, lane, A, P.players, P.discount, nullptr, pbc, sqt, P.seed,
-                                                    gid, P.rng_step, s);                   // :256-268
-        RT_STAMP(6);
-        if (a == 0) {
-            st[RG_LEAF_E] = so.leaf_e; st[RG_LEAF_A] = so.leaf_a; st[RG_VTP] = so.vtp; st[RG_DEPTH] = so.depth;
+    __syncthreads();
+    // ---- every wave: the cached select's entries (mz_tree_device.h
+    // select_path_cached) of the nodes whose argmax this backup can have
+    // changed — the path's, or every expanded node's when min / max moved —
+    // U rows per group and pass, rows dealt round the waves; the entries go to
+    // LDS and to their HBM home.  A path row whose choice leaves the last path
+    // (or ties) bounds the next walk's start: the levels above it are retraced.
+    const int rows = live ? sh_rows[gl] : 0;
+    if (rows > 0) {
+        const bool moved = sh_moved[gl] != 0;
+        const int depth = sh_depth[gl];
+        const uint32_t ver = sh_ver[gl];
+        const float mn = sh_mm[gl][0], mx = sh_mm[gl][1];
+        const bool lg = a < A && ((legal >> a) & 1u);
+        constexpr int U = 4;
+        int Dl = depth;
+        for (int j0 = wave * U; j0 < rows; j0 += nwv * U) {
+            int slot[U], Np[U], ch[U];
+            bool act[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int j = j0 + u;
+                act[u] = j < rows;
+                const int jc = act[u] ? j : 0;
+                if (moved) { slot[u] = jc; Np[u] = nn[jc]; }
+                else { const uint2 l = lvl[jc]; slot[u] = (int)l.x; Np[u] = (int)l.y; }
+            }
+            // the pUCT prior factor from the pb_term triangle in global memory
+            // (L2-resident; its loads overlap across the rows) instead of an f64
+            // division per child
+            cache_rows<GW, true, U>(tree, cache, ver, slot, Np, act, lg, a, A, mn, mx, P.pbterm, lane, nullptr,
+                                    nullptr, cache_g, ch);
+            if (!moved) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int j = j0 + u;
+                    if (j < depth && ch[u] != path[2 * (j + 1)] - slot[u] * A) Dl = Dl < j ? Dl : j;
+                }
+            }
         }
-        // parent h -> prediction input; h *= 2 in place (Q1), read by the dynamics launch.
-        // 16-byte pieces, RT_GU per lane loaded before any is stored (the stores
-        // could alias the loads, so a one-at-a-time loop waits a full memory
-        // round trip per piece)
-        float* hp = P.hid + ((size_t)gg * (S + 1) + so.leaf_e) * H;
-        float* xp = P.x_pred + (size_t)gg * H;
+        if (!moved && a == 0 && Dl < depth) atomicMin(sh_skip + gl, Dl);
+    }
+    __syncthreads();
+    RT_STAMP(5);
+#ifdef MZ_STAMPS
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (P.s & 3) == 0) {
+        P.stamps[1024 + (P.s >> 2) * 16 + 10] = sh_moved[0];
+        P.stamps[1024 + (P.s >> 2) * 16 + 11] = (unsigned long long)sh_depth[0];
+        P.stamps[1024 + (P.s >> 2) * 16 + 12] = (unsigned long long)sh_skip[0];
+    }
+#endif
+    RT_STAMP(6);
+    if (s < S) {
+        // ---- wave 0: select (:256-268), the walk from level D: its node and
+        // the nc word of the edge into it from this game's path (levels 0..D of
+        // the HBM path stay as they are)
+        if (wave == 0 && live) {
+            const int D = sh_skip[gl];
+            const int e0 = D > 0 ? path[2 * D + 1] : 0;
+            const uint32_t npc0 = D > 0 ? tree.nc(path[2 * D]) : 0u;
+            const SelectOut so = select_path_cached<GW, false>(tree, cache, sh_ver[gl], P.path + (size_t)gg * PS, rN,
+                                                               root_tp, legal, mmin, mmax, a, lane, A, P.players,
+                                                               nullptr, P.seed, gid, P.rng_step, s, pbc, sqt, D, e0,
+                                                               npc0);
+            if (a == 0) {
+                st[RG_LEAF_E] = so.leaf_e; st[RG_LEAF_A] = so.leaf_a; st[RG_VTP] = so.vtp; st[RG_DEPTH] = so.depth;
+                sh_leaf[gl] = so.leaf_e;
+            }
+        }
+        __syncthreads();
+        RT_STAMP(7);
+        // ---- every wave: parent h -> prediction input; h *= 2 in place (Q1),
+        // read by the dynamics launch.  16-byte pieces, RT_GU per thread loaded
+        // before any is stored (the stores could alias the loads, so a
+        // one-at-a-time loop waits a full memory round trip per piece)
         if ((H & 3) == 0) {
-            constexpr int RT_GU = 8;
-            float4* hp4 = reinterpret_cast<float4*>(hp);
-            float4* xp4 = reinterpret_cast<float4*>(xp);
-            const int H4 = H >> 2;
-            for (int k0 = 0; k0 < H4; k0 += RT_GU * GW) {
+            constexpr int RT_GU = 4;
+            const int H4 = H >> 2, n4 = NGW * H4, nt = blockDim.x;
+            for (int i0 = tid; i0 < n4; i0 += RT_GU * nt) {
                 float4 v[RT_GU];
 #pragma unroll
                 for (int u = 0; u < RT_GU; ++u) {
-                    const int k = k0 + u * GW + a;
-                    if (k < H4) v[u] = hp4[k];
+                    const int i = i0 + u * nt, g = i / H4, k = i - g * H4;
+                    const int gq = blockIdx.x * NGW + g;
+                    if (i < n4 && gq < P.G)
+                        v[u] = reinterpret_cast<const float4*>(P.hid + ((size_t)gq * (S + 1) + sh_leaf[g]) * H)[k];
                 }
 #pragma unroll
                 for (int u = 0; u < RT_GU; ++u) {
-                    const int k = k0 + u * GW + a;
-                    if (k < H4) {
-                        xp4[k] = v[u];
-                        hp4[k] = make_float4(v[u].x * 2.0f, v[u].y * 2.0f, v[u].z * 2.0f, v[u].w * 2.0f);
+                    const int i = i0 + u * nt, g = i / H4, k = i - g * H4;
+                    const int gq = blockIdx.x * NGW + g;
+                    if (i < n4 && gq < P.G) {
+                        reinterpret_cast<float4*>(P.x_pred + (size_t)gq * H)[k] = v[u];
+                        reinterpret_cast<float4*>(P.hid + ((size_t)gq * (S + 1) + sh_leaf[g]) * H)[k] =
+                            make_float4(v[u].x * 2.0f, v[u].y * 2.0f, v[u].z * 2.0f, v[u].w * 2.0f);
                     }
                 }
             }
-        } else {
+        } else if (wave == 0 && live) {
+            float* hp = P.hid + ((size_t)gg * (S + 1) + sh_leaf[gl]) * H;
+            float* xp = P.x_pred + (size_t)gg * H;
             for (int k = a; k < H; k += GW) {
                 const float hv = hp[k];
                 xp[k] = hv;
                 hp[k] = hv * 2.0f;
             }
         }
-        RT_STAMP(7);
-    } else {                                        // store_search_stats! (:115-122) + select_action (:293-306)
+        RT_STAMP(8);
+    } else if (wave == 0 && live) {                 // store_search_stats! (:115-122) + select_action (:293-306)
         const bool lg = a < A && ((legal >> a) & 1u);
         const int Nc = lg ? (int)(tree.nc(a) & 0xffffu) : 0;
         const int sum = gisum<GW>(Nc);
@@ -1151,10 +1263,10 @@ __device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
         }
     }
 }
-extern "C" __global__ __launch_bounds__(64) void mz_rsearch_tree_lds(RSearchParams P) {
+extern "C" __global__ __launch_bounds__(64 * RT_WAVES) void mz_rsearch_tree_lds(RSearchParams P) {
     rsearch_tree_lds_body<16>(P);
 }
-extern "C" __global__ __launch_bounds__(64) void mz_rsearch_tree_lds32(RSearchParams P) {
+extern "C" __global__ __launch_bounds__(64 * RT_WAVES) void mz_rsearch_tree_lds32(RSearchParams P) {
     rsearch_tree_lds_body<32>(P);
 }
 

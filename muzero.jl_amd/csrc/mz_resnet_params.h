@@ -121,6 +121,7 @@ struct RNetParams {
 // and one network launch (prediction ‖ dynamics).  Per-game state gst[g][16]:
 // legal, root_tp, rootN, rootW, mmin, mmax, leaf_e, leaf_a, vtp, depth.
 enum { RG_LEGAL = 0, RG_ROOT_TP, RG_ROOTN, RG_ROOTW, RG_MMIN, RG_MMAX, RG_LEAF_E, RG_LEAF_A, RG_VTP, RG_DEPTH,
+       RG_VER,                          // the LDS tree step's cached-select tag (mz_tree_device.h select_path_cached)
        RG_INTS = 16 };
 
 struct RSearchParams {
@@ -132,8 +133,11 @@ struct RSearchParams {
     const float* obs; const uint8_t* legal; const int32_t* to_play;
     float* child_visits; float* root_value; int32_t* action_out;
     const double* pbc_tab; const double* sqrt_tab; const float* aval_tab;
+    const double* pbterm;  // the pb_term triangle (mz_tree_device.h pbterm_index), the recompute's table
     char* tree; size_t tree_game_bytes;
     float* hid;            // [G][S+1][H]
+    uint2* cache;          // [G][S+1] the LDS tree step's cached select entries, home between launches
+    int* nN;               // [G][S+1] N of each expanded node (the edge into it; the root's N), for recomputes
     int* path;             // [G][2(S+2)]
     int* gst;              // [G][RG_INTS]
     float* x_pred;         // [G][H] prediction input of this simulation
@@ -159,7 +163,10 @@ struct RSearchParams {
 // Per game: the tree copy (tree_game_bytes, +16 for the dword copy of the
 // to_play bytes), the path [2(S+2)] ints, rr / vin [S+2] floats (1-player
 // backup), the GW-float softmax staging slot.
-struct RsTreeLds { int tables, game, tree, path, rr, vin, stg, total; };
+#ifndef RT_WAVES
+#define RT_WAVES 8                     // waves of the LDS-cached tree step (mz_rsearch_tree_lds*)
+#endif
+struct RsTreeLds { int tables, game, tree, path, rr, vin, stg, cache, lvl, nn, total; };
 __host__ __device__ __forceinline__ int rs_align16(size_t x) { return (int)((x + 15) & ~(size_t)15); }
 __host__ __device__ __forceinline__ RsTreeLds rs_tree_lds(int S, size_t tree_game_bytes, int GW) {
     RsTreeLds L;
@@ -169,7 +176,10 @@ __host__ __device__ __forceinline__ RsTreeLds rs_tree_lds(int S, size_t tree_gam
     L.rr = L.path + rs_align16((size_t)8 * (S + 2));
     L.vin = L.rr + rs_align16((size_t)4 * (S + 2));
     L.stg = L.vin + rs_align16((size_t)4 * (S + 2));
-    L.game = L.stg + rs_align16((size_t)4 * GW);
+    L.cache = L.stg + rs_align16((size_t)4 * GW);           // uint2 [S+1] entries
+    L.lvl = L.cache + rs_align16((size_t)8 * (S + 1));      // uint2 [S+2] (slot, N) per path level (backup)
+    L.nn = L.lvl + rs_align16((size_t)8 * (S + 2));         // int [S+1] N per expanded node
+    L.game = L.nn + rs_align16((size_t)4 * (S + 1));
     L.total = L.tables + (64 / GW) * L.game;
     return L;
 }

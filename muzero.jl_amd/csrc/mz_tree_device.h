@@ -484,7 +484,8 @@ template <int GW, bool TAB, int U>
 __device__ __forceinline__ void cache_rows(const TreeView& t, uint2* cache, uint32_t tag, const int (&slot)[U],
                                            const int (&Np)[U], const bool (&act)[U], bool lg, int a, int A,
                                            float mmin, float mmax, const double* pbterm, int lane,
-                                           const double* pbc_tab, const double* sqrt_tab, uint2* cache_g) {
+                                           const double* pbc_tab, const double* sqrt_tab, uint2* cache_g,
+                                           int* ch_out = nullptr) {
     const int ac = a < A ? a : A - 1;
     float4 ed[U];
 #pragma unroll
@@ -501,6 +502,7 @@ __device__ __forceinline__ void cache_rows(const TreeView& t, uint2* cache, uint
     for (int u = 0; u < U; ++u) {
         const uint32_t msk = grp_mask<GW>(__builtin_amdgcn_ballot_w64(lg && sc[u] == m[u]), lane);
         const int ach = (int)__builtin_ctzll((uint64_t)msk | (1ull << GW));
+        if (ch_out) ch_out[u] = (msk & (msk - 1)) != 0 ? -1 : ach;   // the entry's child (-1: a tie)
         if (act[u] && a == ach) {
             const bool tie = (msk & (msk - 1)) != 0;
             const uint2 v = tie ? make_uint2(0u, 0u)

@@ -5,7 +5,6 @@ configs[4] (GAME=atari, default) or TicTacToe ResNet (GAME=ttt)."""
 import ctypes
 import dataclasses
 import os
-import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -17,14 +16,13 @@ pkg = _mzpkg.load()
 from muzero_jl_amd import abi, build as mzbuild  # noqa: E402
 from muzero_jl_amd.networks import init_nets  # noqa: E402
 
-PH = ["copy issue", "copy wait", "expand", "backup", "write-back", "select", "gather"]
+PH = ["copy issue", "copy wait", "expand", "backup", "recompute", "write-back", "select", "gather"]
 
 
 def main():
     lib = os.path.join(pkg.PKG_DIR, "lib", "libmz_stamps.so")
-    srcs = [os.path.join(pkg.PKG_DIR, "csrc", s) for s in mzbuild.SOURCES]
     if "--no-build" not in sys.argv:
-        subprocess.run(["/opt/rocm/bin/hipcc"] + mzbuild.FLAGS + ["-DMZ_STAMPS", "-o", lib] + srcs, check=True)
+        mzbuild.build(out=lib, objdir=os.path.join(pkg.PKG_DIR, "lib", "obj_stamps"), extra=["-DMZ_STAMPS"])
     abi._lib = None
     L = abi.load_library(lib)
     L.mz_debug_stamps.restype = ctypes.c_int
@@ -55,13 +53,13 @@ def main():
         if not r[0]:
             continue
         prev, cells = r[0], []
-        for k in range(1, 8):
+        for k in range(1, 9):
             if r[k]:
                 cells.append(f"{r[k] - prev:11d}")
                 prev = r[k]
             else:
                 cells.append(f"{'-':>11s}")
-        print(f"{4 * i:4d}  " + " ".join(cells) + f" {prev - r[0]:11d}")
+        print(f"{4 * i:4d}  " + " ".join(cells) + f" {prev - r[0]:11d}  moved {r[10]} depth {r[11]} D {r[12]}")
     eng.close()
 
 
