@@ -2065,8 +2065,13 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
         MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_kernel, dim3((B + U.ng - 1) / U.ng), dim3(RN_THREADS),
                                   args, runroll_lds(h), st));
     } else {                                        // chain on narrow tiles, then the B·K predictions
-        // tiles of one column block: the 1-block instances (a fifth of the code)
-        const bool nb1 = (U.P * U.ng_l + 15) / 16 == 1;
+        // units of one column block (the 1-block instances, a fifth of the code),
+        // also for wider tiles: a Connect4 1x1 conv of 4 row blocks x 3 column
+        // blocks then has 12 units for the 8 waves instead of 4 three-block ones
+        // (the same tiles, bit for bit; configs[3] learner 1.62 k -> 1.75 k
+        // steps/s, tools/gpu_r04d.sh).  MZ_RN_CHAIN_NB3=1: the three-block units
+        static const bool nb3 = std::getenv("MZ_RN_CHAIN_NB3") != nullptr;
+        const bool nb1 = (U.P * U.ng_l + 15) / 16 == 1 || !nb3;
         U.rd_ep_off = (int)(h->rn_lds_l / 4);
         U.rd_trunk_nl = 1 + 2 * h->rhp.num_blocks;
         h->last_lvariant = std::string(h->rd_chain ? (h->rd_nb == 3 ? "mz_runroll_chain_r3" : "mz_runroll_chain_r")

@@ -555,12 +555,12 @@ __device__ __forceinline__ void rn_layer(const RLayer& L, const float* __restric
 }
 
 // This wave's first-unit operands of layer L (no-op for a wave without one)
-template <bool NARROW>
+template <bool NARROW, int NBWMAX = 3>
 __device__ __forceinline__ void rn_prefetch(const RLayer& L, const float* __restrict__ Wimg,
                                             const float* __restrict__ flat, int NG, int P, RnPf& pf) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ncols = L.spatial ? P * NG : NG;
-    const int nbw = rn_nbw<NARROW>(L, NG, P);
+    const int nbw = NBWMAX == 1 ? 1 : rn_nbw<NARROW>(L, NG, P);      // (rn_layer's unit width)
     const int n_grp = (((ncols + 15) >> 4) + nbw - 1) / nbw;
     if (wave < L.n_ob * n_grp) {
         const int ob = wave / n_grp;
@@ -606,7 +606,7 @@ __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const 
         if (i0 >= i1) return;
         RnPf pf;
         RLayer L = rn_layer_at(R, i0);
-        rn_prefetch<NARROW>(L, Wimg, flat, NG, P, pf);
+        rn_prefetch<NARROW, NBWMAX>(L, Wimg, flat, NG, P, pf);
         for (int i = i0; i < i1; ++i) {
             RLayer Ln;
             if (i + 1 < i1) Ln = rn_layer_at(R, i + 1);
@@ -615,7 +615,7 @@ __device__ __forceinline__ void rn_run(const RPlan& R, const float* Wimg, const 
             if (st && i - i0 < 31) dbg = st + 1024 + 8 * (i - i0);
 #endif
             rn_layer<NARROW, true, NBWMAX, PIPE, NOKK, RAWTANH>(L, Wimg, flat, lds, NG, Wb, P, bn_s, bn_r, &pf, dbg);
-            if (i + 1 < i1) rn_prefetch<NARROW>(Ln, Wimg, flat, NG, P, pf);
+            if (i + 1 < i1) rn_prefetch<NARROW, NBWMAX>(Ln, Wimg, flat, NG, P, pf);
 #ifdef MZ_STAMPS
             if (st && (threadIdx.x & 63) == 0 && i - i0 < 31) st[wv * 64 + 2 * (i - i0)] = __builtin_amdgcn_s_memtime();
 #endif

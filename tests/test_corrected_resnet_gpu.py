@@ -1,5 +1,5 @@
 """The corrected-gradient learner on the ResNet nets (MZ_LEARN_CORRECTED;
-mz_backprop.hip mz_rbp_sample / mz_rbp_reduce: backpropagation through
+mz_backprop.hip mz_rbp_sample / mz_rbp_dw: backpropagation through
 convolutions, test-mode BatchNorm, residual blocks and the Dense heads of the
 K-step unroll on f32 MFMA) against the independent torch autograd reference
 (tests/torch_learner_ref.py, float64) at the 1e-5 tolerance of north_star:
