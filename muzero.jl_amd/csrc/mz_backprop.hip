@@ -102,7 +102,7 @@ __device__ __forceinline__ void bp_dense_dx(const BpApp& P, const float* __restr
 }
 
 // Tile arenas, loss terms and reward read-outs zeroed, the observation staged
-__device__ __forceinline__ void bp_prologue(const BpParams& Q, float* T, float* G) {
+__device__ __forceinline__ void bp_prologue(const BpParams& Q, float* T, float* G, float* C = nullptr) {
     const int tid = threadIdx.x, nt = blockDim.x, t0 = blockIdx.x * 16, K1 = Q.K + 1;
     for (int e = tid; e < Q.tile_floats; e += nt) G[e] = 0.0f;
     for (int e = tid; e < 16 * K1 * 3; e += nt) {
@@ -115,7 +115,9 @@ __device__ __forceinline__ void bp_prologue(const BpParams& Q, float* T, float* 
     }
     for (int e = tid; e < Q.obs_feat * 16; e += nt) {        // observation_batch (:347)
         const int f = e >> 4, s = e & 15, b = t0 + s;
-        T[Q.obs_t + e] = b < Q.B ? Q.obs[(size_t)b * Q.obs_feat + f] : 0.0f;
+        const float v = b < Q.B ? Q.obs[(size_t)b * Q.obs_feat + f] : 0.0f;
+        T[Q.obs_t + e] = v;
+        if (C && Q.obs_s >= 0) C[Q.obs_s + e] = v;
     }
 }
 
@@ -272,12 +274,122 @@ __device__ __forceinline__ void bp_lv_run(const BpParams& Q, const BpApp& P, con
     }
 }
 
+// The level kernel's units with the LDS tensor cache C (BpApp xs / ys / gys /
+// gxs): the same arithmetic as bp_dense_fwd_blk / bp_dense_dx_blk, operands
+// read from the cache copies where the host placed them, outputs written to the
+// arena and to their copy, ∂L/∂x accumulated in its copy (the first
+// contribution adds to 0, as into the zeroed arena)
+__device__ __forceinline__ void bp_c_fwd_blk(const BpApp& P, const float* __restrict__ flat, float* T, float* C,
+                                             int ob) {
+    const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
+    const float* W = flat + P.w_off;
+    const float* X = P.xs >= 0 ? C + P.xs : T + P.x;
+    const int nk = (P.in + 3) >> 2;
+    const int o = ob * 16 + m;
+    const bool oin = o < P.out;
+    const bp_f32x4 acc = bp_gemm_block(nk, kq,
+        [&](int i) { return oin && i < P.in ? W[o + (size_t)P.out * i] : 0.0f; },
+        [&](int i) { return i < P.in ? X[i * 16 + m] : 0.0f; });
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int oo = ob * 16 + kq * 4 + r;
+        if (oo < P.out) {
+            const float v = bp_act(P.act, acc[r] + flat[P.b_off + oo]);
+            T[P.y + oo * 16 + m] = v;
+            if (P.ys >= 0) C[P.ys + oo * 16 + m] = v;
+        }
+    }
+}
+__device__ __forceinline__ void bp_c_dx_blk(const BpApp& P, const float* __restrict__ flat, const float* T, float* G,
+                                            float* C, int ib) {
+    const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
+    const float* W = flat + P.w_off;
+    const float* DY = P.gys >= 0 ? C + P.gys : G + P.y;
+    const float* Y = T + P.y;
+    const bool wout = P.gys >= 0 && ib == 0;                  // the copy's final value to the arena (mz_bp_dw)
+    const int nk = (P.out + 3) >> 2;
+    const int i = ib * 16 + m;
+    const bool iin = i < P.in;
+    const bp_f32x4 acc = bp_gemm_block(nk, kq,
+        [&](int o) { return iin && o < P.out ? W[o + (size_t)P.out * i] : 0.0f; },
+        [&](int o) {
+            if (o >= P.out) return 0.0f;
+            const float g = DY[o * 16 + m];
+            if (wout) G[P.y + o * 16 + m] = g;
+            return bp_dz(P.act, g, Y[o * 16 + m]);
+        });
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int ii = ib * 16 + kq * 4 + r;
+        if (ii >= P.in) continue;
+        if (P.gxs >= 0) {
+            float* d = C + P.gxs + ii * 16 + m;
+            *d = (P.gxf ? 0.0f : *d) + acc[r];
+        } else {
+            G[P.x + ii * 16 + m] += acc[r];
+        }
+    }
+}
+__device__ __forceinline__ void bp_c_concat(const BpParams& Q, const BpApp& P, float* T, float* G, float* C, bool fwd) {
+    const int lane = threadIdx.x & 63, t0 = blockIdx.x * 16, K1 = Q.K + 1;
+    if (fwd) {                                                // make_dynamics_input (:293-304)
+        for (int e = lane; e < P.out * 16; e += 64) {
+            const int i = e >> 4, s = e & 15, b = t0 + s;
+            float v;
+            if (i < P.in) v = (P.xs >= 0 ? C[P.xs + e] : T[P.x + e]) * 2.0f;
+            else v = b < Q.B ? Q.actions[(size_t)b * K1 + P.step] / (float)Q.A : 0.0f;
+            T[P.y + e] = v;
+            if (P.ys >= 0) C[P.ys + e] = v;
+        }
+    } else {                                                  // ∂(2h)/∂h
+        for (int e = lane; e < P.in * 16; e += 64) {
+            const float g = 2.0f * (P.gys >= 0 ? C[P.gys + e] : G[P.y + e]);
+            if (P.gxs >= 0) C[P.gxs + e] = (P.gxf ? 0.0f : C[P.gxs + e]) + g;
+            else G[P.x + e] += g;
+        }
+    }
+}
+
 template <bool FWD>
 __device__ __forceinline__ void bp_lv_levels(const BpParams& Q, const BpApp* apps, const int2* units, const int* lev,
-                                             int nlev, float* T, float* G) {
+                                             int nlev, float* T, float* G, const int* sync = nullptr,
+                                             float* C = nullptr) {
     const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
 #if BP_LV_SIMPLE
     const int lane = threadIdx.x & 63;
+    if (C) {                                                  // with the LDS tensor cache
+#ifdef MZ_STAMPS
+        auto stampc = [&](int i) { if (blockIdx.x == 0 && threadIdx.x == 0) Q.stamps[i] = __builtin_amdgcn_s_memtime(); };
+        if (FWD) stampc(0);
+#endif
+        for (int l = 0; l < nlev; ++l) {
+            for (int u = lev[l] + wave; u < lev[l + 1]; u += nw) {
+                const int2 un = units[u];
+                const BpApp P = apps[un.x];
+                if (P.op == BP_DENSE) {
+                    if (FWD) bp_c_fwd_blk(P, Q.flat, T, C, un.y);
+                    else bp_c_dx_blk(P, Q.flat, T, G, C, un.y);
+                } else {
+                    bp_c_concat(Q, P, T, G, C, FWD);
+                }
+            }
+            if (sync[l]) {
+                __syncthreads();
+            } else {                                          // the level's hand-offs are in LDS only
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+            }
+#ifdef MZ_STAMPS
+            stampc((FWD ? 2 : 256) + l);
+#endif
+        }
+        return;
+    }
+#ifdef MZ_STAMPS   // tile 0's level ends: [0] start, forward levels from 2, backward from 256
+    auto stamp = [&](int i) { if (blockIdx.x == 0 && threadIdx.x == 0) Q.stamps[i] = __builtin_amdgcn_s_memtime(); };
+    if (FWD) stamp(0);
+#endif
     for (int l = 0; l < nlev; ++l) {
         for (int u = lev[l] + wave; u < lev[l + 1]; u += nw) {
             const int2 un = units[u];
@@ -292,6 +404,9 @@ __device__ __forceinline__ void bp_lv_levels(const BpParams& Q, const BpApp* app
             }
         }
         __syncthreads();
+#ifdef MZ_STAMPS
+        stamp((FWD ? 2 : 256) + l);
+#endif
     }
 #elif BP_LV_PREFETCH
     BpPre cur;
@@ -333,18 +448,28 @@ extern "C" __global__ __launch_bounds__(BP_LV_THREADS) void mz_bp_tile_lv(BpPara
     int2* bun = fun + Q.n_funit;
     int* flev = reinterpret_cast<int*>(bun + Q.n_bunit);
     int* blev = flev + Q.n_flev + 2;
+    int* fsy = blev + Q.n_blev + 2;
+    int* bsy = fsy + Q.n_flev + 2;
+    float* C = Q.cache_floats > 0
+                   ? reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(bsy + Q.n_blev + 2) + 15) & ~(uintptr_t)15)
+                   : nullptr;
+    for (int i = threadIdx.x; i < Q.n_flev; i += blockDim.x) fsy[i] = Q.fsync[i];
+    for (int i = threadIdx.x; i < Q.n_blev; i += blockDim.x) bsy[i] = Q.bsync[i];
     for (int i = threadIdx.x; i < Q.n_app; i += blockDim.x) apps[i] = Q.apps[i];
     for (int i = threadIdx.x; i < Q.n_funit; i += blockDim.x) fun[i] = Q.funits[i];
     for (int i = threadIdx.x; i < Q.n_bunit; i += blockDim.x) bun[i] = Q.bunits[i];
     for (int i = threadIdx.x; i < Q.n_flev + 2; i += blockDim.x) flev[i] = i <= Q.n_flev ? Q.flev[i] : Q.n_funit;
     for (int i = threadIdx.x; i < Q.n_blev + 2; i += blockDim.x) blev[i] = i <= Q.n_blev ? Q.blev[i] : Q.n_bunit;
-    bp_prologue(Q, T, G);
+    bp_prologue(Q, T, G, C);
     __syncthreads();
 #if BP_LV_LDS
-    bp_lv_levels<true>(Q, apps, fun, flev, Q.n_flev, T, G);
+    bp_lv_levels<true>(Q, apps, fun, flev, Q.n_flev, T, G, fsy, C);
     bp_heads(Q, T, G);
     __syncthreads();
-    bp_lv_levels<false>(Q, apps, bun, blev, Q.n_blev, T, G);
+#ifdef MZ_STAMPS
+    if (blockIdx.x == 0 && threadIdx.x == 0) Q.stamps[1] = __builtin_amdgcn_s_memtime();
+#endif
+    bp_lv_levels<false>(Q, apps, bun, blev, Q.n_blev, T, G, bsy, C);
 #else   // descriptors by scalar loads (wave-uniform values straight into SGPRs)
     bp_lv_levels<true>(Q, Q.apps, Q.funits, Q.flev, Q.n_flev, T, G);
     bp_heads(Q, T, G);
@@ -515,10 +640,13 @@ __device__ __forceinline__ float rbp_xhat(const float* X, const RbpApp& L, int P
 }
 
 // bp_gemm_block with RBP_KC k-steps of operands in flight per full chunk (one
-// workgroup per sample leaves the registers for it) and a tail of four k-steps
-// at a time (measured faster than one predicated chunk: 377 vs 312 steps/s on
-// TicTacToe ResNet, tools/ab_rbp.sh), so short reductions run few padded MFMAs
+// workgroup per sample leaves the registers for it), then the rest in chunks
+// of RBP_KC / 2 whose k-steps past the end are skipped by wave-uniform tests
+// (no padded MFMAs): a 1x1 conv over 64 channels (16 k-steps) is one memory
+// round trip instead of four of the earlier four-k-step tail
+#ifndef RBP_KC
 #define RBP_KC 32
+#endif
 template <class FA, class FB>
 __device__ __forceinline__ bp_f32x4 rbp_gemm_block(int nk, int kq, FA fa, FB fb) {
     bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -534,29 +662,91 @@ __device__ __forceinline__ bp_f32x4 rbp_gemm_block(int nk, int kq, FA fa, FB fb)
 #pragma unroll
         for (int j = 0; j < RBP_KC; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
     }
-    for (; k0 < nk; k0 += 4) {                                // the tail, four k-steps at a time
-        float a[4], b[4];
+    constexpr int KH = RBP_KC / 2;
+    for (; k0 < nk; k0 += KH) {                               // the rest, KH k-steps at a time
+        float a[KH], b[KH];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < KH; ++j) {
             const int k = (k0 + j) * 4 + kq;
-            a[j] = k0 + j < nk ? fa(k) : 0.0f;
-            b[j] = k0 + j < nk ? fb(k) : 0.0f;
+            a[j] = fa(k);                                     // fa / fb are zero past the end
+            b[j] = fb(k);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+        for (int j = 0; j < KH; ++j)
+            if (k0 + j < nk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
     }
     return acc;
 }
 
-// forward: output block (16 channels x 16 positions) u of a conv
-__device__ __forceinline__ void rbp_conv_fwd(const RbpParams& Q, const RbpApp& L, const float* X, float* T, int u) {
+// A k x k conv (odd k, channels a multiple of 4) on a zero-padded board
+// ([channel][(Hb + kh − 1)(Wb + kw − 1)], the halo zero): K in tap-major order
+// (k = tap·nc + c), so a k-step's tap is wave-uniform and each operand address
+// is the lane's base plus a constant — no im2col index arithmetic.  A(row, c,
+// tap) = Ab[c·astride + tap]; B(c, tap) = Bp[c·Pp + bofs + sgn·δ(tap)], δ the
+// tap's board offset dy·Wp + dx (sgn = −1: the transposed conv).  The sum runs
+// in another order than rbp_gemm_block's (within the f32 tolerance).
+__device__ __forceinline__ bool rbp_taps(int kw, int kh, int nc) {
+    return kw * kh > 1 && (kw & 1) && (kh & 1) && (nc & 3) == 0;
+}
+__device__ __forceinline__ bp_f32x4 rbp_taps_gemm(const float* Ab, int astride, bool rok, int kw, int kh, int nc,
+                                                  const float* Bp, int Pp, int Wp, int bofs, int kq, int sgn) {
+    bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int ncs = nc >> 2, kk = kw * kh;
+    for (int tap = 0; tap < kk; ++tap) {
+        const int j = tap / kw, i = tap - j * kw;
+        const int delta = sgn * (((kh - 1 - j) - kh / 2) * Wp + ((kw - 1 - i) - kw / 2));
+        const float* ab = Ab + kq * astride + tap;
+        const float* bb = Bp + kq * Pp + bofs + delta;
+        for (int c0 = 0; c0 < ncs; c0 += 16) {
+            float a[16], b[16];
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {
+                const bool in = c0 + jj < ncs;
+                a[jj] = rok && in ? ab[(size_t)(c0 + jj) * 4 * astride] : 0.0f;
+                b[jj] = in ? bb[(c0 + jj) * 4 * Pp] : 0.0f;
+            }
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj)
+                if (c0 + jj < ncs) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[jj], b[jj], acc, 0, 0, 0);
+        }
+    }
+    return acc;
+}
+// the padded board of a k x k conv: width, cells, the lane's base cell
+__device__ __forceinline__ int rbp_pad_w(const RbpApp& L, int Wb) { return Wb + L.kw - 1; }
+__device__ __forceinline__ int rbp_pad_n(const RbpApp& L, int Wb, int P) { return (P / Wb + L.kh - 1) * (Wb + L.kw - 1); }
+__device__ __forceinline__ int rbp_pad_at(const RbpApp& L, int Wb, int p) {
+    const int py = rbp_div(p, Wb, 1.0f / (float)Wb), px = p - py * Wb;
+    return (py + L.kh / 2) * (Wb + L.kw - 1) + px + L.kw / 2;
+}
+// dst[c][padded cell] = src[c][p] (zero off the board), nc channels, all threads
+__device__ __forceinline__ void rbp_pad_stage(const RbpApp& L, int Wb, int P, int nc, const float* src, float* dst) {
+    const int Wp = rbp_pad_w(L, Wb), Pp = rbp_pad_n(L, Wb, P), Hb = P / Wb;
+    const float rPp = 1.0f / (float)Pp, rWp = 1.0f / (float)Wp;
+    for (int e = threadIdx.x; e < nc * Pp; e += blockDim.x) {
+        const int c = rbp_div(e, Pp, rPp), r = e - c * Pp, ry = rbp_div(r, Wp, rWp), rx = r - ry * Wp;
+        const int x = rx - L.kw / 2, y = ry - L.kh / 2;
+        dst[e] = x >= 0 && x < Wb && y >= 0 && y < Hb ? src[c * P + y * Wb + x] : 0.0f;
+    }
+}
+
+// forward: output block (16 channels x 16 positions) u of a conv; the output
+// to the arena and to its ring slot Y, the residual from its slot R (or the arena).
+// A k x k conv with rbp_taps reads X padded (rbp_pad_stage).
+__device__ __forceinline__ void rbp_conv_fwd(const RbpParams& Q, const RbpApp& L, const float* X, float* T, int u,
+                                             float* Y, const float* R) {
     const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4, P = Q.P;
     const int npb = (P + 15) >> 4, ob = u / npb, pb = u - ob * npb;
     const int K = L.kw * L.kh * L.cin, co = ob * 16 + m, p = pb * 16 + m;
     const float* W = Q.flat + L.w_off;
-    const bp_f32x4 acc = rbp_gemm_block((K + 3) >> 2, kq,
-        [&](int k) { return co < L.cout && k < K ? W[k + (size_t)K * co] : 0.0f; },
-        [&](int k) { return rbp_xhat(X, L, P, Q.Wb, k, p); });
+    bp_f32x4 acc;
+    if (rbp_taps(L.kw, L.kh, L.cin))
+        acc = rbp_taps_gemm(W + (size_t)K * (co < L.cout ? co : 0), L.kw * L.kh, co < L.cout, L.kw, L.kh, L.cin, X,
+                            rbp_pad_n(L, Q.Wb, P), rbp_pad_w(L, Q.Wb), rbp_pad_at(L, Q.Wb, p < P ? p : P - 1), kq, 1);
+    else
+        acc = rbp_gemm_block((K + 3) >> 2, kq,
+            [&](int k) { return co < L.cout && k < K ? W[k + (size_t)K * co] : 0.0f; },
+            [&](int k) { return rbp_xhat(X, L, P, Q.Wb, k, p); });
     const int pc = pb * 16 + m;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -569,40 +759,99 @@ __device__ __forceinline__ void rbp_conv_fwd(const RbpParams& Q, const RbpApp& L
             T[L.z + e] = t;
             v = mz_bn_apply(t, Q.flat[L.bn_off + L.cout + o], Q.flat[L.bn_off + o]);
         }
-        if (L.res >= 0) v = v + T[L.res + e];
-        T[L.y + e] = bp_act(L.act, v);
+        if (L.res >= 0) v = v + (R ? R[e] : T[L.res + e]);
+        v = bp_act(L.act, v);
+        T[L.y + e] = v;
+        if (Y) Y[e] = v;
     }
 }
 
-__device__ __forceinline__ void rbp_dense_fwd(const RbpParams& Q, const RbpApp& L, float* T) {
+// A dense layer for one sample, RBP_DS lanes per output (neighbouring lanes,
+// strided over the inputs, combined by a fixed xor tree): the input staged in
+// XS, so the loads of one lane are independent and in flight together
+#define RBP_DS 8
+__device__ __forceinline__ void rbp_dense_fwd(const RbpParams& Q, const RbpApp& L, const float* XS, float* T,
+                                              float* Y) {
     const float* W = Q.flat + L.w_off;
-    for (int o = threadIdx.x; o < L.cout; o += blockDim.x) {
+    const int s0 = threadIdx.x & (RBP_DS - 1);
+    for (int o = threadIdx.x / RBP_DS; o < L.cout; o += blockDim.x / RBP_DS) {    // whole lane groups
         float s = 0.0f;
-        for (int i = 0; i < L.cin; ++i) s = fmaf(W[o + (size_t)L.cout * i], T[L.x + i], s);
-        T[L.y + o] = bp_act(L.act, s + Q.flat[L.b_off + o]);
+        for (int i = s0; i < L.cin; i += RBP_DS) s = fmaf(W[o + (size_t)L.cout * i], XS[i], s);
+#pragma unroll
+        for (int w = 1; w < RBP_DS; w <<= 1) s += __shfl_xor(s, w);
+        if (s0 == 0) {
+            const float v = bp_act(L.act, s + Q.flat[L.b_off + o]);
+            T[L.y + o] = v;
+            if (Y) Y[o] = v;
+        }
     }
 }
 
-// ∂L/∂t of a conv (t = Wx + b) into DT and the residual input's share of ∂L/∂y
-__device__ __forceinline__ void rbp_conv_dt(const RbpParams& Q, const RbpApp& L, const float* T, float* G, float* DT) {
+// G[x] += Wᵀ DT of a dense layer, RBP_DS lanes per input as rbp_dense_fwd
+__device__ __forceinline__ void rbp_dense_dx(const RbpParams& Q, const RbpApp& L, const float* DT, float* G,
+                                             float* GX) {
+    const float* W = Q.flat + L.w_off;
+    const int s0 = threadIdx.x & (RBP_DS - 1);
+    for (int i = threadIdx.x / RBP_DS; i < L.cin; i += blockDim.x / RBP_DS) {
+        float s = 0.0f;
+        for (int o = s0; o < L.cout; o += RBP_DS) s = fmaf(W[o + (size_t)L.cout * i], DT[o], s);
+#pragma unroll
+        for (int w = 1; w < RBP_DS; w <<= 1) s += __shfl_xor(s, w);
+        if (s0 == 0) {
+            if (GX) GX[i] = (L.gxf ? 0.0f : GX[i]) + s;
+            else G[L.x + i] += s;
+        }
+    }
+}
+
+// ∂L/∂t of a conv (t = Wx + b) into DT and the residual input's share of ∂L/∂y;
+// ∂L/∂y from its ring slot GY (then written out to the arena for mz_rbp_dw) or
+// the arena, the residual share into its slot GR or the arena
+__device__ __forceinline__ void rbp_conv_dt(const RbpParams& Q, const RbpApp& L, const float* T, float* G, float* DT,
+                                            const float* GY, float* GR) {
     const int P = Q.P;
+    // the transposed k x k conv reads DT padded (rbp_taps)
+    const bool pad = !L.step && rbp_taps(L.kw, L.kh, L.cout);
+    const int Pp = pad ? rbp_pad_n(L, Q.Wb, P) : P;
     for (int e = threadIdx.x; e < L.cout * P; e += blockDim.x) {
         const int o = rbp_div(e, P, 1.0f / (float)P);
-        const float du = bp_dz(L.act, G[L.y + e], T[L.y + e]);
-        if (L.res >= 0) G[L.res + e] += du;
-        DT[e] = L.bn_off >= 0 ? du * (Q.flat[L.bn_off + L.cout + o] / MZ_BN_S) : du;
+        const float g = GY ? GY[e] : G[L.y + e];
+        if (GY) G[L.y + e] = g;
+        const float du = bp_dz(L.act, g, T[L.y + e]);
+        if (L.res >= 0) {
+            if (GR) GR[e] = (L.grf ? 0.0f : GR[e]) + du;   // the zeroed arena's sum
+            else G[L.res + e] += du;
+        }
+        const float dt = L.bn_off >= 0 ? du * (Q.flat[L.bn_off + L.cout + o] / MZ_BN_S) : du;
+        if (pad) DT[o * Pp + rbp_pad_at(L, Q.Wb, e - o * P)] = dt;
+        else DT[e] = dt;
+    }
+    if (pad) {                                                // the halo of the padded DT
+        const int Wp = rbp_pad_w(L, Q.Wb), Hb = P / Q.Wb;
+        const float rPp = 1.0f / (float)Pp, rWp = 1.0f / (float)Wp;
+        for (int e = threadIdx.x; e < L.cout * Pp; e += blockDim.x) {
+            const int c = rbp_div(e, Pp, rPp), r = e - c * Pp, ry = rbp_div(r, Wp, rWp), rx = r - ry * Wp;
+            const int x = rx - L.kw / 2, y = ry - L.kh / 2;
+            if (!(x >= 0 && x < Q.Wb && y >= 0 && y < Hb)) DT[e] = 0.0f;
+        }
     }
 }
 
 // G[x] += the transposed conv of DT: input block (16 channels x 16 positions) u
-__device__ __forceinline__ void rbp_conv_dx(const RbpParams& Q, const RbpApp& L, const float* DT, float* G, int u) {
+__device__ __forceinline__ void rbp_conv_dx(const RbpParams& Q, const RbpApp& L, const float* DT, float* G, int u,
+                                            float* GX) {
     const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4, P = Q.P, Wb = Q.Wb;
     const int npb = (P + 15) >> 4, ib = u / npb, pb = u - ib * npb;
     const int kk = L.kw * L.kh, K = kk * L.cin, Kt = kk * L.cout, ci = ib * 16 + m, p = pb * 16 + m;
     const float rkk = 1.0f / (float)kk, rkw = 1.0f / (float)L.kw;
     const int py0 = rbp_div(p, Wb, 1.0f / (float)Wb), px0 = p - py0 * Wb;
     const float* W = Q.flat + L.w_off;
-    const bp_f32x4 acc = rbp_gemm_block((Kt + 3) >> 2, kq,
+    bp_f32x4 acc;
+    if (rbp_taps(L.kw, L.kh, L.cout))                        // DT padded by rbp_conv_dt
+        acc = rbp_taps_gemm(W + (size_t)kk * (ci < L.cin ? ci : 0), K, ci < L.cin, L.kw, L.kh, L.cout, DT,
+                            rbp_pad_n(L, Wb, P), rbp_pad_w(L, Wb), rbp_pad_at(L, Wb, p < P ? p : P - 1), kq, -1);
+    else
+    acc = rbp_gemm_block((Kt + 3) >> 2, kq,
         [&](int k) {
             if (ci >= L.cin || k >= Kt) return 0.0f;
             if (kk == 1) return W[ci + (size_t)L.cin * k];
@@ -619,7 +868,10 @@ __device__ __forceinline__ void rbp_conv_dx(const RbpParams& Q, const RbpApp& L,
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int c = ib * 16 + kq * 4 + r;
-        if (c < L.cin && p < P) G[L.x + c * P + p] += acc[r];
+        if (c < L.cin && p < P) {
+            if (GX) GX[c * P + p] = (L.gxf ? 0.0f : GX[c * P + p]) + acc[r];
+            else G[L.x + c * P + p] += acc[r];
+        }
     }
 }
 
@@ -668,141 +920,255 @@ extern "C" __global__ __launch_bounds__(RBP_THREADS) void mz_rbp_sample(RbpParam
     float* G = Q.grad + (size_t)b * Q.arena;
     float* DT = rbp_lds;                                      // [dt_floats] ∂L/∂t of the current application
     float* XS = rbp_lds + Q.dt_floats;                        // [xs_floats] its input, staged
-    for (int e = tid; e < Q.arena; e += nt) G[e] = 0.0f;
+    float* ring = XS + Q.xs_floats;                           // recent outputs / gradients, [slot][dt_floats]
+    for (int r = 0; r < Q.n_gzero; ++r) {                     // the arena-resident ∂L/∂· (the rest: the ring)
+        const int2 z = Q.gzero[r];
+        for (int e = tid; e < z.y; e += nt) G[z.x + e] = 0.0f;
+    }
     for (int e = tid; e < K1 * 3; e += nt) Q.terms[(size_t)b * K1 * 3 + e] = 0.0f;
     for (int e = tid; e < K1; e += nt) Q.pr[(size_t)b * K1 + e] = 0.0f;        // rewards: 0 at step 0
     for (int e = tid; e < Q.obs_feat; e += nt) T[Q.obs_t + e] = Q.obs[(size_t)b * Q.obs_feat + e];
     __syncthreads();
     const int npb = (Q.P + 15) >> 4;
+#ifdef MZ_STAMPS
+    if (b == 0 && tid == 0) Q.stamps[0] = __builtin_amdgcn_s_memtime();
+#endif
     // ---- forward: representation, K dynamics steps, K+1 predictions (Q10)
+    // An application's input comes from its ring slot or is staged from the
+    // arena; its output goes to both.  The barrier after it is LDS-only unless a
+    // later application reads the arena (fsync: the stores drained first).
+    auto lds_barrier = [] {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
     for (int a = 0; a < Q.n_app; ++a) {
         const RbpApp L = Q.apps[a];
+        float* Y = L.yb >= 0 ? ring + L.yb * Q.dt_floats : nullptr;
+        const float* X = L.xb >= 0 ? ring + L.xb * Q.dt_floats : nullptr;
+        if (L.op == RBP_CONV && rbp_taps(L.kw, L.kh, L.cin)) {   // the padded input (rbp_taps_gemm)
+            rbp_pad_stage(L, Q.Wb, Q.P, L.cin, X ? X : T + L.x, XS);
+            lds_barrier();
+            X = XS;
+        } else if (L.op != RBP_CONCAT && !X) {
+            const int n = L.op == RBP_CONV ? L.cin * Q.P : L.cin;
+            for (int e = tid; e < n; e += nt) XS[e] = T[L.x + e];
+            lds_barrier();
+            X = XS;
+        }
         if (L.op == RBP_CONV) {
-            for (int e = tid; e < L.cin * Q.P; e += nt) XS[e] = T[L.x + e];
-            __syncthreads();
+            const float* R = L.rb >= 0 ? ring + L.rb * Q.dt_floats : nullptr;
             const int units = ((L.cout + 15) >> 4) * npb;
-            for (int u = wave; u < units; u += nw) rbp_conv_fwd(Q, L, XS, T, u);
+            for (int u = wave; u < units; u += nw) rbp_conv_fwd(Q, L, X, T, u, Y, R);
         } else if (L.op == RBP_DENSE) {
-            rbp_dense_fwd(Q, L, T);
+            rbp_dense_fwd(Q, L, X, T, Y);
         } else {                                              // make_dynamics_input (:293-304)
             const float av = Q.actions[(size_t)b * K1 + L.step] / (float)Q.A;
-            for (int f = tid; f < L.cout; f += nt) T[L.y + f] = f < L.cin ? T[L.x + f] * 2.0f : av;
+            for (int f = tid; f < L.cout; f += nt) {
+                const float v = f < L.cin ? (X ? X[f] : T[L.x + f]) * 2.0f : av;
+                T[L.y + f] = v;
+                if (Y) Y[f] = v;
+            }
         }
-        __syncthreads();
+        if (L.fsync) __syncthreads();
+        else lds_barrier();
+#ifdef MZ_STAMPS   // sample 0: [0] start, forward application a ends at 1 + a, backward at 2 + n_app + a
+        if (b == 0 && tid == 0) Q.stamps[1 + a] = __builtin_amdgcn_s_memtime();
+#endif
     }
     rbp_heads(Q, T, G, b);
     __syncthreads();
+#ifdef MZ_STAMPS
+    if (b == 0 && tid == 0) Q.stamps[1 + Q.n_app] = __builtin_amdgcn_s_memtime();
+#endif
     // ---- backward, reverse order: the input gradients (the parameter
     // gradients are mz_rbp_dw's, from the arenas this leaves behind)
     for (int a = Q.n_app - 1; a >= 0; --a) {
         const RbpApp L = Q.apps[a];
+        const float* GY = L.gyb >= 0 ? ring + L.gyb * Q.dt_floats : nullptr;
+        float* GX = L.gxb >= 0 ? ring + L.gxb * Q.dt_floats : nullptr;
         if (L.op == RBP_CONV) {
-            rbp_conv_dt(Q, L, T, G, DT);
+            rbp_conv_dt(Q, L, T, G, DT, GY, L.grb >= 0 ? ring + L.grb * Q.dt_floats : nullptr);
             if (!L.step) {
-                __syncthreads();
+                lds_barrier();
                 const int ndx = ((L.cin + 15) >> 4) * npb;
-                for (int u = wave; u < ndx; u += nw) rbp_conv_dx(Q, L, DT, G, u);
+                for (int u = wave; u < ndx; u += nw) rbp_conv_dx(Q, L, DT, G, u, GX);
             }
         } else if (L.op == RBP_DENSE) {
+            for (int o = tid; o < L.cout; o += nt) {
+                const float g = GY ? GY[o] : G[L.y + o];
+                if (GY) G[L.y + o] = g;
+                DT[o] = bp_dz(L.act, g, T[L.y + o]);
+            }
             if (!L.step) {
-                for (int o = tid; o < L.cout; o += nt) DT[o] = bp_dz(L.act, G[L.y + o], T[L.y + o]);
-                __syncthreads();
-                const float* W = Q.flat + L.w_off;
-                for (int i = tid; i < L.cin; i += nt) {
-                    float s = 0.0f;
-                    for (int o = 0; o < L.cout; ++o) s = fmaf(W[o + (size_t)L.cout * i], DT[o], s);
-                    G[L.x + i] += s;
-                }
+                lds_barrier();
+                rbp_dense_dx(Q, L, DT, G, GX);
             }
         } else {                                              // ∂(2h)/∂h
-            for (int f = tid; f < L.cin; f += nt) G[L.x + f] += 2.0f * G[L.y + f];
+            for (int f = tid; f < L.cout; f += nt) {
+                const float g = GY ? GY[f] : G[L.y + f];
+                if (GY) G[L.y + f] = g;
+                if (f < L.cin) {
+                    if (GX) GX[f] = (L.gxf ? 0.0f : GX[f]) + 2.0f * g;
+                    else G[L.x + f] += 2.0f * g;
+                }
+            }
         }
-        __syncthreads();
+        if (L.bsync) __syncthreads();
+        else lds_barrier();
+#ifdef MZ_STAMPS
+        if (b == 0 && tid == 0) Q.stamps[2 + Q.n_app + a] = __builtin_amdgcn_s_memtime();
+#endif
     }
 }
 
-// The parameter gradients of the ResNet nets, one wave per job (a 16x16 block
-// of a layer's W, or the db / dβ / dγ of 16 output channels): Σ over samples b,
-// the layer's applications u and positions p (f32 MFMA with K = that flattened
-// index, four per step) of ∂L/∂t ⊗ the im2col input — ∂L/∂t re-formed from the
-// arenas (dt = du·γ/√(1+ε) with BatchNorm, du = ∂L/∂y ⊙ act'(y)) as mz_rbp_sample
-// formed it.  Writes the data term and the block's Σθ² (f64, fixed tree).
-__device__ __forceinline__ void rbp_dw_index(int t, int nuP, float rnuP, int P, float rP, int& b, int& u, int& p) {
-    b = rbp_div(t, nuP, rnuP);
-    const int r = t - b * nuP;
-    u = rbp_div(r, P, rP);
-    p = r - u * P;
-}
-extern "C" __global__ __launch_bounds__(64) void mz_rbp_dw(RbpDwParams Q) {
+// The parameter gradients of the ResNet nets, one workgroup of RBP_DW_WAVES
+// waves per job (a 16x16 block of a layer's W, or the db / dβ / dγ of 16 output
+// channels): Σ over samples b, the layer's applications u and positions p (f32
+// MFMA with K = that flattened index, four per step) of ∂L/∂t ⊗ the im2col
+// input — ∂L/∂t re-formed from the arenas (dt = du·γ/√(1+ε) with BatchNorm,
+// du = ∂L/∂y ⊙ act'(y)) as mz_rbp_sample formed it.  Wave w sums the (b, u)
+// pairs w, w + RBP_DW_WAVES, ..; a pair's addresses are wave-uniform and its
+// positions' loads are issued together; the waves' partial sums are added in
+// wave order.  Writes the data term and the block's Σθ² (f64, fixed tree).
+#define RBP_DW_ST 12                          // k-steps (4 positions each) loaded at once
+extern "C" __global__ __launch_bounds__(64 * RBP_DW_WAVES) void mz_rbp_dw(RbpDwParams Q) {
+    __shared__ float red[RBP_DW_WAVES][4][64];
     const RbpJob J = Q.jobs[blockIdx.x];
     const RbpLayer L = Q.layers[J.layer];
-    const int lane = threadIdx.x, m = lane & 15, kq = lane >> 4;
-    const int P = L.conv ? Q.P : 1, nuP = L.n_use * P, n = Q.B * nuP;
-    const float rnuP = 1.0f / (float)(nuP > 0 ? nuP : 1), rP = 1.0f / (float)P;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
+    const int P = L.conv ? Q.P : 1, npair = Q.B * L.n_use;
     const bool bn = L.conv && L.bn_off >= 0;
-    double q = 0.0;
+    // the wave's pairs: pr = wave + RBP_DW_WAVES·i, (b, u) kept incrementally
+    auto pair_walk = [&](auto&& body) {
+        int b = 0, u = wave;
+        while (u >= L.n_use && L.n_use > 0) { u -= L.n_use; ++b; }
+        for (int pr = wave; pr < npair; pr += RBP_DW_WAVES) {
+            body(b, Q.uses[L.use0 + u]);
+            u += RBP_DW_WAVES;
+            while (u >= L.n_use) { u -= L.n_use; ++b; }
+        }
+    };
+    float part[4] = {0.f, 0.f, 0.f, 0.f};
     if (J.kb < 0) {                                           // db, dβ, dγ of channels ob·16 + m
         const int o = J.ob * 16 + m;
         const bool in = o < L.cout;
         const float gr = bn && in ? Q.flat[L.bn_off + L.cout + o] / MZ_BN_S : 1.0f;
         float sb = 0.0f, sbe = 0.0f, sga = 0.0f;
         if (in)
-            for (int t = kq; t < n; t += 4) {                 // quarter kq of the reduction
-                int b, u, p;
-                rbp_dw_index(t, nuP, rnuP, P, rP, b, u, p);
-                const RbpUse U = Q.uses[L.use0 + u];
+            pair_walk([&](int b, const RbpUse& U) {
                 const float* T = Q.act + (size_t)b * Q.arena;
                 const float* G = Q.grad + (size_t)b * Q.arena;
-                const int e = o * P + p;
-                const float du = bp_dz(L.act, G[U.y + e], T[U.y + e]);
-                sb += bn ? du * gr : du;
-                if (bn) { sbe += du; sga += du * (T[U.z + e] / MZ_BN_S); }
-            }
+                for (int p = kq; p < P; p += 4) {             // quarter kq of the positions
+                    const int e = o * P + p;
+                    const float du = bp_dz(L.act, G[U.y + e], T[U.y + e]);
+                    sb += bn ? du * gr : du;
+                    if (bn) { sbe += du; sga += du * (T[U.z + e] / MZ_BN_S); }
+                }
+            });
         // the four quarters in a fixed order: (q0 + q1) + (q2 + q3)
         sb += __shfl_xor(sb, 16); sb += __shfl_xor(sb, 32);
         sbe += __shfl_xor(sbe, 16); sbe += __shfl_xor(sbe, 32);
         sga += __shfl_xor(sga, 16); sga += __shfl_xor(sga, 32);
-        if (kq == 0 && in) {
-            const float tb = Q.flat[L.b_off + o];
-            Q.out[L.b_off + o] = sb;
-            q = (double)tb * (double)tb;
-            if (bn) {
-                const float tbe = Q.flat[L.bn_off + o], tga = Q.flat[L.bn_off + L.cout + o];
-                Q.out[L.bn_off + o] = sbe;
-                Q.out[L.bn_off + L.cout + o] = sga;
-                q += (double)tbe * (double)tbe + (double)tga * (double)tga;
-            }
-        }
+        part[0] = sb; part[1] = sbe; part[2] = sga;
     } else {                                                  // W block (rows ob·16.., columns kb·16..)
         const int K = L.conv ? L.kw * L.kh * L.cin : L.cin;
         const int co = J.ob * 16 + m, kc = J.kb * 16 + m;
         const bool oin = co < L.cout, kin = kc < K;
         const float gr = bn && oin ? Q.flat[L.bn_off + L.cout + co] / MZ_BN_S : 1.0f;
-        const bp_f32x4 acc = rbp_gemm_block((n + 3) >> 2, kq,
-            [&](int t) {
-                if (!oin || t >= n) return 0.0f;
-                int b, u, p;
-                rbp_dw_index(t, nuP, rnuP, P, rP, b, u, p);
-                const RbpUse U = Q.uses[L.use0 + u];
-                const size_t base = (size_t)b * Q.arena + U.y + co * P + p;
-                const float du = bp_dz(L.act, Q.grad[base], Q.act[base]);
-                return bn ? du * gr : du;
-            },
-            [&](int t) {
-                if (!kin || t >= n) return 0.0f;
-                int b, u, p;
-                rbp_dw_index(t, nuP, rnuP, P, rP, b, u, p);
-                const RbpUse U = Q.uses[L.use0 + u];
-                const float* X = Q.act + (size_t)b * Q.arena + U.x;
-                return L.conv ? rbp_xhat_k(X, L.cin, L.kw, L.kh, P, Q.Wb, kc, p) : X[kc];
+        bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        if (L.conv) {
+            // the lane's im2col column kc: channel c, tap offsets (dx, dy) (Flux's
+            // flipped kernel, "same" padding: rbp_xhat_k)
+            const int kk = L.kw * L.kh, c = kin ? kc / kk : 0, tap = kin ? kc - c * kk : 0;
+            const int tj = tap / L.kw, ti = tap - tj * L.kw;
+            const int dx = (L.kw - 1 - ti) - L.kw / 2, dy = (L.kh - 1 - tj) - L.kh / 2, Wb = Q.Wb, Hb = P / Wb;
+            const float rW = 1.0f / (float)Wb;
+            const int nst = (P + 3) >> 2;
+            pair_walk([&](int b, const RbpUse& U) {
+                const float* T = Q.act + (size_t)b * Q.arena;
+                const float* G = Q.grad + (size_t)b * Q.arena;
+                const float* X = T + U.x + c * P;
+                for (int s0 = 0; s0 < nst; s0 += RBP_DW_ST) {
+                    float a[RBP_DW_ST], x[RBP_DW_ST];
+#pragma unroll
+                    for (int j = 0; j < RBP_DW_ST; ++j) {
+                        const int p = (s0 + j) * 4 + kq;
+                        const bool pin = p < P;
+                        const int e = U.y + co * P + p;
+                        const float du = oin && pin ? bp_dz(L.act, G[e], T[e]) : 0.0f;
+                        a[j] = bn ? du * gr : du;
+                        float v = 0.0f;
+                        if (kin && pin) {
+                            if (kk == 1) {
+                                v = X[p];
+                            } else {
+                                const int py = rbp_div(p, Wb, rW), px = p - py * Wb + dx, qy = py + dy;
+                                v = px >= 0 && px < Wb && qy >= 0 && qy < Hb ? X[px + Wb * qy] : 0.0f;
+                            }
+                        }
+                        x[j] = v;
+                    }
+#pragma unroll
+                    for (int j = 0; j < RBP_DW_ST; ++j)
+                        if (s0 + j < nst) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], x[j], acc, 0, 0, 0);
+                }
             });
+        } else {                                              // dense: K = the pairs, four per k-step
+            const int nk = (npair + 3) >> 2, kb0 = nk * wave / RBP_DW_WAVES, kb1 = nk * (wave + 1) / RBP_DW_WAVES;
+            const float rn = 1.0f / (float)L.n_use;
+            acc = rbp_gemm_block(kb1 - kb0, kq,
+                [&](int k) {
+                    const int t = k + 4 * kb0;
+                    if (!oin || t >= npair) return 0.0f;
+                    const int b = rbp_div(t, L.n_use, rn), u = t - b * L.n_use;
+                    const size_t base = (size_t)b * Q.arena + Q.uses[L.use0 + u].y + co;
+                    return bp_dz(L.act, Q.grad[base], Q.act[base]);
+                },
+                [&](int k) {
+                    const int t = k + 4 * kb0;
+                    if (!kin || t >= npair) return 0.0f;
+                    const int b = rbp_div(t, L.n_use, rn), u = t - b * L.n_use;
+                    return Q.act[(size_t)b * Q.arena + Q.uses[L.use0 + u].x + kc];
+                });
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part[r] = acc[r];
+    }
+    // the waves' partial sums, added in wave order
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][r][lane] = part[r];
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float v = red[0][r][lane];
+        for (int w = 1; w < RBP_DW_WAVES; ++w) v += red[w][r][lane];
+        part[r] = v;
+    }
+    double q = 0.0;
+    if (J.kb < 0) {
+        const int o = J.ob * 16 + m;
+        if (kq == 0 && o < L.cout) {
+            const float tb = Q.flat[L.b_off + o];
+            Q.out[L.b_off + o] = part[0];
+            q = (double)tb * (double)tb;
+            if (bn) {
+                const float tbe = Q.flat[L.bn_off + o], tga = Q.flat[L.bn_off + L.cout + o];
+                Q.out[L.bn_off + o] = part[1];
+                Q.out[L.bn_off + L.cout + o] = part[2];
+                q += (double)tbe * (double)tbe + (double)tga * (double)tga;
+            }
+        }
+    } else {
+        const int K = L.conv ? L.kw * L.kh * L.cin : L.cin, kc = J.kb * 16 + m;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int o = J.ob * 16 + kq * 4 + r;
-            if (o < L.cout && kin) {
+            if (o < L.cout && kc < K) {
                 const size_t w = (size_t)L.w_off + (L.conv ? kc + (size_t)K * o : o + (size_t)L.cout * kc);
                 const float th = Q.flat[w];
-                Q.out[w] = acc[r];
+                Q.out[w] = part[r];
                 q += (double)th * (double)th;
             }
         }

@@ -31,6 +31,11 @@ struct BpApp {
     int in, out, act;     // dense: dims, activation; concat: in = H (hidden), out = H + plane
     int x, y;             // arena offsets (floats) of the input / output tensor
     int step;             // concat: action column k (actions[b][k]); dense: layer id
+    // mz_bp_tile_lv's LDS tensor cache (float offsets into it, -1: the arena
+    // only): the forward input / output copies, the backward ∂L/∂y copy (written
+    // out to the arena when read) and the ∂L/∂x accumulator; gxf = 1 on the
+    // tensor's first contribution (the zeroed arena's sum starts there)
+    int xs, ys, gys, gxs, gxf;
 };
 
 struct BpHead {
@@ -64,6 +69,9 @@ struct BpParams {
     int n_flev, n_blev, n_funit, n_bunit;
     const int2* funits; const int* flev;
     const int2* bunits; const int* blev;
+    const int* fsync; const int* bsync;   // per level: 1 = the barrier after it drains the arena stores
+    int cache_floats, obs_s;              // the LDS tensor cache (0: none); the observation's copy (-1: none)
+    unsigned long long* stamps;           // diagnostic build (-DMZ_STAMPS) only: level end cycles of tile 0
 };
 #ifndef BP_LV_THREADS
 #define BP_LV_THREADS 1024                // mz_bp_tile_lv: 16 waves, a unit per wave per level
@@ -119,10 +127,20 @@ struct RbpApp {
     int x, y, z, res;           // arena offsets: input, output (after the activation), the conv's t = Wx + b
                                 // (BatchNorm layers), the residual input (-1: none)
     int step;                   // concat: action column; conv / dense: 1 = no input gradient (the observation)
+    int xb, rb, yb;             // forward LDS ring slots (mz_rbp_sample) of x, res (-1: read from the arena), y
+    int fsync;                  // 1: the barrier after this application drains the arena stores (a later
+                                // one reads the arena); else an LDS-only barrier
+    // backward LDS ring: the slot holding ∂L/∂y (gyb; written out to the arena
+    // when read), the slots accumulating ∂L/∂x and ∂L/∂res (gxb, grb; -1: the
+    // arena), gxf / grf = 1 on a tensor's first contribution (a store, not an
+    // add); bsync as fsync, for the backward
+    int gyb, gxb, grb, gxf, grf, bsync;
 };
 
 struct RbpParams {
     int B, K, A, H, P, Wb, obs_feat, arena, n_app, n_head, obs_t, intermediate_rewards, nflat, dt_floats;
+    int xs_floats;                        // LDS: DT [dt_floats], XS [xs_floats], then the ring [.][dt_floats]
+    const int2* gzero; int n_gzero;       // arena ∂L/∂t ranges {offset, floats} zeroed first (not ring-resident)
     const RbpApp* apps; const BpHead* heads;
     float* act; float* grad;              // [B][arena] activations / their gradients
     // LDS: [dt_floats] the application's ∂L/∂t, then its input (the largest conv input)
@@ -130,6 +148,7 @@ struct RbpParams {
     const float* obs; const float* actions; const float* tv; const float* tr; const float* tp;
     const float* gscale; const float* weights;
     float* terms; float* pv; float* pp; float* pr;
+    unsigned long long* stamps;           // diagnostic build (-DMZ_STAMPS) only: application end cycles of sample 0
 };
 
 // One layer of the ResNet nets (conv or dense) and its applications in the unroll
@@ -141,6 +160,7 @@ struct RbpLayer {
 struct RbpUse { int x, y, z; }; // arena offsets of one application: input, output, pre-BatchNorm t
 struct RbpJob { int layer, ob, kb; };   // a 16x16 block of dW; kb = -1: db (dβ, dγ) of channels ob·16 ..
 
+#define RBP_DW_WAVES 4                    // mz_rbp_dw: waves per job
 struct RbpDwParams {
     int B, P, Wb, arena;
     const RbpJob* jobs; const RbpLayer* layers; const RbpUse* uses;

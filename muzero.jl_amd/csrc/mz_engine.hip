@@ -13,6 +13,7 @@
 #include <array>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -298,6 +299,8 @@ struct mz_handle {
     // the corrected learner for the ResNet nets (mz_rbp_sample / mz_rbp_dw)
     bool rbp_built = false;
     int rbp_n_app = 0, rbp_n_head = 0, rbp_arena = 0, rbp_obs_t = 0, rbp_dt = 0, rbp_xs = 0, rbp_n_job = 0, rbp_cap = 0;
+    int rbp_ring = 0;                      // forward / backward LDS ring slots of mz_rbp_sample
+    int2* d_rbp_gzero = nullptr; int rbp_n_gzero = 0;
     int rbp_threads = 256;
     int rbp_job0[4] = {0, 0, 0, 0};
     RbpApp* d_rbp_apps = nullptr; BpHead* d_rbp_heads = nullptr;
@@ -309,6 +312,7 @@ struct mz_handle {
     BpUse* d_bp_uses = nullptr; BpJob* d_bp_jobs = nullptr;
     int2* d_bp_funits = nullptr; int* d_bp_flev = nullptr; int2* d_bp_bunits = nullptr; int* d_bp_blev = nullptr;
     int bp_n_flev = 0, bp_n_blev = 0, bp_n_funit = 0, bp_n_bunit = 0;
+    int* d_bp_fsync = nullptr; int* d_bp_bsync = nullptr; int bp_cache_floats = 0, bp_obs_s = -1;
     double* d_bp_sq = nullptr; int bp_job0[4] = {0, 0, 0, 0};
     float* d_bp_act = nullptr; float* d_bp_grad = nullptr; float* d_bp_terms = nullptr;
     std::vector<void*> sp_allocs;
@@ -2336,6 +2340,89 @@ static int build_bp(mz_handle* h) {
             }
     }
     blev.push_back((int)bun.size());
+    // mz_bp_tile_lv's LDS tensor cache: slots of the largest tensor.  Forward,
+    // level by level: a tensor read at later levels takes a free slot when it
+    // is produced (its readers read the copy) and frees it after its last
+    // reading level.  Backward: a ∂L/∂x takes a slot at its first contribution
+    // and frees it after its producer's level read it (and wrote it out for
+    // mz_bp_dw).  Everything else stays in the arena: the level that writes it
+    // ends with a barrier that drains the stores (fsync / bsync), as do the
+    // last forward level (the heads and the backward read the arena).
+    std::vector<int> fsync(nfl, 0), bsync(nbl, 0);
+    int cache_floats = 0, obs_s = -1;
+    for (BpApp& a : apps) { a.xs = a.ys = a.gys = a.gxs = -1; a.gxf = 0; }
+#if BP_LV_SIMPLE && !BP_LV_PREFETCH
+    {
+        auto rows16 = [](int r) { return ((r + 3) & ~3) * 16; };
+        int slot = rows16(h->obs_feat);
+        for (const BpApp& a : apps) slot = std::max(slot, rows16(a.out));
+        const size_t sched = (size_t)na * sizeof(BpApp) + (fun.size() + bun.size()) * sizeof(int2) +
+                             (size_t)(2 * (nfl + nbl) + 8) * sizeof(int);
+        const int nslot = (int)std::min<size_t>(64, (kLdsMax - sched - 64) / ((size_t)slot * 4));
+        cache_floats = nslot * slot;
+        std::vector<int> free_s;
+        for (int i = nslot - 1; i >= 0; --i) free_s.push_back(i * slot);
+        // forward
+        std::map<int, int> last_read, fslot;                 // tensor -> last reading level, -> slot
+        for (int a = 0; a < na; ++a) last_read[apps[a].x] = std::max(last_read.count(apps[a].x) ? last_read[apps[a].x] : -1, flv[a]);
+        auto take = [&](int t) {
+            if (!last_read.count(t) || free_s.empty()) return -1;
+            const int o = free_s.back(); free_s.pop_back();
+            fslot[t] = o;
+            return o;
+        };
+        obs_s = take(obs_t);
+        for (int l = 0; l < nfl; ++l) {
+            for (auto it = fslot.begin(); it != fslot.end();) {
+                if (last_read[it->first] < l) { free_s.push_back(it->second); it = fslot.erase(it); }
+                else ++it;
+            }
+            for (int a = 0; a < na; ++a)
+                if (flv[a] == l) { auto f = fslot.find(apps[a].x); apps[a].xs = f != fslot.end() ? f->second : -1; }
+            for (int a = 0; a < na; ++a)
+                if (flv[a] == l) {
+                    apps[a].ys = take(apps[a].y);
+                    if (apps[a].ys < 0 && last_read.count(apps[a].y)) fsync[l] = 1;
+                }
+        }
+        fsync[nfl - 1] = 1;
+        // backward
+        free_s.clear();
+        for (int i = nslot - 1; i >= 0; --i) free_s.push_back(i * slot);
+        std::map<int, int> producer, where, gslot;            // tensor -> app, -> slot or -1 (decided), live slots
+        for (int a = 0; a < na; ++a) producer[apps[a].y] = a;
+        for (const BpHead& hd : heads) where[hd.y] = -1;      // bp_heads writes these to the arena
+        for (int l = 0; l < nbl; ++l) {
+            for (auto it = gslot.begin(); it != gslot.end();) {
+                if (blv[producer[it->first]] < l) { free_s.push_back(it->second); it = gslot.erase(it); }
+                else ++it;
+            }
+            for (int a = 0; a < na; ++a) {
+                if (blv[a] != l) continue;
+                auto g = gslot.find(apps[a].y);
+                apps[a].gys = g != gslot.end() ? g->second : -1;
+            }
+            for (int a = 0; a < na; ++a) {
+                if (blv[a] != l) continue;
+                const int t = apps[a].x;
+                auto w = where.find(t);
+                if (w == where.end()) {
+                    int o = -1;
+                    if (producer.count(t) && !free_s.empty()) {
+                        o = free_s.back(); free_s.pop_back();
+                        gslot[t] = o;
+                        apps[a].gxf = 1;
+                    }
+                    where[t] = o;
+                    apps[a].gxs = o;
+                } else {
+                    apps[a].gxs = w->second;
+                }
+                if (apps[a].gxs < 0) bsync[l] = 1;
+            }
+        }
+    }
+#endif
     // dW: every layer's applications, one wave per 16x16 block (+ one per bias block)
     std::vector<BpLayer> layers(h->layers.size());
     std::vector<BpUse> uses;
@@ -2361,8 +2448,16 @@ static int build_bp(mz_handle* h) {
     };
     if (up(&h->d_bp_apps, apps) || up(&h->d_bp_heads, heads) || up(&h->d_bp_layers, layers) ||
         up(&h->d_bp_uses, uses) || up(&h->d_bp_jobs, jobs) || up(&h->d_bp_funits, fun) ||
-        up(&h->d_bp_flev, flev) || up(&h->d_bp_bunits, bun) || up(&h->d_bp_blev, blev))
+        up(&h->d_bp_flev, flev) || up(&h->d_bp_bunits, bun) || up(&h->d_bp_blev, blev) ||
+        up(&h->d_bp_fsync, fsync) || up(&h->d_bp_bsync, bsync))
         return -1;
+    h->bp_cache_floats = cache_floats; h->bp_obs_s = obs_s;
+    {
+        const size_t lv = (size_t)na * sizeof(BpApp) + (fun.size() + bun.size()) * sizeof(int2) +
+                          (size_t)(2 * (nfl + nbl) + 8) * sizeof(int) + 16 + (size_t)cache_floats * 4;
+        if (lv > kLdsMax) return fail(h, "corrected learner: the level schedule exceeds the LDS");
+        MZ_TRY(h, hipFuncSetAttribute((const void*)mz_bp_tile_lv, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lv));
+    }
     h->bp_n_flev = nfl; h->bp_n_blev = nbl; h->bp_n_funit = (int)fun.size(); h->bp_n_bunit = (int)bun.size();
     h->bp_n_app = (int)apps.size(); h->bp_n_head = (int)heads.size(); h->bp_n_job = (int)jobs.size();
     h->bp_job0[3] = (int)jobs.size();
@@ -2409,8 +2504,13 @@ static int build_rbp(mz_handle* h) {
             a.step = first_obs ? 1 : 0;
             first_obs = false;
             dtf = std::max(dtf, r.conv ? r.cout * P : r.cout);
+            xsf = std::max(xsf, r.conv ? r.cin * P : r.cin);             // the staged input
+            if (r.conv && r.kw * r.kh > 1) {                                // padded (mz_backprop.hip rbp_taps)
+                const int Wb = h->rconf.observation_shape[0], Pp = (P / Wb + r.kh - 1) * (Wb + r.kw - 1);
+                xsf = std::max(xsf, r.cin * Pp);
+                dtf = std::max(dtf, r.cout * Pp);
+            }
             if (r.conv) {
-                xsf = std::max(xsf, r.cin * P);
                 max_units = std::max(max_units, std::max((r.cout + 15) / 16, (r.cin + 15) / 16) * npb);
             }
             apps.push_back(a);
@@ -2425,6 +2525,7 @@ static int build_rbp(mz_handle* h) {
         RbpApp c{};
         c.op = RBP_CONCAT; c.cin = H; c.cout = H + P; c.x = hs[k - 1]; c.y = tensor(c.cout); c.step = k - 1;
         c.bn_off = -1; c.z = -1; c.res = -1;
+        dtf = std::max(dtf, c.cout);                                            // a ring slot holds it too
         apps.push_back(c);
         const int t = chain(MZ_NET_DYN, 0, c.y, false);
         if (k < K) hs[k] = chain(MZ_NET_DYN, 1, t, false);
@@ -2435,6 +2536,79 @@ static int build_rbp(mz_handle* h) {
         heads.push_back(BpHead{BP_HEAD_V, chain(MZ_NET_PRED, 1, t, false), k});
         heads.push_back(BpHead{BP_HEAD_P, chain(MZ_NET_PRED, 2, t, false), k});
     }
+    // mz_rbp_sample's forward LDS ring: application a's output also goes to slot
+    // a mod ns; an input or residual produced fewer than ns applications earlier
+    // is read there, anything else from the arena, after a barrier that drained
+    // the arena stores (fsync on the application before; the backward and the
+    // heads read the arena too)
+    const int ysz = (dtf + 3) & ~3, xsz = (xsf + 3) & ~3;
+    int ns = 4;
+    while (ns > 0 && (size_t)(ysz + xsz + ns * ysz) * 4 > kLdsMax) --ns;
+    {
+        std::map<int, int> producer;
+        for (int a = 0; a < (int)apps.size(); ++a) {
+            RbpApp& A_ = apps[a];
+            auto slot = [&](int t) {
+                auto it = producer.find(t);
+                return it != producer.end() && a - it->second < ns ? it->second % ns : -1;
+            };
+            A_.xb = slot(A_.x);
+            A_.rb = A_.res >= 0 ? slot(A_.res) : -1;
+            A_.yb = ns > 0 ? a % ns : -1;
+            A_.fsync = 0;
+            if ((A_.xb < 0 || (A_.res >= 0 && A_.rb < 0)) && a > 0) apps[a - 1].fsync = 1;
+            producer[A_.y] = a;
+        }
+        apps.back().fsync = 1;
+    }
+    // the backward ring (the same slots): in backward order, a tensor's ∂L/∂·
+    // takes a free slot at its first contribution when its producer follows
+    // within kGLife applications, and frees it when the producer has read it;
+    // otherwise it accumulates in the arena (zeroed first, bsync after each
+    // contribution).  The accumulation order is the arena's.
+    std::vector<int2> gz;
+    {
+        const int kGLife = 6;
+        std::map<int, int> producer, size_of;
+        for (int a = 0; a < (int)apps.size(); ++a) {
+            producer[apps[a].y] = a;
+            size_of[apps[a].y] = apps[a].op == RBP_CONV ? apps[a].cout * P : apps[a].cout;
+        }
+        std::map<int, int> slot_of;          // tensor -> slot (ring-resident, live)
+        std::map<int, int> where;            // tensor -> slot or -1 (decided at the first contribution)
+        std::vector<int> free_slots;
+        for (int i = ns - 1; i >= 0; --i) free_slots.push_back(i);
+        for (int a = (int)apps.size() - 1; a >= 0; --a) {
+            RbpApp& A_ = apps[a];
+            A_.gyb = A_.gxb = A_.grb = -1; A_.gxf = A_.grf = 0; A_.bsync = 0;
+            auto it = slot_of.find(A_.y);
+            if (it != slot_of.end()) A_.gyb = it->second;
+            auto contribute = [&](int t, int& sb, int& first) {
+                auto w = where.find(t);
+                if (w == where.end()) {
+                    auto pr = producer.find(t);
+                    int sl = -1;
+                    if (pr != producer.end() && a - pr->second <= kGLife && !free_slots.empty()) {
+                        sl = free_slots.back(); free_slots.pop_back();
+                        slot_of[t] = sl;
+                        first = 1;
+                    }
+                    where[t] = sl;
+                    sb = sl;
+                } else {
+                    sb = w->second;
+                }
+                if (sb < 0) A_.bsync = 1;
+            };
+            const bool dx = A_.op == RBP_CONCAT || !A_.step;
+            if (dx) contribute(A_.x, A_.gxb, A_.gxf);
+            if (A_.op == RBP_CONV && A_.res >= 0) contribute(A_.res, A_.grb, A_.grf);
+            if (A_.gyb >= 0) { free_slots.push_back(A_.gyb); slot_of.erase(A_.y); }
+        }
+        for (const auto& t : size_of)
+            if (where.find(t.first) == where.end() || where[t.first] < 0) gz.push_back(make_int2(t.first, t.second));
+    }
+    h->rbp_ring = ns;
     // mz_rbp_dw's jobs, net by net (mz_bp_fold sums each net's Σθ² over its job range):
     // per layer its W blocks, then its bias (BatchNorm) blocks; every parameter once
     std::vector<RbpLayer> layers(nl);
@@ -2472,14 +2646,15 @@ static int build_rbp(mz_handle* h) {
         return 0;
     };
     if (up(&h->d_rbp_apps, apps) || up(&h->d_rbp_heads, heads) || up(&h->d_rbp_layers, layers) ||
-        up(&h->d_rbp_uses, uses) || up(&h->d_rbp_jobs, jobs))
+        up(&h->d_rbp_uses, uses) || up(&h->d_rbp_jobs, jobs) || up(&h->d_rbp_gzero, gz))
         return -1;
+    h->rbp_n_gzero = (int)gz.size();
     MZ_TRY(h, dalloc(h, &h->d_rbp_sq, jobs.size()));
     h->rbp_n_app = (int)apps.size(); h->rbp_n_head = (int)heads.size(); h->rbp_n_job = (int)jobs.size();
     h->rbp_arena = off; h->rbp_obs_t = obs_t; h->rbp_dt = (dtf + 3) & ~3; h->rbp_xs = (xsf + 3) & ~3;
     // a wave per 16x16 conv block of a pass (mz_rbp_sample), 4 to 12 waves
     h->rbp_threads = 64 * std::min(12, std::max(4, max_units));
-    const size_t lds = (size_t)(h->rbp_dt + h->rbp_xs) * 4;
+    const size_t lds = (size_t)(h->rbp_dt * (1 + h->rbp_ring) + h->rbp_xs) * 4;
     if (lds > kLdsMax) return fail(h, "corrected learner: a conv's tensors exceed the LDS");
     // above the 64 KB default (e.g. 256 filters on the 6x7 board: ~86 KB)
     MZ_TRY(h, hipFuncSetAttribute((const void*)mz_rbp_sample, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -2503,19 +2678,25 @@ static int rbp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* los
     Q.B = B; Q.K = K; Q.A = h->A; Q.H = h->H; Q.P = h->plane; Q.Wb = h->rconf.observation_shape[0];
     Q.obs_feat = h->rin_feat; Q.arena = h->rbp_arena; Q.n_app = h->rbp_n_app; Q.n_head = h->rbp_n_head;
     Q.obs_t = h->rbp_obs_t; Q.intermediate_rewards = h->conf.intermediate_rewards; Q.nflat = (int)h->nflat;
-    Q.dt_floats = h->rbp_dt;
+    Q.dt_floats = h->rbp_dt; Q.xs_floats = h->rbp_xs; Q.gzero = h->d_rbp_gzero; Q.n_gzero = h->rbp_n_gzero;
     Q.apps = h->d_rbp_apps; Q.heads = h->d_rbp_heads;
     Q.act = h->d_rbp_act; Q.grad = h->d_rbp_grad; Q.flat = h->d_flat;
     Q.obs = b->observation; Q.actions = b->actions; Q.tv = b->target_values; Q.tr = b->target_rewards;
     Q.tp = b->target_policies; Q.gscale = b->gradient_scale; Q.weights = b->weights; Q.terms = h->d_rbp_terms;
     Q.pv = h->d_pv; Q.pp = h->d_pp; Q.pr = h->d_pr;
-    hipLaunchKernelGGL(mz_rbp_sample, dim3(B), dim3(h->rbp_threads), (size_t)(h->rbp_dt + h->rbp_xs) * 4, st, Q);
+    Q.stamps = nullptr;
+#ifdef MZ_STAMPS
+    if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * std::max(h->max_games, 128)));
+    Q.stamps = h->d_stamps;
+#endif
+    hipLaunchKernelGGL(mz_rbp_sample, dim3(B), dim3(h->rbp_threads),
+                       (size_t)(h->rbp_dt * (1 + h->rbp_ring) + h->rbp_xs) * 4, st, Q);
     RbpDwParams D;
     D.B = B; D.P = h->plane; D.Wb = h->rconf.observation_shape[0]; D.arena = h->rbp_arena;
     D.jobs = h->d_rbp_jobs; D.layers = h->d_rbp_layers; D.uses = h->d_rbp_uses;
     D.act = h->d_rbp_act; D.grad = h->d_rbp_grad; D.flat = h->d_flat;
     D.out = grad_dev ? grad_dev : h->d_grad; D.sq = h->d_rbp_sq;
-    hipLaunchKernelGGL(mz_rbp_dw, dim3(h->rbp_n_job), dim3(64), 0, st, D);
+    hipLaunchKernelGGL(mz_rbp_dw, dim3(h->rbp_n_job), dim3(64 * RBP_DW_WAVES), 0, st, D);
     BpFoldParams F;
     F.B = B; F.K = K; F.terms = h->d_rbp_terms; F.gscale = b->gradient_scale; F.weights = b->weights;
     F.flat = h->d_flat; F.netoff = h->d_netoff; F.losses = losses_dev ? losses_dev : h->d_loss;
@@ -2549,9 +2730,15 @@ static int bp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* loss
     Q.tp = b->target_policies; Q.gscale = b->gradient_scale; Q.weights = b->weights; Q.terms = h->d_bp_terms;
     Q.pv = h->d_pv; Q.pp = h->d_pp; Q.pr = h->d_pr;
     Q.n_flev = h->bp_n_flev; Q.n_blev = h->bp_n_blev; Q.n_funit = h->bp_n_funit; Q.n_bunit = h->bp_n_bunit;
+    Q.fsync = h->d_bp_fsync; Q.bsync = h->d_bp_bsync; Q.cache_floats = h->bp_cache_floats; Q.obs_s = h->bp_obs_s;
     const size_t lv_lds = (size_t)Q.n_app * sizeof(BpApp) + (size_t)(Q.n_funit + Q.n_bunit) * sizeof(int2) +
-                          (size_t)(Q.n_flev + Q.n_blev + 4) * sizeof(int);
+                          (size_t)(2 * (Q.n_flev + Q.n_blev) + 8) * sizeof(int) + 16 + (size_t)Q.cache_floats * 4;
     Q.funits = h->d_bp_funits; Q.flev = h->d_bp_flev; Q.bunits = h->d_bp_bunits; Q.blev = h->d_bp_blev;
+    Q.stamps = nullptr;
+#ifdef MZ_STAMPS
+    if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * std::max(h->max_games, 128)));
+    Q.stamps = h->d_stamps;
+#endif
     // the level schedule (default) or the one-application-per-barrier kernel
     // (MZ_BP_SEQ=1, the same bits: tests/test_corrected_learner_gpu.py)
     if (std::getenv("MZ_BP_SEQ")) hipLaunchKernelGGL(mz_bp_tile, dim3(tiles), dim3(256), 0, st, Q);

@@ -11,7 +11,7 @@ timeout -k 10 ${TEST_TIMEOUT:-800} python -u -m pytest tests -m gpu -x -v --time
     ${PYTEST_K:+-k "$PYTEST_K"} > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
 fi
-line() { grep '^{' $1 | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); c=d.get('learner_corrected') or {}; print('$2', d['value'], d['roofline']['frac'], d['roofline']['kernel_ms'], 'learner', d['learner_steps_per_s'], 'corrected', c.get('steps_per_s'), c.get('ms_per_step'))"; }
+line() { grep '^{' $1 | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); c=d.get('learner_corrected') or {}; print('$2', d['value'], d['roofline']['frac'], d['roofline']['kernel_ms'], 'learner', d['learner_steps_per_s'], 'corrected', c.get('learner_steps_per_s'), c.get('step_ms'))"; }
 timeout -k 10 400 python bench.py --net resnet --no-cpu > $O/c2.log 2>&1 || { tail -20 $O/c2.log; exit 1; }
 line $O/c2.log config2
 timeout -k 10 400 python bench.py --game connect4 --net resnet --no-cpu > $O/c3.log 2>&1 || { tail -20 $O/c3.log; exit 1; }
