@@ -29,6 +29,23 @@ __device__ __forceinline__ float bp_dz(int act, float g, float y) {
     return act == MZ_ACT_RELU ? (y > 0.0f ? g : 0.0f) : act == MZ_ACT_TANH ? g * (1.0f - y * y) : g;
 }
 
+// The epilogue of a dense unit's output row oo, sample m: t = W x + b; after a
+// make_dense BatchNorm (use_batch_norm, Learning.jl:70-78) t is kept in the
+// arena for mz_bp_dw and y = act(γ·(t/√(1+ε)) + β), else y = act(t)
+__device__ __forceinline__ float bp_epi(const BpApp& P, const float* __restrict__ flat, float* T, int oo, int m,
+                                        float t) {
+    if (P.bn_off >= 0) {
+        T[P.z + oo * 16 + m] = t;
+        t = mz_bn_apply(t, flat[P.bn_off + P.out + oo], flat[P.bn_off + oo]);
+    }
+    return bp_act(P.act, t);
+}
+// ∂L/∂t of output row o: dY ⊙ act'(y), times γ/√(1+ε) after a BatchNorm
+__device__ __forceinline__ float bp_dt(const BpApp& P, const float* __restrict__ flat, int o, float g, float y) {
+    const float du = bp_dz(P.act, g, y);
+    return P.bn_off >= 0 ? du * (flat[P.bn_off + P.out + o] / MZ_BN_S) : du;
+}
+
 // One 16-row block of a 16-sample MFMA GEMM, C[r][s] = Σ_k A(r, k) B(k, s),
 // its operands gathered BP_KC k-steps at a time (all loads of a chunk in
 // flight before its MFMAs: one memory latency per chunk, not per k-step)
@@ -65,7 +82,7 @@ __device__ __forceinline__ void bp_dense_fwd_blk(const BpApp& P, const float* __
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int oo = ob * 16 + kq * 4 + r;
-        if (oo < P.out) Y[oo * 16 + m] = bp_act(P.act, acc[r] + flat[P.b_off + oo]);
+        if (oo < P.out) Y[oo * 16 + m] = bp_epi(P, flat, T, oo, m, acc[r] + flat[P.b_off + oo]);
     }
 }
 // y = act(W x + b) for the tile (all 256 threads; rows in blocks of 16 per wave)
@@ -88,7 +105,7 @@ __device__ __forceinline__ void bp_dense_dx_blk(const BpApp& P, const float* __r
     const bool iin = i < P.in;
     const bp_f32x4 acc = bp_gemm_block(nk, kq,
         [&](int o) { return iin && o < P.out ? W[o + (size_t)P.out * i] : 0.0f; },
-        [&](int o) { return o < P.out ? bp_dz(P.act, DY[o * 16 + m], Y[o * 16 + m]) : 0.0f; });
+        [&](int o) { return o < P.out ? bp_dt(P, flat, o, DY[o * 16 + m], Y[o * 16 + m]) : 0.0f; });
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int ii = ib * 16 + kq * 4 + r;
@@ -255,7 +272,7 @@ __device__ __forceinline__ void bp_lv_run(const BpParams& Q, const BpApp& P, con
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int oo = ob * 16 + kq * 4 + r;
-            if (oo < P.out) Y[oo * 16 + m] = bp_act(P.act, acc[r] + pr.bias[r]);
+            if (oo < P.out) Y[oo * 16 + m] = bp_epi(P, Q.flat, T, oo, m, acc[r] + pr.bias[r]);
         }
     } else {                                                 // as bp_dense_dx_blk
         const int ib = pr.blk, i = ib * 16 + m;
@@ -265,7 +282,7 @@ __device__ __forceinline__ void bp_lv_run(const BpParams& Q, const BpApp& P, con
         float* DX = G + P.x;
         const bp_f32x4 acc = bp_gemm_block_pre((P.out + 3) >> 2, kq, pr.a,
             [&](int o) { return iin && o < P.out ? W[o + (size_t)P.out * i] : 0.0f; },
-            [&](int o) { return o < P.out ? bp_dz(P.act, DY[o * 16 + m], Y[o * 16 + m]) : 0.0f; });
+            [&](int o) { return o < P.out ? bp_dt(P, Q.flat, o, DY[o * 16 + m], Y[o * 16 + m]) : 0.0f; });
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int ii = ib * 16 + kq * 4 + r;
@@ -294,7 +311,7 @@ __device__ __forceinline__ void bp_c_fwd_blk(const BpApp& P, const float* __rest
     for (int r = 0; r < 4; ++r) {
         const int oo = ob * 16 + kq * 4 + r;
         if (oo < P.out) {
-            const float v = bp_act(P.act, acc[r] + flat[P.b_off + oo]);
+            const float v = bp_epi(P, flat, T, oo, m, acc[r] + flat[P.b_off + oo]);
             T[P.y + oo * 16 + m] = v;
             if (P.ys >= 0) C[P.ys + oo * 16 + m] = v;
         }
@@ -316,7 +333,7 @@ __device__ __forceinline__ void bp_c_dx_blk(const BpApp& P, const float* __restr
             if (o >= P.out) return 0.0f;
             const float g = DY[o * 16 + m];
             if (wout) G[P.y + o * 16 + m] = g;
-            return bp_dz(P.act, g, Y[o * 16 + m]);
+            return bp_dt(P, flat, o, g, Y[o * 16 + m]);
         });
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -521,20 +538,36 @@ extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
     const BpJob J = Q.jobs[blockIdx.x];
     const BpLayer L = Q.layers[J.layer];
     const int lane = threadIdx.x, m = lane & 15, kq = lane >> 4;
-    if (J.ib < 0) {                                           // db = Σ dZ (data term)
+    const bool bn = L.bn_off >= 0;
+    if (J.ib < 0) {                                           // db = Σ dT (data term); BatchNorm: dβ, dγ
         const int o = J.ob * 16 + lane;
         const bool in = lane < 16 && o < L.out;
         double q = 0.0;
         if (in) {
-            float s = 0.0f;
+            const float gr = bn ? Q.flat[L.bn_off + L.out + o] / MZ_BN_S : 1.0f;
+            float s = 0.0f, sbe = 0.0f, sga = 0.0f;
             for (int t = 0; t < Q.tiles; ++t)
                 for (int u = 0; u < L.n_use; ++u) {
-                    const size_t e = (size_t)t * Q.tile_floats + Q.uses[L.use0 + u].y + o * 16;
-                    for (int j = 0; j < 16; ++j) s += bp_dz(L.act, Q.grad[e + j], Q.act[e + j]);
+                    const BpUse U = Q.uses[L.use0 + u];
+                    const size_t e = (size_t)t * Q.tile_floats + U.y + o * 16;
+                    for (int j = 0; j < 16; ++j) {
+                        const float du = bp_dz(L.act, Q.grad[e + j], Q.act[e + j]);
+                        s += bn ? du * gr : du;
+                        if (bn) {
+                            sbe += du;
+                            sga += du * (Q.act[(size_t)t * Q.tile_floats + U.z + o * 16 + j] / MZ_BN_S);
+                        }
+                    }
                 }
             const float th = Q.flat[L.b_off + o];
             Q.out[L.b_off + o] = s;                               // data term (2θ: mz_adam_kernel)
             q = (double)th * (double)th;
+            if (bn) {
+                const float be = Q.flat[L.bn_off + o], ga = Q.flat[L.bn_off + L.out + o];
+                Q.out[L.bn_off + o] = sbe;
+                Q.out[L.bn_off + L.out + o] = sga;
+                q += (double)be * (double)be + (double)ga * (double)ga;
+            }
         }
         for (int d = 32; d > 0; d >>= 1) q += __shfl_xor(q, d);    // fixed tree: Σθ² of the block
         if (lane == 0) Q.sq[blockIdx.x] = q;
@@ -542,6 +575,7 @@ extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
     }
     const int o = J.ob * 16 + m, i = J.ib * 16 + m;
     const bool oin = o < L.out, iin = i < L.in;
+    const float gr = bn && oin ? Q.flat[L.bn_off + L.out + o] / MZ_BN_S : 1.0f;
     bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int t = 0; t < Q.tiles; ++t) {
         const float* gt = Q.grad + (size_t)t * Q.tile_floats;
@@ -551,7 +585,7 @@ extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
 #pragma unroll
             for (int c = 0; c < 4; ++c) {                     // K = the 16 samples, 4 per MFMA
                 const int e = U.y + o * 16 + 4 * c + kq;
-                const float a = oin ? bp_dz(L.act, gt[e], at[e]) : 0.0f;
+                const float a = oin ? bp_dz(L.act, gt[e], at[e]) * gr : 0.0f;
                 const float b = iin ? at[U.x + i * 16 + 4 * c + kq] : 0.0f;
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
             }

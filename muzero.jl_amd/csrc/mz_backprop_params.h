@@ -36,6 +36,10 @@ struct BpApp {
     // out to the arena when read) and the ∂L/∂x accumulator; gxf = 1 on the
     // tensor's first contribution (the zeroed arena's sum starts there)
     int xs, ys, gys, gxs, gxf;
+    // make_dense with use_batch_norm (Learning.jl:70-78): the test-mode
+    // BatchNorm γ·(t/√(1+ε)) + β between the Dense and its relu; β at bn_off,
+    // γ at bn_off + out (-1: none), t = W x + b kept in the arena at z for mz_bp_dw
+    int bn_off, z;
 };
 
 struct BpHead {
@@ -44,10 +48,11 @@ struct BpHead {
     int step;             // unroll step k (targets column)
 };
 
-struct BpUse { int x, y; };   // one application of a dense layer: input / output arena offsets
+struct BpUse { int x, y, z; };   // one application of a dense layer: input / output / pre-BatchNorm t arena offsets
 
 struct BpLayer {
     int w_off, b_off, in, out, act;
+    int bn_off;           // β at bn_off, γ at bn_off + out (-1: no BatchNorm)
     int use0, n_use;      // uses[use0 .. use0 + n_use)
 };
 

@@ -2275,6 +2275,8 @@ static int build_bp(mz_handle* h) {
         BpApp a{};
         a.op = BP_DENSE; a.w_off = (int)L.flux_w; a.b_off = (int)L.flux_b; a.in = L.in; a.out = L.out;
         a.act = L.act; a.x = x; a.y = tensor(L.out); a.step = li;
+        a.bn_off = L.bn ? (int)L.flux_be : -1;                // make_dense's BatchNorm: t kept at z
+        a.z = L.bn ? tensor(L.out) : -1;
         apps.push_back(a);
         return a.y;
     };
@@ -2287,6 +2289,7 @@ static int build_bp(mz_handle* h) {
     for (int k = 1; k <= K; ++k) {                                              // :355-362
         BpApp c{};
         c.op = BP_CONCAT; c.in = H; c.out = H + h->plane; c.x = hs[k - 1]; c.y = tensor(c.out); c.step = k - 1;
+        c.bn_off = c.z = -1;
         apps.push_back(c);
         const int t = chain(MZ_NET_DYN, CH_TRUNK, c.y);
         if (k < K) hs[k] = chain(MZ_NET_DYN, CH_HEAD1, t);
@@ -2433,8 +2436,9 @@ static int build_bp(mz_handle* h) {
         if (h->bp_job0[L.net] < 0) h->bp_job0[L.net] = (int)jobs.size();   // layers are in net order
         BpLayer& bl = layers[li];
         bl.w_off = (int)L.flux_w; bl.b_off = (int)L.flux_b; bl.in = L.in; bl.out = L.out; bl.act = L.act;
+        bl.bn_off = L.bn ? (int)L.flux_be : -1;
         bl.use0 = (int)uses.size();
-        for (const BpApp& a : apps) if (a.op == BP_DENSE && a.step == (int)li) uses.push_back(BpUse{a.x, a.y});
+        for (const BpApp& a : apps) if (a.op == BP_DENSE && a.step == (int)li) uses.push_back(BpUse{a.x, a.y, a.z});
         bl.n_use = (int)uses.size() - bl.use0;
         for (int ob = 0; ob < (L.out + 15) / 16; ++ob) {
             for (int ib = 0; ib < (L.in + 15) / 16; ++ib) jobs.push_back(BpJob{(int)li, ob, ib});
@@ -2765,8 +2769,6 @@ int mz_learner_set_mode(mz_handle* h, int mode) {
     if (mode != MZ_LEARN_REF_SEMANTICS && mode != MZ_LEARN_CORRECTED) return fail(h, "unknown learner mode");
     if (mode == MZ_LEARN_CORRECTED && h->kind == 1 && h->ds)
         return fail(h, "the corrected learner does not backpropagate through the downsampler (ResNetHP.downsample)");
-    if (mode == MZ_LEARN_CORRECTED && h->hp.use_batch_norm)
-        return fail(h, "the corrected learner does not backpropagate through BatchNorm FC layers");
     h->learn_mode = mode;
     return 0;
 }

@@ -9,8 +9,8 @@ CPU: the oracle's forward against torch fp32 (Linear, F.batch_norm in eval
 mode, relu) at 1e-5, and the parameter layout (Python specs, oracle, the
 checkpoint table).  GPU: the engine bit for bit against the oracle — the three
 forwards, searches on the small and tile-16 kernels, learner steps (every
-parameter including β and γ after ADAM) — and the corrected learner refusing
-BatchNorm nets.
+parameter including β and γ after ADAM) — and the corrected learner's
+gradient through the BatchNorm layers against torch float64 autograd.
 """
 import dataclasses
 
@@ -182,12 +182,50 @@ def test_bn_learner_steps_bitexact(ttt, bn_hyper):
 
 
 @pytest.mark.gpu
-def test_bn_corrected_learner_refused(ttt, bn_hyper):
-    from muzero_jl_amd.abi import MzError
-    nets = _bn_nets(ttt.conf, bn_hyper)
-    eng = _engine(ttt.conf, bn_hyper, nets, 4)
-    with pytest.raises(MzError, match="BatchNorm"):
-        eng.learner_set_mode(1)
+@pytest.mark.parametrize("B,K,ir,per", [(32, 5, True, False), (20, 3, False, True)])
+def test_bn_corrected_gradient_matches_torch(ttt, bn_hyper, B, K, ir, per):
+    """The corrected learner through the BatchNorm FC nets: the data gradient of
+    every parameter (W, b, β, γ) of every net, the losses (Σθ² over β and γ
+    too) and the read-outs against torch float64 autograd at 1e-5."""
+    import torch
+    from muzero_jl_amd import abi
+    from test_corrected_learner_gpu import _batch
+    from torch_learner_ref import corrected_loss_and_grads
+    conf = dataclasses.replace(ttt.conf, batch_size=B, num_unroll_steps=K, intermediate_rewards=ir)
+    nets = [n * np.float32(2.0) for n in _bn_nets(conf, bn_hyper, seed=B + K)]   # livelier activations
+    eng = _engine(conf, bn_hyper, nets, 8)
+    eng.learner_set_mode(abi.LEARN_CORRECTED)
+    rng = np.random.default_rng(B)
+    batch = _batch(B, K, 9, 63, rng)
+    wts = (rng.random(B).astype(np.float32) * 0.9 + 0.1) if per else None
+    dev = [torch.from_numpy(np.ascontiguousarray(batch[k])).cuda() for k in
+           ("observation", "actions", "target_values", "target_rewards", "target_policies", "gradient_scale")]
+    dev.append(torch.from_numpy(wts).cuda() if per else None)
+    grad = torch.zeros(eng.grad_count(), dtype=torch.float32, device="cuda")
+    losses = torch.zeros(8, dtype=torch.float32, device="cuda")
+    eng.learner_grad_dev([t.data_ptr() if t is not None else None for t in dev], B, grad.data_ptr(),
+                         losses.data_ptr())
+    eng.sync()
+    ref = corrected_loss_and_grads(conf, bn_hyper, nets, batch, wts)
+    g = grad.cpu().numpy()
+    off = 0
+    for n in range(3):
+        gn = g[off: off + nets[n].size].astype(np.float64)   # the data term (2θ: apply)
+        rn = ref["grads"][n] - 2.0 * nets[n].astype(np.float64)
+        off += nets[n].size
+        scale = np.abs(rn).max()
+        assert scale > 1e-4, f"net {n}: no data gradient reached it"
+        err = np.abs(gn - rn).max() / scale
+        assert err < 1e-5, f"net {n}: data gradient rel. error {err:.3g}"
+    lo = losses.cpu().numpy()
+    np.testing.assert_allclose([lo[0], lo[1], lo[2]], [ref["value"], ref["reward"], ref["policy"]],
+                               rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(lo[3:6], ref["l2"], rtol=1e-5)
+    pv, pp, pr = eng.debug_unroll(B)
+    np.testing.assert_allclose(pv, ref["values"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(pp, ref["policies"], rtol=1e-5, atol=1e-6)
+    if ir:
+        np.testing.assert_allclose(pr, ref["rewards"], rtol=1e-5, atol=1e-6)
     eng.close()
 
 

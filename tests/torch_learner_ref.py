@@ -13,27 +13,38 @@ import torch
 
 
 def _fc_chain(conf, hyper, nets, params):
-    from muzero_jl_amd.networks import unflatten
+    """FC nets; with use_batch_norm every make_dense is Dense then BatchNorm in
+    test mode (μ = 0, σ² = 1, ε = 1e-5) before the relu (Learning.jl:70-78),
+    β and γ after the Dense's W and b."""
+    import torch.nn.functional as F
+    from muzero_jl_amd.networks import layer_specs
 
     def layers(net):
-        # the same slicing as networks.unflatten, on the autograd leaves
+        # the same slicing as networks.unflatten(with_bn=True), on the autograd leaves
         out, off = [], 0
-        for ch, W, b, act in unflatten(conf, hyper, net, np.asarray(nets[net])):
-            o, i = W.shape
+        for ch, i, o, act, bn in layer_specs(conf, hyper, net, True):
             Wt = params[net][off: off + i * o].reshape(i, o).T
             off += i * o
             bt = params[net][off: off + o]
             off += o
-            out.append((ch, Wt, bt, act))
+            bg = None
+            if bn:
+                bg = (params[net][off: off + o], params[net][off + o: off + 2 * o])
+                off += 2 * o
+            out.append((ch, Wt, bt, act, bg))
+        assert off == len(nets[net])
         return out
 
     L = [layers(n) for n in range(3)]
 
     def chain(net, ch, x):
-        for c, W, b, act in L[net]:
+        for c, W, b, act, bg in L[net]:
             if c != ch:
                 continue
             x = x @ W.T + b
+            if bg is not None:
+                x = F.batch_norm(x, torch.zeros(x.shape[1], dtype=x.dtype), torch.ones(x.shape[1], dtype=x.dtype),
+                                 bg[1], bg[0], training=False, eps=1e-5)
             x = torch.relu(x) if act == 1 else torch.tanh(x) if act == 2 else x
         return x
     return chain
