@@ -446,7 +446,7 @@ def main():
     # backprop through the unroll on MFMA; with world > 1 the exchanged
     # gradient is data-dependent
     corrected = None
-    if game is not atari and args.learner_steps > 0 and not args.search_only:
+    if args.learner_steps > 0 and not args.search_only:
         from muzero_jl_amd.abi import LEARN_CORRECTED, LEARN_REF_SEMANTICS
         eng.learner_set_mode(LEARN_CORRECTED)
         for k in range(3):
@@ -471,7 +471,9 @@ def main():
         corrected = {"learner_steps_per_s": round(ncs / float(tcs.item()), 1), "step_ms": round(cms, 5),
                      "flop_per_step": f_fb, "tflops": round(f_fb / (cms * 1e-3) / 1e12, 4),
                      "frac": round(f_fb / (cms * 1e-3) / 1e12 / PEAK_F32, 5),
-                     "kernels": ("mz_rp_sample + mz_rbp_sample + mz_rbp_dw + mz_bp_fold + mz_adam_kernel"
+                     "kernels": (("mz_rp_sample + mz_dsbp_fwd + mz_rbp_sample + mz_dsbp_bwd + mz_dsbp_dw + "
+                                  "mz_rbp_dw + mz_bp_fold + mz_adam_kernel") if game is atari else
+                                 "mz_rp_sample + mz_rbp_sample + mz_rbp_dw + mz_bp_fold + mz_adam_kernel"
                                  if resnet else "mz_rp_sample + mz_bp_tile_lv + mz_bp_dw + mz_bp_fold + mz_adam_kernel")}
         eng.learner_set_mode(LEARN_REF_SEMANTICS)
 

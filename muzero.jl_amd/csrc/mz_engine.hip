@@ -35,6 +35,9 @@ extern "C" __global__ void mz_rsearch_root(RSearchParams P);
 extern "C" __global__ void mz_rsearch_tree(RSearchParams P);
 extern "C" __global__ void mz_rsearch_root32(RSearchParams P);
 extern "C" __global__ void mz_downsample_kernel(DsParams Q);
+extern "C" __global__ void mz_dsbp_fwd(DsBpParams Q);
+extern "C" __global__ void mz_dsbp_bwd(DsBpParams Q);
+extern "C" __global__ void mz_dsbp_dw(DsDwParams Q);
 extern "C" __global__ void mz_rsearch_tree32(RSearchParams P);
 extern "C" __global__ void mz_rsearch_tree_lds(RSearchParams P);
 extern "C" __global__ void mz_rsearch_tree_lds32(RSearchParams P);
@@ -307,6 +310,10 @@ struct mz_handle {
     RbpLayer* d_rbp_layers = nullptr; RbpUse* d_rbp_uses = nullptr; RbpJob* d_rbp_jobs = nullptr;
     float* d_rbp_act = nullptr; float* d_rbp_grad = nullptr;
     float* d_rbp_terms = nullptr; double* d_rbp_sq = nullptr;
+    // ... through the downsampler (mz_dsbp_*): per-sample arenas, one dW job per conv output channel
+    int dsbp_arena = 0, dsbp_dt = 0, dsbp_n_job = 0, dsbp_cap = 0;
+    DsBpLayer* d_dsbp_lay = nullptr; DsDwJob* d_dsbp_jobs = nullptr;
+    float* d_dsbp_act = nullptr; float* d_dsbp_grad = nullptr;
     int bp_n_app = 0, bp_n_head = 0, bp_n_job = 0, bp_tile_floats = 0, bp_obs_t = 0, bp_tiles_cap = 0;
     BpApp* d_bp_apps = nullptr; BpHead* d_bp_heads = nullptr; BpLayer* d_bp_layers = nullptr;
     BpUse* d_bp_uses = nullptr; BpJob* d_bp_jobs = nullptr;
@@ -2491,6 +2498,8 @@ static int build_rbp(mz_handle* h) {
     for (int n = 0; n < 3; ++n) { lbase[n] = nl; nl += (int)sp[n].size(); }
     std::vector<std::vector<RbpUse>> luse(nl);
     const int npb = (P + 15) / 16;
+    // the representation's tail follows the downsampler's parameters in net 0
+    auto fo = [&](int net) { return h->flat_off[net] + (net == MZ_NET_REPR && h->ds ? h->ds_n : 0); };
     auto chain = [&](int net, int ch, int x, bool first_obs) {
         int saved = -1;
         for (size_t si = 0; si < sp[net].size(); ++si) {
@@ -2498,8 +2507,8 @@ static int build_rbp(mz_handle* h) {
             if (r.chain != ch) continue;
             RbpApp a{};
             a.op = r.conv ? RBP_CONV : RBP_DENSE;
-            a.w_off = (int)(h->flat_off[net] + r.woff); a.b_off = (int)(h->flat_off[net] + r.boff);
-            a.bn_off = r.conv && r.bn ? (int)(h->flat_off[net] + r.bnoff) : -1;
+            a.w_off = (int)(fo(net) + r.woff); a.b_off = (int)(fo(net) + r.boff);
+            a.bn_off = r.conv && r.bn ? (int)(fo(net) + r.bnoff) : -1;
             a.cin = r.cin; a.cout = r.cout; a.kw = r.kw; a.kh = r.kh; a.act = r.act;
             a.x = x; a.y = tensor(r.conv ? r.cout * P : r.cout);
             a.z = a.bn_off >= 0 ? tensor(r.cout * P) : -1;
@@ -2524,7 +2533,8 @@ static int build_rbp(mz_handle* h) {
         return x;
     };
     std::vector<int> hs(K + 1, -1);
-    hs[0] = chain(MZ_NET_REPR, 0, obs_t, true);                                 // :347
+    // :347; with the downsampler the first conv also produces ∂L/∂(its input) for mz_dsbp_bwd
+    hs[0] = chain(MZ_NET_REPR, 0, obs_t, !h->ds);
     for (int k = 1; k <= K; ++k) {                                              // :355-362
         RbpApp c{};
         c.op = RBP_CONCAT; c.cin = H; c.cout = H + P; c.x = hs[k - 1]; c.y = tensor(c.cout); c.step = k - 1;
@@ -2611,6 +2621,7 @@ static int build_rbp(mz_handle* h) {
         }
         for (const auto& t : size_of)
             if (where.find(t.first) == where.end() || where[t.first] < 0) gz.push_back(make_int2(t.first, t.second));
+        if (h->ds) gz.push_back(make_int2(obs_t, h->rin_feat));
     }
     h->rbp_ring = ns;
     // mz_rbp_dw's jobs, net by net (mz_bp_fold sums each net's Σθ² over its job range):
@@ -2625,8 +2636,8 @@ static int build_rbp(mz_handle* h) {
             const RSpec& r = sp[n][si];
             const int li = lbase[n] + (int)si;
             RbpLayer& L = layers[li];
-            L.conv = r.conv; L.w_off = (int)(h->flat_off[n] + r.woff); L.b_off = (int)(h->flat_off[n] + r.boff);
-            L.bn_off = r.conv && r.bn ? (int)(h->flat_off[n] + r.bnoff) : -1;
+            L.conv = r.conv; L.w_off = (int)(fo(n) + r.woff); L.b_off = (int)(fo(n) + r.boff);
+            L.bn_off = r.conv && r.bn ? (int)(fo(n) + r.bnoff) : -1;
             L.cin = r.cin; L.cout = r.cout; L.kw = r.kw; L.kh = r.kh; L.act = r.act;
             L.use0 = (int)uses.size(); L.n_use = (int)luse[li].size();
             for (const RbpUse& u : luse[li]) uses.push_back(u);
@@ -2642,6 +2653,34 @@ static int build_rbp(mz_handle* h) {
         }
     }
     h->rbp_job0[3] = (int)jobs.size();
+    // the downsampler (mz_dsbp_*): arena tensors per layer, one dW job per conv output channel
+    std::vector<DsBpLayer> dlay;
+    std::vector<DsDwJob> djobs;
+    if (h->ds) {
+        const DsPlan& D = h->dsplan;
+        int o = 0, maxdt = 0;
+        auto t = [&](int n) { const int r = o; o += (n + 3) & ~3; return r; };
+        dlay.resize(D.n);
+        for (int i = 0; i < D.n; ++i) {
+            const DsLayer& L = D.L[i];
+            const int n = L.cout * L.Wo * L.Ho;
+            dlay[i].x = i == 0 ? -1 : dlay[i - 1].y;
+            dlay[i].y = t(n);
+            dlay[i].z = L.kind == DS_CONV && L.bn ? t(n) : -1;
+            dlay[i].res = L.res_add ? dlay[i - 1].x : -1;
+            if (L.kind != DS_CONV) continue;
+            maxdt = std::max(maxdt, n);
+            const int K = L.kw * L.kh * L.cin;
+            if (K + 3 > DS_DW_THREADS) return fail(h, "corrected learner: a downsampler conv has too many taps");
+            for (int co = 0; co < L.cout; ++co) djobs.push_back(DsDwJob{i, co});
+            for (int e = 0; e < K * L.cout; ++e) covered[(size_t)L.woff + e] = 1;
+            for (int co = 0; co < L.cout; ++co) covered[(size_t)L.boff + co] = 1;
+            if (L.bn) for (int e = 0; e < 2 * L.cout; ++e) covered[(size_t)L.bnoff + e] = 1;
+        }
+        h->dsbp_dt = o;
+        h->dsbp_arena = o + ((maxdt + 3) & ~3);
+        h->dsbp_n_job = (int)djobs.size();
+    }
     for (size_t i = 0; i < h->nflat; ++i)
         if (!covered[i]) return fail(h, "corrected learner: a parameter no gradient job covers");
     auto up = [&](auto** d, const auto& v) -> int {
@@ -2652,8 +2691,10 @@ static int build_rbp(mz_handle* h) {
     if (up(&h->d_rbp_apps, apps) || up(&h->d_rbp_heads, heads) || up(&h->d_rbp_layers, layers) ||
         up(&h->d_rbp_uses, uses) || up(&h->d_rbp_jobs, jobs) || up(&h->d_rbp_gzero, gz))
         return -1;
+    if (h->ds && (up(&h->d_dsbp_lay, dlay) || up(&h->d_dsbp_jobs, djobs))) return -1;
     h->rbp_n_gzero = (int)gz.size();
-    MZ_TRY(h, dalloc(h, &h->d_rbp_sq, jobs.size()));
+    // Σθ² per job: the downsampler's jobs first (net 0), then mz_rbp_dw's
+    MZ_TRY(h, dalloc(h, &h->d_rbp_sq, jobs.size() + djobs.size()));
     h->rbp_n_app = (int)apps.size(); h->rbp_n_head = (int)heads.size(); h->rbp_n_job = (int)jobs.size();
     h->rbp_arena = off; h->rbp_obs_t = obs_t; h->rbp_dt = (dtf + 3) & ~3; h->rbp_xs = (xsf + 3) & ~3;
     // a wave per 16x16 conv block of a pass (mz_rbp_sample), 4 to 12 waves
@@ -2676,6 +2717,20 @@ static int rbp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* los
         MZ_TRY(h, dalloc(h, &h->d_rbp_terms, (size_t)B * (K + 1) * 3));
         h->rbp_cap = B;
     }
+    if (h->ds && B > h->dsbp_cap) {
+        MZ_TRY(h, dalloc(h, &h->d_dsbp_act, (size_t)B * h->dsbp_arena));
+        MZ_TRY(h, dalloc(h, &h->d_dsbp_grad, (size_t)B * h->dsbp_arena));
+        h->dsbp_cap = B;
+    }
+    DsBpParams DP;
+    if (h->ds) {                                  // the downsampler's forward, its output the tail's input
+        if (ensure_dsb(h, B)) return -1;
+        DP.B = B; DP.arena = h->dsbp_arena; DP.bn_s = h->bn_s; DP.plan = h->d_dsplan; DP.lay = h->d_dsbp_lay;
+        DP.flat = h->d_flat; DP.obs = b->observation; DP.act = h->d_dsbp_act; DP.grad = h->d_dsbp_grad;
+        DP.out = h->d_dsb; DP.gout = h->d_rbp_grad; DP.gstride = h->rbp_arena; DP.goff = h->rbp_obs_t;
+        DP.dt_off = h->dsbp_dt;
+        hipLaunchKernelGGL(mz_dsbp_fwd, dim3(B), dim3(DS_THREADS), 0, st, DP);
+    }
     if ((size_t)B * (size_t)std::max(1, K + 1) * (size_t)h->plane >= (1u << 20))
         return fail(h, "corrected learner: batch x unroll x board too large for the dW index");
     RbpParams Q;
@@ -2685,7 +2740,8 @@ static int rbp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* los
     Q.dt_floats = h->rbp_dt; Q.xs_floats = h->rbp_xs; Q.gzero = h->d_rbp_gzero; Q.n_gzero = h->rbp_n_gzero;
     Q.apps = h->d_rbp_apps; Q.heads = h->d_rbp_heads;
     Q.act = h->d_rbp_act; Q.grad = h->d_rbp_grad; Q.flat = h->d_flat;
-    Q.obs = b->observation; Q.actions = b->actions; Q.tv = b->target_values; Q.tr = b->target_rewards;
+    Q.obs = h->ds ? h->d_dsb : b->observation; Q.actions = b->actions; Q.tv = b->target_values;
+    Q.tr = b->target_rewards;
     Q.tp = b->target_policies; Q.gscale = b->gradient_scale; Q.weights = b->weights; Q.terms = h->d_rbp_terms;
     Q.pv = h->d_pv; Q.pp = h->d_pp; Q.pr = h->d_pr;
     Q.stamps = nullptr;
@@ -2695,20 +2751,29 @@ static int rbp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* los
 #endif
     hipLaunchKernelGGL(mz_rbp_sample, dim3(B), dim3(h->rbp_threads),
                        (size_t)(h->rbp_dt * (1 + h->rbp_ring) + h->rbp_xs) * 4, st, Q);
+    const int nds = h->ds ? h->dsbp_n_job : 0;
+    if (h->ds) {                                  // ∂L/∂(downsampler output) is the arena's obs tensor
+        hipLaunchKernelGGL(mz_dsbp_bwd, dim3(B), dim3(DS_THREADS), 0, st, DP);
+        DsDwParams DW;
+        DW.B = B; DW.arena = h->dsbp_arena; DW.n_job = nds; DW.bn_s = h->bn_s; DW.plan = h->d_dsplan;
+        DW.lay = h->d_dsbp_lay; DW.jobs = h->d_dsbp_jobs; DW.obs = b->observation; DW.act = h->d_dsbp_act;
+        DW.grad = h->d_dsbp_grad; DW.flat = h->d_flat; DW.out = grad_dev ? grad_dev : h->d_grad; DW.sq = h->d_rbp_sq;
+        hipLaunchKernelGGL(mz_dsbp_dw, dim3(nds), dim3(DS_DW_THREADS), 0, st, DW);
+    }
     RbpDwParams D;
     D.B = B; D.P = h->plane; D.Wb = h->rconf.observation_shape[0]; D.arena = h->rbp_arena;
     D.jobs = h->d_rbp_jobs; D.layers = h->d_rbp_layers; D.uses = h->d_rbp_uses;
     D.act = h->d_rbp_act; D.grad = h->d_rbp_grad; D.flat = h->d_flat;
-    D.out = grad_dev ? grad_dev : h->d_grad; D.sq = h->d_rbp_sq;
+    D.out = grad_dev ? grad_dev : h->d_grad; D.sq = h->d_rbp_sq + nds;
     hipLaunchKernelGGL(mz_rbp_dw, dim3(h->rbp_n_job), dim3(64 * RBP_DW_WAVES), 0, st, D);
     BpFoldParams F;
     F.B = B; F.K = K; F.terms = h->d_rbp_terms; F.gscale = b->gradient_scale; F.weights = b->weights;
     F.flat = h->d_flat; F.netoff = h->d_netoff; F.losses = losses_dev ? losses_dev : h->d_loss;
     F.sq = h->d_rbp_sq;
-    for (int n = 0; n < 4; ++n) F.job0[n] = h->rbp_job0[n];
+    for (int n = 0; n < 4; ++n) F.job0[n] = n == 0 ? 0 : h->rbp_job0[n] + nds;
     hipLaunchKernelGGL(mz_bp_fold, dim3(4), dim3(256), 0, st, F);
     MZ_TRY(h, hipGetLastError());
-    h->last_lvariant = "mz_rbp_sample+mz_rbp_dw";
+    h->last_lvariant = h->ds ? "mz_dsbp+mz_rbp_sample+mz_rbp_dw" : "mz_rbp_sample+mz_rbp_dw";
     return 0;
 }
 
@@ -2767,8 +2832,6 @@ static int bp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* loss
 int mz_learner_set_mode(mz_handle* h, int mode) {
     if (!h) return -2;
     if (mode != MZ_LEARN_REF_SEMANTICS && mode != MZ_LEARN_CORRECTED) return fail(h, "unknown learner mode");
-    if (mode == MZ_LEARN_CORRECTED && h->kind == 1 && h->ds)
-        return fail(h, "the corrected learner does not backpropagate through the downsampler (ResNetHP.downsample)");
     h->learn_mode = mode;
     return 0;
 }

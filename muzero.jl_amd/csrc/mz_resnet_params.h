@@ -269,3 +269,31 @@ struct DsParams {
     const float* x;          // (in_feat, n_items) column-major
     float* y;                // (out_feat, n_items)
 };
+
+// ---- the corrected learner through the downsampler (mz_dsbp_*, mz_downsample.hip)
+// Per-sample arenas in HBM hold every downsampler layer's output y (the column-
+// major (W, H, C) order) and, for BatchNorm convs, t = W x + b; the gradient
+// arena the same tensors' ∂L/∂y.  The last layer's ∂L/∂y is the ResNet
+// corrected learner's ∂L/∂(representation input) (mz_rbp_sample).
+struct DsBpLayer { int x, y, z, res; };   // arena offsets: input (-1: the observation), output, t (-1), residual
+struct DsBpParams {
+    int B, arena;
+    float bn_s;
+    const DsPlan* plan; const DsBpLayer* lay;
+    const float* flat;
+    const float* obs;                     // (in_feat, B)
+    float* act; float* grad;              // [B][arena]
+    float* out;                           // forward: the downsampler output (out_feat, B)
+    const float* gout; int gstride, goff; // backward: ∂L/∂output of sample b at gout[b·gstride + goff + f]
+    int dt_off;                           // backward: the current conv's ∂L/∂t in the gradient arena
+};
+struct DsDwJob { int layer, co; };        // one output channel of a conv: its W row, b (β, γ)
+#define DS_DW_THREADS 256
+struct DsDwParams {
+    int B, arena, n_job;
+    float bn_s;
+    const DsPlan* plan; const DsBpLayer* lay; const DsDwJob* jobs;
+    const float* obs; const float* act; const float* grad; const float* flat;
+    float* out;                           // Flux-order data term of the gradient
+    double* sq;                           // [n_job]: Σθ² of each job's parameters
+};

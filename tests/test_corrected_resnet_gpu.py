@@ -25,6 +25,18 @@ def _lively(conf, hyper, seed):
     return _perturb_bn(conf, hyper, init_nets(conf, hyper, seed=seed), seed=seed + 1)
 
 
+def _ds_param_count(conf, hyper):
+    """Parameters of the downsampler: net 0's ops up to its last MeanPool (Flux.params order)."""
+    from muzero_jl_amd.networks import resnet_specs
+    ops = resnet_specs(conf, hyper, 0)
+    last = max(i for i, o in enumerate(ops) if o["kind"] == "pool")
+    n = 0
+    for o in ops[:last]:
+        if o["kind"] == "conv":
+            n += o["kw"] * o["kh"] * o["cin"] * o["cout"] + o["cout"] + (2 * o["cout"] if o["bn"] else 0)
+    return n
+
+
 def _batch(B, K, A, feat, rng):
     obs = (rng.random((B, feat)) < 0.4).astype(np.float32)
     tpol = rng.random((B, K + 1, A)).astype(np.float32)
@@ -36,12 +48,14 @@ def _batch(B, K, A, feat, rng):
 
 
 @pytest.mark.parametrize("game,B,K,ir,per", [("ttt", 12, 3, True, False), ("ttt", 7, 0, False, True),
-                                             ("c4", 4, 2, True, True)])
+                                             ("c4", 4, 2, True, True), ("atari", 3, 2, True, True)])
 def test_corrected_resnet_gradient_matches_torch(ttt, game, B, K, ir, per):
+    """atari: configs[4]'s nets, the downsampler (mz_dsbp_*) in front of the
+    representation's tail, 84x84x4 observations."""
     import torch
     from muzero_jl_amd import abi
-    from muzero_jl_amd.games import connect4 as c4
-    mod = ttt if game == "ttt" else c4
+    from muzero_jl_amd.games import atari_synth, connect4 as c4
+    mod = {"ttt": ttt, "c4": c4, "atari": atari_synth}[game]
     conf = dataclasses.replace(mod.conf, batch_size=B, num_unroll_steps=K, intermediate_rewards=ir)
     hyper = mod.resnet_hyper
     nets = _lively(conf, hyper, B + K)
@@ -77,6 +91,12 @@ def test_corrected_resnet_gradient_matches_torch(ttt, game, B, K, ir, per):
         assert scale > 1e-4, f"net {n}: no data gradient reached it"
         err = np.abs(gn - rn).max() / scale
         assert err < 1e-5, f"net {n}: data gradient rel. error {err:.3g}"
+        if n == 0 and game == "atari":               # the downsampler's own slice, on its own scale
+            nd = _ds_param_count(conf, hyper)
+            sd = np.abs(rn[:nd]).max()
+            assert sd > 1e-6, "no data gradient reached the downsampler"
+            ed = np.abs(gn[:nd] - rn[:nd]).max() / sd
+            assert ed < 1e-5, f"downsampler data gradient rel. error {ed:.3g}"
     lo = losses.cpu().numpy()
     np.testing.assert_allclose([lo[0], lo[1], lo[2]], [ref["value"], ref["reward"], ref["policy"]],
                                rtol=1e-5, atol=1e-7)
@@ -92,7 +112,7 @@ def test_corrected_resnet_gradient_matches_torch(ttt, game, B, K, ir, per):
 def test_corrected_resnet_learner_steps(ttt):
     """mz_learner_step in corrected mode = grad_dev + apply (ADAM into the
     ResNet images), bit for bit; the device-sampled learner runs on a
-    self-play shard; the downsampler (configs[4]) is refused."""
+    self-play shard."""
     import torch
     from muzero_jl_amd import abi
     from muzero_jl_amd.config import cos_schedule
@@ -136,10 +156,47 @@ def test_corrected_resnet_learner_steps(ttt):
     e1.sync()
     assert np.all(np.isfinite(out.cpu().numpy()[:6]))
     e1.close(); e2.close()
-    ac = dataclasses.replace(atari_synth.conf, num_iters=4)
-    with pytest.raises(abi.MzError, match="downsampler"):
-        r = abi.Engine(ac, atari_synth.resnet_hyper, device=0, max_games=2, rng_seed=1)
-        try:
-            r.learner_set_mode(abi.LEARN_CORRECTED)
-        finally:
-            r.close()
+
+
+def test_corrected_atari_learner_trains():
+    """configs[4] in corrected mode: grad_dev + apply equals mz_learner_step bit
+    for bit through the downsampler, and the device-sampled learner runs on an
+    Atari-like self-play shard with finite losses."""
+    import torch
+    from muzero_jl_amd import abi
+    from muzero_jl_amd.config import cos_schedule
+    from muzero_jl_amd.games import atari_synth
+    B = 4
+    conf = dataclasses.replace(atari_synth.conf, batch_size=B, num_iters=4, num_unroll_steps=2, max_moves=4,
+                               replay_buffer_size=32)
+    hyper = atari_synth.resnet_hyper
+    nets = _lively(conf, hyper, 5)
+    e1, e2 = (abi.Engine(conf, hyper, device=0, max_games=8, rng_seed=2) for _ in range(2))
+    for e in (e1, e2):
+        for n, w in enumerate(nets):
+            e.set_weights(n, w * np.float32(0.5))
+        e.learner_set_mode(abi.LEARN_CORRECTED)
+    rng = np.random.default_rng(1)
+    grad = torch.zeros(e2.grad_count(), dtype=torch.float32, device="cuda")
+    A = len(conf.action_space)
+    for t in range(1, 3):
+        batch = _batch(B, conf.num_unroll_steps, A, 84 * 84 * 4, rng)
+        l1 = e1.learner_step(batch, 1e-4)
+        dev = [torch.from_numpy(np.ascontiguousarray(batch[k])).cuda() for k in
+               ("observation", "actions", "target_values", "target_rewards", "target_policies", "gradient_scale")]
+        losses = torch.zeros(8, dtype=torch.float32, device="cuda")
+        e2.learner_grad_dev([d.data_ptr() for d in dev] + [None], B, grad.data_ptr(), losses.data_ptr())
+        e2.learner_apply_dev(grad.data_ptr(), 1.0, 1e-4)
+        e2.sync()
+        assert np.array_equal(l1, losses.cpu().numpy()[:6])
+        for n in range(3):
+            assert np.array_equal(e1.get_weights(n), e2.get_weights(n))
+    e1.selfplay_init(abi.ENV_ATARI, 8, 32)
+    for m in range(10):
+        e1.selfplay_move(m)
+    out = torch.zeros(8, dtype=torch.float32, device="cuda")
+    for t in range(3, 5):
+        e1.learner_train_dev(B, t, cos_schedule(t), out.data_ptr())
+    e1.sync()
+    assert np.all(np.isfinite(out.cpu().numpy()[:6]))
+    e1.close(); e2.close()

@@ -54,7 +54,9 @@ def _resnet_chain(conf, hyper, params):
     """The ResNet nets (networks.resnet_specs, Flux-order slices of the leaves):
     convolution = cross-correlation with the kernel flipped, "same" padding,
     BatchNorm in test mode (μ = 0, σ² = 1, ε = 1e-5), residual blocks, the
-    column-major (W,H,C) flatten.  Without the downsampler."""
+    column-major (W,H,C) flatten; with ResNetHP.downsample the representation
+    starts with the downsampler of Learning.jl:175-187 (stride-2 convs, blocks,
+    MeanPool((3,3), stride 2, pad 1) counting the padding)."""
     import torch.nn.functional as F
     from muzero_jl_amd.networks import resnet_board, resnet_specs
     Wb, Hb = resnet_board(conf, hyper)
@@ -64,7 +66,9 @@ def _resnet_chain(conf, hyper, params):
         p = params[net]
         for op in resnet_specs(conf, hyper, net):
             op = dict(op)
-            assert op["kind"] != "pool", "no downsampler"
+            if op["kind"] == "pool":
+                out.append(op)
+                continue
             if op["kind"] == "dense":
                 i, o = op["cin"], op["cout"]
                 op["w"] = p[off: off + i * o].reshape(i, o).T
@@ -92,12 +96,14 @@ def _resnet_chain(conf, hyper, params):
         for op in O[net]:
             if op["chain"] != ch:
                 continue
-            if op["kind"] == "conv":
+            if op["kind"] == "pool":
+                t = F.avg_pool2d(t, 3, stride=2, padding=1, count_include_pad=True)
+            elif op["kind"] == "conv":
                 if t.dim() == 2:                       # (n, W*H*C) column-major -> (n, C, H, W)
-                    t = t.reshape(t.shape[0], op["cin"], Hb, Wb)
+                    t = t.reshape(t.shape[0], op["cin"], op.get("Hi", Hb), op.get("Wi", Wb))
                 if op["res_save"]:
                     res = t
-                y = F.conv2d(t, op["w"], op["b"], padding=(op["kh"] // 2, op["kw"] // 2))
+                y = F.conv2d(t, op["w"], op["b"], stride=op.get("stride", 1), padding=(op["kh"] // 2, op["kw"] // 2))
                 if op["bn"]:
                     y = F.batch_norm(y, torch.zeros(op["cout"], dtype=y.dtype), torch.ones(op["cout"], dtype=y.dtype),
                                      op["gamma"], op["beta"], training=False, eps=1e-5)
@@ -125,7 +131,12 @@ def corrected_loss_and_grads(conf, hyper, nets, batch, weights=None, dtype=torch
     gs = torch.tensor(batch["gradient_scale"], dtype=dtype)
     w = torch.ones_like(gs) if weights is None else torch.tensor(weights, dtype=dtype)
     B = obs.shape[0]
-    plane = conf.observation_shape[0] * conf.observation_shape[1]
+    if isinstance(hyper, ResNetHP):                  # the hidden board (after the downsampler)
+        from muzero_jl_amd.networks import resnet_board
+        Wb, Hb = resnet_board(conf, hyper)
+        plane = Wb * Hb
+    else:
+        plane = conf.observation_shape[0] * conf.observation_shape[1]
     hs = [chain(0, 0, obs)]
     rewards = [torch.zeros(B, dtype=dtype)]
     for k in range(1, K + 1):
