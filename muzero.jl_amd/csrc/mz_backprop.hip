@@ -477,6 +477,10 @@ extern "C" __global__ __launch_bounds__(BP_LV_THREADS) void mz_bp_tile_lv(BpPara
     for (int i = threadIdx.x; i < Q.n_bunit; i += blockDim.x) bun[i] = Q.bunits[i];
     for (int i = threadIdx.x; i < Q.n_flev + 2; i += blockDim.x) flev[i] = i <= Q.n_flev ? Q.flev[i] : Q.n_funit;
     for (int i = threadIdx.x; i < Q.n_blev + 2; i += blockDim.x) blev[i] = i <= Q.n_blev ? Q.blev[i] : Q.n_bunit;
+    // one load per 128-byte line of the parameters: every level's weight reads
+    // then hit this XCD's L2 (ADAM rewrote them through another XCD's)
+    float warm = 0.0f;
+    for (int i = threadIdx.x * 32; i < Q.nflat; i += blockDim.x * 32) warm += Q.flat[i];
     bp_prologue(Q, T, G, C);
     __syncthreads();
 #if BP_LV_LDS
@@ -487,6 +491,7 @@ extern "C" __global__ __launch_bounds__(BP_LV_THREADS) void mz_bp_tile_lv(BpPara
     if (blockIdx.x == 0 && threadIdx.x == 0) Q.stamps[1] = __builtin_amdgcn_s_memtime();
 #endif
     bp_lv_levels<false>(Q, apps, bun, blev, Q.n_blev, T, G, bsy, C);
+    if (Q.B < 0) Q.terms[threadIdx.x] = warm;                // never: keeps the warm-up loads
 #else   // descriptors by scalar loads (wave-uniform values straight into SGPRs)
     bp_lv_levels<true>(Q, Q.apps, Q.funits, Q.flev, Q.n_flev, T, G);
     bp_heads(Q, T, G);

@@ -76,6 +76,7 @@ struct BpParams {
     const int2* bunits; const int* blev;
     const int* fsync; const int* bsync;   // per level: 1 = the barrier after it drains the arena stores
     int cache_floats, obs_s;              // the LDS tensor cache (0: none); the observation's copy (-1: none)
+    int nflat;                            // mz_bp_tile_lv warms the workgroup's L2 with the parameters (all levels read them)
     unsigned long long* stamps;           // diagnostic build (-DMZ_STAMPS) only: level end cycles of tile 0
 };
 #ifndef BP_LV_THREADS

@@ -231,25 +231,25 @@ extern "C" __global__ __launch_bounds__(DS_THREADS) void mz_dsbp_bwd(DsBpParams 
     }
 }
 
-// Parameter gradients: one workgroup per (conv, output channel).  Thread
-// (k, s) sums column k of the channel's im2col product (k < K: W; K: db;
-// K + 1, K + 2: dβ, dγ) over the (sample, position) pairs s, s + S, ..; the S
-// partial sums are added in ascending s.  Also the Σθ² of the job's parameters.
+// Parameter gradients: one workgroup per (conv, output channel co, input
+// channel ci).  Thread (k, s) sums column k of the pair's im2col product
+// (k < kw·kh: the tap's W; with ci = 0 also db, dβ, dγ) over the (sample,
+// position) pairs s, s + S, ..; the S partial sums are added in ascending s.
+// Also the Σθ² of the job's parameters.
 extern "C" __global__ __launch_bounds__(DS_DW_THREADS) void mz_dsbp_dw(DsDwParams Q) {
     __shared__ float red[DS_DW_THREADS];
     const DsPlan& D = *Q.plan;
     const DsDwJob J = Q.jobs[blockIdx.x];
     const DsLayer& L = D.L[J.layer];
     const DsBpLayer A = Q.lay[J.layer];
-    const int tid = threadIdx.x, co = J.co;
+    const int tid = threadIdx.x, co = J.co, c = J.ci;
     const int Wi = L.Wi, Hi = L.Hi, Wo = L.Wo, Pi = Wi * Hi, Po = Wo * L.Ho;
-    const int kk = L.kw * L.kh, K = kk * L.cin, nk = K + (L.bn ? 3 : 1), S = DS_DW_THREADS / nk;
+    const int kk = L.kw * L.kh, K = kk * L.cin, nk = kk + (c == 0 ? (L.bn ? 3 : 1) : 0), S = DS_DW_THREADS / nk;
     const int k = tid % nk, s = tid / nk;
     const float gr = L.bn ? Q.flat[L.bnoff + L.cout + co] / Q.bn_s : 1.0f;
-    int c = 0, dx = 0, dy = 0;
-    if (k < K) {
-        c = k / kk;
-        const int tap = k - c * kk, j = tap / L.kw, i = tap - j * L.kw;
+    int dx = 0, dy = 0;
+    if (k < kk) {
+        const int j = k / L.kw, i = k - j * L.kw;
         dx = (L.kw - 1 - i) - L.pw; dy = (L.kh - 1 - j) - L.ph;
     }
     float acc = 0.0f;
@@ -260,14 +260,14 @@ extern "C" __global__ __launch_bounds__(DS_DW_THREADS) void mz_dsbp_dw(DsDwParam
             const float* G = Q.grad + (size_t)b * Q.arena;
             const int e = co * Po + p;
             const float du = dsbp_dz(L.act, G[A.y + e], T[A.y + e]);
-            if (k < K) {
+            if (k < kk) {
                 const int sx = L.stride * ow + dx, sy = L.stride * oh + dy;
                 const float* X = A.x < 0 ? Q.obs + (size_t)b * D.in_feat : T + A.x;
                 const float xv = sx >= 0 && sx < Wi && sy >= 0 && sy < Hi ? X[sx + Wi * sy + Pi * c] : 0.0f;
                 acc = __builtin_fmaf(du * gr, xv, acc);
-            } else if (k == K) {
+            } else if (k == kk) {
                 acc += du * gr;
-            } else if (k == K + 1) {
+            } else if (k == kk + 1) {
                 acc += du;
             } else {
                 acc += du * (T[A.z + e] / Q.bn_s);
@@ -276,22 +276,25 @@ extern "C" __global__ __launch_bounds__(DS_DW_THREADS) void mz_dsbp_dw(DsDwParam
     }
     red[tid] = acc;
     __syncthreads();
+    const size_t w0 = (size_t)L.woff + (size_t)K * co + (size_t)kk * c;
     if (tid < nk) {
         float t = 0.0f;
         for (int r = 0; r < S; ++r) t += red[tid + r * nk];
-        const size_t dst = tid < K ? (size_t)L.woff + (size_t)K * co + tid
-                         : tid == K ? (size_t)L.boff + co
-                         : tid == K + 1 ? (size_t)L.bnoff + co : (size_t)L.bnoff + L.cout + co;
+        const size_t dst = tid < kk ? w0 + tid
+                         : tid == kk ? (size_t)L.boff + co
+                         : tid == kk + 1 ? (size_t)L.bnoff + co : (size_t)L.bnoff + L.cout + co;
         Q.out[dst] = t;
     }
     if (tid == 0) {
         double q = 0.0;
-        for (int i = 0; i < K; ++i) { const double w = Q.flat[(size_t)L.woff + (size_t)K * co + i]; q += w * w; }
-        const double bb = Q.flat[L.boff + co];
-        q += bb * bb;
-        if (L.bn) {
-            const double be = Q.flat[L.bnoff + co], ga = Q.flat[L.bnoff + L.cout + co];
-            q += be * be + ga * ga;
+        for (int i = 0; i < kk; ++i) { const double w = Q.flat[w0 + i]; q += w * w; }
+        if (c == 0) {
+            const double bb = Q.flat[L.boff + co];
+            q += bb * bb;
+            if (L.bn) {
+                const double be = Q.flat[L.bnoff + co], ga = Q.flat[L.bnoff + L.cout + co];
+                q += be * be + ga * ga;
+            }
         }
         Q.sq[blockIdx.x] = q;
     }

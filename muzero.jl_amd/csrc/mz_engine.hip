@@ -2330,6 +2330,20 @@ static int build_bp(mz_handle* h) {
         }
         blv[a] = l; nbl = std::max(nbl, l + 1);
     }
+    // ... then each backward application as late as those constraints allow
+    // (the same level count): ASAP piles every prediction head of the unroll
+    // into the first levels (~70 units on 16 waves, serialised), ahead of the
+    // dynamics chain they do not gate; ALAP spreads them along the chain.
+    // Application c must precede a (a < c) when a produces c's input or adds
+    // into the same G[x] after it.  MZ_BP_ASAP=1 keeps the ASAP levels.
+    if (!std::getenv("MZ_BP_ASAP")) {
+        for (int c = 0; c < na; ++c) {
+            int l = nbl - 1;
+            for (int a = 0; a < c; ++a)
+                if (apps[c].x == apps[a].y || apps[c].x == apps[a].x) l = std::min(l, blv[a] - 1);
+            blv[c] = l;
+        }
+    }
     std::vector<int2> fun, bun;
     std::vector<int> flev, blev;
     for (int l = 0; l < nfl; ++l) {
@@ -2671,8 +2685,9 @@ static int build_rbp(mz_handle* h) {
             if (L.kind != DS_CONV) continue;
             maxdt = std::max(maxdt, n);
             const int K = L.kw * L.kh * L.cin;
-            if (K + 3 > DS_DW_THREADS) return fail(h, "corrected learner: a downsampler conv has too many taps");
-            for (int co = 0; co < L.cout; ++co) djobs.push_back(DsDwJob{i, co});
+            if (L.kw * L.kh + 3 > DS_DW_THREADS) return fail(h, "corrected learner: a downsampler conv has too many taps");
+            for (int co = 0; co < L.cout; ++co)
+                for (int ci = 0; ci < L.cin; ++ci) djobs.push_back(DsDwJob{i, co, ci});
             for (int e = 0; e < K * L.cout; ++e) covered[(size_t)L.woff + e] = 1;
             for (int co = 0; co < L.cout; ++co) covered[(size_t)L.boff + co] = 1;
             if (L.bn) for (int e = 0; e < 2 * L.cout; ++e) covered[(size_t)L.bnoff + e] = 1;
@@ -2800,6 +2815,8 @@ static int bp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* loss
     Q.pv = h->d_pv; Q.pp = h->d_pp; Q.pr = h->d_pr;
     Q.n_flev = h->bp_n_flev; Q.n_blev = h->bp_n_blev; Q.n_funit = h->bp_n_funit; Q.n_bunit = h->bp_n_bunit;
     Q.fsync = h->d_bp_fsync; Q.bsync = h->d_bp_bsync; Q.cache_floats = h->bp_cache_floats; Q.obs_s = h->bp_obs_s;
+    static const bool no_warm = std::getenv("MZ_BP_NO_WARM") != nullptr;   // A/B only
+    Q.nflat = no_warm ? 0 : (int)h->nflat;
     const size_t lv_lds = (size_t)Q.n_app * sizeof(BpApp) + (size_t)(Q.n_funit + Q.n_bunit) * sizeof(int2) +
                           (size_t)(2 * (Q.n_flev + Q.n_blev) + 8) * sizeof(int) + 16 + (size_t)Q.cache_floats * 4;
     Q.funits = h->d_bp_funits; Q.flev = h->d_bp_flev; Q.bunits = h->d_bp_bunits; Q.blev = h->d_bp_blev;

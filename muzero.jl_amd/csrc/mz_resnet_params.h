@@ -287,7 +287,7 @@ struct DsBpParams {
     const float* gout; int gstride, goff; // backward: ∂L/∂output of sample b at gout[b·gstride + goff + f]
     int dt_off;                           // backward: the current conv's ∂L/∂t in the gradient arena
 };
-struct DsDwJob { int layer, co; };        // one output channel of a conv: its W row, b (β, γ)
+struct DsDwJob { int layer, co, ci; };    // one (output, input) channel pair of a conv: its taps; ci = 0 also b (β, γ)
 #define DS_DW_THREADS 256
 struct DsDwParams {
     int B, arena, n_job;
