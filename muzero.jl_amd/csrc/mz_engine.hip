@@ -1794,6 +1794,8 @@ static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     P.trunk_nl = 1 + 2 * h->rhp.num_blocks; P.dyn_split = h->rn_dyn_split;
     P.trunk = h->d_rtrunk; P.tprog = h->d_tprog;
     P.fault = h->d_fault; P.poll_ticks = h->poll_ticks; P.dbg_skip = h->dbg_skip;
+    static const bool no_moved_skip = std::getenv("MZ_NO_MOVED_SKIP") != nullptr;   // A/B only
+    P.no_moved_skip = no_moved_skip ? 1 : 0;
     const void* kroot = gw == 32 ? (const void*)mz_rsearch_root32 : (const void*)mz_rsearch_root;
     // tree step: LDS-cached (one wave per 64/gw games) unless the tree exceeds the LDS
     const bool tl = h->rtree_lds != 0;

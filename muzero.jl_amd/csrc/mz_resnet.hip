@@ -1010,6 +1010,9 @@ __device__ __forceinline__ void glds_copy(const void* src, void* dst, int n, int
 // (expand, backup, select, the search statistics); every wave shares the
 // copies in, the cached select's recompute rows and the hidden-state gather.
 // The LDS trees already hold a CU alone, so the other waves cost no occupancy.
+#ifndef RT_RECOMP_U
+#define RT_RECOMP_U 4                               // recompute rows per group and pass
+#endif
 template <int GW>
 __device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1156,7 +1159,7 @@ __device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
         const uint32_t ver = sh_ver[gl];
         const float mn = sh_mm[gl][0], mx = sh_mm[gl][1];
         const bool lg = a < A && ((legal >> a) & 1u);
-        constexpr int U = 4;
+        constexpr int U = RT_RECOMP_U;
         int Dl = depth;
         for (int j0 = wave * U; j0 < rows; j0 += nwv * U) {
             int slot[U], Np[U], ch[U];
@@ -1199,7 +1202,24 @@ __device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
         // the nc word of the edge into it from this game's path (levels 0..D of
         // the HBM path stay as they are)
         if (wave == 0 && live) {
-            const int D = sh_skip[gl];
+            int D = sh_skip[gl];
+            if (sh_moved[gl] != 0 && !P.no_moved_skip) {
+                // min / max moved: every expanded node's entry was just recomputed
+                // (current tag), so the walk from the root retraces the last path
+                // down to the first level whose new entry leaves it (or ties)
+                const int depth = sh_depth[gl];
+                const uint32_t ver = sh_ver[gl];
+                int Dl = depth;
+                for (int j = a; j < depth; j += GW) {
+                    const int node = (int)lvl[j].x;
+                    const uint2 ce = cache[node];
+                    const bool on = (ce.x >> 5) == ver && (int)(ce.x & 31u) == path[2 * (j + 1)] - node * A;
+                    if (!on && j < Dl) Dl = j;
+                }
+#pragma unroll
+                for (int o = GW / 2; o > 0; o >>= 1) { const int t = __shfl_xor(Dl, o); Dl = t < Dl ? t : Dl; }
+                D = Dl;
+            }
             const int e0 = D > 0 ? path[2 * D + 1] : 0;
             const uint32_t npc0 = D > 0 ? tree.nc(path[2 * D]) : 0u;
             const SelectOut so = select_path_cached<GW, false>(tree, cache, sh_ver[gl], P.path + (size_t)gg * PS, rN,

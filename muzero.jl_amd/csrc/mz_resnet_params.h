@@ -156,6 +156,7 @@ struct RSearchParams {
     unsigned* fault;                   // MZ_FAULT_RS_TRUNK on a publish that never came (mz_poll_ge)
     unsigned long long poll_ticks;     // the poll's bound (MZ_POLL_TICKS)
     int dbg_skip;                      // debug: the tile whose trunk publish is skipped (-1 = none)
+    int no_moved_skip;                 // A/B only (MZ_NO_MOVED_SKIP): after a min / max move the walk starts at the root
 };
 
 // LDS layout of the LDS-cached tree step (mz_rsearch_tree_lds*): one wave per
