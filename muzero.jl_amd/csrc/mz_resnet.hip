@@ -1044,8 +1044,11 @@ __device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
     // existing nodes 0..n_old-1, the path, the cache entries and N per node
     const int n_old = s > 0 ? s : 1;
     {
+        // the copies go to waves 1.. (wave 0 issues none, so its own loads above
+        // complete on their own and it forms the expansion's prior under the copies)
+        const int nq = nwv > 1 ? nwv - 1 : 1, wq = nwv > 1 ? wave - 1 : wave;
         int k = 0;
-        auto job = [&](auto fn) { if (k++ % nwv == wave) fn(); };
+        auto job = [&](auto fn) { if (k++ % nq == wq) fn(); };
         job([&] { glds_copy<4>(P.pbc_tab, pbc, 2 * (S + 2), lane); });
         job([&] { glds_copy<4>(P.sqrt_tab, sqt, 2 * (S + 2), lane); });
         for (int g = 0; g < NGW; ++g) {
@@ -1054,7 +1057,7 @@ __device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
             const char* src = P.tree + (size_t)gq * P.tree_game_bytes;
             char* dst = lb + L.tables + g * L.game;
             // the edge records in up to nwv pieces of whole 64-record instructions
-            const int ne = n_old * A, per = ((ne + nwv * 64 - 1) / (nwv * 64)) * 64;
+            const int ne = n_old * A, per = ((ne + nq * 64 - 1) / (nq * 64)) * 64;
             for (int c0 = 0; c0 < ne; c0 += per)
                 job([&] { glds_copy<16>(src + 16 * (size_t)c0, dst + 16 * (size_t)c0, ne - c0 < per ? ne - c0 : per, lane); });
             job([&] { glds_copy<4>(src + 16 * (size_t)E, dst + 16 * (size_t)E, n_old, lane); });          // nr
@@ -1067,11 +1070,16 @@ __device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
             }
         }
     }
+    char* gb = lb + L.tables + gl * L.game;
+    // wave 0: double softmax of the leaf's logits (expand_node!, :88-96) for
+    // simulation s-1's node, while the other waves' copies land
+    float prior = 0.0f;
+    if (wave == 0 && live && s > 0)
+        prior = double_softmax_prior<GW>(logit, a, A, (uint32_t)st0.x, reinterpret_cast<float*>(gb + L.stg));
     RT_STAMP(1);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     RT_STAMP(2);
-    char* gb = lb + L.tables + gl * L.game;
     TreeView tree = tree_view(gb, E, NN);
     int* path = reinterpret_cast<int*>(gb + L.path);
     uint2* cache = reinterpret_cast<uint2*>(gb + L.cache);
@@ -1093,7 +1101,6 @@ __device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
             if (a == 0) { cache[0] = make_uint2(0u, 0u); st[RG_VER] = 1; }
         } else {
             const int e_new = s;                        // the node simulation s-1 expanded (:280)
-            const float prior = double_softmax_prior<GW>(logit, a, A, legal, stg);
             init_edges(tree, e_new, a, A, prior);
             const int tl = st2.x;
             depth = st2.y;
