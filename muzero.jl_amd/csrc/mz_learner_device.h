@@ -90,7 +90,12 @@ __device__ __forceinline__ void lg_step_terms(int t, int a, int A, int v_act, in
                                               float* st) {
     const bool in = a < A;
     float* yh = pp + (size_t)t * A;
+    // every input loaded up front, in one round trip (the stores below could
+    // alias them, so the compiler would otherwise issue each load after them)
     const float x = in ? yh[a] : -INFINITY;
+    const float tpa = in ? tp[(size_t)t * A + a] : 0.0f;
+    const float raw = a == 0 ? pv[t] : a == 1 ? pr[t] : 0.0f;
+    const float tvt = a == 0 ? tv[t] : 0.0f;
     const float m = gmax<GW>(x);
     const float e = in ? det_expf(x - m) : 0.0f;
     const float s = gseqsum<GW>(e, A, st, a);
@@ -100,13 +105,13 @@ __device__ __forceinline__ void lg_step_terms(int t, int a, int A, int v_act, in
     const float e2 = in ? det_expf(p - m2) : 0.0f;
     const float se = gseqsum<GW>(e2, A, st, a);
     const float ls = det_logf(se);
-    const float term = in ? tp[(size_t)t * A + a] * ((p - m2) - ls) : 0.0f;
+    const float term = in ? tpa * ((p - m2) - ls) : 0.0f;
     const float ce = gseqsum<GW>(term, A, st, a);
     if (a < 2) {                                // lane 0 the value, lane 1 the reward read-out, at once
-        const float y = mz_post_act(a == 0 ? v_act : r_act, a == 0 ? pv[t] : pr[t]);
+        const float y = mz_post_act(a == 0 ? v_act : r_act, raw);
         if (a == 0) {
             pv[t] = y;
-            const float d = y - tv[t];
+            const float d = y - tvt;
             // read by the last block's fold: agent-scope stores (lg_fold)
             __hip_atomic_store(vsq + t, d * d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(cet + t, ce, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
