@@ -234,6 +234,7 @@ __device__ __forceinline__ void lg_fold(int B, int K, const float* vsq, const fl
         double sv = 0.0, sg = 0.0, sc = 0.0;
         for (int j = lane; j < B; j += 64) {
             float vk[MZ_FOLD_K1], ck[MZ_FOLD_K1];
+            const float gsj = gscale[j], w = wts ? wts[j] : 1.0f;   // issued with the terms below
             float s = 0.0f, c = 0.0f;
             for (int k0 = 0; k0 < K1; k0 += MZ_FOLD_K1) {
 #pragma unroll
@@ -247,10 +248,10 @@ __device__ __forceinline__ void lg_fold(int B, int K, const float* vsq, const fl
                 for (int u = 0; u < MZ_FOLD_K1; ++u)
                     if (k0 + u < K1) { s = s + vk[u]; c = c + (-ck[u]); }
             }
-            const float w = wts ? wts[j] : 1.0f;   // PER importance weights (Learning.jl:271-285)
-            sv += (double)((s / gscale[j]) * w);
+            // w: the PER importance weights (Learning.jl:271-285)
+            sv += (double)((s / gsj) * w);
             sc += (double)c;                    // Σ_k ce_k
-            sg += (double)w / (double)gscale[j];   // Σ_j w_j/g_j
+            sg += (double)w / (double)gsj;      // Σ_j w_j/g_j
         }
         for (int o = 32; o >= 1; o >>= 1) {
             sv += __shfl_xor(sv, o, 64); sg += __shfl_xor(sg, o, 64); sc += __shfl_xor(sc, o, 64);
@@ -261,10 +262,22 @@ __device__ __forceinline__ void lg_fold(int B, int K, const float* vsq, const fl
             out[2] = (float)(sc * sg / ((double)B * (double)B));  // mean over (1,B,B), Q11
         }
     } else if (wave == 1) {                     // Σθ² of the three nets: fixed pairs, then a fixed tree
+        constexpr int NP = (MZ_L2_BLOCKS + 63) / 64;
+        double pq[3][NP];                       // every partial loaded first: one round trip, not three
+#pragma unroll
+        for (int net = 0; net < 3; ++net)
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+                const int b = lane + 64 * i;
+                pq[net][i] = b < MZ_L2_BLOCKS ? __hip_atomic_load(part + net * MZ_L2_BLOCKS + b, __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+            }
+#pragma unroll
         for (int net = 0; net < 3; ++net) {
             double s = 0.0;
-            for (int b = lane; b < MZ_L2_BLOCKS; b += 64)
-                s += __hip_atomic_load(part + net * MZ_L2_BLOCKS + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int i = 0; i < NP; ++i)
+                if (lane + 64 * i < MZ_L2_BLOCKS) s += pq[net][i];
             for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
             if (lane == 0) out[3 + net] = (float)s;
         }
