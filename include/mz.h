@@ -234,8 +234,8 @@ int mz_learner_step(mz_handle* h, const mz_batch* batch, double eta, float* loss
 
 /* Learner mode.  MZ_LEARN_REF_SEMANTICS (default): the reference as written
  * — its pullbacks see only sum(sqnorm, params), so ∇ = 2θ (quirk Q11), and
- * the reported policy loss is Q11's broadcast.  MZ_LEARN_CORRECTED (FC nets
- * without BatchNorm, and the ResNet nets without the downsampler): the loss
+ * the reported policy loss is Q11's broadcast.  MZ_LEARN_CORRECTED (every
+ * net: FC with or without BatchNorm, ResNet with or without the downsampler): the loss
  * Learning.jl:261-288 means, differentiated through the unroll (real
  * backpropagation on MFMA, mz_backprop.hip), as a per-sample mean so a
  * data-parallel all-reduce-mean equals the global batch:

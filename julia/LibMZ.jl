@@ -145,7 +145,7 @@ function learner_step!(e::Engine, batch, eta::Real)
 end
 
 """learner_mode!(e, LEARN_CORRECTED) — real backpropagation through the unroll
-(FC nets, and ResNet nets without the downsampler) instead of the reference's
+(FC nets with or without BatchNorm, ResNet nets with or without the downsampler) instead of the reference's
 ∇ = 2θ (quirk Q11)."""
 learner_mode!(e::Engine, mode::Cint) =
     check(e, ccall((:mz_learner_set_mode, libmz), Cint, (Ptr{Cvoid}, Cint), e.h, mode))
