@@ -207,6 +207,27 @@ def workload(game, resnet, G, S):
     return f"TicTacToe FC (params.jl hyper), {G} games/GPU x {S} sims/move ({cfg})"
 
 
+def replica_check(eng, world, leg):
+    """DP replicas stay bit-identical (Learning.jl:395-397 on every rank): a
+    digest of every rank's flat parameters (all three nets, Flux order) is
+    all-gathered and must agree; a mismatch fails the run before the JSON line."""
+    import hashlib
+    h = hashlib.sha256()
+    for n in range(3):
+        h.update(np.ascontiguousarray(eng.get_weights(n)).tobytes())
+    d = torch.tensor([int.from_bytes(h.digest()[:7], "little")], dtype=torch.int64)
+    if dist.get_backend() == "nccl":                    # (RCCL gathers device tensors)
+        d = d.cuda()
+    got = [torch.zeros_like(d) for _ in range(world)]
+    dist.all_gather(got, d)
+    vals = [int(x.item()) for x in got]
+    assert all(v == vals[0] for v in vals), f"{leg}: replicas diverged (parameter digests {vals})"
+    REPLICA_CHECKS.append(leg)
+
+
+REPLICA_CHECKS = []
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -220,6 +241,9 @@ def main():
                     help="timed moves of the device self-play loop (0 = skip that leg)")
     ap.add_argument("--sims", type=int, default=None, help="sims per move (default 50; atari 200)")
     ap.add_argument("--learner-steps", type=int, default=50)
+    ap.add_argument("--learner-chunk", type=int, default=64,
+                    help="FC, one GPU: consecutive ref_semantics learner steps per mz_learner_train_multi_dev call "
+                         "(1..256, sub-chunks of 16; 1 = the one-step form only)")
     ap.add_argument("--batch", type=int, default=None,
                     help="learner batch size (default conf.batch_size = 32; SURVEY §8d config 3 also names 2048)")
     ap.add_argument("--train-moves", type=int, default=20,
@@ -336,6 +360,7 @@ def main():
         t_ms, n_l = eng.debug_kernel_time()
         eng.debug_enable(0)
         kern_ms = t_ms / n_l
+    eng.sync()
     acts = d_act.cpu().numpy()
     bad = np.flatnonzero(~legal[np.arange(G), acts - 1])
     assert len(bad) == 0, f"illegal action selected in games {bad[:8]} (actions {acts[bad[:8]]})"
@@ -367,6 +392,7 @@ def main():
             mv += 1
         torch.cuda.synchronize()
         tpl = torch.tensor([time.perf_counter() - tp0], dtype=torch.float64, device=dev)
+        eng.sync()
         if world > 1:
             dist.all_reduce(tpl, op=dist.ReduceOp.MAX)
         tpl = float(tpl.item())
@@ -386,13 +412,14 @@ def main():
     # batches sampled on the device from this rank's replay shard (§8f-2),
     # gradient bucket all-reduced over RCCL when world > 1
     B, K = args.batch or conf.batch_size, conf.num_unroll_steps
-    learner_sps = lstep_ms = lkern = None
+    learner_sps = lstep_ms = lkern = learner_1step = None
+    multi = None
     if not args.search_only:
         grad = torch.empty(eng.grad_count(), dtype=torch.float32, device=dev)
         losses = torch.empty(8, dtype=torch.float32, device=dev)
 
         def lstep(k):
-            if world == 1:                                  # get_batch + unroll, losses + ADAM: two launches
+            if world == 1:                                  # get_batch + unroll, losses + ADAM: one launch (FC)
                 eng.learner_train_dev(B, k + 1, cos_schedule(k + 1), losses.data_ptr(), stream=sp)
                 return
             else:                  # get_batch fused into the unroll; the data term of ∇ exchanged, 2θ added by apply
@@ -413,7 +440,8 @@ def main():
         tl = torch.tensor([time.perf_counter() - tl0], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(tl, op=dist.ReduceOp.MAX)
-        learner_sps = args.learner_steps / float(tl.item())
+        learner_1step = learner_sps = args.learner_steps / float(tl.item())
+        eng.sync()                                          # a device fault of the leg fails the run here
         # per-step device time: events around each step on the launch stream, in
         # a separate loop (recording events between steps adds host work)
         nev = 20
@@ -424,6 +452,7 @@ def main():
             lev[k][1].record(stream)
         torch.cuda.synchronize()
         lstep_ms = float(np.mean([a.elapsed_time(b) for a, b in lev]))
+        tnext = 5 + args.learner_steps + nev + 1           # the next learner step number
         # the learner's dominant kernel: FC world 1 = the whole step is one launch
         # (mz_learn_small*), timed by the events around it; ResNet = the unroll
         # (chain + predictions, the pair mz_learner_variant names), timed by the engine's events on its launch stream
@@ -431,7 +460,8 @@ def main():
             eng.debug_enable(4)
             eng.debug_kernel_time()
             for k in range(5):
-                lstep(5 + args.learner_steps + nev + k)
+                lstep(tnext - 1 + k)
+            tnext += 5
             torch.cuda.synchronize()
             t_ms, n_l = eng.debug_kernel_time()
             eng.debug_enable(0)
@@ -441,6 +471,54 @@ def main():
             # records it); world > 1: unroll, all-reduce and ADAM are separate launches (no single kernel)
             lkern = eng.learner_variant() if world == 1 else None
             lkern_ms = lstep_ms
+        # L consecutive steps per launch pair (mz_learner_train_multi_dev; ref_semantics, Q11: the
+        # update does not read the data and PER-off batches are keyed by the step): the FC headline
+        # learner number on one GPU; the one-step form above stays in the line (learner_steps_per_s_1step)
+        if world == 1 and not resnet and args.learner_chunk > 1:
+            L = args.learner_chunk
+            lm = torch.empty((L, 8), dtype=torch.float32, device=dev)
+
+            def lchunk(t0):
+                eng.learner_train_multi_dev(B, t0, [cos_schedule(t0 + i) for i in range(L)], lm.data_ptr(),
+                                            stream=sp)
+
+            for _ in range(2):
+                lchunk(tnext)
+                tnext += L
+            torch.cuda.synchronize()
+            nch = max(4, (args.learner_steps * 8 + L - 1) // L)
+            tm0 = time.perf_counter()
+            for _ in range(nch):
+                lchunk(tnext)
+                tnext += L
+            torch.cuda.synchronize()
+            tm = time.perf_counter() - tm0
+            eng.sync()
+            mev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+            for a, b in mev:
+                a.record(stream)
+                lchunk(tnext)
+                tnext += L
+                b.record(stream)
+            torch.cuda.synchronize()
+            chunk_ms = float(np.mean([a.elapsed_time(b) for a, b in mev]))
+            eng.debug_enable(4)                             # the unroll launches alone (engine events)
+            eng.debug_kernel_time()
+            for _ in range(5):
+                lchunk(tnext)
+                tnext += L
+            torch.cuda.synchronize()
+            t_ms, n_l = eng.debug_kernel_time()
+            eng.debug_enable(0)
+            lkern, lkern_ms = eng.learner_variant().split("+")[-1], t_ms / n_l
+            learner_sps = nch * L / tm
+            lstep_ms = chunk_ms / L
+            multi = {"steps_per_call": L, "steps_per_unroll_launch": 5 * L / n_l,
+                     "learner_steps_per_s": round(learner_sps, 1), "call_ms": round(chunk_ms, 5),
+                     "unroll_launch_ms": round(lkern_ms, 5), "kernels": eng.learner_variant(),
+                     "steps_timed": nch * L}
+        if world > 1:                                       # the DP replicas must still be bit-identical
+            replica_check(eng, world, "learner")
 
     # ---- corrected-gradient learner (MZ_LEARN_CORRECTED; FC and ResNet nets): real
     # backprop through the unroll on MFMA; with world > 1 the exchanged
@@ -476,6 +554,9 @@ def main():
                                  "mz_rp_sample + mz_rbp_sample + mz_rbp_dw + mz_bp_fold + mz_adam_kernel"
                                  if resnet else "mz_rp_sample + mz_bp_tile_lv + mz_bp_dw + mz_bp_fold + mz_adam_kernel")}
         eng.learner_set_mode(LEARN_REF_SEMANTICS)
+        eng.sync()
+        if world > 1:
+            replica_check(eng, world, "learner_corrected")
 
     # ---- actor-learner loop (row a12, self_play! || learning!, Q16): self-play
     # moves with the actors' nets and one learner step per finished game, the
@@ -491,6 +572,7 @@ def main():
         st0 = eng.train_run(args.train_moves, move0=mv, game_offset=rank * G, stream=sp)
         torch.cuda.synchronize()
         ttr = time.perf_counter() - tt0
+        eng.sync()
         mv += args.train_moves
         train = {"moves": args.train_moves, "ms_per_move": round(ttr / args.train_moves * 1e3, 4),
                  "node_expansions_per_s": round(G * S * args.train_moves / ttr, 1),
@@ -533,6 +615,14 @@ def main():
             lbytes = 28 * nparam if not resnet else \
                 4 * nparam + 4 * B * (obs.shape[1] + (K + 1)) + 4 * B * (K + 1) * (A + 2)
             lbytes_step = 28 * nparam
+            if multi:
+                # mz_learn_multi*: L unrolls + loss terms per launch (the ADAM chain runs in mz_learn_chain):
+                # each step reads its θ image (4 B/param), its batch (observations, actions, value / policy
+                # targets, gradient_scale) and writes its read-outs and loss terms
+                Lm = multi["steps_per_unroll_launch"]
+                lflop = Lm * f_unroll
+                lbytes = Lm * (4 * nparam + 4 * B * (obs.shape[1] + 2 * (K + 1) + (K + 1) * A + 1) +
+                               4 * B * (K + 1) * (A + 4))
             lach = lflop / (lkern_ms * 1e-3) / 1e12
             ltraffic, ltraffic_src, lpmc = pmc_record(lkern, pmc_line)
             hbm_gbs = (ltraffic if ltraffic else lbytes) / (lkern_ms * 1e-3) / 1e9
@@ -563,11 +653,18 @@ def main():
                        "games_per_gpu": G, "sims_per_move": S, "global_games": G * world,
                        "parallelism": f"games sharded x{world}, learner dp{world} (RCCL all-reduce)"},
             "learner_steps_per_s": round(learner_sps, 1) if learner_sps else None,
+            "learner_steps_per_s_1step": round(learner_1step, 1) if learner_1step else None,
+            "learner_multi": multi,
+            "replica_checks": REPLICA_CHECKS if world > 1 else None,
             "learner_step_ms": round(lstep_ms, 5) if lstep_ms else None,
             "learner_roofline": lroof,
             "learner_corrected": corrected,
             "train_loop": train,
             "learner_config": {"batch_size": B, "num_unroll_steps": K, "mode": "ref_semantics",
+                               "form": (f"mz_learner_train_multi_dev: {multi['steps_per_call']} consecutive steps "
+                                        f"per call, {multi['steps_per_unroll_launch']:g} per unroll launch "
+                                        f"({multi['kernels']}); the one-step form (mz_learner_train_dev) in "
+                                        "learner_steps_per_s_1step" if multi else "one step per call"),
                                "batch_source": (("mz_learner_train_dev: one launch — unroll + losses, ADAM into the second "
                                  "image set, and step t+1's device get_batch + make_target into the other batch "
                                  "set (step t's was drawn by the previous launch)" if not resnet else

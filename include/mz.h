@@ -181,7 +181,8 @@ int mz_set_sync_stream(mz_handle* h, void* stream, int narrow);
 /* Debug/parity: flags & 1 = keep a copy of every search's final tree in HBM
  * (the LDS-resident tree is otherwise discarded at kernel exit); flags & 2 =
  * time the ResNet search's network launches, flags & 4 = the ResNet
- * learner's unroll launches (mz_debug_kernel_time). */
+ * learner's unroll launches and the unroll launch of each
+ * mz_learner_train_multi_dev (mz_learn_multi*) (mz_debug_kernel_time). */
 int mz_debug_enable(mz_handle* h, int flags);
 
 /* Debug/parity: copy the last search's tree statistics to host.  Per game,
@@ -194,7 +195,7 @@ int mz_debug_tree(mz_handle* h, int G, int32_t* edge_N, float* edge_W, float* ed
 
 /* Measurement: with mz_debug_enable(h, 2) every network launch of the
  * ResNet search (mz_rsearch_nets, its dominant kernel), with flag 4 every
- * learner unroll launch (mz_runroll_kernel), is bracketed by HIP events on
+ * learner unroll launch (mz_runroll_kernel, mz_learn_multi*), is bracketed by HIP events on
  * its stream; this returns the summed duration and the launch count since
  * the previous call, and resets them.                                      */
 int mz_debug_kernel_time(mz_handle* h, double* total_ms, int* launches);
@@ -205,6 +206,9 @@ int mz_debug_kernel_time(mz_handle* h, double* total_ms, int* launches);
  * loss reads (Q10 alignment: step 0 and step 1 both predict from h0,
  * reward 0 at step 0).  Any pointer may be NULL.                          */
 int mz_debug_unroll(mz_handle* h, int B, float* values, float* policies, float* rewards);
+/* The same read-outs of step step0 + i of the last mz_learner_train_multi_dev
+ * that ran its two-launch form (0 <= i < L).                               */
+int mz_debug_unroll_step(mz_handle* h, int i, int B, float* values, float* policies, float* rewards);
 
 /* One learner batch, the tuple returned by get_batch (ReplayBuffer.jl:216),
  * column-major as in the reference:
@@ -368,6 +372,22 @@ int mz_learner_grad_sampled_dev(mz_handle* h, int32_t B, uint32_t step, float* g
 int mz_learner_train_dev(mz_handle* h, int32_t B, uint32_t step, double eta, float* losses_dev,
                          void* stream);
 
+/* L consecutive learner iterations (Learning.jl:327-404) at steps step0 ..
+ * step0+L-1, eta[i] the learning rate of step step0+i (host array): the
+ * results of L mz_learner_train_dev calls, bit for bit.  In ref_semantics
+ * (Q11) the update θ_{s+1} = ADAM(θ_s, 2θ_s) does not read the data, and with
+ * PER off step s's batch is keyed by s, so the FC engine runs the L ADAM
+ * iterations in one launch and the L unrolls + losses side by side in a
+ * second (L·B workgroups instead of B); any other configuration (ResNet, the
+ * corrected mode, PER) runs the L steps one after another.  losses_dev:
+ * NULL or [L][8] (per step the six losses of mz_learner_train_dev);
+ * theta_dev: NULL or [L][nflat], the flat parameters (Flux order, the
+ * mz_weights_get layout of all three nets back to back) after each step.
+ * 1 <= L <= 256: the steps run in sub-chunks of up to 16 (one ADAM launch
+ * and one unroll launch each).  Replaces L iterations of the learner loop. */
+int mz_learner_train_multi_dev(mz_handle* h, int32_t B, uint32_t step0, int32_t L, const double* eta,
+                               float* losses_dev, float* theta_dev, void* stream);
+
 /* PER (conf.PER, ReplayBuffer.jl:133-145, 168-183; Learning.jl:400-404).
  * With PER the shard keeps per-position priorities (initialised by
  * save_game: |root_value − target_value|^PER_alpha, game priority = max),
@@ -458,7 +478,15 @@ const char* mz_search_variant(const mz_handle* h);
  * (e.g. mz_runroll_chain_r+mz_runroll_pred_n1), for profiles; "none" before. */
 const char* mz_learner_variant(const mz_handle* h);
 
-/* Synchronize the handle's stream. */
+/* Wait for the engine's work (the device, or the pair mz_set_sync_stream
+ * named) and report a device fault.  A kernel that gives up waiting for a
+ * cross-workgroup publish (a bounded poll, 2 s) sets a fault word instead of
+ * hanging; this and every host-synchronous call then fail once with the
+ * message.  What it invalidates: the outputs of the launches since the last
+ * synchronisation — search results, the games self-play stored from them in
+ * the replay shard, losses and read-outs.  The ref_semantics weights and
+ * ADAM state stay valid (their update does not read those outputs, Q11);
+ * after a fault re-create the shard (mz_selfplay_init) before training on it. */
 int mz_sync(mz_handle* h);
 
 #ifdef __cplusplus

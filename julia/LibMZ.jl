@@ -171,6 +171,12 @@ end
 learner_train!(e::Engine, B, step, eta; losses=C_NULL) =  # get_batch + learning! on the device shard
     check(e, ccall((:mz_learner_train_dev, libmz), Cint, (Ptr{Cvoid}, Int32, UInt32, Float64, Ptr{Float32}, Ptr{Cvoid}),
                    e.h, B, step, eta, losses, C_NULL))
+# length(etas) consecutive learning! iterations from step0 (ref_semantics, Q11: the ADAM chain in one
+# launch, the unrolls side by side in a second); losses: C_NULL or a device [8, L] buffer
+learner_train_multi!(e::Engine, B, step0, etas::Vector{Float64}; losses=C_NULL) =
+    check(e, ccall((:mz_learner_train_multi_dev, libmz), Cint,
+                   (Ptr{Cvoid}, Int32, UInt32, Int32, Ptr{Float64}, Ptr{Float32}, Ptr{Float32}, Ptr{Cvoid}),
+                   e.h, B, step0, length(etas), etas, losses, C_NULL, C_NULL))
 
 """The actor–learner loop of self_play! ‖ learning! (src/SelfPlay.jl:384-419,
 src/Learning.jl:306-438; quirk Q16) on one GPU: `moves` self-play moves with the

@@ -75,6 +75,9 @@ SIGNATURES = {
     "mz_replay_sample": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.POINTER(MzBatch), _VP, _VP]),
     "mz_learner_grad_sampled_dev": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, _VP, _VP, _VP]),
     "mz_learner_train_dev": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.c_double, _VP, _VP]),
+    "mz_learner_train_multi_dev": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int32,
+                                                  ctypes.POINTER(ctypes.c_double), _VP, _VP, _VP]),
+    "mz_debug_unroll_step": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP]),
     "mz_replay_update_priorities": (ctypes.c_int, [_VP, _VP]),
     "mz_replay_get_priorities": (ctypes.c_int, [_VP, ctypes.c_int32, _VP, _VP]),
     "mz_replay_get_game": (ctypes.c_int, [_VP, ctypes.c_int32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
@@ -272,6 +275,15 @@ class Engine:
         self._check(self.lib.mz_debug_unroll(self.h, B, _p(pv), _p(pp), _p(pr)), "mz_debug_unroll")
         return pv, pp, pr
 
+    def debug_unroll_step(self, i, B):
+        """debug_unroll of step step0 + i of the last learner_train_multi_dev."""
+        K1 = self.conf.num_unroll_steps + 1
+        pv = np.empty((B, K1), np.float32)
+        pp = np.empty((B, K1, self.A), np.float32)
+        pr = np.empty((B, K1), np.float32)
+        self._check(self.lib.mz_debug_unroll_step(self.h, i, B, _p(pv), _p(pp), _p(pr)), "mz_debug_unroll_step")
+        return pv, pp, pr
+
     # ---- learner
     def learner_step(self, batch, eta):
         """batch: dict with observation (B, F), actions (B, K+1), target_values (B, K+1),
@@ -408,6 +420,15 @@ class Engine:
         """One GPU: replay_sample + learner_grad_dev + learner_apply_dev(scale 1) in two launches."""
         self._check(self.lib.mz_learner_train_dev(self.h, B, step, float(eta), losses_ptr, stream),
                     "mz_learner_train_dev")
+
+    def learner_train_multi_dev(self, B, step0, etas, losses_ptr=None, theta_ptr=None, stream=None):
+        """len(etas) consecutive learner_train_dev steps step0 .. step0+L-1 (ref_semantics FC: the ADAM
+        chain in one launch, the L unrolls + losses side by side in a second); losses_ptr: [L][8] floats,
+        theta_ptr: [L][nflat] floats (the parameters after each step), both optional device pointers."""
+        e = np.ascontiguousarray(etas, dtype=np.float64)
+        self._check(self.lib.mz_learner_train_multi_dev(self.h, B, step0, e.size,
+                                                        e.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                                        losses_ptr, theta_ptr, stream), "mz_learner_train_multi_dev")
 
     # ---- data-parallel learner over RCCL through the C ABI (SURVEY §8e)
     @staticmethod

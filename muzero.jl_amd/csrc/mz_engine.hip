@@ -79,6 +79,9 @@ extern "C" __global__ void mz_unroll_small1(SmallUnrollParams P);
 extern "C" __global__ void mz_unroll_small2(SmallUnrollParams P);
 extern "C" __global__ void mz_learn_small1(SmallUnrollParams P, LearnParams L);
 extern "C" __global__ void mz_learn_small2(SmallUnrollParams P, LearnParams L);
+extern "C" __global__ void mz_learn_chain(ChainParams C);
+extern "C" __global__ void mz_learn_multi1(SmallUnrollParams P, LearnMultiParams M);
+extern "C" __global__ void mz_learn_multi2(SmallUnrollParams P, LearnMultiParams M);
 extern "C" __global__ void mz_search_kernel_hbm_res(SearchParams P);
 
 extern "C" __global__ void mz_unroll_kernel(UnrollParams P);
@@ -209,6 +212,7 @@ struct mz_handle {
     char* d_tree = nullptr; size_t tree_game_bytes = 0; bool lds_tree = false; int dump_tree = 0;
     int time_nets = 0;                      // mz_debug_enable flag 2: events around each ResNet nets launch
     int time_unroll = 0;                    // flag 4: events around each ResNet learner unroll launch
+                                            // (and each mz_learn_multi* launch)
     std::vector<hipEvent_t> tev; size_t tev_used = 0;
     bool use_res = false;                   // register-resident sim-plan kernel
     // small-batch kernel (mz_small.hip): schedule images + LDS layout
@@ -287,6 +291,17 @@ struct mz_handle {
     int pf_cap = 0, pf_cur = 0;
     long long* d_pf_hdr = nullptr;          // [2][4]
     long long pf_epoch = 1;
+    // L learner steps per launch pair (mz_learner_train_multi_dev, ChainParams): the bank of
+    // MZ_MULTI_MAX small-kernel images (θ_t .. θ_{t+L-1}), per-step batches, read-outs,
+    // loss terms, Σθ² partials, fold counters and losses, for batches up to ml_cap
+    float* d_bank_w = nullptr; float* d_bank_b = nullptr;
+    int ml_cap = 0, ml_cap_L = 0, ml_last_B = 0, ml_last_L = 0;
+    float *d_ml_obs = nullptr, *d_ml_act = nullptr, *d_ml_tv = nullptr, *d_ml_tr = nullptr, *d_ml_tp = nullptr,
+          *d_ml_gs = nullptr, *d_ml_pv = nullptr, *d_ml_pp = nullptr, *d_ml_pr = nullptr, *d_ml_terms = nullptr,
+          *d_ml_out = nullptr;
+    int32_t* d_ml_index = nullptr;
+    double* d_ml_part = nullptr;
+    unsigned* d_ml_cnt = nullptr;
     // actor–learner loop (mz_train_*): the actors' weight set (flat + the
     // search images), the queued nets (remote_NNs, flat), the learner step t
     struct WSet { float* flat = nullptr; float* Wp = nullptr; float* Bp = nullptr; float* smw = nullptr;
@@ -361,10 +376,14 @@ static int check_fault(mz_handle* h) {
     MZ_TRY(h, hipMemcpy(&v, h->d_fault, 4, hipMemcpyDeviceToHost));
     if (!v) return 0;
     MZ_TRY(h, hipMemset(h->d_fault, 0, 4));
-    std::string m = "device fault: a workgroup waited 2 s for a publish that never came (";
+    char wait[32];
+    std::snprintf(wait, sizeof(wait), "%.3g s", (double)h->poll_ticks / 1e8);   // the 100 MHz constant clock
+    std::string m = std::string("device fault: a workgroup waited ") + wait + " for a publish that never came (";
     if (v & MZ_FAULT_RS_TRUNK) m += "mz_rsearch_nets trunk hand-off ";
     if (v & MZ_FAULT_RD_PROGRESS) m += "mz_runroll_fused_r chain progress ";
-    h->err = m + "); the results of the launches since the last synchronisation are invalid";
+    h->err = m + "); the results of the launches since the last synchronisation are invalid (search results, "
+                 "games self-play stored from them, losses, read-outs; the ref_semantics weights and ADAM state "
+                 "do not read them and stay valid)";
     return -1;
 }
 
@@ -1599,10 +1618,11 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
     if (h->small_ok) {
         CK(al(&h->d_Wp2, h->packed_w_n)); CK(al(&h->d_Bp2, h->packed_b_n));
         CK(al(&h->d_sm_w2, h->sm_w_n)); CK(al(&h->d_sm_bias2, h->sm_b_n));
-        const void* kl[2] = {(const void*)mz_learn_small1, (const void*)mz_learn_small2};
-        for (int ti = 0; ti < 2; ++ti)
+        const void* kl[4] = {(const void*)mz_learn_small1, (const void*)mz_learn_small2,
+                             (const void*)mz_learn_multi1, (const void*)mz_learn_multi2};
+        for (int ti = 0; ti < 4; ++ti)
             CK(hipFuncSetAttribute(kl[ti], hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)unroll_small_lds(h, ti)) == hipSuccess
+                                   (int)unroll_small_lds(h, ti & 1)) == hipSuccess
                    ? 0 : fail(h, "hipFuncSetAttribute(learn_small)"));
     }
     CK(hipMemset(h->d_flat, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
@@ -2194,15 +2214,18 @@ static int fc_unroll(mz_handle* h, const mz_batch* b, hipStream_t st, const RpSa
     return 0;
 }
 
+// the small unroll holds the nets with T = ti + 1 samples per workgroup
+static bool small_unroll_fits(const mz_handle* h, int ti) {
+    const int K = h->conf.num_unroll_steps, A = h->A;
+    // one item per thread in the unroll's per-step loops; a/|A| staging of 64 floats
+    return h->small_ok && (ti + 1) * h->H <= 256 && (ti + 1) * h->plane <= 256 &&
+           (ti + 1) * (A + 2) <= SM_THREADS && (ti + 1) * (K + 1) <= 64 &&
+           (ti + 1) * h->obs_feat <= SM_THREADS;                // one observation item per thread (setup)
+}
 // T = 2 when B exceeds 4 samples per CU; -1 if the small unroll cannot hold the nets
 static int small_unroll_ti(const mz_handle* h, int B) {
-    const int K = h->conf.num_unroll_steps, A = h->A;
     const int ti_u = B <= 4 * h->n_cu ? 0 : 1;         // (two per workgroup at B = 32: 29.5 k vs 34.0 k steps/s)
-    // one item per thread in the unroll's per-step loops; a/|A| staging of 64 floats
-    const bool ok = h->small_ok && (ti_u + 1) * h->H <= 256 && (ti_u + 1) * h->plane <= 256 &&
-                    (ti_u + 1) * (A + 2) <= SM_THREADS && (ti_u + 1) * (K + 1) <= 64 &&
-                    (ti_u + 1) * h->obs_feat <= SM_THREADS;      // one observation item per thread (setup)
-    return ok ? ti_u : -1;
+    return small_unroll_fits(h, ti_u) ? ti_u : -1;
 }
 
 // parameters of mz_unroll_small* / mz_learn_small* for batch b (T = ti + 1
@@ -2384,7 +2407,9 @@ static int build_bp(mz_handle* h) {
         for (const BpApp& a : apps) slot = std::max(slot, rows16(a.out));
         const size_t sched = (size_t)na * sizeof(BpApp) + (fun.size() + bun.size()) * sizeof(int2) +
                              (size_t)(2 * (nfl + nbl) + 8) * sizeof(int);
-        const int nslot = (int)std::min<size_t>(64, (kLdsMax - sched - 64) / ((size_t)slot * 4));
+        // (a schedule that leaves no room for the cache runs without it, not with a wrapped count)
+        const int nslot = sched + 64 < kLdsMax
+                              ? (int)std::min<size_t>(64, (kLdsMax - sched - 64) / ((size_t)slot * 4)) : 0;
         cache_floats = nslot * slot;
         std::vector<int> free_s;
         for (int i = nslot - 1; i >= 0; --i) free_s.push_back(i * slot);
@@ -3566,6 +3591,179 @@ int mz_learner_train_dev(mz_handle* h, int32_t B, uint32_t step, double eta, flo
     return learner_sampled(h, B, step, nullptr, losses_dev, stream ? (hipStream_t)stream : h->stream, true, eta);
 }
 
+// ---- L consecutive ref_semantics learner steps (ChainParams, mz_small_params.h;
+// Learning.jl:327-404 with get_batch keyed by the step, Q11).  The L steps run
+// as sub-chunks of up to MZ_MULTI_MAX steps, each one chain launch (the ADAM
+// iterations) and one unroll launch, in stream order.  (Measured: the next
+// sub-chunk's chain on a second stream, ordered by events, beside the unroll
+// launch — 228.8 k vs 279.5 k steps/s at L = 64, 114.6 k vs ~170 k at L = 8:
+// the cross-stream event waits cost more than the chain they hide.)
+static bool multi_ok(const mz_handle* h) {
+    return h->kind == 0 && h->learn_mode == MZ_LEARN_REF_SEMANTICS && !h->conf.PER && h->small_ok && h->A <= 16 &&
+           h->d_sm_w2 && !std::getenv("MZ_NO_MULTI");
+}
+// Sub-chunk length Ls and T per workgroup for L steps of B samples: one sample
+// per workgroup while the L·B workgroups fit one per CU; else two, with as
+// many steps per sub-chunk as keep one workgroup per CU (16 at B = 32)
+static int multi_plan(const mz_handle* h, int B, int L, int* Ls) {
+    static const int force = std::getenv("MZ_MULTI_T") ? std::atoi(std::getenv("MZ_MULTI_T")) : 0;   // tests / A/B
+    static const int ls_env = std::getenv("MZ_MULTI_LS") ? std::atoi(std::getenv("MZ_MULTI_LS")) : 0;
+    int ti;
+    if ((force == 1 || force == 2) && small_unroll_fits(h, force - 1)) ti = force - 1;
+    else if ((size_t)L * B <= (size_t)h->n_cu && small_unroll_fits(h, 0)) ti = 0;
+    else if (small_unroll_fits(h, 1)) ti = 1;
+    else if (small_unroll_fits(h, 0)) ti = 0;
+    else return -1;
+    const int nU = (B + ti) / (ti + 1);
+    int ls = std::max(1, std::min(MZ_MULTI_MAX, h->n_cu / nU));
+    if (ls_env > 0) ls = std::min(MZ_MULTI_MAX, ls_env);
+    *Ls = std::min(ls, L);
+    return ti;
+}
+static int ensure_multi(mz_handle* h, int B, int L) {
+    if (!h->d_bank_w) {
+        // two halves of MZ_MULTI_MAX images: sub-chunk k writes half k mod 2 (a chain launch
+        // never writes the images an unroll launch still in flight reads)
+        MZ_TRY(h, dalloc(h, &h->d_bank_w, (size_t)2 * MZ_MULTI_MAX * h->sm_w_n));
+        MZ_TRY(h, dalloc(h, &h->d_bank_b, (size_t)2 * MZ_MULTI_MAX * h->sm_b_n));
+        // the positions no parameter maps to (zero chunks, unused rows) as in the
+        // engine's images; every mapped position is rewritten by each chain launch
+        for (int i = 0; i < 2 * MZ_MULTI_MAX; ++i) {
+            MZ_TRY(h, hipMemcpy(h->d_bank_w + (size_t)i * h->sm_w_n, h->d_sm_w, h->sm_w_n * 4, hipMemcpyDeviceToDevice));
+            MZ_TRY(h, hipMemcpy(h->d_bank_b + (size_t)i * h->sm_b_n, h->d_sm_bias, h->sm_b_n * 4,
+                                hipMemcpyDeviceToDevice));
+        }
+    }
+    if (B <= h->ml_cap && L <= h->ml_cap_L) return 0;
+    const int cb = std::max(B, h->ml_cap), cl = std::max(L, h->ml_cap_L);
+    const size_t K1 = (size_t)h->conf.num_unroll_steps + 1, A = (size_t)h->A, n = (size_t)cl * cb;
+    MZ_TRY(h, dalloc(h, &h->d_ml_obs, n * h->obs_feat));
+    MZ_TRY(h, dalloc(h, &h->d_ml_act, n * K1)); MZ_TRY(h, dalloc(h, &h->d_ml_tv, n * K1));
+    MZ_TRY(h, dalloc(h, &h->d_ml_tr, n * K1)); MZ_TRY(h, dalloc(h, &h->d_ml_tp, n * K1 * A));
+    MZ_TRY(h, dalloc(h, &h->d_ml_gs, n)); MZ_TRY(h, dalloc(h, &h->d_ml_index, 2 * n));
+    MZ_TRY(h, dalloc(h, &h->d_ml_pv, n * K1)); MZ_TRY(h, dalloc(h, &h->d_ml_pp, n * K1 * A));
+    MZ_TRY(h, dalloc(h, &h->d_ml_pr, n * K1)); MZ_TRY(h, dalloc(h, &h->d_ml_terms, 2 * n * K1));
+    MZ_TRY(h, dalloc(h, &h->d_ml_part, (size_t)cl * 3 * MZ_L2_BLOCKS));
+    MZ_TRY(h, dalloc(h, &h->d_ml_cnt, (size_t)cl * MZ_MULTI_CNT_STRIDE));
+    MZ_TRY(h, hipMemset(h->d_ml_cnt, 0, (size_t)cl * MZ_MULTI_CNT_STRIDE * 4));
+    MZ_TRY(h, dalloc(h, &h->d_ml_out, (size_t)cl * 8));
+    h->ml_cap = cb; h->ml_cap_L = cl;
+    return 0;
+}
+
+// out_last: also (instead of losses[L-1]) the last step's losses there (mz_train_run)
+static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, const double* eta, float* losses_dev,
+                         float* theta_dev, hipStream_t st, float* out_last = nullptr) {
+    MZ_TRY(h, hipSetDevice(h->device));
+    int Ls = 0;
+    const int ti = multi_ok(h) ? multi_plan(h, B, L, &Ls) : -1;
+    if (ti < 0) {
+        // the same L steps one launch each (ResNet, the corrected mode, PER, wide nets)
+        for (int i = 0; i < L; ++i) {
+            float* lo = losses_dev ? losses_dev + 8 * i : (i == L - 1 ? out_last : nullptr);
+            if (learner_sampled(h, B, step0 + (uint32_t)i, nullptr, lo, st, true, eta[i])) return -1;
+            if (i == L - 1 && out_last && losses_dev)
+                MZ_TRY(h, hipMemcpyAsync(out_last, lo, 8 * 4, hipMemcpyDeviceToDevice, st));
+            if (theta_dev)
+                MZ_TRY(h, hipMemcpyAsync(theta_dev + (size_t)i * h->nflat, h->d_flat, h->nflat * 4,
+                                         hipMemcpyDeviceToDevice, st));
+        }
+        return 0;
+    }
+    RpSampleParams Q;
+    mz_batch b;
+    if (rs_params(h, B, step0, st, &Q, &b, true)) return -1;   // (the shard; set 0 is not touched)
+    if (ensure_batch(h, B) || ensure_multi(h, B, L)) return -1;
+    const size_t K1 = (size_t)h->conf.num_unroll_steps + 1, A = (size_t)h->A;
+    const size_t s_obs = (size_t)B * h->obs_feat, s_k1 = (size_t)B * K1, s_tp = (size_t)B * K1 * A;
+    Q.obs = h->d_ml_obs; Q.actions = h->d_ml_act; Q.tv = h->d_ml_tv; Q.tr = h->d_ml_tr; Q.tpol = h->d_ml_tp;
+    Q.gscale = h->d_ml_gs; Q.index = h->d_ml_index;
+    static const bool chain_sample = std::getenv("MZ_MULTI_CHAIN_SAMPLE") != nullptr;   // A/B
+    SmallUnrollParams U;
+    if (small_unroll_params(h, &b, ti, nullptr, &U)) return -1;
+    const int T = ti + 1, nU = (B + T - 1) / T;
+    static const bool no_xcd = std::getenv("MZ_MULTI_NO_XCD") != nullptr;
+    double p1 = h->bp1, p2 = h->bp2;
+    for (int k = 0, i0 = 0; i0 < L; ++k, i0 += Ls) {
+        const int n = std::min(Ls, L - i0), half = k & 1;
+        // 1. the ADAM chain θ_{t+i0} .. θ_{t+i0+n} into bank half k mod 2
+        ChainParams C;
+        std::memset(&C, 0, sizeof(C));
+        C.L = n; C.flat = h->d_flat; C.M = h->d_m; C.V = h->d_v; C.netoff = h->d_netoff;
+        C.inv_tile = h->d_inv_tile; C.inv_small = h->d_inv_small;
+        C.Wp = h->d_Wp; C.Bp = h->d_Bp; C.smw = h->d_sm_w; C.smb = h->d_sm_bias;
+        C.bank_w = h->d_bank_w + (size_t)half * MZ_MULTI_MAX * h->sm_w_n;
+        C.bank_b = h->d_bank_b + (size_t)half * MZ_MULTI_MAX * h->sm_b_n;
+        C.bws = h->sm_w_n; C.bbs = h->sm_b_n;
+        C.theta = theta_dev ? theta_dev + (size_t)i0 * h->nflat : nullptr;
+        C.nflat = h->nflat; C.part = h->d_ml_part + (size_t)i0 * 3 * MZ_L2_BLOCKS;
+        for (int i = 0; i < n; ++i) {               // adam_advance's products, step by step
+            C.bp1[i] = p1; C.bp2[i] = p2; C.eta[i] = eta[i0 + i];
+            p1 = p1 * 0.9; p2 = p2 * 0.999;
+        }
+        RpSampleParams Qk = Q;                      // this sub-chunk's batches: steps step0 + i0 ..
+        Qk.step = step0 + (uint32_t)i0;
+        Qk.obs += i0 * s_obs; Qk.actions += i0 * s_k1; Qk.tv += i0 * s_k1; Qk.tr += i0 * s_k1;
+        Qk.tpol += i0 * s_tp; Qk.gscale += (size_t)i0 * B; Qk.index += (size_t)i0 * 2 * B;
+        C.B = B; C.q = Qk; C.s_obs = s_obs; C.s_k1 = s_k1; C.s_tp = s_tp;
+        const int nsb = chain_sample ? (n * B + MZ_THREADS / 64 - 1) / (MZ_THREADS / 64) : 0;
+        hipLaunchKernelGGL(mz_learn_chain, dim3(3 * MZ_L2_BLOCKS + nsb), dim3(MZ_THREADS), 0, st, C);
+        MZ_TRY(h, hipGetLastError());
+        // 2. the n unrolls (with their get_batch), loss terms and per-step folds
+        LearnMultiParams M;
+        std::memset(&M, 0, sizeof(M));
+        M.L = n; M.nU = nU;
+        M.xcd = !no_xcd && n > 1;
+        M.bank_w = C.bank_w; M.bank_b = C.bank_b; M.bws = h->sm_w_n; M.bbs = h->sm_b_n;
+        M.s_obs = s_obs; M.s_k1 = s_k1; M.s_tp = s_tp;
+        M.obs = Qk.obs; M.act = Qk.actions; M.tv = Qk.tv; M.tp = Qk.tpol; M.gs = Qk.gscale;
+        M.pv = h->d_ml_pv + i0 * s_k1; M.pp = h->d_ml_pp + i0 * s_tp; M.pr = h->d_ml_pr + i0 * s_k1;
+        M.terms = h->d_ml_terms + 2 * i0 * s_k1;
+        M.part = C.part; M.counter = h->d_ml_cnt + (size_t)i0 * MZ_MULTI_CNT_STRIDE;
+        M.out = (losses_dev ? losses_dev : h->d_ml_out) + 8 * i0;
+        M.out_last = i0 + n == L ? out_last : nullptr;
+        M.sample = chain_sample ? 0 : 1;
+        M.q = Qk;
+        const int grid = M.xcd ? 8 * ((n + 7) / 8) * nU : n * nU;
+        void* args[] = {&U, &M};
+        hipEvent_t e0 = nullptr, e1 = nullptr;     // mz_debug_enable flag 4: the unroll launch's duration
+        if (h->time_unroll) {
+            if (timing_events(h, &e0, &e1)) return -1;
+            MZ_TRY(h, hipEventRecord(e0, st));
+        }
+        MZ_TRY(h, hipLaunchKernel(ti == 0 ? (const void*)mz_learn_multi1 : (const void*)mz_learn_multi2, dim3(grid),
+                                  dim3(SM_THREADS), args, unroll_small_lds(h, ti), st));
+        if (e1) MZ_TRY(h, hipEventRecord(e1, st));
+    }
+    h->last_lvariant = ti == 0 ? "mz_learn_chain+mz_learn_multi1" : "mz_learn_chain+mz_learn_multi2";
+    for (int i = 0; i < L; ++i) adam_advance(h);
+    h->ml_last_B = B; h->ml_last_L = L;
+    return 0;
+}
+
+int mz_learner_train_multi_dev(mz_handle* h, int32_t B, uint32_t step0, int32_t L, const double* eta,
+                               float* losses_dev, float* theta_dev, void* stream) {
+    if (!h) return -2;
+    if (L < 1 || L > MZ_MULTI_LMAX) return fail(h, "L must be in 1 .. 256");
+    if (!eta) return fail(h, "eta: one learning rate per step");
+    if (B < 1) return fail(h, "batch_size must be >= 1");
+    return learner_multi(h, B, step0, L, eta, losses_dev, theta_dev, stream ? (hipStream_t)stream : h->stream);
+}
+
+int mz_debug_unroll_step(mz_handle* h, int i, int B, float* values, float* policies, float* rewards) {
+    if (!h) return -2;
+    if (i < 0 || i >= h->ml_last_L || B < 0 || B > h->ml_last_B)
+        return fail(h, "no such step / batch in the last mz_learner_train_multi_dev");
+    MZ_TRY(h, hipSetDevice(h->device));
+    MZ_SYNC(h);
+    const size_t K1 = (size_t)h->conf.num_unroll_steps + 1, A = (size_t)h->A, s = (size_t)h->ml_last_B * K1;
+    const size_t n = (size_t)B * K1;
+    if (values) MZ_TRY(h, hipMemcpy(values, h->d_ml_pv + i * s, n * 4, hipMemcpyDeviceToHost));
+    if (policies) MZ_TRY(h, hipMemcpy(policies, h->d_ml_pp + i * s * A, n * A * 4, hipMemcpyDeviceToHost));
+    if (rewards) MZ_TRY(h, hipMemcpy(rewards, h->d_ml_pr + i * s, n * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
 int mz_replay_get_game(mz_handle* h, int32_t i, int32_t* T, uint8_t* obs, int32_t* actions, float* rewards,
                        int32_t* to_play, float* child_visits, float* root_values) {
     if (!h) return -2;
@@ -3595,6 +3793,8 @@ int mz_replay_get_game(mz_handle* h, int32_t i, int32_t* T, uint8_t* obs, int32_
 int mz_selfplay_slots(mz_handle* h, int32_t* history_len, uint8_t* board, int32_t* player) {
     if (!h) return -2;
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
+    if (h->sp_reset_pending)       // the initial games are keyed by the first move's game_offset
+        return fail(h, "the Atari-like env draws its initial games at the first mz_selfplay_move");
     MZ_TRY(h, hipSetDevice(h->device));
     MZ_SYNC(h);
     const size_t G = (size_t)h->sp_G;
@@ -3699,18 +3899,38 @@ int mz_train_run(mz_handle* h, int32_t moves, uint32_t move0, uint32_t game_offs
         wset_swap(h, h->tr_actor);
         if (rc) return rc;
         // 2. games saved this move (save_game in slot order, inside the move)
+        // (the fault word rides along: one stream wait per move, no second blocking copy)
         MZ_TRY(h, hipMemcpyAsync(h->h_tr_cnt, h->d_sp_counters, sizeof(long long), hipMemcpyDeviceToHost, st));
+        h->h_tr_cnt[1] = 0;
+        if (h->d_fault) MZ_TRY(h, hipMemcpyAsync(h->h_tr_cnt + 1, h->d_fault, 4, hipMemcpyDeviceToHost, st));
         MZ_TRY(h, hipStreamSynchronize(st));
-        if (check_fault(h)) return -1;
+        if (h->h_tr_cnt[1] && check_fault(h)) return -1;
         const int64_t nfin = h->h_tr_cnt[0] - h->tr_games;
         h->tr_games = h->h_tr_cnt[0];
         // 3. one learner step per saved game while t <= training_steps (Learning.jl:327),
-        //    get_batch keyed by the step number, eta = Cos(step)
-        for (int64_t k = 0; k < nfin && h->tr_t <= h->conf.training_steps; ++k) {
-            const int64_t t = h->tr_t + 1;
-            if (mz_learner_train_dev(h, h->tr_B, (uint32_t)t, cos_schedule(t), losses_dev, st)) return -1;
+        //    get_batch keyed by the step number, eta = Cos(step).  The shard does not change
+        //    between them, so consecutive steps up to the next checkpoint run as one
+        //    mz_learner_train_multi_dev chunk (results identical to one call per step)
+        static const int chunk_env = std::getenv("MZ_TRAIN_L") ? std::atoi(std::getenv("MZ_TRAIN_L")) : 0;
+        const int chunk_max = std::max(1, std::min(MZ_MULTI_MAX, chunk_env > 0 ? chunk_env : MZ_MULTI_MAX));
+        for (int64_t k = 0; k < nfin && h->tr_t <= h->conf.training_steps;) {
+            const int64_t t0 = h->tr_t + 1, ci = h->conf.checkpoint_interval;
+            int64_t tb = (t0 + ci - 1) / ci * ci;              // the chunk ends at the next refresh step
+            if (tb <= 1) tb += ci;                              // (t % ci == 0 && t > 1)
+            const int64_t n = std::min<int64_t>({nfin - k, (int64_t)h->conf.training_steps + 1 - h->tr_t,
+                                                 tb - t0 + 1, (int64_t)chunk_max});
+            const int64_t t = t0 + n - 1;
+            if (n == 1) {
+                if (mz_learner_train_dev(h, h->tr_B, (uint32_t)t, cos_schedule(t), losses_dev, st)) return -1;
+            } else {
+                double eta[MZ_MULTI_MAX];
+                for (int64_t i = 0; i < n; ++i) eta[i] = cos_schedule(t0 + i);
+                if (learner_multi(h, h->tr_B, (uint32_t)t0, (int32_t)n, eta, nullptr, nullptr, st, losses_dev))
+                    return -1;
+            }
             h->tr_t = t;
-            ++steps;
+            steps += n;
+            k += n;
             // 4. checkpoint: the actors take the queued nets, the learner's nets are queued
             //    (SelfPlay.jl:399-401 / Learning.jl:416-418: one checkpoint behind)
             if (t % h->conf.checkpoint_interval == 0 && t > 1) {
@@ -3752,8 +3972,10 @@ int mz_train_weights_get(mz_handle* h, int which, int net, float* flat, size_t n
 int mz_sync(mz_handle* h) {
     if (!h) return -2;
     MZ_TRY(h, hipSetDevice(h->device));
-    MZ_TRY(h, hipStreamSynchronize(h->stream));
-    return check_fault(h);
+    // every stream `_dev` work may have gone to (the device, or the narrowed pair of
+    // mz_set_sync_stream), so a fault of work queued on a caller stream is reported here
+    MZ_SYNC(h);
+    return 0;
 }
 
 }  // extern "C"

@@ -64,6 +64,17 @@ __device__ __forceinline__ void adam_update4(const LgAdam& ad, float* P, size_t 
         mz_scatter(xn, is[u], ad.smw, ad.smb);
     }
 }
+// One ADAM step of one parameter with ∇ = 2x (Q11): lg_adam_store's arithmetic
+// in the same order (the multi-step chain, mz_learn_chain)
+__device__ __forceinline__ float adam_2theta(float x, float& m, float& v, double bp1, double bp2, double eta) {
+    const double b1 = 0.9, b2 = 0.999, eps = 1e-8;
+    const float g = x * 2.0f;
+    m = (float)(b1 * (double)m + (1.0 - b1) * (double)g);
+    const float g2 = g * g;
+    v = (float)(b2 * (double)v + (1.0 - b2) * (double)g2);
+    const float d = (float)((double)m / (1.0 - bp1) / (sqrt((double)v / (1.0 - bp2)) + eps) * eta);
+    return x - d;
+}
 __device__ __forceinline__ void adam_update(const LgAdam& ad, float* P, size_t i, float g) {
     const double b1 = 0.9, b2 = 0.999, eps = 1e-8;
     const float m = (float)(b1 * (double)ad.M[i] + (1.0 - b1) * (double)g);
@@ -214,8 +225,10 @@ __device__ __forceinline__ void lg_tree256(double* red, int tid) {
 // counter.  Returns without work in every other block.  out: [0] value, [1]
 // reward (0, intermediate_rewards = false), [2] policy, [3..5] Σθ² of repr /
 // pred / dyn.
+// nblk: the blocks that count on `counter` (0: the whole grid).
 __device__ __forceinline__ void lg_fold(int B, int K, const float* vsq, const float* cet, const float* gscale,
-                                        const float* wts, const double* part, unsigned* counter, float* out) {
+                                        const float* wts, const double* part, unsigned* counter, float* out,
+                                        unsigned nblk = 0) {
     __shared__ bool last;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // the block's fold inputs (loss terms, Σθ² partial) are agent-scope stores,
@@ -225,7 +238,8 @@ __device__ __forceinline__ void lg_fold(int B, int K, const float* vsq, const fl
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0)
-        last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+        last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (nblk ? nblk : gridDim.x) - 1;
     __syncthreads();
     if (!last) return;
     __threadfence();

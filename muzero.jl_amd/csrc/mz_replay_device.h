@@ -186,7 +186,9 @@ __device__ __forceinline__ void rp_sample_one(const RpSampleParams& Q, int b, in
                     pos, Q.osz, Q.P, Q.stacked, lane);
     if (lane == 0) {
         const int gs = T + 1 - pos;                                // :212 min(K, len(action_history)+1-pos)
-        Q.gscale[b] = (float)(Q.K < gs ? Q.K : gs);
+        // write-through (agent scope): the fold of a learner launch that draws its
+        // batch in place reads every sample's gradient_scale from another workgroup
+        __hip_atomic_store(Q.gscale + b, (float)(Q.K < gs ? Q.K : gs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         Q.index[2 * b] = (int)num;
         Q.index[2 * b + 1] = pos;
     }

@@ -536,8 +536,19 @@ extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_search_small4(Sma
 // of step i, pr at 0 = 0.  Policy = softmax of the logits in the oracle's
 // order; value / reward with their read-out activations — applied by the
 // loss kernel, which visits every (sample, step) pair in parallel.
+// The per-call arrays of one unroll: the batch, the raw read-outs and the
+// weight image (the one-step kernels pass P's own, sm_io; the multi-step
+// kernel its step's batch set and bank image)
+struct SmIO {
+    const float* obs; const float* actions; float* pv; float* pp; float* pr;
+    const float* w_sim; const float* w_root; const float* bias;
+};
+__device__ __forceinline__ SmIO sm_io(const SmallUnrollParams& P) {
+    return SmIO{P.obs, P.actions, P.pv, P.pp, P.pr, P.w_sim, P.w_root, P.bias};
+}
+
 template <int T>
-__device__ __forceinline__ void unroll_body(const SmallUnrollParams& P, int lb) {
+__device__ __forceinline__ void unroll_body(const SmallUnrollParams& P, int lb, const SmIO& io) {
 #ifdef MZ_STAMPS
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long st_last = __builtin_amdgcn_s_memtime();
@@ -573,21 +584,21 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P, int lb) 
         const int ic = i < nri ? i : 0;
         const int4 r = reinterpret_cast<const int4*>(P.rec)[ic];
         rx[u] = r.x; ry[u] = r.y; rz[u] = r.z;
-        bv[u] = P.bias[ic];
+        bv[u] = io.bias[ic];
     }
     const int o_i = tid / P.obs_feat, o_k = tid - o_i * P.obs_feat;   // observation item: tid < T*obs_feat
     const int a_i = tid / (K + 1), a_k = tid - a_i * (K + 1);        // action item: tid < T*(K+1)
     const bool o_in = tid < T * P.obs_feat && tile0 + o_i < P.B, a_in = tid < T * (K + 1) && tile0 + a_i < P.B;
-    float ov = o_in ? P.obs[(size_t)(tile0 + o_i) * P.obs_feat + o_k] : 0.0f;
-    float av = a_in ? P.actions[(size_t)(tile0 + a_i) * (K + 1) + a_k] : 0.0f;
+    float ov = o_in ? io.obs[(size_t)(tile0 + o_i) * P.obs_feat + o_k] : 0.0f;
+    float av = a_in ? io.actions[(size_t)(tile0 + a_i) * (K + 1) + a_k] : 0.0f;
     float wr[SM_MAX_SIM][16];
     // the representation runs on register sets RO.. (RO + n_root), so the first
     // RO sim stages are loaded now and step 1 starts on them while the sets
     // the representation used are reloaded (no exposed reload)
     constexpr int RO = SM_MAX_SIM - SM_MAX_ROOT;
-    sm_load<SM_MAX_SIM, RO>(0, P.n_root, P.w_root, wr, P.nzm + P.n_sim, P.zero16);
-    sm_load<SM_MAX_SIM>(0, RO < P.n_sim ? RO : P.n_sim, P.w_sim, wr, P.nzm, P.zero16);
-    sm_load<SM_MAX_SIM>(RO + P.n_root, P.n_sim, P.w_sim, wr, P.nzm, P.zero16);
+    sm_load<SM_MAX_SIM, RO>(0, P.n_root, io.w_root, wr, P.nzm + P.n_sim, P.zero16);
+    sm_load<SM_MAX_SIM>(0, RO < P.n_sim ? RO : P.n_sim, io.w_sim, wr, P.nzm, P.zero16);
+    sm_load<SM_MAX_SIM>(RO + P.n_root, P.n_sim, io.w_sim, wr, P.nzm, P.zero16);
     // a prefetched batch (the previous launch sampled this step's) is used
     // while its header still matches the shard; otherwise (the first step after
     // the shard changed) waves 0..T-1 sample in place and the batch is re-read
@@ -597,8 +608,8 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P, int lb) 
         if ((tid >> 6) < T && tile0 + (tid >> 6) < P.B) rp_sample_one(P.rp, tile0 + (tid >> 6), tid & 63);
         __threadfence_block();
         __syncthreads();
-        ov = o_in ? P.obs[(size_t)(tile0 + o_i) * P.obs_feat + o_k] : 0.0f;
-        av = a_in ? P.actions[(size_t)(tile0 + a_i) * (K + 1) + a_k] : 0.0f;
+        ov = o_in ? io.obs[(size_t)(tile0 + o_i) * P.obs_feat + o_k] : 0.0f;
+        av = a_in ? io.actions[(size_t)(tile0 + a_i) * (K + 1) + a_k] : 0.0f;
     }
     for (int i = tid; i < P.act_total; i += SM_THREADS) act[i] = 0.0f;
 #pragma unroll
@@ -608,7 +619,7 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P, int lb) 
     }
     if (tid < SM_REC_INTS / 4) reinterpret_cast<int4*>(rec)[nri + tid] = make_int4(0, 0, -1, 0);   // slack stage
     if (P.bn)
-        for (int i = tid; i < nri; i += SM_THREADS) bnl[i] = make_float2(P.bias[nri + i], P.bias[2 * nri + i]);
+        for (int i = tid; i < nri; i += SM_THREADS) bnl[i] = make_float2(io.bias[nri + i], io.bias[2 * nri + i]);
     __syncthreads();                               // act zeroed before the inputs land in it
     if (o_in) act[P.x_rep + o_k * T + o_i] = ov;
     if (a_in) aval[a_i * (K + 1) + a_k] = av / (float)A;           // make_dynamics_input's a/|A| (:294)
@@ -621,7 +632,7 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P, int lb) 
     sm_run<T, SM_MAX_SIM, 0, RO>(P.n_root, wr, rec_root, act, nullptr, bn_root);
     SM_STAMP(1);                                   // repr stages
     // reload the representation's sets; in flight under step 1's first RO stages
-    sm_load<SM_MAX_SIM>(RO, RO + P.n_root < P.n_sim ? RO + P.n_root : P.n_sim, P.w_sim, wr, P.nzm, P.zero16);
+    sm_load<SM_MAX_SIM>(RO, RO + P.n_root < P.n_sim ? RO + P.n_root : P.n_sim, io.w_sim, wr, P.nzm, P.zero16);
     SM_STAMP(2);                                   // sim reload (issue only)
     for (int i = 1; i <= K; ++i) {
         // make_dynamics_input (:293-304) fused into the first stage: it reads
@@ -642,16 +653,16 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P, int lb) 
             float* dst0 = nullptr;
             if (c < A) {
                 x = act[P.p_out + c * T + gl];
-                dst = P.pp + ((size_t)bb * (K + 1) + i) * A + c;
-                if (i == 1) dst0 = P.pp + ((size_t)bb * (K + 1)) * A + c;
+                dst = io.pp + ((size_t)bb * (K + 1) + i) * A + c;
+                if (i == 1) dst0 = io.pp + ((size_t)bb * (K + 1)) * A + c;
             } else if (c == A) {
                 x = act[P.v_out + gl];
-                dst = P.pv + (size_t)bb * (K + 1) + i;
-                if (i == 1) dst0 = P.pv + (size_t)bb * (K + 1);
+                dst = io.pv + (size_t)bb * (K + 1) + i;
+                if (i == 1) dst0 = io.pv + (size_t)bb * (K + 1);
             } else {
                 x = act[P.r_out + gl];
-                dst = P.pr + (size_t)bb * (K + 1) + i;
-                if (i == 1) P.pr[(size_t)bb * (K + 1)] = 0.0f;   // raw 0: every read-out maps 0 to 0
+                dst = io.pr + (size_t)bb * (K + 1) + i;
+                if (i == 1) io.pr[(size_t)bb * (K + 1)] = 0.0f;   // raw 0: every read-out maps 0 to 0
             }
             *dst = x;
             if (dst0) *dst0 = x;
@@ -666,8 +677,8 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P, int lb) 
 #endif
 }
 
-extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small1(SmallUnrollParams P) { unroll_body<1>(P, blockIdx.x); }
-extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small2(SmallUnrollParams P) { unroll_body<2>(P, blockIdx.x); }
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small1(SmallUnrollParams P) { unroll_body<1>(P, blockIdx.x, sm_io(P)); }
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small2(SmallUnrollParams P) { unroll_body<2>(P, blockIdx.x, sm_io(P)); }
 
 // One learner iteration in one launch (LearnParams): unroll (+ get_batch) and
 // each tile's loss terms ‖ Σθ² + ADAM into the second image set; last block
@@ -691,7 +702,7 @@ __device__ __forceinline__ void learn_body(const SmallUnrollParams& P, const Lea
     const int pb = (int)blockIdx.x;
     const int lb = L.xcd ? ((pb & 7) == 0 ? pb >> 3 : L.nU + pb - (pb >> 3) - 1) : pb;
     if (lb < L.nU) {
-        unroll_body<T>(P, lb);
+        unroll_body<T>(P, lb, sm_io(P));
 #ifdef MZ_STAMPS
         const unsigned long long t_unroll = __builtin_amdgcn_s_memtime();
 #endif
@@ -746,3 +757,124 @@ extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_small2(Smal
     learn_body<2>(P, L);
 }
 
+
+// ------------------------------------------------ L learner steps per launch pair
+// (ChainParams / LearnMultiParams, mz_small_params.h)
+// mz_learn_chain: blocks [0, 3·MZ_L2_BLOCKS) are lg_l2_slice's slices (net, blk):
+// each thread runs its parameters' L ADAM iterations (∇ = 2θ, Q11) in registers
+// and keeps one Σθ_{t+i}² per step in lg_l2_slice's order; the per-step trees
+// are lg_tree256's, level by level.  The blocks after them draw the L batches.
+// At most 112 VGPRs: one wave per SIMD fits beside a resident mz_learn_multi*
+// workgroup (2 waves x 197 of the 512), so the next sub-chunk's chain runs on
+// the CUs the unroll launch occupies (learner_multi's two streams).
+extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learn_chain(ChainParams C) {
+    // per step i: this thread's Σθ_{t+i}² (accumulated in place: no register
+    // array, so one wave per SIMD fits beside a resident mz_learn_multi*
+    // workgroup and the next sub-chunk's chain runs under the unroll launch)
+    __shared__ double red[MZ_MULTI_MAX][MZ_THREADS];
+    __shared__ double sbp[3][MZ_MULTI_MAX];         // β1^t, β2^t, η of step t+i
+    const int tid = threadIdx.x, blk = (int)blockIdx.x;
+    constexpr int NSL = 3 * MZ_L2_BLOCKS;
+    const int L = C.L;
+    if (blk >= NSL) {                               // get_batch of step t+i, sample b (ReplayBuffer.jl:188-217)
+        const int q = (blk - NSL) * (MZ_THREADS / 64) + (tid >> 6);
+        if (q >= L * C.B) return;
+        const int i = q / C.B, b = q - i * C.B;
+        RpSampleParams Q = C.q;
+        Q.step += (uint32_t)i;
+        Q.obs += i * C.s_obs; Q.actions += i * C.s_k1; Q.tv += i * C.s_k1; Q.tr += i * C.s_k1;
+        Q.tpol += i * C.s_tp; Q.gscale += (size_t)i * C.B; Q.index += (size_t)i * 2 * C.B;
+        rp_sample_one(Q, b, tid & 63);
+        return;
+    }
+    if (tid < MZ_MULTI_MAX) { sbp[0][tid] = C.bp1[tid]; sbp[1][tid] = C.bp2[tid]; sbp[2][tid] = C.eta[tid]; }
+    for (int i = 0; i < L; ++i) red[i][tid] = 0.0;
+    __syncthreads();
+    const int net = blk / MZ_L2_BLOCKS, sb = blk - net * MZ_L2_BLOCKS;
+    const size_t off = C.netoff[net], cnt = C.netoff[3 + net];
+    const size_t stride = (size_t)MZ_L2_BLOCKS * MZ_THREADS;
+    for (size_t e = (size_t)sb * MZ_THREADS + tid; e < cnt; e += stride) {
+        const size_t p = off + e;
+        float x = C.flat[p], m = C.M[p], v = C.V[p];
+        const int it = C.inv_tile[p], is = C.inv_small[p];
+        float* bw = C.bank_w;
+        float* bb = C.bank_b;
+        float* th = C.theta ? C.theta + p : nullptr;
+        for (int i = 0; i < L; ++i) {
+            red[i][tid] += (double)x * (double)x;                   // step t+i's Σθ² reads θ_{t+i}
+#ifndef MZ_DBG_NO_BANK   // diagnostic only (wrong results): the chain without the bank scatter
+            mz_scatter(x, is, bw, bb);
+#endif
+            x = adam_2theta(x, m, v, sbp[0][i], sbp[1][i], sbp[2][i]);   // Learning.jl:395-397
+            if (th) { *th = x; th += C.nflat; }
+            bw += C.bws; bb += C.bbs;
+        }
+        C.flat[p] = x; C.M[p] = m; C.V[p] = v;
+        mz_scatter(x, it, C.Wp, C.Bp);
+        mz_scatter(x, is, C.smw, C.smb);
+    }
+    __syncthreads();
+    for (int o = MZ_THREADS / 2; o > 0; o >>= 1) {   // lg_tree256, per step
+        if (tid < o)
+            for (int i = 0; i < L; ++i) red[i][tid] += red[i][tid + o];
+        __syncthreads();
+    }
+    if (tid < L) C.part[(size_t)tid * NSL + blk] = red[tid][0];
+}
+
+// mz_learn_multi{1,2}: workgroup (step i, tile lb).  With M.xcd, step i's
+// workgroups are the physical blocks on XCD i mod 8 (round-robin dispatch), so
+// each XCD's L2 holds its steps' bank images only.
+template <int T>
+__device__ __forceinline__ void learn_multi_body(const SmallUnrollParams& P, const LearnMultiParams& M) {
+    __shared__ float stg[SM_THREADS];
+    const int tid = threadIdx.x, pb = (int)blockIdx.x;
+    int i, lb;
+    if (M.xcd) {
+        const int r = pb >> 3;
+        i = (pb & 7) + 8 * (r / M.nU);
+        lb = r % M.nU;
+    } else {
+        i = pb / M.nU;
+        lb = pb - i * M.nU;
+    }
+    if (i >= M.L) return;                           // (xcd grids round L up to a multiple of 8)
+    const int K1 = P.K + 1;
+    if (M.sample) {                                 // get_batch of step t+i (ReplayBuffer.jl:188-217), this tile
+        const int w = tid >> 6, b = lb * T + w;
+        if (w < T && b < P.B) {
+            RpSampleParams Q = M.q;
+            Q.step += (uint32_t)i;
+            Q.obs += i * M.s_obs; Q.actions += i * M.s_k1; Q.tv += i * M.s_k1; Q.tr += i * M.s_k1;
+            Q.tpol += i * M.s_tp; Q.gscale += (size_t)i * P.B; Q.index += (size_t)i * 2 * P.B;
+            rp_sample_one(Q, b, tid & 63);
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+    SmIO io;
+    io.obs = M.obs + i * M.s_obs; io.actions = M.act + i * M.s_k1;
+    io.pv = M.pv + i * M.s_k1; io.pp = M.pp + i * M.s_tp; io.pr = M.pr + i * M.s_k1;
+    io.w_sim = M.bank_w + i * M.bws;
+    io.w_root = io.w_sim + (size_t)P.n_sim * SM_SLOTS * 256 * 16;
+    io.bias = M.bank_b + i * M.bbs;
+    unroll_body<T>(P, lb, io);
+    __syncthreads();                                // the tile's raw outputs -> its loss groups
+    float* vsq = M.terms + 2 * i * M.s_k1;
+    float* cet = vsq + M.s_k1;
+    const int g16 = tid >> 4, a = tid & 15, gl = g16 / K1, k = g16 - gl * K1;
+    const int b = lb * T + gl;
+    if (gl < T && b < P.B)
+        lg_step_terms<16>(b * K1 + k, a, P.A, P.v_act, P.r_act, io.pv, io.pp, io.pr, M.tv + i * M.s_k1,
+                          M.tp + i * M.s_tp, vsq, cet, stg + (tid & ~15));
+    lg_fold(P.B, P.K, vsq, cet, M.gs + (size_t)i * P.B, nullptr, M.part + (size_t)i * 3 * MZ_L2_BLOCKS,
+            M.counter + i * MZ_MULTI_CNT_STRIDE, M.out_last && i == M.L - 1 ? M.out_last : M.out + 8 * i,
+            (unsigned)M.nU);
+}
+
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_multi1(SmallUnrollParams P, LearnMultiParams M) {
+    learn_multi_body<1>(P, M);
+}
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_multi2(SmallUnrollParams P, LearnMultiParams M) {
+    learn_multi_body<2>(P, M);
+}

@@ -126,6 +126,49 @@ struct LearnParams {
     long long* pf_hdr_next;
     long long pf_epoch;
 };
+// L consecutive ref_semantics learner steps t .. t+L-1 (mz_learner_train_multi_dev).
+// Q11: the update θ_{s+1} = ADAM(θ_s, ∇ = 2θ_s) is elementwise and does not
+// read the data, and with PER off step s's batch is keyed by s alone, so the L
+// unrolls and losses are independent once θ_t .. θ_{t+L-1} exist.  Two launches:
+//  * mz_learn_chain (256 threads): blocks [0, 3·MZ_L2_BLOCKS) run the L ADAM
+//    iterations of their Σθ² slice in registers — Σθ_{t+i}² of the slice per i
+//    (lg_l2_slice's order), θ_{t+i} scattered into bank image i, θ_{t+L} into
+//    flat / M / V and the engine's current images;
+//  * mz_learn_multi{1,2} (SM_THREADS): the L·⌈B/T⌉ unroll workgroups, each on
+//    its step's bank image: waves 0..T-1 first draw the workgroup's samples of
+//    step t+i (get_batch keyed by the step, one wave per sample), then the
+//    unroll and the loss terms; the last workgroup of step i folds step i's
+//    losses with the chain launch's Σθ² partials.  (MZ_MULTI_CHAIN_SAMPLE=1:
+//    the chain launch draws the L batches in blocks after its slices instead.)
+#define MZ_MULTI_MAX 16           // steps per sub-chunk (one chain + one unroll launch)
+#define MZ_MULTI_LMAX 256         // steps per mz_learner_train_multi_dev call
+#define MZ_MULTI_CNT_STRIDE 32   // per-step fold counters on their own 128-byte lines
+struct ChainParams {
+    int L;
+    float* flat; float* M; float* V; const size_t* netoff;
+    const int* inv_tile; const int* inv_small;
+    float* Wp; float* Bp; float* smw; float* smb;     // the current images: θ_{t+L}
+    float* bank_w; float* bank_b; size_t bws, bbs;     // bank image i (small-kernel W, bias): θ_{t+i}
+    float* theta;                                      // NULL or [L][nflat]: θ after step t+i
+    size_t nflat;
+    double* part;                                      // [L][3·MZ_L2_BLOCKS] Σθ_{t+i}² partials
+    double bp1[MZ_MULTI_MAX], bp2[MZ_MULTI_MAX], eta[MZ_MULTI_MAX];   // step t+i's β powers, learning rate
+    int B;                                             // batches: sample q = i·B + b, one wave each
+    RpSampleParams q;                                  // step t's get_batch; step i's arrays at + i·stride
+    size_t s_obs, s_k1, s_tp;                          // per-step strides: B·F, B·(K+1), B·(K+1)·A
+};
+struct LearnMultiParams {
+    int L, nU, xcd;                                    // xcd: step i on XCD i mod 8 (learn_multi_body)
+    const float* bank_w; const float* bank_b; size_t bws, bbs;
+    size_t s_obs, s_k1, s_tp;                          // as ChainParams (batch, read-outs, policies)
+    const float* obs; const float* act; const float* tv; const float* tp; const float* gs;
+    float* pv; float* pp; float* pr; float* terms;     // terms: [L][2·B·(K+1)]
+    const double* part; unsigned* counter; float* out; // [L][3·MZ_L2_BLOCKS], [L][MZ_MULTI_CNT_STRIDE], [L][8]
+    float* out_last;                                   // non-NULL: step L-1's losses go here instead (mz_train_run)
+    int sample;                                        // waves 0..T-1 draw their samples (else mz_learn_chain did)
+    RpSampleParams q;                                  // as ChainParams::q
+};
+
 // Σθ² / ADAM workgroups of the fused learner: 48 (each 256-thread half takes
 // every 96th of the 3·MZ_L2_BLOCKS slices in turn; measured: one slice per
 // half, 192 workgroups at 128 slices, ran 33.3 k vs 34.5 k steps/s at 48)

@@ -127,3 +127,18 @@ def test_atari_learner_steps():
         for n in range(3):
             assert np.array_equal(eng.get_weights(n), o.params[n]), f"step {t} net {n} params differ"
     eng.close()
+
+
+def test_atari_slots_before_first_move(at_eng):
+    """The Atari-like env keys its initial games by the first move's
+    game_offset, so the slots hold no games between mz_selfplay_init and the
+    first mz_selfplay_move: mz_selfplay_slots fails there instead of
+    returning zeroed slots, and works after the move."""
+    from muzero_jl_amd import abi
+    conf, hyper, o, eng, nets = at_eng
+    eng.selfplay_init(abi.ENV_ATARI, 4, 8)
+    with pytest.raises(abi.MzError, match="first mz_selfplay_move"):
+        eng.selfplay_slots()
+    eng.selfplay_move(0, game_offset=3)
+    ln, board, player = eng.selfplay_slots()
+    assert np.all(player == 1) and np.all(ln == 1)

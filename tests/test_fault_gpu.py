@@ -82,4 +82,15 @@ def test_fused_learner_progress_fault_reported(ttt, monkeypatch, skip):
     else:
         eng.sync()
         assert np.all(np.isfinite(out.cpu().numpy()[:6]))
+    # the faulted step's outputs are invalid, its weights are not: the ref_semantics
+    # ADAM step (∇ = 2θ, Q11) does not read the unroll — equal to a clean engine's step
+    ref = _engine(ttt, monkeypatch, False)
+    ref.selfplay_init(abi.ENV_TICTACTOE, 16, 64)
+    for m in range(12):
+        ref.selfplay_move(m)
+    ref.learner_train_dev(32, 1, 1e-4, out.data_ptr())
+    ref.sync()
+    for n in range(3):
+        assert np.array_equal(eng.get_weights(n), ref.get_weights(n)), n
+    ref.close()
     eng.close()
