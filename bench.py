@@ -552,7 +552,8 @@ def main():
                      "kernels": (("mz_rp_sample + mz_dsbp_fwd + mz_rbp_sample + mz_dsbp_bwd + mz_dsbp_dw + "
                                   "mz_rbp_dw + mz_bp_fold + mz_adam_kernel") if game is atari else
                                  "mz_rp_sample + mz_rbp_sample + mz_rbp_dw + mz_bp_fold + mz_adam_kernel"
-                                 if resnet else "mz_rp_sample + mz_bp_tile_lv + mz_bp_dw + mz_bp_fold + mz_adam_kernel")}
+                                 if resnet else "mz_rp_sample + mz_bp_tile_lv%s + mz_bp_dw + mz_bp_fold + mz_adam_kernel"
+                                 % ("" if hyper.use_batch_norm else "_nobn"))}
         eng.learner_set_mode(LEARN_REF_SEMANTICS)
         eng.sync()
         if world > 1:

@@ -32,18 +32,30 @@ __device__ __forceinline__ float bp_dz(int act, float g, float y) {
 // The epilogue of a dense unit's output row oo, sample m: t = W x + b; after a
 // make_dense BatchNorm (use_batch_norm, Learning.jl:70-78) t is kept in the
 // arena for mz_bp_dw and y = act(γ·(t/√(1+ε)) + β), else y = act(t)
+// BN: the app has a BatchNorm (P.bn_off >= 0), a compile-time choice so the
+// default nets' code carries no BatchNorm test or load (the level kernel
+// dispatches per application)
+template <bool BN>
 __device__ __forceinline__ float bp_epi(const BpApp& P, const float* __restrict__ flat, float* T, int oo, int m,
                                         float t) {
-    if (P.bn_off >= 0) {
+    if (BN) {
         T[P.z + oo * 16 + m] = t;
         t = mz_bn_apply(t, flat[P.bn_off + P.out + oo], flat[P.bn_off + oo]);
     }
     return bp_act(P.act, t);
 }
+__device__ __forceinline__ float bp_epi(const BpApp& P, const float* __restrict__ flat, float* T, int oo, int m,
+                                        float t) {
+    return P.bn_off >= 0 ? bp_epi<true>(P, flat, T, oo, m, t) : bp_epi<false>(P, flat, T, oo, m, t);
+}
 // ∂L/∂t of output row o: dY ⊙ act'(y), times γ/√(1+ε) after a BatchNorm
+template <bool BN>
 __device__ __forceinline__ float bp_dt(const BpApp& P, const float* __restrict__ flat, int o, float g, float y) {
     const float du = bp_dz(P.act, g, y);
-    return P.bn_off >= 0 ? du * (flat[P.bn_off + P.out + o] / MZ_BN_S) : du;
+    return BN ? du * (flat[P.bn_off + P.out + o] / MZ_BN_S) : du;
+}
+__device__ __forceinline__ float bp_dt(const BpApp& P, const float* __restrict__ flat, int o, float g, float y) {
+    return P.bn_off >= 0 ? bp_dt<true>(P, flat, o, g, y) : bp_dt<false>(P, flat, o, g, y);
 }
 
 // One 16-row block of a 16-sample MFMA GEMM, C[r][s] = Σ_k A(r, k) B(k, s),
@@ -296,6 +308,9 @@ __device__ __forceinline__ void bp_lv_run(const BpParams& Q, const BpApp& P, con
 // read from the cache copies where the host placed them, outputs written to the
 // arena and to their copy, ∂L/∂x accumulated in its copy (the first
 // contribution adds to 0, as into the zeroed arena)
+// MAYBN: the nets may hold BatchNorm layers (checked per application); false
+// compiles the check and its loads out (the kernel for nets without any)
+template <bool MAYBN>
 __device__ __forceinline__ void bp_c_fwd_blk(const BpApp& P, const float* __restrict__ flat, float* T, float* C,
                                              int ob) {
     const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
@@ -311,12 +326,14 @@ __device__ __forceinline__ void bp_c_fwd_blk(const BpApp& P, const float* __rest
     for (int r = 0; r < 4; ++r) {
         const int oo = ob * 16 + kq * 4 + r;
         if (oo < P.out) {
-            const float v = bp_epi(P, flat, T, oo, m, acc[r] + flat[P.b_off + oo]);
+            const float v = MAYBN ? bp_epi(P, flat, T, oo, m, acc[r] + flat[P.b_off + oo])
+                                  : bp_epi<false>(P, flat, T, oo, m, acc[r] + flat[P.b_off + oo]);
             T[P.y + oo * 16 + m] = v;
             if (P.ys >= 0) C[P.ys + oo * 16 + m] = v;
         }
     }
 }
+template <bool MAYBN>
 __device__ __forceinline__ void bp_c_dx_blk(const BpApp& P, const float* __restrict__ flat, const float* T, float* G,
                                             float* C, int ib) {
     const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
@@ -333,7 +350,7 @@ __device__ __forceinline__ void bp_c_dx_blk(const BpApp& P, const float* __restr
             if (o >= P.out) return 0.0f;
             const float g = DY[o * 16 + m];
             if (wout) G[P.y + o * 16 + m] = g;
-            return bp_dt(P, flat, o, g, Y[o * 16 + m]);
+            return MAYBN ? bp_dt(P, flat, o, g, Y[o * 16 + m]) : bp_dt<false>(P, flat, o, g, Y[o * 16 + m]);
         });
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -367,7 +384,7 @@ __device__ __forceinline__ void bp_c_concat(const BpParams& Q, const BpApp& P, f
     }
 }
 
-template <bool FWD>
+template <bool FWD, bool MAYBN = true>
 __device__ __forceinline__ void bp_lv_levels(const BpParams& Q, const BpApp* apps, const int2* units, const int* lev,
                                              int nlev, float* T, float* G, const int* sync = nullptr,
                                              float* C = nullptr) {
@@ -384,8 +401,8 @@ __device__ __forceinline__ void bp_lv_levels(const BpParams& Q, const BpApp* app
                 const int2 un = units[u];
                 const BpApp P = apps[un.x];
                 if (P.op == BP_DENSE) {
-                    if (FWD) bp_c_fwd_blk(P, Q.flat, T, C, un.y);
-                    else bp_c_dx_blk(P, Q.flat, T, G, C, un.y);
+                    if (FWD) bp_c_fwd_blk<MAYBN>(P, Q.flat, T, C, un.y);
+                    else bp_c_dx_blk<MAYBN>(P, Q.flat, T, G, C, un.y);
                 } else {
                     bp_c_concat(Q, P, T, G, C, FWD);
                 }
@@ -453,7 +470,8 @@ __device__ __forceinline__ void bp_lv_levels(const BpParams& Q, const BpApp* app
 #endif
 }
 
-extern "C" __global__ __launch_bounds__(BP_LV_THREADS) void mz_bp_tile_lv(BpParams Q) {
+template <bool MAYBN>
+__device__ __forceinline__ void bp_tile_lv_body(const BpParams& Q) {
     extern __shared__ __attribute__((aligned(16))) int bp_lds[];
     float* T = Q.act + (size_t)blockIdx.x * Q.tile_floats;
     float* G = Q.grad + (size_t)blockIdx.x * Q.tile_floats;
@@ -484,13 +502,13 @@ extern "C" __global__ __launch_bounds__(BP_LV_THREADS) void mz_bp_tile_lv(BpPara
     bp_prologue(Q, T, G, C);
     __syncthreads();
 #if BP_LV_LDS
-    bp_lv_levels<true>(Q, apps, fun, flev, Q.n_flev, T, G, fsy, C);
+    bp_lv_levels<true, MAYBN>(Q, apps, fun, flev, Q.n_flev, T, G, fsy, C);
     bp_heads(Q, T, G);
     __syncthreads();
 #ifdef MZ_STAMPS
     if (blockIdx.x == 0 && threadIdx.x == 0) Q.stamps[1] = __builtin_amdgcn_s_memtime();
 #endif
-    bp_lv_levels<false>(Q, apps, bun, blev, Q.n_blev, T, G, bsy, C);
+    bp_lv_levels<false, MAYBN>(Q, apps, bun, blev, Q.n_blev, T, G, bsy, C);
     if (Q.B < 0) Q.terms[threadIdx.x] = warm;                // never: keeps the warm-up loads
 #else   // descriptors by scalar loads (wave-uniform values straight into SGPRs)
     bp_lv_levels<true>(Q, Q.apps, Q.funits, Q.flev, Q.n_flev, T, G);
@@ -498,6 +516,12 @@ extern "C" __global__ __launch_bounds__(BP_LV_THREADS) void mz_bp_tile_lv(BpPara
     __syncthreads();
     bp_lv_levels<false>(Q, Q.apps, Q.bunits, Q.blev, Q.n_blev, T, G);
 #endif
+}
+
+extern "C" __global__ __launch_bounds__(BP_LV_THREADS) void mz_bp_tile_lv(BpParams Q) { bp_tile_lv_body<true>(Q); }
+// the same for nets without BatchNorm layers (use_batch_norm = false, the default)
+extern "C" __global__ __launch_bounds__(BP_LV_THREADS) void mz_bp_tile_lv_nobn(BpParams Q) {
+    bp_tile_lv_body<false>(Q);
 }
 
 // ---- heads: dL/dy of the value / policy / reward outputs, loss terms
@@ -539,48 +563,12 @@ __device__ void bp_heads(const BpParams& Q, float* T, float* G) {
     }
 }
 
-extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
-    const BpJob J = Q.jobs[blockIdx.x];
-    const BpLayer L = Q.layers[J.layer];
-    const int lane = threadIdx.x, m = lane & 15, kq = lane >> 4;
-    const bool bn = L.bn_off >= 0;
-    if (J.ib < 0) {                                           // db = Σ dT (data term); BatchNorm: dβ, dγ
-        const int o = J.ob * 16 + lane;
-        const bool in = lane < 16 && o < L.out;
-        double q = 0.0;
-        if (in) {
-            const float gr = bn ? Q.flat[L.bn_off + L.out + o] / MZ_BN_S : 1.0f;
-            float s = 0.0f, sbe = 0.0f, sga = 0.0f;
-            for (int t = 0; t < Q.tiles; ++t)
-                for (int u = 0; u < L.n_use; ++u) {
-                    const BpUse U = Q.uses[L.use0 + u];
-                    const size_t e = (size_t)t * Q.tile_floats + U.y + o * 16;
-                    for (int j = 0; j < 16; ++j) {
-                        const float du = bp_dz(L.act, Q.grad[e + j], Q.act[e + j]);
-                        s += bn ? du * gr : du;
-                        if (bn) {
-                            sbe += du;
-                            sga += du * (Q.act[(size_t)t * Q.tile_floats + U.z + o * 16 + j] / MZ_BN_S);
-                        }
-                    }
-                }
-            const float th = Q.flat[L.b_off + o];
-            Q.out[L.b_off + o] = s;                               // data term (2θ: mz_adam_kernel)
-            q = (double)th * (double)th;
-            if (bn) {
-                const float be = Q.flat[L.bn_off + o], ga = Q.flat[L.bn_off + L.out + o];
-                Q.out[L.bn_off + o] = sbe;
-                Q.out[L.bn_off + L.out + o] = sga;
-                q += (double)be * (double)be + (double)ga * (double)ga;
-            }
-        }
-        for (int d = 32; d > 0; d >>= 1) q += __shfl_xor(q, d);    // fixed tree: Σθ² of the block
-        if (lane == 0) Q.sq[blockIdx.x] = q;
-        return;
-    }
-    const int o = J.ob * 16 + m, i = J.ib * 16 + m;
-    const bool oin = o < L.out, iin = i < L.in;
-    const float gr = bn && oin ? Q.flat[L.bn_off + L.out + o] / MZ_BN_S : 1.0f;
+// Σ over tiles, applications and samples of dZ ⊗ x for one 16x16 dW block
+// (BN: dZ ⊙ γ/√(1+ε); compile-time, so the default nets' loop has no factor)
+template <bool BN>
+__device__ __forceinline__ bp_f32x4 bp_dw_acc(const BpDwParams& Q, const BpLayer& L, int o, int i, bool oin, bool iin,
+                                              int kq) {
+    const float gr = BN && oin ? Q.flat[L.bn_off + L.out + o] / MZ_BN_S : 1.0f;
     bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int t = 0; t < Q.tiles; ++t) {
         const float* gt = Q.grad + (size_t)t * Q.tile_floats;
@@ -590,12 +578,75 @@ extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
 #pragma unroll
             for (int c = 0; c < 4; ++c) {                     // K = the 16 samples, 4 per MFMA
                 const int e = U.y + o * 16 + 4 * c + kq;
-                const float a = oin ? bp_dz(L.act, gt[e], at[e]) * gr : 0.0f;
+                const float dz = oin ? bp_dz(L.act, gt[e], at[e]) : 0.0f;
+                const float a = BN ? dz * gr : dz;
                 const float b = iin ? at[U.x + i * 16 + 4 * c + kq] : 0.0f;
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
             }
         }
     }
+    return acc;
+}
+
+// db of output row o (one lane): Σ over tiles, applications and the 16 samples
+// of dT in that order (16 contiguous floats per application: their loads are
+// issued together, then the ordered sum); BatchNorm: also dβ, dγ.  Writes the
+// data terms, returns the rows' θ² (bias, β, γ).
+template <bool BN>
+__device__ __forceinline__ double bp_db(const BpDwParams& Q, const BpLayer& L, int o) {
+    const float gr = BN ? Q.flat[L.bn_off + L.out + o] / MZ_BN_S : 1.0f;
+    float s = 0.0f, sbe = 0.0f, sga = 0.0f;
+    for (int t = 0; t < Q.tiles; ++t)
+        for (int u = 0; u < L.n_use; ++u) {
+            const BpUse U = Q.uses[L.use0 + u];
+            const size_t e = (size_t)t * Q.tile_floats + U.y + o * 16;
+            const size_t ez = (size_t)t * Q.tile_floats + U.z + o * 16;
+            float g[16], y[16], z[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                g[j] = Q.grad[e + j];
+                y[j] = Q.act[e + j];
+                z[j] = BN ? Q.act[ez + j] : 0.0f;
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const float du = bp_dz(L.act, g[j], y[j]);
+                s += BN ? du * gr : du;
+                if (BN) {
+                    sbe += du;
+                    sga += du * (z[j] / MZ_BN_S);
+                }
+            }
+        }
+    const float th = Q.flat[L.b_off + o];
+    Q.out[L.b_off + o] = s;                                   // data term (2θ: mz_adam_kernel)
+    double q = (double)th * (double)th;
+    if (BN) {
+        const float be = Q.flat[L.bn_off + o], ga = Q.flat[L.bn_off + L.out + o];
+        Q.out[L.bn_off + o] = sbe;
+        Q.out[L.bn_off + L.out + o] = sga;
+        q += (double)be * (double)be + (double)ga * (double)ga;
+    }
+    return q;
+}
+
+extern "C" __global__ __launch_bounds__(64) void mz_bp_dw(BpDwParams Q) {
+    const BpJob J = Q.jobs[blockIdx.x];
+    const BpLayer L = Q.layers[J.layer];
+    const int lane = threadIdx.x, m = lane & 15, kq = lane >> 4;
+    const bool bn = L.bn_off >= 0;
+    if (J.ib < 0) {                                           // db = Σ dT (data term); BatchNorm: dβ, dγ
+        const int o = J.ob * 16 + lane;
+        const bool in = lane < 16 && o < L.out;
+        double q = 0.0;
+        if (in) q = bn ? bp_db<true>(Q, L, o) : bp_db<false>(Q, L, o);
+        for (int d = 32; d > 0; d >>= 1) q += __shfl_xor(q, d);    // fixed tree: Σθ² of the block
+        if (lane == 0) Q.sq[blockIdx.x] = q;
+        return;
+    }
+    const int o = J.ob * 16 + m, i = J.ib * 16 + m;
+    const bool oin = o < L.out, iin = i < L.in;
+    const bp_f32x4 acc = bn ? bp_dw_acc<true>(Q, L, o, i, oin, iin, kq) : bp_dw_acc<false>(Q, L, o, i, oin, iin, kq);
     double q = 0.0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {

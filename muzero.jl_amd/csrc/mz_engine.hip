@@ -46,6 +46,7 @@ extern "C" __global__ void mz_runroll_kernel(RUnrollParams U);
 extern "C" __global__ void mz_runroll_chain(RUnrollParams U);
 extern "C" __global__ void mz_bp_tile(BpParams Q);
 extern "C" __global__ void mz_bp_tile_lv(BpParams Q);
+extern "C" __global__ void mz_bp_tile_lv_nobn(BpParams Q);
 extern "C" __global__ void mz_bp_dw(BpDwParams Q);
 extern "C" __global__ void mz_rbp_sample(RbpParams Q);
 extern "C" __global__ void mz_rbp_dw(RbpDwParams Q);
@@ -1237,6 +1238,7 @@ static size_t ds_build(mz_handle* h, DsPlan& D) {
         L.woff = (int)n; n += (size_t)kw * kh * cin * cout;
         L.boff = (int)n; n += (size_t)cout;
         if (bn) { L.bnoff = (int)n; n += (size_t)2 * cout; }
+        L.pn = (int)(n - (size_t)L.woff);
         D.w_floats = std::max(D.w_floats, kw * kh * cin * cout);
         w = L.Wo; hh = L.Ho;
         return L;
@@ -1277,7 +1279,18 @@ static size_t ds_build(mz_handle* h, DsPlan& D) {
     h->rconf = c;
     h->rconf.observation_shape[0] = w; h->rconf.observation_shape[1] = hh; h->rconf.observation_shape[2] = 2 * C;
     h->rconf.stacked_observations = 0;
-    h->ds_lds = ((size_t)2 * D.buf_floats + D.w_floats + 512) * 4;
+    // LDS: buffer 0 | buffer 1 (from buf_floats; the staged observation for layer 0 when it fits, layer 0
+    // writing buffer 0) | one conv's packed parameters | the generic conv's weights and tap tables
+    for (int i = 0; i < D.n; ++i) D.pn_max = std::max(D.pn_max, D.L[i].pn);
+    D.pn_max = (D.pn_max + 3) & ~3;
+    const size_t gen = (size_t)D.pn_max + D.w_floats + 512;
+    const size_t in4 = ((size_t)D.in_feat + 3) & ~(size_t)3;
+    D.ptot = (int)(n - (size_t)D.L[0].woff);
+    D.stage_in = D.L[0].kind == DS_CONV && D.L[0].in_buf < 0 && D.L[0].out_buf == 0 && D.in_feat % 4 == 0 &&
+                 D.L[0].woff % 4 == 0 && (size_t)2 * D.buf_floats + D.ptot <= in4 &&
+                 ((size_t)D.buf_floats + std::max<size_t>(D.buf_floats, in4) + gen) * 4 <= kLdsMax;
+    D.lds_floats = (int)((size_t)D.buf_floats + (D.stage_in ? std::max<size_t>(D.buf_floats, in4) : D.buf_floats));
+    h->ds_lds = ((size_t)D.lds_floats + gen) * 4;
     return n;
 }
 
@@ -1285,6 +1298,11 @@ static size_t ds_build(mz_handle* h, DsPlan& D) {
 static int ds_launch(mz_handle* h, const float* x, float* y, int n, hipStream_t st) {
     DsParams Q;
     Q.n_items = n; Q.bn_s = h->bn_s; Q.plan = h->d_dsplan; Q.flat = h->d_flat; Q.x = x; Q.y = y;
+    Q.stamps = nullptr;
+#ifdef MZ_STAMPS
+    if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * std::max(h->max_games, 128)));
+    Q.stamps = h->d_stamps;
+#endif
     void* args[] = {&Q};
     MZ_TRY(h, hipLaunchKernel((const void*)mz_downsample_kernel, dim3(n), dim3(DS_THREADS), args, h->ds_lds, st));
     return 0;
@@ -2509,6 +2527,8 @@ static int build_bp(mz_handle* h) {
                           (size_t)(2 * (nfl + nbl) + 8) * sizeof(int) + 16 + (size_t)cache_floats * 4;
         if (lv > kLdsMax) return fail(h, "corrected learner: the level schedule exceeds the LDS");
         MZ_TRY(h, hipFuncSetAttribute((const void*)mz_bp_tile_lv, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lv));
+        MZ_TRY(h, hipFuncSetAttribute((const void*)mz_bp_tile_lv_nobn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lv));
     }
     h->bp_n_flev = nfl; h->bp_n_blev = nbl; h->bp_n_funit = (int)fun.size(); h->bp_n_bunit = (int)bun.size();
     h->bp_n_app = (int)apps.size(); h->bp_n_head = (int)heads.size(); h->bp_n_job = (int)jobs.size();
@@ -2855,7 +2875,9 @@ static int bp_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float* loss
     // the level schedule (default) or the one-application-per-barrier kernel
     // (MZ_BP_SEQ=1, the same bits: tests/test_corrected_learner_gpu.py)
     if (std::getenv("MZ_BP_SEQ")) hipLaunchKernelGGL(mz_bp_tile, dim3(tiles), dim3(256), 0, st, Q);
-    else if (lv_lds <= kLdsMax) hipLaunchKernelGGL(mz_bp_tile_lv, dim3(tiles), dim3(BP_LV_THREADS), lv_lds, st, Q);
+    else if (lv_lds <= kLdsMax)                   // (no BatchNorm layer: the kernel without its per-layer test)
+        hipLaunchKernelGGL(h->hp.use_batch_norm ? mz_bp_tile_lv : mz_bp_tile_lv_nobn, dim3(tiles), dim3(BP_LV_THREADS),
+                           lv_lds, st, Q);
     else return fail(h, "corrected learner: the level schedule exceeds the LDS");
     BpDwParams D;
     D.tiles = tiles; D.tile_floats = h->bp_tile_floats; D.n_job = h->bp_n_job; D.jobs = h->d_bp_jobs;

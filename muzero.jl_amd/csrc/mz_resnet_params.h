@@ -243,7 +243,7 @@ struct RUnrollParams {
 // (84, 84, C) observation to (6, 6, 2C), which the representation's tail
 // (conv 2C -> nf + blocks, an RPlan) reads.  One workgroup per item; the
 // activations ping-pong between two LDS buffers [c][h][w] (the column-major
-// (W, H, C) order), the first layer reads the observation from HBM.
+// (W, H, C) order); the observation is staged in LDS for the first layer.
 #define DS_MAX_LAYERS 32
 #define DS_THREADS 512
 enum { DS_CONV = 0, DS_POOL = 1 };
@@ -254,6 +254,7 @@ struct DsLayer {
     int woff, boff, bnoff;   // absolute offsets in the flat parameters (conv)
     int in_buf, out_buf;     // LDS buffer 0 / 1, or -1 = the observation (in) / the output (out)
     int res_buf;             // residual buffer (res_add)
+    int pn;                  // conv: its parameters W, b (, β, γ) contiguous from woff (pn floats); pool: 0
 };
 struct DsPlan {
     int n;
@@ -261,6 +262,13 @@ struct DsPlan {
     int buf_floats;          // floats per activation buffer
     int w_floats;            // largest conv weight block (K x cout)
     int in_feat, out_feat;   // W*H*C of the observation / of the output
+    // mz_downsample_kernel's LDS beyond the two buffers: the observation staged
+    // for layer 0 (stage_in: from buf_floats, where buffer 1 starts, over
+    // in_feat floats); after layer 0 every conv's parameters (W, b, β, γ,
+    // contiguous from L[0].woff over ptot floats) at 2·buf_floats, inside the
+    // staging region; layer 0's own at lds_floats (pn_max floats)
+    int stage_in, pn_max, ptot;
+    int lds_floats;          // buffers + staging region
 };
 struct DsParams {
     int n_items;
@@ -269,6 +277,7 @@ struct DsParams {
     const float* flat;
     const float* x;          // (in_feat, n_items) column-major
     float* y;                // (out_feat, n_items)
+    unsigned long long* stamps;   // -DMZ_STAMPS builds: item 0's s_memtime at each layer's end (else unused)
 };
 
 // ---- the corrected learner through the downsampler (mz_dsbp_*, mz_downsample.hip)
