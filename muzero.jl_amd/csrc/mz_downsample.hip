@@ -114,6 +114,53 @@ __device__ __forceinline__ void ds_conv_mfma(const DsLayer& L, ds_lptr in, ds_lp
     }
 }
 
+// The same conv on the VALU, one thread per output position: its K taps loaded
+// once (branch-free), then all COUT outputs from them as the canonical four
+// k-quarter fmaf chains; the weights are wave-uniform LDS reads (broadcasts).
+// For the 4-channel layers, whose MFMA tiles would be 3/4 padding rows.
+template <int CIN, int COUT, int S>
+__device__ __forceinline__ void ds_conv_valu(const DsLayer& L, ds_lptr in, ds_lptr out, ds_lptr res, ds_lptr pw,
+                                             float bn_s) {
+    constexpr int K = 9 * CIN, KQ = 4 * ((K + 15) / 16);
+    const int Wi = L.Wi, Hi = L.Hi, Wo = L.Wo, Po = Wo * L.Ho, Pi = Wi * Hi;
+    const bool bn = L.bn != 0, relu = L.act == MZ_ACT_RELU, has_res = L.res_add != 0;
+    for (int p = threadIdx.x; p < Po; p += blockDim.x) {
+        asm volatile("" ::: "memory");                  // the weights re-read per position, not K·COUT live values
+        const int oh = p / Wo, ow = p - oh * Wo;
+        bool okx[3], oky[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {                   // tap i (j): dx (dy) = 1 - i (1 - j)
+            okx[t] = (unsigned)(S * ow + 1 - t) < (unsigned)Wi;
+            oky[t] = (unsigned)(S * oh + 1 - t) < (unsigned)Hi;
+        }
+        const int base = (S * oh) * Wi + S * ow;
+        float x[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int i = k % 3, j = (k / 3) % 3, c = k / 9;
+            const bool ok = okx[i] & oky[j];
+            const float v = in[ok ? base + c * Pi + (1 - j) * Wi + (1 - i) : 0];
+            x[k] = ok ? v : 0.0f;
+        }
+#pragma unroll
+        for (int co = 0; co < COUT; ++co) {
+            float part[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float acc = 0.0f;
+#pragma unroll
+                for (int k = q * KQ; k < (q + 1) * KQ && k < K; ++k) acc = __builtin_fmaf(pw[K * co + k], x[k], acc);
+                part[q] = acc;
+            }
+            float t = ((part[0] + part[1]) + (part[2] + part[3])) + pw[K * COUT + co];
+            if (bn) t = pw[K * COUT + 2 * COUT + co] * ((t - 0.0f) / bn_s) + pw[K * COUT + COUT + co];
+            const int o = co * Po + p;
+            if (has_res) t = t + res[o];
+            out[o] = relu ? mz_relu(t) : t;
+        }
+    }
+}
+
 // The generic layer (any kernel size / channel count): one thread per output,
 // the taps through the LDS offset tables kt / kd, the same canonical order
 __device__ __forceinline__ void ds_conv_generic(const DsLayer& L, const float* in, float* out, const float* res,
@@ -205,6 +252,7 @@ extern "C" __global__ __launch_bounds__(DS_THREADS) void mz_downsample_kernel(Ds
     const float* xg = Q.x + (size_t)item * D.in_feat;
     float* yg = Q.y + (size_t)item * D.out_feat;
     const int w0 = D.L[0].woff;
+    const float* flat = Q.per_step > 0 ? Q.flat + (size_t)(item / Q.per_step) * Q.flat_stride : Q.flat;
     // (LDS pointers as address-space-3 values: offset 0, buffer 0, is that
     // space's null, so nothing below tests them for null)
     const ds_lptr lb0 = (ds_lptr)buf[0], lb1 = (ds_lptr)buf[1];
@@ -215,7 +263,7 @@ extern "C" __global__ __launch_bounds__(DS_THREADS) void mz_downsample_kernel(Ds
         const float4* src = reinterpret_cast<const float4*>(xg);
         float4* dst = reinterpret_cast<float4*>(buf[1]);
         for (int i = tid; i < D.in_feat / 4; i += DS_THREADS) dst[i] = src[i];
-        for (int i = tid; i < D.L[0].pn; i += DS_THREADS) pwl[i] = Q.flat[w0 + i];
+        for (int i = tid; i < D.L[0].pn; i += DS_THREADS) pwl[i] = flat[w0 + i];
     }
     for (int li = 0; li < nl; ++li) {
         const DsLayer L = D.L[li];
@@ -223,7 +271,7 @@ extern "C" __global__ __launch_bounds__(DS_THREADS) void mz_downsample_kernel(Ds
         if (li == 1 && stage) {
             // the staged observation is consumed: every conv's parameters into its
             // region (one batch of loads, one wait), then the barrier
-            const float4* src = reinterpret_cast<const float4*>(Q.flat + w0);
+            const float4* src = reinterpret_cast<const float4*>(flat + w0);
             float4* dst = reinterpret_cast<float4*>(pall);
             for (int i = tid; i < (D.ptot + 3) / 4; i += DS_THREADS) dst[i] = src[i];
             __syncthreads();
@@ -236,23 +284,23 @@ extern "C" __global__ __launch_bounds__(DS_THREADS) void mz_downsample_kernel(Ds
         const ds_lptr resl = L.res_buf == 0 ? lb0 : lb1;
         (void)Pi; (void)Hi;
         if (L.kind == DS_CONV) {
-            // the 3x3 shapes of the configs[4] downsampler (4 -> 4 stride 2, 4 -> 4, 4 -> 8 stride 2,
-            // 8 -> 8; relu or identity), LDS to LDS, on MFMA; any other layer the generic way
+            // the 3x3 shapes of the configs[4] downsampler (4 -> 4 stride 2, 4 -> 4 on the VALU; 4 -> 8
+            // stride 2, 8 -> 8 on MFMA; relu or identity), LDS to LDS; any other layer the generic way
             const bool k3 = stage && L.out_buf >= 0 && L.kw == 3 && L.kh == 3 && L.pw == 1 &&
                             L.ph == 1 && (L.act == MZ_ACT_RELU || L.act == MZ_ACT_IDENTITY);
             const int sel = !k3 ? -1
                           : L.cin == 4 && L.cout == 4 ? (L.stride == 2 ? 0 : L.stride == 1 ? 1 : -1)
                           : L.cin == 4 && L.cout == 8 && L.stride == 2 ? 2
                           : L.cin == 8 && L.cout == 8 && L.stride == 1 ? 3 : -1;
-            if (sel == 0) ds_conv_mfma<4, 4, 2>(L, inl, outl, resl, lpw, Q.bn_s);
-            else if (sel == 1) ds_conv_mfma<4, 4, 1>(L, inl, outl, resl, lpw, Q.bn_s);
+            if (sel == 0) ds_conv_valu<4, 4, 2>(L, inl, outl, resl, lpw, Q.bn_s);
+            else if (sel == 1) ds_conv_valu<4, 4, 1>(L, inl, outl, resl, lpw, Q.bn_s);
             else if (sel == 2) ds_conv_mfma<4, 8, 2>(L, inl, outl, resl, lpw, Q.bn_s);
             else if (sel == 3) ds_conv_mfma<8, 8, 1>(L, inl, outl, resl, lpw, Q.bn_s);
             else {
                 const float* in = L.in_buf < 0 ? (stage ? buf[1] : xg) : buf[L.in_buf];
                 float* out = L.out_buf < 0 ? nullptr : buf[L.out_buf];
                 const float* res = L.res_add ? buf[L.res_buf] : nullptr;
-                ds_conv_generic(L, in, out, res, Q.flat, Q.bn_s, yg, wl, kt, kd);
+                ds_conv_generic(L, in, out, res, flat, Q.bn_s, yg, wl, kt, kd);
             }
         } else {
             ds_pool(L, inl, outl, yg);                       // (pools read an LDS buffer: never layer 0)

@@ -83,6 +83,8 @@ extern "C" __global__ void mz_learn_small2(SmallUnrollParams P, LearnParams L);
 extern "C" __global__ void mz_learn_chain(ChainParams C);
 extern "C" __global__ void mz_learn_multi1(SmallUnrollParams P, LearnMultiParams M);
 extern "C" __global__ void mz_learn_multi2(SmallUnrollParams P, LearnMultiParams M);
+extern "C" __global__ void mz_learner_loss_multi(LossMultiParams M);
+extern "C" __global__ void mz_learner_loss_multi32(LossMultiParams M);
 extern "C" __global__ void mz_search_kernel_hbm_res(SearchParams P);
 
 extern "C" __global__ void mz_unroll_kernel(UnrollParams P);
@@ -296,6 +298,12 @@ struct mz_handle {
     // MZ_MULTI_MAX small-kernel images (θ_t .. θ_{t+L-1}), per-step batches, read-outs,
     // loss terms, Σθ² partials, fold counters and losses, for batches up to ml_cap
     float* d_bank_w = nullptr; float* d_bank_b = nullptr;
+    // ResNet nets: the MFMA image bank (W, B), the flat-parameter bank, per-step unroll scratch (h, trunk
+    // outputs), progress words and downsampled batches
+    float* d_tbank_w = nullptr; float* d_tbank_b = nullptr; float* d_fbank = nullptr;
+    float* d_ml_hs = nullptr; float* d_ml_ts = nullptr; float* d_ml_dsb = nullptr;
+    unsigned long long* d_ml_prog = nullptr;
+    unsigned long long ml_prog_epoch = 0;   // multi-step fused launches (d_ml_prog's prog_base = epoch · 64)
     int ml_cap = 0, ml_cap_L = 0, ml_last_B = 0, ml_last_L = 0;
     float *d_ml_obs = nullptr, *d_ml_act = nullptr, *d_ml_tv = nullptr, *d_ml_tr = nullptr, *d_ml_tp = nullptr,
           *d_ml_gs = nullptr, *d_ml_pv = nullptr, *d_ml_pp = nullptr, *d_ml_pr = nullptr, *d_ml_terms = nullptr,
@@ -1294,11 +1302,16 @@ static size_t ds_build(mz_handle* h, DsPlan& D) {
     return n;
 }
 
-// run the downsampler over n items: x (in_feat, n) -> y (rin_feat, n)
-static int ds_launch(mz_handle* h, const float* x, float* y, int n, hipStream_t st) {
+// run the downsampler over n items: x (in_feat, n) -> y (rin_feat, n); with
+// per_step > 0 item i uses the parameters flat + (i / per_step)·nflat (the
+// multi-step learner's per-step bank), else the engine's
+static int ds_launch(mz_handle* h, const float* x, float* y, int n, hipStream_t st, const float* flat = nullptr,
+                     int per_step = 0) {
     DsParams Q;
     Q.n_items = n; Q.bn_s = h->bn_s; Q.plan = h->d_dsplan; Q.flat = h->d_flat; Q.x = x; Q.y = y;
     Q.stamps = nullptr;
+    Q.per_step = per_step; Q.flat_stride = h->nflat;
+    if (flat) Q.flat = flat;
 #ifdef MZ_STAMPS
     if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * std::max(h->max_games, 128)));
     Q.stamps = h->d_stamps;
@@ -2070,6 +2083,7 @@ static int rlearner_grad(mz_handle* h, const mz_batch* b, float* grad_dev, float
     if (ensure_batch(h, B)) return -1;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     RUnrollParams U;
+    std::memset(&U, 0, sizeof(U));                 // (ms = 0: one step; the fused-ADAM fields unused unless set)
     U.B = B; U.K = h->conf.num_unroll_steps; U.A = h->A; U.H = h->H;
     U.W = h->rconf.observation_shape[0]; U.P = h->plane; U.obs_feat = h->rin_feat; U.ng = h->rn_ng; U.bn_s = h->bn_s;
     U.obs = b->observation; U.actions = b->actions;
@@ -3643,7 +3657,20 @@ static int multi_plan(const mz_handle* h, int B, int L, int* Ls) {
     return ti;
 }
 static int ensure_multi(mz_handle* h, int B, int L) {
-    if (!h->d_bank_w) {
+    if (h->kind == 1 && !h->d_tbank_w) {
+        // the ResNet image bank: 2 halves of MZ_MULTI_MAX copies of the MFMA image (positions no parameter
+        // maps to as in the engine's image), the flat bank (θ of each step)
+        const size_t nw = h->packed_w_n, nb = std::max<size_t>(h->packed_b_n, 1);
+        MZ_TRY(h, dalloc(h, &h->d_tbank_w, (size_t)2 * MZ_MULTI_MAX * nw));
+        MZ_TRY(h, dalloc(h, &h->d_tbank_b, (size_t)2 * MZ_MULTI_MAX * nb));
+        MZ_TRY(h, dalloc(h, &h->d_fbank, (size_t)2 * MZ_MULTI_MAX * h->nflat));
+        for (int i = 0; i < 2 * MZ_MULTI_MAX; ++i) {
+            MZ_TRY(h, hipMemcpy(h->d_tbank_w + (size_t)i * nw, h->d_Wp, nw * 4, hipMemcpyDeviceToDevice));
+            if (h->packed_b_n)
+                MZ_TRY(h, hipMemcpy(h->d_tbank_b + (size_t)i * nb, h->d_Bp, nb * 4, hipMemcpyDeviceToDevice));
+        }
+    }
+    if (h->kind != 1 && !h->d_bank_w) {
         // two halves of MZ_MULTI_MAX images: sub-chunk k writes half k mod 2 (a chain launch
         // never writes the images an unroll launch still in flight reads)
         MZ_TRY(h, dalloc(h, &h->d_bank_w, (size_t)2 * MZ_MULTI_MAX * h->sm_w_n));
@@ -3669,7 +3696,160 @@ static int ensure_multi(mz_handle* h, int B, int L) {
     MZ_TRY(h, dalloc(h, &h->d_ml_cnt, (size_t)cl * MZ_MULTI_CNT_STRIDE));
     MZ_TRY(h, hipMemset(h->d_ml_cnt, 0, (size_t)cl * MZ_MULTI_CNT_STRIDE * 4));
     MZ_TRY(h, dalloc(h, &h->d_ml_out, (size_t)cl * 8));
+    if (h->kind == 1) {
+        const size_t KH = (size_t)std::max(h->conf.num_unroll_steps, 1);
+        MZ_TRY(h, dalloc(h, &h->d_ml_hs, n * KH * h->H)); MZ_TRY(h, dalloc(h, &h->d_ml_ts, n * KH * h->H));
+        MZ_TRY(h, dalloc(h, &h->d_ml_prog, n));
+        MZ_TRY(h, hipMemset(h->d_ml_prog, 0, n * sizeof(unsigned long long)));
+        h->ml_prog_epoch = 0;
+        if (h->ds) MZ_TRY(h, dalloc(h, &h->d_ml_dsb, n * h->rin_feat));
+    }
     h->ml_cap = cb; h->ml_cap_L = cl;
+    return 0;
+}
+
+// ResNet nets (ref_semantics, no PER): per sub-chunk of Ls steps, the chain launch (ADAM
+// iterations into the MFMA image bank and the flat bank, Σθ² per step, the Ls batches), the
+// downsampler over the Ls·B observations (Atari), the unroll launch(es) of rlearner_grad's
+// form with the steps on gridDim.z (the fused form: step-major chain blocks, then the items;
+// RUnrollParams.ms) and one loss launch of Ls·nlb blocks
+static bool rmulti_ok(const mz_handle* h) {
+    return h->kind == 1 && h->learn_mode == MZ_LEARN_REF_SEMANTICS && !h->conf.PER && !std::getenv("MZ_NO_MULTI") &&
+           !std::getenv("MZ_RUNROLL_FUSED");
+}
+static int ensure_multi(mz_handle* h, int B, int L);
+static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, const double* eta, float* losses_dev,
+                          float* theta_dev, hipStream_t st, float* out_last) {
+    RpSampleParams Q;
+    mz_batch b;
+    if (rs_params(h, B, step0, st, &Q, &b, true)) return -1;
+    if (ensure_batch(h, B) || ensure_multi(h, B, L)) return -1;
+    static const int ls_env = std::getenv("MZ_MULTI_LS") ? std::atoi(std::getenv("MZ_MULTI_LS")) : 0;
+    const int Ls = std::min(L, ls_env > 0 ? std::min(MZ_MULTI_MAX, ls_env) : MZ_MULTI_MAX);
+    const int K = h->conf.num_unroll_steps, KH = std::max(K, 1), A = h->A;
+    const size_t K1 = (size_t)K + 1;
+    const size_t s_obs = (size_t)B * h->obs_feat, s_k1 = (size_t)B * K1, s_tp = (size_t)B * K1 * A;
+    const size_t nw = h->packed_w_n, nb = std::max<size_t>(h->packed_b_n, 1);
+    Q.obs = h->d_ml_obs; Q.actions = h->d_ml_act; Q.tv = h->d_ml_tv; Q.tr = h->d_ml_tr; Q.tpol = h->d_ml_tp;
+    Q.gscale = h->d_ml_gs; Q.index = h->d_ml_index;
+    // rlearner_grad's form for one step of B samples
+    RUnrollParams U;
+    std::memset(&U, 0, sizeof(U));
+    U.B = B; U.K = K; U.A = A; U.H = h->H;
+    U.W = h->rconf.observation_shape[0]; U.P = h->plane; U.obs_feat = h->rin_feat; U.ng = h->rn_ng; U.bn_s = h->bn_s;
+    U.plans = h->d_rplan; U.plans_l = h->d_rplan_l; U.ng_l = h->rn_ng_l;
+    U.dyn_split = h->rn_dyn_split; U.otab = h->d_rtab;
+    U.rd_ep_off = (int)(h->rn_lds_l / 4); U.rd_trunk_nl = 1 + 2 * h->rhp.num_blocks;
+    U.rp_nv = 3 + h->rhp.depth_value;
+    U.fault = h->d_fault; U.poll_ticks = h->poll_ticks; U.dbg_skip = h->dbg_skip;
+    U.ms_wimg = nw; U.ms_flat = h->nflat; U.ms_obs = (size_t)B * (h->ds ? h->rin_feat : h->obs_feat);
+    U.ms_k1 = s_k1; U.ms_tp = s_tp; U.ms_hs = (size_t)B * KH * h->H;
+    static const bool wide_env = std::getenv("MZ_RN_PRED_WIDE") != nullptr;
+    static const bool no_fuse = std::getenv("MZ_RN_NO_FUSE") != nullptr;
+    static const bool nb3 = std::getenv("MZ_RN_CHAIN_NB3") != nullptr;
+    const bool wide_p = wide_env || (B * KH + U.ng - 1) / U.ng >= h->n_cu;
+    const bool fused = h->rd_chain && h->rp_pred && !wide_p && !no_fuse && U.ng_l == 1 && K + 1 < 64 && !h->ds;
+    const bool nb1 = (U.P * U.ng_l + 15) / 16 == 1 || !nb3;
+    const int gw = A > 16 ? 32 : 16;
+    const int nlb = (B * (int)K1 + MZ_THREADS / gw - 1) / (MZ_THREADS / gw);
+    double p1 = h->bp1, p2 = h->bp2;
+    for (int k = 0, i0 = 0; i0 < L; ++k, i0 += Ls) {
+        const int n = std::min(Ls, L - i0), half = k & 1;
+        ChainParams C;                              // 1. ADAM chain + the n batches
+        std::memset(&C, 0, sizeof(C));
+        C.L = n; C.flat = h->d_flat; C.M = h->d_m; C.V = h->d_v; C.netoff = h->d_netoff;
+        C.inv_tile = h->d_inv_tile; C.inv_small = h->d_inv_small;
+        C.Wp = h->d_Wp; C.Bp = h->d_Bp; C.smw = h->d_sm_w; C.smb = h->d_sm_bias;
+        C.tbank_w = h->d_tbank_w + (size_t)half * MZ_MULTI_MAX * nw;
+        C.tbank_b = h->d_tbank_b + (size_t)half * MZ_MULTI_MAX * nb;
+        C.tws = nw; C.tbs = nb;
+        C.fbank = h->d_fbank + (size_t)half * MZ_MULTI_MAX * h->nflat;
+        C.theta = theta_dev ? theta_dev + (size_t)i0 * h->nflat : nullptr;
+        C.nflat = h->nflat; C.part = h->d_ml_part + (size_t)i0 * 3 * MZ_L2_BLOCKS;
+        for (int i = 0; i < n; ++i) {
+            C.bp1[i] = p1; C.bp2[i] = p2; C.eta[i] = eta[i0 + i];
+            p1 = p1 * 0.9; p2 = p2 * 0.999;
+        }
+        RpSampleParams Qk = Q;
+        Qk.step = step0 + (uint32_t)i0;
+        Qk.obs += i0 * s_obs; Qk.actions += i0 * s_k1; Qk.tv += i0 * s_k1; Qk.tr += i0 * s_k1;
+        Qk.tpol += i0 * s_tp; Qk.gscale += (size_t)i0 * B; Qk.index += (size_t)i0 * 2 * B;
+        C.B = B; C.q = Qk; C.s_obs = s_obs; C.s_k1 = s_k1; C.s_tp = s_tp;
+        const int nsb = (n * B + MZ_THREADS / 64 - 1) / (MZ_THREADS / 64);
+        hipLaunchKernelGGL(mz_learn_chain, dim3(3 * MZ_L2_BLOCKS + nsb), dim3(MZ_THREADS), 0, st, C);
+        MZ_TRY(h, hipGetLastError());
+        // 2. representation input (Atari: the downsampler with step z's parameters), the unrolls
+        U.ms = n;
+        U.Wimg = C.tbank_w; U.flat = C.fbank;
+        U.obs = Qk.obs; U.actions = Qk.actions;
+        if (h->ds) {
+            float* y = h->d_ml_dsb + (size_t)i0 * B * h->rin_feat;
+            if (ds_launch(h, Qk.obs, y, n * B, st, C.fbank, B)) return -1;
+            U.obs = y;
+        }
+        U.pv = h->d_ml_pv + i0 * s_k1; U.pp = h->d_ml_pp + i0 * s_tp; U.pr = h->d_ml_pr + i0 * s_k1;
+        U.hs = h->d_ml_hs + (size_t)i0 * U.ms_hs; U.ts = h->d_ml_ts + (size_t)i0 * U.ms_hs;
+        void* args[] = {&U};
+        hipEvent_t e0 = nullptr, e1 = nullptr;     // mz_debug_enable flag 4: the unroll launch's duration
+        if (h->time_unroll) {
+            if (timing_events(h, &e0, &e1)) return -1;
+            MZ_TRY(h, hipEventRecord(e0, st));
+        }
+        if (fused) {
+            U.prog = h->d_ml_prog + (size_t)i0 * B;
+            U.prog_base = (++h->ml_prog_epoch) * 64ull;
+            U.n_chain = B; U.fuse_sample = 0; U.n_l2 = 0;
+            const int nitems = B * KH * (K > 0 ? 3 : 2);
+            MZ_TRY(h, hipLaunchKernel(h->rd_nb == 3 ? (const void*)mz_runroll_fused_r3 : (const void*)mz_runroll_fused_r,
+                                      dim3(n * (B + nitems)), dim3(RD_THREADS), args,
+                                      std::max(rd_chain_lds(h), rp_pred_lds(h)), st));
+        } else {
+            if (h->rd_chain)
+                MZ_TRY(h, hipLaunchKernel(h->rd_nb == 3 ? (const void*)mz_runroll_chain_r3
+                                                        : (const void*)mz_runroll_chain_r,
+                                          dim3((B + U.ng_l - 1) / U.ng_l, 1, n), dim3(RD_THREADS), args,
+                                          rd_chain_lds(h), st));
+            else
+                MZ_TRY(h, hipLaunchKernel(nb1 ? (const void*)mz_runroll_chain1 : (const void*)mz_runroll_chain,
+                                          dim3((B + U.ng_l - 1) / U.ng_l, 1, n), dim3(RN_THREADS), args,
+                                          h->rn_lds_l, st));
+            if (wide_p)
+                MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred,
+                                          dim3((B * KH + U.ng - 1) / U.ng, K > 0 ? 2 : 1, n), dim3(RN_THREADS), args,
+                                          runroll_lds(h), st));
+            else if (h->rp_pred)
+                MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred_r,
+                                          dim3((B * KH + U.ng_l - 1) / U.ng_l, K > 0 ? 2 : 1, n), dim3(RD_THREADS),
+                                          args, rp_pred_lds(h), st));
+            else
+                MZ_TRY(h, hipLaunchKernel(nb1 ? (const void*)mz_runroll_pred_n1 : (const void*)mz_runroll_pred_n,
+                                          dim3((B * KH + U.ng_l - 1) / U.ng_l, K > 0 ? 2 : 1, n), dim3(RN_THREADS),
+                                          args, h->rn_lds_l, st));
+        }
+        if (e1) MZ_TRY(h, hipEventRecord(e1, st));
+        // 3. the loss terms and per-step folds (Σθ² from the chain launch)
+        LossMultiParams M;
+        std::memset(&M, 0, sizeof(M));
+        M.B = B; M.K = K; M.A = A; M.v_act = MZ_ACT_IDENTITY; M.r_act = MZ_ACT_IDENTITY; M.nlb = nlb; M.L = n;
+        M.s_k1 = s_k1; M.s_tp = s_tp; M.pv = U.pv; M.pp = U.pp; M.pr = U.pr;
+        M.tv = Qk.tv; M.tp = Qk.tpol; M.gs = Qk.gscale;
+        M.terms = h->d_ml_terms + 2 * i0 * s_k1; M.part = C.part;
+        M.counter = h->d_ml_cnt + (size_t)i0 * MZ_MULTI_CNT_STRIDE;
+        M.out = (losses_dev ? losses_dev : h->d_ml_out) + 8 * i0;
+        M.out_last = i0 + n == L ? out_last : nullptr;
+        hipLaunchKernelGGL(gw == 32 ? mz_learner_loss_multi32 : mz_learner_loss_multi, dim3(nlb, n), dim3(MZ_THREADS),
+                           0, st, M);
+        MZ_TRY(h, hipGetLastError());
+    }
+    const std::string chain = h->rd_chain ? (h->rd_nb == 3 ? "mz_runroll_chain_r3" : "mz_runroll_chain_r")
+                                          : nb1 ? "mz_runroll_chain1" : "mz_runroll_chain";
+    const std::string pred = wide_p ? "mz_runroll_pred" : h->rp_pred ? "mz_runroll_pred_r"
+                                                        : nb1 ? "mz_runroll_pred_n1" : "mz_runroll_pred_n";
+    h->last_lvariant = std::string("mz_learn_chain+") + (h->ds ? "mz_downsample_kernel+" : "") +
+                       (fused ? (h->rd_nb == 3 ? "mz_runroll_fused_r3" : "mz_runroll_fused_r") : chain + "+" + pred) +
+                       "+mz_learner_loss_multi";
+    for (int i = 0; i < L; ++i) adam_advance(h);
+    h->ml_last_B = B; h->ml_last_L = L;
     return 0;
 }
 
@@ -3677,6 +3857,7 @@ static int ensure_multi(mz_handle* h, int B, int L) {
 static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, const double* eta, float* losses_dev,
                          float* theta_dev, hipStream_t st, float* out_last = nullptr) {
     MZ_TRY(h, hipSetDevice(h->device));
+    if (rmulti_ok(h)) return rlearner_multi(h, B, step0, L, eta, losses_dev, theta_dev, st, out_last);
     int Ls = 0;
     const int ti = multi_ok(h) ? multi_plan(h, B, L, &Ls) : -1;
     if (ti < 0) {

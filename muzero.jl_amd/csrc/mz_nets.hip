@@ -6,6 +6,7 @@
 #include "mz_mlp_device.h"
 #include "mz_tree_device.h"
 #include "mz_learner_device.h"
+#include "mz_small_params.h"
 
 // One plan over tiles of 16 samples: x (in_feat, n) column-major in HBM ->
 // LDS -> plan -> out0 (o0 rows) / out1 (o1 rows, softmaxed if sm1).
@@ -138,6 +139,31 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_grad_kernel(
 }
 extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_grad_kernel32(MZ_LG_ARGS) {
     learner_grad_body<32>(MZ_LG_CALL);
+}
+
+// mz_learner_loss_multi: the loss blocks of mz_learner_grad_kernel for step
+// blockIdx.y of a multi-step sub-chunk (LossMultiParams), folded per step
+template <int GW>
+__device__ __forceinline__ void loss_multi_body(const LossMultiParams& M) {
+    __shared__ float stg[MZ_THREADS];
+    const int tid = threadIdx.x, z = blockIdx.y;
+    const int n = M.B * (M.K + 1);
+    float* vsq = M.terms + 2 * z * M.s_k1;
+    float* cet = vsq + M.s_k1;
+    float* pv = M.pv + z * M.s_k1;
+    float* pp = M.pp + z * M.s_tp;
+    float* pr = M.pr + z * M.s_k1;
+    const int t = blockIdx.x * (MZ_THREADS / GW) + tid / GW, a = tid % GW;
+    if (t < n)
+        lg_step_terms<GW>(t, a, M.A, M.v_act, M.r_act, pv, pp, pr, M.tv + z * M.s_k1, M.tp + z * M.s_tp, vsq, cet,
+                          stg + (tid & ~(GW - 1)));
+    lg_fold(M.B, M.K, vsq, cet, M.gs + (size_t)z * M.B, nullptr, M.part + (size_t)z * 3 * MZ_L2_BLOCKS,
+            M.counter + z * MZ_MULTI_CNT_STRIDE, M.out_last && z == M.L - 1 ? M.out_last : M.out + 8 * z,
+            (unsigned)M.nlb);
+}
+extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_loss_multi(LossMultiParams M) { loss_multi_body<16>(M); }
+extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learner_loss_multi32(LossMultiParams M) {
+    loss_multi_body<32>(M);
 }
 
 // ADAM over all parameters (adam_update): ∇ = G[i]·gscale + 2θ_i, G the

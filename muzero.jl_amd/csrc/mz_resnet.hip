@@ -1429,6 +1429,23 @@ extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RS
 // Forward unroll of the learner (Learning.jl:347-370): representation, then
 // for i = 1..K prediction(h_{i-1}) -> step i (step 0 is the same prediction of
 // h0, written once for both), dynamics(2h ⊕ a_i/|A|) -> h_i, r_i; r_0 = 0.
+// The parameters of this workgroup's step in a multi-step launch (U.ms > 0,
+// blockIdx.z = the step; RUnrollParams.ms), else U itself
+__device__ __forceinline__ RUnrollParams rn_step(const RUnrollParams& U, int zs = -1) {
+    RUnrollParams V = U;
+    if (U.ms) {
+        const size_t z = zs >= 0 ? (size_t)zs : blockIdx.z, B = (size_t)U.B;
+        V.Wimg += z * U.ms_wimg; V.flat += z * U.ms_flat;
+        V.obs += z * U.ms_obs; V.actions += z * U.ms_k1;
+        V.pv += z * U.ms_k1; V.pp += z * U.ms_tp; V.pr += z * U.ms_k1;
+        V.hs += z * U.ms_hs; V.ts += z * U.ms_hs; V.prog += z * B;
+        V.rq.step += (uint32_t)z;
+        V.rq.obs += z * U.ms_obs; V.rq.actions += z * U.ms_k1; V.rq.tv += z * U.ms_k1; V.rq.tr += z * U.ms_k1;
+        V.rq.tpol += z * U.ms_tp; V.rq.gscale += z * B; V.rq.index += z * 2 * B;
+    }
+    return V;
+}
+
 extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_kernel(RUnrollParams U) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const RPlan& Rr = U.plans[MZ_NET_REPR];
@@ -1546,8 +1563,12 @@ __device__ __forceinline__ void runroll_chain_body(const RUnrollParams& U) {
     }
 }
 
-extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrollParams U) { runroll_chain_body<3>(U); }
-extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain1(RUnrollParams U) { runroll_chain_body<1>(U); }
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain(RUnrollParams U) {
+    runroll_chain_body<3>(rn_step(U));
+}
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_chain1(RUnrollParams U) {
+    runroll_chain_body<1>(rn_step(U));
+}
 
 // ---- the chain with a register-resident dynamics path (mz_runroll_chain_r)
 // The K dynamics steps run the same RD_NL trunk + state-head layers K times:
@@ -1817,10 +1838,10 @@ __device__ __forceinline__ void runroll_chain_r_body(const RUnrollParams& U, int
 // TicTacToe resnet_hyper (2 blocks: 10 chain layers, 3x3 board: one column
 // block) and Connect4 ResNet-8 (4 blocks: 18 layers, 6x7 board: three)
 extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r(RUnrollParams U) {
-    runroll_chain_r_body<RD_NL, 1>(U, blockIdx.x);
+    runroll_chain_r_body<RD_NL, 1>(rn_step(U), blockIdx.x);
 }
 extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_chain_r3(RUnrollParams U) {
-    runroll_chain_r_body<RD_NL3, 3>(U, blockIdx.x);
+    runroll_chain_r_body<RD_NL3, 3>(rn_step(U), blockIdx.x);
 }
 
 // blockIdx.y = 0: prediction(h_s) for items i = b·KH + s (KH = max(K, 1)):
@@ -1935,7 +1956,7 @@ __device__ __forceinline__ void runroll_pred_r_body(const RUnrollParams& U, bool
     }
 }
 extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_pred_r(RUnrollParams U) {
-    runroll_pred_r_body<false>(U, blockIdx.y == 1, blockIdx.x);
+    runroll_pred_r_body<false>(rn_step(U), blockIdx.y == 1, blockIdx.x);
 }
 
 #include "mz_learner_device.h"
@@ -1966,8 +1987,7 @@ __device__ __forceinline__ void runroll_l2_block(const RUnrollParams& U, int j) 
 }
 
 template <int NL, int NB>
-__device__ __forceinline__ void runroll_fused_r_body(const RUnrollParams& U) {
-    const int bi = blockIdx.x;
+__device__ __forceinline__ void runroll_fused_r_body(const RUnrollParams& U, int bi) {
 #ifdef MZ_STAMPS   // diagnostic build: per block {start, input published / chain's last publish, end} (s_memrealtime)
     unsigned long long* fs = U.stamps ? U.stamps + 2048 + 4 * bi : nullptr;
     if (fs && threadIdx.x == 0) fs[0] = __builtin_amdgcn_s_memrealtime();
@@ -1986,17 +2006,37 @@ __device__ __forceinline__ void runroll_fused_r_body(const RUnrollParams& U) {
     RD_FS_END();
 #undef RD_FS_END
 }
+// A multi-step launch (U.ms steps, one-dimensional grid): the chain blocks of
+// every step first (step-major), so each step's chains are dispatched before
+// any item of any step waits on them, then the items step by step
+template <int NL, int NB>
+__device__ __forceinline__ void runroll_fused_r_entry(const RUnrollParams& U) {
+    const int bi = blockIdx.x;
+    if (!U.ms) { runroll_fused_r_body<NL, NB>(U, bi); return; }
+    const int nc = U.n_chain, per = (U.K > 0 ? 3 : 2) * U.B * (U.K > 0 ? U.K : 1);
+    if (bi < U.ms * nc) {
+        const int z = bi / nc;
+        runroll_fused_r_body<NL, NB>(rn_step(U, z), bi - z * nc);
+    } else {
+        const int j = bi - U.ms * nc, z = j / per;
+        runroll_fused_r_body<NL, NB>(rn_step(U, z), nc + U.n_l2 + (j - z * per));
+    }
+}
 extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_fused_r(RUnrollParams U) {
-    runroll_fused_r_body<RD_NL, 1>(U);
+    runroll_fused_r_entry<RD_NL, 1>(U);
 }
 extern "C" __global__ __launch_bounds__(RD_THREADS) void mz_runroll_fused_r3(RUnrollParams U) {
-    runroll_fused_r_body<RD_NL3, 3>(U);
+    runroll_fused_r_entry<RD_NL3, 3>(U);
 }
 
 // wide tiles of ng items (plans), or one item per workgroup on the narrow
 // (chain) plans — B·K workgroups, a short per-layer critical path
-extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred(RUnrollParams U) { runroll_pred_body<false>(U); }
-extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred_n(RUnrollParams U) { runroll_pred_body<true>(U); }
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred(RUnrollParams U) {
+    runroll_pred_body<false>(rn_step(U));
+}
+extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred_n(RUnrollParams U) {
+    runroll_pred_body<true>(rn_step(U));
+}
 extern "C" __global__ __launch_bounds__(RN_THREADS) void mz_runroll_pred_n1(RUnrollParams U) {
-    runroll_pred_body<true, 1>(U);
+    runroll_pred_body<true, 1>(rn_step(U));
 }

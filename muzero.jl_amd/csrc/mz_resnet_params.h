@@ -228,6 +228,12 @@ struct RUnrollParams {
     unsigned* fault;                   // MZ_FAULT_RD_PROGRESS on a publish that never came (mz_poll_ge)
     unsigned long long poll_ticks;     // the poll's bound (MZ_POLL_TICKS)
     int dbg_skip;                      // debug: the chain block (sample) whose publishes are skipped (-1 = none)
+    // ms > 0: a multi-step launch (mz_learner_train_multi_dev, ref_semantics): blockIdx.z = step z of the
+    // sub-chunk, which reads its own parameters (Wimg + z·ms_wimg, flat + z·ms_flat) and batch (obs,
+    // actions, rq at + z·strides), writes its read-outs and scratch at + z·strides and publishes / polls its
+    // own progress words (prog + z·B); rq.step + z keys its get_batch (rn_step)
+    int ms;
+    size_t ms_wimg, ms_flat, ms_obs, ms_k1, ms_tp, ms_hs;
 };
 // mz_runroll_chain_r: the dynamics chain's layers ([0, dyn_split) = RD_NL:
 // trunk + state head of 2-block towers) with register-resident A fragments
@@ -278,6 +284,8 @@ struct DsParams {
     const float* x;          // (in_feat, n_items) column-major
     float* y;                // (out_feat, n_items)
     unsigned long long* stamps;   // -DMZ_STAMPS builds: item 0's s_memtime at each layer's end (else unused)
+    int per_step;            // > 0 (multi-step learner): item i uses the parameters flat + (i / per_step)·flat_stride
+    size_t flat_stride;
 };
 
 // ---- the corrected learner through the downsampler (mz_dsbp_*, mz_downsample.hip)

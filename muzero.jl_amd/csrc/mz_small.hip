@@ -797,17 +797,16 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learn_chain(ChainPar
         const size_t p = off + e;
         float x = C.flat[p], m = C.M[p], v = C.V[p];
         const int it = C.inv_tile[p], is = C.inv_small[p];
-        float* bw = C.bank_w;
-        float* bb = C.bank_b;
-        float* th = C.theta ? C.theta + p : nullptr;
+        const bool sbank = C.bank_w != nullptr, tbank = C.tbank_w != nullptr;   // (uniform)
         for (int i = 0; i < L; ++i) {
             red[i][tid] += (double)x * (double)x;                   // step t+i's Σθ² reads θ_{t+i}
 #ifndef MZ_DBG_NO_BANK   // diagnostic only (wrong results): the chain without the bank scatter
-            mz_scatter(x, is, bw, bb);
+            if (sbank) mz_scatter(x, is, C.bank_w + i * C.bws, C.bank_b + i * C.bbs);
 #endif
+            if (tbank) mz_scatter(x, it, C.tbank_w + i * C.tws, C.tbank_b + i * C.tbs);
+            if (C.fbank) C.fbank[i * C.nflat + p] = x;
             x = adam_2theta(x, m, v, sbp[0][i], sbp[1][i], sbp[2][i]);   // Learning.jl:395-397
-            if (th) { *th = x; th += C.nflat; }
-            bw += C.bws; bb += C.bbs;
+            if (C.theta) C.theta[i * C.nflat + p] = x;
         }
         C.flat[p] = x; C.M[p] = m; C.V[p] = v;
         mz_scatter(x, it, C.Wp, C.Bp);

@@ -148,7 +148,9 @@ struct ChainParams {
     float* flat; float* M; float* V; const size_t* netoff;
     const int* inv_tile; const int* inv_small;
     float* Wp; float* Bp; float* smw; float* smb;     // the current images: θ_{t+L}
-    float* bank_w; float* bank_b; size_t bws, bbs;     // bank image i (small-kernel W, bias): θ_{t+i}
+    float* bank_w; float* bank_b; size_t bws, bbs;     // bank image i (small-kernel W, bias): θ_{t+i} (or NULL)
+    float* tbank_w; float* tbank_b; size_t tws, tbs;   // bank image i of the tile / ResNet MFMA image (or NULL)
+    float* fbank;                                      // NULL or [L][nflat]: θ_{t+i}, the flat parameters of step t+i
     float* theta;                                      // NULL or [L][nflat]: θ after step t+i
     size_t nflat;
     double* part;                                      // [L][3·MZ_L2_BLOCKS] Σθ_{t+i}² partials
@@ -167,6 +169,17 @@ struct LearnMultiParams {
     float* out_last;                                   // non-NULL: step L-1's losses go here instead (mz_train_run)
     int sample;                                        // waves 0..T-1 draw their samples (else mz_learn_chain did)
     RpSampleParams q;                                  // as ChainParams::q
+};
+
+// The loss terms and per-step folds of a multi-step sub-chunk whose unrolls
+// ran in other launches (the ResNet nets, mz_learner_loss_multi): grid (nlb,
+// L), step z = blockIdx.y on its arrays at + z·strides, the chain launch's
+// Σθ² partials of the step, one fold counter per step.
+struct LossMultiParams {
+    int B, K, A, v_act, r_act, nlb, L;
+    size_t s_k1, s_tp;
+    float* pv; float* pp; float* pr; const float* tv; const float* tp; const float* gs; float* terms;
+    const double* part; unsigned* counter; float* out; float* out_last;
 };
 
 // Σθ² / ADAM workgroups of the fused learner: 48 (each 256-thread half takes

@@ -6,7 +6,9 @@ and all three nets' θ after the step —
 * against L mz_learner_train_dev calls on an engine holding the same replay
   shard (FC TicTacToe / Connect4, FC + BatchNorm, chunks of 1..50 steps —
   several sub-chunks with alternating bank halves — T = 1 and T = 2 samples
-  per workgroup, single steps before and after the chunk);
+  per workgroup, single steps before and after the chunk; the ResNet nets of
+  TicTacToe (configs[2], the fused unroll launch), Connect4 and the Atari-like
+  env (downsampler, split unroll launches) with the steps on gridDim.z);
 * against the oracle's ora_learner_step fed the same device get_batch samples.
 """
 import dataclasses
@@ -19,27 +21,33 @@ pytestmark = pytest.mark.gpu
 
 def _mods(kind):
     from muzero_jl_amd import abi
-    from muzero_jl_amd.games import connect4, tictactoe
-    return (tictactoe, abi.ENV_TICTACTOE) if kind in ("ttt", "ttt-bn") else (connect4, abi.ENV_CONNECT4)
+    from muzero_jl_amd.games import atari_synth, connect4, tictactoe
+    if kind == "atari":
+        return atari_synth, abi.ENV_ATARI
+    return (tictactoe, abi.ENV_TICTACTOE) if kind.startswith("ttt") else (connect4, abi.ENV_CONNECT4)
 
 
 def _pair(kind, G=16, cap=64, seed=5):
-    """Two engines with the same weights whose device self-play fills identical replay shards."""
+    """Two engines with the same weights whose device self-play fills identical replay shards
+    (kinds: FC TicTacToe / Connect4, "ttt-bn" FC + BatchNorm, "ttt-rn" / "c4-rn" / "atari" ResNet)."""
     from muzero_jl_amd import abi
     from muzero_jl_amd.networks import init_nets
     mod, env_kind = _mods(kind)
-    conf = dataclasses.replace(mod.conf, num_iters=6, replay_buffer_size=cap)
-    hyper = mod.hyper
+    conf = dataclasses.replace(mod.conf, num_iters=6 if kind != "atari" else 2, replay_buffer_size=cap)
+    hyper = mod.resnet_hyper if kind.endswith("-rn") or kind == "atari" else mod.hyper
     if kind == "ttt-bn":
         hyper = dataclasses.replace(hyper, use_batch_norm=True)
+    if kind == "atari":
+        G = 32
     nets = init_nets(conf, hyper, seed=seed + 100)
+    moves = {"ttt": 14, "ttt-bn": 14, "ttt-rn": 14, "c4": 30, "c4-rn": 30, "atari": 48}[kind]
     out = []
     for _ in range(2):
         e = abi.Engine(conf, hyper, device=0, max_games=G, rng_seed=seed)
         for n, w in enumerate(nets):
             e.set_weights(n, w)
         e.selfplay_init(env_kind, G, cap)
-        for m in range(14 if kind != "c4" else 30):
+        for m in range(moves):
             e.selfplay_move(100 + m, game_offset=7)
         out.append(e)
     assert out[0].replay_counts()[0][0] > 0
@@ -51,7 +59,9 @@ def _theta(e):
 
 
 @pytest.mark.parametrize("kind,B,L", [("ttt", 32, 8), ("ttt", 32, 16), ("ttt", 32, 1), ("ttt", 40, 5),
-                                      ("c4", 24, 10), ("ttt-bn", 32, 6), ("ttt", 32, 37), ("ttt", 40, 50)])
+                                      ("c4", 24, 10), ("ttt-bn", 32, 6), ("ttt", 32, 37), ("ttt", 40, 50),
+                                      ("ttt-rn", 32, 8), ("ttt-rn", 32, 21), ("ttt-rn", 7, 3), ("c4-rn", 16, 6),
+                                      ("atari", 8, 5)])
 def test_multi_matches_sequential_steps(kind, B, L):
     import torch
     from muzero_jl_amd.config import cos_schedule
@@ -72,8 +82,10 @@ def test_multi_matches_sequential_steps(kind, B, L):
             want.append((l1.cpu().numpy()[:6].copy(), _theta(e1), [x.copy() for x in e1.debug_unroll(B)]))
         e2.learner_train_multi_dev(B, t0, etas, lm.data_ptr(), th.data_ptr())
         e2.sync()
-        # the two-launch form wherever the one-launch step runs (else the steps one after another)
-        assert ("multi" in e2.learner_variant()) == e1.learner_variant().startswith("mz_learn_small"), \
+        # FC: the two-launch form wherever the one-launch step runs (else the steps one after
+        # another); ResNet: always the multi-step form
+        rn = kind.endswith("-rn") or kind == "atari"
+        assert ("multi" in e2.learner_variant()) == (rn or e1.learner_variant().startswith("mz_learn_small")), \
             (e1.learner_variant(), e2.learner_variant())
         multi = "multi" in e2.learner_variant()
         got_l, got_t = lm.cpu().numpy(), th.cpu().numpy()
