@@ -242,7 +242,7 @@ def main():
     ap.add_argument("--sims", type=int, default=None, help="sims per move (default 50; atari 200)")
     ap.add_argument("--learner-steps", type=int, default=50)
     ap.add_argument("--learner-chunk", type=int, default=64,
-                    help="FC, one GPU: consecutive ref_semantics learner steps per mz_learner_train_multi_dev call "
+                    help="one GPU: consecutive ref_semantics learner steps per mz_learner_train_multi_dev call "
                          "(1..256, sub-chunks of 16; 1 = the one-step form only)")
     ap.add_argument("--batch", type=int, default=None,
                     help="learner batch size (default conf.batch_size = 32; SURVEY §8d config 3 also names 2048)")
@@ -474,7 +474,7 @@ def main():
         # L consecutive steps per launch pair (mz_learner_train_multi_dev; ref_semantics, Q11: the
         # update does not read the data and PER-off batches are keyed by the step): the FC headline
         # learner number on one GPU; the one-step form above stays in the line (learner_steps_per_s_1step)
-        if world == 1 and not resnet and args.learner_chunk > 1:
+        if world == 1 and args.learner_chunk > 1:
             L = args.learner_chunk
             lm = torch.empty((L, 8), dtype=torch.float32, device=dev)
 
@@ -510,7 +510,10 @@ def main():
             torch.cuda.synchronize()
             t_ms, n_l = eng.debug_kernel_time()
             eng.debug_enable(0)
-            lkern, lkern_ms = eng.learner_variant().split("+")[-1], t_ms / n_l
+            # the unroll launch(es): FC mz_learn_multi*, ResNet the mz_runroll_* kernels of the variant
+            parts = eng.learner_variant().split("+")
+            lkern = "+".join(k for k in parts if k.startswith("mz_runroll")) if resnet else parts[-1]
+            lkern_ms = t_ms / n_l
             learner_sps = nch * L / tm
             lstep_ms = chunk_ms / L
             multi = {"steps_per_call": L, "steps_per_unroll_launch": 5 * L / n_l,
@@ -623,7 +626,8 @@ def main():
                 Lm = multi["steps_per_unroll_launch"]
                 lflop = Lm * f_unroll
                 lbytes = Lm * (4 * nparam + 4 * B * (obs.shape[1] + 2 * (K + 1) + (K + 1) * A + 1) +
-                               4 * B * (K + 1) * (A + 4))
+                               4 * B * (K + 1) * (A + 4)) if not resnet else Lm * lbytes
+                # (ResNet: the unroll launches per step as the one-step form; the losses run after them)
             lach = lflop / (lkern_ms * 1e-3) / 1e12
             ltraffic, ltraffic_src, lpmc = pmc_record(lkern, pmc_line)
             hbm_gbs = (ltraffic if ltraffic else lbytes) / (lkern_ms * 1e-3) / 1e9
