@@ -2,7 +2,11 @@
 // CU with 512 threads (8 waves, two per SIMD):
 //   (a) s_barrier alone;
 //   (b) ds_write -> s_barrier -> dependent ds_read (the stage hand-off);
-//   (c) (b) + a 16-step dependent v_fmac_f32_dpp chain x2 games per lane.
+//   (c) (b) + a 16-step dependent v_fmac_f32_dpp chain x2 games per lane;
+//   (d) (c) + mz_small.hip sm_stage's epilogue: the next stage's int4 record
+//       from LDS, the permlane16/32 swap sums ((p0+p1)+(p2+p3)) of both games,
+//       DPP row 0 adding the bias, relu, and storing both games' rows — the
+//       whole stage of the search kernel without its weights' register image.
 // Prints s_memtime ticks per iteration (wave 0 lane 0, median over blocks).
 // Build: hipcc --offload-arch=gfx950 -O3 tools/barrier_probe.hip -o tools/barrier_probe
 #include <hip/hip_runtime.h>
@@ -28,9 +32,14 @@ __device__ __forceinline__ void chain(float w, float x0, float x1, float& a0, fl
 
 extern "C" __global__ __launch_bounds__(512, 1) void probe(int mode, unsigned long long* out, float* sink) {
     __shared__ float buf[2][1024];
+    __shared__ int4 rec[2][512];
     const int tid = threadIdx.x;
     buf[0][tid] = (float)tid; buf[1][tid] = 0.0f;
+    buf[0][tid + 512] = 0.0f; buf[1][tid + 512] = 0.0f;
+    rec[0][tid] = make_int4(0, 4, (1 << 30) | (tid & 255) * 2, __float_as_int(0.5f));
+    rec[1][tid] = rec[0][tid];
     __syncthreads();
+    int4 R = rec[0][tid];
     float acc = 0.0f;
     const float w = 1.0f + tid * 1e-7f;
     unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -41,10 +50,36 @@ extern "C" __global__ __launch_bounds__(512, 1) void probe(int mode, unsigned lo
             const int src = it & 1;
             const float2 x = *reinterpret_cast<const float2*>(&buf[src][(tid * 7) & 1022]);
             float a0 = acc, a1 = 0.0f;
-            if (mode == 2) chain(w, x.x, x.y, a0, a1);
+            if (mode >= 2) chain(w, x.x, x.y, a0, a1);
             else { a0 += x.x; a1 += x.y; }
-            buf[src ^ 1][tid] = a0 + a1;
-            acc = a0 * 1e-3f;
+            if (mode == 3) {
+                const int4 Rn = rec[src ^ 1][tid];
+                float r[2] = {a0, a1};
+#pragma unroll
+                for (int g = 0; g < 2; ++g) {
+                    const auto s1 = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, r[g]),
+                                                                     __builtin_bit_cast(unsigned, r[g]), false, false);
+                    const float t = __builtin_bit_cast(float, (unsigned)s1[0]) + __builtin_bit_cast(float, (unsigned)s1[1]);
+                    const auto s2 = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, t),
+                                                                     __builtin_bit_cast(unsigned, t), false, false);
+                    r[g] = __builtin_bit_cast(float, (unsigned)s2[0]) + __builtin_bit_cast(float, (unsigned)s2[1]);
+                }
+                if (((tid >> 4) & 3) == 0 && R.z >= 0) {
+                    const int o = R.z & 0x1fffffff;
+                    const bool relu = (R.z >> 30) != 0;
+                    const float bias = __int_as_float(R.w);
+#pragma unroll
+                    for (int g = 0; g < 2; ++g) {
+                        const float d = r[g] + bias;
+                        buf[src ^ 1][o + g] = relu ? fmaxf(d, 0.0f) : d;
+                    }
+                }
+                R = Rn;
+                acc = r[0] * 1e-3f;
+            } else {
+                buf[src ^ 1][tid] = a0 + a1;
+                acc = a0 * 1e-3f;
+            }
             __syncthreads();
         }
     }
@@ -57,14 +92,15 @@ int main() {
     const int blocks = 256;
     unsigned long long* d; float* sink;
     hipMalloc(&d, blocks * 8); hipMalloc(&sink, 4096);
-    const char* names[3] = {"barrier only", "ds_write+barrier+ds_read", "+ 16-step x2 dpp fmac chain"};
-    for (int mode = 0; mode < 3; ++mode) {
+    const char* names[4] = {"barrier only", "ds_write+barrier+ds_read", "+ 16-step x2 dpp fmac chain",
+                            "+ sm_stage epilogue (record, permlane sums, row-0 bias/relu/store)"};
+    for (int mode = 0; mode < 4; ++mode) {
         for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL(probe, dim3(blocks), dim3(512), 0, 0, mode, d, sink);
         hipDeviceSynchronize();
         std::vector<unsigned long long> h(blocks);
         hipMemcpy(h.data(), d, blocks * 8, hipMemcpyDeviceToHost);
         std::sort(h.begin(), h.end());
-        printf("%-32s %8.1f ticks/iter (median over %d blocks)\n", names[mode], (double)h[blocks / 2] / ITERS, blocks);
+        printf("%-68s %8.1f ticks/iter (median over %d blocks)\n", names[mode], (double)h[blocks / 2] / ITERS, blocks);
     }
     return 0;
 }
