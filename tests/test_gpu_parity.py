@@ -107,6 +107,8 @@ def test_search_bitexact(ttt, nets, S, G, explore, temp, seed, kernel, monkeypat
     cv, rv, act = eng.mcts_search(obs, legal, tp, exploration=explore, rng_step=seed * 3, game_offset=100,
                                   temperature=temp)
     tree_g = eng.debug_tree(G)
+    if kernel[0] == "small" and S <= 50:             # (the kernel the case is for, not a silent fallback)
+        assert eng.search_variant().startswith("mz_search_small"), eng.search_variant()
     cv2, rv2, act2, tree_o, _ = ora.mcts_search(obs, legal, tp, exploration=explore, rng_step=seed * 3,
                                                 game_offset=100, temperature=temp, dump=True)
     _compare_trees(tree_g, tree_o, G)

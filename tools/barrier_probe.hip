@@ -6,7 +6,15 @@
 //   (d) (c) + mz_small.hip sm_stage's epilogue: the next stage's int4 record
 //       from LDS, the permlane16/32 swap sums ((p0+p1)+(p2+p3)) of both games,
 //       DPP row 0 adding the bias, relu, and storing both games' rows — the
-//       whole stage of the search kernel without its weights' register image.
+//       whole stage of the search kernel without its weights' register image;
+//   (e) (c) with the quarter sums moved to the consumer: every lane stores its
+//       two partials, the next stage reads the four partials of its input
+//       element per game (two 16-byte reads) and forms ((p0+p1)+(p2+p3)) + b,
+//       relu — no permlane chain and no row-0 branch;
+//   (f) (d) with the quarter sums through wave-private LDS instead of the
+//       permlane swaps (partials stored, row 0 reads its four back);
+//   (g) (d) without the quarter sums (row 0 writes its own partial: the
+//       permlane chain's share of (d)).
 // Prints s_memtime ticks per iteration (wave 0 lane 0, median over blocks).
 // Build: hipcc --offload-arch=gfx950 -O3 tools/barrier_probe.hip -o tools/barrier_probe
 #include <hip/hip_runtime.h>
@@ -33,30 +41,61 @@ __device__ __forceinline__ void chain(float w, float x0, float x1, float& a0, fl
 extern "C" __global__ __launch_bounds__(512, 1) void probe(int mode, unsigned long long* out, float* sink) {
     __shared__ float buf[2][1024];
     __shared__ int4 rec[2][512];
+    __shared__ float4 part[2][2][256];                  // [buffer][game][element] the four quarter partials
+    __shared__ float wpart[8][2][64];                    // (f): per wave, per game, the lanes' partials
     const int tid = threadIdx.x;
     buf[0][tid] = (float)tid; buf[1][tid] = 0.0f;
     buf[0][tid + 512] = 0.0f; buf[1][tid + 512] = 0.0f;
     rec[0][tid] = make_int4(0, 4, (1 << 30) | (tid & 255) * 2, __float_as_int(0.5f));
     rec[1][tid] = rec[0][tid];
+    part[0][0][tid & 255] = make_float4(1.f, 2.f, 3.f, 4.f); part[0][1][tid & 255] = make_float4(1.f, 2.f, 3.f, 4.f);
     __syncthreads();
     int4 R = rec[0][tid];
+    const float bias_e = 0.25f;
     float acc = 0.0f;
     const float w = 1.0f + tid * 1e-7f;
     unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int it = 0; it < ITERS; ++it) {
         if (mode == 0) {
             __syncthreads();
+        } else if (mode == 4) {
+            const int src = it & 1, e = (tid * 7) & 255, q = (tid >> 4) & 3, row = (tid & 15) | ((tid >> 6) << 4);
+            const float4 u0 = part[src][0][e], u1 = part[src][1][e];
+            const int4 mt = rec[src][e];                      // the element's producer: bias, relu flag
+            const int4 Rn = rec[src ^ 1][tid];
+            const float be = __int_as_float(mt.w) + bias_e;
+            const bool rl = (mt.z >> 30) != 0;
+            const float y0 = ((u0.x + u0.y) + (u0.z + u0.w)) + be, y1 = ((u1.x + u1.y) + (u1.z + u1.w)) + be;
+            const float x0 = rl ? fmaxf(y0, 0.0f) : y0, x1 = rl ? fmaxf(y1, 0.0f) : y1;
+            float a0 = 0.0f, a1 = 0.0f;
+            chain(w, x0, x1, a0, a1);
+            R = Rn;
+            reinterpret_cast<float*>(&part[src ^ 1][0][row])[q] = a0;
+            reinterpret_cast<float*>(&part[src ^ 1][1][row])[q] = a1;
+            acc = a0 * 1e-3f;
+            __syncthreads();
         } else {
             const int src = it & 1;
             const float2 x = *reinterpret_cast<const float2*>(&buf[src][(tid * 7) & 1022]);
+            const int4 Rn = rec[src ^ 1][tid];               // (sm_stage: the next record before the chain)
             float a0 = acc, a1 = 0.0f;
             if (mode >= 2) chain(w, x.x, x.y, a0, a1);
             else { a0 += x.x; a1 += x.y; }
-            if (mode == 3) {
-                const int4 Rn = rec[src ^ 1][tid];
+            if (mode == 3 || mode == 5 || mode == 6) {
                 float r[2] = {a0, a1};
+                if (mode == 5) {
+                    const int wv = tid >> 6, ln = tid & 63;
+                    wpart[wv][0][ln] = a0; wpart[wv][1][ln] = a1;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    const int i16 = ln & 15;
 #pragma unroll
-                for (int g = 0; g < 2; ++g) {
+                    for (int g = 0; g < 2; ++g)
+                        r[g] = (wpart[wv][g][i16] + wpart[wv][g][16 + i16]) + (wpart[wv][g][32 + i16] + wpart[wv][g][48 + i16]);
+                }
+#pragma unroll
+                for (int g = 0; g < 2 && mode == 3; ++g) {
                     const auto s1 = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, r[g]),
                                                                      __builtin_bit_cast(unsigned, r[g]), false, false);
                     const float t = __builtin_bit_cast(float, (unsigned)s1[0]) + __builtin_bit_cast(float, (unsigned)s1[1]);
@@ -92,9 +131,12 @@ int main() {
     const int blocks = 256;
     unsigned long long* d; float* sink;
     hipMalloc(&d, blocks * 8); hipMalloc(&sink, 4096);
-    const char* names[4] = {"barrier only", "ds_write+barrier+ds_read", "+ 16-step x2 dpp fmac chain",
-                            "+ sm_stage epilogue (record, permlane sums, row-0 bias/relu/store)"};
-    for (int mode = 0; mode < 4; ++mode) {
+    const char* names[7] = {"barrier only", "ds_write+barrier+ds_read", "+ 16-step x2 dpp fmac chain",
+                            "+ sm_stage epilogue (record, permlane sums, row-0 bias/relu/store)",
+                            "chain + partials stored, quarter sums by the consumer",
+                            "(d) with the quarter sums through wave-private LDS",
+                            "(d) without the quarter sums"};
+    for (int mode = 0; mode < 7; ++mode) {
         for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL(probe, dim3(blocks), dim3(512), 0, 0, mode, d, sink);
         hipDeviceSynchronize();
         std::vector<unsigned long long> h(blocks);
