@@ -3629,8 +3629,9 @@ int mz_learner_train_dev(mz_handle* h, int32_t B, uint32_t step, double eta, flo
 
 // ---- L consecutive ref_semantics learner steps (ChainParams, mz_small_params.h;
 // Learning.jl:327-404 with get_batch keyed by the step, Q11).  The L steps run
-// as sub-chunks of up to MZ_MULTI_MAX steps, each one chain launch (the ADAM
-// iterations) and one unroll launch, in stream order.  (Measured: the next
+// as chunks of up to MZ_MULTI_MAX steps, each one chain launch (the ADAM
+// iterations) and unroll launches of up to MZ_MULTI_UNROLL steps, in stream
+// order (32-step chains: the chain's fixed costs over twice the steps).  (Measured: the next
 // sub-chunk's chain on a second stream, ordered by events, beside the unroll
 // launch — 228.8 k vs 279.5 k steps/s at L = 64, 114.6 k vs ~170 k at L = 8:
 // the cross-stream event waits cost more than the chain they hide.)
@@ -3651,8 +3652,8 @@ static int multi_plan(const mz_handle* h, int B, int L, int* Ls) {
     else if (small_unroll_fits(h, 0)) ti = 0;
     else return -1;
     const int nU = (B + ti) / (ti + 1);
-    int ls = std::max(1, std::min(MZ_MULTI_MAX, h->n_cu / nU));
-    if (ls_env > 0) ls = std::min(MZ_MULTI_MAX, ls_env);
+    int ls = std::max(1, std::min(MZ_MULTI_UNROLL, h->n_cu / nU));
+    if (ls_env > 0) ls = std::min(MZ_MULTI_UNROLL, ls_env);
     *Ls = std::min(ls, L);
     return ti;
 }
@@ -3725,7 +3726,7 @@ static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, co
     if (rs_params(h, B, step0, st, &Q, &b, true)) return -1;
     if (ensure_batch(h, B) || ensure_multi(h, B, L)) return -1;
     static const int ls_env = std::getenv("MZ_MULTI_LS") ? std::atoi(std::getenv("MZ_MULTI_LS")) : 0;
-    const int Ls = std::min(L, ls_env > 0 ? std::min(MZ_MULTI_MAX, ls_env) : MZ_MULTI_MAX);
+    const int Ls = std::min(L, ls_env > 0 ? std::min(MZ_MULTI_UNROLL, ls_env) : MZ_MULTI_UNROLL);
     const int K = h->conf.num_unroll_steps, KH = std::max(K, 1), A = h->A;
     const size_t K1 = (size_t)K + 1;
     const size_t s_obs = (size_t)B * h->obs_feat, s_k1 = (size_t)B * K1, s_tp = (size_t)B * K1 * A;
@@ -3753,93 +3754,103 @@ static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, co
     const int gw = A > 16 ? 32 : 16;
     const int nlb = (B * (int)K1 + MZ_THREADS / gw - 1) / (MZ_THREADS / gw);
     double p1 = h->bp1, p2 = h->bp2;
-    for (int k = 0, i0 = 0; i0 < L; ++k, i0 += Ls) {
-        const int n = std::min(Ls, L - i0), half = k & 1;
-        ChainParams C;                              // 1. ADAM chain + the n batches
+    // chain launches of up to MZ_MULTI_MAX steps (bank half k mod 2), each followed by its steps' unroll
+    // launches of up to Ls steps
+    const int Lc = std::min(L, std::max(Ls, MZ_MULTI_MAX / Ls * Ls));
+    for (int k = 0, c0 = 0; c0 < L; ++k, c0 += Lc) {
+        const int nc = std::min(Lc, L - c0), half = k & 1;
+        ChainParams C;                              // 1. ADAM chain + the nc batches
         std::memset(&C, 0, sizeof(C));
-        C.L = n; C.flat = h->d_flat; C.M = h->d_m; C.V = h->d_v; C.netoff = h->d_netoff;
+        C.L = nc; C.flat = h->d_flat; C.M = h->d_m; C.V = h->d_v; C.netoff = h->d_netoff;
         C.inv_tile = h->d_inv_tile; C.inv_small = h->d_inv_small;
         C.Wp = h->d_Wp; C.Bp = h->d_Bp; C.smw = h->d_sm_w; C.smb = h->d_sm_bias;
         C.tbank_w = h->d_tbank_w + (size_t)half * MZ_MULTI_MAX * nw;
         C.tbank_b = h->d_tbank_b + (size_t)half * MZ_MULTI_MAX * nb;
         C.tws = nw; C.tbs = nb;
         C.fbank = h->d_fbank + (size_t)half * MZ_MULTI_MAX * h->nflat;
-        C.theta = theta_dev ? theta_dev + (size_t)i0 * h->nflat : nullptr;
-        C.nflat = h->nflat; C.part = h->d_ml_part + (size_t)i0 * 3 * MZ_L2_BLOCKS;
-        for (int i = 0; i < n; ++i) {
-            C.bp1[i] = p1; C.bp2[i] = p2; C.eta[i] = eta[i0 + i];
+        C.theta = theta_dev ? theta_dev + (size_t)c0 * h->nflat : nullptr;
+        C.nflat = h->nflat; C.part = h->d_ml_part + (size_t)c0 * 3 * MZ_L2_BLOCKS;
+        for (int i = 0; i < nc; ++i) {
+            C.bp1[i] = p1; C.bp2[i] = p2; C.eta[i] = eta[c0 + i];
             p1 = p1 * 0.9; p2 = p2 * 0.999;
         }
-        RpSampleParams Qk = Q;
-        Qk.step = step0 + (uint32_t)i0;
-        Qk.obs += i0 * s_obs; Qk.actions += i0 * s_k1; Qk.tv += i0 * s_k1; Qk.tr += i0 * s_k1;
-        Qk.tpol += i0 * s_tp; Qk.gscale += (size_t)i0 * B; Qk.index += (size_t)i0 * 2 * B;
-        C.B = B; C.q = Qk; C.s_obs = s_obs; C.s_k1 = s_k1; C.s_tp = s_tp;
-        const int nsb = (n * B + MZ_THREADS / 64 - 1) / (MZ_THREADS / 64);
+        RpSampleParams Qc = Q;
+        Qc.step = step0 + (uint32_t)c0;
+        Qc.obs += c0 * s_obs; Qc.actions += c0 * s_k1; Qc.tv += c0 * s_k1; Qc.tr += c0 * s_k1;
+        Qc.tpol += c0 * s_tp; Qc.gscale += (size_t)c0 * B; Qc.index += (size_t)c0 * 2 * B;
+        C.B = B; C.q = Qc; C.s_obs = s_obs; C.s_k1 = s_k1; C.s_tp = s_tp;
+        const int nsb = (nc * B + MZ_THREADS / 64 - 1) / (MZ_THREADS / 64);
         hipLaunchKernelGGL(mz_learn_chain, dim3(3 * MZ_L2_BLOCKS + nsb), dim3(MZ_THREADS), 0, st, C);
         MZ_TRY(h, hipGetLastError());
-        // 2. representation input (Atari: the downsampler with step z's parameters), the unrolls
-        U.ms = n;
-        U.Wimg = C.tbank_w; U.flat = C.fbank;
-        U.obs = Qk.obs; U.actions = Qk.actions;
-        if (h->ds) {
-            float* y = h->d_ml_dsb + (size_t)i0 * B * h->rin_feat;
-            if (ds_launch(h, Qk.obs, y, n * B, st, C.fbank, B)) return -1;
-            U.obs = y;
+        for (int j0 = 0; j0 < nc; j0 += Ls) {
+            const int n = std::min(Ls, nc - j0), i0 = c0 + j0;
+            RpSampleParams Qk = Q;                  // steps step0 + i0 ..
+            Qk.step = step0 + (uint32_t)i0;
+            Qk.obs += i0 * s_obs; Qk.actions += i0 * s_k1; Qk.tv += i0 * s_k1; Qk.tr += i0 * s_k1;
+            Qk.tpol += i0 * s_tp; Qk.gscale += (size_t)i0 * B; Qk.index += (size_t)i0 * 2 * B;
+            // 2. representation input (Atari: the downsampler with step z's parameters), the unrolls
+            U.ms = n;
+            U.Wimg = C.tbank_w + (size_t)j0 * nw; U.flat = C.fbank + (size_t)j0 * h->nflat;
+            U.obs = Qk.obs; U.actions = Qk.actions;
+            if (h->ds) {
+                float* y = h->d_ml_dsb + (size_t)i0 * B * h->rin_feat;
+                if (ds_launch(h, Qk.obs, y, n * B, st, C.fbank + (size_t)j0 * h->nflat, B)) return -1;
+                U.obs = y;
+            }
+            U.pv = h->d_ml_pv + i0 * s_k1; U.pp = h->d_ml_pp + i0 * s_tp; U.pr = h->d_ml_pr + i0 * s_k1;
+            U.hs = h->d_ml_hs + (size_t)i0 * U.ms_hs; U.ts = h->d_ml_ts + (size_t)i0 * U.ms_hs;
+            void* args[] = {&U};
+            hipEvent_t e0 = nullptr, e1 = nullptr;     // mz_debug_enable flag 4: the unroll launch's duration
+            if (h->time_unroll) {
+                if (timing_events(h, &e0, &e1)) return -1;
+                MZ_TRY(h, hipEventRecord(e0, st));
+            }
+            if (fused) {
+                U.prog = h->d_ml_prog + (size_t)i0 * B;
+                U.prog_base = (++h->ml_prog_epoch) * 64ull;
+                U.n_chain = B; U.fuse_sample = 0; U.n_l2 = 0;
+                const int nitems = B * KH * (K > 0 ? 3 : 2);
+                MZ_TRY(h, hipLaunchKernel(h->rd_nb == 3 ? (const void*)mz_runroll_fused_r3 : (const void*)mz_runroll_fused_r,
+                                          dim3(n * (B + nitems)), dim3(RD_THREADS), args,
+                                          std::max(rd_chain_lds(h), rp_pred_lds(h)), st));
+            } else {
+                if (h->rd_chain)
+                    MZ_TRY(h, hipLaunchKernel(h->rd_nb == 3 ? (const void*)mz_runroll_chain_r3
+                                                            : (const void*)mz_runroll_chain_r,
+                                              dim3((B + U.ng_l - 1) / U.ng_l, 1, n), dim3(RD_THREADS), args,
+                                              rd_chain_lds(h), st));
+                else
+                    MZ_TRY(h, hipLaunchKernel(nb1 ? (const void*)mz_runroll_chain1 : (const void*)mz_runroll_chain,
+                                              dim3((B + U.ng_l - 1) / U.ng_l, 1, n), dim3(RN_THREADS), args,
+                                              h->rn_lds_l, st));
+                if (wide_p)
+                    MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred,
+                                              dim3((B * KH + U.ng - 1) / U.ng, K > 0 ? 2 : 1, n), dim3(RN_THREADS), args,
+                                              runroll_lds(h), st));
+                else if (h->rp_pred)
+                    MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred_r,
+                                              dim3((B * KH + U.ng_l - 1) / U.ng_l, K > 0 ? 2 : 1, n), dim3(RD_THREADS),
+                                              args, rp_pred_lds(h), st));
+                else
+                    MZ_TRY(h, hipLaunchKernel(nb1 ? (const void*)mz_runroll_pred_n1 : (const void*)mz_runroll_pred_n,
+                                              dim3((B * KH + U.ng_l - 1) / U.ng_l, K > 0 ? 2 : 1, n), dim3(RN_THREADS),
+                                              args, h->rn_lds_l, st));
+            }
+            if (e1) MZ_TRY(h, hipEventRecord(e1, st));
+            // 3. the loss terms and per-step folds (Σθ² from the chain launch)
+            LossMultiParams M;
+            std::memset(&M, 0, sizeof(M));
+            M.B = B; M.K = K; M.A = A; M.v_act = MZ_ACT_IDENTITY; M.r_act = MZ_ACT_IDENTITY; M.nlb = nlb; M.L = n;
+            M.s_k1 = s_k1; M.s_tp = s_tp; M.pv = U.pv; M.pp = U.pp; M.pr = U.pr;
+            M.tv = Qk.tv; M.tp = Qk.tpol; M.gs = Qk.gscale;
+            M.terms = h->d_ml_terms + 2 * i0 * s_k1; M.part = h->d_ml_part + (size_t)i0 * 3 * MZ_L2_BLOCKS;
+            M.counter = h->d_ml_cnt + (size_t)i0 * MZ_MULTI_CNT_STRIDE;
+            M.out = (losses_dev ? losses_dev : h->d_ml_out) + 8 * i0;
+            M.out_last = i0 + n == L ? out_last : nullptr;
+            hipLaunchKernelGGL(gw == 32 ? mz_learner_loss_multi32 : mz_learner_loss_multi, dim3(nlb, n), dim3(MZ_THREADS),
+                               0, st, M);
+            MZ_TRY(h, hipGetLastError());
         }
-        U.pv = h->d_ml_pv + i0 * s_k1; U.pp = h->d_ml_pp + i0 * s_tp; U.pr = h->d_ml_pr + i0 * s_k1;
-        U.hs = h->d_ml_hs + (size_t)i0 * U.ms_hs; U.ts = h->d_ml_ts + (size_t)i0 * U.ms_hs;
-        void* args[] = {&U};
-        hipEvent_t e0 = nullptr, e1 = nullptr;     // mz_debug_enable flag 4: the unroll launch's duration
-        if (h->time_unroll) {
-            if (timing_events(h, &e0, &e1)) return -1;
-            MZ_TRY(h, hipEventRecord(e0, st));
-        }
-        if (fused) {
-            U.prog = h->d_ml_prog + (size_t)i0 * B;
-            U.prog_base = (++h->ml_prog_epoch) * 64ull;
-            U.n_chain = B; U.fuse_sample = 0; U.n_l2 = 0;
-            const int nitems = B * KH * (K > 0 ? 3 : 2);
-            MZ_TRY(h, hipLaunchKernel(h->rd_nb == 3 ? (const void*)mz_runroll_fused_r3 : (const void*)mz_runroll_fused_r,
-                                      dim3(n * (B + nitems)), dim3(RD_THREADS), args,
-                                      std::max(rd_chain_lds(h), rp_pred_lds(h)), st));
-        } else {
-            if (h->rd_chain)
-                MZ_TRY(h, hipLaunchKernel(h->rd_nb == 3 ? (const void*)mz_runroll_chain_r3
-                                                        : (const void*)mz_runroll_chain_r,
-                                          dim3((B + U.ng_l - 1) / U.ng_l, 1, n), dim3(RD_THREADS), args,
-                                          rd_chain_lds(h), st));
-            else
-                MZ_TRY(h, hipLaunchKernel(nb1 ? (const void*)mz_runroll_chain1 : (const void*)mz_runroll_chain,
-                                          dim3((B + U.ng_l - 1) / U.ng_l, 1, n), dim3(RN_THREADS), args,
-                                          h->rn_lds_l, st));
-            if (wide_p)
-                MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred,
-                                          dim3((B * KH + U.ng - 1) / U.ng, K > 0 ? 2 : 1, n), dim3(RN_THREADS), args,
-                                          runroll_lds(h), st));
-            else if (h->rp_pred)
-                MZ_TRY(h, hipLaunchKernel((const void*)mz_runroll_pred_r,
-                                          dim3((B * KH + U.ng_l - 1) / U.ng_l, K > 0 ? 2 : 1, n), dim3(RD_THREADS),
-                                          args, rp_pred_lds(h), st));
-            else
-                MZ_TRY(h, hipLaunchKernel(nb1 ? (const void*)mz_runroll_pred_n1 : (const void*)mz_runroll_pred_n,
-                                          dim3((B * KH + U.ng_l - 1) / U.ng_l, K > 0 ? 2 : 1, n), dim3(RN_THREADS),
-                                          args, h->rn_lds_l, st));
-        }
-        if (e1) MZ_TRY(h, hipEventRecord(e1, st));
-        // 3. the loss terms and per-step folds (Σθ² from the chain launch)
-        LossMultiParams M;
-        std::memset(&M, 0, sizeof(M));
-        M.B = B; M.K = K; M.A = A; M.v_act = MZ_ACT_IDENTITY; M.r_act = MZ_ACT_IDENTITY; M.nlb = nlb; M.L = n;
-        M.s_k1 = s_k1; M.s_tp = s_tp; M.pv = U.pv; M.pp = U.pp; M.pr = U.pr;
-        M.tv = Qk.tv; M.tp = Qk.tpol; M.gs = Qk.gscale;
-        M.terms = h->d_ml_terms + 2 * i0 * s_k1; M.part = C.part;
-        M.counter = h->d_ml_cnt + (size_t)i0 * MZ_MULTI_CNT_STRIDE;
-        M.out = (losses_dev ? losses_dev : h->d_ml_out) + 8 * i0;
-        M.out_last = i0 + n == L ? out_last : nullptr;
-        hipLaunchKernelGGL(gw == 32 ? mz_learner_loss_multi32 : mz_learner_loss_multi, dim3(nlb, n), dim3(MZ_THREADS),
-                           0, st, M);
-        MZ_TRY(h, hipGetLastError());
     }
     const std::string chain = h->rd_chain ? (h->rd_nb == 3 ? "mz_runroll_chain_r3" : "mz_runroll_chain_r")
                                           : nb1 ? "mz_runroll_chain1" : "mz_runroll_chain";
@@ -3887,56 +3898,68 @@ static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, con
     const int T = ti + 1, nU = (B + T - 1) / T;
     static const bool no_xcd = std::getenv("MZ_MULTI_NO_XCD") != nullptr;
     double p1 = h->bp1, p2 = h->bp2;
-    for (int k = 0, i0 = 0; i0 < L; ++k, i0 += Ls) {
-        const int n = std::min(Ls, L - i0), half = k & 1;
-        // 1. the ADAM chain θ_{t+i0} .. θ_{t+i0+n} into bank half k mod 2
+    // chain launches of up to MZ_MULTI_MAX steps (bank half k mod 2), each followed by its steps' unroll
+    // launches of Ls steps (one workgroup per CU)
+    const int Lc = std::min(L, std::max(Ls, MZ_MULTI_MAX / Ls * Ls));
+    for (int k = 0, c0 = 0; c0 < L; ++k, c0 += Lc) {
+        const int nc = std::min(Lc, L - c0), half = k & 1;
+        // 1. the ADAM chain θ_{t+c0} .. θ_{t+c0+nc} into bank half k mod 2
         ChainParams C;
         std::memset(&C, 0, sizeof(C));
-        C.L = n; C.flat = h->d_flat; C.M = h->d_m; C.V = h->d_v; C.netoff = h->d_netoff;
+        C.L = nc; C.flat = h->d_flat; C.M = h->d_m; C.V = h->d_v; C.netoff = h->d_netoff;
         C.inv_tile = h->d_inv_tile; C.inv_small = h->d_inv_small;
         C.Wp = h->d_Wp; C.Bp = h->d_Bp; C.smw = h->d_sm_w; C.smb = h->d_sm_bias;
         C.bank_w = h->d_bank_w + (size_t)half * MZ_MULTI_MAX * h->sm_w_n;
         C.bank_b = h->d_bank_b + (size_t)half * MZ_MULTI_MAX * h->sm_b_n;
         C.bws = h->sm_w_n; C.bbs = h->sm_b_n;
-        C.theta = theta_dev ? theta_dev + (size_t)i0 * h->nflat : nullptr;
-        C.nflat = h->nflat; C.part = h->d_ml_part + (size_t)i0 * 3 * MZ_L2_BLOCKS;
-        for (int i = 0; i < n; ++i) {               // adam_advance's products, step by step
-            C.bp1[i] = p1; C.bp2[i] = p2; C.eta[i] = eta[i0 + i];
+        C.theta = theta_dev ? theta_dev + (size_t)c0 * h->nflat : nullptr;
+        C.nflat = h->nflat; C.part = h->d_ml_part + (size_t)c0 * 3 * MZ_L2_BLOCKS;
+        for (int i = 0; i < nc; ++i) {              // adam_advance's products, step by step
+            C.bp1[i] = p1; C.bp2[i] = p2; C.eta[i] = eta[c0 + i];
             p1 = p1 * 0.9; p2 = p2 * 0.999;
         }
-        RpSampleParams Qk = Q;                      // this sub-chunk's batches: steps step0 + i0 ..
-        Qk.step = step0 + (uint32_t)i0;
-        Qk.obs += i0 * s_obs; Qk.actions += i0 * s_k1; Qk.tv += i0 * s_k1; Qk.tr += i0 * s_k1;
-        Qk.tpol += i0 * s_tp; Qk.gscale += (size_t)i0 * B; Qk.index += (size_t)i0 * 2 * B;
-        C.B = B; C.q = Qk; C.s_obs = s_obs; C.s_k1 = s_k1; C.s_tp = s_tp;
-        const int nsb = chain_sample ? (n * B + MZ_THREADS / 64 - 1) / (MZ_THREADS / 64) : 0;
+        RpSampleParams Qc = Q;                      // this chunk's batches: steps step0 + c0 ..
+        Qc.step = step0 + (uint32_t)c0;
+        Qc.obs += c0 * s_obs; Qc.actions += c0 * s_k1; Qc.tv += c0 * s_k1; Qc.tr += c0 * s_k1;
+        Qc.tpol += c0 * s_tp; Qc.gscale += (size_t)c0 * B; Qc.index += (size_t)c0 * 2 * B;
+        C.B = B; C.q = Qc; C.s_obs = s_obs; C.s_k1 = s_k1; C.s_tp = s_tp;
+        const int nsb = chain_sample ? (nc * B + MZ_THREADS / 64 - 1) / (MZ_THREADS / 64) : 0;
         hipLaunchKernelGGL(mz_learn_chain, dim3(3 * MZ_L2_BLOCKS + nsb), dim3(MZ_THREADS), 0, st, C);
         MZ_TRY(h, hipGetLastError());
-        // 2. the n unrolls (with their get_batch), loss terms and per-step folds
-        LearnMultiParams M;
-        std::memset(&M, 0, sizeof(M));
-        M.L = n; M.nU = nU;
-        M.xcd = !no_xcd && n > 1;
-        M.bank_w = C.bank_w; M.bank_b = C.bank_b; M.bws = h->sm_w_n; M.bbs = h->sm_b_n;
-        M.s_obs = s_obs; M.s_k1 = s_k1; M.s_tp = s_tp;
-        M.obs = Qk.obs; M.act = Qk.actions; M.tv = Qk.tv; M.tp = Qk.tpol; M.gs = Qk.gscale;
-        M.pv = h->d_ml_pv + i0 * s_k1; M.pp = h->d_ml_pp + i0 * s_tp; M.pr = h->d_ml_pr + i0 * s_k1;
-        M.terms = h->d_ml_terms + 2 * i0 * s_k1;
-        M.part = C.part; M.counter = h->d_ml_cnt + (size_t)i0 * MZ_MULTI_CNT_STRIDE;
-        M.out = (losses_dev ? losses_dev : h->d_ml_out) + 8 * i0;
-        M.out_last = i0 + n == L ? out_last : nullptr;
-        M.sample = chain_sample ? 0 : 1;
-        M.q = Qk;
-        const int grid = M.xcd ? 8 * ((n + 7) / 8) * nU : n * nU;
-        void* args[] = {&U, &M};
-        hipEvent_t e0 = nullptr, e1 = nullptr;     // mz_debug_enable flag 4: the unroll launch's duration
-        if (h->time_unroll) {
-            if (timing_events(h, &e0, &e1)) return -1;
-            MZ_TRY(h, hipEventRecord(e0, st));
+        for (int j0 = 0; j0 < nc; j0 += Ls) {
+            const int n = std::min(Ls, nc - j0), i0 = c0 + j0;
+            RpSampleParams Qk = Q;                  // steps step0 + i0 ..
+            Qk.step = step0 + (uint32_t)i0;
+            Qk.obs += i0 * s_obs; Qk.actions += i0 * s_k1; Qk.tv += i0 * s_k1; Qk.tr += i0 * s_k1;
+            Qk.tpol += i0 * s_tp; Qk.gscale += (size_t)i0 * B; Qk.index += (size_t)i0 * 2 * B;
+            // 2. the n unrolls (with their get_batch), loss terms and per-step folds
+            LearnMultiParams M;
+            std::memset(&M, 0, sizeof(M));
+            M.L = n; M.nU = nU;
+            M.xcd = !no_xcd && n > 1;
+            M.bank_w = C.bank_w + (size_t)j0 * h->sm_w_n; M.bank_b = C.bank_b + (size_t)j0 * h->sm_b_n;
+            M.bws = h->sm_w_n; M.bbs = h->sm_b_n;
+            M.s_obs = s_obs; M.s_k1 = s_k1; M.s_tp = s_tp;
+            M.obs = Qk.obs; M.act = Qk.actions; M.tv = Qk.tv; M.tp = Qk.tpol; M.gs = Qk.gscale;
+            M.pv = h->d_ml_pv + i0 * s_k1; M.pp = h->d_ml_pp + i0 * s_tp; M.pr = h->d_ml_pr + i0 * s_k1;
+            M.terms = h->d_ml_terms + 2 * i0 * s_k1;
+            M.part = h->d_ml_part + (size_t)i0 * 3 * MZ_L2_BLOCKS;
+            M.counter = h->d_ml_cnt + (size_t)i0 * MZ_MULTI_CNT_STRIDE;
+            M.out = (losses_dev ? losses_dev : h->d_ml_out) + 8 * i0;
+            M.out_last = i0 + n == L ? out_last : nullptr;
+            M.sample = chain_sample ? 0 : 1;
+            M.q = Qk;
+            const int grid = M.xcd ? 8 * ((n + 7) / 8) * nU : n * nU;
+            void* args[] = {&U, &M};
+            hipEvent_t e0 = nullptr, e1 = nullptr; // mz_debug_enable flag 4: the unroll launch's duration
+            if (h->time_unroll) {
+                if (timing_events(h, &e0, &e1)) return -1;
+                MZ_TRY(h, hipEventRecord(e0, st));
+            }
+            MZ_TRY(h, hipLaunchKernel(ti == 0 ? (const void*)mz_learn_multi1 : (const void*)mz_learn_multi2,
+                                      dim3(grid), dim3(SM_THREADS), args, unroll_small_lds(h, ti), st));
+            if (e1) MZ_TRY(h, hipEventRecord(e1, st));
         }
-        MZ_TRY(h, hipLaunchKernel(ti == 0 ? (const void*)mz_learn_multi1 : (const void*)mz_learn_multi2, dim3(grid),
-                                  dim3(SM_THREADS), args, unroll_small_lds(h, ti), st));
-        if (e1) MZ_TRY(h, hipEventRecord(e1, st));
     }
     h->last_lvariant = ti == 0 ? "mz_learn_chain+mz_learn_multi1" : "mz_learn_chain+mz_learn_multi2";
     for (int i = 0; i < L; ++i) adam_advance(h);

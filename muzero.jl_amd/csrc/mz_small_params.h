@@ -140,7 +140,8 @@ struct LearnParams {
 //    unroll and the loss terms; the last workgroup of step i folds step i's
 //    losses with the chain launch's Σθ² partials.  (MZ_MULTI_CHAIN_SAMPLE=1:
 //    the chain launch draws the L batches in blocks after its slices instead.)
-#define MZ_MULTI_MAX 16           // steps per sub-chunk (one chain + one unroll launch)
+#define MZ_MULTI_MAX 32           // steps per chain launch (a bank half holds their images)
+#define MZ_MULTI_UNROLL 16        // steps per unroll launch (FC: one workgroup per CU at B = 32, T = 2)
 #define MZ_MULTI_LMAX 256         // steps per mz_learner_train_multi_dev call
 #define MZ_MULTI_CNT_STRIDE 32   // per-step fold counters on their own 128-byte lines
 struct ChainParams {
