@@ -124,39 +124,59 @@ __device__ __forceinline__ void ds_conv_valu(const DsLayer& L, ds_lptr in, ds_lp
     constexpr int K = 9 * CIN, KQ = 4 * ((K + 15) / 16);
     const int Wi = L.Wi, Hi = L.Hi, Wo = L.Wo, Po = Wo * L.Ho, Pi = Wi * Hi;
     const bool bn = L.bn != 0, relu = L.act == MZ_ACT_RELU, has_res = L.res_add != 0;
-    for (int p = threadIdx.x; p < Po; p += blockDim.x) {
-        asm volatile("" ::: "memory");                  // the weights re-read per position, not K·COUT live values
-        const int oh = p / Wo, ow = p - oh * Wo;
-        bool okx[3], oky[3];
+    // two positions per pass (p, p + blockDim): each weight read (an LDS
+    // broadcast) feeds both positions' chains, and one position's taps load
+    // under the other's fmas (a position past the layer computes on zeros,
+    // stores nothing)
+    const int nt = blockDim.x, pe = Po;
+    for (int pa = (int)threadIdx.x; pa < pe; pa += 2 * nt) {
+        asm volatile("" ::: "memory");                  // the weights re-read per pass, not K·COUT live values
+        int pp[2];
+        bool pin[2];
+        float x[2][K];
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {                   // tap i (j): dx (dy) = 1 - i (1 - j)
-            okx[t] = (unsigned)(S * ow + 1 - t) < (unsigned)Wi;
-            oky[t] = (unsigned)(S * oh + 1 - t) < (unsigned)Hi;
-        }
-        const int base = (S * oh) * Wi + S * ow;
-        float x[K];
+        for (int h = 0; h < 2; ++h) {
+            pp[h] = pa + h * nt;
+            pin[h] = pp[h] < pe;
+            const int pc = pin[h] ? pp[h] : pa, oh = pc / Wo, ow = pc - oh * Wo;
+            bool okx[3], oky[3];
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int i = k % 3, j = (k / 3) % 3, c = k / 9;
-            const bool ok = okx[i] & oky[j];
-            const float v = in[ok ? base + c * Pi + (1 - j) * Wi + (1 - i) : 0];
-            x[k] = ok ? v : 0.0f;
+            for (int t = 0; t < 3; ++t) {               // tap i (j): dx (dy) = 1 - i (1 - j)
+                okx[t] = pin[h] & ((unsigned)(S * ow + 1 - t) < (unsigned)Wi);
+                oky[t] = (unsigned)(S * oh + 1 - t) < (unsigned)Hi;
+            }
+            const int base = (S * oh) * Wi + S * ow;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int i = k % 3, j = (k / 3) % 3, c = k / 9;
+                const bool ok = okx[i] & oky[j];
+                const float v = in[ok ? base + c * Pi + (1 - j) * Wi + (1 - i) : 0];
+                x[h][k] = ok ? v : 0.0f;
+            }
         }
 #pragma unroll
         for (int co = 0; co < COUT; ++co) {
-            float part[4];
+            float part[2][4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                float acc = 0.0f;
+                float a0 = 0.0f, a1 = 0.0f;
 #pragma unroll
-                for (int k = q * KQ; k < (q + 1) * KQ && k < K; ++k) acc = __builtin_fmaf(pw[K * co + k], x[k], acc);
-                part[q] = acc;
+                for (int k = q * KQ; k < (q + 1) * KQ && k < K; ++k) {
+                    const float wk = pw[K * co + k];
+                    a0 = __builtin_fmaf(wk, x[0][k], a0);
+                    a1 = __builtin_fmaf(wk, x[1][k], a1);
+                }
+                part[0][q] = a0; part[1][q] = a1;
             }
-            float t = ((part[0] + part[1]) + (part[2] + part[3])) + pw[K * COUT + co];
-            if (bn) t = pw[K * COUT + 2 * COUT + co] * ((t - 0.0f) / bn_s) + pw[K * COUT + COUT + co];
-            const int o = co * Po + p;
-            if (has_res) t = t + res[o];
-            out[o] = relu ? mz_relu(t) : t;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (!pin[h]) continue;
+                float t = ((part[h][0] + part[h][1]) + (part[h][2] + part[h][3])) + pw[K * COUT + co];
+                if (bn) t = pw[K * COUT + 2 * COUT + co] * ((t - 0.0f) / bn_s) + pw[K * COUT + COUT + co];
+                const int o = co * Po + pp[h];
+                if (has_res) t = t + res[o];
+                out[o] = relu ? mz_relu(t) : t;
+            }
         }
     }
 }
