@@ -3653,7 +3653,7 @@ static int multi_plan(const mz_handle* h, int B, int L, int* Ls) {
     else return -1;
     const int nU = (B + ti) / (ti + 1);
     int ls = std::max(1, std::min(MZ_MULTI_UNROLL, h->n_cu / nU));
-    if (ls_env > 0) ls = std::min(MZ_MULTI_UNROLL, ls_env);
+    if (ls_env > 0) ls = std::min(MZ_MULTI_MAX, ls_env);          // (A/B: more than one workgroup per CU)
     *Ls = std::min(ls, L);
     return ti;
 }
