@@ -60,8 +60,14 @@ __device__ __forceinline__ float bp_dt(const BpApp& P, const float* __restrict__
 
 // One 16-row block of a 16-sample MFMA GEMM, C[r][s] = Σ_k A(r, k) B(k, s),
 // its operands gathered BP_KC k-steps at a time (all loads of a chunk in
-// flight before its MFMAs: one memory latency per chunk, not per k-step)
+// flight before its MFMAs: one memory latency per chunk, not per k-step).
+// BP_SKIP: a chunk's groups of 4 k-steps past nk (wave-uniform; their operands
+// are zeros, adding nothing) skip their MFMAs — the nets' 27- / 36-row inputs
+// and 27 / 9 / 1-row outputs fill 7, 9, 7, 3 or 1 of the chunk's 16 k-steps
 #define BP_KC 16
+#ifndef BP_SKIP
+#define BP_SKIP 1
+#endif
 template <class FA, class FB>
 __device__ __forceinline__ bp_f32x4 bp_gemm_block(int nk, int kq, FA fa, FB fb) {
     bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -73,8 +79,18 @@ __device__ __forceinline__ bp_f32x4 bp_gemm_block(int nk, int kq, FA fa, FB fb) 
             a[j] = k0 + j < nk ? fa(k) : 0.0f;
             b[j] = k0 + j < nk ? fb(k) : 0.0f;
         }
+#if BP_SKIP
+#pragma unroll
+        for (int q = 0; q < BP_KC; q += 4) {
+            if (k0 + q < nk) {
+#pragma unroll
+                for (int j = q; j < q + 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+            }
+        }
+#else
 #pragma unroll
         for (int j = 0; j < BP_KC; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+#endif
     }
     return acc;
 }
@@ -221,8 +237,18 @@ __device__ __forceinline__ bp_f32x4 bp_gemm_block_pre(int nk, int kq, const floa
             a[j] = k0 == 0 ? a0[j] : k0 + j < nk ? fa(k) : 0.0f;
             b[j] = k0 + j < nk ? fb(k) : 0.0f;
         }
+#if BP_SKIP
+#pragma unroll
+        for (int q = 0; q < BP_KC; q += 4) {
+            if (k0 + q < nk) {
+#pragma unroll
+                for (int j = q; j < q + 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+            }
+        }
+#else
 #pragma unroll
         for (int j = 0; j < BP_KC; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+#endif
     }
     return acc;
 }
@@ -564,24 +590,41 @@ __device__ void bp_heads(const BpParams& Q, float* T, float* G) {
 }
 
 // Σ over tiles, applications and samples of dZ ⊗ x for one 16x16 dW block
-// (BN: dZ ⊙ γ/√(1+ε); compile-time, so the default nets' loop has no factor)
+// (BN: dZ ⊙ γ/√(1+ε); compile-time, so the default nets' loop has no factor).
+// The (tile, application) pairs run in groups of BP_DW_U: a group's operand
+// loads are all issued before its MFMAs (one memory latency per group, not
+// per pair), the MFMAs in the same ascending order
+#ifndef BP_DW_U
+#define BP_DW_U 4
+#endif
 template <bool BN>
 __device__ __forceinline__ bp_f32x4 bp_dw_acc(const BpDwParams& Q, const BpLayer& L, int o, int i, bool oin, bool iin,
                                               int kq) {
     const float gr = BN && oin ? Q.flat[L.bn_off + L.out + o] / MZ_BN_S : 1.0f;
     bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t < Q.tiles; ++t) {
-        const float* gt = Q.grad + (size_t)t * Q.tile_floats;
-        const float* at = Q.act + (size_t)t * Q.tile_floats;
-        for (int u = 0; u < L.n_use; ++u) {
-            const BpUse U = Q.uses[L.use0 + u];
+    const int nu = L.n_use, nn = Q.tiles * nu;
+    for (int n0 = 0; n0 < nn; n0 += BP_DW_U) {
+        float a[BP_DW_U][4], b[BP_DW_U][4];
+#pragma unroll
+        for (int q = 0; q < BP_DW_U; ++q) {
+            const bool ok = n0 + q < nn;
+            const int n = ok ? n0 + q : 0, t = n / nu;        // (past the end: pair 0, its values unused)
+            const BpUse U = Q.uses[L.use0 + n - t * nu];
+            const float* gt = Q.grad + (size_t)t * Q.tile_floats;
+            const float* at = Q.act + (size_t)t * Q.tile_floats;
 #pragma unroll
             for (int c = 0; c < 4; ++c) {                     // K = the 16 samples, 4 per MFMA
                 const int e = U.y + o * 16 + 4 * c + kq;
-                const float dz = oin ? bp_dz(L.act, gt[e], at[e]) : 0.0f;
-                const float a = BN ? dz * gr : dz;
-                const float b = iin ? at[U.x + i * 16 + 4 * c + kq] : 0.0f;
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+                const float dz = ok && oin ? bp_dz(L.act, gt[e], at[e]) : 0.0f;
+                a[q][c] = BN ? dz * gr : dz;
+                b[q][c] = ok && iin ? at[U.x + i * 16 + 4 * c + kq] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < BP_DW_U; ++q) {
+            if (n0 + q < nn) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][c], b[q][c], acc, 0, 0, 0);
             }
         }
     }
@@ -596,28 +639,37 @@ template <bool BN>
 __device__ __forceinline__ double bp_db(const BpDwParams& Q, const BpLayer& L, int o) {
     const float gr = BN ? Q.flat[L.bn_off + L.out + o] / MZ_BN_S : 1.0f;
     float s = 0.0f, sbe = 0.0f, sga = 0.0f;
-    for (int t = 0; t < Q.tiles; ++t)
-        for (int u = 0; u < L.n_use; ++u) {
-            const BpUse U = Q.uses[L.use0 + u];
+    const int nu = L.n_use, nn = Q.tiles * nu;
+    for (int n0 = 0; n0 < nn; n0 += 2) {                      // two (tile, application) pairs' loads at once
+        float g[2][16], y[2][16], z[2][16];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const bool ok = n0 + q < nn;
+            const int n = ok ? n0 + q : 0, t = n / nu;        // (past the end: pair 0, its values unused)
+            const BpUse U = Q.uses[L.use0 + n - t * nu];
             const size_t e = (size_t)t * Q.tile_floats + U.y + o * 16;
             const size_t ez = (size_t)t * Q.tile_floats + U.z + o * 16;
-            float g[16], y[16], z[16];
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
-                g[j] = Q.grad[e + j];
-                y[j] = Q.act[e + j];
-                z[j] = BN ? Q.act[ez + j] : 0.0f;
+                g[q][j] = ok ? Q.grad[e + j] : 0.0f;
+                y[q][j] = ok ? Q.act[e + j] : 0.0f;
+                z[q][j] = BN && ok ? Q.act[ez + j] : 0.0f;
             }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            if (n0 + q >= nn) break;
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
-                const float du = bp_dz(L.act, g[j], y[j]);
+                const float du = bp_dz(L.act, g[q][j], y[q][j]);
                 s += BN ? du * gr : du;
                 if (BN) {
                     sbe += du;
-                    sga += du * (z[j] / MZ_BN_S);
+                    sga += du * (z[q][j] / MZ_BN_S);
                 }
             }
         }
+    }
     const float th = Q.flat[L.b_off + o];
     Q.out[L.b_off + o] = s;                                   // data term (2θ: mz_adam_kernel)
     double q = (double)th * (double)th;
