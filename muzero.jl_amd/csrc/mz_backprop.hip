@@ -341,13 +341,15 @@ __device__ __forceinline__ void bp_c_fwd_blk(const BpApp& P, const float* __rest
                                              int ob) {
     const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
     const float* W = flat + P.w_off;
-    const float* X = P.xs >= 0 ? C + P.xs : T + P.x;
     const int nk = (P.in + 3) >> 2;
     const int o = ob * 16 + m;
     const bool oin = o < P.out;
-    const bp_f32x4 acc = bp_gemm_block(nk, kq,
-        [&](int i) { return oin && i < P.in ? W[o + (size_t)P.out * i] : 0.0f; },
-        [&](int i) { return i < P.in ? X[i * 16 + m] : 0.0f; });
+    auto fa = [&](int i) { return oin && i < P.in ? W[o + P.out * i] : 0.0f; };
+    // the input from its LDS copy or the arena: one branch, so each side's
+    // loads are LDS or global ones (not generic loads waiting on both counters)
+    const bp_f32x4 acc =
+        P.xs >= 0 ? bp_gemm_block(nk, kq, fa, [&](int i) { return i < P.in ? C[P.xs + i * 16 + m] : 0.0f; })
+                  : bp_gemm_block(nk, kq, fa, [&](int i) { return i < P.in ? T[P.x + i * 16 + m] : 0.0f; });
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int oo = ob * 16 + kq * 4 + r;
@@ -364,20 +366,63 @@ __device__ __forceinline__ void bp_c_dx_blk(const BpApp& P, const float* __restr
                                             float* C, int ib) {
     const int lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
     const float* W = flat + P.w_off;
-    const float* DY = P.gys >= 0 ? C + P.gys : G + P.y;
-    const float* Y = T + P.y;
     const bool wout = P.gys >= 0 && ib == 0;                  // the copy's final value to the arena (mz_bp_dw)
     const int nk = (P.out + 3) >> 2;
     const int i = ib * 16 + m;
     const bool iin = i < P.in;
-    const bp_f32x4 acc = bp_gemm_block(nk, kq,
-        [&](int o) { return iin && o < P.out ? W[o + (size_t)P.out * i] : 0.0f; },
-        [&](int o) {
-            if (o >= P.out) return 0.0f;
-            const float g = DY[o * 16 + m];
-            if (wout) G[P.y + o * 16 + m] = g;
-            return MAYBN ? bp_dt(P, flat, o, g, Y[o * 16 + m]) : bp_dt<false>(P, flat, o, g, Y[o * 16 + m]);
-        });
+    // per k-chunk: every operand load issued first (W, y from the arena, ∂L/∂y
+    // from its LDS copy or the arena, on one branch), the copy's write-out to
+    // the arena after them, then the MFMAs (a store among the loads made each
+    // k-step wait for the previous one's loads: one memory latency per k-step)
+    bp_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < nk; k0 += BP_KC) {
+        float a[BP_KC], g[BP_KC], y[BP_KC], b[BP_KC];
+#pragma unroll
+        for (int j = 0; j < BP_KC; ++j) {
+            const int o = (k0 + j) * 4 + kq;
+            const bool ok = k0 + j < nk && o < P.out;
+            a[j] = ok && iin ? W[o + P.out * i] : 0.0f;          // (32-bit offsets from uniform bases)
+            y[j] = ok ? T[P.y + o * 16 + m] : 0.0f;
+        }
+        if (P.gys >= 0) {
+#pragma unroll
+            for (int j = 0; j < BP_KC; ++j) {
+                const int o = (k0 + j) * 4 + kq;
+                g[j] = k0 + j < nk && o < P.out ? C[P.gys + o * 16 + m] : 0.0f;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < BP_KC; ++j) {
+                const int o = (k0 + j) * 4 + kq;
+                g[j] = k0 + j < nk && o < P.out ? G[P.y + o * 16 + m] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < BP_KC; ++j) {
+            const int o = (k0 + j) * 4 + kq;
+            b[j] = k0 + j < nk && o < P.out
+                       ? (MAYBN ? bp_dt(P, flat, o, g[j], y[j]) : bp_dt<false>(P, flat, o, g[j], y[j])) : 0.0f;
+        }
+        if (wout) {
+#pragma unroll
+            for (int j = 0; j < BP_KC; ++j) {
+                const int o = (k0 + j) * 4 + kq;
+                if (k0 + j < nk && o < P.out) G[P.y + o * 16 + m] = g[j];
+            }
+        }
+#if BP_SKIP
+#pragma unroll
+        for (int q = 0; q < BP_KC; q += 4) {
+            if (k0 + q < nk) {
+#pragma unroll
+                for (int j = q; j < q + 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+            }
+        }
+#else
+#pragma unroll
+        for (int j = 0; j < BP_KC; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+#endif
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int ii = ib * 16 + kq * 4 + r;
@@ -511,9 +556,9 @@ __device__ __forceinline__ void bp_tile_lv_body(const BpParams& Q) {
     int* blev = flev + Q.n_flev + 2;
     int* fsy = blev + Q.n_blev + 2;
     int* bsy = fsy + Q.n_flev + 2;
-    float* C = Q.cache_floats > 0
-                   ? reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(bsy + Q.n_blev + 2) + 15) & ~(uintptr_t)15)
-                   : nullptr;
+    // (an offset from bp_lds, not an integer round trip: the cache accesses stay LDS instructions)
+    const int c_off = ((int)(bsy + Q.n_blev + 2 - bp_lds) + 3) & ~3;
+    float* C = Q.cache_floats > 0 ? reinterpret_cast<float*>(bp_lds + c_off) : nullptr;
     for (int i = threadIdx.x; i < Q.n_flev; i += blockDim.x) fsy[i] = Q.fsync[i];
     for (int i = threadIdx.x; i < Q.n_blev; i += blockDim.x) bsy[i] = Q.bsync[i];
     for (int i = threadIdx.x; i < Q.n_app; i += blockDim.x) apps[i] = Q.apps[i];
