@@ -701,9 +701,10 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
 // = leaf value, v_in(d-1) = R_d + γ·v_in(d), which the sequential loop
 // evaluates node by node.  Here the lanes first stage R_d (node d's reward)
 // in `rr`, every lane runs the same f32 chain over the staged values (two
-// ops per level, no memory on the critical path) and lane 0 stores v_in(d)
-// in `vin`; then each lane updates its own levels as the sequential loop
-// would (W + v, N + 1, q = W/N, R + γq).  Same f32 operations, same results;
+// ops per level, no memory on the critical path; round 5: GW rewards per LDS
+// wait and v_in kept in registers, +0.7 % on configs[4], tools/gpu_r05y.sh)
+// and stores v_in(d) in `vin`; then each lane updates its own levels as the
+// sequential loop would (W + v, N + 1, q = W/N, R + γq).  Same f32 operations, same results;
 // `rr`/`vin` hold depth + 1 floats (LDS, this group's own).
 template <int GW>
 __device__ __forceinline__ void backup_path_1p(const TreeView& t, const int* path, int depth, float value,
@@ -714,19 +715,27 @@ __device__ __forceinline__ void backup_path_1p(const TreeView& t, const int* pat
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
     float v = value;
-    if (a == 0) vin[depth] = v;
-    int d = depth;
-    for (; d >= 4; d -= 4) {                         // four staged rewards per LDS wait
-        const float r0 = rr[d], r1 = rr[d - 1], r2 = rr[d - 2], r3 = rr[d - 3];
-        const float v0 = r0 + discount * v;
-        const float v1 = r1 + discount * v0;
-        const float v2 = r2 + discount * v1;
-        v = r3 + discount * v2;
-        if (a == 0) { vin[d - 1] = v0; vin[d - 2] = v1; vin[d - 3] = v2; vin[d - 4] = v; }
-    }
-    for (; d >= 1; --d) {
-        v = rr[d] + discount * v;
-        if (a == 0) vin[d - 1] = v;
+    // GW levels per LDS wait: the group's staged rewards of levels cGW ..
+    // cGW+GW-1 as one broadcast batch, the chain over registers, lane l
+    // keeping v_in(cGW + l) by a select beside the chain (one store per batch
+    // instead of one per level).  Levels outside 1..depth leave v as it is.
+    for (int c = depth / GW; c >= 0; --c) {
+        float r[GW];
+        const float4* r4 = reinterpret_cast<const float4*>(rr + c * GW);
+#pragma unroll
+        for (int q = 0; q < GW / 4; ++q) {
+            const float4 x = r4[q];
+            r[4 * q] = x.x; r[4 * q + 1] = x.y; r[4 * q + 2] = x.z; r[4 * q + 3] = x.w;
+        }
+        float mine = v;
+#pragma unroll
+        for (int l = GW - 1; l >= 0; --l) {
+            const int lv = c * GW + l;
+            mine = a == l ? v : mine;                 // v_in(lv)
+            const float nv = r[l] + discount * v;
+            v = lv >= 1 && lv <= depth ? nv : v;
+        }
+        if (c * GW + a <= depth) vin[c * GW + a] = mine;
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();

@@ -1,8 +1,25 @@
 #!/bin/bash
-# ResNet corrected learner A/B (rbp_conv_dt loads batched): its torch-f64 tests, then base / head alternated
+# Alternating A/B of the configs[4] search-only line: libmz (8 waves per tree-step
+# workgroup) vs libmz_w16 (-DRT_WAVES=16), after the Atari parity subset on
+# the variant.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-cd "$R" && mkdir -p gpurun_out/r05w
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_corrected_resnet_gpu.py tests/test_dp_libmz_gpu.py > gpurun_out/r05w/tests.log 2>&1 || { tail -30 gpurun_out/r05w/tests.log; exit 1; }
-tail -2 gpurun_out/r05w/tests.log
-LIBS="${LIBS:-base head base head}" bash tools/ab_rbp.sh
+cd "$R" && mkdir -p gpurun_out/r5w && export TMPDIR=/tmp
+O=$R/gpurun_out/r5w
+MZ_LIB=$R/muzero.jl_amd/lib/libmz_w16.so timeout -k 10 400 python -u -m pytest tests/test_atari_gpu.py tests/test_bench_launch_gpu.py tests/test_bench_sizes_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread -k "atari or configs4 or depth" > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
+tail -1 $O/t.log
+v() { grep '^{' $1 | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['value']/1e6,3))"; }
+for i in 1 2 3; do
+  for n in base w16; do
+    if [ $n = base ]; then unset MZ_LIB; else export MZ_LIB=$R/muzero.jl_amd/lib/libmz_$n.so; fi
+    timeout -k 10 300 python bench.py --game atari --no-cpu --search-only --steps 3 --warmup 1 > $O/a_${n}_$i.log 2>&1 || { tail -20 $O/a_${n}_$i.log; exit 1; }
+    echo "atari $n $i $(v $O/a_${n}_$i.log)"
+  done
+done
+for i in 1 2; do
+  for n in base w16; do
+    if [ $n = base ]; then unset MZ_LIB; else export MZ_LIB=$R/muzero.jl_amd/lib/libmz_$n.so; fi
+    timeout -k 10 300 python bench.py --game connect4 --net resnet --no-cpu --search-only --steps 3 --warmup 1 > $O/c_${n}_$i.log 2>&1 || { tail -20 $O/c_${n}_$i.log; exit 1; }
+    echo "connect4 $n $i $(v $O/c_${n}_$i.log)"
+  done
+done
