@@ -741,55 +741,6 @@ __device__ __forceinline__ void backup_path_1p(const TreeView& t, const int* pat
     __builtin_amdgcn_wave_barrier();
     float lmin = INFINITY, lmax = -INFINITY;
     int rN = root_N; float rW = root_W;
-#ifdef MZ_BK1P_PRE
-    // BK of this lane's levels per pass, every read issued before any store:
-    // the path's edges are distinct records, so no store of the pass can feed
-    // one of its reads (the compiler cannot know that and serialises them)
-    constexpr int BK = 4;
-    for (int b0 = a; b0 <= depth; b0 += BK * GW) {
-        int ii[BK], cc[BK];
-        float4 edk[BK];
-        float vik[BK], Rk[BK];
-#pragma unroll
-        for (int k = 0; k < BK; ++k) {
-            const int d0 = b0 + k * GW;
-            const bool on = d0 <= depth && d0 > 0;
-            ii[k] = on ? path[2 * d0] : 0;
-            cc[k] = on ? path[2 * d0 + 1] : 0;
-        }
-#pragma unroll
-        for (int k = 0; k < BK; ++k) {
-            const int d0 = b0 + k * GW;
-            const bool on = d0 <= depth;
-            edk[k] = t.e[ii[k]];
-            vik[k] = on ? vin[d0] : 0.0f;
-            Rk[k] = on && d0 > 0 ? rr[d0] : 0.0f;
-        }
-#pragma unroll
-        for (int k = 0; k < BK; ++k) {
-            const int d0 = b0 + k * GW;
-            if (d0 > depth) break;
-            const int i = ii[k];
-            const float4 ed = edk[k];
-            const float vi = vik[k];
-            uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
-            int N; float W, R;
-            if (d0 > 0) { N = (int)(nc & 0xffffu); W = ed.y; R = Rk[k]; }
-            else { N = root_N; W = root_W; R = 0.0f; }
-            W = W + vi; N += 1;
-            const float q = W / (float)N;
-            const float upd = R + discount * q;
-            lmin = lmin < upd ? lmin : upd;
-            lmax = lmax > upd ? lmax : upd;
-            if (d0 > 0) {
-                nc = (nc & 0xffff0000u) | (uint32_t)N;
-                t.nc(i) = nc; t.w(i) = W; t.ev(i) = R + discount * q;
-            } else { rN = N; rW = W; }
-            if (lvl) { lvl[d0] = make_uint2((uint32_t)cc[k], (uint32_t)N); nN[cc[k]] = N; }
-        }
-    }
-    if (false)
-#endif
     for (int d0 = a; d0 <= depth; d0 += GW) {
         const int i = d0 > 0 ? path[2 * d0] : 0;
         const float4 ed = t.e[i];
