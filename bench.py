@@ -412,6 +412,8 @@ def main():
     # batches sampled on the device from this rank's replay shard (§8f-2),
     # gradient bucket all-reduced over RCCL when world > 1
     B, K = args.batch or conf.batch_size, conf.num_unroll_steps
+    # the global batch B is split over the ranks, each drawing B/world samples from its own shard
+    Br = B // world + (1 if rank < B % world else 0)
     learner_sps = lstep_ms = lkern = learner_1step = None
     multi = None
     if not args.search_only:
@@ -422,10 +424,10 @@ def main():
             if world == 1:                                  # get_batch + unroll, losses + ADAM: one launch (FC)
                 eng.learner_train_dev(B, k + 1, cos_schedule(k + 1), losses.data_ptr(), stream=sp)
                 return
-            else:                  # get_batch fused into the unroll; the data term of ∇ exchanged, 2θ added by apply
-                eng.learner_grad_sampled_dev(B, k + 1, grad.data_ptr(), losses.data_ptr(), stream=sp)
-            if world > 1:
-                dist.all_reduce(grad)
+            # get_batch fused into the unroll (B/world samples of this rank's shard); the data term of ∇
+            # exchanged, 2θ added by apply
+            eng.learner_grad_sampled_dev(Br, k + 1, grad.data_ptr(), losses.data_ptr(), stream=sp)
+            dist.all_reduce(grad)
             eng.learner_apply_dev(grad.data_ptr(), 1.0 / world, cos_schedule(k + 1), stream=sp)
 
         for k in range(5):
@@ -472,27 +474,40 @@ def main():
             lkern = eng.learner_variant() if world == 1 else None
             lkern_ms = lstep_ms
         # L consecutive steps per launch pair (mz_learner_train_multi_dev; ref_semantics, Q11: the
-        # update does not read the data and PER-off batches are keyed by the step): the FC headline
-        # learner number on one GPU; the one-step form above stays in the line (learner_steps_per_s_1step)
-        if world == 1 and args.learner_chunk > 1:
+        # update does not read the data and PER-off batches are keyed by the step): the headline learner
+        # number; the one-step form above stays in the line (learner_steps_per_s_1step).  World > 1: every
+        # rank runs the same update on B/world samples of its own shard (the data term of ∇ is zero in
+        # ref_semantics, so no gradient crosses the ranks) and the per-step losses are averaged over the
+        # ranks once per call
+        if args.learner_chunk > 1:
             L = args.learner_chunk
             lm = torch.empty((L, 8), dtype=torch.float32, device=dev)
 
             def lchunk(t0):
-                eng.learner_train_multi_dev(B, t0, [cos_schedule(t0 + i) for i in range(L)], lm.data_ptr(),
+                eng.learner_train_multi_dev(Br, t0, [cos_schedule(t0 + i) for i in range(L)], lm.data_ptr(),
                                             stream=sp)
+                if world > 1:
+                    dist.all_reduce(lm)
+                    lm.div_(world)
 
             for _ in range(2):
                 lchunk(tnext)
                 tnext += L
             torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
             nch = max(4, (args.learner_steps * 8 + L - 1) // L)
             tm0 = time.perf_counter()
             for _ in range(nch):
                 lchunk(tnext)
                 tnext += L
             torch.cuda.synchronize()
-            tm = time.perf_counter() - tm0
+            if world > 1:
+                dist.barrier()
+            tm = torch.tensor([time.perf_counter() - tm0], dtype=torch.float64, device=dev)
+            if world > 1:
+                dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+            tm = float(tm.item())
             eng.sync()
             mev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
             for a, b in mev:
@@ -546,7 +561,7 @@ def main():
         tcs = torch.tensor([time.perf_counter() - tc0], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(tcs, op=dist.ReduceOp.MAX)
-        f_fb = 3 * 2 * B * (net_macs(conf, hyper, 0) + (K + 1) * net_macs(conf, hyper, 1) +
+        f_fb = 3 * 2 * Br * (net_macs(conf, hyper, 0) + (K + 1) * net_macs(conf, hyper, 1) +
                             K * net_macs(conf, hyper, 2))     # forward + backward (dX, dW) ≈ 3x forward
         cms = ev0.elapsed_time(ev1) / ncs
         corrected = {"learner_steps_per_s": round(ncs / float(tcs.item()), 1), "step_ms": round(cms, 5),
@@ -564,27 +579,54 @@ def main():
 
     # ---- actor-learner loop (row a12, self_play! || learning!, Q16): self-play
     # moves with the actors' nets and one learner step per finished game, the
-    # actors refreshed one checkpoint behind (mz_train_run, one GPU)
+    # actors refreshed one checkpoint behind (mz_train_run).  World > 1: each rank
+    # plays its own G games; per move the finished-game counts are summed over the
+    # ranks and every rank takes that many learner steps on B/world samples of its
+    # shard (mz_train_move -> all_reduce -> mz_train_learn), so the replicas stay
+    # identical
     train = None
-    if args.train_moves > 0 and world == 1 and not args.search_only:
+    if args.train_moves > 0 and not args.search_only:
         eng.selfplay_init(env_kind, G, cap)
-        eng.train_init(conf.batch_size)
-        eng.train_run(3, move0=mv, game_offset=rank * G, stream=sp)
+        eng.train_init(Br)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+
+        def train_moves(n, m0):
+            if world == 1:
+                return eng.train_run(n, move0=m0, game_offset=rank * G, stream=sp)
+            tot = 0
+            for m in range(n):
+                cnt.fill_(eng.train_move(m0 + m, game_offset=rank * G, stream=sp))
+                dist.all_reduce(cnt)
+                st_ = eng.train_learn(int(cnt.item()), stream=sp)
+                tot += st_[3]
+            return st_[:3] + (tot,)
+
+        train_moves(3, mv)
         mv += 3
         torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
         tt0 = time.perf_counter()
-        st0 = eng.train_run(args.train_moves, move0=mv, game_offset=rank * G, stream=sp)
+        st0 = train_moves(args.train_moves, mv)
         torch.cuda.synchronize()
-        ttr = time.perf_counter() - tt0
+        ttr = torch.tensor([time.perf_counter() - tt0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(ttr, op=dist.ReduceOp.MAX)
+        ttr = float(ttr.item())
         eng.sync()
         mv += args.train_moves
+        if world > 1:
+            replica_check(eng, world, "train_loop")
         train = {"moves": args.train_moves, "ms_per_move": round(ttr / args.train_moves * 1e3, 4),
-                 "node_expansions_per_s": round(G * S * args.train_moves / ttr, 1),
+                 "node_expansions_per_s": round(world * G * S * args.train_moves / ttr, 1),
                  "learner_steps": st0[3], "learner_steps_per_s": round(st0[3] / ttr, 1),
                  "games_finished": st0[1], "actor_refreshes": st0[2],
                  "schedule": "mz_train_run: one self-play move of all games with the actors' nets, then one "
                              "learner step (B = batch_size, device get_batch) per finished game; actors take "
-                             "the queued nets every checkpoint_interval steps"}
+                             "the queued nets every checkpoint_interval steps; the learner steps of a move run "
+                             "as one multi-step chunk across the refresh points" +
+                             ("; world > 1: mz_train_move, the finished-game count all-reduced, mz_train_learn "
+                              "with B/world samples per rank" if world > 1 else "")}
 
     if rank == 0:
         total_exp = world * G * S * args.steps
@@ -609,7 +651,7 @@ def main():
         lroof = None
         if lkern is not None:
             nparam = sum(int(x.size) for x in nets)
-            f_unroll = 2 * B * (net_macs(conf, hyper, 0) + (K + 1) * net_macs(conf, hyper, 1) +
+            f_unroll = 2 * Br * (net_macs(conf, hyper, 0) + (K + 1) * net_macs(conf, hyper, 1) +
                                 K * net_macs(conf, hyper, 2))
             # ResNet: the timed launch pair is the unroll alone (ADAM runs in the loss kernel after it)
             lflop = f_unroll + (0 if resnet else 10 * nparam)
@@ -617,7 +659,7 @@ def main():
             # once (4 B/param), the batch's observations and actions, and writes value / reward / A logits
             # per (sample, step)
             lbytes = 28 * nparam if not resnet else \
-                4 * nparam + 4 * B * (obs.shape[1] + (K + 1)) + 4 * B * (K + 1) * (A + 2)
+                4 * nparam + 4 * Br * (obs.shape[1] + (K + 1)) + 4 * Br * (K + 1) * (A + 2)
             lbytes_step = 28 * nparam
             if multi:
                 # mz_learn_multi*: L unrolls + loss terms per launch (the ADAM chain runs in mz_learn_chain):
@@ -625,8 +667,8 @@ def main():
                 # targets, gradient_scale) and writes its read-outs and loss terms
                 Lm = multi["steps_per_unroll_launch"]
                 lflop = Lm * f_unroll
-                lbytes = Lm * (4 * nparam + 4 * B * (obs.shape[1] + 2 * (K + 1) + (K + 1) * A + 1) +
-                               4 * B * (K + 1) * (A + 4)) if not resnet else Lm * lbytes
+                lbytes = Lm * (4 * nparam + 4 * Br * (obs.shape[1] + 2 * (K + 1) + (K + 1) * A + 1) +
+                               4 * Br * (K + 1) * (A + 4)) if not resnet else Lm * lbytes
                 # (ResNet: the unroll launches per step as the one-step form; the losses run after them)
             lach = lflop / (lkern_ms * 1e-3) / 1e12
             ltraffic, ltraffic_src, lpmc = pmc_record(lkern, pmc_line)
@@ -656,7 +698,8 @@ def main():
                      "learner batches sampled on the device from the self-play replay shard"),
             "config": {"workload": workload(game, resnet, G, S),
                        "games_per_gpu": G, "sims_per_move": S, "global_games": G * world,
-                       "parallelism": f"games sharded x{world}, learner dp{world} (RCCL all-reduce)"},
+                       "parallelism": f"games sharded x{world}, learner dp{world} (global batch {B}, "
+                                      f"{B // world}{'+' if B % world else ''} samples per rank)"},
             "learner_steps_per_s": round(learner_sps, 1) if learner_sps else None,
             "learner_steps_per_s_1step": round(learner_1step, 1) if learner_1step else None,
             "learner_multi": multi,
@@ -665,7 +708,11 @@ def main():
             "learner_roofline": lroof,
             "learner_corrected": corrected,
             "train_loop": train,
-            "learner_config": {"batch_size": B, "num_unroll_steps": K, "mode": "ref_semantics",
+            "learner_config": {"batch_size": B, "batch_per_rank": Br, "num_unroll_steps": K, "mode": "ref_semantics",
+                               "note": ("learner_steps_per_s is the multi-step form (learner_multi), valid because "
+                                        "in ref_semantics the update θ <- ADAM(θ, 2θ) reads no data (Q11); "
+                                        "learner_steps_per_s_1step is the one-step form, the rounds 1-4 metric"
+                                        if multi else None),
                                "form": (f"mz_learner_train_multi_dev: {multi['steps_per_call']} consecutive steps "
                                         f"per call, {multi['steps_per_unroll_launch']:g} per unroll launch "
                                         f"({multi['kernels']}); the one-step form (mz_learner_train_dev) in "
@@ -675,6 +722,9 @@ def main():
                                  "set (step t's was drawn by the previous launch)" if not resnet else
                                  "mz_learner_train_dev: device get_batch + make_target, ResNet unroll chain + "
                                  "predictions, losses with ADAM") if world == 1 else
+                                "multi-step form: mz_learner_train_multi_dev on B/world samples of each rank's "
+                                "shard, the per-step losses all-reduced once per call (the data term of the "
+                                "gradient is zero in ref_semantics); one-step form and corrected mode: "
                                 "mz_learner_grad_sampled_dev (device get_batch fused into the unroll) + RCCL "
                                 "all-reduce + mz_learner_apply_dev")},
             "selfplay_pipeline": pipe,

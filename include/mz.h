@@ -376,15 +376,19 @@ int mz_learner_train_dev(mz_handle* h, int32_t B, uint32_t step, double eta, flo
  * step0+L-1, eta[i] the learning rate of step step0+i (host array): the
  * results of L mz_learner_train_dev calls, bit for bit.  In ref_semantics
  * (Q11) the update θ_{s+1} = ADAM(θ_s, 2θ_s) does not read the data, and with
- * PER off step s's batch is keyed by s, so the FC engine runs the L ADAM
- * iterations in one launch and the L unrolls + losses side by side in a
- * second (L·B workgroups instead of B); any other configuration (ResNet, the
- * corrected mode, PER) runs the L steps one after another.  losses_dev:
+ * PER off step s's batch is keyed by s, so the engine runs the ADAM
+ * iterations of many steps in one launch and their unrolls + losses side by
+ * side (L·B workgroups instead of B).  losses_dev:
  * NULL or [L][8] (per step the six losses of mz_learner_train_dev);
  * theta_dev: NULL or [L][nflat], the flat parameters (Flux order, the
  * mz_weights_get layout of all three nets back to back) after each step.
- * 1 <= L <= 256: the steps run in sub-chunks of up to 16 (one ADAM launch
- * and one unroll launch each).  Replaces L iterations of the learner loop. */
+ * 1 <= L <= 256.  FC: chain launches (mz_learn_chain: the ADAM iterations,
+ * each step's θ scattered into its own image in a bank, Σθ² per step, the
+ * batches) of up to 32 steps, each followed by unroll launches
+ * (mz_learn_multi*) of up to 16 steps side by side; ResNet: the same chain
+ * launches feeding the mz_runroll_* launches with the steps on gridDim.z
+ * (rlearner_multi).  The corrected mode and PER run the L steps one after
+ * another.  Replaces L iterations of the learner loop.                      */
 int mz_learner_train_multi_dev(mz_handle* h, int32_t B, uint32_t step0, int32_t L, const double* eta,
                                float* losses_dev, float* theta_dev, void* stream);
 
@@ -445,17 +449,31 @@ int mz_selfplay_slots(mz_handle* h, int32_t* history_len, uint8_t* board, int32_
  *     (SelfPlay.jl:399-401).  Reads the shard's game counter back once per
  *     move (one sync).  state_out[4] = {t, num_played_games, actor refreshes,
  *     learner steps of this call}; losses_dev (device, 6 floats, or NULL) =
- *     the last step's.
+ *     the last step's.  The learner steps of one move run as one
+ *     mz_learner_train_multi_dev chunk across the refresh points (the chain
+ *     launch copies out θ of the last two refresh steps for the actors' and
+ *     queued sets; with a networks path the chunks end at each refresh).
+ *     Data parallel (after mz_dp_init, world > 1): the move's finished-game
+ *     count is summed over the ranks (RCCL) and every rank takes that many
+ *     learner steps on its own shard, so the ref_semantics replicas stay
+ *     bit-identical.
+ *   mz_train_move / mz_train_learn: the two halves of one mz_train_run move,
+ *     for a host that exchanges the count itself (torch.distributed, a Julia
+ *     Distributed host): mz_train_move plays one move and returns the games it
+ *     saved on this rank (*nfin); mz_train_learn takes `steps` learner steps
+ *     (capped at training_steps) with the refreshes, state_out as above.
  *   mz_train_set_networks_path: conf.networks_path (Constructors.jl:47) for
  *     the periodic checkpoints; NULL or "" (the default) writes none.
  *   mz_train_weights_get: the learner's, actors' or queued nets (Flux order).
- * One GPU (world = 1).  oracle/mz_oracle.c ora_train_loop restates it.      */
+ * oracle/mz_oracle.c ora_train_loop restates it.                            */
 enum { MZ_TRAIN_LEARNER = 0, MZ_TRAIN_ACTOR = 1, MZ_TRAIN_QUEUED = 2 };
 int mz_train_init(mz_handle* h, int32_t batch_size);
 int mz_train_init_at(mz_handle* h, int32_t batch_size, int64_t t0);
 int mz_train_set_networks_path(mz_handle* h, const char* networks_path);
 int mz_train_run(mz_handle* h, int32_t moves, uint32_t move0, uint32_t game_offset, int64_t* state_out,
                  float* losses_dev, void* stream);
+int mz_train_move(mz_handle* h, uint32_t move, uint32_t game_offset, int64_t* nfin, void* stream);
+int mz_train_learn(mz_handle* h, int64_t steps, float* losses_dev, int64_t* state_out, void* stream);
 int mz_train_weights_get(mz_handle* h, int which, int net, float* flat, size_t n);
 
 /* ---- Checkpoints -------------------------------------------

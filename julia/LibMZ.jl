@@ -189,6 +189,20 @@ function train_run!(e::Engine, moves; move0=0, offset=0)
                    e.h, moves, move0, offset, st, C_NULL, C_NULL))
     Tuple(st)
 end
+# the two halves of one train_run! move, for a Distributed.jl host that sums `nfin` over the workers itself:
+# every worker then takes the global count of learner steps (the replicas stay identical, SURVEY §8e)
+function train_move!(e::Engine, move; offset=0)
+    n = zeros(Int64, 1)
+    check(e, ccall((:mz_train_move, libmz), Cint, (Ptr{Cvoid}, UInt32, UInt32, Ptr{Int64}, Ptr{Cvoid}),
+                   e.h, move, offset, n, C_NULL))
+    n[1]
+end
+function train_learn!(e::Engine, steps)
+    st = zeros(Int64, 4)
+    check(e, ccall((:mz_train_learn, libmz), Cint, (Ptr{Cvoid}, Int64, Ptr{Float32}, Ptr{Int64}, Ptr{Cvoid}),
+                   e.h, steps, C_NULL, st, C_NULL))
+    Tuple(st)
+end
 function train_weights(e::Engine, which::Cint, net::Cint)
     flat = similar(get_weights(e, net))
     check(e, ccall((:mz_train_weights_get, libmz), Cint, (Ptr{Cvoid}, Cint, Cint, Ptr{Float32}, Csize_t),

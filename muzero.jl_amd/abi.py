@@ -87,6 +87,8 @@ SIGNATURES = {
     "mz_train_init_at": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_int64]),
     "mz_train_set_networks_path": (ctypes.c_int, [_VP, ctypes.c_char_p]),
     "mz_train_run": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, _VP, _VP, _VP]),
+    "mz_train_move": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32, _VP, _VP]),
+    "mz_train_learn": (ctypes.c_int, [_VP, ctypes.c_int64, _VP, _VP, _VP]),
     "mz_train_weights_get": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP, ctypes.c_size_t]),
     "mz_checkpoint_save": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int64]),
     "mz_checkpoint_load": (ctypes.c_int, [_VP, ctypes.c_char_p, _VP]),
@@ -113,7 +115,10 @@ def load_library(path=LIB_PATH):
     except ImportError:
         pass
     lib = ctypes.CDLL(path)
+    variant = bool(os.environ.get("MZ_LIB")) and path == os.environ.get("MZ_LIB")
     for name, (res, args) in SIGNATURES.items():
+        if variant and not hasattr(lib, name):
+            continue                 # an older A/B variant library (MZ_LIB) without this entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -349,6 +354,20 @@ class Engine:
         st = np.zeros(4, np.int64)
         self._check(self.lib.mz_train_run(self.h, moves, move0, game_offset, _p(st), losses_ptr, stream),
                     "mz_train_run")
+        return tuple(int(x) for x in st)
+
+    def train_move(self, move, game_offset=0, stream=None):
+        """One self-play move of the actor-learner loop with the actors' nets; returns the games it saved
+        (this rank's shard).  A data-parallel host sums that over the ranks and passes it to train_learn."""
+        n = np.zeros(1, np.int64)
+        self._check(self.lib.mz_train_move(self.h, move, game_offset, _p(n), stream), "mz_train_move")
+        return int(n[0])
+
+    def train_learn(self, steps, losses_ptr=None, stream=None):
+        """`steps` learner steps (capped at training_steps) with the actor refreshes; returns
+        (t, num_played_games, actor refreshes, learner steps of this call)."""
+        st = np.zeros(4, np.int64)
+        self._check(self.lib.mz_train_learn(self.h, int(steps), losses_ptr, _p(st), stream), "mz_train_learn")
         return tuple(int(x) for x in st)
 
     def train_weights(self, which, net):

@@ -212,6 +212,7 @@ struct mz_handle {
     long long* d_per_total = nullptr;
     int rs_last_B = 0;                                       // batch size of the last get_batch
     void* dp_comm = nullptr; int dp_world = 0, dp_rank = 0;  // mz_dp_init: RCCL communicator
+    float* d_dp_cnt = nullptr;              // mz_train_run at world > 1: the finished-game count exchange
     char* d_tree = nullptr; size_t tree_game_bytes = 0; bool lds_tree = false; int dump_tree = 0;
     int time_nets = 0;                      // mz_debug_enable flag 2: events around each ResNet nets launch
     int time_unroll = 0;                    // flag 4: events around each ResNet learner unroll launch
@@ -222,6 +223,7 @@ struct mz_handle {
     bool small_ok = false;
     int n_cu = 256;
     int sm_n_sim = 0, sm_n_root = 0;
+    int sm_tail = 0;                        // SmallParams.tail (sm_schedule_tail)
     float* d_sm_w = nullptr;                // [n_sim + n_root][2][256][16] weight image (sim then root)
     float* d_sm_bias = nullptr;             // [n_sim + n_root][2][64]
     // FC engines: a second image set (tile16 W/B, small W/bias) that the one-launch
@@ -390,6 +392,7 @@ static int check_fault(mz_handle* h) {
     std::string m = std::string("device fault: a workgroup waited ") + wait + " for a publish that never came (";
     if (v & MZ_FAULT_RS_TRUNK) m += "mz_rsearch_nets trunk hand-off ";
     if (v & MZ_FAULT_RD_PROGRESS) m += "mz_runroll_fused_r chain progress ";
+    if (v & MZ_FAULT_SM_TAIL) m += "mz_search_small tail reward hand-off ";
     h->err = m + "); the results of the launches since the last synchronisation are invalid (search results, "
                  "games self-play stored from them, losses, read-outs; the ref_semantics weights and ADAM state "
                  "do not read them and stay valid)";
@@ -635,6 +638,60 @@ static bool sm_schedule(const mz_handle* h, const std::vector<int>& set, const s
     return true;
 }
 
+// The tail schedule (round 6): the four head outputs — value (pred head 1),
+// policy (pred head 2), state (dyn head 1), reward (dyn head 2), each the last
+// layer of its chain — alone in the last of SM_MAX_SIM stages, pinned to the
+// waves that consume them in the search (mz_small.hip small_body), one per
+// SIMD where it can be (wave w runs on SIMD w mod 4): value on slot 0 group 0
+// (wave 0: read-outs + backup, SIMD 0 to itself), reward on slot 0 group 1
+// (wave 1, handed to wave 0 through LDS), policy on slot 0 group 2 (wave 2:
+// expand), the state rows on the last groups of slot 1 (waves 8 − nb .. 7,
+// stored straight into the hidden-state store).  The search then runs SM_MAX_SIM − 1 barrier stages and
+// the tail beside the tree phases; the learner runs every stage as before (the
+// same image, the same dot order, so the same bits).  Every other layer is
+// list-scheduled into the first SM_MAX_SIM − 1 stages, which it must fill
+// exactly (so the tail sits on register set SM_MAX_SIM − 1).  Returns the
+// number of state waves, or 0 if the nets do not fit this shape.
+static int sm_schedule_tail(const mz_handle* h, const std::vector<int>& set, const std::vector<std::vector<int>>& deps,
+                            std::vector<int>& st, std::vector<int>& sl, std::vector<int>& b0,
+                            std::vector<std::array<int, 2>>& stage_kq) {
+    if (SM_SLOTS != 2) return 0;
+    const int n = (int)set.size();
+    const int onet[4] = {MZ_NET_PRED, MZ_NET_PRED, MZ_NET_DYN, MZ_NET_DYN};
+    const int och[4] = {CH_HEAD1, CH_HEAD2, CH_HEAD1, CH_HEAD2};
+    const int nbs = (h->layers[h->chains[MZ_NET_DYN][CH_HEAD1].empty() ? 0 : h->chains[MZ_NET_DYN][CH_HEAD1].back()]
+                         .out + 15) / 16;
+    const int oslot[4] = {0, 0, 1, 0}, ogrp[4] = {0, 2, 4 - nbs, 1}, omax[4] = {1, 1, 3, 1};
+    int opos[4];
+    for (int o = 0; o < 4; ++o) {
+        const auto& ch = h->chains[onet[o]][och[o]];
+        if (ch.empty()) return 0;
+        opos[o] = (int)(std::find(set.begin(), set.end(), ch.back()) - set.begin());
+        if (opos[o] >= n || (h->layers[ch.back()].out + 15) / 16 > omax[o]) return 0;
+    }
+    std::vector<int> body, bidx(n, -1);
+    for (int i = 0; i < n; ++i)
+        if (std::find(opos, opos + 4, i) == opos + 4) { bidx[i] = (int)body.size(); body.push_back(i); }
+    std::vector<int> bset;
+    std::vector<std::vector<int>> bdeps;
+    for (int i : body) {
+        bset.push_back(set[i]);
+        bdeps.emplace_back();
+        for (int d : deps[i]) {
+            if (bidx[d] < 0) return 0;                  // (an output feeding another layer)
+            bdeps.back().push_back(bidx[d]);
+        }
+    }
+    std::vector<int> bst, bsl, bb0;
+    if (!sm_schedule(h, bset, bdeps, SM_MAX_SIM - 1, bst, bsl, bb0, stage_kq)) return 0;
+    if ((int)stage_kq.size() != SM_MAX_SIM - 1) return 0;
+    st.assign(n, -1); sl.assign(n, -1); b0.assign(n, -1);
+    for (size_t j = 0; j < body.size(); ++j) { st[body[j]] = bst[j]; sl[body[j]] = bsl[j]; b0[body[j]] = bb0[j]; }
+    for (int o = 0; o < 4; ++o) { st[opos[o]] = SM_MAX_SIM - 1; sl[opos[o]] = oslot[o]; b0[opos[o]] = 4 * ogrp[o]; }
+    stage_kq.push_back({0, 0});
+    return (h->layers[h->chains[MZ_NET_DYN][CH_HEAD1].back()].out + 15) / 16;
+}
+
 static int build_small(mz_handle* h) {
     for (const LayerSpec& L : h->layers)
         if (L.in > 64 || L.out > 64) return 0;          // not eligible: tile-16 kernel only
@@ -659,7 +716,10 @@ static int build_small(mz_handle* h) {
     };
     std::vector<int> st_s, sl_s, b0_s, st_r, sl_r, b0_r;
     std::vector<std::array<int, 2>> kq_s, kq_r;
-    if (!sm_schedule(h, sim, deps_of(sim), SM_MAX_SIM, st_s, sl_s, b0_s, kq_s)) return 0;
+    const char* no_tail = getenv("MZ_NO_TAIL");          // A/B: every stage a barrier stage
+    h->sm_tail = no_tail && *no_tail && *no_tail != '0' ? 0
+                                                        : sm_schedule_tail(h, sim, deps_of(sim), st_s, sl_s, b0_s, kq_s);
+    if (!h->sm_tail && !sm_schedule(h, sim, deps_of(sim), SM_MAX_SIM, st_s, sl_s, b0_s, kq_s)) return 0;
     if (!sm_schedule(h, root, deps_of(root), SM_MAX_ROOT, st_r, sl_r, b0_r, kq_r)) return 0;
     h->sm_n_sim = (int)kq_s.size();
     h->sm_n_root = (int)kq_r.size();
@@ -1926,6 +1986,8 @@ static int search_dev(mz_handle* h, int G, const float* obs, const uint8_t* lega
         Q.w_sim = h->d_sm_w;
         std::memcpy(Q.nzm, h->sm_nzm.data(), sizeof(Q.nzm));
         Q.bn = h->sm_bn;
+        Q.tail = h->sm_tail;
+        Q.fault = h->d_fault;
         Q.zero16 = reinterpret_cast<const float4*>(h->d_zero16);
         Q.w_root = h->d_sm_w + (size_t)h->sm_n_sim * SM_SLOTS * 256 * 16;
         Q.rec = h->d_sm_rec[ti]; Q.bias = h->d_sm_bias;
@@ -3719,8 +3781,21 @@ static bool rmulti_ok(const mz_handle* h) {
            !std::getenv("MZ_RUNROLL_FUSED");
 }
 static int ensure_multi(mz_handle* h, int B, int L);
+// θ after up to two given steps, copied out by the chain launch that computes them (mz_train_run:
+// the actors' and the queued sets at refresh steps inside one learner chunk)
+struct MultiCap {
+    int64_t t[2];                                   // absolute learner steps (< 0: none)
+    float* dst[2];                                  // nflat floats each
+};
+static void set_caps(ChainParams& C, const MultiCap* cap, int64_t first, int nc) {
+    for (int j = 0; j < 2; ++j) {
+        const bool in = cap && cap->t[j] >= first && cap->t[j] < first + nc;
+        C.cap_i[j] = in ? (int)(cap->t[j] - first) : -1;
+        C.cap_dst[j] = in ? cap->dst[j] : nullptr;
+    }
+}
 static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, const double* eta, float* losses_dev,
-                          float* theta_dev, hipStream_t st, float* out_last) {
+                          float* theta_dev, hipStream_t st, float* out_last, const MultiCap* cap) {
     RpSampleParams Q;
     mz_batch b;
     if (rs_params(h, B, step0, st, &Q, &b, true)) return -1;
@@ -3770,6 +3845,7 @@ static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, co
         C.fbank = h->d_fbank + (size_t)half * MZ_MULTI_MAX * h->nflat;
         C.theta = theta_dev ? theta_dev + (size_t)c0 * h->nflat : nullptr;
         C.nflat = h->nflat; C.part = h->d_ml_part + (size_t)c0 * 3 * MZ_L2_BLOCKS;
+        set_caps(C, cap, (int64_t)step0 + c0, nc);
         for (int i = 0; i < nc; ++i) {
             C.bp1[i] = p1; C.bp2[i] = p2; C.eta[i] = eta[c0 + i];
             p1 = p1 * 0.9; p2 = p2 * 0.999;
@@ -3866,9 +3942,9 @@ static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, co
 
 // out_last: also (instead of losses[L-1]) the last step's losses there (mz_train_run)
 static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, const double* eta, float* losses_dev,
-                         float* theta_dev, hipStream_t st, float* out_last = nullptr) {
+                         float* theta_dev, hipStream_t st, float* out_last = nullptr, const MultiCap* cap = nullptr) {
     MZ_TRY(h, hipSetDevice(h->device));
-    if (rmulti_ok(h)) return rlearner_multi(h, B, step0, L, eta, losses_dev, theta_dev, st, out_last);
+    if (rmulti_ok(h)) return rlearner_multi(h, B, step0, L, eta, losses_dev, theta_dev, st, out_last, cap);
     int Ls = 0;
     const int ti = multi_ok(h) ? multi_plan(h, B, L, &Ls) : -1;
     if (ti < 0) {
@@ -3881,7 +3957,11 @@ static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, con
             if (theta_dev)
                 MZ_TRY(h, hipMemcpyAsync(theta_dev + (size_t)i * h->nflat, h->d_flat, h->nflat * 4,
                                          hipMemcpyDeviceToDevice, st));
+            for (int j = 0; j < 2; ++j)
+                if (cap && cap->t[j] == (int64_t)step0 + i)
+                    MZ_TRY(h, hipMemcpyAsync(cap->dst[j], h->d_flat, h->nflat * 4, hipMemcpyDeviceToDevice, st));
         }
+        h->ml_last_L = 0;                           // (no multi-step read-outs: mz_debug_unroll_step refuses)
         return 0;
     }
     RpSampleParams Q;
@@ -3914,6 +3994,7 @@ static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, con
         C.bws = h->sm_w_n; C.bbs = h->sm_b_n;
         C.theta = theta_dev ? theta_dev + (size_t)c0 * h->nflat : nullptr;
         C.nflat = h->nflat; C.part = h->d_ml_part + (size_t)c0 * 3 * MZ_L2_BLOCKS;
+        set_caps(C, cap, (int64_t)step0 + c0, nc);
         for (int i = 0; i < nc; ++i) {              // adam_advance's products, step by step
             C.bp1[i] = p1; C.bp2[i] = p2; C.eta[i] = eta[c0 + i];
             p1 = p1 * 0.9; p2 = p2 * 0.999;
@@ -4078,7 +4159,6 @@ int mz_train_init_at(mz_handle* h, int32_t B, int64_t t0) {
     if (t0 < 0) return fail(h, "the starting training step must be >= 0");
     if (h->sp_env < 0) return fail(h, "mz_selfplay_init first");
     if (B < 1) return fail(h, "batch_size must be >= 1");
-    if (h->dp_world > 1) return fail(h, "mz_train_run is the single-GPU loop (world = 1)");
     if (h->conf.checkpoint_interval < 1) return fail(h, "checkpoint_interval must be >= 1");
     MZ_TRY(h, hipSetDevice(h->device));
     MZ_SYNC(h);
@@ -4105,6 +4185,149 @@ int mz_train_init_at(mz_handle* h, int32_t B, int64_t t0) {
     return 0;
 }
 
+// 1. one self-play move with the actors' nets (SelfPlay.jl:343-380); temperature
+//    visit_softmax_temperature_fn(t) (:48-56, 396-397) for the games that start on
+//    this move (a game in progress keeps its own).  *nfin = the games save_game
+//    stored (slot order, inside the move).  The fault word rides along with the
+//    counter copy: one stream wait per move, no second blocking copy.
+static int train_move(mz_handle* h, uint32_t move, uint32_t game_offset, int64_t* nfin, hipStream_t st) {
+    const float temp = temp_fn(h->tr_t);
+    wset_swap(h, h->tr_actor);
+    h->sp_latch = true;
+    const int rc = mz_selfplay_move(h, move, game_offset, temp, st);
+    h->sp_latch = false;
+    wset_swap(h, h->tr_actor);
+    if (rc) return rc;
+    MZ_TRY(h, hipMemcpyAsync(h->h_tr_cnt, h->d_sp_counters, sizeof(long long), hipMemcpyDeviceToHost, st));
+    h->h_tr_cnt[1] = 0;
+    if (h->d_fault) MZ_TRY(h, hipMemcpyAsync(h->h_tr_cnt + 1, h->d_fault, 4, hipMemcpyDeviceToHost, st));
+    MZ_TRY(h, hipStreamSynchronize(st));
+    if (h->h_tr_cnt[1] && check_fault(h)) return -1;
+    *nfin = h->h_tr_cnt[0] - h->tr_games;
+    h->tr_games = h->h_tr_cnt[0];
+    return 0;
+}
+
+// the actors take the queued nets, the learner's nets are queued (SelfPlay.jl:399-401 /
+// Learning.jl:416-418: one checkpoint behind); past round(0.9 training_steps) the nets
+// go to disk (Learning.jl:427-432, round half to even as Julia's round)
+static int train_refresh(mz_handle* h, int64_t t, hipStream_t st) {
+    MZ_TRY(h, hipMemcpyAsync(h->tr_actor.flat, h->d_tr_queued, h->nflat * 4, hipMemcpyDeviceToDevice, st));
+    if (wset_repack(h, h->tr_actor, st)) return -1;
+    MZ_TRY(h, hipMemcpyAsync(h->d_tr_queued, h->d_flat, h->nflat * 4, hipMemcpyDeviceToDevice, st));
+    ++h->tr_refresh;
+    if (!h->tr_ckpt_path.empty() && (double)t > std::nearbyint(0.9 * (double)h->conf.training_steps)) {
+        MZ_TRY(h, hipStreamSynchronize(st));
+        const std::string path = h->tr_ckpt_path + "/" + std::to_string(t) + ".safetensors";
+        if (mz_checkpoint_save(h, path.c_str(), t)) return -1;
+    }
+    return 0;
+}
+
+// 2. `nreq` learner steps while t <= training_steps (Learning.jl:327), get_batch keyed by
+//    the step number, eta = Cos(step); every checkpoint_interval steps (t % ci == 0, t > 1)
+//    an actor refresh.  Round 6: the steps of one call run as ONE mz_learner_train_multi_dev
+//    chunk across the refresh points (up to 256 steps per call; MZ_TRAIN_L caps it): nothing
+//    reads the actors' or the queued nets between two learner steps of one move, so only
+//    the sets after the last refresh matter — θ of the last refresh step is queued, θ of the
+//    one before it (or, with one refresh, the previously queued nets) goes to the actors, and
+//    the chain launch that computes those θ copies them out (MultiCap).  With periodic
+//    checkpoint files (networks_path) or MZ_TRAIN_PER_REFRESH=1 the chunks end at every
+//    refresh step as in round 5 (the checkpoint writes the learner's nets of that step).
+static int train_learn(mz_handle* h, int64_t nreq, float* losses_dev, hipStream_t st, int64_t* done) {
+    static const int chunk_env = std::getenv("MZ_TRAIN_L") ? std::atoi(std::getenv("MZ_TRAIN_L")) : 0;
+    static const bool per_refresh_env = std::getenv("MZ_TRAIN_PER_REFRESH") != nullptr;
+    const int chunk_max = std::max(1, std::min(MZ_MULTI_LMAX, chunk_env > 0 ? chunk_env : MZ_MULTI_LMAX));
+    const bool per_refresh = per_refresh_env || !h->tr_ckpt_path.empty();
+    const int64_t ci = h->conf.checkpoint_interval;
+    auto is_refresh = [&](int64_t t) { return t % ci == 0 && t > 1; };
+    const int64_t n_all = std::max<int64_t>(0, std::min<int64_t>(nreq, (int64_t)h->conf.training_steps + 1 - h->tr_t));
+    *done = 0;
+    if (n_all == 0) return 0;
+    MultiCap cap{{-1, -1}, {h->tr_actor.flat, h->d_tr_queued}};
+    int64_t nref = 0;
+    if (!per_refresh) {
+        // the refresh steps in (t, t + n]: the last two
+        const int64_t t_lo = h->tr_t, t_hi = h->tr_t + n_all;
+        for (int64_t r = t_hi / ci * ci; r > t_lo && nref < 2; r -= ci)
+            if (is_refresh(r)) { cap.t[1 - nref] = r; ++nref; }
+        const int64_t first = (t_lo / ci + 1) * ci;   // the total count
+        nref = 0;
+        for (int64_t r = first; r <= t_hi; r += ci) nref += is_refresh(r) ? 1 : 0;
+        if (nref == 1) {               // the actors take the nets queued before this call
+            MZ_TRY(h, hipMemcpyAsync(h->tr_actor.flat, h->d_tr_queued, h->nflat * 4, hipMemcpyDeviceToDevice, st));
+            cap.t[0] = -1;
+        }
+    }
+    double eta[MZ_MULTI_LMAX];
+    for (int64_t k = 0; k < n_all;) {
+        const int64_t t0 = h->tr_t + 1;
+        int64_t n = std::min<int64_t>(n_all - k, chunk_max);
+        if (per_refresh) {                                 // the chunk ends at the next refresh step
+            int64_t tb = (t0 + ci - 1) / ci * ci;
+            if (tb <= 1) tb += ci;
+            n = std::min<int64_t>(n, tb - t0 + 1);
+        }
+        const int64_t t = t0 + n - 1;
+        if (n == 1) {
+            if (mz_learner_train_dev(h, h->tr_B, (uint32_t)t, cos_schedule(t), losses_dev, st)) return -1;
+            for (int j = 0; j < 2; ++j)
+                if (cap.t[j] == t)
+                    MZ_TRY(h, hipMemcpyAsync(cap.dst[j], h->d_flat, h->nflat * 4, hipMemcpyDeviceToDevice, st));
+        } else {
+            for (int64_t i = 0; i < n; ++i) eta[i] = cos_schedule(t0 + i);
+            if (learner_multi(h, h->tr_B, (uint32_t)t0, (int32_t)n, eta, nullptr, nullptr, st, losses_dev,
+                              per_refresh ? nullptr : &cap))
+                return -1;
+        }
+        h->tr_t = t;
+        *done += n;
+        k += n;
+        if (per_refresh && is_refresh(t) && train_refresh(h, t, st)) return -1;
+    }
+    if (!per_refresh && nref > 0) {
+        if (wset_repack(h, h->tr_actor, st)) return -1;
+        h->tr_refresh += nref;
+    }
+    return 0;
+}
+
+// a count summed over the ranks of the handle's RCCL communicator (exact below 2^24)
+static int dp_sum_count(mz_handle* h, int64_t* v, hipStream_t st) {
+    if (!h->d_dp_cnt) MZ_TRY(h, dalloc(h, &h->d_dp_cnt, 1));
+    float f = (float)*v;
+    MZ_TRY(h, hipMemcpyAsync(h->d_dp_cnt, &f, 4, hipMemcpyHostToDevice, st));
+    const int rc = rccl().allreduce(h->d_dp_cnt, h->d_dp_cnt, 1, 7, 0, h->dp_comm, st);   // ncclFloat32, ncclSum
+    if (rc != 0) return fail(h, std::string("ncclAllReduce: ") + (rccl().err ? rccl().err(rc) : "error"));
+    MZ_TRY(h, hipMemcpyAsync(&f, h->d_dp_cnt, 4, hipMemcpyDeviceToHost, st));
+    MZ_TRY(h, hipStreamSynchronize(st));
+    *v = (int64_t)f;
+    return 0;
+}
+
+int mz_train_move(mz_handle* h, uint32_t move, uint32_t game_offset, int64_t* nfin, void* stream) {
+    if (!h) return -2;
+    if (!h->tr_B) return fail(h, "mz_train_init first");
+    MZ_TRY(h, hipSetDevice(h->device));
+    int64_t n = 0;
+    if (train_move(h, move, game_offset, &n, stream ? (hipStream_t)stream : h->stream)) return -1;
+    if (nfin) *nfin = n;
+    return 0;
+}
+
+int mz_train_learn(mz_handle* h, int64_t steps, float* losses_dev, int64_t* state_out, void* stream) {
+    if (!h) return -2;
+    if (!h->tr_B) return fail(h, "mz_train_init first");
+    if (steps < 0) return fail(h, "steps must be >= 0");
+    MZ_TRY(h, hipSetDevice(h->device));
+    int64_t done = 0;
+    if (train_learn(h, steps, losses_dev, stream ? (hipStream_t)stream : h->stream, &done)) return -1;
+    if (state_out) {
+        state_out[0] = h->tr_t; state_out[1] = h->tr_games; state_out[2] = h->tr_refresh; state_out[3] = done;
+    }
+    return 0;
+}
+
 int mz_train_run(mz_handle* h, int32_t moves, uint32_t move0, uint32_t game_offset, int64_t* state_out,
                  float* losses_dev, void* stream) {
     if (!h) return -2;
@@ -4114,66 +4337,13 @@ int mz_train_run(mz_handle* h, int32_t moves, uint32_t move0, uint32_t game_offs
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     int64_t steps = 0;
     for (int32_t mv = 0; mv < moves; ++mv) {
-        // 1. self-play move with the actors' nets (SelfPlay.jl:343-380); temperature
-        //    visit_softmax_temperature_fn(t) (:48-56, 396-397)
-        //    for the games that start on this move; a game in progress keeps its own
-        const float temp = temp_fn(h->tr_t);
-        wset_swap(h, h->tr_actor);
-        h->sp_latch = true;
-        const int rc = mz_selfplay_move(h, move0 + (uint32_t)mv, game_offset, temp, st);
-        h->sp_latch = false;
-        wset_swap(h, h->tr_actor);
-        if (rc) return rc;
-        // 2. games saved this move (save_game in slot order, inside the move)
-        // (the fault word rides along: one stream wait per move, no second blocking copy)
-        MZ_TRY(h, hipMemcpyAsync(h->h_tr_cnt, h->d_sp_counters, sizeof(long long), hipMemcpyDeviceToHost, st));
-        h->h_tr_cnt[1] = 0;
-        if (h->d_fault) MZ_TRY(h, hipMemcpyAsync(h->h_tr_cnt + 1, h->d_fault, 4, hipMemcpyDeviceToHost, st));
-        MZ_TRY(h, hipStreamSynchronize(st));
-        if (h->h_tr_cnt[1] && check_fault(h)) return -1;
-        const int64_t nfin = h->h_tr_cnt[0] - h->tr_games;
-        h->tr_games = h->h_tr_cnt[0];
-        // 3. one learner step per saved game while t <= training_steps (Learning.jl:327),
-        //    get_batch keyed by the step number, eta = Cos(step).  The shard does not change
-        //    between them, so consecutive steps up to the next checkpoint run as one
-        //    mz_learner_train_multi_dev chunk (results identical to one call per step)
-        static const int chunk_env = std::getenv("MZ_TRAIN_L") ? std::atoi(std::getenv("MZ_TRAIN_L")) : 0;
-        const int chunk_max = std::max(1, std::min(MZ_MULTI_MAX, chunk_env > 0 ? chunk_env : MZ_MULTI_MAX));
-        for (int64_t k = 0; k < nfin && h->tr_t <= h->conf.training_steps;) {
-            const int64_t t0 = h->tr_t + 1, ci = h->conf.checkpoint_interval;
-            int64_t tb = (t0 + ci - 1) / ci * ci;              // the chunk ends at the next refresh step
-            if (tb <= 1) tb += ci;                              // (t % ci == 0 && t > 1)
-            const int64_t n = std::min<int64_t>({nfin - k, (int64_t)h->conf.training_steps + 1 - h->tr_t,
-                                                 tb - t0 + 1, (int64_t)chunk_max});
-            const int64_t t = t0 + n - 1;
-            if (n == 1) {
-                if (mz_learner_train_dev(h, h->tr_B, (uint32_t)t, cos_schedule(t), losses_dev, st)) return -1;
-            } else {
-                double eta[MZ_MULTI_MAX];
-                for (int64_t i = 0; i < n; ++i) eta[i] = cos_schedule(t0 + i);
-                if (learner_multi(h, h->tr_B, (uint32_t)t0, (int32_t)n, eta, nullptr, nullptr, st, losses_dev))
-                    return -1;
-            }
-            h->tr_t = t;
-            steps += n;
-            k += n;
-            // 4. checkpoint: the actors take the queued nets, the learner's nets are queued
-            //    (SelfPlay.jl:399-401 / Learning.jl:416-418: one checkpoint behind)
-            if (t % h->conf.checkpoint_interval == 0 && t > 1) {
-                MZ_TRY(h, hipMemcpyAsync(h->tr_actor.flat, h->d_tr_queued, h->nflat * 4, hipMemcpyDeviceToDevice, st));
-                if (wset_repack(h, h->tr_actor, st)) return -1;
-                MZ_TRY(h, hipMemcpyAsync(h->d_tr_queued, h->d_flat, h->nflat * 4, hipMemcpyDeviceToDevice, st));
-                ++h->tr_refresh;
-                // Learning.jl:427-432: past round(Int, 0.9 training_steps) the nets go to disk
-                // (round half to even, as Julia's round)
-                if (!h->tr_ckpt_path.empty() &&
-                    (double)t > std::nearbyint(0.9 * (double)h->conf.training_steps)) {
-                    MZ_TRY(h, hipStreamSynchronize(st));
-                    const std::string path = h->tr_ckpt_path + "/" + std::to_string(t) + ".safetensors";
-                    if (mz_checkpoint_save(h, path.c_str(), t)) return -1;
-                }
-            }
-        }
+        int64_t nfin = 0, done = 0;
+        if (train_move(h, move0 + (uint32_t)mv, game_offset, &nfin, st)) return -1;
+        // data parallel (mz_dp_init): every rank takes the learner steps of the games all
+        // ranks finished, so the replicas stay identical
+        if (h->dp_comm && h->dp_world > 1 && dp_sum_count(h, &nfin, st)) return -1;
+        if (train_learn(h, nfin, losses_dev, st, &done)) return -1;
+        steps += done;
     }
     if (state_out) {
         state_out[0] = h->tr_t; state_out[1] = h->tr_games; state_out[2] = h->tr_refresh; state_out[3] = steps;

@@ -93,6 +93,56 @@ struct SmFusedIn {
     int NN, H, plane, x_pred, x_dyn;
 };
 
+// ((p0+p1)+(p2+p3)) in every lane: with both operands equal, the two halves
+// of a permlane swap are {own, partner} in row order, so their sum is
+// p_even + p_odd in both rows of each pair
+template <int T>
+__device__ __forceinline__ void sm_qsum(float (&acc)[T]) {
+#pragma unroll
+    for (int g = 0; g < T; ++g) {
+        const auto s1 = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, acc[g]),
+                                                         __builtin_bit_cast(unsigned, acc[g]), false, false);
+        const float t = __builtin_bit_cast(float, (unsigned)s1[0]) + __builtin_bit_cast(float, (unsigned)s1[1]);
+        const auto s2 = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, t),
+                                                         __builtin_bit_cast(unsigned, t), false, false);
+        acc[g] = __builtin_bit_cast(float, (unsigned)s2[0]) + __builtin_bit_cast(float, (unsigned)s2[1]);
+    }
+}
+
+// The search's tail stage (SmallParams.tail, mz_engine.hip sm_schedule_tail):
+// the last register set holds only the four head outputs, each on its own
+// wave — value on wave 0, reward on wave 1, policy on wave 2, the state rows
+// on the last P.tail waves — so each is consumed by the wave that computes it, with no
+// workgroup barrier: the stage's dot (the same chain, sums and epilogue
+// arithmetic as sm_stage, hence the same bits) without the store.  Returns
+// this lane's row for game q = its DPP row (every DPP row holds the sums).
+template <int T>
+__device__ __forceinline__ float sm_tail_row(const float (&w)[16], int4 R, const float* lds, const float2* bnp) {
+    const int q = (threadIdx.x >> 4) & 3, i = threadIdx.x & 15;
+    const float* xp = lds + R.x + (q * R.y + i) * T;
+    float x[T];
+#pragma unroll
+    for (int g = 0; g < T; ++g) x[g] = xp[g];
+    float acc[T];
+#pragma unroll
+    for (int g = 0; g < T; ++g) acc[g] = 0.0f;
+    sm_chain<T>(w, x, acc);
+    sm_qsum<T>(acc);
+    float v = acc[0];
+#pragma unroll
+    for (int g = 1; g < T; ++g) v = q == g ? acc[g] : v;
+    float d = v + __int_as_float(R.w);
+    if ((R.z >> 29) & 1) { const float2 gb = *bnp; d = mz_bn_apply(d, gb.x, gb.y); }
+    return (R.z >> 30) & 1 ? mz_relu(d) : d;
+}
+
+// lane 0 of each 16-lane DPP row to the whole row (row_newbcast:0)
+__device__ __forceinline__ float sm_row_bcast0(float v) {
+    float r;
+    asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v));
+    return r;
+}
+
 // One stage.  R = this thread's record of stage K; the record of stage K+1
 // (constant for the whole kernel) is fetched while stage K computes.
 template <int T, int FI = 0>
@@ -133,18 +183,7 @@ __device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int
 #pragma unroll
     for (int g = 0; g < T; ++g) acc[g] = 0.0f;
     sm_chain<T>(w, x, acc);
-    // ((p0+p1)+(p2+p3)) in every lane: with both operands equal, the two
-    // halves of a permlane swap are {own, partner} in row order, so their sum
-    // is p_even + p_odd in both rows of each pair
-#pragma unroll
-    for (int g = 0; g < T; ++g) {
-        const auto s1 = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, acc[g]),
-                                                         __builtin_bit_cast(unsigned, acc[g]), false, false);
-        const float t = __builtin_bit_cast(float, (unsigned)s1[0]) + __builtin_bit_cast(float, (unsigned)s1[1]);
-        const auto s2 = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, t),
-                                                         __builtin_bit_cast(unsigned, t), false, false);
-        acc[g] = __builtin_bit_cast(float, (unsigned)s2[0]) + __builtin_bit_cast(float, (unsigned)s2[1]);
-    }
+    sm_qsum<T>(acc);
     if (q == 0 && R.z >= 0) {
         const int o = R.z & 0x1fffffff;
         const bool relu = (R.z >> 30) != 0;
@@ -246,7 +285,9 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     int* sg_vtp = si + 128;
     int* sg_depth = si + 144;
     float* sg_stage = reinterpret_cast<float*>(si + 160);       // [4][16]
-    // si + 224 .. 231: unused (formerly the leaf value / reward read-outs)
+    float* sg_rew = reinterpret_cast<float*>(si + 224);           // [4] tail: the reward wave's read-outs
+    int* sg_rflag = si + 228;                                     // tail: simulation + 1 once sg_rew holds it
+    // si + 229 .. 231: unused
     float* sg_noise = reinterpret_cast<float*>(si + 232);       // [4][16] root exploration noise
     int* sg_path = si + 296;                                      // [T][2(S+2)]
     // select / gather tables in LDS (they sit on the per-level critical path)
@@ -311,6 +352,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     }
     for (int i = tid; i < T * NN; i += SM_THREADS) c_cache[i] = make_uint2(0u, 0u);
     if (tid < 4) { c_hdr[tid] = make_int4(0, -1, 1, 0); c_mmx[tid] = make_float2(0.0f, 0.0f); c_skip[tid] = 0; }
+    if (tid == 0) *sg_rflag = 0;
     int ver = 1;                                                  // wave 0: the tag of this lane's game
     if (tree_thread && a == 0) {
         uint32_t m = 0;
@@ -392,29 +434,55 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         __syncthreads();
         SM_STAMP(2);
         // ---- prediction(parent.h) ‖ dynamics(2h ⊕ a/|A|): the first stage
-        // reads the parent's h from the hidden-state store (gather fused)
-        sm_run<T, SM_MAX_SIM, 1>(P.n_sim, wr, rec_sim, act, &fin, bn_sim);
+        // reads the parent's h from the hidden-state store (gather fused).
+        // With the tail schedule the last stage is not a barrier stage: its
+        // four head outputs are computed below by the waves that consume them.
+        const bool tail = P.tail > 0;
+        sm_run<T, SM_MAX_SIM, 1>(tail ? P.n_sim - 1 : P.n_sim, wr, rec_sim, act, &fin, bn_sim);
         SM_STAMP(3);
         const int e_new = s + 1;
+        const int wv = tid >> 6;
+        constexpr int KT = SM_MAX_SIM - 1;
+        float tl_v = 0.0f;                      // this lane's tail row (sm_tail_row)
+        if (tail && (wv <= 2 || wv >= 8 - P.tail))
+            tl_v = sm_tail_row<T>(wr[KT], rec_sim[KT * (SM_SLOTS * 64)], act, bn_sim + KT * (SM_SLOTS * 64));
         // expand (wave 2) runs beside the read-outs + backup (wave 0): they
         // touch disjoint LDS — the new slot's edges vs the path edges, the
         // leaf edge's child link and the new slot's reward / to_play
         if (tid < 64) {
             // ---- value / reward read-out activations, then backpropagate! (:190-217)
-            if (active) {
+            float val, rew;
+            if (tail) {
+                // the value row is this wave's (row 0 of DPP row g); the reward
+                // comes from wave 1 through LDS (flag = the simulation + 1)
+                val = mz_post_act(P.v_act, sm_row_bcast0(tl_v));
+                unsigned n = 0;
+                while (__hip_atomic_load(sg_rflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != s + 1) {
+                    if (++n > (1u << 24)) {             // cannot happen (wave 4 always publishes): reported
+                        if (P.fault && lane == 0)
+                            __hip_atomic_fetch_or(P.fault, (unsigned)MZ_FAULT_SM_TAIL, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                rew = sg_rew[g];
+            } else {
                 // one activation per lane (even lanes the value, odd the reward, both
-                // f64 tanh chains run at once), then each quad's lanes 0 / 1 to all
+                // tanh chains run at once), then each quad's lanes 0 / 1 to all
                 // four by DPP quad_perm [0,0,0,0] / [1,1,1,1]
                 const bool odd = (a & 1) != 0;
                 const float ro = mz_post_act(odd ? P.r_act : P.v_act, act[(odd ? P.r_out : P.v_out) + g]);
-                const float val = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                val = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
                     0, __builtin_bit_cast(int, ro), 0x00, 0xF, 0xF, false));
-                const float rew = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                rew = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
                     0, __builtin_bit_cast(int, ro), 0x55, 0xF, 0xF, false));
+            }
 #ifdef MZ_STAMPS
-                if (threadIdx.x == 0) asm volatile("" :: "v"(val), "v"(rew));
+            if (threadIdx.x == 0) asm volatile("" :: "v"(val), "v"(rew));
 #endif
-                SM_STAMP(5);                    // stamp build: slot 5 = the read-out activations
+            SM_STAMP(5);                        // stamp build: slot 5 = the read-out activations
+            if (active) {
                 const int tl = sg_vtp[g];
                 const int depth = sg_depth[g];
                 if (a == 0) {
@@ -444,9 +512,26 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
             const int g2 = (tid - 128) >> 4;
             const bool active2 = tile0 + g2 < P.G;
             TreeView tree2 = tree_view(lds_tree + (size_t)g2 * P.tree_game_bytes, E, NN);
-            const float prior = double_softmax_prior(a < A ? act[P.p_out + a * T + g2] : 0.0f, a, A, sg_legal[g2],
-                                                     sg_stage + 16 * g2);
+            const float logit = tail ? tl_v : act[P.p_out + a * T + g2];   // (tail: row a of DPP row g2)
+            const float prior = double_softmax_prior(a < A ? logit : 0.0f, a, A, sg_legal[g2], sg_stage + 16 * g2);
             if (active2) init_edges(tree2, e_new, a, A, prior);
+        } else if (tail) {
+            if (wv == 1) {                      // the reward row (row 0 of DPP row g) -> wave 0
+                const int q = (tid >> 4) & 3;
+                if ((tid & 15) == 0 && q < T) sg_rew[q] = mz_post_act(P.r_act, tl_v);
+                if (lane == 0) __hip_atomic_store(sg_rflag, s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if (wv >= 8 - P.tail) {      // h' rows 16(wv - 8 + tail) + i of game q, stored in place
+                const int q = (tid >> 4) & 3, row = 16 * (wv - 8 + P.tail) + (tid & 15);
+                if (q < T && row < H) hid[((size_t)q * NN + e_new) * H + row] = tl_v;
+            } else if (wv == 3) {               // parent h *= 2 (Q1)
+                for (int i = lane; i < T * H; i += 64) {
+                    const int gl = i / H, k = i - gl * H;
+                    if (tile0 + gl < P.G) {
+                        float* hp = hid + ((size_t)gl * NN + sg_leaf_e[gl]) * H + k;
+                        *hp = *hp * 2.0f;
+                    }
+                }
+            }
         } else if (tid >= 192) {
             for (int i = tid - 192; i < T * H; i += SM_THREADS - 192) {   // store h'; parent h *= 2 (Q1)
                 const int gl = i / H, k = i - gl * H;
@@ -807,6 +892,8 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learn_chain(ChainPar
             if (C.fbank) C.fbank[i * C.nflat + p] = x;
             x = adam_2theta(x, m, v, sbp[0][i], sbp[1][i], sbp[2][i]);   // Learning.jl:395-397
             if (C.theta) C.theta[i * C.nflat + p] = x;
+            if (i == C.cap_i[0]) C.cap_dst[0][p] = x;
+            if (i == C.cap_i[1]) C.cap_dst[1][p] = x;
         }
         C.flat[p] = x; C.M[p] = m; C.V[p] = v;
         mz_scatter(x, it, C.Wp, C.Bp);
