@@ -207,7 +207,9 @@ int mz_debug_kernel_time(mz_handle* h, double* total_ms, int* launches);
  * reward 0 at step 0).  Any pointer may be NULL.                          */
 int mz_debug_unroll(mz_handle* h, int B, float* values, float* policies, float* rewards);
 /* The same read-outs of step step0 + i of the last mz_learner_train_multi_dev
- * that ran its two-launch form (0 <= i < L).                               */
+ * that ran its multi-step form, 0 <= i < L; the per-step scratch is a ring of
+ * at least 33 steps (the largest multiple of the chain-launch length <= 64),
+ * so steps older than that are refused.                                     */
 int mz_debug_unroll_step(mz_handle* h, int i, int B, float* values, float* policies, float* rewards);
 
 /* One learner batch, the tuple returned by get_batch (ReplayBuffer.jl:216),

@@ -12,8 +12,10 @@
 // γ·((t - 0)/s) + β, the block input, the activation; MeanPool sums the
 // in-board window rows outer / columns inner and multiplies by f32(1/9).
 // The work is small (≈ 3.3 M MACs per item, once per move) next to the
-// S simulations of the search, so it runs on the VALU; what bounds it is the
-// latency of one item's 20 dependent layers, so each position's taps are
+// S simulations of the search; what bounds it is the latency of one item's
+// 20 dependent layers.  The 8-channel convs run as f32 MFMA implicit GEMMs
+// (ds_conv_mfma, since round 5); the 4-channel convs stay on the VALU
+// (ds_conv3: 16x16 MFMA tiles would be ¾ padding), each position's taps
 // loaded once, in one batch, and reused for every output channel.
 #include <hip/hip_runtime.h>
 #include "mz_internal.h"

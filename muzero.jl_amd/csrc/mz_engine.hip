@@ -76,6 +76,9 @@ extern "C" __global__ void mz_rp_per_update(SpHist ring, const long long* counte
 extern "C" __global__ void mz_search_small1(SmallParams P);
 extern "C" __global__ void mz_search_small2(SmallParams P);
 extern "C" __global__ void mz_search_small4(SmallParams P);
+extern "C" __global__ void mz_search_small1_bn(SmallParams P);
+extern "C" __global__ void mz_search_small2_bn(SmallParams P);
+extern "C" __global__ void mz_search_small4_bn(SmallParams P);
 extern "C" __global__ void mz_unroll_small1(SmallUnrollParams P);
 extern "C" __global__ void mz_unroll_small2(SmallUnrollParams P);
 extern "C" __global__ void mz_learn_small1(SmallUnrollParams P, LearnParams L);
@@ -223,7 +226,6 @@ struct mz_handle {
     bool small_ok = false;
     int n_cu = 256;
     int sm_n_sim = 0, sm_n_root = 0;
-    int sm_tail = 0;                        // SmallParams.tail (sm_schedule_tail)
     float* d_sm_w = nullptr;                // [n_sim + n_root][2][256][16] weight image (sim then root)
     float* d_sm_bias = nullptr;             // [n_sim + n_root][2][64]
     // FC engines: a second image set (tile16 W/B, small W/bias) that the one-launch
@@ -306,7 +308,7 @@ struct mz_handle {
     float* d_ml_hs = nullptr; float* d_ml_ts = nullptr; float* d_ml_dsb = nullptr;
     unsigned long long* d_ml_prog = nullptr;
     unsigned long long ml_prog_epoch = 0;   // multi-step fused launches (d_ml_prog's prog_base = epoch · 64)
-    int ml_cap = 0, ml_cap_L = 0, ml_last_B = 0, ml_last_L = 0;
+    int ml_cap = 0, ml_cap_L = 0, ml_last_B = 0, ml_last_L = 0, ml_last_R = 0;   // (ring: ensure_multi)
     float *d_ml_obs = nullptr, *d_ml_act = nullptr, *d_ml_tv = nullptr, *d_ml_tr = nullptr, *d_ml_tp = nullptr,
           *d_ml_gs = nullptr, *d_ml_pv = nullptr, *d_ml_pp = nullptr, *d_ml_pr = nullptr, *d_ml_terms = nullptr,
           *d_ml_out = nullptr;
@@ -392,7 +394,6 @@ static int check_fault(mz_handle* h) {
     std::string m = std::string("device fault: a workgroup waited ") + wait + " for a publish that never came (";
     if (v & MZ_FAULT_RS_TRUNK) m += "mz_rsearch_nets trunk hand-off ";
     if (v & MZ_FAULT_RD_PROGRESS) m += "mz_runroll_fused_r chain progress ";
-    if (v & MZ_FAULT_SM_TAIL) m += "mz_search_small tail reward hand-off ";
     h->err = m + "); the results of the launches since the last synchronisation are invalid (search results, "
                  "games self-play stored from them, losses, read-outs; the ref_semantics weights and ADAM state "
                  "do not read them and stay valid)";
@@ -411,6 +412,13 @@ static hipError_t dalloc(mz_handle* h, T** p, size_t n) {
     hipError_t e = hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T) + 16);
     if (e == hipSuccess) h->allocs.push_back(*p);
     return e;
+}
+// free one dalloc'd buffer before the handle is destroyed (the caller has drained the work using it)
+static hipError_t dfree(mz_handle* h, void* p) {
+    auto it = std::find(h->allocs.begin(), h->allocs.end(), p);
+    if (it == h->allocs.end()) return hipErrorInvalidValue;
+    h->allocs.erase(it);
+    return hipFree(p);
 }
 
 // ------------------------------------------------------------ specs & plans
@@ -638,60 +646,6 @@ static bool sm_schedule(const mz_handle* h, const std::vector<int>& set, const s
     return true;
 }
 
-// The tail schedule (round 6): the four head outputs — value (pred head 1),
-// policy (pred head 2), state (dyn head 1), reward (dyn head 2), each the last
-// layer of its chain — alone in the last of SM_MAX_SIM stages, pinned to the
-// waves that consume them in the search (mz_small.hip small_body), one per
-// SIMD where it can be (wave w runs on SIMD w mod 4): value on slot 0 group 0
-// (wave 0: read-outs + backup, SIMD 0 to itself), reward on slot 0 group 1
-// (wave 1, handed to wave 0 through LDS), policy on slot 0 group 2 (wave 2:
-// expand), the state rows on the last groups of slot 1 (waves 8 − nb .. 7,
-// stored straight into the hidden-state store).  The search then runs SM_MAX_SIM − 1 barrier stages and
-// the tail beside the tree phases; the learner runs every stage as before (the
-// same image, the same dot order, so the same bits).  Every other layer is
-// list-scheduled into the first SM_MAX_SIM − 1 stages, which it must fill
-// exactly (so the tail sits on register set SM_MAX_SIM − 1).  Returns the
-// number of state waves, or 0 if the nets do not fit this shape.
-static int sm_schedule_tail(const mz_handle* h, const std::vector<int>& set, const std::vector<std::vector<int>>& deps,
-                            std::vector<int>& st, std::vector<int>& sl, std::vector<int>& b0,
-                            std::vector<std::array<int, 2>>& stage_kq) {
-    if (SM_SLOTS != 2) return 0;
-    const int n = (int)set.size();
-    const int onet[4] = {MZ_NET_PRED, MZ_NET_PRED, MZ_NET_DYN, MZ_NET_DYN};
-    const int och[4] = {CH_HEAD1, CH_HEAD2, CH_HEAD1, CH_HEAD2};
-    const int nbs = (h->layers[h->chains[MZ_NET_DYN][CH_HEAD1].empty() ? 0 : h->chains[MZ_NET_DYN][CH_HEAD1].back()]
-                         .out + 15) / 16;
-    const int oslot[4] = {0, 0, 1, 0}, ogrp[4] = {0, 2, 4 - nbs, 1}, omax[4] = {1, 1, 3, 1};
-    int opos[4];
-    for (int o = 0; o < 4; ++o) {
-        const auto& ch = h->chains[onet[o]][och[o]];
-        if (ch.empty()) return 0;
-        opos[o] = (int)(std::find(set.begin(), set.end(), ch.back()) - set.begin());
-        if (opos[o] >= n || (h->layers[ch.back()].out + 15) / 16 > omax[o]) return 0;
-    }
-    std::vector<int> body, bidx(n, -1);
-    for (int i = 0; i < n; ++i)
-        if (std::find(opos, opos + 4, i) == opos + 4) { bidx[i] = (int)body.size(); body.push_back(i); }
-    std::vector<int> bset;
-    std::vector<std::vector<int>> bdeps;
-    for (int i : body) {
-        bset.push_back(set[i]);
-        bdeps.emplace_back();
-        for (int d : deps[i]) {
-            if (bidx[d] < 0) return 0;                  // (an output feeding another layer)
-            bdeps.back().push_back(bidx[d]);
-        }
-    }
-    std::vector<int> bst, bsl, bb0;
-    if (!sm_schedule(h, bset, bdeps, SM_MAX_SIM - 1, bst, bsl, bb0, stage_kq)) return 0;
-    if ((int)stage_kq.size() != SM_MAX_SIM - 1) return 0;
-    st.assign(n, -1); sl.assign(n, -1); b0.assign(n, -1);
-    for (size_t j = 0; j < body.size(); ++j) { st[body[j]] = bst[j]; sl[body[j]] = bsl[j]; b0[body[j]] = bb0[j]; }
-    for (int o = 0; o < 4; ++o) { st[opos[o]] = SM_MAX_SIM - 1; sl[opos[o]] = oslot[o]; b0[opos[o]] = 4 * ogrp[o]; }
-    stage_kq.push_back({0, 0});
-    return (h->layers[h->chains[MZ_NET_DYN][CH_HEAD1].back()].out + 15) / 16;
-}
-
 static int build_small(mz_handle* h) {
     for (const LayerSpec& L : h->layers)
         if (L.in > 64 || L.out > 64) return 0;          // not eligible: tile-16 kernel only
@@ -716,10 +670,7 @@ static int build_small(mz_handle* h) {
     };
     std::vector<int> st_s, sl_s, b0_s, st_r, sl_r, b0_r;
     std::vector<std::array<int, 2>> kq_s, kq_r;
-    const char* no_tail = getenv("MZ_NO_TAIL");          // A/B: every stage a barrier stage
-    h->sm_tail = no_tail && *no_tail && *no_tail != '0' ? 0
-                                                        : sm_schedule_tail(h, sim, deps_of(sim), st_s, sl_s, b0_s, kq_s);
-    if (!h->sm_tail && !sm_schedule(h, sim, deps_of(sim), SM_MAX_SIM, st_s, sl_s, b0_s, kq_s)) return 0;
+    if (!sm_schedule(h, sim, deps_of(sim), SM_MAX_SIM, st_s, sl_s, b0_s, kq_s)) return 0;
     if (!sm_schedule(h, root, deps_of(root), SM_MAX_ROOT, st_r, sl_r, b0_r, kq_r)) return 0;
     h->sm_n_sim = (int)kq_s.size();
     h->sm_n_root = (int)kq_r.size();
@@ -1365,12 +1316,15 @@ static size_t ds_build(mz_handle* h, DsPlan& D) {
 // run the downsampler over n items: x (in_feat, n) -> y (rin_feat, n); with
 // per_step > 0 item i uses the parameters flat + (i / per_step)·nflat (the
 // multi-step learner's per-step bank), else the engine's
+// the flat bank's per-step stride (rlearner_multi): nflat rounded up to 4 floats, so the downsampler's
+// float4 parameter staging (DsParams.per_step) reads 16-byte aligned rows
+static size_t fbank_stride(const mz_handle* h) { return (h->nflat + 3) / 4 * 4; }
 static int ds_launch(mz_handle* h, const float* x, float* y, int n, hipStream_t st, const float* flat = nullptr,
                      int per_step = 0) {
     DsParams Q;
     Q.n_items = n; Q.bn_s = h->bn_s; Q.plan = h->d_dsplan; Q.flat = h->d_flat; Q.x = x; Q.y = y;
     Q.stamps = nullptr;
-    Q.per_step = per_step; Q.flat_stride = h->nflat;
+    Q.per_step = per_step; Q.flat_stride = fbank_stride(h);
     if (flat) Q.flat = flat;
 #ifdef MZ_STAMPS
     if (!h->d_stamps) MZ_TRY(h, dalloc(h, &h->d_stamps, (size_t)8 * std::max(h->max_games, 128)));
@@ -1688,10 +1642,11 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
         const char* ft = std::getenv("MZ_SMALL_T");
         if (ft) { const int t = std::atoi(ft); h->force_T = (t == 1 || t == 2 || t == 4) ? t : 0; }
         if (h->small_ok) {
-            const void* ks[3] = {(const void*)mz_search_small1, (const void*)mz_search_small2,
-                                 (const void*)mz_search_small4};
-            for (int ti = 0; ti < 3; ++ti)
-                CK(hipFuncSetAttribute(ks[ti], hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->sm_lds[ti]) ==
+            const void* ks[6] = {(const void*)mz_search_small1, (const void*)mz_search_small2,
+                                 (const void*)mz_search_small4, (const void*)mz_search_small1_bn,
+                                 (const void*)mz_search_small2_bn, (const void*)mz_search_small4_bn};
+            for (int ti = 0; ti < 6; ++ti)
+                CK(hipFuncSetAttribute(ks[ti], hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->sm_lds[ti % 3]) ==
                            hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(small)"));
             const void* ku[2] = {(const void*)mz_unroll_small1, (const void*)mz_unroll_small2};
             for (int ti = 0; ti < 2; ++ti)
@@ -1986,8 +1941,6 @@ static int search_dev(mz_handle* h, int G, const float* obs, const uint8_t* lega
         Q.w_sim = h->d_sm_w;
         std::memcpy(Q.nzm, h->sm_nzm.data(), sizeof(Q.nzm));
         Q.bn = h->sm_bn;
-        Q.tail = h->sm_tail;
-        Q.fault = h->d_fault;
         Q.zero16 = reinterpret_cast<const float4*>(h->d_zero16);
         Q.w_root = h->d_sm_w + (size_t)h->sm_n_sim * SM_SLOTS * 256 * 16;
         Q.rec = h->d_sm_rec[ti]; Q.bias = h->d_sm_bias;
@@ -2001,11 +1954,14 @@ static int search_dev(mz_handle* h, int G, const float* obs, const uint8_t* lega
 #ifdef MZ_STAMPS
         Q.stamps = h->d_stamps;
 #endif
-        const void* k = T == 1 ? (const void*)mz_search_small1 : T == 2 ? (const void*)mz_search_small2
-                                                                        : (const void*)mz_search_small4;
+        const void* k = h->sm_bn ? (T == 1 ? (const void*)mz_search_small1_bn : T == 2 ? (const void*)mz_search_small2_bn
+                                                                                   : (const void*)mz_search_small4_bn)
+                                 : (T == 1 ? (const void*)mz_search_small1 : T == 2 ? (const void*)mz_search_small2
+                                                                                   : (const void*)mz_search_small4);
         void* args[] = {&Q};
         MZ_TRY(h, hipLaunchKernel(k, dim3((G + T - 1) / T), dim3(SM_THREADS), args, h->sm_lds[ti], st));
-        h->last_variant = T == 1 ? "mz_search_small1" : T == 2 ? "mz_search_small2" : "mz_search_small4";
+        h->last_variant = std::string(T == 1 ? "mz_search_small1" : T == 2 ? "mz_search_small2" : "mz_search_small4") +
+                          (h->sm_bn ? "_bn" : "");
     } else {
         hipLaunchKernelGGL(search_kernel(h), dim3((G + MZ_TILE - 1) / MZ_TILE), dim3(MZ_THREADS),
                            search_lds_bytes(h), st, P);
@@ -3726,7 +3682,7 @@ static int ensure_multi(mz_handle* h, int B, int L) {
         const size_t nw = h->packed_w_n, nb = std::max<size_t>(h->packed_b_n, 1);
         MZ_TRY(h, dalloc(h, &h->d_tbank_w, (size_t)2 * MZ_MULTI_MAX * nw));
         MZ_TRY(h, dalloc(h, &h->d_tbank_b, (size_t)2 * MZ_MULTI_MAX * nb));
-        MZ_TRY(h, dalloc(h, &h->d_fbank, (size_t)2 * MZ_MULTI_MAX * h->nflat));
+        MZ_TRY(h, dalloc(h, &h->d_fbank, (size_t)2 * MZ_MULTI_MAX * fbank_stride(h)));
         for (int i = 0; i < 2 * MZ_MULTI_MAX; ++i) {
             MZ_TRY(h, hipMemcpy(h->d_tbank_w + (size_t)i * nw, h->d_Wp, nw * 4, hipMemcpyDeviceToDevice));
             if (h->packed_b_n)
@@ -3746,8 +3702,23 @@ static int ensure_multi(mz_handle* h, int B, int L) {
                                 hipMemcpyDeviceToDevice));
         }
     }
+    // per-step scratch (batches, read-outs, loss terms, partials) is a ring of at most 2·MZ_MULTI_MAX
+    // steps (slot = step mod R, R = the largest multiple of the chain length Lc <= 2·MZ_MULTI_MAX, so a
+    // chain launch's steps and an unroll launch's steps are contiguous, and a chain launch that reuses
+    // an earlier launch's slots runs after its unrolls in stream order); on growth the old arrays are
+    // freed after the device drains
+    L = std::min(L, 2 * MZ_MULTI_MAX);
     if (B <= h->ml_cap && L <= h->ml_cap_L) return 0;
     const int cb = std::max(B, h->ml_cap), cl = std::max(L, h->ml_cap_L);
+    if (h->ml_cap) {
+        MZ_TRY(h, hipDeviceSynchronize());
+        void* olds[] = {h->d_ml_obs, h->d_ml_act, h->d_ml_tv, h->d_ml_tr, h->d_ml_tp, h->d_ml_gs, h->d_ml_index,
+                        h->d_ml_pv, h->d_ml_pp, h->d_ml_pr, h->d_ml_terms, h->d_ml_part, h->d_ml_cnt, h->d_ml_out,
+                        h->d_ml_hs, h->d_ml_ts, h->d_ml_prog, h->d_ml_dsb};
+        for (void* o : olds) if (o && dfree(h, o)) return -1;
+        h->d_ml_hs = h->d_ml_ts = h->d_ml_dsb = nullptr;
+        h->d_ml_prog = nullptr;
+    }
     const size_t K1 = (size_t)h->conf.num_unroll_steps + 1, A = (size_t)h->A, n = (size_t)cl * cb;
     MZ_TRY(h, dalloc(h, &h->d_ml_obs, n * h->obs_feat));
     MZ_TRY(h, dalloc(h, &h->d_ml_act, n * K1)); MZ_TRY(h, dalloc(h, &h->d_ml_tv, n * K1));
@@ -3818,7 +3789,7 @@ static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, co
     U.rd_ep_off = (int)(h->rn_lds_l / 4); U.rd_trunk_nl = 1 + 2 * h->rhp.num_blocks;
     U.rp_nv = 3 + h->rhp.depth_value;
     U.fault = h->d_fault; U.poll_ticks = h->poll_ticks; U.dbg_skip = h->dbg_skip;
-    U.ms_wimg = nw; U.ms_flat = h->nflat; U.ms_obs = (size_t)B * (h->ds ? h->rin_feat : h->obs_feat);
+    U.ms_wimg = nw; U.ms_flat = fbank_stride(h); U.ms_obs = (size_t)B * (h->ds ? h->rin_feat : h->obs_feat);
     U.ms_k1 = s_k1; U.ms_tp = s_tp; U.ms_hs = (size_t)B * KH * h->H;
     static const bool wide_env = std::getenv("MZ_RN_PRED_WIDE") != nullptr;
     static const bool no_fuse = std::getenv("MZ_RN_NO_FUSE") != nullptr;
@@ -3832,8 +3803,9 @@ static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, co
     // chain launches of up to MZ_MULTI_MAX steps (bank half k mod 2), each followed by its steps' unroll
     // launches of up to Ls steps
     const int Lc = std::min(L, std::max(Ls, MZ_MULTI_MAX / Ls * Ls));
+    const int R = 2 * MZ_MULTI_MAX / Lc * Lc;       // the per-step scratch ring (ensure_multi)
     for (int k = 0, c0 = 0; c0 < L; ++k, c0 += Lc) {
-        const int nc = std::min(Lc, L - c0), half = k & 1;
+        const int nc = std::min(Lc, L - c0), half = k & 1, cr = c0 % R;
         ChainParams C;                              // 1. ADAM chain + the nc batches
         std::memset(&C, 0, sizeof(C));
         C.L = nc; C.flat = h->d_flat; C.M = h->d_m; C.V = h->d_v; C.netoff = h->d_netoff;
@@ -3842,9 +3814,10 @@ static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, co
         C.tbank_w = h->d_tbank_w + (size_t)half * MZ_MULTI_MAX * nw;
         C.tbank_b = h->d_tbank_b + (size_t)half * MZ_MULTI_MAX * nb;
         C.tws = nw; C.tbs = nb;
-        C.fbank = h->d_fbank + (size_t)half * MZ_MULTI_MAX * h->nflat;
+        C.fbank = h->d_fbank + (size_t)half * MZ_MULTI_MAX * fbank_stride(h);
+        C.fstride = fbank_stride(h);
         C.theta = theta_dev ? theta_dev + (size_t)c0 * h->nflat : nullptr;
-        C.nflat = h->nflat; C.part = h->d_ml_part + (size_t)c0 * 3 * MZ_L2_BLOCKS;
+        C.nflat = h->nflat; C.part = h->d_ml_part + (size_t)cr * 3 * MZ_L2_BLOCKS;
         set_caps(C, cap, (int64_t)step0 + c0, nc);
         for (int i = 0; i < nc; ++i) {
             C.bp1[i] = p1; C.bp2[i] = p2; C.eta[i] = eta[c0 + i];
@@ -3852,29 +3825,29 @@ static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, co
         }
         RpSampleParams Qc = Q;
         Qc.step = step0 + (uint32_t)c0;
-        Qc.obs += c0 * s_obs; Qc.actions += c0 * s_k1; Qc.tv += c0 * s_k1; Qc.tr += c0 * s_k1;
-        Qc.tpol += c0 * s_tp; Qc.gscale += (size_t)c0 * B; Qc.index += (size_t)c0 * 2 * B;
+        Qc.obs += cr * s_obs; Qc.actions += cr * s_k1; Qc.tv += cr * s_k1; Qc.tr += cr * s_k1;
+        Qc.tpol += cr * s_tp; Qc.gscale += (size_t)cr * B; Qc.index += (size_t)cr * 2 * B;
         C.B = B; C.q = Qc; C.s_obs = s_obs; C.s_k1 = s_k1; C.s_tp = s_tp;
         const int nsb = (nc * B + MZ_THREADS / 64 - 1) / (MZ_THREADS / 64);
         hipLaunchKernelGGL(mz_learn_chain, dim3(3 * MZ_L2_BLOCKS + nsb), dim3(MZ_THREADS), 0, st, C);
         MZ_TRY(h, hipGetLastError());
         for (int j0 = 0; j0 < nc; j0 += Ls) {
-            const int n = std::min(Ls, nc - j0), i0 = c0 + j0;
+            const int n = std::min(Ls, nc - j0), i0 = c0 + j0, ir = i0 % R;
             RpSampleParams Qk = Q;                  // steps step0 + i0 ..
             Qk.step = step0 + (uint32_t)i0;
-            Qk.obs += i0 * s_obs; Qk.actions += i0 * s_k1; Qk.tv += i0 * s_k1; Qk.tr += i0 * s_k1;
-            Qk.tpol += i0 * s_tp; Qk.gscale += (size_t)i0 * B; Qk.index += (size_t)i0 * 2 * B;
+            Qk.obs += ir * s_obs; Qk.actions += ir * s_k1; Qk.tv += ir * s_k1; Qk.tr += ir * s_k1;
+            Qk.tpol += ir * s_tp; Qk.gscale += (size_t)ir * B; Qk.index += (size_t)ir * 2 * B;
             // 2. representation input (Atari: the downsampler with step z's parameters), the unrolls
             U.ms = n;
-            U.Wimg = C.tbank_w + (size_t)j0 * nw; U.flat = C.fbank + (size_t)j0 * h->nflat;
+            U.Wimg = C.tbank_w + (size_t)j0 * nw; U.flat = C.fbank + (size_t)j0 * fbank_stride(h);
             U.obs = Qk.obs; U.actions = Qk.actions;
             if (h->ds) {
-                float* y = h->d_ml_dsb + (size_t)i0 * B * h->rin_feat;
-                if (ds_launch(h, Qk.obs, y, n * B, st, C.fbank + (size_t)j0 * h->nflat, B)) return -1;
+                float* y = h->d_ml_dsb + (size_t)ir * B * h->rin_feat;
+                if (ds_launch(h, Qk.obs, y, n * B, st, C.fbank + (size_t)j0 * fbank_stride(h), B)) return -1;
                 U.obs = y;
             }
-            U.pv = h->d_ml_pv + i0 * s_k1; U.pp = h->d_ml_pp + i0 * s_tp; U.pr = h->d_ml_pr + i0 * s_k1;
-            U.hs = h->d_ml_hs + (size_t)i0 * U.ms_hs; U.ts = h->d_ml_ts + (size_t)i0 * U.ms_hs;
+            U.pv = h->d_ml_pv + ir * s_k1; U.pp = h->d_ml_pp + ir * s_tp; U.pr = h->d_ml_pr + ir * s_k1;
+            U.hs = h->d_ml_hs + (size_t)ir * U.ms_hs; U.ts = h->d_ml_ts + (size_t)ir * U.ms_hs;
             void* args[] = {&U};
             hipEvent_t e0 = nullptr, e1 = nullptr;     // mz_debug_enable flag 4: the unroll launch's duration
             if (h->time_unroll) {
@@ -3882,7 +3855,7 @@ static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, co
                 MZ_TRY(h, hipEventRecord(e0, st));
             }
             if (fused) {
-                U.prog = h->d_ml_prog + (size_t)i0 * B;
+                U.prog = h->d_ml_prog + (size_t)ir * B;
                 U.prog_base = (++h->ml_prog_epoch) * 64ull;
                 U.n_chain = B; U.fuse_sample = 0; U.n_l2 = 0;
                 const int nitems = B * KH * (K > 0 ? 3 : 2);
@@ -3919,9 +3892,9 @@ static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, co
             M.B = B; M.K = K; M.A = A; M.v_act = MZ_ACT_IDENTITY; M.r_act = MZ_ACT_IDENTITY; M.nlb = nlb; M.L = n;
             M.s_k1 = s_k1; M.s_tp = s_tp; M.pv = U.pv; M.pp = U.pp; M.pr = U.pr;
             M.tv = Qk.tv; M.tp = Qk.tpol; M.gs = Qk.gscale;
-            M.terms = h->d_ml_terms + 2 * i0 * s_k1; M.part = h->d_ml_part + (size_t)i0 * 3 * MZ_L2_BLOCKS;
-            M.counter = h->d_ml_cnt + (size_t)i0 * MZ_MULTI_CNT_STRIDE;
-            M.out = (losses_dev ? losses_dev : h->d_ml_out) + 8 * i0;
+            M.terms = h->d_ml_terms + 2 * ir * s_k1; M.part = h->d_ml_part + (size_t)ir * 3 * MZ_L2_BLOCKS;
+            M.counter = h->d_ml_cnt + (size_t)ir * MZ_MULTI_CNT_STRIDE;
+            M.out = losses_dev ? losses_dev + 8 * i0 : h->d_ml_out + 8 * ir;
             M.out_last = i0 + n == L ? out_last : nullptr;
             hipLaunchKernelGGL(gw == 32 ? mz_learner_loss_multi32 : mz_learner_loss_multi, dim3(nlb, n), dim3(MZ_THREADS),
                                0, st, M);
@@ -3936,7 +3909,7 @@ static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, co
                        (fused ? (h->rd_nb == 3 ? "mz_runroll_fused_r3" : "mz_runroll_fused_r") : chain + "+" + pred) +
                        "+mz_learner_loss_multi";
     for (int i = 0; i < L; ++i) adam_advance(h);
-    h->ml_last_B = B; h->ml_last_L = L;
+    h->ml_last_B = B; h->ml_last_L = L; h->ml_last_R = R;
     return 0;
 }
 
@@ -3981,8 +3954,9 @@ static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, con
     // chain launches of up to MZ_MULTI_MAX steps (bank half k mod 2), each followed by its steps' unroll
     // launches of Ls steps (one workgroup per CU)
     const int Lc = std::min(L, std::max(Ls, MZ_MULTI_MAX / Ls * Ls));
+    const int R = 2 * MZ_MULTI_MAX / Lc * Lc;       // the per-step scratch ring (ensure_multi)
     for (int k = 0, c0 = 0; c0 < L; ++k, c0 += Lc) {
-        const int nc = std::min(Lc, L - c0), half = k & 1;
+        const int nc = std::min(Lc, L - c0), half = k & 1, cr = c0 % R;
         // 1. the ADAM chain θ_{t+c0} .. θ_{t+c0+nc} into bank half k mod 2
         ChainParams C;
         std::memset(&C, 0, sizeof(C));
@@ -3993,7 +3967,7 @@ static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, con
         C.bank_b = h->d_bank_b + (size_t)half * MZ_MULTI_MAX * h->sm_b_n;
         C.bws = h->sm_w_n; C.bbs = h->sm_b_n;
         C.theta = theta_dev ? theta_dev + (size_t)c0 * h->nflat : nullptr;
-        C.nflat = h->nflat; C.part = h->d_ml_part + (size_t)c0 * 3 * MZ_L2_BLOCKS;
+        C.nflat = h->nflat; C.part = h->d_ml_part + (size_t)cr * 3 * MZ_L2_BLOCKS;
         set_caps(C, cap, (int64_t)step0 + c0, nc);
         for (int i = 0; i < nc; ++i) {              // adam_advance's products, step by step
             C.bp1[i] = p1; C.bp2[i] = p2; C.eta[i] = eta[c0 + i];
@@ -4001,18 +3975,18 @@ static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, con
         }
         RpSampleParams Qc = Q;                      // this chunk's batches: steps step0 + c0 ..
         Qc.step = step0 + (uint32_t)c0;
-        Qc.obs += c0 * s_obs; Qc.actions += c0 * s_k1; Qc.tv += c0 * s_k1; Qc.tr += c0 * s_k1;
-        Qc.tpol += c0 * s_tp; Qc.gscale += (size_t)c0 * B; Qc.index += (size_t)c0 * 2 * B;
+        Qc.obs += cr * s_obs; Qc.actions += cr * s_k1; Qc.tv += cr * s_k1; Qc.tr += cr * s_k1;
+        Qc.tpol += cr * s_tp; Qc.gscale += (size_t)cr * B; Qc.index += (size_t)cr * 2 * B;
         C.B = B; C.q = Qc; C.s_obs = s_obs; C.s_k1 = s_k1; C.s_tp = s_tp;
         const int nsb = chain_sample ? (nc * B + MZ_THREADS / 64 - 1) / (MZ_THREADS / 64) : 0;
         hipLaunchKernelGGL(mz_learn_chain, dim3(3 * MZ_L2_BLOCKS + nsb), dim3(MZ_THREADS), 0, st, C);
         MZ_TRY(h, hipGetLastError());
         for (int j0 = 0; j0 < nc; j0 += Ls) {
-            const int n = std::min(Ls, nc - j0), i0 = c0 + j0;
+            const int n = std::min(Ls, nc - j0), i0 = c0 + j0, ir = i0 % R;
             RpSampleParams Qk = Q;                  // steps step0 + i0 ..
             Qk.step = step0 + (uint32_t)i0;
-            Qk.obs += i0 * s_obs; Qk.actions += i0 * s_k1; Qk.tv += i0 * s_k1; Qk.tr += i0 * s_k1;
-            Qk.tpol += i0 * s_tp; Qk.gscale += (size_t)i0 * B; Qk.index += (size_t)i0 * 2 * B;
+            Qk.obs += ir * s_obs; Qk.actions += ir * s_k1; Qk.tv += ir * s_k1; Qk.tr += ir * s_k1;
+            Qk.tpol += ir * s_tp; Qk.gscale += (size_t)ir * B; Qk.index += (size_t)ir * 2 * B;
             // 2. the n unrolls (with their get_batch), loss terms and per-step folds
             LearnMultiParams M;
             std::memset(&M, 0, sizeof(M));
@@ -4022,11 +3996,11 @@ static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, con
             M.bws = h->sm_w_n; M.bbs = h->sm_b_n;
             M.s_obs = s_obs; M.s_k1 = s_k1; M.s_tp = s_tp;
             M.obs = Qk.obs; M.act = Qk.actions; M.tv = Qk.tv; M.tp = Qk.tpol; M.gs = Qk.gscale;
-            M.pv = h->d_ml_pv + i0 * s_k1; M.pp = h->d_ml_pp + i0 * s_tp; M.pr = h->d_ml_pr + i0 * s_k1;
-            M.terms = h->d_ml_terms + 2 * i0 * s_k1;
-            M.part = h->d_ml_part + (size_t)i0 * 3 * MZ_L2_BLOCKS;
-            M.counter = h->d_ml_cnt + (size_t)i0 * MZ_MULTI_CNT_STRIDE;
-            M.out = (losses_dev ? losses_dev : h->d_ml_out) + 8 * i0;
+            M.pv = h->d_ml_pv + ir * s_k1; M.pp = h->d_ml_pp + ir * s_tp; M.pr = h->d_ml_pr + ir * s_k1;
+            M.terms = h->d_ml_terms + 2 * ir * s_k1;
+            M.part = h->d_ml_part + (size_t)ir * 3 * MZ_L2_BLOCKS;
+            M.counter = h->d_ml_cnt + (size_t)ir * MZ_MULTI_CNT_STRIDE;
+            M.out = losses_dev ? losses_dev + 8 * i0 : h->d_ml_out + 8 * ir;
             M.out_last = i0 + n == L ? out_last : nullptr;
             M.sample = chain_sample ? 0 : 1;
             M.q = Qk;
@@ -4044,7 +4018,7 @@ static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, con
     }
     h->last_lvariant = ti == 0 ? "mz_learn_chain+mz_learn_multi1" : "mz_learn_chain+mz_learn_multi2";
     for (int i = 0; i < L; ++i) adam_advance(h);
-    h->ml_last_B = B; h->ml_last_L = L;
+    h->ml_last_B = B; h->ml_last_L = L; h->ml_last_R = R;
     return 0;
 }
 
@@ -4059,15 +4033,16 @@ int mz_learner_train_multi_dev(mz_handle* h, int32_t B, uint32_t step0, int32_t 
 
 int mz_debug_unroll_step(mz_handle* h, int i, int B, float* values, float* policies, float* rewards) {
     if (!h) return -2;
-    if (i < 0 || i >= h->ml_last_L || B < 0 || B > h->ml_last_B)
+    if (i < 0 || i >= h->ml_last_L || i < h->ml_last_L - h->ml_last_R || B < 0 || B > h->ml_last_B)
         return fail(h, "no such step / batch in the last mz_learner_train_multi_dev");
     MZ_TRY(h, hipSetDevice(h->device));
     MZ_SYNC(h);
     const size_t K1 = (size_t)h->conf.num_unroll_steps + 1, A = (size_t)h->A, s = (size_t)h->ml_last_B * K1;
     const size_t n = (size_t)B * K1;
-    if (values) MZ_TRY(h, hipMemcpy(values, h->d_ml_pv + i * s, n * 4, hipMemcpyDeviceToHost));
-    if (policies) MZ_TRY(h, hipMemcpy(policies, h->d_ml_pp + i * s * A, n * A * 4, hipMemcpyDeviceToHost));
-    if (rewards) MZ_TRY(h, hipMemcpy(rewards, h->d_ml_pr + i * s, n * 4, hipMemcpyDeviceToHost));
+    const size_t ir = (size_t)(i % h->ml_last_R);   // the ring slot of step i (ensure_multi)
+    if (values) MZ_TRY(h, hipMemcpy(values, h->d_ml_pv + ir * s, n * 4, hipMemcpyDeviceToHost));
+    if (policies) MZ_TRY(h, hipMemcpy(policies, h->d_ml_pp + ir * s * A, n * A * 4, hipMemcpyDeviceToHost));
+    if (rewards) MZ_TRY(h, hipMemcpy(rewards, h->d_ml_pr + ir * s, n * 4, hipMemcpyDeviceToHost));
     return 0;
 }
 

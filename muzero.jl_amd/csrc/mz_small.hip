@@ -93,68 +93,21 @@ struct SmFusedIn {
     int NN, H, plane, x_pred, x_dyn;
 };
 
-// ((p0+p1)+(p2+p3)) in every lane: with both operands equal, the two halves
-// of a permlane swap are {own, partner} in row order, so their sum is
-// p_even + p_odd in both rows of each pair
-template <int T>
-__device__ __forceinline__ void sm_qsum(float (&acc)[T]) {
-#pragma unroll
-    for (int g = 0; g < T; ++g) {
-        const auto s1 = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, acc[g]),
-                                                         __builtin_bit_cast(unsigned, acc[g]), false, false);
-        const float t = __builtin_bit_cast(float, (unsigned)s1[0]) + __builtin_bit_cast(float, (unsigned)s1[1]);
-        const auto s2 = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, t),
-                                                         __builtin_bit_cast(unsigned, t), false, false);
-        acc[g] = __builtin_bit_cast(float, (unsigned)s2[0]) + __builtin_bit_cast(float, (unsigned)s2[1]);
-    }
-}
-
-// The search's tail stage (SmallParams.tail, mz_engine.hip sm_schedule_tail):
-// the last register set holds only the four head outputs, each on its own
-// wave — value on wave 0, reward on wave 1, policy on wave 2, the state rows
-// on the last P.tail waves — so each is consumed by the wave that computes it, with no
-// workgroup barrier: the stage's dot (the same chain, sums and epilogue
-// arithmetic as sm_stage, hence the same bits) without the store.  Returns
-// this lane's row for game q = its DPP row (every DPP row holds the sums).
-template <int T>
-__device__ __forceinline__ float sm_tail_row(const float (&w)[16], int4 R, const float* lds, const float2* bnp) {
-    const int q = (threadIdx.x >> 4) & 3, i = threadIdx.x & 15;
-    const float* xp = lds + R.x + (q * R.y + i) * T;
-    float x[T];
-#pragma unroll
-    for (int g = 0; g < T; ++g) x[g] = xp[g];
-    float acc[T];
-#pragma unroll
-    for (int g = 0; g < T; ++g) acc[g] = 0.0f;
-    sm_chain<T>(w, x, acc);
-    sm_qsum<T>(acc);
-    float v = acc[0];
-#pragma unroll
-    for (int g = 1; g < T; ++g) v = q == g ? acc[g] : v;
-    float d = v + __int_as_float(R.w);
-    if ((R.z >> 29) & 1) { const float2 gb = *bnp; d = mz_bn_apply(d, gb.x, gb.y); }
-    return (R.z >> 30) & 1 ? mz_relu(d) : d;
-}
-
-// lane 0 of each 16-lane DPP row to the whole row (row_newbcast:0)
-__device__ __forceinline__ float sm_row_bcast0(float v) {
-    float r;
-    asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v));
-    return r;
-}
-
 // One stage.  R = this thread's record of stage K; the record of stage K+1
 // (constant for the whole kernel) is fetched while stage K computes.
-template <int T, int FI = 0>
+// BNM: 1 = the record's BatchNorm bit is tested (make_dense with BatchNorm, test mode), 0 = the
+// nets have no BatchNorm layer (the search kernels' plain instances: no test, no (γ, β) load)
+template <int T, int FI = 0, int BNM = 1>
 __device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int4* rec_next, float* lds,
                                          const SmFusedIn* fi = nullptr, const float2* bnp = nullptr) {
     const int q = (threadIdx.x >> 4) & 3, i = threadIdx.x & 15;
     // x[q*kq + i] of the T games (rows beyond kq meet zero weights; the 64-row
-    // input buffers are zero beyond K, so every step is exact)
-    const float* xp = lds + R.x + (q * R.y + i) * T;
+    // input buffers are zero beyond K, so every step is exact); q·kq as a
+    // 24-bit multiply (full rate, where a 32-bit one is quarter rate)
+    const int k = (int)__umul24((unsigned)q, (unsigned)R.y) + i;
+    const float* xp = lds + R.x + k * T;
     float x[T];
     if constexpr (FI != 0) {
-        const int k = q * R.y + i;
         const bool pred = R.x == fi->x_pred, dyn = R.x == fi->x_dyn;
 #pragma unroll
         for (int g = 0; g < T; ++g) {
@@ -183,35 +136,45 @@ __device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int
 #pragma unroll
     for (int g = 0; g < T; ++g) acc[g] = 0.0f;
     sm_chain<T>(w, x, acc);
-    sm_qsum<T>(acc);
-    if (q == 0 && R.z >= 0) {
-        const int o = R.z & 0x1fffffff;
-        const bool relu = (R.z >> 30) != 0;
-        const float bias = __int_as_float(R.w);
-        const bool bn = (R.z >> 29) & 1;                  // make_dense with BatchNorm (test mode)
-        const float2 gb = bn ? *bnp : make_float2(1.0f, 0.0f);
+    // ((p0+p1)+(p2+p3)) in every lane: with both operands equal, the two
+    // halves of a permlane swap are {own, partner} in row order, so their sum
+    // is p_even + p_odd in both rows of each pair
 #pragma unroll
-        for (int g = 0; g < T; ++g) {
-            float d = acc[g] + bias;
-            if (bn) d = mz_bn_apply(d, gb.x, gb.y);
-            lds[o + g] = relu ? mz_relu(d) : d;
-        }
+    for (int g = 0; g < T; ++g) {
+        const auto s1 = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, acc[g]),
+                                                         __builtin_bit_cast(unsigned, acc[g]), false, false);
+        const float t = __builtin_bit_cast(float, (unsigned)s1[0]) + __builtin_bit_cast(float, (unsigned)s1[1]);
+        const auto s2 = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, t),
+                                                         __builtin_bit_cast(unsigned, t), false, false);
+        acc[g] = __builtin_bit_cast(float, (unsigned)s2[0]) + __builtin_bit_cast(float, (unsigned)s2[1]);
+    }
+    // every DPP row now holds the T sums: DPP row q < T writes game q's row,
+    // so the T epilogues run side by side on different lanes
+    if (q < T && R.z >= 0) {
+        float v = acc[0];
+#pragma unroll
+        for (int g = 1; g < T; ++g) v = q == g ? acc[g] : v;
+        const int o = R.z & 0x1fffffff;
+        float d = v + __int_as_float(R.w);
+        if constexpr (BNM != 0)
+            if ((R.z >> 29) & 1) { const float2 gb = *bnp; d = mz_bn_apply(d, gb.x, gb.y); }
+        lds[o + q] = (R.z >> 30) != 0 ? mz_relu(d) : d;
     }
     __syncthreads();
     return Rn;
 }
 
 // rec: this thread's record of stage 0 ([stage][slot][row] int4, stride 128)
-template <int T, int NMAX, int FI, int OFF, int K = 0>
+template <int T, int NMAX, int FI, int OFF, int BNM, int K = 0>
 __device__ __forceinline__ void sm_run_k(int n, const float (&wr)[NMAX][16], int4 R, const int4* rec, float* lds,
                                          const SmFusedIn* fi, const float2* bnp) {
     if constexpr (K + OFF < NMAX) {
         if (K < n) {
             const float2* bk = bnp + K * (SM_SLOTS * 64);
             const int4 Rn = K == 0 && FI != 0
-                ? sm_stage<T, FI>(wr[K + OFF], R, rec + (K + 1) * (SM_SLOTS * 64), lds, fi, bk)
-                : sm_stage<T>(wr[K + OFF], R, rec + (K + 1) * (SM_SLOTS * 64), lds, nullptr, bk);
-            sm_run_k<T, NMAX, FI, OFF, K + 1>(n, wr, Rn, rec, lds, fi, bnp);
+                ? sm_stage<T, FI, BNM>(wr[K + OFF], R, rec + (K + 1) * (SM_SLOTS * 64), lds, fi, bk)
+                : sm_stage<T, 0, BNM>(wr[K + OFF], R, rec + (K + 1) * (SM_SLOTS * 64), lds, nullptr, bk);
+            sm_run_k<T, NMAX, FI, OFF, BNM, K + 1>(n, wr, Rn, rec, lds, fi, bnp);
         }
     }
 }
@@ -219,10 +182,10 @@ __device__ __forceinline__ void sm_run_k(int n, const float (&wr)[NMAX][16], int
 // FI: 0 = inputs from the activation buffer, 1 = the search's fused first
 // stage, 2 = the learner's (SmFusedIn).  Stage K runs on register set K + OFF.
 // bnp: this thread's (γ, β) column, laid out as `rec` (read only by BatchNorm rows).
-template <int T, int NMAX, int FI = 0, int OFF = 0>
+template <int T, int NMAX, int FI = 0, int OFF = 0, int BNM = 1>
 __device__ __forceinline__ void sm_run(int n, const float (&wr)[NMAX][16], const int4* rec, float* lds,
                                        const SmFusedIn* fi, const float2* bnp) {
-    sm_run_k<T, NMAX, FI, OFF>(n, wr, rec[0], rec, lds, fi, bnp);
+    sm_run_k<T, NMAX, FI, OFF, BNM>(n, wr, rec[0], rec, lds, fi, bnp);
 }
 
 // Weights of this thread's (slot, row, quarter) for stages 0..n-1 from the
@@ -259,7 +222,7 @@ __device__ __forceinline__ void sm_load(int k0, int k1, const float* W, float (&
     }
 }
 
-template <int T>
+template <int T, int BNM>
 __device__ __forceinline__ void small_body(const SmallParams& P) {
 #ifdef MZ_STAMPS
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -285,9 +248,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     int* sg_vtp = si + 128;
     int* sg_depth = si + 144;
     float* sg_stage = reinterpret_cast<float*>(si + 160);       // [4][16]
-    float* sg_rew = reinterpret_cast<float*>(si + 224);           // [4] tail: the reward wave's read-outs
-    int* sg_rflag = si + 228;                                     // tail: simulation + 1 once sg_rew holds it
-    // si + 229 .. 231: unused
+    // si + 224 .. 231: unused (formerly the leaf value / reward read-outs)
     float* sg_noise = reinterpret_cast<float*>(si + 232);       // [4][16] root exploration noise
     int* sg_path = si + 296;                                      // [T][2(S+2)]
     // select / gather tables in LDS (they sit on the per-level critical path)
@@ -352,7 +313,6 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     }
     for (int i = tid; i < T * NN; i += SM_THREADS) c_cache[i] = make_uint2(0u, 0u);
     if (tid < 4) { c_hdr[tid] = make_int4(0, -1, 1, 0); c_mmx[tid] = make_float2(0.0f, 0.0f); c_skip[tid] = 0; }
-    if (tid == 0) *sg_rflag = 0;
     int ver = 1;                                                  // wave 0: the tag of this lane's game
     if (tree_thread && a == 0) {
         uint32_t m = 0;
@@ -371,7 +331,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     if (P.exploration && active)
         sg_noise[16 * g + a] = root_noise_lane(sg_legal[g], a, A, P.seed, gid, P.rng_step, P.dirichlet_alpha,
                                                sg_stage + 16 * g);
-    sm_run<T, SM_MAX_SIM>(P.n_root, wr, rec_root, act, nullptr, bn_root);
+    sm_run<T, SM_MAX_SIM, 0, 0, BNM>(P.n_root, wr, rec_root, act, nullptr, bn_root);
     for (int i = tid; i < T * H; i += SM_THREADS) {     // h -> hidden slot 0 and the prediction input
         const int gl = i / H, k = i - gl * H;
         const float h = act[P.h_out + k * T + gl];
@@ -382,7 +342,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     sm_load<SM_MAX_SIM>(0, P.n_root < P.n_sim ? P.n_root : P.n_sim, P.w_sim, wr, P.nzm, P.zero16);
     __syncthreads();
     // prediction(h) for the root (:239); the dynamics half runs on zeros, unused
-    sm_run<T, SM_MAX_SIM>(P.n_sim, wr, rec_sim, act, nullptr, bn_sim);
+    sm_run<T, SM_MAX_SIM, 0, 0, BNM>(P.n_sim, wr, rec_sim, act, nullptr, bn_sim);
 
     const uint32_t legal = tree_thread ? sg_legal[g] : 0u;
     if (tree_thread) {   // expand_node!(root, legal, to_play, 0, policy, h) (:245)
@@ -434,55 +394,29 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         __syncthreads();
         SM_STAMP(2);
         // ---- prediction(parent.h) ‖ dynamics(2h ⊕ a/|A|): the first stage
-        // reads the parent's h from the hidden-state store (gather fused).
-        // With the tail schedule the last stage is not a barrier stage: its
-        // four head outputs are computed below by the waves that consume them.
-        const bool tail = P.tail > 0;
-        sm_run<T, SM_MAX_SIM, 1>(tail ? P.n_sim - 1 : P.n_sim, wr, rec_sim, act, &fin, bn_sim);
+        // reads the parent's h from the hidden-state store (gather fused)
+        sm_run<T, SM_MAX_SIM, 1, 0, BNM>(P.n_sim, wr, rec_sim, act, &fin, bn_sim);
         SM_STAMP(3);
         const int e_new = s + 1;
-        const int wv = tid >> 6;
-        constexpr int KT = SM_MAX_SIM - 1;
-        float tl_v = 0.0f;                      // this lane's tail row (sm_tail_row)
-        if (tail && (wv <= 2 || wv >= 8 - P.tail))
-            tl_v = sm_tail_row<T>(wr[KT], rec_sim[KT * (SM_SLOTS * 64)], act, bn_sim + KT * (SM_SLOTS * 64));
         // expand (wave 2) runs beside the read-outs + backup (wave 0): they
         // touch disjoint LDS — the new slot's edges vs the path edges, the
         // leaf edge's child link and the new slot's reward / to_play
         if (tid < 64) {
             // ---- value / reward read-out activations, then backpropagate! (:190-217)
-            float val, rew;
-            if (tail) {
-                // the value row is this wave's (row 0 of DPP row g); the reward
-                // comes from wave 1 through LDS (flag = the simulation + 1)
-                val = mz_post_act(P.v_act, sm_row_bcast0(tl_v));
-                unsigned n = 0;
-                while (__hip_atomic_load(sg_rflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != s + 1) {
-                    if (++n > (1u << 24)) {             // cannot happen (wave 4 always publishes): reported
-                        if (P.fault && lane == 0)
-                            __hip_atomic_fetch_or(P.fault, (unsigned)MZ_FAULT_SM_TAIL, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                rew = sg_rew[g];
-            } else {
+            if (active) {
                 // one activation per lane (even lanes the value, odd the reward, both
-                // tanh chains run at once), then each quad's lanes 0 / 1 to all
+                // f64 tanh chains run at once), then each quad's lanes 0 / 1 to all
                 // four by DPP quad_perm [0,0,0,0] / [1,1,1,1]
                 const bool odd = (a & 1) != 0;
                 const float ro = mz_post_act(odd ? P.r_act : P.v_act, act[(odd ? P.r_out : P.v_out) + g]);
-                val = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                const float val = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
                     0, __builtin_bit_cast(int, ro), 0x00, 0xF, 0xF, false));
-                rew = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                const float rew = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
                     0, __builtin_bit_cast(int, ro), 0x55, 0xF, 0xF, false));
-            }
 #ifdef MZ_STAMPS
-            if (threadIdx.x == 0) asm volatile("" :: "v"(val), "v"(rew));
+                if (threadIdx.x == 0) asm volatile("" :: "v"(val), "v"(rew));
 #endif
-            SM_STAMP(5);                        // stamp build: slot 5 = the read-out activations
-            if (active) {
+                SM_STAMP(5);                    // stamp build: slot 5 = the read-out activations
                 const int tl = sg_vtp[g];
                 const int depth = sg_depth[g];
                 if (a == 0) {
@@ -512,26 +446,9 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
             const int g2 = (tid - 128) >> 4;
             const bool active2 = tile0 + g2 < P.G;
             TreeView tree2 = tree_view(lds_tree + (size_t)g2 * P.tree_game_bytes, E, NN);
-            const float logit = tail ? tl_v : act[P.p_out + a * T + g2];   // (tail: row a of DPP row g2)
-            const float prior = double_softmax_prior(a < A ? logit : 0.0f, a, A, sg_legal[g2], sg_stage + 16 * g2);
+            const float prior = double_softmax_prior(a < A ? act[P.p_out + a * T + g2] : 0.0f, a, A, sg_legal[g2],
+                                                     sg_stage + 16 * g2);
             if (active2) init_edges(tree2, e_new, a, A, prior);
-        } else if (tail) {
-            if (wv == 1) {                      // the reward row (row 0 of DPP row g) -> wave 0
-                const int q = (tid >> 4) & 3;
-                if ((tid & 15) == 0 && q < T) sg_rew[q] = mz_post_act(P.r_act, tl_v);
-                if (lane == 0) __hip_atomic_store(sg_rflag, s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else if (wv >= 8 - P.tail) {      // h' rows 16(wv - 8 + tail) + i of game q, stored in place
-                const int q = (tid >> 4) & 3, row = 16 * (wv - 8 + P.tail) + (tid & 15);
-                if (q < T && row < H) hid[((size_t)q * NN + e_new) * H + row] = tl_v;
-            } else if (wv == 3) {               // parent h *= 2 (Q1)
-                for (int i = lane; i < T * H; i += 64) {
-                    const int gl = i / H, k = i - gl * H;
-                    if (tile0 + gl < P.G) {
-                        float* hp = hid + ((size_t)gl * NN + sg_leaf_e[gl]) * H + k;
-                        *hp = *hp * 2.0f;
-                    }
-                }
-            }
         } else if (tid >= 192) {
             for (int i = tid - 192; i < T * H; i += SM_THREADS - 192) {   // store h'; parent h *= 2 (Q1)
                 const int gl = i / H, k = i - gl * H;
@@ -609,9 +526,13 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
 #endif
 }
 
-extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_search_small1(SmallParams P) { small_body<1>(P); }
-extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_search_small2(SmallParams P) { small_body<2>(P); }
-extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_search_small4(SmallParams P) { small_body<4>(P); }
+// (the _bn instances: nets with BatchNorm FC layers, SmallParams.bn)
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_search_small1(SmallParams P) { small_body<1, 0>(P); }
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_search_small2(SmallParams P) { small_body<2, 0>(P); }
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_search_small4(SmallParams P) { small_body<4, 0>(P); }
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_search_small1_bn(SmallParams P) { small_body<1, 1>(P); }
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_search_small2_bn(SmallParams P) { small_body<2, 1>(P); }
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_search_small4_bn(SmallParams P) { small_body<4, 1>(P); }
 
 // ---------------------------------------------------------------- learner
 // K-step unroll of Learning.jl:327-343 (Q10 alignment, as mz_unroll_kernel):
@@ -849,13 +770,46 @@ extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_small2(Smal
 // each thread runs its parameters' L ADAM iterations (∇ = 2θ, Q11) in registers
 // and keeps one Σθ_{t+i}² per step in lg_l2_slice's order; the per-step trees
 // are lg_tree256's, level by level.  The blocks after them draw the L batches.
-// At most 112 VGPRs: one wave per SIMD fits beside a resident mz_learn_multi*
-// workgroup (2 waves x 197 of the 512), so the next sub-chunk's chain runs on
-// the CUs the unroll launch occupies (learner_multi's two streams).
+// The chain and the unroll launches run one after another in stream order
+// (a two-stream variant that overlapped them measured slower, mz_engine.hip
+// learner_multi), so the chain's 66 KB of static LDS never shares a CU with
+// an unroll workgroup.
+// this thread's parameters of slice (net, sb): L ADAM iterations in registers; CAP: θ after steps
+// cap_i[0] / cap_i[1] also copied out (a separate instance: the plain chain carries no per-step tests)
+template <bool CAP>
+__device__ __forceinline__ void chain_slice(const ChainParams& C, int net, int sb, double (*red)[MZ_THREADS],
+                                            double (*sbp)[MZ_MULTI_MAX]) {
+    const int tid = threadIdx.x, L = C.L;
+    const size_t off = C.netoff[net], cnt = C.netoff[3 + net];
+    const size_t stride = (size_t)MZ_L2_BLOCKS * MZ_THREADS;
+    for (size_t e = (size_t)sb * MZ_THREADS + tid; e < cnt; e += stride) {
+        const size_t p = off + e;
+        float x = C.flat[p], m = C.M[p], v = C.V[p];
+        const int it = C.inv_tile[p], is = C.inv_small[p];
+        const bool sbank = C.bank_w != nullptr, tbank = C.tbank_w != nullptr;   // (uniform)
+        for (int i = 0; i < L; ++i) {
+            red[i][tid] += (double)x * (double)x;                   // step t+i's Σθ² reads θ_{t+i}
+#ifndef MZ_DBG_NO_BANK   // diagnostic only (wrong results): the chain without the bank scatter
+            if (sbank) mz_scatter(x, is, C.bank_w + i * C.bws, C.bank_b + i * C.bbs);
+#endif
+            if (tbank) mz_scatter(x, it, C.tbank_w + i * C.tws, C.tbank_b + i * C.tbs);
+            if (C.fbank) C.fbank[i * C.fstride + p] = x;
+            x = adam_2theta(x, m, v, sbp[0][i], sbp[1][i], sbp[2][i]);   // Learning.jl:395-397
+            if (C.theta) C.theta[i * C.nflat + p] = x;
+            if constexpr (CAP) {
+                if (i == C.cap_i[0]) C.cap_dst[0][p] = x;
+                if (i == C.cap_i[1]) C.cap_dst[1][p] = x;
+            }
+        }
+        C.flat[p] = x; C.M[p] = m; C.V[p] = v;
+        mz_scatter(x, it, C.Wp, C.Bp);
+        mz_scatter(x, is, C.smw, C.smb);
+    }
+}
+
 extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learn_chain(ChainParams C) {
-    // per step i: this thread's Σθ_{t+i}² (accumulated in place: no register
-    // array, so one wave per SIMD fits beside a resident mz_learn_multi*
-    // workgroup and the next sub-chunk's chain runs under the unroll launch)
+    // per step i: this thread's Σθ_{t+i}² (accumulated in place in LDS: no
+    // register array indexed by the runtime step)
     __shared__ double red[MZ_MULTI_MAX][MZ_THREADS];
     __shared__ double sbp[3][MZ_MULTI_MAX];         // β1^t, β2^t, η of step t+i
     const int tid = threadIdx.x, blk = (int)blockIdx.x;
@@ -876,29 +830,8 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learn_chain(ChainPar
     for (int i = 0; i < L; ++i) red[i][tid] = 0.0;
     __syncthreads();
     const int net = blk / MZ_L2_BLOCKS, sb = blk - net * MZ_L2_BLOCKS;
-    const size_t off = C.netoff[net], cnt = C.netoff[3 + net];
-    const size_t stride = (size_t)MZ_L2_BLOCKS * MZ_THREADS;
-    for (size_t e = (size_t)sb * MZ_THREADS + tid; e < cnt; e += stride) {
-        const size_t p = off + e;
-        float x = C.flat[p], m = C.M[p], v = C.V[p];
-        const int it = C.inv_tile[p], is = C.inv_small[p];
-        const bool sbank = C.bank_w != nullptr, tbank = C.tbank_w != nullptr;   // (uniform)
-        for (int i = 0; i < L; ++i) {
-            red[i][tid] += (double)x * (double)x;                   // step t+i's Σθ² reads θ_{t+i}
-#ifndef MZ_DBG_NO_BANK   // diagnostic only (wrong results): the chain without the bank scatter
-            if (sbank) mz_scatter(x, is, C.bank_w + i * C.bws, C.bank_b + i * C.bbs);
-#endif
-            if (tbank) mz_scatter(x, it, C.tbank_w + i * C.tws, C.tbank_b + i * C.tbs);
-            if (C.fbank) C.fbank[i * C.nflat + p] = x;
-            x = adam_2theta(x, m, v, sbp[0][i], sbp[1][i], sbp[2][i]);   // Learning.jl:395-397
-            if (C.theta) C.theta[i * C.nflat + p] = x;
-            if (i == C.cap_i[0]) C.cap_dst[0][p] = x;
-            if (i == C.cap_i[1]) C.cap_dst[1][p] = x;
-        }
-        C.flat[p] = x; C.M[p] = m; C.V[p] = v;
-        mz_scatter(x, it, C.Wp, C.Bp);
-        mz_scatter(x, is, C.smw, C.smb);
-    }
+    if (C.cap_i[0] < 0 && C.cap_i[1] < 0) chain_slice<false>(C, net, sb, red, sbp);
+    else chain_slice<true>(C, net, sb, red, sbp);             // (mz_train_run's refresh steps in this chain)
     __syncthreads();
     for (int o = MZ_THREADS / 2; o > 0; o >>= 1) {   // lg_tree256, per step
         if (tid < o)

@@ -72,10 +72,6 @@ struct SmallParams {
     const float4* zero16;    // 16 zero bytes: the address of a skipped chunk's load
     uint32_t nzm[SM_NZM_ALLOC];  // nonzero-chunk masks [wave][stage]: sim stages, then root stages (+ pad)
     int bn;                  // BatchNorm FC layers: `bias` has γ and β sections after the biases
-    // the tail schedule (mz_engine.hip sm_schedule_tail): 0 = off, else the number of
-    // waves (from wave 5) holding the state head's output rows in the last register set
-    int tail;
-    unsigned* fault;         // device fault word (MZ_FAULT_SM_TAIL)
 };
 
 // Learner unroll on the small-kernel schedule (mz_unroll_small*): T samples
@@ -155,7 +151,8 @@ struct ChainParams {
     float* Wp; float* Bp; float* smw; float* smb;     // the current images: θ_{t+L}
     float* bank_w; float* bank_b; size_t bws, bbs;     // bank image i (small-kernel W, bias): θ_{t+i} (or NULL)
     float* tbank_w; float* tbank_b; size_t tws, tbs;   // bank image i of the tile / ResNet MFMA image (or NULL)
-    float* fbank;                                      // NULL or [L][nflat]: θ_{t+i}, the flat parameters of step t+i
+    float* fbank;                                      // NULL or [L][fstride]: θ_{t+i}, the flat parameters of step t+i
+    size_t fstride;                                    // nflat rounded up to 4 (16-byte rows: the downsampler's float4 reads)
     float* theta;                                      // NULL or [L][nflat]: θ after step t+i
     int cap_i[2]; float* cap_dst[2];                   // θ after step t+cap_i[j] -> cap_dst[j] (cap_i < 0: none;
                                                        // mz_train_run's actor / queued sets at refresh steps)
