@@ -81,11 +81,17 @@ extern "C" __global__ void mz_search_small2_bn(SmallParams P);
 extern "C" __global__ void mz_search_small4_bn(SmallParams P);
 extern "C" __global__ void mz_unroll_small1(SmallUnrollParams P);
 extern "C" __global__ void mz_unroll_small2(SmallUnrollParams P);
+extern "C" __global__ void mz_unroll_small1_bn(SmallUnrollParams P);
+extern "C" __global__ void mz_unroll_small2_bn(SmallUnrollParams P);
 extern "C" __global__ void mz_learn_small1(SmallUnrollParams P, LearnParams L);
 extern "C" __global__ void mz_learn_small2(SmallUnrollParams P, LearnParams L);
+extern "C" __global__ void mz_learn_small1_bn(SmallUnrollParams P, LearnParams L);
+extern "C" __global__ void mz_learn_small2_bn(SmallUnrollParams P, LearnParams L);
 extern "C" __global__ void mz_learn_chain(ChainParams C);
 extern "C" __global__ void mz_learn_multi1(SmallUnrollParams P, LearnMultiParams M);
 extern "C" __global__ void mz_learn_multi2(SmallUnrollParams P, LearnMultiParams M);
+extern "C" __global__ void mz_learn_multi1_bn(SmallUnrollParams P, LearnMultiParams M);
+extern "C" __global__ void mz_learn_multi2_bn(SmallUnrollParams P, LearnMultiParams M);
 extern "C" __global__ void mz_learner_loss_multi(LossMultiParams M);
 extern "C" __global__ void mz_learner_loss_multi32(LossMultiParams M);
 extern "C" __global__ void mz_search_kernel_hbm_res(SearchParams P);
@@ -1648,10 +1654,11 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
             for (int ti = 0; ti < 6; ++ti)
                 CK(hipFuncSetAttribute(ks[ti], hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->sm_lds[ti % 3]) ==
                            hipSuccess ? 0 : fail(h, "hipFuncSetAttribute(small)"));
-            const void* ku[2] = {(const void*)mz_unroll_small1, (const void*)mz_unroll_small2};
-            for (int ti = 0; ti < 2; ++ti)
+            const void* ku[4] = {(const void*)mz_unroll_small1, (const void*)mz_unroll_small2,
+                                 (const void*)mz_unroll_small1_bn, (const void*)mz_unroll_small2_bn};
+            for (int ti = 0; ti < 4; ++ti)
                 CK(hipFuncSetAttribute(ku[ti], hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)unroll_small_lds(h, ti)) == hipSuccess
+                                       (int)unroll_small_lds(h, ti & 1)) == hipSuccess
                        ? 0 : fail(h, "hipFuncSetAttribute(unroll_small)"));
         }
     }
@@ -1664,9 +1671,11 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
     if (h->small_ok) {
         CK(al(&h->d_Wp2, h->packed_w_n)); CK(al(&h->d_Bp2, h->packed_b_n));
         CK(al(&h->d_sm_w2, h->sm_w_n)); CK(al(&h->d_sm_bias2, h->sm_b_n));
-        const void* kl[4] = {(const void*)mz_learn_small1, (const void*)mz_learn_small2,
-                             (const void*)mz_learn_multi1, (const void*)mz_learn_multi2};
-        for (int ti = 0; ti < 4; ++ti)
+        const void* kl[8] = {(const void*)mz_learn_small1, (const void*)mz_learn_small2,
+                             (const void*)mz_learn_multi1, (const void*)mz_learn_multi2,
+                             (const void*)mz_learn_small1_bn, (const void*)mz_learn_small2_bn,
+                             (const void*)mz_learn_multi1_bn, (const void*)mz_learn_multi2_bn};
+        for (int ti = 0; ti < 8; ++ti)
             CK(hipFuncSetAttribute(kl[ti], hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)unroll_small_lds(h, ti & 1)) == hipSuccess
                    ? 0 : fail(h, "hipFuncSetAttribute(learn_small)"));
@@ -2244,7 +2253,8 @@ static int fc_unroll(mz_handle* h, const mz_batch* b, hipStream_t st, const RpSa
         SmallUnrollParams U;
         if (small_unroll_params(h, b, ti, rp, &U)) return -1;
         void* args[] = {&U};
-        MZ_TRY(h, hipLaunchKernel(ti == 0 ? (const void*)mz_unroll_small1 : (const void*)mz_unroll_small2,
+        MZ_TRY(h, hipLaunchKernel(h->sm_bn ? (ti == 0 ? (const void*)mz_unroll_small1_bn : (const void*)mz_unroll_small2_bn)
+                                           : (ti == 0 ? (const void*)mz_unroll_small1 : (const void*)mz_unroll_small2),
                                   dim3((B + T - 1) / T), dim3(SM_THREADS), args, unroll_small_lds(h, ti), st));
         h->last_lvariant = ti == 0 ? "mz_unroll_small1" : "mz_unroll_small2";
     } else {
@@ -3548,7 +3558,8 @@ static int learner_sampled(mz_handle* h, int32_t B, uint32_t step, float* grad_d
         static const bool xcd = std::getenv("MZ_LEARN_XCD") != nullptr;
         L.xcd = xcd && L.nU <= h->n_cu / 8 && 8 * L.nU >= roles;
         void* args[] = {&U, &L};
-        MZ_TRY(h, hipLaunchKernel(ti == 0 ? (const void*)mz_learn_small1 : (const void*)mz_learn_small2,
+        MZ_TRY(h, hipLaunchKernel(h->sm_bn ? (ti == 0 ? (const void*)mz_learn_small1_bn : (const void*)mz_learn_small2_bn)
+                                           : (ti == 0 ? (const void*)mz_learn_small1 : (const void*)mz_learn_small2),
                                   dim3(L.xcd ? 8 * L.nU : roles), dim3(SM_THREADS), args,
                                   unroll_small_lds(h, ti), st));
         if (pf) h->pf_cur = 1 - cur;
@@ -4011,7 +4022,8 @@ static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, con
                 if (timing_events(h, &e0, &e1)) return -1;
                 MZ_TRY(h, hipEventRecord(e0, st));
             }
-            MZ_TRY(h, hipLaunchKernel(ti == 0 ? (const void*)mz_learn_multi1 : (const void*)mz_learn_multi2,
+            MZ_TRY(h, hipLaunchKernel(h->sm_bn ? (ti == 0 ? (const void*)mz_learn_multi1_bn : (const void*)mz_learn_multi2_bn)
+                                               : (ti == 0 ? (const void*)mz_learn_multi1 : (const void*)mz_learn_multi2),
                                       dim3(grid), dim3(SM_THREADS), args, unroll_small_lds(h, ti), st));
             if (e1) MZ_TRY(h, hipEventRecord(e1, st));
         }

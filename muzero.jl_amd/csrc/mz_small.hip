@@ -408,7 +408,14 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
                 // f64 tanh chains run at once), then each quad's lanes 0 / 1 to all
                 // four by DPP quad_perm [0,0,0,0] / [1,1,1,1]
                 const bool odd = (a & 1) != 0;
+#ifdef MZ_DIAG_TANH_TWICE     // diagnostic (same results): the read-out activations twice
+                float rin = act[(odd ? P.r_out : P.v_out) + g];
+                const float ro0 = mz_post_act(odd ? P.r_act : P.v_act, rin);
+                asm volatile("" : "+v"(rin) : "v"(ro0));
+                const float ro = mz_post_act(odd ? P.r_act : P.v_act, rin);
+#else
                 const float ro = mz_post_act(odd ? P.r_act : P.v_act, act[(odd ? P.r_out : P.v_out) + g]);
+#endif
                 const float val = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
                     0, __builtin_bit_cast(int, ro), 0x00, 0xF, 0xF, false));
                 const float rew = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
@@ -446,8 +453,15 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
             const int g2 = (tid - 128) >> 4;
             const bool active2 = tile0 + g2 < P.G;
             TreeView tree2 = tree_view(lds_tree + (size_t)g2 * P.tree_game_bytes, E, NN);
+#ifdef MZ_DIAG_EXPAND_TWICE   // diagnostic (same results): the double softmax twice — is expand on the critical path?
+            float lgt = act[P.p_out + a * T + g2];
+            const float prior0 = double_softmax_prior(a < A ? lgt : 0.0f, a, A, sg_legal[g2], sg_stage + 16 * g2);
+            asm volatile("" : "+v"(lgt) : "v"(prior0));
+            const float prior = double_softmax_prior(a < A ? lgt : 0.0f, a, A, sg_legal[g2], sg_stage + 16 * g2);
+#else
             const float prior = double_softmax_prior(a < A ? act[P.p_out + a * T + g2] : 0.0f, a, A, sg_legal[g2],
                                                      sg_stage + 16 * g2);
+#endif
             if (active2) init_edges(tree2, e_new, a, A, prior);
         } else if (tid >= 192) {
             for (int i = tid - 192; i < T * H; i += SM_THREADS - 192) {   // store h'; parent h *= 2 (Q1)
@@ -553,7 +567,7 @@ __device__ __forceinline__ SmIO sm_io(const SmallUnrollParams& P) {
     return SmIO{P.obs, P.actions, P.pv, P.pp, P.pr, P.w_sim, P.w_root, P.bias};
 }
 
-template <int T>
+template <int T, int BNM>
 __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P, int lb, const SmIO& io) {
 #ifdef MZ_STAMPS
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -635,7 +649,7 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P, int lb, 
     const int4* rec_root = rec_sim + P.n_sim * (SM_SLOTS * 64);
     const float2* bn_sim = bnl + sm_slot_row(tid);
     const float2* bn_root = bn_sim + P.n_sim * (SM_SLOTS * 64);
-    sm_run<T, SM_MAX_SIM, 0, RO>(P.n_root, wr, rec_root, act, nullptr, bn_root);
+    sm_run<T, SM_MAX_SIM, 0, RO, BNM>(P.n_root, wr, rec_root, act, nullptr, bn_root);
     SM_STAMP(1);                                   // repr stages
     // reload the representation's sets; in flight under step 1's first RO stages
     sm_load<SM_MAX_SIM>(RO, RO + P.n_root < P.n_sim ? RO + P.n_root : P.n_sim, io.w_sim, wr, P.nzm, P.zero16);
@@ -646,7 +660,7 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P, int lb, 
         // ago) and the step's a/|A|
         const SmFusedIn fin{act + P.h_out, nullptr, nullptr, aval + (i - 1), K + 1, H, P.plane, P.x_pred, P.x_dyn};
         SM_STAMP(3);                               // step inputs (none left: fused)
-        sm_run<T, SM_MAX_SIM, 2>(P.n_sim, wr, rec_sim, act, &fin, bn_sim);
+        sm_run<T, SM_MAX_SIM, 2, 0, BNM>(P.n_sim, wr, rec_sim, act, &fin, bn_sim);
         SM_STAMP(4);                               // the 8 stages
         // raw outputs (logits, value, reward before their read-out
         // activations); mz_learner_grad_kernel applies softmax / tanh for all
@@ -683,15 +697,17 @@ __device__ __forceinline__ void unroll_body(const SmallUnrollParams& P, int lb, 
 #endif
 }
 
-extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small1(SmallUnrollParams P) { unroll_body<1>(P, blockIdx.x, sm_io(P)); }
-extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small2(SmallUnrollParams P) { unroll_body<2>(P, blockIdx.x, sm_io(P)); }
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small1(SmallUnrollParams P) { unroll_body<1, 0>(P, blockIdx.x, sm_io(P)); }
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small2(SmallUnrollParams P) { unroll_body<2, 0>(P, blockIdx.x, sm_io(P)); }
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small1_bn(SmallUnrollParams P) { unroll_body<1, 1>(P, blockIdx.x, sm_io(P)); }
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_unroll_small2_bn(SmallUnrollParams P) { unroll_body<2, 1>(P, blockIdx.x, sm_io(P)); }
 
 // One learner iteration in one launch (LearnParams): unroll (+ get_batch) and
 // each tile's loss terms ‖ Σθ² + ADAM into the second image set; last block
 // folds.  Same results as mz_unroll_small* + mz_learner_grad_kernel (fused
 // ADAM): the loss terms, the θ² slices (256-thread groups) and the fold are
 // the same code on the same decomposition.
-template <int T>
+template <int T, int BNM>
 __device__ __forceinline__ void learn_body(const SmallUnrollParams& P, const LearnParams& L) {
     __shared__ float stg[SM_THREADS];
     __shared__ double red[SM_THREADS];
@@ -708,7 +724,7 @@ __device__ __forceinline__ void learn_body(const SmallUnrollParams& P, const Lea
     const int pb = (int)blockIdx.x;
     const int lb = L.xcd ? ((pb & 7) == 0 ? pb >> 3 : L.nU + pb - (pb >> 3) - 1) : pb;
     if (lb < L.nU) {
-        unroll_body<T>(P, lb, sm_io(P));
+        unroll_body<T, BNM>(P, lb, sm_io(P));
 #ifdef MZ_STAMPS
         const unsigned long long t_unroll = __builtin_amdgcn_s_memtime();
 #endif
@@ -757,10 +773,16 @@ __device__ __forceinline__ void learn_body(const SmallUnrollParams& P, const Lea
 }
 
 extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_small1(SmallUnrollParams P, LearnParams L) {
-    learn_body<1>(P, L);
+    learn_body<1, 0>(P, L);
 }
 extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_small2(SmallUnrollParams P, LearnParams L) {
-    learn_body<2>(P, L);
+    learn_body<2, 0>(P, L);
+}
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_small1_bn(SmallUnrollParams P, LearnParams L) {
+    learn_body<1, 1>(P, L);
+}
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_small2_bn(SmallUnrollParams P, LearnParams L) {
+    learn_body<2, 1>(P, L);
 }
 
 
@@ -844,7 +866,7 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learn_chain(ChainPar
 // mz_learn_multi{1,2}: workgroup (step i, tile lb).  With M.xcd, step i's
 // workgroups are the physical blocks on XCD i mod 8 (round-robin dispatch), so
 // each XCD's L2 holds its steps' bank images only.
-template <int T>
+template <int T, int BNM>
 __device__ __forceinline__ void learn_multi_body(const SmallUnrollParams& P, const LearnMultiParams& M) {
     __shared__ float stg[SM_THREADS];
     const int tid = threadIdx.x, pb = (int)blockIdx.x;
@@ -877,7 +899,7 @@ __device__ __forceinline__ void learn_multi_body(const SmallUnrollParams& P, con
     io.w_sim = M.bank_w + i * M.bws;
     io.w_root = io.w_sim + (size_t)P.n_sim * SM_SLOTS * 256 * 16;
     io.bias = M.bank_b + i * M.bbs;
-    unroll_body<T>(P, lb, io);
+    unroll_body<T, BNM>(P, lb, io);
     __syncthreads();                                // the tile's raw outputs -> its loss groups
     float* vsq = M.terms + 2 * i * M.s_k1;
     float* cet = vsq + M.s_k1;
@@ -892,8 +914,14 @@ __device__ __forceinline__ void learn_multi_body(const SmallUnrollParams& P, con
 }
 
 extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_multi1(SmallUnrollParams P, LearnMultiParams M) {
-    learn_multi_body<1>(P, M);
+    learn_multi_body<1, 0>(P, M);
 }
 extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_multi2(SmallUnrollParams P, LearnMultiParams M) {
-    learn_multi_body<2>(P, M);
+    learn_multi_body<2, 0>(P, M);
+}
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_multi1_bn(SmallUnrollParams P, LearnMultiParams M) {
+    learn_multi_body<1, 1>(P, M);
+}
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_multi2_bn(SmallUnrollParams P, LearnMultiParams M) {
+    learn_multi_body<2, 1>(P, M);
 }
