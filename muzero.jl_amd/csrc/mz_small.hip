@@ -93,21 +93,30 @@ struct SmFusedIn {
     int NN, H, plane, x_pred, x_dyn;
 };
 
-// One stage.  R = this thread's record of stage K; the record of stage K+1
-// (constant for the whole kernel) is fetched while stage K computes.
+// This thread's input offset in a stage with record R: x[q*kq + i] of the T
+// games (rows beyond kq meet zero weights; the 64-row input buffers are zero
+// beyond K, so every step is exact); q·kq as a 24-bit multiply (full rate,
+// where a 32-bit one is quarter rate)
+template <int T>
+__device__ __forceinline__ int sm_xoff(int4 R) {      // (in bytes)
+    const int q = (threadIdx.x >> 4) & 3, i = threadIdx.x & 15;
+    return (R.x + ((int)__umul24((unsigned)q, (unsigned)R.y) + i) * T) * 4;
+}
+
+// One stage.  R = this thread's record of stage K, xo its input offset
+// (sm_xoff); the record of stage K+1 (constant for the whole kernel) is
+// fetched while stage K computes, and its offset formed before the barrier,
+// so the next stage's input load issues right after it (xo is updated).
 // BNM: 1 = the record's BatchNorm bit is tested (make_dense with BatchNorm, test mode), 0 = the
 // nets have no BatchNorm layer (the search kernels' plain instances: no test, no (γ, β) load)
 template <int T, int FI = 0, int BNM = 1>
-__device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int4* rec_next, float* lds,
+__device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, int& xo, const int4* rec_next, float* lds,
                                          const SmFusedIn* fi = nullptr, const float2* bnp = nullptr) {
-    const int q = (threadIdx.x >> 4) & 3, i = threadIdx.x & 15;
-    // x[q*kq + i] of the T games (rows beyond kq meet zero weights; the 64-row
-    // input buffers are zero beyond K, so every step is exact); q·kq as a
-    // 24-bit multiply (full rate, where a 32-bit one is quarter rate)
-    const int k = (int)__umul24((unsigned)q, (unsigned)R.y) + i;
-    const float* xp = lds + R.x + k * T;
+    const int q = (threadIdx.x >> 4) & 3;
+    const float* xp = reinterpret_cast<const float*>(reinterpret_cast<const char*>(lds) + xo);
     float x[T];
     if constexpr (FI != 0) {
+        const int k = (int)__umul24((unsigned)q, (unsigned)R.y) + (int)(threadIdx.x & 15);
         const bool pred = R.x == fi->x_pred, dyn = R.x == fi->x_dyn;
 #pragma unroll
         for (int g = 0; g < T; ++g) {
@@ -160,21 +169,23 @@ __device__ __forceinline__ int4 sm_stage(const float (&w)[16], int4 R, const int
             if ((R.z >> 29) & 1) { const float2 gb = *bnp; d = mz_bn_apply(d, gb.x, gb.y); }
         lds[o + q] = (R.z >> 30) != 0 ? mz_relu(d) : d;
     }
+    xo = sm_xoff<T>(Rn);
+    asm volatile("" : "+v"(xo));     // formed here, not sunk below the barrier
     __syncthreads();
     return Rn;
 }
 
 // rec: this thread's record of stage 0 ([stage][slot][row] int4, stride 128)
 template <int T, int NMAX, int FI, int OFF, int BNM, int K = 0>
-__device__ __forceinline__ void sm_run_k(int n, const float (&wr)[NMAX][16], int4 R, const int4* rec, float* lds,
-                                         const SmFusedIn* fi, const float2* bnp) {
+__device__ __forceinline__ void sm_run_k(int n, const float (&wr)[NMAX][16], int4 R, int xo, const int4* rec,
+                                         float* lds, const SmFusedIn* fi, const float2* bnp) {
     if constexpr (K + OFF < NMAX) {
         if (K < n) {
             const float2* bk = bnp + K * (SM_SLOTS * 64);
             const int4 Rn = K == 0 && FI != 0
-                ? sm_stage<T, FI, BNM>(wr[K + OFF], R, rec + (K + 1) * (SM_SLOTS * 64), lds, fi, bk)
-                : sm_stage<T, 0, BNM>(wr[K + OFF], R, rec + (K + 1) * (SM_SLOTS * 64), lds, nullptr, bk);
-            sm_run_k<T, NMAX, FI, OFF, BNM, K + 1>(n, wr, Rn, rec, lds, fi, bnp);
+                ? sm_stage<T, FI, BNM>(wr[K + OFF], R, xo, rec + (K + 1) * (SM_SLOTS * 64), lds, fi, bk)
+                : sm_stage<T, 0, BNM>(wr[K + OFF], R, xo, rec + (K + 1) * (SM_SLOTS * 64), lds, nullptr, bk);
+            sm_run_k<T, NMAX, FI, OFF, BNM, K + 1>(n, wr, Rn, xo, rec, lds, fi, bnp);
         }
     }
 }
@@ -185,7 +196,8 @@ __device__ __forceinline__ void sm_run_k(int n, const float (&wr)[NMAX][16], int
 template <int T, int NMAX, int FI = 0, int OFF = 0, int BNM = 1>
 __device__ __forceinline__ void sm_run(int n, const float (&wr)[NMAX][16], const int4* rec, float* lds,
                                        const SmFusedIn* fi, const float2* bnp) {
-    sm_run_k<T, NMAX, FI, OFF, BNM>(n, wr, rec[0], rec, lds, fi, bnp);
+    const int4 R0 = rec[0];
+    sm_run_k<T, NMAX, FI, OFF, BNM>(n, wr, R0, sm_xoff<T>(R0), rec, lds, fi, bnp);
 }
 
 // Weights of this thread's (slot, row, quarter) for stages 0..n-1 from the

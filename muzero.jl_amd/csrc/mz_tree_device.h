@@ -128,6 +128,10 @@ template <int GW> __device__ __forceinline__ int gisum(int v) {
 // lane returns the same value (the oracle's `s = s + y[i]` loop order).  The
 // values are staged through this group's GW-float LDS slot `st` (same wave:
 // LDS ops complete in order) and read back as GW/4 broadcast b128 loads.
+// Every caller's lanes n..GW-1 hold +0, and a partial sum that starts at +0 is
+// never -0 (x + -0 = x for x = +0 in round-to-nearest), so adding them is exact:
+// the sum runs in blocks of four, a block skipped by a wave-uniform branch once
+// it starts past n — a plain dependent add chain, with no per-element select.
 template <int GW>
 __device__ __forceinline__ float gseqsum(float v, int n, float* st, int a) {
     st[a] = v;
@@ -139,9 +143,12 @@ __device__ __forceinline__ float gseqsum(float v, int n, float* st, int a) {
         x[b] = q.x; x[b + 1] = q.y; x[b + 2] = q.z; x[b + 3] = q.w;
     }
     __builtin_amdgcn_wave_barrier();
-    float s = 0.0f;
+    const int nu = __builtin_amdgcn_readfirstlane(n);
+    float s = x[0] + 0.0f;                  // (= 0.0f + x[0], the oracle's first step)
+    s = s + x[1]; s = s + x[2]; s = s + x[3];
 #pragma unroll
-    for (int b = 0; b < GW; ++b) if (b < n) s = s + x[b];
+    for (int b = 4; b < GW; b += 4)
+        if (b < nu) { s = s + x[b]; s = s + x[b + 1]; s = s + x[b + 2]; s = s + x[b + 3]; }
     return s;
 }
 __device__ __forceinline__ float g16_seqsum(float v, int n, float* st, int a) { return gseqsum<16>(v, n, st, a); }

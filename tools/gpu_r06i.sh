@@ -1,10 +1,15 @@
 #!/bin/bash
-# Round 6: which post-network phase is on the critical path — the search line with the expand's
-# double softmax computed twice (x_exp2) and with the read-out activations twice (x_tanh2), same results.
+# Round 6: (1) parity of the search / learner kernels on this tree (the next stage's input offset
+# formed before the barrier); (2) which post-network phase is on the critical path — the search line
+# with the expand's double softmax computed twice (x_exp2) and with the read-out activations twice
+# (x_tanh2), both same results, against the previous commit's library (prev) and this tree (cur).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R" && mkdir -p gpurun_out/r6i && export TMPDIR=/tmp
 O=$R/gpurun_out/r6i
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_fc_bn.py \
+  tests/test_learner_multi_gpu.py tests/test_gpu_parity.py tests/test_bench_sizes_gpu.py tests/test_golden.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
 for i in 1 2; do
   for v in cur x_exp2 x_tanh2; do
     unset MZ_LIB
