@@ -33,8 +33,14 @@
             st_acc[i] += t_ - st_last; st_last = t_;                             \
         }                                                                        \
     } while (0)
+// the post-network phase per wave (thread 0: backup, 128: expand, 192: h' store),
+// written to the second half of the stamps array (blocks gridDim.x + b)
+#define W_STAMP0() unsigned long long w_t0_ = __builtin_amdgcn_s_memtime()
+#define W_STAMP(k) do { w_acc[k] += __builtin_amdgcn_s_memtime() - w_t0_; } while (0)
 #else
 #define SM_STAMP(i) do {} while (0)
+#define W_STAMP0() do {} while (0)
+#define W_STAMP(k) do {} while (0)
 #endif
 
 // Thread -> (slot, slot row, quarter): see the header comment.
@@ -239,6 +245,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
 #ifdef MZ_STAMPS
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long st_last = __builtin_amdgcn_s_memtime();
+    unsigned long long w_acc[3] = {0, 0, 0};
 #endif
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int A = P.A, S = P.S, H = P.H;
@@ -416,6 +423,10 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
         if (tid < 64) {
             // ---- value / reward read-out activations, then backpropagate! (:190-217)
             if (active) {
+                // the backup's loads first (two players): in flight under the read-outs
+                const int tl = sg_vtp[g];
+                const int depth = sg_depth[g];
+                const BackupPre bpre = backup_preload(tree, path, depth, a);
                 // one activation per lane (even lanes the value, odd the reward, both
                 // f64 tanh chains run at once), then each quad's lanes 0 / 1 to all
                 // four by DPP quad_perm [0,0,0,0] / [1,1,1,1]
@@ -436,8 +447,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
                 if (threadIdx.x == 0) asm volatile("" :: "v"(val), "v"(rew));
 #endif
                 SM_STAMP(5);                    // stamp build: slot 5 = the read-out activations
-                const int tl = sg_vtp[g];
-                const int depth = sg_depth[g];
+                W_STAMP0();
                 if (a == 0) {
                     const int li = sg_leaf_e[g] * A + sg_leaf_a[g];
                     tree.nc(li) = (tree.nc(li) & 0xffffu) | ((uint32_t)(e_new + 1) << 16);
@@ -449,8 +459,12 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
                 int rN = sg_rootN[g];
                 float rW = sg_rootW[g], mmin = sg_mmin[g], mmax = sg_mmax[g];
                 const uint32_t omin = __float_as_uint(mmin), omax = __float_as_uint(mmax);
-                backup_path(tree, path, depth, val, tl, A, P.players, P.discount, rN, rW, sg_root_tp[g], mmin,
-                            mmax, a, c_lvl + g * (S + 2), c_nN + g * NN);
+                if (P.players == 2)
+                    backup_path_pre(tree, path, bpre, depth, val, rew, e_new, tl, P.discount, rN, rW, sg_root_tp[g],
+                                    mmin, mmax, a, c_lvl + g * (S + 2), c_nN + g * NN);
+                else
+                    backup_path(tree, path, depth, val, tl, A, P.players, P.discount, rN, rW, sg_root_tp[g], mmin,
+                                mmax, a, c_lvl + g * (S + 2), c_nN + g * NN);
                 const bool moved = __float_as_uint(mmin) != omin || __float_as_uint(mmax) != omax;
                 ver += moved ? 1 : 0;                     // min / max moved: every entry is stale
                 if (a == 0) {
@@ -459,8 +473,10 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
                     c_mmx[g] = make_float2(mmin, mmax);
                     c_skip[g] = moved ? 0 : depth;            // lowered by the recompute's path rows
                 }
+                W_STAMP(0);
             }
         } else if (tid >= 128 && tid < 128 + 16 * T) {
+            W_STAMP0();
             // ---- expand slot s+1 (:280): wave 2 lanes 16 g2 + a2 (g2, a2 as wave 0's g, a)
             const int g2 = (tid - 128) >> 4;
             const bool active2 = tile0 + g2 < P.G;
@@ -475,7 +491,9 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
                                                      sg_stage + 16 * g2);
 #endif
             if (active2) init_edges(tree2, e_new, a, A, prior);
+            W_STAMP(1);
         } else if (tid >= 192) {
+            W_STAMP0();
             for (int i = tid - 192; i < T * H; i += SM_THREADS - 192) {   // store h'; parent h *= 2 (Q1)
                 const int gl = i / H, k = i - gl * H;
                 hid[((size_t)gl * NN + e_new) * H + k] = act[P.h_out + k * T + gl];
@@ -484,6 +502,7 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
                     *hp = *hp * 2.0f;
                 }
             }
+            W_STAMP(2);
         }
         __syncthreads();
         SM_STAMP(4);
@@ -549,6 +568,10 @@ __device__ __forceinline__ void small_body(const SmallParams& P) {
     SM_STAMP(6);
     if (threadIdx.x == 0 && P.stamps)
         for (int i = 0; i < 8; ++i) P.stamps[blockIdx.x * 8 + i] = st_acc[i];
+    if (P.stamps && (threadIdx.x == 0 || threadIdx.x == 128 || threadIdx.x == 192)) {
+        const int k = threadIdx.x == 0 ? 0 : threadIdx.x == 128 ? 1 : 2;
+        P.stamps[(gridDim.x + blockIdx.x) * 8 + k] = w_acc[k];
+    }
 #endif
 }
 

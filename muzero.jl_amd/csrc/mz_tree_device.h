@@ -703,6 +703,116 @@ __device__ __forceinline__ void backup_path(const TreeView& t, const int* path, 
     }
 }
 
+// The two-player backup of the small kernels with its loads issued early:
+// backup_preload reads lane d's path entries, edge record and the children's
+// reward / to_play for the first GW levels BEFORE the read-out activations
+// (the f64 tanh chains) and before the leaf's expansion writes (the child
+// link of the leaf edge, the new slot's reward / to_play, path[2·depth+1]);
+// backup_path_pre then patches exactly those values in registers (the new slot
+// e_new is referenced only by the leaf level: a fresh slot no older path entry
+// points to) and runs backup_path's arithmetic, in the same order, on them.
+// Same loads and stores as the caller's writes + backup_path, so the same bits;
+// the LDS round trips overlap the read-outs.  Deep paths (depth >= GW) run the
+// levels past the first block as backup_path does, after the writes.
+struct BackupPre {
+    int i, c, c1, c2, tpc, tp1;
+    float4 ed;
+    float Rc, R1, R2;
+};
+template <int GW = 16>
+__device__ __forceinline__ BackupPre backup_preload(const TreeView& t, const int* path, int depth, int a) {
+    BackupPre b;
+    const int d = a < GW ? a : 0;
+    b.i = d > 0 && d <= depth ? path[2 * d] : 0;
+    b.c = d > 0 && d < depth ? path[2 * d + 1] : 0;
+    b.c1 = d + 1 < depth ? path[2 * d + 3] : 0;
+    b.c2 = d + 2 < depth ? path[2 * d + 5] : 0;
+    b.ed = t.e[b.i];
+    b.Rc = t.nr[b.c]; b.tpc = t.ntp[b.c];
+    b.R1 = t.nr[b.c1]; b.tp1 = t.ntp[b.c1];
+    b.R2 = t.nr[b.c2];
+    return b;
+}
+template <int GW = 16>
+__device__ __forceinline__ void backup_path_pre(const TreeView& t, const int* path, BackupPre b, int depth, float value,
+                                                float rew, int e_new, int tl, float discount, int& root_N,
+                                                float& root_W, int root_tp, float& mmin, float& mmax, int a,
+                                                uint2* lvl, int* nN) {
+    float lmin = INFINITY, lmax = -INFINITY;
+    int rN = root_N; float rW = root_W;
+    {
+        const int d = a;
+        if (d <= depth && d < GW) {
+            // the leaf's expansion, as the caller has just written it
+            if (d == depth && d > 0) {
+                b.c = e_new; b.Rc = rew; b.tpc = tl;
+                b.ed.x = __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, b.ed.x) & 0xffffu) |
+                                                   ((uint32_t)(e_new + 1) << 16));
+            }
+            if (d + 1 == depth) { b.c1 = e_new; b.R1 = rew; b.tp1 = tl; }
+            if (d + 2 == depth) { b.c2 = e_new; b.R2 = rew; }
+            uint32_t nc = __builtin_bit_cast(uint32_t, b.ed.x);
+            int N; float W, R; int tp;
+            if (d > 0) { N = (int)(nc & 0xffffu); W = b.ed.y; R = b.Rc; tp = b.tpc; }
+            else { N = root_N; W = root_W; R = 0.0f; tp = root_tp; }
+            float vin;
+            if (d == depth) vin = value;
+            else if (b.tp1 == tl) vin = -b.R1;
+            else vin = b.R1 + discount * (-b.R2);
+            W = tp == tl ? W + vin : W - vin;
+            N += 1;
+            const float q = W / (float)N;
+            const float upd = R + discount * q;
+            lmin = lmin < upd ? lmin : upd;
+            lmax = lmax > upd ? lmax : upd;
+            if (d > 0) {
+                nc = (nc & 0xffff0000u) | (uint32_t)N;
+                t.nc(b.i) = nc; t.w(b.i) = W; t.ev(b.i) = R + discount * (-q);
+            } else { rN = N; rW = W; }
+            lvl[d] = make_uint2((uint32_t)b.c, (uint32_t)N); nN[b.c] = N;
+        }
+    }
+    for (int base = GW; base <= depth; base += GW) {        // deep paths: backup_path's loop
+        const int d = base + a;
+        if (d <= depth) {
+            const int i = path[2 * d];
+            const int c = path[2 * d + 1];
+            const int c1 = d + 1 <= depth ? path[2 * d + 3] : 0;
+            const int c2 = d + 2 <= depth ? path[2 * d + 5] : 0;
+            const float4 ed = t.e[i];
+            const float Rc = t.nr[c];
+            const int tpc = t.ntp[c];
+            const float R1 = t.nr[c1], R2 = t.nr[c2];
+            const int tp1 = t.ntp[c1];
+            uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
+            int N = (int)(nc & 0xffffu); float W = ed.y;
+            float vin;
+            if (d == depth) vin = value;
+            else if (tp1 == tl) vin = -R1;
+            else vin = R1 + discount * (-R2);
+            W = tpc == tl ? W + vin : W - vin;
+            N += 1;
+            const float q = W / (float)N;
+            const float upd = Rc + discount * q;
+            lmin = lmin < upd ? lmin : upd;
+            lmax = lmax > upd ? lmax : upd;
+            nc = (nc & 0xffff0000u) | (uint32_t)N;
+            t.nc(i) = nc; t.w(i) = W; t.ev(i) = Rc + discount * (-q);
+            lvl[d] = make_uint2((uint32_t)c, (uint32_t)N); nN[c] = N;
+        }
+    }
+    lmin = gmin<GW>(lmin);
+    lmax = gmax<GW>(lmax);
+    mmin = mmin < lmin ? mmin : lmin;
+    mmax = mmax > lmax ? mmax : lmax;
+    if constexpr (GW == 16) {
+        root_N = __builtin_amdgcn_update_dpp(0, rN, 0x150, 0xF, 0xF, false);
+        root_W = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, rW), 0x150, 0xF, 0xF, false));
+    } else {
+        root_N = __shfl(rN, 0, GW); root_W = __shfl(rW, 0, GW);
+    }
+}
+
 // backpropagate! (SelfPlay.jl:190-217) for 1-player games, lane-parallel.
 // Without to_play resets the incoming value is the linear chain v_in(depth)
 // = leaf value, v_in(d-1) = R_d + γ·v_in(d), which the sequential loop

@@ -42,8 +42,16 @@ def main():
         eng.mcts_search(obs, legal, tp, rng_step=k)
     out = np.zeros((G, 8), np.uint64)
     assert L.mz_debug_stamps(eng.h, out.ctypes.data_as(ctypes.c_void_p), G) == 0
+    var = eng.search_variant()
+    nb = -(-G // int(var.split("small")[1][0])) if "small" in var else G
+    wv = out[nb:2 * nb].astype(np.float64) if 2 * nb <= G else None   # per-wave post-network phase (small*)
+    out = out[:nb]
     out = out[out.sum(1) > 0]
-    print("variant", eng.search_variant(), "blocks", len(out))
+    print("variant", var, "blocks", len(out))
+    if wv is not None and wv.sum() > 0:
+        med = np.median(wv, axis=0)
+        print(f"  post-network phase per wave, per sim: wave 0 backup {med[0] / S:.0f}, wave 2 expand "
+              f"{med[1] / S:.0f}, wave 3 h' store {med[2] / S:.0f} (ticks)")
     levels = out[:, 7].astype(np.float64)
     out[:, 7] = 0
     tot = out.sum(1).astype(np.float64)
