@@ -140,16 +140,35 @@ MZ_HD double det_log(double x) {
 
 MZ_HD float det_logf(float x) { return (float)det_log((double)x); }
 
-/* tanh via f64: (e^{2|x|} − 1)/(e^{2|x|} + 1), sign restored. */
+/* tanh in f32 (round 6; rounds 1-5 evaluated (e^{2|x|} − 1)/(e^{2|x|} + 1) in
+ * f64, ~1 k cycles of dependent f64 work on the search's read-out path):
+ *   |x| < 2^-12          x (tanh(x) rounds to x);
+ *   |x| < 0.55           x + x³·P(x²), P of degree 4 fitted to the relative
+ *                        error of tanh on [0, 0.55] (tools/fit_tanhf.py), Horner;
+ *   |x| < 9.5            (1 − e)/(1 + e), e = det_expf(−2|x|) (no cancellation:
+ *                        e ≤ e^{-1.1});
+ *   else                 ±1.
+ * Exhaustive over every f32 in [2^-12, 9.5] (tools/fit_tanhf.py): 0 ulp for
+ * 87 %, 1 ulp for 13 %, 2 ulp for 3 inputs against tanh in f64 rounded to f32. */
 MZ_HD float det_tanhf(float xf) {
     if (xf != xf) return xf;
-    float axf = fabsf(xf);
-    if (axf < 0.000244140625f) return xf;           /* |x| < 2^-12: tanh(x) rounds to x */
-    if (axf > 9.5f) return xf > 0.0f ? 1.0f : -1.0f;
-    double e = det_exp(2.0 * (double)axf);
-    double t = (e - 1.0) / (e + 1.0);
-    float tf = (float)t;
-    return xf > 0.0f ? tf : -tf;
+    float ax = fabsf(xf), r;
+    if (ax < 0.000244140625f) return xf;
+    if (ax < 0.55f) {
+        float s = ax * ax;
+        float p = -0.006275205872952938f;
+        p = fmaf(p, s, 0.021072300150990486f);
+        p = fmaf(p, s, -0.053852442651987076f);
+        p = fmaf(p, s, 0.13332587480545044f);
+        p = fmaf(p, s, -0.33333316445350647f);
+        r = fmaf(ax * s, p, ax);
+    } else if (ax < 9.5f) {
+        float e = det_expf(-2.0f * ax);
+        r = (1.0f - e) / (1.0f + e);
+    } else {
+        r = 1.0f;
+    }
+    return xf < 0.0f ? -r : r;
 }
 
 /* Flux relu = max(0, x) (Julia max: +0 for ±0 input) */

@@ -23,7 +23,7 @@ pmc() {  # tag, bench args, kernels...
 B1="--steps 10 --warmup 2 --no-cpu --pipeline-moves 0 --train-moves 0 --learner-steps 50"
 if [ -z "$SKIP_DEFAULT" ]; then
 run kt_default 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_default -o run -- python bench.py
-pmc default "$B1" mz_search_small2 mz_learn_small1 mz_bp_tile_lv mz_bp_dw mz_bp_fold
+pmc default "$B1" mz_search_small2 mz_learn_small1 mz_learn_multi2 mz_learn_chain mz_bp_tile_lv mz_bp_dw mz_bp_fold
 fi
 if [ -z "$SKIP_RESNET" ]; then
 BR="--net resnet --steps 4 --warmup 1 --no-cpu --pipeline-moves 0 --train-moves 0 --learner-steps 10"
