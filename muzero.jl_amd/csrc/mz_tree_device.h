@@ -416,12 +416,22 @@ __device__ __forceinline__ int mz_vsel(uint64_t m, int if_set, int if_clear) {
     return r;
 }
 
+// diagnostic (same results): MZ_DIAG_DIV_TWICE computes the pUCT normalisation and the backup's
+// W / N quotients twice — are those divisions on the critical path?
+__device__ __forceinline__ float mz_div_diag(float x, float y) {
+#ifdef MZ_DIAG_DIV_TWICE
+    float q0 = x / y;
+    asm volatile("" : "+v"(x) : "v"(q0));
+#endif
+    return x / y;
+}
+
 __device__ __forceinline__ float pucb_score(const float4& ed, const double* prow, int Np, bool lg, bool norm,
                                             float mmin, float den) {
     const uint32_t nc = __builtin_bit_cast(uint32_t, ed.x);
     const int Nc = (int)(nc & 0xffffu);
     const double pb_c = prow[Nc < Np ? Nc : Np];
-    const float vn = (ed.w - mmin) / den;
+    const float vn = mz_div_diag(ed.w - mmin, den);
     const float vs = Nc > 0 ? (norm ? vn : ed.w) : 0.0f;
     const double prior_score = pb_c * (double)ed.z;
     const float us = (float)(prior_score + (double)vs);
@@ -761,7 +771,7 @@ __device__ __forceinline__ void backup_path_pre(const TreeView& t, const int* pa
             else vin = b.R1 + discount * (-b.R2);
             W = tp == tl ? W + vin : W - vin;
             N += 1;
-            const float q = W / (float)N;
+            const float q = mz_div_diag(W, (float)N);
             const float upd = R + discount * q;
             lmin = lmin < upd ? lmin : upd;
             lmax = lmax > upd ? lmax : upd;
