@@ -890,9 +890,14 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learn_chain(ChainPar
     if (C.cap_i[0] < 0 && C.cap_i[1] < 0) chain_slice<false>(C, net, sb, red, sbp);
     else chain_slice<true>(C, net, sb, red, sbp);             // (mz_train_run's refresh steps in this chain)
     __syncthreads();
-    for (int o = MZ_THREADS / 2; o > 0; o >>= 1) {   // lg_tree256, per step
-        if (tid < o)
-            for (int i = 0; i < L; ++i) red[i][tid] += red[i][tid + o];
+    // lg_tree256 per step: level o adds red[i][j + o] into red[i][j] for j < o, every step i; the o·L
+    // adds of a level are spread over all 256 threads (each the same add as the per-step tree's, so
+    // the same bits), not L in sequence on the first o threads
+    for (int o = MZ_THREADS / 2; o > 0; o >>= 1) {
+        for (int x = tid; x < o * L; x += MZ_THREADS) {
+            const int i = x / o, j = x - i * o;
+            red[i][j] += red[i][j + o];
+        }
         __syncthreads();
     }
     if (tid < L) C.part[(size_t)tid * NSL + blk] = red[tid][0];
