@@ -91,6 +91,8 @@ extern "C" __global__ void mz_learn_chain(ChainParams C);
 extern "C" __global__ void mz_learn_multi1(SmallUnrollParams P, LearnMultiParams M);
 extern "C" __global__ void mz_learn_multi2(SmallUnrollParams P, LearnMultiParams M);
 extern "C" __global__ void mz_learn_multi1_bn(SmallUnrollParams P, LearnMultiParams M);
+extern "C" __global__ void mz_learn_multi4(SmallUnrollParams P, LearnMultiParams M);
+extern "C" __global__ void mz_learn_multi4_bn(SmallUnrollParams P, LearnMultiParams M);
 extern "C" __global__ void mz_learn_multi2_bn(SmallUnrollParams P, LearnMultiParams M);
 extern "C" __global__ void mz_learner_loss_multi(LossMultiParams M);
 extern "C" __global__ void mz_learner_loss_multi32(LossMultiParams M);
@@ -1679,6 +1681,11 @@ int mz_engine_create(const mz_config* conf, const mz_ffhp* hyper, int device, in
             CK(hipFuncSetAttribute(kl[ti], hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)unroll_small_lds(h, ti & 1)) == hipSuccess
                    ? 0 : fail(h, "hipFuncSetAttribute(learn_small)"));
+        const void* k4[2] = {(const void*)mz_learn_multi4, (const void*)mz_learn_multi4_bn};
+        for (int j = 0; j < 2; ++j)
+            CK(hipFuncSetAttribute(k4[j], hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)unroll_small_lds(h, 2)) == hipSuccess
+                   ? 0 : fail(h, "hipFuncSetAttribute(learn_multi4)"));
     }
     CK(hipMemset(h->d_flat, 0, h->nflat * 4) == hipSuccess ? 0 : fail(h, "memset"));
     CK(repack(h));
@@ -3675,13 +3682,20 @@ static int multi_plan(const mz_handle* h, int B, int L, int* Ls) {
     static const int force = std::getenv("MZ_MULTI_T") ? std::atoi(std::getenv("MZ_MULTI_T")) : 0;   // tests / A/B
     static const int ls_env = std::getenv("MZ_MULTI_LS") ? std::atoi(std::getenv("MZ_MULTI_LS")) : 0;
     int ti;
-    if ((force == 1 || force == 2) && small_unroll_fits(h, force - 1)) ti = force - 1;
-    else if ((size_t)L * B <= (size_t)h->n_cu && small_unroll_fits(h, 0)) ti = 0;
+    // T = 4 (round 6) when the call has the steps to fill the chip with 4 samples per workgroup
+    // (twice the steps per unroll launch as T = 2 for about 1.1x a stage's cost); T = 2 when L·B
+    // exceeds the CUs; T = 1 below
+    const int nU4 = (B + 3) / 4;
+    if ((force == 1 || force == 2 || force == 4) && small_unroll_fits(h, force == 4 ? 2 : force - 1))
+        ti = force == 4 ? 2 : force - 1;
+    else if (!force && (size_t)L * B <= (size_t)h->n_cu && small_unroll_fits(h, 0)) ti = 0;
+    else if (!force && L >= std::min(MZ_MULTI_MAX, h->n_cu / nU4) && (size_t)L * nU4 >= (size_t)h->n_cu &&
+             small_unroll_fits(h, 2) && !std::getenv("MZ_MULTI_NO_T4")) ti = 2;
     else if (small_unroll_fits(h, 1)) ti = 1;
     else if (small_unroll_fits(h, 0)) ti = 0;
     else return -1;
-    const int nU = (B + ti) / (ti + 1);
-    int ls = std::max(1, std::min(MZ_MULTI_UNROLL, h->n_cu / nU));
+    const int T = ti == 2 ? 4 : ti + 1, nU = (B + T - 1) / T;
+    int ls = std::max(1, std::min(ti == 2 ? MZ_MULTI_MAX : MZ_MULTI_UNROLL, h->n_cu / nU));
     if (ls_env > 0) ls = std::min(MZ_MULTI_MAX, ls_env);          // (A/B: more than one workgroup per CU)
     *Ls = std::min(ls, L);
     return ti;
@@ -3959,7 +3973,7 @@ static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, con
     static const bool chain_sample = std::getenv("MZ_MULTI_CHAIN_SAMPLE") != nullptr;   // A/B
     SmallUnrollParams U;
     if (small_unroll_params(h, &b, ti, nullptr, &U)) return -1;
-    const int T = ti + 1, nU = (B + T - 1) / T;
+    const int T = ti == 2 ? 4 : ti + 1, nU = (B + T - 1) / T;
     static const bool no_xcd = std::getenv("MZ_MULTI_NO_XCD") != nullptr;
     double p1 = h->bp1, p2 = h->bp2;
     // chain launches of up to MZ_MULTI_MAX steps (bank half k mod 2), each followed by its steps' unroll
@@ -4022,13 +4036,17 @@ static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, con
                 if (timing_events(h, &e0, &e1)) return -1;
                 MZ_TRY(h, hipEventRecord(e0, st));
             }
-            MZ_TRY(h, hipLaunchKernel(h->sm_bn ? (ti == 0 ? (const void*)mz_learn_multi1_bn : (const void*)mz_learn_multi2_bn)
-                                               : (ti == 0 ? (const void*)mz_learn_multi1 : (const void*)mz_learn_multi2),
+            const void* kbn[3] = {(const void*)mz_learn_multi1_bn, (const void*)mz_learn_multi2_bn,
+                                  (const void*)mz_learn_multi4_bn};
+            const void* kpl[3] = {(const void*)mz_learn_multi1, (const void*)mz_learn_multi2,
+                                  (const void*)mz_learn_multi4};
+            MZ_TRY(h, hipLaunchKernel(h->sm_bn ? kbn[ti] : kpl[ti],
                                       dim3(grid), dim3(SM_THREADS), args, unroll_small_lds(h, ti), st));
             if (e1) MZ_TRY(h, hipEventRecord(e1, st));
         }
     }
-    h->last_lvariant = ti == 0 ? "mz_learn_chain+mz_learn_multi1" : "mz_learn_chain+mz_learn_multi2";
+    h->last_lvariant = ti == 0 ? "mz_learn_chain+mz_learn_multi1"
+                     : ti == 1 ? "mz_learn_chain+mz_learn_multi2" : "mz_learn_chain+mz_learn_multi4";
     for (int i = 0; i < L; ++i) adam_advance(h);
     h->ml_last_B = B; h->ml_last_L = L; h->ml_last_R = R;
     return 0;

@@ -959,6 +959,12 @@ extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_multi1(Smal
 extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_multi2(SmallUnrollParams P, LearnMultiParams M) {
     learn_multi_body<2, 0>(P, M);
 }
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_multi4(SmallUnrollParams P, LearnMultiParams M) {
+    learn_multi_body<4, 0>(P, M);
+}
+extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_multi4_bn(SmallUnrollParams P, LearnMultiParams M) {
+    learn_multi_body<4, 1>(P, M);
+}
 extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_multi1_bn(SmallUnrollParams P, LearnMultiParams M) {
     learn_multi_body<1, 1>(P, M);
 }
