@@ -194,6 +194,9 @@ struct mz_handle {
     float* d_rtrunk = nullptr;              // [max_games][H] dynamics trunk outputs (mz_rsearch_nets rew_split)
     unsigned long long* d_tprog = nullptr;  // [tiles] their publish words
     unsigned long long tprog_epoch = 0;     // mz_rsearch_nets launches
+    float* d_chx = nullptr;                 // [MZ_MULTI_MAX][hx_n] mz_learn_chain helpers' θ (ChainParams::hx)
+    unsigned long long* d_chprog = nullptr; // [helpers] their publish words
+    unsigned long long chain_epoch = 0;     // mz_learn_chain launches with helpers
     unsigned long long prog_epoch = 0;      // launches of mz_runroll_fused_r (prog_base = epoch · 64)
     std::vector<int> rtab;                  // offset tables of the narrow (chain) plans
     int* d_rtab = nullptr;
@@ -402,6 +405,7 @@ static int check_fault(mz_handle* h) {
     std::string m = std::string("device fault: a workgroup waited ") + wait + " for a publish that never came (";
     if (v & MZ_FAULT_RS_TRUNK) m += "mz_rsearch_nets trunk hand-off ";
     if (v & MZ_FAULT_RD_PROGRESS) m += "mz_runroll_fused_r chain progress ";
+    if (v & MZ_FAULT_CHAIN_HELPER) m += "mz_learn_chain helper theta ";
     h->err = m + "); the results of the launches since the last synchronisation are invalid (search results, "
                  "games self-play stored from them, losses, read-outs; the ref_semantics weights and ADAM state "
                  "do not read them and stay valid)";
@@ -3783,6 +3787,35 @@ struct MultiCap {
     int64_t t[2];                                   // absolute learner steps (< 0: none)
     float* dst[2];                                  // nflat floats each
 };
+// mz_learn_chain's helper workgroups (ChainParams::nh) for the nets with more parameters than one pass
+// of the slices (MZ_CHAIN_HELP=0: off, A/B).  Measured (tools/gpu_r06t.sh): FC 32.1 -> 24.8 us per
+// 32-step chain, ResNet configs[2] 63.3 -> 44.2 us.  Returns the helper count.
+static int chain_helpers(mz_handle* h, ChainParams& C) {
+    static const char* env = std::getenv("MZ_CHAIN_HELP");
+    const size_t stride = (size_t)MZ_L2_BLOCKS * MZ_THREADS;
+    int nht = 0;
+    size_t hx_n = 0;
+    for (int n = 0; n < 3; ++n) {
+        const size_t c = h->nparams[n];
+        C.nh[n] = c > stride ? (int)((c - stride + MZ_THREADS - 1) / MZ_THREADS) : 0;
+        C.hoff[n] = hx_n;
+        hx_n += c > stride ? c - stride : 0;
+        nht += C.nh[n];
+    }
+    const bool on = nht > 0 && (!env || std::atoi(env) != 0);
+    if (!on) {
+        C.nh[0] = C.nh[1] = C.nh[2] = 0;
+        return 0;
+    }
+    if (!h->d_chprog) {
+        MZ_TRY(h, dalloc(h, &h->d_chx, (size_t)MZ_MULTI_MAX * hx_n));
+        MZ_TRY(h, dalloc(h, &h->d_chprog, (size_t)nht));
+        MZ_TRY(h, hipMemset(h->d_chprog, 0, (size_t)nht * sizeof(unsigned long long)));
+    }
+    C.hx = h->d_chx; C.hx_n = hx_n; C.hprog = h->d_chprog; C.epoch = ++h->chain_epoch;
+    C.poll_ticks = h->poll_ticks; C.fault = h->d_fault;
+    return nht;
+}
 static void set_caps(ChainParams& C, const MultiCap* cap, int64_t first, int nc) {
     for (int j = 0; j < 2; ++j) {
         const bool in = cap && cap->t[j] >= first && cap->t[j] < first + nc;
@@ -3854,7 +3887,9 @@ static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, co
         Qc.tpol += cr * s_tp; Qc.gscale += (size_t)cr * B; Qc.index += (size_t)cr * 2 * B;
         C.B = B; C.q = Qc; C.s_obs = s_obs; C.s_k1 = s_k1; C.s_tp = s_tp;
         const int nsb = (nc * B + MZ_THREADS / 64 - 1) / (MZ_THREADS / 64);
-        hipLaunchKernelGGL(mz_learn_chain, dim3(3 * MZ_L2_BLOCKS + nsb), dim3(MZ_THREADS), 0, st, C);
+        const int nht = chain_helpers(h, C);
+        if (nht < 0) return -1;
+        hipLaunchKernelGGL(mz_learn_chain, dim3(nht + 3 * MZ_L2_BLOCKS + nsb), dim3(MZ_THREADS), 0, st, C);
         MZ_TRY(h, hipGetLastError());
         for (int j0 = 0; j0 < nc; j0 += Ls) {
             const int n = std::min(Ls, nc - j0), i0 = c0 + j0, ir = i0 % R;
@@ -4004,7 +4039,9 @@ static int learner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, con
         Qc.tpol += cr * s_tp; Qc.gscale += (size_t)cr * B; Qc.index += (size_t)cr * 2 * B;
         C.B = B; C.q = Qc; C.s_obs = s_obs; C.s_k1 = s_k1; C.s_tp = s_tp;
         const int nsb = chain_sample ? (nc * B + MZ_THREADS / 64 - 1) / (MZ_THREADS / 64) : 0;
-        hipLaunchKernelGGL(mz_learn_chain, dim3(3 * MZ_L2_BLOCKS + nsb), dim3(MZ_THREADS), 0, st, C);
+        const int nht = chain_helpers(h, C);
+        if (nht < 0) return -1;
+        hipLaunchKernelGGL(mz_learn_chain, dim3(nht + 3 * MZ_L2_BLOCKS + nsb), dim3(MZ_THREADS), 0, st, C);
         MZ_TRY(h, hipGetLastError());
         for (int j0 = 0; j0 < nc; j0 += Ls) {
             const int n = std::min(Ls, nc - j0), i0 = c0 + j0, ir = i0 % R;

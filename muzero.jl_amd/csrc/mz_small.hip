@@ -823,54 +823,72 @@ extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_small2_bn(S
 
 // ------------------------------------------------ L learner steps per launch pair
 // (ChainParams / LearnMultiParams, mz_small_params.h)
-// mz_learn_chain: blocks [0, 3·MZ_L2_BLOCKS) are lg_l2_slice's slices (net, blk):
-// each thread runs its parameters' L ADAM iterations (∇ = 2θ, Q11) in registers
-// and keeps one Σθ_{t+i}² per step in lg_l2_slice's order; the per-step trees
-// are lg_tree256's, level by level.  The blocks after them draw the L batches.
-// The chain and the unroll launches run one after another in stream order
-// (a two-stream variant that overlapped them measured slower, mz_engine.hip
-// learner_multi), so the chain's 66 KB of static LDS never shares a CU with
-// an unroll workgroup.
-// this thread's parameters of slice (net, sb): L ADAM iterations in registers; CAP: θ after steps
+// one parameter p's L ADAM iterations in registers; its θ_{t+i} feed step t+i's Σθ² (the slice: added to
+// rd[i·MZ_THREADS] in place; a helper: stored to hx[i·hx_n] for the owning slice); CAP: θ after steps
 // cap_i[0] / cap_i[1] also copied out (a separate instance: the plain chain carries no per-step tests)
+template <bool CAP, bool HELP>
+__device__ __forceinline__ void chain_param(const ChainParams& C, size_t p, double* rd, float* hx,
+                                            const double (*sbp)[MZ_MULTI_MAX]) {
+    const int L = C.L;
+    float x = C.flat[p], m = C.M[p], v = C.V[p];
+    const int it = C.inv_tile[p], is = C.inv_small[p];
+    const bool sbank = C.bank_w != nullptr, tbank = C.tbank_w != nullptr;   // (uniform)
+    for (int i = 0; i < L; ++i) {
+        if constexpr (HELP) __hip_atomic_store(hx + (size_t)i * C.hx_n, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else rd[i * MZ_THREADS] += (double)x * (double)x;           // step t+i's Σθ² reads θ_{t+i}
+#ifndef MZ_DBG_NO_BANK   // diagnostic only (wrong results): the chain without the bank scatter
+        if (sbank) mz_scatter(x, is, C.bank_w + i * C.bws, C.bank_b + i * C.bbs);
+#endif
+        if (tbank) mz_scatter(x, it, C.tbank_w + i * C.tws, C.tbank_b + i * C.tbs);
+        if (C.fbank) C.fbank[i * C.fstride + p] = x;
+        x = adam_2theta(x, m, v, sbp[0][i], sbp[1][i], sbp[2][i]);   // Learning.jl:395-397
+        if (C.theta) C.theta[i * C.nflat + p] = x;
+        if constexpr (CAP) {
+            if (i == C.cap_i[0]) C.cap_dst[0][p] = x;
+            if (i == C.cap_i[1]) C.cap_dst[1][p] = x;
+        }
+    }
+    C.flat[p] = x; C.M[p] = m; C.V[p] = v;
+    mz_scatter(x, it, C.Wp, C.Bp);
+    mz_scatter(x, is, C.smw, C.smb);
+}
+
+// this thread's parameters of slice (net, sb): e = sb·256 + tid + k·stride in k order (with helpers
+// for the net: k = 0 only)
 template <bool CAP>
 __device__ __forceinline__ void chain_slice(const ChainParams& C, int net, int sb, double (*red)[MZ_THREADS],
                                             double (*sbp)[MZ_MULTI_MAX]) {
-    const int tid = threadIdx.x, L = C.L;
+    const int tid = threadIdx.x;
     const size_t off = C.netoff[net], cnt = C.netoff[3 + net];
     const size_t stride = (size_t)MZ_L2_BLOCKS * MZ_THREADS;
     for (size_t e = (size_t)sb * MZ_THREADS + tid; e < cnt; e += stride) {
-        const size_t p = off + e;
-        float x = C.flat[p], m = C.M[p], v = C.V[p];
-        const int it = C.inv_tile[p], is = C.inv_small[p];
-        const bool sbank = C.bank_w != nullptr, tbank = C.tbank_w != nullptr;   // (uniform)
-        for (int i = 0; i < L; ++i) {
-            red[i][tid] += (double)x * (double)x;                   // step t+i's Σθ² reads θ_{t+i}
-#ifndef MZ_DBG_NO_BANK   // diagnostic only (wrong results): the chain without the bank scatter
-            if (sbank) mz_scatter(x, is, C.bank_w + i * C.bws, C.bank_b + i * C.bbs);
+        chain_param<CAP, false>(C, off + e, &red[0][tid], nullptr, sbp);
+#ifdef MZ_DBG_ONE_ELEM   // diagnostic only (wrong results): each thread's first parameter alone
+        break;
 #endif
-            if (tbank) mz_scatter(x, it, C.tbank_w + i * C.tws, C.tbank_b + i * C.tbs);
-            if (C.fbank) C.fbank[i * C.fstride + p] = x;
-            x = adam_2theta(x, m, v, sbp[0][i], sbp[1][i], sbp[2][i]);   // Learning.jl:395-397
-            if (C.theta) C.theta[i * C.nflat + p] = x;
-            if constexpr (CAP) {
-                if (i == C.cap_i[0]) C.cap_dst[0][p] = x;
-                if (i == C.cap_i[1]) C.cap_dst[1][p] = x;
-            }
-        }
-        C.flat[p] = x; C.M[p] = m; C.V[p] = v;
-        mz_scatter(x, it, C.Wp, C.Bp);
-        mz_scatter(x, is, C.smw, C.smb);
+        if (C.nh[net]) break;
     }
 }
 
+// mz_learn_chain: blocks [0, nh) are the helpers (ChainParams::nh), then
+// [nh, nh + 3·MZ_L2_BLOCKS) lg_l2_slice's slices (net, blk): each thread runs its
+// parameters' L ADAM iterations (∇ = 2θ, Q11) in registers and keeps one
+// Σθ_{t+i}² per step in lg_l2_slice's order; the per-step trees are
+// lg_tree256's, level by level.  The blocks after them draw the L batches.
+// Helpers come first in dispatch order and wait on nothing, so every helper is
+// resident before a slice waits on it (the wait is bounded all the same).
+// The chain and the unroll launches run one after another in stream order
+// (a two-stream variant that overlapped them measured slower, mz_engine.hip
+// learner_multi).
 extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learn_chain(ChainParams C) {
     // per step i: this thread's Σθ_{t+i}² (accumulated in place in LDS: no
     // register array indexed by the runtime step)
     __shared__ double red[MZ_MULTI_MAX][MZ_THREADS];
     __shared__ double sbp[3][MZ_MULTI_MAX];         // β1^t, β2^t, η of step t+i
-    const int tid = threadIdx.x, blk = (int)blockIdx.x;
+    const int tid = threadIdx.x, nht = C.nh[0] + C.nh[1] + C.nh[2];
+    int blk = (int)blockIdx.x - nht;
     constexpr int NSL = 3 * MZ_L2_BLOCKS;
+    const size_t stride = (size_t)MZ_L2_BLOCKS * MZ_THREADS;
     const int L = C.L;
     if (blk >= NSL) {                               // get_batch of step t+i, sample b (ReplayBuffer.jl:188-217)
         const int q = (blk - NSL) * (MZ_THREADS / 64) + (tid >> 6);
@@ -884,11 +902,49 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learn_chain(ChainPar
         return;
     }
     if (tid < MZ_MULTI_MAX) { sbp[0][tid] = C.bp1[tid]; sbp[1][tid] = C.bp2[tid]; sbp[2][tid] = C.eta[tid]; }
+    if (blk < 0) {                                  // helper hb of net n: parameter e = stride + hb·256 + tid
+        int hb = (int)blockIdx.x, n = 0;
+        while (hb >= C.nh[n]) hb -= C.nh[n++];
+        const size_t e1 = (size_t)hb * MZ_THREADS + tid, cnt = C.netoff[3 + n];
+        __syncthreads();
+        if (stride + e1 < cnt) {
+            if (C.cap_i[0] < 0 && C.cap_i[1] < 0)
+                chain_param<false, true>(C, C.netoff[n] + stride + e1, nullptr, C.hx + C.hoff[n] + e1, sbp);
+            else
+                chain_param<true, true>(C, C.netoff[n] + stride + e1, nullptr, C.hx + C.hoff[n] + e1, sbp);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");            // this wave's θ stores performed
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(C.hprog + blockIdx.x, C.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     for (int i = 0; i < L; ++i) red[i][tid] = 0.0;
     __syncthreads();
     const int net = blk / MZ_L2_BLOCKS, sb = blk - net * MZ_L2_BLOCKS;
     if (C.cap_i[0] < 0 && C.cap_i[1] < 0) chain_slice<false>(C, net, sb, red, sbp);
     else chain_slice<true>(C, net, sb, red, sbp);             // (mz_train_run's refresh steps in this chain)
+    if (C.nh[net]) {
+        // the helpers' parameters e = k·stride + sb·256 + tid, k >= 1, in k order: helper (k − 1)·128 + sb
+        // of the net (its block: the nets before it first)
+        const size_t cnt = C.netoff[3 + net], o = (size_t)sb * MZ_THREADS + tid;
+        const int hb0 = net == 0 ? 0 : net == 1 ? C.nh[0] : C.nh[0] + C.nh[1];
+        if (tid == 0)
+            for (int hb = sb; hb < C.nh[net]; hb += MZ_L2_BLOCKS)   // bounded: a publish that never comes is reported
+                mz_poll_ge(C.hprog + hb0 + hb, C.epoch, C.fault, MZ_FAULT_CHAIN_HELPER, C.poll_ticks);
+        __syncthreads();
+        // (the MZ_MULTI_MAX rows of hx are all allocated: the loads are issued together, sc1 like the stores)
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(C.hx, (short)0, (int)(MZ_MULTI_MAX * C.hx_n * 4), 0x00020000);
+        for (size_t e = o + stride; e < cnt; e += stride) {
+            const int b0 = (int)((C.hoff[net] + (e - stride)) * 4);
+            float xv[MZ_MULTI_MAX];
+#pragma unroll
+            for (int i = 0; i < MZ_MULTI_MAX; ++i)
+                xv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, b0 + (int)(i * C.hx_n * 4), 0, 16));
+#pragma unroll
+            for (int i = 0; i < MZ_MULTI_MAX; ++i)
+                if (i < L) red[i][tid] += (double)xv[i] * (double)xv[i];
+        }
+    }
     __syncthreads();
     // lg_tree256 per step: level o adds red[i][j + o] into red[i][j] for j < o, every step i; the o·L
     // adds of a level are spread over all 256 threads (each the same add as the per-step tree's, so

@@ -162,6 +162,17 @@ struct ChainParams {
     int B;                                             // batches: sample q = i·B + b, one wave each
     RpSampleParams q;                                  // step t's get_batch; step i's arrays at + i·stride
     size_t s_obs, s_k1, s_tp;                          // per-step strides: B·F, B·(K+1), B·(K+1)·A
+    // helper workgroups (blocks [0, nh[0] + nh[1] + nh[2]), dispatched before the slices): net n's
+    // parameters past the slices' first pass (e >= MZ_L2_BLOCKS·MZ_THREADS), one per thread, so no thread
+    // runs two parameters' chains in sequence; each stores its θ_{t+i} to hx[i·hx_n + hoff[n] + e − stride]
+    // (agent scope) and publishes hprog[helper] = epoch; the owning slice adds their squares after its own,
+    // in lg_l2_slice's order (nh[n] = 0: the slice runs them itself)
+    int nh[3];
+    size_t hoff[3], hx_n;
+    float* hx;
+    unsigned long long* hprog;
+    unsigned long long epoch, poll_ticks;
+    unsigned* fault;                                   // MZ_FAULT_CHAIN_HELPER on a publish that never came
 };
 struct LearnMultiParams {
     int L, nU, xcd;                                    // xcd: step i on XCD i mod 8 (learn_multi_body)
