@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <algorithm>
@@ -195,7 +196,7 @@ struct mz_handle {
     unsigned long long* d_tprog = nullptr;  // [tiles] their publish words
     unsigned long long tprog_epoch = 0;     // mz_rsearch_nets launches
     float* d_chx = nullptr;                 // [MZ_MULTI_MAX][hx_n] mz_learn_chain helpers' θ (ChainParams::hx)
-    unsigned long long* d_chprog = nullptr; // [helpers] their publish words
+    unsigned long long* d_chcnt = nullptr;  // [3·MZ_L2_BLOCKS] their slots' arrival counters
     unsigned long long chain_epoch = 0;     // mz_learn_chain launches with helpers
     unsigned long long prog_epoch = 0;      // launches of mz_runroll_fused_r (prog_base = epoch · 64)
     std::vector<int> rtab;                  // offset tables of the narrow (chain) plans
@@ -335,6 +336,8 @@ struct mz_handle {
     int tr_B = 0;
     int64_t tr_t = 0, tr_games = 0, tr_refresh = 0;
     long long* h_tr_cnt = nullptr;          // pinned: num_played_games read back once per move
+    long long* h_tr_pub = nullptr;          // coherent pinned: mz_tr_publish's {count, fault, sequence}
+    long long tr_pub_seq = 0;
     // corrected-gradient learner (mz_backprop.hip): the unrolled graph and its arenas
     int learn_mode = MZ_LEARN_REF_SEMANTICS;
     bool bp_built = false;
@@ -405,7 +408,6 @@ static int check_fault(mz_handle* h) {
     std::string m = std::string("device fault: a workgroup waited ") + wait + " for a publish that never came (";
     if (v & MZ_FAULT_RS_TRUNK) m += "mz_rsearch_nets trunk hand-off ";
     if (v & MZ_FAULT_RD_PROGRESS) m += "mz_runroll_fused_r chain progress ";
-    if (v & MZ_FAULT_CHAIN_HELPER) m += "mz_learn_chain helper theta ";
     h->err = m + "); the results of the launches since the last synchronisation are invalid (search results, "
                  "games self-play stored from them, losses, read-outs; the ref_semantics weights and ADAM state "
                  "do not read them and stay valid)";
@@ -1602,6 +1604,7 @@ void mz_engine_destroy(mz_handle* h) {
     for (void* p : h->sp_allocs) (void)hipFree(p);
     if (h->d_dsb) (void)hipFree(h->d_dsb);
     if (h->h_tr_cnt) (void)hipHostFree(h->h_tr_cnt);
+    if (h->h_tr_pub) (void)hipHostFree(h->h_tr_pub);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     dp_destroy(h);
     delete h;
@@ -3786,6 +3789,8 @@ static int ensure_multi(mz_handle* h, int B, int L);
 struct MultiCap {
     int64_t t[2];                                   // absolute learner steps (< 0: none)
     float* dst[2];                                  // nflat floats each
+    const mz_handle::WSet* img0;                    // NULL or set 0's search images, written by the chain too
+    bool* imaged0;                                  // set when a chain launch wrote them
 };
 // mz_learn_chain's helper workgroups (ChainParams::nh) for the nets with more parameters than one pass
 // of the slices (MZ_CHAIN_HELP=0: off, A/B).  Measured (tools/gpu_r06t.sh): FC 32.1 -> 24.8 us per
@@ -3799,7 +3804,7 @@ static int chain_helpers(mz_handle* h, ChainParams& C) {
         const size_t c = h->nparams[n];
         C.nh[n] = c > stride ? (int)((c - stride + MZ_THREADS - 1) / MZ_THREADS) : 0;
         C.hoff[n] = hx_n;
-        hx_n += c > stride ? c - stride : 0;
+        hx_n += c > stride ? c : 0;
         nht += C.nh[n];
     }
     const bool on = nht > 0 && (!env || std::atoi(env) != 0);
@@ -3807,13 +3812,12 @@ static int chain_helpers(mz_handle* h, ChainParams& C) {
         C.nh[0] = C.nh[1] = C.nh[2] = 0;
         return 0;
     }
-    if (!h->d_chprog) {
+    if (!h->d_chcnt) {
         MZ_TRY(h, dalloc(h, &h->d_chx, (size_t)MZ_MULTI_MAX * hx_n));
-        MZ_TRY(h, dalloc(h, &h->d_chprog, (size_t)nht));
-        MZ_TRY(h, hipMemset(h->d_chprog, 0, (size_t)nht * sizeof(unsigned long long)));
+        MZ_TRY(h, dalloc(h, &h->d_chcnt, (size_t)3 * MZ_L2_BLOCKS));
+        MZ_TRY(h, hipMemset(h->d_chcnt, 0, (size_t)3 * MZ_L2_BLOCKS * sizeof(unsigned long long)));
     }
-    C.hx = h->d_chx; C.hx_n = hx_n; C.hprog = h->d_chprog; C.epoch = ++h->chain_epoch;
-    C.poll_ticks = h->poll_ticks; C.fault = h->d_fault;
+    C.hx = h->d_chx; C.hx_n = hx_n; C.hcnt = h->d_chcnt; C.epoch = ++h->chain_epoch;
     return nht;
 }
 static void set_caps(ChainParams& C, const MultiCap* cap, int64_t first, int nc) {
@@ -3821,6 +3825,11 @@ static void set_caps(ChainParams& C, const MultiCap* cap, int64_t first, int nc)
         const bool in = cap && cap->t[j] >= first && cap->t[j] < first + nc;
         C.cap_i[j] = in ? (int)(cap->t[j] - first) : -1;
         C.cap_dst[j] = in ? cap->dst[j] : nullptr;
+    }
+    if (C.cap_i[0] >= 0 && cap->img0) {
+        C.cap_img[0] = cap->img0->Wp; C.cap_img[1] = cap->img0->Bp;
+        C.cap_img[2] = cap->img0->smw; C.cap_img[3] = cap->img0->smb;
+        if (cap->imaged0) *cap->imaged0 = true;
     }
 }
 static int rlearner_multi(mz_handle* h, int32_t B, uint32_t step0, int32_t L, const double* eta, float* losses_dev,
@@ -4212,6 +4221,9 @@ int mz_train_init_at(mz_handle* h, int32_t B, int64_t t0) {
         if (h->small_ok) { MZ_TRY(h, dalloc(h, &w.smw, h->sm_w_n)); MZ_TRY(h, dalloc(h, &w.smb, h->sm_b_n)); }
         MZ_TRY(h, dalloc(h, &h->d_tr_queued, h->nflat));
         MZ_TRY(h, hipHostMalloc(reinterpret_cast<void**>(&h->h_tr_cnt), 4 * sizeof(long long)));
+        MZ_TRY(h, hipHostMalloc(reinterpret_cast<void**>(&h->h_tr_pub), 4 * sizeof(long long), hipHostMallocCoherent));
+        std::memset(h->h_tr_pub, 0, 4 * sizeof(long long));
+        h->tr_pub_seq = 0;
     }
     // actors and the queue start from the learner's current (initial) nets (main.jl:23)
     MZ_TRY(h, hipMemcpyAsync(w.flat, h->d_flat, h->nflat * 4, hipMemcpyDeviceToDevice, h->stream));
@@ -4224,6 +4236,32 @@ int mz_train_init_at(mz_handle* h, int32_t B, int64_t t0) {
     MZ_TRY(h, hipMemcpy(h->d_sp_tgame, tg.data(), tg.size() * 4, hipMemcpyHostToDevice));
     h->tr_B = B; h->tr_t = t0; h->tr_refresh = 0;
     h->tr_games = h->h_tr_cnt[0];
+    return 0;
+}
+
+// the move's hand-back to the host: the finished-game count and the fault word, then a sequence
+// number, stored into coherent pinned host memory at system scope; the host spins on the sequence
+// number instead of two copy launches and a stream synchronisation (measured in the trace: 30-60 us
+// from the copies' end to the next launch)
+extern "C" __global__ void mz_tr_publish(const long long* counters, const unsigned* fault, long long* host,
+                                         long long seq) {
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(host + 0, counters[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host + 1, fault ? (long long)*fault : 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+// wait for publish `seq` (bounded: after 60 s the stream is synchronised, which reports a launch error)
+static int tr_wait_publish(mz_handle* h, long long seq, hipStream_t st) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned n = 0; __atomic_load_n(h->h_tr_pub + 2, __ATOMIC_ACQUIRE) != seq; ++n) {
+        if ((n & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+            MZ_TRY(h, hipStreamSynchronize(st));
+            if (__atomic_load_n(h->h_tr_pub + 2, __ATOMIC_ACQUIRE) == seq) break;
+            return fail(h, "mz_train: the move's publish never arrived");
+        }
+        __builtin_ia32_pause();
+    }
     return 0;
 }
 
@@ -4240,10 +4278,21 @@ static int train_move(mz_handle* h, uint32_t move, uint32_t game_offset, int64_t
     h->sp_latch = false;
     wset_swap(h, h->tr_actor);
     if (rc) return rc;
-    MZ_TRY(h, hipMemcpyAsync(h->h_tr_cnt, h->d_sp_counters, sizeof(long long), hipMemcpyDeviceToHost, st));
-    h->h_tr_cnt[1] = 0;
-    if (h->d_fault) MZ_TRY(h, hipMemcpyAsync(h->h_tr_cnt + 1, h->d_fault, 4, hipMemcpyDeviceToHost, st));
-    MZ_TRY(h, hipStreamSynchronize(st));
+    static const bool copy_sync = std::getenv("MZ_TRAIN_SYNC") != nullptr;   // A/B: round 6's copies + sync
+    if (copy_sync) {
+        MZ_TRY(h, hipMemcpyAsync(h->h_tr_cnt, h->d_sp_counters, sizeof(long long), hipMemcpyDeviceToHost, st));
+        h->h_tr_cnt[1] = 0;
+        if (h->d_fault) MZ_TRY(h, hipMemcpyAsync(h->h_tr_cnt + 1, h->d_fault, 4, hipMemcpyDeviceToHost, st));
+        MZ_TRY(h, hipStreamSynchronize(st));
+    } else {
+        const long long seq = ++h->tr_pub_seq;
+        hipLaunchKernelGGL(mz_tr_publish, dim3(1), dim3(64), 0, st, (const long long*)h->d_sp_counters,
+                           (const unsigned*)h->d_fault, h->h_tr_pub, seq);
+        MZ_TRY(h, hipGetLastError());
+        if (tr_wait_publish(h, seq, st)) return -1;
+        h->h_tr_cnt[0] = h->h_tr_pub[0];
+        h->h_tr_cnt[1] = h->h_tr_pub[1];
+    }
     if (h->h_tr_cnt[1] && check_fault(h)) return -1;
     *nfin = h->h_tr_cnt[0] - h->tr_games;
     h->tr_games = h->h_tr_cnt[0];
@@ -4286,7 +4335,11 @@ static int train_learn(mz_handle* h, int64_t nreq, float* losses_dev, hipStream_
     const int64_t n_all = std::max<int64_t>(0, std::min<int64_t>(nreq, (int64_t)h->conf.training_steps + 1 - h->tr_t));
     *done = 0;
     if (n_all == 0) return 0;
-    MultiCap cap{{-1, -1}, {h->tr_actor.flat, h->d_tr_queued}};
+    // the actors' set: θ of the next-to-last refresh step, its search images written by the chain launch
+    // that computes it (else repacked after the call)
+    bool imaged = false;
+    static const bool no_cap_img = std::getenv("MZ_TRAIN_REPACK") != nullptr;   // A/B
+    MultiCap cap{{-1, -1}, {h->tr_actor.flat, h->d_tr_queued}, no_cap_img ? nullptr : &h->tr_actor, &imaged};
     int64_t nref = 0;
     if (!per_refresh) {
         // the refresh steps in (t, t + n]: the last two
@@ -4328,7 +4381,7 @@ static int train_learn(mz_handle* h, int64_t nreq, float* losses_dev, hipStream_
         if (per_refresh && is_refresh(t) && train_refresh(h, t, st)) return -1;
     }
     if (!per_refresh && nref > 0) {
-        if (wset_repack(h, h->tr_actor, st)) return -1;
+        if (!(nref >= 2 && imaged) && wset_repack(h, h->tr_actor, st)) return -1;
         h->tr_refresh += nref;
     }
     return 0;

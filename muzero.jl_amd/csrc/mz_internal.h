@@ -29,8 +29,7 @@
 // fails that call with a message (mz_last_error) — a producer that never
 // publishes is reported, never silently consumed as stale data.
 enum { MZ_FAULT_RS_TRUNK = 1,      // mz_rsearch_nets: the dynamics workgroup's trunk publish
-       MZ_FAULT_RD_PROGRESS = 2,   // mz_runroll_fused_r: a chain block's h_s / trunk publish
-       MZ_FAULT_CHAIN_HELPER = 4 }; // mz_learn_chain: a helper workgroup's θ publish
+       MZ_FAULT_RD_PROGRESS = 2 }; // mz_runroll_fused_r: a chain block's h_s / trunk publish
 #define MZ_POLL_TICKS 200000000ull // 2 s of the 100 MHz s_memrealtime clock
 
 // One lane polls a 64-bit progress word (relaxed, agent scope) until it

@@ -823,8 +823,8 @@ extern "C" __global__ __launch_bounds__(SM_THREADS, 1) void mz_learn_small2_bn(S
 
 // ------------------------------------------------ L learner steps per launch pair
 // (ChainParams / LearnMultiParams, mz_small_params.h)
-// one parameter p's L ADAM iterations in registers; its θ_{t+i} feed step t+i's Σθ² (the slice: added to
-// rd[i·MZ_THREADS] in place; a helper: stored to hx[i·hx_n] for the owning slice); CAP: θ after steps
+// one parameter p's L ADAM iterations in registers; its θ_{t+i} feed step t+i's Σθ² (added to
+// rd[i·MZ_THREADS] in place, or with HELP stored to hx[i·hx_n] for the slot's last block); CAP: θ after steps
 // cap_i[0] / cap_i[1] also copied out (a separate instance: the plain chain carries no per-step tests)
 template <bool CAP, bool HELP>
 __device__ __forceinline__ void chain_param(const ChainParams& C, size_t p, double* rd, float* hx,
@@ -844,7 +844,13 @@ __device__ __forceinline__ void chain_param(const ChainParams& C, size_t p, doub
         x = adam_2theta(x, m, v, sbp[0][i], sbp[1][i], sbp[2][i]);   // Learning.jl:395-397
         if (C.theta) C.theta[i * C.nflat + p] = x;
         if constexpr (CAP) {
-            if (i == C.cap_i[0]) C.cap_dst[0][p] = x;
+            if (i == C.cap_i[0]) {
+                C.cap_dst[0][p] = x;
+                if (C.cap_img[0]) {                         // (the actors' images: no repack after the call)
+                    mz_scatter(x, it, C.cap_img[0], C.cap_img[1]);
+                    mz_scatter(x, is, C.cap_img[2], C.cap_img[3]);
+                }
+            }
             if (i == C.cap_i[1]) C.cap_dst[1][p] = x;
         }
     }
@@ -853,8 +859,7 @@ __device__ __forceinline__ void chain_param(const ChainParams& C, size_t p, doub
     mz_scatter(x, is, C.smw, C.smb);
 }
 
-// this thread's parameters of slice (net, sb): e = sb·256 + tid + k·stride in k order (with helpers
-// for the net: k = 0 only)
+// this thread's parameters of slice (net, sb): e = sb·256 + tid + k·stride in k order
 template <bool CAP>
 __device__ __forceinline__ void chain_slice(const ChainParams& C, int net, int sb, double (*red)[MZ_THREADS],
                                             double (*sbp)[MZ_MULTI_MAX]) {
@@ -866,8 +871,62 @@ __device__ __forceinline__ void chain_slice(const ChainParams& C, int net, int s
 #ifdef MZ_DBG_ONE_ELEM   // diagnostic only (wrong results): each thread's first parameter alone
         break;
 #endif
-        if (C.nh[net]) break;
     }
+}
+
+// lg_tree256 per step: level o adds red[i][j + o] into red[i][j] for j < o, every step i; the o·L adds of
+// a level are spread over all 256 threads (each the same add as the per-step tree's, so the same bits),
+// not L in sequence on the first o threads; step i's sum -> part[i·NSL]
+__device__ __forceinline__ void chain_tree(double (*red)[MZ_THREADS], int L, double* part) {
+    const int tid = threadIdx.x;
+    for (int o = MZ_THREADS / 2; o > 0; o >>= 1) {
+        for (int x = tid; x < o * L; x += MZ_THREADS) {
+            const int i = x / o, j = x - i * o;
+            red[i][j] += red[i][j + o];
+        }
+        __syncthreads();
+    }
+    if (tid < L) part[(size_t)tid * 3 * MZ_L2_BLOCKS] = red[tid][0];
+}
+
+// slot (net, sb)'s blocks: the slice and its helpers (k − 1)·128 + sb, k >= 1
+__device__ __forceinline__ int chain_npart(const ChainParams& C, int net, int sb) {
+    return 1 + (C.nh[net] > sb ? (C.nh[net] - 1 - sb) / MZ_L2_BLOCKS + 1 : 0);
+}
+
+// a block of a slot with helpers: its θ stores performed, it counts itself in (agent scope); the last of
+// the slot's blocks (of this launch: the counter runs to epoch·npart) forms the slot's per-step Σθ²
+// from every parameter's stored θ_{t+i}, in lg_l2_slice's k order, and its tree.  No block waits for
+// another, so the launch completes whatever else shares the GPU.
+__device__ __forceinline__ void chain_arrive(const ChainParams& C, int net, int sb, double (*red)[MZ_THREADS],
+                                             int* last) {
+    const int tid = threadIdx.x, L = C.L;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                // this wave's θ stores performed
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned long long np = (unsigned long long)chain_npart(C, net, sb);
+        const unsigned long long old = __hip_atomic_fetch_add(C.hcnt + net * MZ_L2_BLOCKS + sb, 1ull,
+                                                              __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        *last = old + 1 == C.epoch * np;
+    }
+    __syncthreads();
+    if (!*last) return;
+    const size_t cnt = C.netoff[3 + net], stride = (size_t)MZ_L2_BLOCKS * MZ_THREADS;
+    // (the MZ_MULTI_MAX rows of hx are all allocated: the loads are issued together, sc1 like the stores)
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(C.hx, (short)0, (int)(MZ_MULTI_MAX * C.hx_n * 4), 0x00020000);
+    for (int i = 0; i < L; ++i) red[i][tid] = 0.0;
+    for (size_t e = (size_t)sb * MZ_THREADS + tid; e < cnt; e += stride) {
+        const int b0 = (int)((C.hoff[net] + e) * 4);
+        float xv[MZ_MULTI_MAX];
+#pragma unroll
+        for (int i = 0; i < MZ_MULTI_MAX; ++i)
+            xv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, b0 + (int)(i * C.hx_n * 4), 0, 16));
+#pragma unroll
+        for (int i = 0; i < MZ_MULTI_MAX; ++i)
+            if (i < L) red[i][tid] += (double)xv[i] * (double)xv[i];
+    }
+    __syncthreads();
+    chain_tree(red, L, C.part + net * MZ_L2_BLOCKS + sb);
 }
 
 // mz_learn_chain: blocks [0, nh) are the helpers (ChainParams::nh), then
@@ -875,8 +934,6 @@ __device__ __forceinline__ void chain_slice(const ChainParams& C, int net, int s
 // parameters' L ADAM iterations (∇ = 2θ, Q11) in registers and keeps one
 // Σθ_{t+i}² per step in lg_l2_slice's order; the per-step trees are
 // lg_tree256's, level by level.  The blocks after them draw the L batches.
-// Helpers come first in dispatch order and wait on nothing, so every helper is
-// resident before a slice waits on it (the wait is bounded all the same).
 // The chain and the unroll launches run one after another in stream order
 // (a two-stream variant that overlapped them measured slower, mz_engine.hip
 // learner_multi).
@@ -885,11 +942,13 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learn_chain(ChainPar
     // register array indexed by the runtime step)
     __shared__ double red[MZ_MULTI_MAX][MZ_THREADS];
     __shared__ double sbp[3][MZ_MULTI_MAX];         // β1^t, β2^t, η of step t+i
+    __shared__ int last;
     const int tid = threadIdx.x, nht = C.nh[0] + C.nh[1] + C.nh[2];
-    int blk = (int)blockIdx.x - nht;
+    const int blk = (int)blockIdx.x - nht;
     constexpr int NSL = 3 * MZ_L2_BLOCKS;
     const size_t stride = (size_t)MZ_L2_BLOCKS * MZ_THREADS;
     const int L = C.L;
+    const bool cap = C.cap_i[0] >= 0 || C.cap_i[1] >= 0;   // (mz_train_run's refresh steps in this chain)
     if (blk >= NSL) {                               // get_batch of step t+i, sample b (ReplayBuffer.jl:188-217)
         const int q = (blk - NSL) * (MZ_THREADS / 64) + (tid >> 6);
         if (q >= L * C.B) return;
@@ -902,61 +961,37 @@ extern "C" __global__ __launch_bounds__(MZ_THREADS) void mz_learn_chain(ChainPar
         return;
     }
     if (tid < MZ_MULTI_MAX) { sbp[0][tid] = C.bp1[tid]; sbp[1][tid] = C.bp2[tid]; sbp[2][tid] = C.eta[tid]; }
-    if (blk < 0) {                                  // helper hb of net n: parameter e = stride + hb·256 + tid
-        int hb = (int)blockIdx.x, n = 0;
-        while (hb >= C.nh[n]) hb -= C.nh[n++];
-        const size_t e1 = (size_t)hb * MZ_THREADS + tid, cnt = C.netoff[3 + n];
-        __syncthreads();
-        if (stride + e1 < cnt) {
-            if (C.cap_i[0] < 0 && C.cap_i[1] < 0)
-                chain_param<false, true>(C, C.netoff[n] + stride + e1, nullptr, C.hx + C.hoff[n] + e1, sbp);
-            else
-                chain_param<true, true>(C, C.netoff[n] + stride + e1, nullptr, C.hx + C.hoff[n] + e1, sbp);
+    __syncthreads();
+    // a helper (blk < 0: helper hb of net n, parameter e = stride + hb·256 + tid) or the slice of a slot
+    // with helpers: θ stored, the slot's last block sums
+    int net, sb;
+    size_t e;
+    if (blk < 0) {
+        int hb = (int)blockIdx.x;
+        net = 0;
+        while (hb >= C.nh[net]) hb -= C.nh[net++];
+        e = stride + (size_t)hb * MZ_THREADS + tid;
+        sb = hb % MZ_L2_BLOCKS;
+    } else {
+        net = blk / MZ_L2_BLOCKS;
+        sb = blk - net * MZ_L2_BLOCKS;
+        e = (size_t)sb * MZ_THREADS + tid;
+    }
+    if (blk < 0 || chain_npart(C, net, sb) > 1) {
+        if (e < C.netoff[3 + net]) {
+            float* hx = C.hx + C.hoff[net] + e;
+            if (cap) chain_param<true, true>(C, C.netoff[net] + e, nullptr, hx, sbp);
+            else chain_param<false, true>(C, C.netoff[net] + e, nullptr, hx, sbp);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");            // this wave's θ stores performed
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store(C.hprog + blockIdx.x, C.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        chain_arrive(C, net, sb, red, &last);
         return;
     }
     for (int i = 0; i < L; ++i) red[i][tid] = 0.0;
     __syncthreads();
-    const int net = blk / MZ_L2_BLOCKS, sb = blk - net * MZ_L2_BLOCKS;
-    if (C.cap_i[0] < 0 && C.cap_i[1] < 0) chain_slice<false>(C, net, sb, red, sbp);
-    else chain_slice<true>(C, net, sb, red, sbp);             // (mz_train_run's refresh steps in this chain)
-    if (C.nh[net]) {
-        // the helpers' parameters e = k·stride + sb·256 + tid, k >= 1, in k order: helper (k − 1)·128 + sb
-        // of the net (its block: the nets before it first)
-        const size_t cnt = C.netoff[3 + net], o = (size_t)sb * MZ_THREADS + tid;
-        const int hb0 = net == 0 ? 0 : net == 1 ? C.nh[0] : C.nh[0] + C.nh[1];
-        if (tid == 0)
-            for (int hb = sb; hb < C.nh[net]; hb += MZ_L2_BLOCKS)   // bounded: a publish that never comes is reported
-                mz_poll_ge(C.hprog + hb0 + hb, C.epoch, C.fault, MZ_FAULT_CHAIN_HELPER, C.poll_ticks);
-        __syncthreads();
-        // (the MZ_MULTI_MAX rows of hx are all allocated: the loads are issued together, sc1 like the stores)
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc(C.hx, (short)0, (int)(MZ_MULTI_MAX * C.hx_n * 4), 0x00020000);
-        for (size_t e = o + stride; e < cnt; e += stride) {
-            const int b0 = (int)((C.hoff[net] + (e - stride)) * 4);
-            float xv[MZ_MULTI_MAX];
-#pragma unroll
-            for (int i = 0; i < MZ_MULTI_MAX; ++i)
-                xv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, b0 + (int)(i * C.hx_n * 4), 0, 16));
-#pragma unroll
-            for (int i = 0; i < MZ_MULTI_MAX; ++i)
-                if (i < L) red[i][tid] += (double)xv[i] * (double)xv[i];
-        }
-    }
+    if (cap) chain_slice<true>(C, net, sb, red, sbp);
+    else chain_slice<false>(C, net, sb, red, sbp);
     __syncthreads();
-    // lg_tree256 per step: level o adds red[i][j + o] into red[i][j] for j < o, every step i; the o·L
-    // adds of a level are spread over all 256 threads (each the same add as the per-step tree's, so
-    // the same bits), not L in sequence on the first o threads
-    for (int o = MZ_THREADS / 2; o > 0; o >>= 1) {
-        for (int x = tid; x < o * L; x += MZ_THREADS) {
-            const int i = x / o, j = x - i * o;
-            red[i][j] += red[i][j + o];
-        }
-        __syncthreads();
-    }
-    if (tid < L) C.part[(size_t)tid * NSL + blk] = red[tid][0];
+    chain_tree(red, L, C.part + blk);
 }
 
 // mz_learn_multi{1,2}: workgroup (step i, tile lb).  With M.xcd, step i's

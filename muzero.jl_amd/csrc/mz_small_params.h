@@ -156,23 +156,24 @@ struct ChainParams {
     float* theta;                                      // NULL or [L][nflat]: θ after step t+i
     int cap_i[2]; float* cap_dst[2];                   // θ after step t+cap_i[j] -> cap_dst[j] (cap_i < 0: none;
                                                        // mz_train_run's actor / queued sets at refresh steps)
+    float* cap_img[4];                                 // NULL or cap 0's search images (Wp, Bp, smw, smb): θ after
+                                                       // step t+cap_i[0] scattered as into the engine's images
     size_t nflat;
     double* part;                                      // [L][3·MZ_L2_BLOCKS] Σθ_{t+i}² partials
     double bp1[MZ_MULTI_MAX], bp2[MZ_MULTI_MAX], eta[MZ_MULTI_MAX];   // step t+i's β powers, learning rate
     int B;                                             // batches: sample q = i·B + b, one wave each
     RpSampleParams q;                                  // step t's get_batch; step i's arrays at + i·stride
     size_t s_obs, s_k1, s_tp;                          // per-step strides: B·F, B·(K+1), B·(K+1)·A
-    // helper workgroups (blocks [0, nh[0] + nh[1] + nh[2]), dispatched before the slices): net n's
-    // parameters past the slices' first pass (e >= MZ_L2_BLOCKS·MZ_THREADS), one per thread, so no thread
-    // runs two parameters' chains in sequence; each stores its θ_{t+i} to hx[i·hx_n + hoff[n] + e − stride]
-    // (agent scope) and publishes hprog[helper] = epoch; the owning slice adds their squares after its own,
-    // in lg_l2_slice's order (nh[n] = 0: the slice runs them itself)
+    // helper workgroups (blocks [0, nh[0] + nh[1] + nh[2]), before the slices): net n's parameters past
+    // the slices' first pass (e >= MZ_L2_BLOCKS·MZ_THREADS), one per thread, so no thread runs two
+    // parameters' chains in sequence.  Every block of a slot with helpers stores its θ_{t+i} to
+    // hx[i·hx_n + hoff[n] + e] (agent scope) and counts itself in at hcnt[n·MZ_L2_BLOCKS + slot]; the
+    // last one adds the squares in lg_l2_slice's order (nh[n] = 0: the slice runs them itself)
     int nh[3];
     size_t hoff[3], hx_n;
     float* hx;
-    unsigned long long* hprog;
-    unsigned long long epoch, poll_ticks;
-    unsigned* fault;                                   // MZ_FAULT_CHAIN_HELPER on a publish that never came
+    unsigned long long* hcnt;                          // [3·MZ_L2_BLOCKS], epoch·npart after this launch
+    unsigned long long epoch;
 };
 struct LearnMultiParams {
     int L, nU, xcd;                                    // xcd: step i on XCD i mod 8 (learn_multi_body)
