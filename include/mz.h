@@ -449,12 +449,15 @@ int mz_selfplay_slots(mz_handle* h, int32_t* history_len, uint8_t* board, int32_
  *     a refresh reaches every slot at once, games in progress included; the
  *     reference's single actor takes new nets only between games
  *     (SelfPlay.jl:399-401).  Reads the shard's game counter back once per
- *     move (one sync).  state_out[4] = {t, num_played_games, actor refreshes,
+ *     move (one kernel stores it into pinned host memory and the host spins
+ *     on it, bounded; the stream's work up to that move is then complete).
+ *     state_out[4] = {t, num_played_games, actor refreshes,
  *     learner steps of this call}; losses_dev (device, 6 floats, or NULL) =
  *     the last step's.  The learner steps of one move run as one
  *     mz_learner_train_multi_dev chunk across the refresh points (the chain
  *     launch copies out θ of the last two refresh steps for the actors' and
- *     queued sets; with a networks path the chunks end at each refresh).
+ *     queued sets, and writes the actors' search images; with a networks path
+ *     the chunks end at each refresh).
  *     Data parallel (after mz_dp_init, world > 1): the move's finished-game
  *     count is summed over the ranks (RCCL) and every rank takes that many
  *     learner steps on its own shard, so the ref_semantics replicas stay
