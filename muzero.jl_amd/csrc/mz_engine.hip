@@ -197,7 +197,6 @@ struct mz_handle {
     unsigned long long tprog_epoch = 0;     // mz_rsearch_nets launches
     float* d_chx = nullptr;                 // [MZ_MULTI_MAX][hx_n] mz_learn_chain helpers' θ (ChainParams::hx)
     unsigned long long* d_chcnt = nullptr;  // [3·MZ_L2_BLOCKS] their slots' arrival counters
-    unsigned long long chain_epoch = 0;     // mz_learn_chain launches with helpers
     unsigned long long prog_epoch = 0;      // launches of mz_runroll_fused_r (prog_base = epoch · 64)
     std::vector<int> rtab;                  // offset tables of the narrow (chain) plans
     int* d_rtab = nullptr;
@@ -3817,7 +3816,7 @@ static int chain_helpers(mz_handle* h, ChainParams& C) {
         MZ_TRY(h, dalloc(h, &h->d_chcnt, (size_t)3 * MZ_L2_BLOCKS));
         MZ_TRY(h, hipMemset(h->d_chcnt, 0, (size_t)3 * MZ_L2_BLOCKS * sizeof(unsigned long long)));
     }
-    C.hx = h->d_chx; C.hx_n = hx_n; C.hcnt = h->d_chcnt; C.epoch = ++h->chain_epoch;
+    C.hx = h->d_chx; C.hx_n = hx_n; C.hcnt = h->d_chcnt;
     return nht;
 }
 static void set_caps(ChainParams& C, const MultiCap* cap, int64_t first, int nc) {

@@ -895,7 +895,7 @@ __device__ __forceinline__ int chain_npart(const ChainParams& C, int net, int sb
 }
 
 // a block of a slot with helpers: its θ stores performed, it counts itself in (agent scope); the last of
-// the slot's blocks (of this launch: the counter runs to epoch·npart) forms the slot's per-step Σθ²
+// the slot's blocks (the counter reaches a multiple of npart) forms the slot's per-step Σθ²
 // from every parameter's stored θ_{t+i}, in lg_l2_slice's k order, and its tree.  No block waits for
 // another, so the launch completes whatever else shares the GPU.
 __device__ __forceinline__ void chain_arrive(const ChainParams& C, int net, int sb, double (*red)[MZ_THREADS],
@@ -907,7 +907,7 @@ __device__ __forceinline__ void chain_arrive(const ChainParams& C, int net, int 
         const unsigned long long np = (unsigned long long)chain_npart(C, net, sb);
         const unsigned long long old = __hip_atomic_fetch_add(C.hcnt + net * MZ_L2_BLOCKS + sb, 1ull,
                                                               __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        *last = old + 1 == C.epoch * np;
+        *last = (old + 1) % np == 0;                  // (np arrivals per launch: self-aligning)
     }
     __syncthreads();
     if (!*last) return;

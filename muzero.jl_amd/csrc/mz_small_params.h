@@ -172,8 +172,7 @@ struct ChainParams {
     int nh[3];
     size_t hoff[3], hx_n;
     float* hx;
-    unsigned long long* hcnt;                          // [3·MZ_L2_BLOCKS], epoch·npart after this launch
-    unsigned long long epoch;
+    unsigned long long* hcnt;                          // [3·MZ_L2_BLOCKS], a multiple of npart between launches
 };
 struct LearnMultiParams {
     int L, nU, xcd;                                    // xcd: step i on XCD i mod 8 (learn_multi_body)
