@@ -841,7 +841,11 @@ __device__ __forceinline__ void chain_param(const ChainParams& C, size_t p, doub
 #endif
         if (tbank) mz_scatter(x, it, C.tbank_w + i * C.tws, C.tbank_b + i * C.tbs);
         if (C.fbank) C.fbank[i * C.fstride + p] = x;
+#ifdef MZ_DBG_CHEAP_ADAM   // diagnostic only (wrong results): the chain without ADAM's f64 arithmetic
+        x = x * 0.999f + (float)sbp[2][i];
+#else
         x = adam_2theta(x, m, v, sbp[0][i], sbp[1][i], sbp[2][i]);   // Learning.jl:395-397
+#endif
         if (C.theta) C.theta[i * C.nflat + p] = x;
         if constexpr (CAP) {
             if (i == C.cap_i[0]) {
