@@ -184,7 +184,7 @@ struct mz_handle {
     float bn_s = 1.0f;
     int* d_rpath = nullptr; int* d_rgst = nullptr;          // ResNet search: [G][2(S+2)], [G][RG_INTS]
     uint2* d_rcache = nullptr; int* d_rnN = nullptr;        // [G][S+1]: the LDS tree step's cached select
-    float* d_rxpred = nullptr; float* d_rov = nullptr; float* d_rologit = nullptr; float* d_ror = nullptr;
+    int* d_rhk = nullptr; float* d_rov = nullptr; float* d_rologit = nullptr; float* d_ror = nullptr;
     float* d_rhs = nullptr;                 // [bcap][K][H] learner unroll scratch (h between the nets)
     float* d_rts = nullptr;                 // [bcap][K][H] dynamics trunk outputs (the reward heads' input)
     int rn_dyn_split = 0;                   // first reward-head layer of the dynamics plan
@@ -1550,7 +1550,7 @@ int mz_engine_create_resnet(const mz_config* conf, const mz_resnet_hp* hyper, in
         }
         CK(al(&h->d_rpath, G * 2 * (S + 2))); CK(al(&h->d_rgst, G * RG_INTS));
         CK(al(&h->d_rcache, G * (S + 1))); CK(al(&h->d_rnN, G * (S + 1)));
-        CK(al(&h->d_rxpred, G * H)); CK(al(&h->d_rov, G)); CK(al(&h->d_rologit, G * A)); CK(al(&h->d_ror, G));
+        CK(al(&h->d_rhk, G * (S + 1))); CK(al(&h->d_rov, G)); CK(al(&h->d_rologit, G * A)); CK(al(&h->d_ror, G));
         CK(al(&h->d_obs, G * h->obs_feat)); CK(al(&h->d_legal, G * A)); CK(al(&h->d_tp, G));
         CK(al(&h->d_cv, G * A)); CK(al(&h->d_rv, G)); CK(al(&h->d_act, G));
     }
@@ -1856,7 +1856,7 @@ static int rsearch(mz_handle* h, int G, const float* obs, const uint8_t* legal_m
     P.pbc_tab = h->d_pbc; P.sqrt_tab = h->d_sqrt; P.aval_tab = h->d_aval; P.pbterm = h->d_pbterm;
     P.tree = h->d_tree; P.tree_game_bytes = h->tree_game_bytes; P.hid = h->d_hid;
     P.cache = h->d_rcache; P.nN = h->d_rnN;
-    P.path = h->d_rpath; P.gst = h->d_rgst; P.x_pred = h->d_rxpred;
+    P.path = h->d_rpath; P.gst = h->d_rgst; P.hk = h->d_rhk;
     P.o_v = h->d_rov; P.o_logit = h->d_rologit; P.o_r = h->d_ror;
     P.ng = h->rn_ng; P.bn_s = h->bn_s; P.plans = h->d_rplan; P.Wimg = h->d_Wp; P.flat = h->d_flat;
 #ifdef MZ_STAMPS

@@ -687,13 +687,13 @@ __device__ __forceinline__ void rn_unstage_l(const float* src, int kb, int NG, i
     for (int f = t.f0; f < n; f += t.fs) put(f, src[rn_conv_idx(1, f, t.g, NG, P)]);
 }
 
-// LDS tile [f][g] (plain or k-blocked) <- scale · row_g[f] for f < H (H % 4 == 0,
+// LDS tile [f][g] (plain or k-blocked) <- row_g[f] · 2^ex(g) for f < H (H % 4 == 0,
 // rows 16-byte aligned; row_g = nullptr: zeros): lane l reads the 16-byte piece
 // l / NG of row l mod NG (a wave instruction: 64 bytes of each of 16 rows, where
 // rn_stage's layout reads 4 bytes of each), four pieces in flight per thread;
 // the LDS writes of consecutive lanes stay on consecutive games' banks
-template <class RowFn>
-__device__ __forceinline__ void rn_stage_rows(float* dst, int kb, int NG, int P, int H, float scale, RowFn row) {
+template <class ExpFn, class RowFn>
+__device__ __forceinline__ void rn_stage_rows(float* dst, int kb, int NG, int P, int H, ExpFn ex, RowFn row) {
     const int H4 = H >> 2, n4 = NG * H4, nt = blockDim.x, lg = __ffs(NG) - 1;   // NG a power of two
     for (int i0 = threadIdx.x; i0 < n4; i0 += 4 * nt) {
         float4 v[4];
@@ -711,11 +711,11 @@ __device__ __forceinline__ void rn_stage_rows(float* dst, int kb, int NG, int P,
         for (int u = 0; u < 4; ++u) {
             const int i = i0 + u * nt;
             if (i < n4) {
-                const int g = i & (NG - 1), f = (i >> lg) * 4;
-                dst[rn_conv_idx(kb, f, g, NG, P)] = v[u].x * scale;
-                dst[rn_conv_idx(kb, f + 1, g, NG, P)] = v[u].y * scale;
-                dst[rn_conv_idx(kb, f + 2, g, NG, P)] = v[u].z * scale;
-                dst[rn_conv_idx(kb, f + 3, g, NG, P)] = v[u].w * scale;
+                const int g = i & (NG - 1), f = (i >> lg) * 4, e = ex(g);   // x·2^e: exact
+                dst[rn_conv_idx(kb, f, g, NG, P)] = ldexpf(v[u].x, e);
+                dst[rn_conv_idx(kb, f + 1, g, NG, P)] = ldexpf(v[u].y, e);
+                dst[rn_conv_idx(kb, f + 2, g, NG, P)] = ldexpf(v[u].z, e);
+                dst[rn_conv_idx(kb, f + 3, g, NG, P)] = ldexpf(v[u].w, e);
             }
         }
     }
@@ -887,6 +887,7 @@ __device__ __forceinline__ void rsearch_root_body(const RSearchParams& P) {
             st[RG_ROOTN] = 0; st[RG_ROOTW] = __float_as_int(0.0f);
             st[RG_MMIN] = __float_as_int(INFINITY); st[RG_MMAX] = __float_as_int(-INFINITY);   // :251
             st[RG_LEAF_E] = 0; st[RG_LEAF_A] = 0; st[RG_VTP] = 1; st[RG_DEPTH] = 0;
+            P.hk[(size_t)gg * (P.S + 1)] = 0;                                   // h0 not used yet
         }
     }
 }
@@ -943,14 +944,10 @@ __device__ __forceinline__ void rsearch_tree_body(const RSearchParams& P) {
                                                 gid, P.rng_step, P.s);                    // :256-268
         if (a == 0) {
             st[RG_LEAF_E] = so.leaf_e; st[RG_LEAF_A] = so.leaf_a; st[RG_VTP] = so.vtp; st[RG_DEPTH] = so.depth;
-        }
-        // parent h -> prediction input; h *= 2 in place (Q1), read by the dynamics launch
-        float* hp = P.hid + ((size_t)gg * (S + 1) + so.leaf_e) * H;
-        float* xp = P.x_pred + (size_t)gg * H;
-        for (int k = a; k < H; k += GW) {
-            const float hv = hp[k];
-            xp[k] = hv;
-            hp[k] = hv * 2.0f;
+            int* hk = P.hk + (size_t)gg * (S + 1) + so.leaf_e;   // the parent's h *= 2 in place (Q1): counted
+            const int k = *hk;
+            st[RG_XK] = k;
+            *hk = k + 1;
         }
     } else {                                        // store_search_stats! (:115-122) + select_action (:293-306)
         const bool lg = a < A && ((legal >> a) & 1u);
@@ -1018,7 +1015,7 @@ __device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     // per game of the workgroup: rows to recompute, moved, depth, the select's
     // start level (atomicMin over the rows), the tag, the selected leaf's parent
-    __shared__ int sh_rows[4], sh_moved[4], sh_depth[4], sh_skip[4], sh_leaf[4];
+    __shared__ int sh_rows[4], sh_moved[4], sh_depth[4], sh_skip[4];
     __shared__ uint32_t sh_ver[4];
     __shared__ float sh_mm[4][2];                   // min / max after the backup
     RT_STAMP(0);
@@ -1235,47 +1232,13 @@ __device__ __forceinline__ void rsearch_tree_lds_body(const RSearchParams& P) {
                                                                npc0);
             if (a == 0) {
                 st[RG_LEAF_E] = so.leaf_e; st[RG_LEAF_A] = so.leaf_a; st[RG_VTP] = so.vtp; st[RG_DEPTH] = so.depth;
-                sh_leaf[gl] = so.leaf_e;
+                int* hk = P.hk + (size_t)gg * (S + 1) + so.leaf_e;   // the parent's h *= 2 in place (Q1): counted
+                const int k = *hk;
+                st[RG_XK] = k;
+                *hk = k + 1;
             }
         }
-        __syncthreads();
         RT_STAMP(7);
-        // ---- every wave: parent h -> prediction input; h *= 2 in place (Q1),
-        // read by the dynamics launch.  16-byte pieces, RT_GU per thread loaded
-        // before any is stored (the stores could alias the loads, so a
-        // one-at-a-time loop waits a full memory round trip per piece)
-        if ((H & 3) == 0) {
-            constexpr int RT_GU = 4;
-            const int H4 = H >> 2, n4 = NGW * H4, nt = blockDim.x;
-            for (int i0 = tid; i0 < n4; i0 += RT_GU * nt) {
-                float4 v[RT_GU];
-#pragma unroll
-                for (int u = 0; u < RT_GU; ++u) {
-                    const int i = i0 + u * nt, g = i / H4, k = i - g * H4;
-                    const int gq = blockIdx.x * NGW + g;
-                    if (i < n4 && gq < P.G)
-                        v[u] = reinterpret_cast<const float4*>(P.hid + ((size_t)gq * (S + 1) + sh_leaf[g]) * H)[k];
-                }
-#pragma unroll
-                for (int u = 0; u < RT_GU; ++u) {
-                    const int i = i0 + u * nt, g = i / H4, k = i - g * H4;
-                    const int gq = blockIdx.x * NGW + g;
-                    if (i < n4 && gq < P.G) {
-                        reinterpret_cast<float4*>(P.x_pred + (size_t)gq * H)[k] = v[u];
-                        reinterpret_cast<float4*>(P.hid + ((size_t)gq * (S + 1) + sh_leaf[g]) * H)[k] =
-                            make_float4(v[u].x * 2.0f, v[u].y * 2.0f, v[u].z * 2.0f, v[u].w * 2.0f);
-                    }
-                }
-            }
-        } else if (wave == 0 && live) {
-            float* hp = P.hid + ((size_t)gg * (S + 1) + sh_leaf[gl]) * H;
-            float* xp = P.x_pred + (size_t)gg * H;
-            for (int k = a; k < H; k += GW) {
-                const float hv = hp[k];
-                xp[k] = hv;
-                hp[k] = hv * 2.0f;
-            }
-        }
         RT_STAMP(8);
     } else if (wave == 0 && live) {                 // store_search_stats! (:115-122) + select_action (:293-306)
         const bool lg = a < A && ((legal >> a) & 1u);
@@ -1320,25 +1283,33 @@ extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RS
     const RnLane t = rn_lane(NG);
     const int gg = t0 + t.g;
     const bool ok = gg < P.G;
-    // prediction(parent h) and dynamics(2h ⊕ a/|A|) both read x_pred, the
-    // parent's h before the tree step doubled it in place (Q1): 2·x_pred is that
-    // doubled value bit for bit.  The dynamics' a/|A| plane (features H ..
-    // in_feat - 1): the leaf actions are loaded first, so their latency overlaps
-    // the row loads; a/|A| as the host's table, (float)((a + 1) / |A|) in f64
+    // prediction(parent h) and dynamics(2h ⊕ a/|A|) read the parent's stored h'
+    // (hid[leaf_e]) times 2^hk and 2^(hk+1): the value make_state_action (Q1)
+    // leaves in place after the node's hk earlier uses, and the doubled value of
+    // this use, bit for bit (powers of two are exact; RSearchParams::hk).  The
+    // dynamics' a/|A| plane (features H .. in_feat - 1): the leaf actions are
+    // loaded first, so their latency overlaps the row loads; a/|A| as the host's
+    // table, (float)((a + 1) / |A|) in f64
     const int np = R.in_feat - H, npl = net == MZ_NET_DYN ? NG * np : 0;
     int la = 0;
     if ((int)threadIdx.x < npl) {
         const int gq = t0 + (int)threadIdx.x / np;
         if (gq < P.G) la = P.gst[(size_t)gq * RG_INTS + RG_LEAF_A];
     }
+    const int e1 = net == MZ_NET_DYN ? 1 : 0;
     if ((H & 3) == 0) {
-        rn_stage_rows(lds + R.in_off, R.in_kb, NG, P.P, H, net == MZ_NET_PRED ? 1.0f : 2.0f, [&](int g) {
-            return t0 + g < P.G ? P.x_pred + (size_t)(t0 + g) * H : nullptr;
-        });
+        rn_stage_rows(lds + R.in_off, R.in_kb, NG, P.P, H,
+                      [&](int g) { return t0 + g < P.G ? P.gst[(size_t)(t0 + g) * RG_INTS + RG_XK] + e1 : 0; },
+                      [&](int g) -> const float* {
+                          if (t0 + g >= P.G) return nullptr;
+                          const int sl = P.gst[(size_t)(t0 + g) * RG_INTS + RG_LEAF_E];
+                          return P.hid + ((size_t)(t0 + g) * (S + 1) + sl) * H;
+                      });
     } else {
-        const float* x = P.x_pred + (size_t)(ok ? gg : 0) * H;
-        const float sc = net == MZ_NET_PRED ? 1.0f : 2.0f;
-        rn_stage_l(lds + R.in_off, R.in_kb, NG, P.P, H, t, [&](int f) { return ok ? x[f] * sc : 0.0f; });
+        const int* q = P.gst + (size_t)(ok ? gg : 0) * RG_INTS;
+        const float* x = P.hid + ((size_t)(ok ? gg : 0) * (S + 1) + q[RG_LEAF_E]) * H;
+        const int e = q[RG_XK] + e1;
+        rn_stage_l(lds + R.in_off, R.in_kb, NG, P.P, H, t, [&](int f) { return ok ? ldexpf(x[f], e) : 0.0f; });
     }
     for (int i = threadIdx.x; i < npl; i += blockDim.x) {
         const int g = i / np, f = H + (i - g * np);
@@ -1379,6 +1350,8 @@ extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RS
                 float* o = P.hid + ((size_t)gg * (S + 1) + P.s + 1) * H;
                 rn_unstage_l(lds + R.out0_off, R.out0_kb, NG, P.P, H, t, [&](int f, float v) { o[f] = v; });
             }
+            if ((int)threadIdx.x < NG && t0 + (int)threadIdx.x < P.G)     // the new node's h' not used yet
+                P.hk[(size_t)(t0 + threadIdx.x) * (S + 1) + P.s + 1] = 0;
             return;
         }
         rn_run<false, false, 3, false, true, true>(R, P.Wimg, P.flat, lds, NG, P.W, P.P, P.bn_s, st);
@@ -1422,6 +1395,7 @@ extern "C" __global__ __launch_bounds__(RN_THREADS_NETS) void mz_rsearch_nets(RS
         float* o = P.hid + ((size_t)gg * (S + 1) + P.s + 1) * H;
         rn_unstage_l(lds + R.out0_off, R.out0_kb, NG, P.P, H, t, [&](int f, float v) { o[f] = v; });
         if (t.f0 == 0) P.o_r[gg] = rn_act(R.out1_act, lds[R.out1_off + t.g]);
+        if (t.f0 == 0) P.hk[(size_t)gg * (S + 1) + P.s + 1] = 0;   // the new node's h' not used yet
     }
 }
 

@@ -122,6 +122,7 @@ struct RNetParams {
 // legal, root_tp, rootN, rootW, mmin, mmax, leaf_e, leaf_a, vtp, depth.
 enum { RG_LEGAL = 0, RG_ROOT_TP, RG_ROOTN, RG_ROOTW, RG_MMIN, RG_MMAX, RG_LEAF_E, RG_LEAF_A, RG_VTP, RG_DEPTH,
        RG_VER,                          // the LDS tree step's cached-select tag (mz_tree_device.h select_path_cached)
+       RG_XK,                           // doublings of the leaf_e node's h before this simulation (RSearchParams::hk)
        RG_INTS = 16 };
 
 struct RSearchParams {
@@ -140,7 +141,11 @@ struct RSearchParams {
     int* nN;               // [G][S+1] N of each expanded node (the edge into it; the root's N), for recomputes
     int* path;             // [G][2(S+2)]
     int* gst;              // [G][RG_INTS]
-    float* x_pred;         // [G][H] prediction input of this simulation
+    // make_state_action (Q1) doubles the parent's stored h in place at every use; a node's stored h is its
+    // h' times 2^hk (hk = its uses so far, exact: powers of two), so the tree step only counts the use
+    // (gst[RG_XK] = hk before it, then hk + 1) and the network launch reads hid[leaf_e] scaled by 2^hk
+    // (prediction) and 2^(hk+1) (dynamics) — no copy of h, no rewrite of hid
+    int* hk;               // [G][S+1]
     float* o_v; float* o_logit; float* o_r;   // [G], [G][A], [G]
     int ng; float bn_s;
     const RPlan* plans;    // repr, pred, dyn
