@@ -76,6 +76,33 @@ def test_resnet_search_bitexact(ttt, S, G, explore, temp, seed):
     eng.close()
 
 
+def test_resnet_search_hbm_tree_bitexact(ttt, monkeypatch):
+    """The tree step on the HBM tree (`mz_rsearch_tree`, used when a game's tree
+    exceeds the LDS; MZ_RTREE_HBM=1 at create forces it), with the parent's h by
+    reference (use counts, 2^k in the network launch)."""
+    import dataclasses
+    from conftest import random_positions
+    from muzero_jl_amd import abi
+    from test_gpu_parity import _compare_trees
+    monkeypatch.setenv("MZ_RTREE_HBM", "1")
+    S, G, seed = 20, 24, 6
+    conf = dataclasses.replace(ttt.conf, num_iters=S)
+    o, nets = _resnet_oracle(conf, ttt.resnet_hyper, seed=seed)
+    eng = abi.Engine(conf, ttt.resnet_hyper, device=0, max_games=G, rng_seed=o.seed)
+    for n, w in enumerate(nets):
+        o.set_weights(n, w)
+        eng.set_weights(n, w)
+    obs, legal, tp = random_positions(G, 60)
+    eng.debug_enable(1)
+    cv, rv, act = eng.mcts_search(obs, legal, tp, exploration=True, rng_step=5, game_offset=3, temperature=1.0)
+    tree_g = eng.debug_tree(G)
+    cv2, rv2, act2, tree_o, _ = o.mcts_search(obs, legal, tp, exploration=True, rng_step=5, game_offset=3,
+                                              temperature=1.0, dump=True)
+    _compare_trees(tree_g, tree_o, G)
+    assert np.array_equal(cv, cv2) and np.array_equal(rv, rv2) and np.array_equal(act, act2)
+    eng.close()
+
+
 @pytest.mark.parametrize("B,K", [(20, 5), (33, 3), (7, 0), (832, 5)])
 def test_resnet_learner_steps(ttt, B, K):
     """ResNet learner (unroll on the network kernels + the shared loss/∇ = 2θ
