@@ -561,9 +561,12 @@ __device__ __forceinline__ SelectOut select_path_cached(const TreeView& t, const
     int e = D > 0 ? e0 : 0, dg = D, lach = 0, pe = 0, pc = 0;
     uint32_t npc = D > 0 ? npc0 : (uint32_t)root_N;
     uint64_t am = __builtin_amdgcn_ballot_w64(true);
+    // the next level's entry is read as soon as its node is known, before this
+    // level's path bookkeeping, so the LDS latency runs under that bookkeeping
+    uint2 cn = cache[e];
     for (int it = 1;; ++it) {
         const int lv = D + it;
-        uint2 ce = cache[e];
+        uint2 ce = cn;
         asm volatile("" : "+v"(ce.x), "+v"(ce.y));       // one ds_read_b64 (not split into the branches)
         int ach = (int)(ce.x & 31u);
         uint32_t ncc = ce.y;
@@ -590,6 +593,9 @@ __device__ __forceinline__ SelectOut select_path_cached(const TreeView& t, const
         }
         const int ei = (int)__umul24((unsigned)e, (unsigned)A) + ach;
         const int Cch = (int)(ncc >> 16);                 // child slot + 1, 0 = the leaf
+        const uint64_t nm = mz_vcmp_ne((uint32_t)Cch, 0u) & am;   // groups still walking after this level
+        const int en = mz_vsel(nm, Cch - 1, e);
+        cn = cache[en];                                   // (a frozen group re-reads its own node: harmless)
         const uint64_t km = mz_vcmp_eq((uint32_t)a, (uint32_t)lv) & am;   // lane `lv` keeps the level
         pe = mz_vsel(km, ei, pe);
         pc = mz_vsel(km, Cch, pc);
@@ -601,8 +607,7 @@ __device__ __forceinline__ SelectOut select_path_cached(const TreeView& t, const
             asm volatile("" : "+s"(wm));                  // the lane test stays inside this branch
             if (a == 0 && ((wm >> lane) & 1u)) { path[2 * lv] = ei; path[2 * lv + 1] = Cch - 1; }
         }
-        const uint64_t nm = mz_vcmp_ne((uint32_t)Cch, 0u) & am;   // groups still walking after this level
-        e = mz_vsel(nm, Cch - 1, e);
+        e = en;
         npc = (uint32_t)mz_vsel(nm, (int)ncc, (int)npc);
         am = nm;
         if (am == 0) break;
